@@ -1,0 +1,224 @@
+"""Benchmark: batched extend attempts/s on synth-rough-1024 (BASELINE config 3).
+
+A step = one pass of the hot path (gbp_validate_pairs: isValidStateActionPair /
+...Reverse for every attempt) over one resident batch of 262,144 attempts per
+GPU (s_near ~ randomState | STANCE-valid, action =
+getRandomAction(normal at a random target), FORWARD/REVERSE alternating,
+seed 20251018).  Inputs are generated on the GPU before timing (Philox-keyed,
+so rank r's shard [r*B, (r+1)*B) is the same data wherever it is generated).
+
+Multi-GPU: one process per GPU (torchrun), each rank its own contiguous shard,
+no data-path collective ("scaling": "weak"); only the timing max and the
+counter sums cross ranks.
+
+Extra fields: `roofline` for the validate kernel (algorithmic bytes per
+SURVEY §8(d): 144 B in + 76 B out + 32 B x (G + V) per attempt, G/V = the
+executed getGroundHeight / isValidState calls reported by the kernel itself,
+over the HIP-event-timed kernel duration), `cpu_baseline` (the CPU
+restatement with the reference's O(N) scans, one host thread, rank 0, N=1).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import global_body_planner_amd as gbp  # noqa: E402
+from global_body_planner_amd import _lib as L  # noqa: E402
+from global_body_planner_amd import terrain_data as td  # noqa: E402
+from global_body_planner_amd import workload as W  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md chip table)
+BYTES_IN, BYTES_OUT, BYTES_PER_LOOKUP = 144, 76, 32
+METRIC = "valid extend-attempts/sec + time-to-first-solution, 1024×1024 rough_terrain"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--batch", type=int, default=262144, help="attempts per GPU per step")
+    p.add_argument("--terrain", default="synth-rough-1024")
+    p.add_argument("--seed", type=int, default=W.CONFIG_SEEDS[3])
+    p.add_argument("--kernel", choices=["persistent", "direct"], default="persistent")
+    p.add_argument("--waves", type=int, default=2)
+    p.add_argument("--grid-per-cu", type=int, default=8)
+    p.add_argument("--adaptive", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=15.0,
+                   help="bounded CPU-baseline sample (0 disables)")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    p.add_argument("--out", default=None, help="also write the JSON line here")
+    return p.parse_args()
+
+
+def cpu_baseline(data, s, a, d, seconds):
+    """The oracle (reference algorithm, O(N) scans) on this host, 1 thread."""
+    try:
+        import oracle
+    except Exception as e:  # pragma: no cover
+        return {"value": None, "error": f"oracle unavailable: {e}"}
+    O = oracle.OracleTerrain.from_data(data)
+    oracle.set_scan_mode(0)
+    n_total, done, chunk = s.shape[0], 0, 256
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds and done < n_total:
+        hi = min(n_total, done + chunk)
+        O.validate_pairs(s[done:hi], a[done:hi], d[done:hi], nthreads=1)
+        done = hi
+    dt = time.perf_counter() - t0
+    return {"value": round(done / dt, 1), "unit": "extend-attempts/s", "cores": 1,
+            "kind": "port",
+            "sample": f"first {done} attempts of the same batch on the host CPU "
+                      f"({dt:.1f} s, 1 thread, oracle/gbp_oracle.c linear-scan brackets)",
+            "host_cpu": _cpu_model(), "host_threads_available": os.cpu_count()}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    data = td.by_name(args.terrain)
+    T = gbp.Terrain.from_data(data, device=local)
+    T.set_option(L.OPT_KERNEL, L.KERNEL_PERSISTENT if args.kernel == "persistent" else L.KERNEL_DIRECT)
+    T.set_option(L.OPT_WAVES, args.waves)
+    T.set_option(L.OPT_GRID_PER_CU, args.grid_per_cu)
+    B = args.batch
+    s, a, d, _, tries = W.make_attempts(T, B, args.seed, index_base=rank * B)
+    res = T.validate_pairs(s, a, d, adaptive=args.adaptive)
+    torch.cuda.synchronize()
+    # per-launch algorithmic bytes from the kernel's own G/V counters
+    c = res.counts.to(torch.int64) & 0xFFFFFFFF
+    gv = int(((c & 0xFFFF) + (c >> 16)).sum().item())
+    n_valid = int(res.valid.to(torch.int64).sum().item())
+    flags = res.flags.to(torch.int64) & 0xFFFFFFFF
+    n_ood = int(((flags & L.F_OOD) != 0).sum().item())
+    n_frag = int(((flags & L.F_FRAGILE) != 0).sum().item())
+    bytes_per_launch = B * (BYTES_IN + BYTES_OUT) + BYTES_PER_LOOKUP * gv
+
+    stream = torch.cuda.current_stream(dev)
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    import ctypes
+    VP = ctypes.c_void_p
+    ptrs = [VP(t.data_ptr()) for t in (s, a, d, res.valid, res.s_new, res.t_new, res.flags, res.counts)]
+
+    def step():
+        rc = T.validate_pairs_raw(B, ptrs[0], ptrs[1], ptrs[2], 0, int(args.adaptive), ptrs[3],
+                                  ptrs[4], ptrs[5], ptrs[6], ptrs[7], VP(sp))
+        if rc != 0:
+            raise gbp.GbpError(rc, "validate_pairs")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in ev:
+        e0.record(stream)
+        step()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+
+    tm = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    sums = torch.tensor([B, n_valid, n_ood, n_frag, gv], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+    elapsed = float(tm.item())
+    tot_attempts = float(sums[0].item()) * args.steps
+    value = tot_attempts / elapsed
+
+    if rank == 0:
+        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        if args.traffic_json and os.path.exists(args.traffic_json):
+            try:
+                with open(args.traffic_json) as f:
+                    tj = json.load(f)
+                if tj.get("terrain") == args.terrain and tj.get("batch") == B:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "extend-attempts/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SURVEY §8(d) synth-rough-1024, Philox-keyed attempts)",
+            "config": {
+                "workload": "config 3: synth-rough-1024, 262,144-attempt batch per GPU, "
+                            "isValidStateActionPair[Reverse] 50/50",
+                "terrain": args.terrain, "batch_per_gpu": B, "global_batch": int(sums[0].item()),
+                "seed": args.seed, "kernel": args.kernel, "waves": args.waves,
+                "adaptive": args.adaptive, "terrain_storage": ["auto", "f32", "f64"][T.info()["storage"]],
+                "parallelism": f"shard{world} (no collective on the data path)",
+            },
+            "valid_true_per_s": round(float(sums[1].item()) * args.steps / elapsed, 1),
+            "valid_fraction": float(sums[1].item()) / float(sums[0].item()),
+            "ood_fraction": float(sums[2].item()) / float(sums[0].item()),
+            "fragile": int(sums[3].item()),
+            "lookups_per_attempt": float(sums[4].item()) / float(sums[0].item()),
+            "kernel_ms_per_launch": round(kern_ms, 4),
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "kernel": "k_validate_persistent" if args.kernel == "persistent" else "k_validate_direct",
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+            },
+            "time_to_first_solution": None,
+        }
+        if world == 1 and args.cpu_seconds > 0:
+            out["cpu_baseline"] = cpu_baseline(data, s.cpu().numpy(), a.cpu().numpy(),
+                                               d.cpu().numpy(), args.cpu_seconds)
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,104 @@
+"""ctypes binding of libgbp.so (the C ABI in include/gbp.h).
+
+The library is built in-tree (global_body_planner_amd/lib/libgbp.so) by
+__graft_entry__.build() / `make -C global_body_planner_amd/csrc`.  There is no
+fallback: if the library is missing or fails to load, importing the engine
+raises, so a GPU run can never silently compute on the CPU.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libgbp.so")
+
+# ---- constants mirrored from include/gbp.h ---------------------------------
+OK = 0
+FLIGHT, STANCE, CONNECT_STANCE = 0, 1, 2
+FORWARD, REVERSE = 0, 1
+TRAPPED, ADVANCED, REACHED = 0, 1, 2
+NUM_GEN_STATES = 6
+F_VALID, F_OOD, F_NAN, F_SNEW_SET, F_TNEW_SET, F_FRAGILE, F_LIMIT = 1, 2, 4, 8, 16, 32, 64
+MAX_SAMPLES = 4096
+F_STAGE_SHIFT = 8
+F_STAGE_MASK = 0xF << F_STAGE_SHIFT
+STORAGE_AUTO, STORAGE_F32, STORAGE_F64 = 0, 1, 2
+OPT_KERNEL, OPT_BLOCK, OPT_GRID_PER_CU, OPT_WAVES = 1, 2, 3, 4
+KERNEL_DIRECT, KERNEL_PERSISTENT = 0, 1
+
+EXPORTS = [
+    "gbp_version", "gbp_status_string", "gbp_device_count", "gbp_device_alloc",
+    "gbp_device_free", "gbp_memcpy_h2d", "gbp_memcpy_d2h", "gbp_stream_synchronize",
+    "gbp_terrain_create", "gbp_terrain_destroy", "gbp_terrain_info",
+    "gbp_terrain_set_option", "gbp_terrain_get_option",
+    "gbp_height_batch_dev", "gbp_height_batch_host",
+    "gbp_normal_batch_dev", "gbp_normal_batch_host",
+    "gbp_valid_states_dev", "gbp_valid_states_host",
+    "gbp_validate_pairs_dev", "gbp_validate_pairs_host",
+    "gbp_sample_states_dev", "gbp_sample_actions_dev",
+    "gbp_extend_batch_dev", "gbp_extend_batch_host",
+    "gbp_nearest_batch_dev", "gbp_nearest_batch_host",
+]
+
+
+class GbpError(RuntimeError):
+    def __init__(self, status, what=""):
+        self.status = status
+        msg = _lib.gbp_status_string(status).decode() if _lib is not None else str(status)
+        super().__init__(f"{what}: gbp status {status} ({msg})")
+
+
+_lib = None
+
+
+def load():
+    """Load libgbp.so (raises OSError / FileNotFoundError if it is not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(
+            f"{LIB_PATH} is missing: build the HIP engine first "
+            "(python -c 'import __graft_entry__ as g; g.build()')")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, I64, U64, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t
+    sig = {
+        "gbp_version": (I, []),
+        "gbp_status_string": (ctypes.c_char_p, [I]),
+        "gbp_device_count": (I, [P]),
+        "gbp_device_alloc": (I, [I, SZ, P]),
+        "gbp_device_free": (I, [P]),
+        "gbp_memcpy_h2d": (I, [P, P, SZ, P]),
+        "gbp_memcpy_d2h": (I, [P, P, SZ, P]),
+        "gbp_stream_synchronize": (I, [P]),
+        "gbp_terrain_create": (I, [I, I, I, P, P, P, P, P, P, I, P]),
+        "gbp_terrain_destroy": (I, [P]),
+        "gbp_terrain_info": (I, [P, P, P, P, P, P]),
+        "gbp_terrain_set_option": (I, [P, I, I64]),
+        "gbp_terrain_get_option": (I, [P, I, P]),
+        "gbp_height_batch_dev": (I, [P, I64, P, P, P, P, P]),
+        "gbp_height_batch_host": (I, [P, I64, P, P, P, P]),
+        "gbp_normal_batch_dev": (I, [P, I64, P, P, P, P]),
+        "gbp_normal_batch_host": (I, [P, I64, P, P, P]),
+        "gbp_valid_states_dev": (I, [P, I64, P, P, I, P, P, P, P]),
+        "gbp_valid_states_host": (I, [P, I64, P, P, I, P, P, P]),
+        "gbp_validate_pairs_dev": (I, [P, I64, P, P, P, I, I, P, P, P, P, P, P]),
+        "gbp_validate_pairs_host": (I, [P, I64, P, P, P, I, I, P, P, P, P, P]),
+        "gbp_sample_states_dev": (I, [P, I64, U64, U64, I64, I, I, P, P, P]),
+        "gbp_sample_actions_dev": (I, [I64, P, U64, U64, I64, P, P]),
+        "gbp_extend_batch_dev": (I, [P, I64, P, P, P, I, I, U64, I64, P, P, P, P, P, P]),
+        "gbp_extend_batch_host": (I, [P, I64, P, P, P, I, I, U64, I64, P, P, P, P, P]),
+        "gbp_nearest_batch_dev": (I, [I64, P, I64, P, P, P, P]),
+        "gbp_nearest_batch_host": (I, [I64, P, I64, P, P, P]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return _lib
+
+
+def check(status, what=""):
+    if status != OK:
+        raise GbpError(status, what)
+    return status

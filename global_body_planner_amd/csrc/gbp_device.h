@@ -1,0 +1,560 @@
+// gbp_device.h — device-side building blocks of the MI355X extend/validity engine.
+//
+// Everything here is FP64 in the reference's operation order; the translation
+// unit is compiled with -ffp-contract=off (and the pragma below) so no
+// v_fma_f64 is formed: hipcc contracts a*b+c by default on gfx950.
+// Reference citations are given per function (paths relative to the reference
+// repository root).
+#pragma once
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gbp.h"
+
+namespace gbp {
+
+// ---- constants: include/global_body_planner/planning_utils.h:21-66 --------
+constexpr double H_MAX = 0.4;
+constexpr double H_MIN = 0.075;
+constexpr double V_MAX = 2.0;
+constexpr double V_NOM = 0.75;
+constexpr double P_MAX = 1.0;
+constexpr double ANG_ACC_MAX = 7.0;
+constexpr double ROBOT_L = 0.3;
+constexpr double ROBOT_W = 0.3;
+constexpr double ROBOT_H = 0.05;
+constexpr double M_CONST = 13;
+constexpr double G_CONST = 9.81;
+constexpr double F_MAX = 637;
+constexpr double MU = 1.0;
+constexpr double T_F_MAX = 0.5;
+constexpr double T_F_MIN = 0.0;
+constexpr double KINEMATICS_RES = 0.05;
+constexpr double BACKUP_RATIO = 0.5;
+constexpr double GOAL_BOUNDS = 0.5;
+constexpr double MY_PI = 3.14159;
+constexpr double FRAGILE_EPS = 1e-12;
+constexpr uint32_t PURPOSE_STATE = 1u;
+constexpr uint32_t PURPOSE_ACTION = 2u;
+
+__device__ __forceinline__ double std_min(double a, double b) { return (b < a) ? b : a; }
+__device__ __forceinline__ double std_max(double a, double b) { return (a < b) ? b : a; }
+
+// ---- device terrain view ----------------------------------------------------
+// x-major height grid z[ix*ny + iy] (== FastTerrainMap::z_data_[ix][iy]) in
+// fp32 (lossless for grid_map maps, whose layers are float) or fp64.
+template <class ZT>
+struct TerrainView {
+  const double *x, *y;           // coordinates (ascending)
+  const ZT *z;                   // heights, x-major
+  const double *dx, *dy, *dz;    // slope layers, x-major fp64, may be null
+  int nx, ny;
+  double x0, xN, y0, yN;         // x[0], x[nx-1], y[0], y[ny-1]
+  double inv_hx, inv_hy;         // 1 / mean spacing (bracket guess only)
+};
+
+// First i with d[i] <= v < d[i+1] (fast_terrain_map.cpp:101-117).  O(1): a
+// guess from the mean spacing, then a fix-up against the actual coordinates,
+// so the result equals the reference's linear scan for any ascending vector.
+// No bracket: BR_LOW when v is NaN or below d[0] (the scan never reads past
+// the end; the reference keeps index 0), BR_HIGH when v >= d[n-1] (the scan
+// reads d[n]: UB).
+constexpr int BR_LOW = -1;
+constexpr int BR_HIGH = -2;
+
+__device__ __forceinline__ int bracket(const double *__restrict__ d, int n, double d0,
+                                       double dN, double inv, double v) {
+  if (!(v >= d0 && v < dN)) return (v >= dN) ? BR_HIGH : BR_LOW;
+  const double g = (v - d0) * inv;
+  int i = (int)g;
+  i = i < 0 ? 0 : (i > n - 2 ? n - 2 : i);
+  while (i > 0 && v < d[i]) --i;
+  while (i < n - 2 && v >= d[i + 1]) ++i;
+  return i;
+}
+
+template <class ZT>
+__device__ __forceinline__ void load_quad(const TerrainView<ZT> &T, int ix, int iy, double &f11,
+                                          double &f12, double &f21, double &f22) {
+  const ZT *p = T.z + (size_t)ix * T.ny + iy;
+  f11 = (double)p[0];
+  f12 = (double)p[1];
+  f21 = (double)p[T.ny];
+  f22 = (double)p[T.ny + 1];
+}
+
+// FastTerrainMap::heightIsNan (fast_terrain_map.cpp:135-157): -1 = UB
+// (BR_HIGH on an axis), else the reference's bool (BR_LOW -> index 0)
+template <class ZT>
+__device__ __forceinline__ int nan_at(const TerrainView<ZT> &T, double x, double y) {
+  const int ix = bracket(T.x, T.nx, T.x0, T.xN, T.inv_hx, x);
+  const int iy = bracket(T.y, T.ny, T.y0, T.yN, T.inv_hy, y);
+  if (ix == BR_HIGH || iy == BR_HIGH) return -1;
+  double f11, f12, f21, f22;
+  load_quad(T, ix < 0 ? 0 : ix, iy < 0 ? 0 : iy, f11, f12, f21, f22);
+  return (isnan(f11) || isnan(f12) || isnan(f21) || isnan(f22)) ? 1 : 0;
+}
+
+// fast_terrain_map.cpp:124-126 (left-to-right evaluation, no contraction)
+__device__ __forceinline__ double bilinear(double f11, double f12, double f21, double f22,
+                                           double x1, double x2, double y1, double y2,
+                                           double x, double y) {
+  return 1.0 / ((x2 - x1) * (y2 - y1)) *
+         (f11 * (x2 - x) * (y2 - y) + f21 * (x - x1) * (y2 - y) + f12 * (x2 - x) * (y - y1) +
+          f22 * (x - x1) * (y - y1));
+}
+
+// FastTerrainMap::getGroundHeight (fast_terrain_map.cpp:94-132).  Returns
+// false for UB (finite point without bracket).  NaN coordinates give NaN
+// (whatever the uninitialised x1..y2 hold).  `near` is set when the point is
+// within FRAGILE_EPS of a grid line.
+template <class ZT>
+__device__ __forceinline__ bool height_at(const TerrainView<ZT> &T, double x, double y,
+                                          double &h, bool &near) {
+  if (isnan(x) || isnan(y)) {
+    h = __builtin_nan("");
+    return true;
+  }
+  const int ix = bracket(T.x, T.nx, T.x0, T.xN, T.inv_hx, x);
+  const int iy = bracket(T.y, T.ny, T.y0, T.yN, T.inv_hy, y);
+  if (ix < 0 || iy < 0) return false;
+  const double x1 = T.x[ix], x2 = T.x[ix + 1], y1 = T.y[iy], y2 = T.y[iy + 1];
+  double f11, f12, f21, f22;
+  load_quad(T, ix, iy, f11, f12, f21, f22);
+  near = near || fabs(x - x1) < FRAGILE_EPS || fabs(x2 - x) < FRAGILE_EPS ||
+         fabs(y - y1) < FRAGILE_EPS || fabs(y2 - y) < FRAGILE_EPS;
+  h = bilinear(f11, f12, f21, f22, x1, x2, y1, y2, x, y);
+  return true;
+}
+
+// fast_terrain_map.cpp:160-213
+template <class ZT>
+__device__ __forceinline__ bool surface_normal(const TerrainView<ZT> &T, double x, double y,
+                                               double n[3]) {
+  const int ix = bracket(T.x, T.nx, T.x0, T.xN, T.inv_hx, x);
+  const int iy = bracket(T.y, T.ny, T.y0, T.yN, T.inv_hy, y);
+  if (isnan(x) || isnan(y) || ix < 0 || iy < 0) {
+    n[0] = n[1] = n[2] = __builtin_nan("");
+    return isnan(x) || isnan(y);  // NaN coordinates: deterministic NaN, not UB
+  }
+  if (!T.dx) {
+    n[0] = 0.0; n[1] = 0.0; n[2] = 1.0;
+    return true;
+  }
+  double x1 = T.x[ix], x2 = T.x[ix + 1], y1 = T.y[iy], y2 = T.y[iy + 1];
+  size_t b = (size_t)ix * T.ny + iy;
+  const double *L[3] = {T.dx, T.dy, T.dz};
+#pragma unroll
+  for (int k = 0; k < 3; k++)
+    n[k] = bilinear(L[k][b], L[k][b + 1], L[k][b + T.ny], L[k][b + T.ny + 1], x1, x2, y1, y2, x,
+                    y);
+  return true;
+}
+
+// ---- propagation --------------------------------------------------------------
+// planning_utils.cpp:237-274
+__device__ __forceinline__ void apply_stance(const double *s, const double *a, double t,
+                                             double *o) {
+  const double a_x_td = a[0], a_y_td = a[1], a_z_td = a[2];
+  const double a_x_to = a[3], a_y_to = a[4], a_z_to = a[5];
+  const double t_s = a[6], a_p_td = a[8], a_p_to = a[9];
+  o[0] = s[0] + s[3] * t + 0.5 * a_x_td * t * t + (a_x_to - a_x_td) * (t * t * t) / (6.0 * t_s);
+  o[1] = s[1] + s[4] * t + 0.5 * a_y_td * t * t + (a_y_to - a_y_td) * (t * t * t) / (6.0 * t_s);
+  o[2] = s[2] + s[5] * t + 0.5 * a_z_td * t * t + (a_z_to - a_z_td) * (t * t * t) / (6.0 * t_s);
+  o[3] = s[3] + a_x_td * t + (a_x_to - a_x_td) * t * t / (2.0 * t_s);
+  o[4] = s[4] + a_y_td * t + (a_y_to - a_y_td) * t * t / (2.0 * t_s);
+  o[5] = s[5] + a_z_td * t + (a_z_to - a_z_td) * t * t / (2.0 * t_s);
+  o[6] = s[6] + s[7] * t + 0.5 * a_p_td * t * t + (a_p_to - a_p_td) * (t * t * t) / (6.0 * t_s);
+  o[7] = s[7] + a_p_td * t + (a_p_to - a_p_td) * t * t / (2.0 * t_s);
+}
+
+// planning_utils.cpp:282-306 (g is the literal 9.81)
+__device__ __forceinline__ void apply_flight(const double *s, double t_f, double *o) {
+  const double g = 9.81;
+  o[0] = s[0] + s[3] * t_f;
+  o[1] = s[1] + s[4] * t_f;
+  o[2] = s[2] + s[5] * t_f - 0.5 * g * t_f * t_f;
+  o[3] = s[3];
+  o[4] = s[4];
+  o[5] = s[5] - g * t_f;
+  o[6] = s[6] + s[7] * t_f;
+  o[7] = s[7];
+}
+
+// planning_utils.cpp:324-367
+__device__ __forceinline__ void apply_stance_reverse(const double *s, const double *a, double t,
+                                                     double *o) {
+  const double a_x_td = a[0], a_y_td = a[1], a_z_td = a[2];
+  const double a_x_to = a[3], a_y_to = a[4], a_z_to = a[5];
+  const double t_s = a[6], a_p_td = a[8], a_p_to = a[9];
+  const double cx = s[3] - a_x_td * t_s - 0.5 * (a_x_to - a_x_td) * t_s;
+  const double cy = s[4] - a_y_td * t_s - 0.5 * (a_y_to - a_y_td) * t_s;
+  const double cz = s[5] - a_z_td * t_s - 0.5 * (a_z_to - a_z_td) * t_s;
+  const double cp = s[7] - a_p_td * t_s - 0.5 * (a_p_to - a_p_td) * t_s;
+  const double d1 = t_s - t, d2 = t_s * t_s - t * t, d3 = t_s * t_s * t_s - t * t * t;
+  o[0] = s[0] - cx * d1 - 0.5 * a_x_td * d2 - (a_x_to - a_x_td) * d3 / (6.0 * t_s);
+  o[1] = s[1] - cy * d1 - 0.5 * a_y_td * d2 - (a_y_to - a_y_td) * d3 / (6.0 * t_s);
+  o[2] = s[2] - cz * d1 - 0.5 * a_z_td * d2 - (a_z_to - a_z_td) * d3 / (6.0 * t_s);
+  o[3] = s[3] - a_x_td * d1 - (a_x_to - a_x_td) * d2 / (2.0 * t_s);
+  o[4] = s[4] - a_y_td * d1 - (a_y_to - a_y_td) * d2 / (2.0 * t_s);
+  o[5] = s[5] - a_z_td * d1 - (a_z_to - a_z_td) * d2 / (2.0 * t_s);
+  o[7] = s[7] - a_p_td * d1 - (a_p_to - a_p_td) * d2 / (2.0 * t_s);
+  o[6] = s[6] - cp * d1 - 0.5 * a_p_td * d2 - (a_p_to - a_p_td) * d3 / (6.0 * t_s);
+}
+
+// planning_utils.cpp:519-556
+__device__ __forceinline__ bool is_valid_action(const double *a) {
+  if ((a[6] <= 0) || (a[7] < 0)) return false;
+  const double m = M_CONST, g = G_CONST, mu = MU;
+  const double f_x_td = m * a[0], f_y_td = m * a[1], f_z_td = m * (a[2] + g);
+  const double f_x_to = m * a[3], f_y_to = m * a[4], f_z_to = m * (a[5] + g);
+  if ((sqrt(f_x_td * f_x_td + f_y_td * f_y_td + f_z_td * f_z_td) >= F_MAX) ||
+      (sqrt(f_x_to * f_x_to + f_y_to * f_y_to + f_z_to * f_z_to) >= F_MAX) || (f_z_td < 0) ||
+      (f_z_to < 0) || (a[8] >= F_MAX) || (a[9] >= F_MAX))
+    return false;
+  if ((sqrt(f_x_td * f_x_td + f_y_td * f_y_td) >= mu * f_z_td) ||
+      (sqrt(f_x_to * f_x_to + f_y_to * f_y_to) >= mu * f_z_to))
+    return false;
+  return true;
+}
+
+// ---- state validity: planning_utils.cpp:562-635 ------------------------------
+// Out-of-domain convention: a reached lookup with no bracket makes
+// the state invalid; GBP_F_OOD marks the cases where the reference's decision
+// depends on its UB read.  G/V follow the reference's executed calls.
+struct Acc {
+  uint32_t G, V, flags;
+};
+
+template <class ZT>
+__device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int phase, Acc &acc) {
+  if (acc.V >= GBP_MAX_SAMPLES) {  // engine guard: the reference loop would not terminate
+    acc.flags |= GBP_F_LIMIT;
+    return false;
+  }
+  acc.V++;
+  // (1) heightIsNan(centre) :564
+  const int r = nan_at(T, s[0], s[1]);
+  if (r < 0) {  // x or y >= the last coordinate: rejected by (2) unless exactly equal
+    const bool in_closed = !(s[0] < T.x0 || s[0] > T.xN || s[1] < T.y0 || s[1] > T.yN);
+    if (in_closed) acc.flags |= GBP_F_OOD;
+    return false;
+  }
+  if (r) {
+    acc.flags |= GBP_F_NAN;
+    return false;
+  }
+  // (2) bounds + |pitch| :568-571
+  if ((s[0] < T.x0) || (s[0] > T.xN) || (s[1] < T.y0) || (s[1] > T.yN) || (fabs(s[6]) >= P_MAX))
+    return false;
+  // (3) horizontal speed :574
+  if (sqrt(s[3] * s[3] + s[4] * s[4]) > V_MAX) return false;
+  // (4) rotation :578-594
+#ifdef GBP_EXPERIMENT_NO_TRIG
+  const double yaw = s[4] * s[3];
+  const double cy = yaw * 0.5, sy = yaw * 0.25;
+  const double pitch = s[6];
+  const double cp = pitch * 0.5, sp = pitch * 0.25;
+#else
+  const double yaw = atan2(s[4], s[3]);
+  const double cy = cos(yaw), sy = sin(yaw);
+  const double pitch = s[6];
+  const double cp = cos(pitch), sp = sin(pitch);
+#endif
+  const double R_11 = cy * cp, R_12 = -sy, R_13 = cy * sp;
+  const double R_21 = sy * cp, R_22 = cy, R_23 = sy * sp;
+  const double R_31 = -sp, R_32 = 0, R_33 = cp;
+  const double z_body = -ROBOT_H;
+  // (5) four corners :601-627, x_body outer, y_body inner (not unrolled: keeps
+  // one corner's cells live at a time)
+#pragma unroll 1
+  for (int k = 0; k < 4; k++) {
+    const double x_body = (k < 2) ? -0.5 * ROBOT_L : 0.5 * ROBOT_L;
+    const double y_body = (k & 1) ? 0.5 * ROBOT_W : -0.5 * ROBOT_W;
+    const double x_leg = s[0] + R_11 * x_body + R_12 * y_body;
+    const double y_leg = s[1] + R_21 * x_body + R_22 * y_body;
+    const double z_leg = s[2] + R_31 * x_body + R_32 * y_body;
+    const double x_corner = x_leg + R_13 * z_body;
+    const double y_corner = y_leg + R_23 * z_body;
+    const double z_corner = z_leg + R_33 * z_body;
+    const int rl = nan_at(T, x_leg, y_leg);  // heightIsNan(leg) :614
+    if (rl < 0) {
+      acc.flags |= GBP_F_OOD;
+      return false;
+    }
+    if (rl) {
+      acc.flags |= GBP_F_NAN;
+      return false;
+    }
+    acc.G += 2;  // both heights computed before the test :618-619
+    double gl, gc;
+    bool near = false;
+    const bool okl = height_at(T, x_leg, y_leg, gl, near);
+    if (near) acc.flags |= GBP_F_FRAGILE;
+    if (!okl) {
+      acc.flags |= GBP_F_OOD;
+      return false;
+    }
+    const bool okc = height_at(T, x_corner, y_corner, gc, near);
+    if (near) acc.flags |= GBP_F_FRAGILE;
+    if (!okc) {
+      acc.flags |= GBP_F_OOD;
+      return false;
+    }
+    const double leg_height = z_leg - gl;
+    const double corner_height = z_corner - gc;
+    if (fabs(corner_height - H_MIN) < FRAGILE_EPS ||
+        (phase == GBP_STANCE && fabs(leg_height - H_MAX) < FRAGILE_EPS))
+      acc.flags |= GBP_F_FRAGILE;
+    if ((corner_height < H_MIN) || ((phase == GBP_STANCE) && (leg_height > H_MAX))) return false;
+  }
+  // (6) underside centre :630-632
+  acc.G++;
+  double gu;
+  bool near = false;
+  const bool oku = height_at(T, s[0] + R_13 * z_body, s[1] + R_23 * z_body, gu, near);
+  if (near) acc.flags |= GBP_F_FRAGILE;
+  if (!oku) {
+    acc.flags |= GBP_F_OOD;
+    return false;
+  }
+  const double height = (s[2] + R_33 * z_body) - gu;
+  if (fabs(height - H_MIN) < FRAGILE_EPS) acc.flags |= GBP_F_FRAGILE;
+  if (height < H_MIN) return false;
+  return true;
+}
+
+__device__ __forceinline__ uint32_t stage_bits(uint32_t k) { return k << GBP_F_STAGE_SHIFT; }
+
+// ---- pair checks, one lane per attempt (the "direct" form) ------------------
+// planning_utils.cpp:713-753 (plain) and :651-712 (adaptive)
+template <class ZT, bool ADAPTIVE>
+__device__ bool pair_forward(const TerrainView<ZT> &T, const double *s, const double *a,
+                             double *s_new, double &t_new, Acc &acc, uint32_t &f) {
+  const double t_s = a[6], t_f = a[7];
+  double sc[8];
+  double time_step = KINEMATICS_RES, t_pre_success = 0;
+  f = (f & ~GBP_F_STAGE_MASK) | stage_bits(GBP_STAGE_FWD_STANCE);
+  for (double t = 0; t <= t_s; t += (ADAPTIVE ? time_step : KINEMATICS_RES)) {
+    apply_stance(s, a, t, sc);
+    if (!is_valid_state(T, sc, GBP_STANCE, acc)) {
+      if (acc.flags & GBP_F_LIMIT) return false;
+      if (!ADAPTIVE || (KINEMATICS_RES - 0.01 <= time_step && time_step <= KINEMATICS_RES + 0.01)) {
+        apply_stance(s, a, (1.0 - BACKUP_RATIO) * t, s_new);
+        f |= GBP_F_SNEW_SET;
+        return false;
+      }
+      time_step = KINEMATICS_RES;
+      t = t_pre_success;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++) s_new[k] = sc[k];
+      t_new = t;
+      f |= GBP_F_SNEW_SET | GBP_F_TNEW_SET;
+      if (ADAPTIVE) {
+        time_step += KINEMATICS_RES;
+        t_pre_success = t;
+      }
+    }
+  }
+  double s_takeoff[8];
+  apply_stance(s, a, a[6], s_takeoff);
+  time_step = KINEMATICS_RES;
+  f = (f & ~GBP_F_STAGE_MASK) | stage_bits(GBP_STAGE_FWD_FLIGHT);
+  for (double t = 0; t < t_f; t += (ADAPTIVE ? time_step : KINEMATICS_RES)) {
+    apply_flight(s_takeoff, t, sc);
+    if (!is_valid_state(T, sc, GBP_FLIGHT, acc)) return false;
+    if (ADAPTIVE) time_step += KINEMATICS_RES;
+  }
+  f = (f & ~GBP_F_STAGE_MASK) | stage_bits(GBP_STAGE_FWD_LAND);
+  apply_flight(s_takeoff, t_f, sc);
+  if (!is_valid_state(T, sc, GBP_STANCE, acc)) return false;
+#pragma unroll
+  for (int k = 0; k < 8; k++) s_new[k] = sc[k];
+  t_new = t_s + t_f;
+  f |= GBP_F_SNEW_SET | GBP_F_TNEW_SET;
+  return true;
+}
+
+// planning_utils.cpp:837-876 (plain) and :774-836 (adaptive)
+template <class ZT, bool ADAPTIVE>
+__device__ bool pair_reverse(const TerrainView<ZT> &T, const double *s, const double *a,
+                             double *s_new, double &t_new, Acc &acc, uint32_t &f) {
+  const double t_s = a[6], t_f = a[7];
+  double sc[8];
+  double time_step = KINEMATICS_RES, t_pre_success = 0;
+  f = (f & ~GBP_F_STAGE_MASK) | stage_bits(GBP_STAGE_REV_FLIGHT);
+  for (double t = 0; t < t_f; t += (ADAPTIVE ? time_step : KINEMATICS_RES)) {
+    apply_flight(s, -t, sc);
+    if (!is_valid_state(T, sc, GBP_FLIGHT, acc)) return false;
+    if (ADAPTIVE) time_step += KINEMATICS_RES;
+  }
+  double s_takeoff[8];
+  apply_flight(s, -t_f, s_takeoff);
+  time_step = KINEMATICS_RES;
+  f = (f & ~GBP_F_STAGE_MASK) | stage_bits(GBP_STAGE_REV_STANCE);
+  for (double t = t_s; t >= 0; t -= (ADAPTIVE ? time_step : KINEMATICS_RES)) {
+    apply_stance_reverse(s_takeoff, a, t, sc);
+    if (!is_valid_state(T, sc, GBP_STANCE, acc)) {
+      if (acc.flags & GBP_F_LIMIT) return false;
+      if (!ADAPTIVE || (KINEMATICS_RES - 0.01 <= time_step && time_step <= KINEMATICS_RES + 0.01)) {
+        apply_stance(s, a, t + BACKUP_RATIO * (t_s - t), s_new);  // forward stance, as written (:857)
+        f |= GBP_F_SNEW_SET;
+        return false;
+      }
+      time_step = KINEMATICS_RES;
+      t = t_pre_success;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++) s_new[k] = sc[k];
+      t_new = t_s - t;
+      f |= GBP_F_SNEW_SET | GBP_F_TNEW_SET;
+      if (ADAPTIVE) {
+        time_step += KINEMATICS_RES;
+        t_pre_success = t;
+      }
+    }
+  }
+  f = (f & ~GBP_F_STAGE_MASK) | stage_bits(GBP_STAGE_REV_START);
+  apply_stance_reverse(s_takeoff, a, 0, sc);
+  if (!is_valid_state(T, sc, GBP_STANCE, acc)) return false;
+#pragma unroll
+  for (int k = 0; k < 8; k++) s_new[k] = sc[k];
+  t_new = t_s;
+  f |= GBP_F_SNEW_SET | GBP_F_TNEW_SET;
+  return true;
+}
+
+// ---- distances: planning_utils.cpp:106-127 -------------------------------------
+__device__ __forceinline__ double state_distance(const double *q1, const double *q2) {
+  double sum = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) sum = sum + 1.0 * (q2[i] - q1[i]) * (q2[i] - q1[i]);
+  return sqrt(sum);
+}
+
+// ---- Philox4x32-10 counter RNG (Salmon et al., SC'11) -------------------------
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+    const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0;
+    c[1] = lo1;
+    c[2] = n2;
+    c[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+// two uniforms in [0,1) for (seed, stream_id, purpose, index, draw)
+__device__ __forceinline__ void uniform2(uint64_t seed, uint64_t stream_id, uint32_t purpose,
+                                         int64_t index, uint32_t draw, double &u0, double &u1) {
+  uint32_t c[4] = {draw, (uint32_t)(uint64_t)index, (uint32_t)((uint64_t)index >> 32),
+                   (uint32_t)stream_id ^ (purpose << 24)};
+  philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(stream_id >> 32));
+  const uint64_t w0 = ((uint64_t)c[1] << 32) | c[0];
+  const uint64_t w1 = ((uint64_t)c[3] << 32) | c[2];
+  u0 = (double)(w0 >> 11) * 0x1p-53;
+  u1 = (double)(w1 >> 11) * 0x1p-53;
+}
+
+__device__ __forceinline__ void box_muller(double u1, double u2, double &z0, double &z1) {
+  const double r = sqrt(-2.0 * log(1.0 - u1));
+  const double th = 6.283185307179586 * u2;
+  z0 = r * cos(th);
+  z1 = r * sin(th);
+}
+
+// planning_utils.cpp:198-231 (Eigen cross / norm / I + [v]x + [v]x^2 (1-c)/s^2)
+__device__ __forceinline__ void rotate_grf(const double *n, const double *f, double *out) {
+  const double v0 = n[1] * 1.0 - n[2] * 0.0;
+  const double v1 = n[2] * 0.0 - n[0] * 1.0;
+  const double v2 = n[0] * 0.0 - n[1] * 0.0;
+  const double s = sqrt(v0 * v0 + v1 * v1 + v2 * v2);
+  const double c = n[0] * 0.0 + n[1] * 0.0 + n[2] * 1.0;
+  if (s < 0.000001) {
+    out[0] = f[0]; out[1] = f[1]; out[2] = f[2];
+    return;
+  }
+  const double K[3][3] = {{0, -v2, v1}, {v2, 0, -v0}, {-v1, v0, 0}};
+  double R[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const double kk = K[i][0] * K[0][j] + K[i][1] * K[1][j] + K[i][2] * K[2][j];
+      R[i][j] = (i == j ? 1.0 : 0.0) + K[i][j] + kk * (1 - c) / (s * s);
+    }
+#pragma unroll
+  for (int i = 0; i < 3; i++) out[i] = R[i][0] * f[0] + R[i][1] * f[1] + R[i][2] * f[2];
+}
+
+// planning_utils.cpp:392-442, the reference's rand()/RAND_MAX replaced by
+// counter-addressed uniforms (draws 0..4 of (stream_id, index)).
+__device__ __forceinline__ void sample_action(const double *nrm, uint64_t seed, uint64_t stream_id,
+                                              int64_t index, double *a) {
+  double u[10];
+#pragma unroll
+  for (uint32_t d = 0; d < 5; d++) uniform2(seed, stream_id, PURPOSE_ACTION, index, d, u[2 * d], u[2 * d + 1]);
+  const double f_z_td = F_MAX * u[0];
+  const double f_z_to = F_MAX * u[1];
+  const double f_td[3] = {2 * MU * f_z_td * u[2] - MU * f_z_td, 2 * MU * f_z_td * u[4] - MU * f_z_td,
+                          f_z_td};
+  const double f_to[3] = {2 * MU * f_z_to * u[3] - MU * f_z_to, 2 * MU * f_z_to * u[5] - MU * f_z_to,
+                          f_z_to};
+  double r_td[3], r_to[3];
+  rotate_grf(nrm, f_td, r_td);
+  rotate_grf(nrm, f_to, r_to);
+  a[0] = r_td[0] / M_CONST;
+  a[1] = r_td[1] / M_CONST;
+  a[2] = r_td[2] / M_CONST - G_CONST;
+  a[3] = r_to[0] / M_CONST;
+  a[4] = r_to[1] / M_CONST;
+  a[5] = r_to[2] / M_CONST - G_CONST;
+  a[6] = 0.3;
+  a[7] = (T_F_MAX - T_F_MIN) * u[6] + T_F_MIN;
+  double z0, z1;
+  box_muller(u[8], u[9], z0, z1);
+  a[8] = std_max(std_min(z0 * (ANG_ACC_MAX / 4.0) + 0.0, ANG_ACC_MAX), -ANG_ACC_MAX);
+  a[9] = std_max(std_min(z1 * (ANG_ACC_MAX / 4.0) + 0.0, ANG_ACC_MAX), -ANG_ACC_MAX);
+}
+
+// planner_class.cpp:38-76, one try k of index i (draws 4k .. 4k+3)
+template <class ZT>
+__device__ __forceinline__ void sample_state_try(const TerrainView<ZT> &T, uint64_t seed,
+                                                 uint64_t stream_id, int64_t index, int k,
+                                                 double *q) {
+  const double z_min_rel = H_MIN + ROBOT_H, z_max_rel = H_MAX + ROBOT_H;
+  const double mean = 0.5 * (z_max_rel + z_min_rel);
+  const double sd = (z_max_rel - z_min_rel) * (1.0 / (2 * 3.0));
+  double u00, u01, u10, u11, u20, u21, u30, u31;
+  uniform2(seed, stream_id, PURPOSE_STATE, index, 4u * k + 0, u00, u01);
+  uniform2(seed, stream_id, PURPOSE_STATE, index, 4u * k + 1, u10, u11);
+  uniform2(seed, stream_id, PURPOSE_STATE, index, 4u * k + 2, u20, u21);
+  uniform2(seed, stream_id, PURPOSE_STATE, index, 4u * k + 3, u30, u31);
+  double z0, z1;
+  box_muller(u10, u11, z0, z1);
+  const double hz = z0 * sd + mean;
+  q[0] = (T.xN - T.x0) * u00 + T.x0;
+  q[1] = (T.yN - T.y0) * u01 + T.y0;
+  double g;
+  bool near = false;
+  if (!height_at(T, q[0], q[1], g, near)) g = __builtin_nan("");
+  q[2] = std_max(std_min(hz, z_max_rel), z_min_rel) + g;
+  const double phi = (2.0 * MY_PI) * u20;
+  const double cos_theta = 2.0 * u21 - 1.0;
+  const double theta = acos(cos_theta);
+  const double v = u30 * V_MAX;
+  q[3] = v * sin(theta) * cos(phi);
+  q[4] = v * sin(theta) * sin(phi);
+  q[5] = v * cos(theta);
+  q[6] = 2 * P_MAX * u31 - P_MAX;
+  q[7] = 0.0;
+}
+
+}  // namespace gbp

@@ -1,0 +1,1206 @@
+// gbp_engine.hip — HIP kernels (gfx950, wave64) + the C ABI of include/gbp.h.
+//
+// Kernels:
+//   K1 k_height / k_normal        batched FastTerrainMap lookups
+//   K2 k_validate_direct          one lane per state-action pair
+//   K2 k_validate_persistent      persistent waves; every lane evaluates ONE
+//                                 sampled state per step and refills from a
+//                                 global work counter as soon as its pair is
+//                                 decided, so a wave never idles behind one
+//                                 long-lived attempt (divergence is the cost
+//                                 centre: most pairs die in 1-3 samples, a few
+//                                 run ~19, SURVEY §7 "Divergence")
+//   K3 k_sample_states / k_sample_actions / k_extend_prep / k_extend_select
+//   K5 k_nearest                  (distance, index) lexicographic argmin
+// MFMA is not used: there is no dense contraction on this path.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "gbp.h"
+#include "gbp_device.h"
+
+using namespace gbp;
+
+namespace {
+
+constexpr uint64_t EXTEND_STREAM = 0x45585444ull;  // "EXTD"
+constexpr int WAVE = 64;
+
+// ============================================================================
+// K1: batched terrain queries
+// ============================================================================
+template <class ZT>
+__global__ void k_height(TerrainView<ZT> T, int64_t n, const double *__restrict__ xy,
+                         double *__restrict__ h, uint8_t *__restrict__ is_nan,
+                         uint8_t *__restrict__ ood) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const double x = xy[2 * i], y = xy[2 * i + 1];
+    double v;
+    bool near = false;
+    const bool ok = height_at(T, x, y, v, near);      // getGroundHeight
+    const int r = nan_at(T, x, y);                     // heightIsNan
+    if (h) h[i] = ok ? v : __builtin_nan("");
+    if (is_nan) is_nan[i] = r != 0 ? 1 : 0;            // UB (-1) reported as 1, like ood
+    if (ood) ood[i] = (!ok || r < 0) ? 1 : 0;
+  }
+}
+
+template <class ZT>
+__global__ void k_normal(TerrainView<ZT> T, int64_t n, const double *__restrict__ xy,
+                         double *__restrict__ nrm, uint8_t *__restrict__ ood) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double v[3];
+    const bool ok = surface_normal(T, xy[2 * i], xy[2 * i + 1], v);
+    nrm[3 * i] = v[0];
+    nrm[3 * i + 1] = v[1];
+    nrm[3 * i + 2] = v[2];
+    if (ood) ood[i] = ok ? 0 : 1;
+  }
+}
+
+template <class ZT>
+__global__ void k_valid_states(TerrainView<ZT> T, int64_t n, const double *__restrict__ states,
+                               const uint8_t *__restrict__ phase, int phase_all,
+                               uint8_t *__restrict__ valid, uint32_t *__restrict__ flags,
+                               uint32_t *__restrict__ counts) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double s[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) s[k] = states[8 * i + k];
+    Acc acc{0, 0, 0};
+    const bool v = is_valid_state(T, s, phase ? phase[i] : phase_all, acc);
+    if (valid) valid[i] = v;
+    if (flags) flags[i] = acc.flags | (v ? GBP_F_VALID : 0u);
+    if (counts) counts[i] = (acc.G & 0xFFFFu) | (acc.V << 16);
+  }
+}
+
+// ============================================================================
+// K2 (direct): one lane per pair, the reference loops as written
+// ============================================================================
+// W = minimum waves per SIMD requested from the register allocator
+// (__launch_bounds__ 2nd argument): 1 -> up to 512 VGPR+AGPR, 2 -> 256, 4 -> 128.
+template <class ZT, bool ADAPTIVE, int W>
+__global__ __launch_bounds__(256, W) void k_validate_direct(
+    TerrainView<ZT> T, int64_t n, const double *__restrict__ S, const double *__restrict__ A,
+    const uint8_t *__restrict__ dir, int dir_all, uint8_t *__restrict__ valid,
+    double *__restrict__ s_new, double *__restrict__ t_new, uint32_t *__restrict__ flags,
+    uint32_t *__restrict__ counts) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s[8], a[10], sn[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) s[k] = S[8 * i + k];
+#pragma unroll
+  for (int k = 0; k < 10; k++) a[k] = A[10 * i + k];
+  double tn = 0;
+  Acc acc{0, 0, 0};
+  uint32_t f = 0;
+  const int d = dir ? dir[i] : dir_all;
+  const bool v = (d == GBP_FORWARD) ? pair_forward<ZT, ADAPTIVE>(T, s, a, sn, tn, acc, f)
+                                    : pair_reverse<ZT, ADAPTIVE>(T, s, a, sn, tn, acc, f);
+  f |= acc.flags | (v ? GBP_F_VALID : 0u);
+  if (valid) valid[i] = v;
+  if (s_new && (f & GBP_F_SNEW_SET)) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) s_new[8 * i + k] = sn[k];
+  }
+  if (t_new && (f & GBP_F_TNEW_SET)) t_new[i] = tn;
+  flags[i] = f;
+  if (counts) counts[i] = (acc.G & 0xFFFFu) | (acc.V << 16);
+}
+
+// ============================================================================
+// K2 (persistent): per-sample state machine with lane re-packing
+// ============================================================================
+enum : int {
+  ST_IDLE = 0,
+  ST_FWD_STANCE = GBP_STAGE_FWD_STANCE,
+  ST_FWD_FLIGHT = GBP_STAGE_FWD_FLIGHT,
+  ST_FWD_LAND = GBP_STAGE_FWD_LAND,
+  ST_REV_FLIGHT = GBP_STAGE_REV_FLIGHT,
+  ST_REV_STANCE = GBP_STAGE_REV_STANCE,
+  ST_REV_START = GBP_STAGE_REV_START,
+};
+// deferred s_new: recomputed once at the end from (kind, param) — the same
+// closed form and the same operands the reference assigned it from
+enum : int { SN_NONE = 0, SN_STANCE_S = 1, SN_FLIGHT_B = 2, SN_STANCE_REV_B = 3 };
+
+struct Lane {
+  double s[8], a[10], b[8];  // input state, action, take-off state of the phase
+  double t, ts, tpre;        // sample time, adaptive step, last success time
+  double snew_p, tnew;
+  int stage, snew_kind;
+  uint32_t f, tnew_set;
+  Acc acc;
+  int idx;
+};
+
+// enter a stage, skipping loops whose condition is false on entry
+__device__ __forceinline__ void enter_stage(Lane &L, int st) {
+  for (;;) {
+    L.f = (L.f & ~GBP_F_STAGE_MASK) | stage_bits((uint32_t)st);
+    L.stage = st;
+    L.ts = KINEMATICS_RES;
+    L.tpre = 0;
+    switch (st) {
+      case ST_FWD_STANCE:  // planning_utils.cpp:718
+        L.t = 0;
+        if (L.t <= L.a[6]) return;
+        st = ST_FWD_FLIGHT;
+        break;
+      case ST_FWD_FLIGHT:  // :732-735
+        apply_stance(L.s, L.a, L.a[6], L.b);
+        L.t = 0;
+        if (L.t < L.a[7]) return;
+        st = ST_FWD_LAND;
+        break;
+      case ST_REV_FLIGHT:  // :842
+        L.t = 0;
+        if (L.t < L.a[7]) return;
+        st = ST_REV_STANCE;
+        break;
+      case ST_REV_STANCE:  // :849-852
+        apply_flight(L.s, -L.a[7], L.b);
+        L.t = L.a[6];
+        if (L.t >= 0) return;
+        st = ST_REV_START;
+        break;
+      default:  // FWD_LAND, REV_START: exactly one sample
+        return;
+    }
+  }
+}
+
+template <bool ADAPTIVE>
+__device__ __forceinline__ bool small_step(double ts) {
+  return !ADAPTIVE || (KINEMATICS_RES - 0.01 <= ts && ts <= KINEMATICS_RES + 0.01);
+}
+
+// returns true when the pair is decided (L.f has VALID set or not)
+template <class ZT, bool ADAPTIVE>
+__device__ __forceinline__ bool step_lane(const TerrainView<ZT> &T, Lane &L) {
+  double sc[8];
+  int phase = GBP_STANCE;
+  switch (L.stage) {
+    case ST_FWD_STANCE: apply_stance(L.s, L.a, L.t, sc); break;
+    case ST_FWD_FLIGHT: apply_flight(L.b, L.t, sc); phase = GBP_FLIGHT; break;
+    case ST_FWD_LAND: apply_flight(L.b, L.a[7], sc); break;
+    case ST_REV_FLIGHT: apply_flight(L.s, -L.t, sc); phase = GBP_FLIGHT; break;
+    case ST_REV_STANCE: apply_stance_reverse(L.b, L.a, L.t, sc); break;
+    default: apply_stance_reverse(L.b, L.a, 0, sc); break;  // ST_REV_START
+  }
+  const bool ok = is_valid_state(T, sc, phase, L.acc);
+  if (L.acc.flags & GBP_F_LIMIT) return true;  // stopped: reported invalid
+  const double step = ADAPTIVE ? 0.0 : KINEMATICS_RES;  // plain loops: constant increment
+  switch (L.stage) {
+    case ST_FWD_STANCE:
+      if (!ok) {
+        if (small_step<ADAPTIVE>(L.ts)) {
+          L.snew_kind = SN_STANCE_S;
+          L.snew_p = (1.0 - BACKUP_RATIO) * L.t;
+          return true;
+        }
+        L.ts = KINEMATICS_RES;
+        L.t = L.tpre;
+        L.t += L.ts;
+      } else {
+        L.snew_kind = SN_STANCE_S;
+        L.snew_p = L.t;
+        L.tnew = L.t;
+        L.tnew_set = 1;
+        if (ADAPTIVE) {
+          L.ts += KINEMATICS_RES;
+          L.tpre = L.t;
+          L.t += L.ts;
+        } else {
+          L.t += step;
+        }
+      }
+      if (!(L.t <= L.a[6])) enter_stage(L, ST_FWD_FLIGHT);
+      return false;
+    case ST_FWD_FLIGHT:
+      if (!ok) return true;
+      if (ADAPTIVE) {
+        L.ts += KINEMATICS_RES;
+        L.tpre = L.t;
+        L.t += L.ts;
+      } else {
+        L.t += step;
+      }
+      if (!(L.t < L.a[7])) enter_stage(L, ST_FWD_LAND);
+      return false;
+    case ST_FWD_LAND:
+      if (!ok) return true;
+      L.snew_kind = SN_FLIGHT_B;
+      L.snew_p = L.a[7];
+      L.tnew = L.a[6] + L.a[7];
+      L.tnew_set = 1;
+      L.f |= GBP_F_VALID;
+      return true;
+    case ST_REV_FLIGHT:
+      if (!ok) return true;
+      if (ADAPTIVE) {
+        L.ts += KINEMATICS_RES;
+        L.tpre = L.t;
+        L.t += L.ts;
+      } else {
+        L.t += step;
+      }
+      if (!(L.t < L.a[7])) enter_stage(L, ST_REV_STANCE);
+      return false;
+    case ST_REV_STANCE:
+      if (!ok) {
+        if (small_step<ADAPTIVE>(L.ts)) {
+          L.snew_kind = SN_STANCE_S;  // forward stance on the end state (:857)
+          L.snew_p = L.t + BACKUP_RATIO * (L.a[6] - L.t);
+          return true;
+        }
+        L.ts = KINEMATICS_RES;
+        L.t = L.tpre;
+        L.t -= L.ts;
+      } else {
+        L.snew_kind = SN_STANCE_REV_B;
+        L.snew_p = L.t;
+        L.tnew = L.a[6] - L.t;
+        L.tnew_set = 1;
+        if (ADAPTIVE) {
+          L.ts += KINEMATICS_RES;
+          L.tpre = L.t;
+          L.t -= L.ts;
+        } else {
+          L.t -= step;
+        }
+      }
+      if (!(L.t >= 0)) enter_stage(L, ST_REV_START);
+      return false;
+    default:  // ST_REV_START
+      if (!ok) return true;
+      L.snew_kind = SN_STANCE_REV_B;
+      L.snew_p = 0;
+      L.tnew = L.a[6];
+      L.tnew_set = 1;
+      L.f |= GBP_F_VALID;
+      return true;
+  }
+}
+
+template <class ZT, bool ADAPTIVE, int W>
+__global__ __launch_bounds__(256, W) void k_validate_persistent(
+    TerrainView<ZT> T, int n, const double *__restrict__ S, const double *__restrict__ A,
+    const uint8_t *__restrict__ dir, int dir_all, uint8_t *__restrict__ valid,
+    double *__restrict__ s_new, double *__restrict__ t_new, uint32_t *__restrict__ flags,
+    uint32_t *__restrict__ counts, unsigned int *__restrict__ head) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  Lane L;
+  L.stage = ST_IDLE;
+  bool exhausted = false;
+  for (;;) {
+    const bool need = (L.stage == ST_IDLE) && !exhausted;
+    const unsigned long long m = __ballot(need);
+    if (m) {
+      const int leader = __ffsll((long long)m) - 1;
+      unsigned int base = 0;
+      if (lane == leader) base = atomicAdd(head, (unsigned int)__popcll(m));
+      base = __shfl(base, leader);
+      if (need) {
+        const unsigned int i = base + (unsigned int)__popcll(m & ((1ull << lane) - 1ull));
+        if (i < (unsigned int)n) {
+          L.idx = (int)i;
+#pragma unroll
+          for (int k = 0; k < 8; k++) L.s[k] = S[8 * (size_t)i + k];
+#pragma unroll
+          for (int k = 0; k < 10; k++) L.a[k] = A[10 * (size_t)i + k];
+          L.f = 0;
+          L.acc = Acc{0, 0, 0};
+          L.snew_kind = SN_NONE;
+          L.tnew_set = 0;
+          const int d = dir ? dir[i] : dir_all;
+          enter_stage(L, d == GBP_FORWARD ? ST_FWD_STANCE : ST_REV_FLIGHT);
+        } else {
+          exhausted = true;
+        }
+      }
+    }
+    if (!__any(L.stage != ST_IDLE)) break;
+    if (L.stage != ST_IDLE) {
+      if (step_lane<ZT, ADAPTIVE>(T, L)) {
+        const size_t i = (size_t)L.idx;
+        uint32_t f = L.f | L.acc.flags;
+        if (L.snew_kind != SN_NONE) f |= GBP_F_SNEW_SET;
+        if (L.tnew_set) f |= GBP_F_TNEW_SET;
+        if (valid) valid[i] = (f & GBP_F_VALID) ? 1 : 0;
+        if (s_new && L.snew_kind != SN_NONE) {
+          double o[8];
+          if (L.snew_kind == SN_STANCE_S) apply_stance(L.s, L.a, L.snew_p, o);
+          else if (L.snew_kind == SN_FLIGHT_B) apply_flight(L.b, L.snew_p, o);
+          else apply_stance_reverse(L.b, L.a, L.snew_p, o);
+#pragma unroll
+          for (int k = 0; k < 8; k++) s_new[8 * i + k] = o[k];
+        }
+        if (t_new && L.tnew_set) t_new[i] = L.tnew;
+        flags[i] = f;
+        if (counts) counts[i] = (L.acc.G & 0xFFFFu) | (L.acc.V << 16);
+        L.stage = ST_IDLE;
+      }
+    }
+  }
+}
+
+// ============================================================================
+// K3: samplers and the batched extend
+// ============================================================================
+template <class ZT>
+__global__ void k_sample_states(TerrainView<ZT> T, int64_t n, uint64_t seed, uint64_t stream_id,
+                                int64_t index_base, int require_phase, int max_tries,
+                                double *__restrict__ states, int32_t *__restrict__ tries) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double q[8];
+    int got = -1;
+    const int mt = max_tries > 0 ? max_tries : 1;
+    for (int k = 0; k < mt; k++) {
+      sample_state_try(T, seed, stream_id, index_base + i, k, q);
+      if (require_phase < 0) { got = k + 1; break; }
+      Acc acc{0, 0, 0};
+      if (is_valid_state(T, q, require_phase, acc)) { got = k + 1; break; }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) states[8 * i + k] = q[k];
+    if (tries) tries[i] = got;
+  }
+}
+
+__global__ void k_sample_actions(int64_t n, const double *__restrict__ normals, uint64_t seed,
+                                 uint64_t stream_id, int64_t index_base,
+                                 double *__restrict__ actions) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const double nv[3] = {normals[3 * i], normals[3 * i + 1], normals[3 * i + 2]};
+    double a[10];
+    sample_action(nv, seed, stream_id, index_base + i, a);
+#pragma unroll
+    for (int k = 0; k < 10; k++) actions[10 * i + k] = a[k];
+  }
+}
+
+// one thread per (extend i, candidate j): candidate action j of extend i is
+// getRandomAction(getSurfaceNormal(target_i)) from stream (seed, EXTD, (base+i)*8+j)
+template <class ZT>
+__global__ void k_extend_prep(TerrainView<ZT> T, int64_t n, const double *__restrict__ s_near,
+                              const double *__restrict__ target, const uint8_t *__restrict__ dir,
+                              int dir_all, uint64_t seed, int64_t extend_base,
+                              double *__restrict__ cand_s, double *__restrict__ cand_a,
+                              uint8_t *__restrict__ cand_dir) {
+  const int64_t m = n * GBP_NUM_GEN_STATES;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < m;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = c / GBP_NUM_GEN_STATES;
+    const int j = (int)(c - i * GBP_NUM_GEN_STATES);
+    double nv[3];
+    surface_normal(T, target[8 * i], target[8 * i + 1], nv);  // rrt.cpp:25
+    double a[10];
+    sample_action(nv, seed, EXTEND_STREAM, (extend_base + i) * 8 + j, a);
+#pragma unroll
+    for (int k = 0; k < 10; k++) cand_a[10 * c + k] = a[k];
+#pragma unroll
+    for (int k = 0; k < 8; k++) cand_s[8 * c + k] = s_near[8 * i + k];
+    cand_dir[c] = dir ? dir[i] : (uint8_t)dir_all;
+  }
+}
+
+// rrt.cpp:20-70 selection + rrt.cpp:84-101 acceptance
+__global__ void k_extend_select(int64_t n, const double *__restrict__ s_near,
+                                const double *__restrict__ target,
+                                const double *__restrict__ cand_a,
+                                const double *__restrict__ cand_snew,
+                                const uint32_t *__restrict__ cand_flags,
+                                const uint32_t *__restrict__ cand_counts,
+                                int32_t *__restrict__ result, int32_t *__restrict__ chosen,
+                                double *__restrict__ s_new, double *__restrict__ a_new,
+                                uint32_t *__restrict__ counts) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double sn[8], tg[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      sn[k] = s_near[8 * i + k];
+      tg[k] = target[8 * i + k];
+    }
+    int found = -1;
+    uint32_t G = 0, V = 0;
+    for (int j = 0; j < GBP_NUM_GEN_STATES; j++) {
+      const int64_t c = i * GBP_NUM_GEN_STATES + j;
+      G += GBP_COUNT_G(cand_counts[c]);
+      V += GBP_COUNT_V(cand_counts[c]);
+      if (cand_flags[c] & GBP_F_VALID) {
+        found = j;
+        break;
+      }
+    }
+    const double d0 = state_distance(sn, tg);
+    double best = d0;
+    double st[8];
+    if (found >= 0) {
+      const int64_t c = i * GBP_NUM_GEN_STATES + found;
+#pragma unroll
+      for (int k = 0; k < 8; k++) st[k] = cand_snew[8 * c + k];
+      const double cur = state_distance(st, tg);
+      if (cur < best) {
+        best = cur;
+#pragma unroll
+        for (int k = 0; k < 8; k++) s_new[8 * i + k] = st[k];
+#pragma unroll
+        for (int k = 0; k < 10; k++) a_new[10 * i + k] = cand_a[10 * c + k];
+      }
+    }
+    int r;
+    if (best == state_distance(sn, tg)) r = GBP_TRAPPED;
+    else r = (state_distance(st, tg) <= GOAL_BOUNDS) ? GBP_REACHED : GBP_ADVANCED;
+    result[i] = r;
+    if (chosen) chosen[i] = found;
+    if (counts) counts[i] = (G & 0xFFFFu) | (V << 16);
+  }
+}
+
+// ============================================================================
+// K5: nearest neighbour, one workgroup per query
+// ============================================================================
+__device__ __forceinline__ void lex_min(double &d, int &i, double d2, int i2) {
+  if (d2 < d || (d2 == d && i2 < i)) {
+    d = d2;
+    i = i2;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_nearest(int64_t n_query, const double *__restrict__ q,
+                                                 int64_t n_vert, const double *__restrict__ v,
+                                                 int32_t *__restrict__ idx,
+                                                 double *__restrict__ dist) {
+  __shared__ double sd[256 / WAVE];
+  __shared__ int si[256 / WAVE];
+  for (int64_t qi = blockIdx.x; qi < n_query; qi += gridDim.x) {
+    double qq[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) qq[k] = q[8 * qi + k];
+    double best = INFINITY;
+    int bi = 0x7FFFFFFF;
+    for (int64_t j = threadIdx.x; j < n_vert; j += blockDim.x) {
+      double vv[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) vv[k] = v[8 * j + k];
+      const double c = state_distance(qq, vv);  // stateDistance(q, vertex), planner_class.cpp:193
+      if (c < best) {  // strict <, increasing j: lowest index among equals
+        best = c;
+        bi = (int)j;
+      }
+    }
+#pragma unroll
+    for (int off = WAVE / 2; off > 0; off >>= 1) {
+      const double d2 = __shfl_down(best, off);
+      const int i2 = __shfl_down(bi, off);
+      lex_min(best, bi, d2, i2);
+    }
+    const int w = threadIdx.x / WAVE;
+    if ((threadIdx.x & (WAVE - 1)) == 0) {
+      sd[w] = best;
+      si[w] = bi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int k = 1; k < (int)(blockDim.x / WAVE); k++) lex_min(best, bi, sd[k], si[k]);
+      if (bi == 0x7FFFFFFF) bi = 0;  // nothing < INFINITY: the reference keeps index 0
+      idx[qi] = bi;
+      if (dist) dist[qi] = best;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+struct gbp_terrain {
+  int device = 0;
+  int nx = 0, ny = 0;
+  int storage = GBP_STORAGE_F64;
+  double bounds[4] = {0, 0, 0, 0};
+  double inv_hx = 0, inv_hy = 0;
+  double *d_x = nullptr, *d_y = nullptr;
+  void *d_z = nullptr;
+  double *d_dx = nullptr, *d_dy = nullptr, *d_dz = nullptr;
+  int num_cus = 256;
+  int64_t opt_kernel = GBP_KERNEL_PERSISTENT;
+  int64_t opt_block = 256;
+  int64_t opt_grid_per_cu = 8;
+  int64_t opt_waves = 2;            // register budget of the validate kernels (waves/SIMD)
+  unsigned int *d_head = nullptr;   // persistent-kernel work counter (zeroed per launch)
+  hipStream_t host_stream = nullptr;
+  void *ws = nullptr;               // grow-only device workspace
+  size_t ws_bytes = 0;
+  void *ws2 = nullptr;              // second workspace (extend candidates)
+  size_t ws2_bytes = 0;
+};
+
+namespace {
+
+#define HIPCHK(expr)                      \
+  do {                                    \
+    hipError_t e_ = (expr);               \
+    if (e_ != hipSuccess) return GBP_E_HIP; \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+template <class ZT>
+TerrainView<ZT> view(const gbp_terrain *t) {
+  TerrainView<ZT> v;
+  v.x = t->d_x;
+  v.y = t->d_y;
+  v.z = (const ZT *)t->d_z;
+  v.dx = t->d_dx;
+  v.dy = t->d_dy;
+  v.dz = t->d_dz;
+  v.nx = t->nx;
+  v.ny = t->ny;
+  v.x0 = t->bounds[0];
+  v.xN = t->bounds[1];
+  v.y0 = t->bounds[2];
+  v.yN = t->bounds[3];
+  v.inv_hx = t->inv_hx;
+  v.inv_hy = t->inv_hy;
+  return v;
+}
+
+inline unsigned grid_for(int64_t n, int block, int cap = 65535 * 8) {
+  int64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+int ensure_ws(gbp_terrain *t, void **ws, size_t *have, size_t need) {
+  if (*have >= need) return GBP_OK;
+  if (*ws) (void)hipFree(*ws);
+  *ws = nullptr;
+  *have = 0;
+  size_t sz = std::max(need, (size_t)1 << 20);
+  if (hipMalloc(ws, sz) != hipSuccess) {
+    *ws = nullptr;
+    return GBP_E_ALLOC;
+  }
+  *have = sz;
+  return GBP_OK;
+}
+
+template <class ZT, bool AD, int W>
+int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *a,
+                      const uint8_t *dir, int dir_all, uint8_t *valid, double *s_new,
+                      double *t_new, uint32_t *flags, uint32_t *counts, hipStream_t st) {
+  const TerrainView<ZT> T = view<ZT>(t);
+  const int block = (int)t->opt_block;
+  const int64_t chunk = (int64_t)1 << 30;
+  const int64_t want = (int64_t)t->num_cus * t->opt_grid_per_cu;
+  for (int64_t off = 0; off < n; off += chunk) {
+    const int64_t m = std::min<int64_t>(n - off, chunk);
+    const uint8_t *d = dir ? dir + off : nullptr;
+    uint8_t *v = valid ? valid + off : nullptr;
+    double *sn = s_new ? s_new + 8 * off : nullptr;
+    double *tn = t_new ? t_new + off : nullptr;
+    uint32_t *c = counts ? counts + off : nullptr;
+    if (t->opt_kernel == GBP_KERNEL_DIRECT) {
+      const unsigned g = (unsigned)((m + block - 1) / block);
+      hipLaunchKernelGGL((k_validate_direct<ZT, AD, W>), dim3(g), dim3(block), 0, st, T, m,
+                         s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn, flags + off, c);
+    } else {
+      // persistent: grid sized to residency; the work counter is zeroed per launch
+      const int64_t g = std::max<int64_t>(1, std::min<int64_t>(want, (m + block - 1) / block));
+      HIPCHK(hipMemsetAsync(t->d_head, 0, sizeof(unsigned int), st));
+      hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W>), dim3((unsigned)g), dim3(block), 0,
+                         st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
+                         flags + off, c, t->d_head);
+    }
+    HIPCHK(hipGetLastError());
+  }
+  return GBP_OK;
+}
+
+template <class ZT>
+int launch_validate(gbp_terrain *t, int64_t n, const double *s, const double *a,
+                    const uint8_t *dir, int dir_all, int adaptive, uint8_t *valid,
+                    double *s_new, double *t_new, uint32_t *flags, uint32_t *counts,
+                    hipStream_t st) {
+#define GBP_LV(AD, W) \
+  launch_validate_w<ZT, AD, W>(t, n, s, a, dir, dir_all, valid, s_new, t_new, flags, counts, st)
+  const int64_t w = t->opt_waves;
+  if (adaptive) return w >= 4 ? GBP_LV(true, 4) : (w >= 2 ? GBP_LV(true, 2) : GBP_LV(true, 1));
+  return w >= 4 ? GBP_LV(false, 4) : (w >= 2 ? GBP_LV(false, 2) : GBP_LV(false, 1));
+#undef GBP_LV
+}
+
+bool valid_handle(const gbp_terrain *t) { return t != nullptr && t->d_z != nullptr; }
+
+// host-pointer entry points: one synchronous staging round trip through the
+// handle's workspace on its private stream (used by the C++ adapters that
+// re-export the reference API).
+struct Stage {
+  gbp_terrain *t;
+  char *base;
+  size_t off = 0;
+  template <class T>
+  T *take(size_t count) {
+    off = (off + 255) & ~(size_t)255;
+    T *p = (T *)(base + off);
+    off += count * sizeof(T);
+    return p;
+  }
+};
+size_t rnd(size_t b) { return (b + 255) & ~(size_t)255; }
+
+}  // namespace
+
+extern "C" {
+
+int gbp_version(void) { return 100; /* 0.1.0 */ }
+
+const char *gbp_status_string(int status) {
+  switch (status) {
+    case GBP_OK: return "ok";
+    case GBP_E_INVALID_ARG: return "invalid argument";
+    case GBP_E_BAD_HANDLE: return "bad handle";
+    case GBP_E_ALLOC: return "device allocation failed";
+    case GBP_E_HIP: return "HIP runtime error";
+    case GBP_E_SHAPE: return "bad shape";
+    case GBP_E_NO_DEVICE: return "no HIP device";
+    case GBP_E_UNSUPPORTED: return "unsupported";
+    default: return "unknown status";
+  }
+}
+
+int gbp_device_count(int *count) {
+  if (!count) return GBP_E_INVALID_ARG;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *count = c;
+  return c > 0 ? GBP_OK : GBP_E_NO_DEVICE;
+}
+
+int gbp_device_alloc(int device, size_t bytes, void **ptr) {
+  if (!ptr) return GBP_E_INVALID_ARG;
+  DeviceGuard g(device);
+  if (hipMalloc(ptr, bytes ? bytes : 1) != hipSuccess) return GBP_E_ALLOC;
+  return GBP_OK;
+}
+
+int gbp_device_free(void *ptr) {
+  if (ptr) HIPCHK(hipFree(ptr));
+  return GBP_OK;
+}
+
+int gbp_memcpy_h2d(void *dst, const void *src, size_t bytes, gbp_stream stream) {
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+  return GBP_OK;
+}
+
+int gbp_memcpy_d2h(void *dst, const void *src, size_t bytes, gbp_stream stream) {
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  return GBP_OK;
+}
+
+int gbp_stream_synchronize(gbp_stream stream) {
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return GBP_OK;
+}
+
+int gbp_terrain_create(int device, int nx, int ny, const double *x, const double *y,
+                       const double *z, const double *dx, const double *dy, const double *dz,
+                       int storage, gbp_terrain **out) {
+  if (!out || !x || !y || !z) return GBP_E_INVALID_ARG;
+  *out = nullptr;
+  if (nx < 2 || ny < 2) return GBP_E_SHAPE;
+  if ((dx == nullptr) != (dy == nullptr) || (dx == nullptr) != (dz == nullptr))
+    return GBP_E_INVALID_ARG;
+  for (int i = 0; i + 1 < nx; i++)
+    if (!(x[i] <= x[i + 1])) return GBP_E_INVALID_ARG;  // ascending (fast_terrain_map.cpp:101-108)
+  for (int i = 0; i + 1 < ny; i++)
+    if (!(y[i] <= y[i + 1])) return GBP_E_INVALID_ARG;
+  const size_t cells = (size_t)nx * ny;
+  if (storage == GBP_STORAGE_AUTO) {
+    storage = GBP_STORAGE_F32;
+    for (size_t i = 0; i < cells; i++) {
+      const double v = z[i];
+      if (!std::isnan(v) && (double)(float)v != v) {
+        storage = GBP_STORAGE_F64;
+        break;
+      }
+    }
+  } else if (storage != GBP_STORAGE_F32 && storage != GBP_STORAGE_F64) {
+    return GBP_E_INVALID_ARG;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GBP_E_NO_DEVICE;
+  if (device < 0 || device >= ndev) return GBP_E_INVALID_ARG;
+  DeviceGuard g(device);
+  gbp_terrain *t = new (std::nothrow) gbp_terrain();
+  if (!t) return GBP_E_ALLOC;
+  t->device = device;
+  t->nx = nx;
+  t->ny = ny;
+  t->storage = storage;
+  t->bounds[0] = x[0];
+  t->bounds[1] = x[nx - 1];
+  t->bounds[2] = y[0];
+  t->bounds[3] = y[ny - 1];
+  t->inv_hx = (x[nx - 1] > x[0]) ? (double)(nx - 1) / (x[nx - 1] - x[0]) : 0.0;
+  t->inv_hy = (y[ny - 1] > y[0]) ? (double)(ny - 1) / (y[ny - 1] - y[0]) : 0.0;
+  (void)hipDeviceGetAttribute(&t->num_cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (t->num_cus <= 0) t->num_cus = 256;
+  int rc = GBP_OK;
+  auto fail = [&](int code) {
+    gbp_terrain_destroy(t);
+    return code;
+  };
+  if (hipMalloc((void **)&t->d_x, sizeof(double) * nx) != hipSuccess) return fail(GBP_E_ALLOC);
+  if (hipMalloc((void **)&t->d_y, sizeof(double) * ny) != hipSuccess) return fail(GBP_E_ALLOC);
+  if (hipMemcpy(t->d_x, x, sizeof(double) * nx, hipMemcpyHostToDevice) != hipSuccess)
+    return fail(GBP_E_HIP);
+  if (hipMemcpy(t->d_y, y, sizeof(double) * ny, hipMemcpyHostToDevice) != hipSuccess)
+    return fail(GBP_E_HIP);
+  if (storage == GBP_STORAGE_F32) {
+    std::vector<float> zf(cells);
+    for (size_t i = 0; i < cells; i++) zf[i] = (float)z[i];
+    if (hipMalloc(&t->d_z, sizeof(float) * cells) != hipSuccess) return fail(GBP_E_ALLOC);
+    if (hipMemcpy(t->d_z, zf.data(), sizeof(float) * cells, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(GBP_E_HIP);
+  } else {
+    if (hipMalloc(&t->d_z, sizeof(double) * cells) != hipSuccess) return fail(GBP_E_ALLOC);
+    if (hipMemcpy(t->d_z, z, sizeof(double) * cells, hipMemcpyHostToDevice) != hipSuccess)
+      return fail(GBP_E_HIP);
+  }
+  if (dx) {
+    const double *src[3] = {dx, dy, dz};
+    double **dst[3] = {&t->d_dx, &t->d_dy, &t->d_dz};
+    for (int k = 0; k < 3; k++) {
+      if (hipMalloc((void **)dst[k], sizeof(double) * cells) != hipSuccess)
+        return fail(GBP_E_ALLOC);
+      if (hipMemcpy(*dst[k], src[k], sizeof(double) * cells, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(GBP_E_HIP);
+    }
+  }
+  if (hipMalloc((void **)&t->d_head, 256) != hipSuccess) return fail(GBP_E_ALLOC);
+  if (hipStreamCreateWithFlags(&t->host_stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(GBP_E_HIP);
+  (void)rc;
+  *out = t;
+  return GBP_OK;
+}
+
+int gbp_terrain_destroy(gbp_terrain *t) {
+  if (!t) return GBP_E_BAD_HANDLE;
+  DeviceGuard g(t->device);
+  if (t->host_stream) (void)hipStreamSynchronize(t->host_stream);
+  void *ptrs[] = {t->d_x, t->d_y, t->d_z, t->d_dx, t->d_dy, t->d_dz, t->d_head, t->ws, t->ws2};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  if (t->host_stream) (void)hipStreamDestroy(t->host_stream);
+  delete t;
+  return GBP_OK;
+}
+
+int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage, double bounds[4],
+                     int *device) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (nx) *nx = t->nx;
+  if (ny) *ny = t->ny;
+  if (storage) *storage = t->storage;
+  if (bounds) memcpy(bounds, t->bounds, sizeof t->bounds);
+  if (device) *device = t->device;
+  return GBP_OK;
+}
+
+int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  switch (key) {
+    case GBP_OPT_KERNEL:
+      if (value != GBP_KERNEL_DIRECT && value != GBP_KERNEL_PERSISTENT) return GBP_E_INVALID_ARG;
+      t->opt_kernel = value;
+      return GBP_OK;
+    case GBP_OPT_BLOCK:
+      if (value < 64 || value > 256 || value % 64) return GBP_E_INVALID_ARG;
+      t->opt_block = value;
+      return GBP_OK;
+    case GBP_OPT_GRID_PER_CU:
+      if (value < 1 || value > 64) return GBP_E_INVALID_ARG;
+      t->opt_grid_per_cu = value;
+      return GBP_OK;
+    case GBP_OPT_WAVES:
+      if (value != 1 && value != 2 && value != 4) return GBP_E_INVALID_ARG;
+      t->opt_waves = value;
+      return GBP_OK;
+    default:
+      return GBP_E_INVALID_ARG;
+  }
+}
+
+int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (!value) return GBP_E_INVALID_ARG;
+  switch (key) {
+    case GBP_OPT_KERNEL: *value = t->opt_kernel; return GBP_OK;
+    case GBP_OPT_BLOCK: *value = t->opt_block; return GBP_OK;
+    case GBP_OPT_GRID_PER_CU: *value = t->opt_grid_per_cu; return GBP_OK;
+    case GBP_OPT_WAVES: *value = t->opt_waves; return GBP_OK;
+    default: return GBP_E_INVALID_ARG;
+  }
+}
+
+// ---- K1 --------------------------------------------------------------------
+int gbp_height_batch_dev(gbp_terrain *t, int64_t n, const double *xy, double *height,
+                         uint8_t *is_nan, uint8_t *ood, gbp_stream stream) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || (n > 0 && !xy)) return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  DeviceGuard g(t->device);
+  const unsigned grid = grid_for(n, 256, t->num_cus * 16);
+  if (t->storage == GBP_STORAGE_F32)
+    hipLaunchKernelGGL(k_height<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       view<float>(t), n, xy, height, is_nan, ood);
+  else
+    hipLaunchKernelGGL(k_height<double>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       view<double>(t), n, xy, height, is_nan, ood);
+  HIPCHK(hipGetLastError());
+  return GBP_OK;
+}
+
+int gbp_normal_batch_dev(gbp_terrain *t, int64_t n, const double *xy, double *normal,
+                         uint8_t *ood, gbp_stream stream) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || (n > 0 && (!xy || !normal))) return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  DeviceGuard g(t->device);
+  const unsigned grid = grid_for(n, 256, t->num_cus * 16);
+  if (t->storage == GBP_STORAGE_F32)
+    hipLaunchKernelGGL(k_normal<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       view<float>(t), n, xy, normal, ood);
+  else
+    hipLaunchKernelGGL(k_normal<double>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       view<double>(t), n, xy, normal, ood);
+  HIPCHK(hipGetLastError());
+  return GBP_OK;
+}
+
+int gbp_valid_states_dev(gbp_terrain *t, int64_t n, const double *states, const uint8_t *phase,
+                         int phase_all, uint8_t *valid, uint32_t *flags, uint32_t *counts,
+                         gbp_stream stream) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || (n > 0 && !states)) return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  DeviceGuard g(t->device);
+  const unsigned grid = grid_for(n, 256, t->num_cus * 16);
+  if (t->storage == GBP_STORAGE_F32)
+    hipLaunchKernelGGL(k_valid_states<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       view<float>(t), n, states, phase, phase_all, valid, flags, counts);
+  else
+    hipLaunchKernelGGL(k_valid_states<double>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       view<double>(t), n, states, phase, phase_all, valid, flags, counts);
+  HIPCHK(hipGetLastError());
+  return GBP_OK;
+}
+
+// ---- K2: the hot path ---------------------------------------------------------
+int gbp_validate_pairs_dev(gbp_terrain *t, int64_t n, const double *s, const double *a,
+                           const uint8_t *direction, int direction_all, int adaptive,
+                           uint8_t *valid, double *s_new, double *t_new, uint32_t *flags,
+                           uint32_t *counts, gbp_stream stream) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || (n > 0 && (!s || !a || !flags))) return GBP_E_INVALID_ARG;
+  if (!direction && direction_all != GBP_FORWARD && direction_all != GBP_REVERSE)
+    return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  DeviceGuard g(t->device);
+  if (t->storage == GBP_STORAGE_F32)
+    return launch_validate<float>(t, n, s, a, direction, direction_all, adaptive, valid, s_new,
+                                  t_new, flags, counts, (hipStream_t)stream);
+  return launch_validate<double>(t, n, s, a, direction, direction_all, adaptive, valid, s_new,
+                                 t_new, flags, counts, (hipStream_t)stream);
+}
+
+// ---- K3 ---------------------------------------------------------------------
+int gbp_sample_states_dev(gbp_terrain *t, int64_t n, uint64_t seed, uint64_t stream_id,
+                          int64_t index_base, int require_phase, int max_tries, double *states,
+                          int32_t *tries, gbp_stream stream) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || (n > 0 && !states)) return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  DeviceGuard g(t->device);
+  const unsigned grid = grid_for(n, 256, t->num_cus * 16);
+  if (t->storage == GBP_STORAGE_F32)
+    hipLaunchKernelGGL(k_sample_states<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       view<float>(t), n, seed, stream_id, index_base, require_phase, max_tries,
+                       states, tries);
+  else
+    hipLaunchKernelGGL(k_sample_states<double>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       view<double>(t), n, seed, stream_id, index_base, require_phase, max_tries,
+                       states, tries);
+  HIPCHK(hipGetLastError());
+  return GBP_OK;
+}
+
+int gbp_sample_actions_dev(int64_t n, const double *normals, uint64_t seed, uint64_t stream_id,
+                           int64_t index_base, double *actions, gbp_stream stream) {
+  if (n < 0 || (n > 0 && (!normals || !actions))) return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  hipLaunchKernelGGL(k_sample_actions, dim3(grid_for(n, 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, n, normals, seed, stream_id, index_base, actions);
+  HIPCHK(hipGetLastError());
+  return GBP_OK;
+}
+
+int gbp_extend_batch_dev(gbp_terrain *t, int64_t n, const double *s_near, const double *target,
+                         const uint8_t *direction, int direction_all, int adaptive, uint64_t seed,
+                         int64_t extend_base, int32_t *result, int32_t *chosen, double *s_new,
+                         double *a_new, uint32_t *counts, gbp_stream stream) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || (n > 0 && (!s_near || !target || !result || !s_new || !a_new)))
+    return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  DeviceGuard g(t->device);
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t m = n * GBP_NUM_GEN_STATES;
+  // candidate workspace: s (8) + a (10) + s_new (8) doubles, flags + counts u32, dir u8
+  const size_t need = (size_t)m * (26 * sizeof(double) + 2 * sizeof(uint32_t) + 1) + 256;
+  int rc = ensure_ws(t, &t->ws2, &t->ws2_bytes, need);
+  if (rc) return rc;
+  char *p = (char *)t->ws2;
+  double *cs = (double *)p; p += (size_t)m * 8 * sizeof(double);
+  double *ca = (double *)p; p += (size_t)m * 10 * sizeof(double);
+  double *csn = (double *)p; p += (size_t)m * 8 * sizeof(double);
+  uint32_t *cf = (uint32_t *)p; p += (size_t)m * sizeof(uint32_t);
+  uint32_t *cc = (uint32_t *)p; p += (size_t)m * sizeof(uint32_t);
+  uint8_t *cd = (uint8_t *)p;
+  const unsigned grid = grid_for(m, 256, t->num_cus * 16);
+  if (t->storage == GBP_STORAGE_F32)
+    hipLaunchKernelGGL(k_extend_prep<float>, dim3(grid), dim3(256), 0, st, view<float>(t), n,
+                       s_near, target, direction, direction_all, seed, extend_base, cs, ca, cd);
+  else
+    hipLaunchKernelGGL(k_extend_prep<double>, dim3(grid), dim3(256), 0, st, view<double>(t), n,
+                       s_near, target, direction, direction_all, seed, extend_base, cs, ca, cd);
+  HIPCHK(hipGetLastError());
+  rc = gbp_validate_pairs_dev(t, m, cs, ca, cd, 0, adaptive, nullptr, csn, nullptr, cf, cc,
+                              stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_extend_select, dim3(grid_for(n, 256, t->num_cus * 16)), dim3(256), 0, st,
+                     n, s_near, target, ca, csn, cf, cc, result, chosen, s_new, a_new, counts);
+  HIPCHK(hipGetLastError());
+  return GBP_OK;
+}
+
+// ---- K5 ---------------------------------------------------------------------
+int gbp_nearest_batch_dev(int64_t n_query, const double *queries, int64_t n_vert,
+                          const double *vertices, int32_t *index, double *dist,
+                          gbp_stream stream) {
+  if (n_query < 0 || n_vert < 0 || (n_query > 0 && (!queries || !index))) return GBP_E_INVALID_ARG;
+  if (n_vert > 0x7FFFFFFE) return GBP_E_SHAPE;
+  if (n_query == 0) return GBP_OK;
+  if (n_vert > 0 && !vertices) return GBP_E_INVALID_ARG;
+  const unsigned grid = (unsigned)std::min<int64_t>(n_query, 65535);
+  hipLaunchKernelGGL(k_nearest, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_query, queries,
+                     n_vert, vertices, index, dist);
+  HIPCHK(hipGetLastError());
+  return GBP_OK;
+}
+
+// ---- host-pointer convenience entry points (see the Stage helper above) ----------
+
+#define H2D(dst, src, bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st))
+#define D2H(dst, src, bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st))
+
+int gbp_height_batch_host(gbp_terrain *t, int64_t n, const double *xy, double *height,
+                          uint8_t *is_nan, uint8_t *ood) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n <= 0) return n == 0 ? GBP_OK : GBP_E_INVALID_ARG;
+  DeviceGuard g(t->device);
+  hipStream_t st = t->host_stream;
+  int rc = ensure_ws(t, &t->ws, &t->ws_bytes, rnd(16 * n) + rnd(8 * n) + 2 * rnd(n) + 1024);
+  if (rc) return rc;
+  Stage S{t, (char *)t->ws};
+  double *dxy = S.take<double>(2 * n), *dh = S.take<double>(n);
+  uint8_t *dn = S.take<uint8_t>(n), *dood = S.take<uint8_t>(n);
+  H2D(dxy, xy, 16 * n);
+  rc = gbp_height_batch_dev(t, n, dxy, dh, dn, dood, st);
+  if (rc) return rc;
+  if (height) D2H(height, dh, 8 * n);
+  if (is_nan) D2H(is_nan, dn, n);
+  if (ood) D2H(ood, dood, n);
+  HIPCHK(hipStreamSynchronize(st));
+  return GBP_OK;
+}
+
+int gbp_normal_batch_host(gbp_terrain *t, int64_t n, const double *xy, double *normal,
+                          uint8_t *ood) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n <= 0) return n == 0 ? GBP_OK : GBP_E_INVALID_ARG;
+  if (!normal) return GBP_E_INVALID_ARG;
+  DeviceGuard g(t->device);
+  hipStream_t st = t->host_stream;
+  int rc = ensure_ws(t, &t->ws, &t->ws_bytes, rnd(16 * n) + rnd(24 * n) + rnd(n) + 1024);
+  if (rc) return rc;
+  Stage S{t, (char *)t->ws};
+  double *dxy = S.take<double>(2 * n), *dn = S.take<double>(3 * n);
+  uint8_t *dood = S.take<uint8_t>(n);
+  H2D(dxy, xy, 16 * n);
+  rc = gbp_normal_batch_dev(t, n, dxy, dn, dood, st);
+  if (rc) return rc;
+  D2H(normal, dn, 24 * n);
+  if (ood) D2H(ood, dood, n);
+  HIPCHK(hipStreamSynchronize(st));
+  return GBP_OK;
+}
+
+int gbp_valid_states_host(gbp_terrain *t, int64_t n, const double *states, const uint8_t *phase,
+                          int phase_all, uint8_t *valid, uint32_t *flags, uint32_t *counts) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n <= 0) return n == 0 ? GBP_OK : GBP_E_INVALID_ARG;
+  DeviceGuard g(t->device);
+  hipStream_t st = t->host_stream;
+  int rc = ensure_ws(t, &t->ws, &t->ws_bytes,
+                     rnd(64 * n) + 2 * rnd(n) + 2 * rnd(4 * n) + 2048);
+  if (rc) return rc;
+  Stage S{t, (char *)t->ws};
+  double *ds = S.take<double>(8 * n);
+  uint8_t *dp = S.take<uint8_t>(n), *dv = S.take<uint8_t>(n);
+  uint32_t *df = S.take<uint32_t>(n), *dc = S.take<uint32_t>(n);
+  H2D(ds, states, 64 * n);
+  if (phase) H2D(dp, phase, n);
+  rc = gbp_valid_states_dev(t, n, ds, phase ? dp : nullptr, phase_all, dv, df, dc, st);
+  if (rc) return rc;
+  if (valid) D2H(valid, dv, n);
+  if (flags) D2H(flags, df, 4 * n);
+  if (counts) D2H(counts, dc, 4 * n);
+  HIPCHK(hipStreamSynchronize(st));
+  return GBP_OK;
+}
+
+int gbp_validate_pairs_host(gbp_terrain *t, int64_t n, const double *s, const double *a,
+                            const uint8_t *direction, int direction_all, int adaptive,
+                            uint8_t *valid, double *s_new, double *t_new, uint32_t *flags,
+                            uint32_t *counts) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n <= 0) return n == 0 ? GBP_OK : GBP_E_INVALID_ARG;
+  if (!s || !a) return GBP_E_INVALID_ARG;
+  DeviceGuard g(t->device);
+  hipStream_t st = t->host_stream;
+  int rc = ensure_ws(t, &t->ws, &t->ws_bytes,
+                     rnd(64 * n) + rnd(80 * n) + rnd(64 * n) + rnd(8 * n) + 2 * rnd(n) +
+                         2 * rnd(4 * n) + 4096);
+  if (rc) return rc;
+  Stage S{t, (char *)t->ws};
+  double *ds = S.take<double>(8 * n), *da = S.take<double>(10 * n);
+  double *dsn = S.take<double>(8 * n), *dtn = S.take<double>(n);
+  uint8_t *dd = S.take<uint8_t>(n), *dv = S.take<uint8_t>(n);
+  uint32_t *df = S.take<uint32_t>(n), *dc = S.take<uint32_t>(n);
+  H2D(ds, s, 64 * n);
+  H2D(da, a, 80 * n);
+  if (direction) H2D(dd, direction, n);
+  // in/out semantics: untouched outputs keep the caller's contents
+  if (s_new) H2D(dsn, s_new, 64 * n);
+  if (t_new) H2D(dtn, t_new, 8 * n);
+  rc = gbp_validate_pairs_dev(t, n, ds, da, direction ? dd : nullptr, direction_all, adaptive,
+                              dv, dsn, dtn, df, dc, st);
+  if (rc) return rc;
+  if (valid) D2H(valid, dv, n);
+  if (s_new) D2H(s_new, dsn, 64 * n);
+  if (t_new) D2H(t_new, dtn, 8 * n);
+  if (flags) D2H(flags, df, 4 * n);
+  if (counts) D2H(counts, dc, 4 * n);
+  HIPCHK(hipStreamSynchronize(st));
+  return GBP_OK;
+}
+
+int gbp_extend_batch_host(gbp_terrain *t, int64_t n, const double *s_near, const double *target,
+                          const uint8_t *direction, int direction_all, int adaptive,
+                          uint64_t seed, int64_t extend_base, int32_t *result, int32_t *chosen,
+                          double *s_new, double *a_new, uint32_t *counts) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n <= 0) return n == 0 ? GBP_OK : GBP_E_INVALID_ARG;
+  if (!s_near || !target || !result || !s_new || !a_new) return GBP_E_INVALID_ARG;
+  DeviceGuard g(t->device);
+  hipStream_t st = t->host_stream;
+  int rc = ensure_ws(t, &t->ws, &t->ws_bytes,
+                     3 * rnd(64 * n) + rnd(80 * n) + rnd(n) + 3 * rnd(4 * n) + 4096);
+  if (rc) return rc;
+  Stage S{t, (char *)t->ws};
+  double *dsn = S.take<double>(8 * n), *dtg = S.take<double>(8 * n);
+  double *dnew = S.take<double>(8 * n), *danew = S.take<double>(10 * n);
+  uint8_t *dd = S.take<uint8_t>(n);
+  int32_t *dr = S.take<int32_t>(n), *dch = S.take<int32_t>(n);
+  uint32_t *dc = S.take<uint32_t>(n);
+  H2D(dsn, s_near, 64 * n);
+  H2D(dtg, target, 64 * n);
+  H2D(dnew, s_new, 64 * n);
+  H2D(danew, a_new, 80 * n);
+  if (direction) H2D(dd, direction, n);
+  rc = gbp_extend_batch_dev(t, n, dsn, dtg, direction ? dd : nullptr, direction_all, adaptive,
+                            seed, extend_base, dr, dch, dnew, danew, dc, st);
+  if (rc) return rc;
+  D2H(result, dr, 4 * n);
+  if (chosen) D2H(chosen, dch, 4 * n);
+  D2H(s_new, dnew, 64 * n);
+  D2H(a_new, danew, 80 * n);
+  if (counts) D2H(counts, dc, 4 * n);
+  HIPCHK(hipStreamSynchronize(st));
+  return GBP_OK;
+}
+
+int gbp_nearest_batch_host(int64_t n_query, const double *queries, int64_t n_vert,
+                           const double *vertices, int32_t *index, double *dist) {
+  if (n_query <= 0) return n_query == 0 ? GBP_OK : GBP_E_INVALID_ARG;
+  if (!queries || !index || (n_vert > 0 && !vertices)) return GBP_E_INVALID_ARG;
+  void *buf = nullptr;
+  const size_t need = rnd(64 * n_query) + rnd(64 * (n_vert > 0 ? n_vert : 1)) +
+                      rnd(4 * n_query) + rnd(8 * n_query) + 1024;
+  if (hipMalloc(&buf, need) != hipSuccess) return GBP_E_ALLOC;
+  char *p = (char *)buf;
+  double *dq = (double *)p; p += rnd(64 * n_query);
+  double *dv = (double *)p; p += rnd(64 * (n_vert > 0 ? n_vert : 1));
+  int32_t *di = (int32_t *)p; p += rnd(4 * n_query);
+  double *dd = (double *)p;
+  hipStream_t st = nullptr;
+  int rc = GBP_OK;
+  if (hipMemcpy(dq, queries, 64 * n_query, hipMemcpyHostToDevice) != hipSuccess) rc = GBP_E_HIP;
+  if (!rc && n_vert > 0 &&
+      hipMemcpy(dv, vertices, 64 * n_vert, hipMemcpyHostToDevice) != hipSuccess)
+    rc = GBP_E_HIP;
+  if (!rc) rc = gbp_nearest_batch_dev(n_query, dq, n_vert, dv, di, dd, st);
+  if (!rc && hipMemcpy(index, di, 4 * n_query, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = GBP_E_HIP;
+  if (!rc && dist && hipMemcpy(dist, dd, 8 * n_query, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = GBP_E_HIP;
+  (void)hipFree(buf);
+  return rc;
+}
+
+}  // extern "C"

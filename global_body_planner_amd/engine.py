@@ -1,0 +1,273 @@
+"""Device-side engine API over the C ABI (torch tensors for HBM residency/streams).
+
+`Terrain` owns one gbp_terrain handle (one GPU).  Every batched call takes
+device tensors (float64 AoS states [n, 8] / actions [n, 10]) and enqueues the
+HIP kernels on torch's current stream for that device; results are device
+tensors.  Host (numpy) variants mirror the `_host` C entry points.
+"""
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from ._lib import check
+
+_VP = ctypes.c_void_p
+
+
+def _ptr(t):
+    return None if t is None else _VP(t.data_ptr())
+
+
+def _np_ptr(a):
+    return None if a is None else a.ctypes.data_as(_VP)
+
+
+def _stream(device):
+    return _VP(torch.cuda.current_stream(device).cuda_stream)
+
+
+@dataclass
+class PairResult:
+    valid: torch.Tensor     # uint8 [n]
+    s_new: torch.Tensor     # float64 [n, 8] (rows untouched where flags lack SNEW_SET)
+    t_new: torch.Tensor     # float64 [n]
+    flags: torch.Tensor     # int32 view of the uint32 flag word [n]
+    counts: torch.Tensor    # int32 view of G | V << 16 [n]
+
+
+@dataclass
+class ExtendResult:
+    result: torch.Tensor    # int32 TRAPPED / ADVANCED / REACHED
+    chosen: torch.Tensor    # int32 candidate index or -1
+    s_new: torch.Tensor
+    a_new: torch.Tensor
+    counts: torch.Tensor
+
+
+class Terrain:
+    """A FastTerrainMap resident in HBM (x-major heights, fp32 when lossless)."""
+
+    def __init__(self, x, y, z, dx=None, dy=None, dz=None, device=0,
+                 storage=L.STORAGE_AUTO, kernel=None):
+        self._lib = L.load()
+        self.device = int(device)
+        self.torch_device = torch.device("cuda", self.device)
+        x = np.ascontiguousarray(x, np.float64)
+        y = np.ascontiguousarray(y, np.float64)
+        z = np.ascontiguousarray(z, np.float64)
+        if z.shape != (x.size, y.size):
+            raise ValueError(f"z must be x-major [{x.size}][{y.size}], got {z.shape}")
+        nl = [None if v is None else np.ascontiguousarray(v, np.float64) for v in (dx, dy, dz)]
+        h = _VP()
+        check(self._lib.gbp_terrain_create(self.device, x.size, y.size, _np_ptr(x), _np_ptr(y),
+                                           _np_ptr(z), *[_np_ptr(v) for v in nl], int(storage),
+                                           ctypes.byref(h)), "gbp_terrain_create")
+        self._h = h
+        self.nx, self.ny = x.size, y.size
+        if kernel is not None:
+            self.set_option(L.OPT_KERNEL, kernel)
+
+    @classmethod
+    def from_data(cls, td, **kw):
+        return cls(td.x, td.y, td.z, td.dx, td.dy, td.dz, **kw)
+
+    # ---- handle ---------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.gbp_terrain_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self):
+        nx, ny, st, dev = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        b = (ctypes.c_double * 4)()
+        check(self._lib.gbp_terrain_info(self._h, ctypes.byref(nx), ctypes.byref(ny),
+                                         ctypes.byref(st), b, ctypes.byref(dev)), "info")
+        return {"nx": nx.value, "ny": ny.value, "storage": st.value, "bounds": tuple(b),
+                "device": dev.value}
+
+    def set_option(self, key, value):
+        check(self._lib.gbp_terrain_set_option(self._h, int(key), int(value)), "set_option")
+
+    def get_option(self, key):
+        v = ctypes.c_int64()
+        check(self._lib.gbp_terrain_get_option(self._h, int(key), ctypes.byref(v)), "get_option")
+        return v.value
+
+    # ---- helpers --------------------------------------------------------------
+    def _dev(self, t, dtype, shape_tail=None, name="tensor"):
+        if not isinstance(t, torch.Tensor):
+            t = torch.as_tensor(np.asarray(t))
+        t = t.to(device=self.torch_device, dtype=dtype).contiguous()
+        if shape_tail is not None:
+            t = t.reshape(-1, *shape_tail)
+        return t
+
+    def _empty(self, shape, dtype):
+        return torch.empty(shape, dtype=dtype, device=self.torch_device)
+
+    # ---- K1 -------------------------------------------------------------------
+    def height(self, xy):
+        xy = self._dev(xy, torch.float64, (2,))
+        n = xy.shape[0]
+        h = self._empty(n, torch.float64)
+        nan = self._empty(n, torch.uint8)
+        ood = self._empty(n, torch.uint8)
+        check(self._lib.gbp_height_batch_dev(self._h, n, _ptr(xy), _ptr(h), _ptr(nan), _ptr(ood),
+                                             _stream(self.device)), "height")
+        return h, nan, ood
+
+    def normal(self, xy):
+        xy = self._dev(xy, torch.float64, (2,))
+        n = xy.shape[0]
+        nrm = self._empty((n, 3), torch.float64)
+        ood = self._empty(n, torch.uint8)
+        check(self._lib.gbp_normal_batch_dev(self._h, n, _ptr(xy), _ptr(nrm), _ptr(ood),
+                                             _stream(self.device)), "normal")
+        return nrm, ood
+
+    def valid_states(self, states, phase):
+        s = self._dev(states, torch.float64, (8,))
+        n = s.shape[0]
+        ph, pall = (None, int(phase)) if np.ndim(phase) == 0 and not isinstance(phase, torch.Tensor) \
+            else (self._dev(phase, torch.uint8), 0)
+        v = self._empty(n, torch.uint8)
+        f = self._empty(n, torch.int32)
+        c = self._empty(n, torch.int32)
+        check(self._lib.gbp_valid_states_dev(self._h, n, _ptr(s), _ptr(ph), pall, _ptr(v), _ptr(f),
+                                             _ptr(c), _stream(self.device)), "valid_states")
+        return v, f, c
+
+    # ---- K2: the hot path -----------------------------------------------------
+    def validate_pairs(self, s, a, direction, adaptive=False, s_new=None, t_new=None,
+                       out=None):
+        """Batched isValidStateActionPair[Reverse] (planning_utils.cpp:645-881).
+
+        `s_new` / `t_new` (optional, device) are in/out like the reference's
+        reference parameters: rows the reference would not assign keep their
+        contents.  `out` may carry preallocated PairResult buffers (bench)."""
+        s = self._dev(s, torch.float64, (8,))
+        a = self._dev(a, torch.float64, (10,))
+        n = s.shape[0]
+        if a.shape[0] != n:
+            raise ValueError("s and a batch sizes differ")
+        if isinstance(direction, torch.Tensor) or np.ndim(direction) > 0:
+            d, dall = self._dev(direction, torch.uint8), 0
+        else:
+            d, dall = None, int(direction)
+        if out is None:
+            out = PairResult(
+                valid=self._empty(n, torch.uint8),
+                s_new=self._dev(s_new, torch.float64, (8,)) if s_new is not None
+                else torch.full((n, 8), float("nan"), dtype=torch.float64, device=self.torch_device),
+                t_new=self._dev(t_new, torch.float64) if t_new is not None
+                else torch.full((n,), float("nan"), dtype=torch.float64, device=self.torch_device),
+                flags=self._empty(n, torch.int32),
+                counts=self._empty(n, torch.int32))
+        check(self._lib.gbp_validate_pairs_dev(
+            self._h, n, _ptr(s), _ptr(a), _ptr(d), dall, int(bool(adaptive)), _ptr(out.valid),
+            _ptr(out.s_new), _ptr(out.t_new), _ptr(out.flags), _ptr(out.counts),
+            _stream(self.device)), "validate_pairs")
+        return out
+
+    def validate_pairs_raw(self, n, s_ptr, a_ptr, d_ptr, dall, adaptive, valid_ptr, snew_ptr,
+                           tnew_ptr, flags_ptr, counts_ptr, stream_ptr):
+        """Pointer-level call for the timed loop (no allocation, no checks)."""
+        return self._lib.gbp_validate_pairs_dev(self._h, n, s_ptr, a_ptr, d_ptr, dall, adaptive,
+                                                valid_ptr, snew_ptr, tnew_ptr, flags_ptr,
+                                                counts_ptr, stream_ptr)
+
+    # ---- K3 -------------------------------------------------------------------
+    def sample_states(self, n, seed, stream_id, index_base=0, require_phase=-1, max_tries=1):
+        st = self._empty((n, 8), torch.float64)
+        tries = self._empty(n, torch.int32)
+        check(self._lib.gbp_sample_states_dev(self._h, n, seed, stream_id, index_base,
+                                              int(require_phase), int(max_tries), _ptr(st),
+                                              _ptr(tries), _stream(self.device)), "sample_states")
+        return st, tries
+
+    def sample_actions(self, normals, seed, stream_id, index_base=0):
+        nr = self._dev(normals, torch.float64, (3,))
+        n = nr.shape[0]
+        a = self._empty((n, 10), torch.float64)
+        check(self._lib.gbp_sample_actions_dev(n, _ptr(nr), seed, stream_id, index_base, _ptr(a),
+                                               _stream(self.device)), "sample_actions")
+        return a
+
+    def extend(self, s_near, target, direction, seed, extend_base=0, adaptive=False):
+        """Batched RRTClass::newConfig + extend acceptance (rrt.cpp:20-102)."""
+        sn = self._dev(s_near, torch.float64, (8,))
+        tg = self._dev(target, torch.float64, (8,))
+        n = sn.shape[0]
+        if isinstance(direction, torch.Tensor) or np.ndim(direction) > 0:
+            d, dall = self._dev(direction, torch.uint8), 0
+        else:
+            d, dall = None, int(direction)
+        r = ExtendResult(
+            result=self._empty(n, torch.int32), chosen=self._empty(n, torch.int32),
+            s_new=torch.full((n, 8), float("nan"), dtype=torch.float64, device=self.torch_device),
+            a_new=torch.full((n, 10), float("nan"), dtype=torch.float64, device=self.torch_device),
+            counts=self._empty(n, torch.int32))
+        check(self._lib.gbp_extend_batch_dev(self._h, n, _ptr(sn), _ptr(tg), _ptr(d), dall,
+                                             int(bool(adaptive)), seed, extend_base, _ptr(r.result),
+                                             _ptr(r.chosen), _ptr(r.s_new), _ptr(r.a_new),
+                                             _ptr(r.counts), _stream(self.device)), "extend")
+        return r
+
+    # ---- host variants (numpy in/out) -------------------------------------------
+    def validate_pairs_host(self, s, a, direction, adaptive=False):
+        s = np.ascontiguousarray(s, np.float64).reshape(-1, 8)
+        a = np.ascontiguousarray(a, np.float64).reshape(-1, 10)
+        n = s.shape[0]
+        if np.ndim(direction) > 0:
+            d, dall = np.ascontiguousarray(direction, np.uint8), 0
+        else:
+            d, dall = None, int(direction)
+        valid = np.empty(n, np.uint8)
+        s_new = np.full((n, 8), np.nan)
+        t_new = np.full(n, np.nan)
+        flags = np.empty(n, np.uint32)
+        counts = np.empty(n, np.uint32)
+        check(self._lib.gbp_validate_pairs_host(self._h, n, _np_ptr(s), _np_ptr(a), _np_ptr(d),
+                                                dall, int(bool(adaptive)), _np_ptr(valid),
+                                                _np_ptr(s_new), _np_ptr(t_new), _np_ptr(flags),
+                                                _np_ptr(counts)), "validate_pairs_host")
+        return valid, s_new, t_new, flags, counts
+
+    def height_host(self, xy):
+        xy = np.ascontiguousarray(xy, np.float64).reshape(-1, 2)
+        n = xy.shape[0]
+        h = np.empty(n)
+        nan = np.empty(n, np.uint8)
+        ood = np.empty(n, np.uint8)
+        check(self._lib.gbp_height_batch_host(self._h, n, _np_ptr(xy), _np_ptr(h), _np_ptr(nan),
+                                              _np_ptr(ood)), "height_host")
+        return h, nan, ood
+
+
+def nearest(queries, vertices):
+    """Batched PlannerClass::getNearestNeighbor (planner_class.cpp:185-200)."""
+    lib = L.load()
+    q = queries.contiguous()
+    v = vertices.contiguous()
+    n = q.shape[0]
+    idx = torch.empty(n, dtype=torch.int32, device=q.device)
+    dist = torch.empty(n, dtype=torch.float64, device=q.device)
+    check(lib.gbp_nearest_batch_dev(n, _ptr(q), v.shape[0], _ptr(v), _ptr(idx), _ptr(dist),
+                                    _stream(q.device.index or 0)), "nearest")
+    return idx, dist
+
+
+def device_count():
+    lib = L.load()
+    c = ctypes.c_int(0)
+    lib.gbp_device_count(ctypes.byref(c))
+    return c.value

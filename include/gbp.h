@@ -1,0 +1,226 @@
+/*
+ * gbp.h — C ABI of the MI355X batched RRT-Connect extend/validity engine.
+ *
+ * This is the drop-in boundary for the hot path of LiuShenLan/global_body_planner
+ * (reference snapshot 2025-02-04).  Every entry point below replaces one reference
+ * C++ interface; the reference file:line it stands in for is cited on each.
+ *
+ *   - plain C: opaque handles, int status codes (GBP_OK = 0, < 0 = error), no
+ *     exceptions cross this boundary, no torch / HIP types in the signatures
+ *     (a stream is passed as an opaque `void*` = hipStream_t, NULL = default).
+ *   - State  = double[8]  {x, y, z, dx, dy, dz, p, dp}   (planning_utils.h:57-61)
+ *   - Action = double[10] {a_x_td, a_y_td, a_z_td, a_x_to, a_y_to, a_z_to,
+ *                          t_s, t_f, a_p_td, a_p_to}     (planning_utils.h:58-62)
+ *     Batches are AoS `double[n][8]` / `double[n][10]`, i.e. exactly the
+ *     std::array layout, so a std::vector<State> can be passed as-is.
+ *   - All arithmetic is IEEE FP64 in the reference operation order, compiled
+ *     without FMA contraction, so decisions are bit-exact with the reference
+ *     algorithm (see DESIGN.md "Parity").
+ *   - `_dev` entry points take DEVICE pointers and enqueue on `stream`
+ *     (asynchronous); `_host` entry points take host pointers and block.
+ *   - A handle is used by one host thread at a time; there is no global mutable
+ *     state, so distinct handles (e.g. one per GPU) are fully reentrant.
+ */
+#ifndef GBP_H
+#define GBP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define GBP_OK              0
+#define GBP_E_INVALID_ARG  (-1)
+#define GBP_E_BAD_HANDLE   (-2)
+#define GBP_E_ALLOC        (-3)
+#define GBP_E_HIP          (-4)
+#define GBP_E_SHAPE        (-5)
+#define GBP_E_NO_DEVICE    (-6)
+#define GBP_E_UNSUPPORTED  (-7)
+
+/* ---- reference enums (planning_utils.h:50-54, rrt.h:7-9) ---------------- */
+#define GBP_FLIGHT          0
+#define GBP_STANCE          1
+#define GBP_CONNECT_STANCE  2
+#define GBP_FORWARD         0
+#define GBP_REVERSE         1
+#define GBP_TRAPPED         0
+#define GBP_ADVANCED        1
+#define GBP_REACHED         2
+
+#define GBP_STATE_DIM       8
+#define GBP_ACTION_DIM     10
+#define GBP_NUM_GEN_STATES  6   /* planning_utils.h:45 */
+
+/* ---- per-attempt flag word (output of the validate/extend entry points) -- */
+#define GBP_F_VALID      (1u << 0)  /* the pair check returned true                      */
+#define GBP_F_OOD        (1u << 1)  /* a lookup whose reference result is UB (point outside
+                                       [x_0,x_{N-1}) x [y_0,y_{N-1}), fast_terrain_map.cpp:96-117)
+                                       was reached; by this engine's convention the state is
+                                       invalid (DESIGN.md "Out-of-domain convention")       */
+#define GBP_F_NAN        (1u << 2)  /* a state failed on a NaN terrain cell                 */
+#define GBP_F_SNEW_SET   (1u << 3)  /* the reference assigned s_new (else buffer untouched) */
+#define GBP_F_TNEW_SET   (1u << 4)  /* the reference assigned t_new (else buffer untouched) */
+#define GBP_F_FRAGILE    (1u << 5)  /* a trig-dependent comparison was within 1e-12 of its
+                                       threshold (decision could differ across libm builds) */
+#define GBP_F_LIMIT      (1u << 6)  /* the pair needed more than GBP_MAX_SAMPLES state checks
+                                       (e.g. t_s = inf: the reference never terminates); the
+                                       check is stopped and reported invalid                 */
+#define GBP_MAX_SAMPLES  4096u
+#define GBP_F_STAGE_SHIFT 8u        /* bits 8..11: stage in which the check ended          */
+#define GBP_F_STAGE_MASK  (0xFu << GBP_F_STAGE_SHIFT)
+#define GBP_STAGE_FWD_STANCE 1u     /* planning_utils.cpp:718-730 */
+#define GBP_STAGE_FWD_FLIGHT 2u     /* :735-741 */
+#define GBP_STAGE_FWD_LAND   3u     /* :743-749 */
+#define GBP_STAGE_REV_FLIGHT 4u     /* :842-847 */
+#define GBP_STAGE_REV_STANCE 5u     /* :852-863 */
+#define GBP_STAGE_REV_START  6u     /* :866-872 */
+
+/* lookup counters: counts[i] = G | (V << 16), G = executed getGroundHeight calls,
+   V = executed isValidState calls (reference semantics).         */
+#define GBP_COUNT_G(c) ((c) & 0xFFFFu)
+#define GBP_COUNT_V(c) ((c) >> 16)
+
+/* ---- opaque handles ------------------------------------------------------ */
+typedef struct gbp_terrain gbp_terrain;
+typedef void *gbp_stream; /* hipStream_t; NULL = the device's null stream */
+
+/* ---- library / device ---------------------------------------------------- */
+int         gbp_version(void);                 /* 10000*major + 100*minor + patch */
+const char *gbp_status_string(int status);
+int         gbp_device_count(int *count);
+int         gbp_device_alloc(int device, size_t bytes, void **ptr);
+int         gbp_device_free(void *ptr);
+int         gbp_memcpy_h2d(void *dst, const void *src, size_t bytes, gbp_stream stream);
+int         gbp_memcpy_d2h(void *dst, const void *src, size_t bytes, gbp_stream stream);
+int         gbp_stream_synchronize(gbp_stream stream);
+
+/* ---- terrain (replaces FastTerrainMap storage + loadData,
+ *      fast_terrain_map.h:97-118, fast_terrain_map.cpp:10-28) -------------- */
+#define GBP_STORAGE_AUTO 0  /* fp32 if every z value round-trips through float, else fp64 */
+#define GBP_STORAGE_F32  1  /* lossless for grid_map-sourced maps (fast_terrain_map.cpp:60) */
+#define GBP_STORAGE_F64  2
+
+/* x[nx], y[ny] ascending coordinates; z, dx, dy, dz are x-major [nx][ny]
+ * (z[ix*ny + iy] == z_data_[ix][iy]).  dx/dy/dz may be NULL => (0, 0, 1),
+ * as loadDataFromGridMap does for maps without slope layers (:70-74). */
+int gbp_terrain_create(int device, int nx, int ny, const double *x, const double *y,
+                       const double *z, const double *dx, const double *dy,
+                       const double *dz, int storage, gbp_terrain **out);
+int gbp_terrain_destroy(gbp_terrain *t);
+/* bounds = {x_0, x_{N-1}, y_0, y_{M-1}} (the getXData().front()/back() values) */
+int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage,
+                     double bounds[4], int *device);
+
+/* engine options (per handle) */
+#define GBP_OPT_KERNEL        1  /* GBP_KERNEL_* for the validate/extend entry points */
+#define GBP_OPT_BLOCK         2  /* threads per workgroup (multiple of 64)            */
+#define GBP_OPT_GRID_PER_CU   3  /* persistent kernel: workgroups per CU              */
+#define GBP_OPT_WAVES         4  /* register budget: min waves per SIMD (1, 2 or 4)   */
+#define GBP_KERNEL_DIRECT     0  /* one lane per attempt                              */
+#define GBP_KERNEL_PERSISTENT 1  /* persistent waves, lanes re-packed per sample      */
+int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value);
+int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value);
+
+/* ---- batched terrain queries ---------------------------------------------
+ * FastTerrainMap::getGroundHeight + heightIsNan (fast_terrain_map.cpp:94-157)
+ * xy[n][2] in; height[n], is_nan[n], ood[n] out (any output may be NULL).
+ * An ood point gets height NaN and is_nan 1 (reference: undefined). */
+int gbp_height_batch_dev(gbp_terrain *t, int64_t n, const double *xy, double *height,
+                         uint8_t *is_nan, uint8_t *ood, gbp_stream stream);
+int gbp_height_batch_host(gbp_terrain *t, int64_t n, const double *xy, double *height,
+                          uint8_t *is_nan, uint8_t *ood);
+/* FastTerrainMap::getSurfaceNormal (fast_terrain_map.cpp:160-213): normal[n][3] */
+int gbp_normal_batch_dev(gbp_terrain *t, int64_t n, const double *xy, double *normal,
+                         uint8_t *ood, gbp_stream stream);
+int gbp_normal_batch_host(gbp_terrain *t, int64_t n, const double *xy, double *normal,
+                          uint8_t *ood);
+
+/* ---- state validity (planning_utils::isValidState, planning_utils.cpp:562-635)
+ * states[n][8], phase[n] (or NULL => phase_all) -> valid[n], flags[n], counts[n] */
+int gbp_valid_states_dev(gbp_terrain *t, int64_t n, const double *states,
+                         const uint8_t *phase, int phase_all, uint8_t *valid,
+                         uint32_t *flags, uint32_t *counts, gbp_stream stream);
+int gbp_valid_states_host(gbp_terrain *t, int64_t n, const double *states,
+                          const uint8_t *phase, int phase_all, uint8_t *valid,
+                          uint32_t *flags, uint32_t *counts);
+
+/* ---- THE HOT PATH: batched state-action pair checks ----------------------
+ * planning_utils::isValidStateActionPair / isValidStateActionPairReverse
+ * (+ the AdaptiveStepSize variants when adaptive != 0),
+ * planning_utils.cpp:645-881.
+ *   s[n][8], a[n][10]; direction[n] (GBP_FORWARD / GBP_REVERSE) or NULL =>
+ *   direction_all.  Outputs (any may be NULL except flags):
+ *   valid[n]      the returned bool
+ *   s_new[n][8]   written ONLY where the reference assigns s_new (GBP_F_SNEW_SET),
+ *                 otherwise the caller's contents are left untouched, exactly
+ *                 like the reference's in/out reference parameter
+ *   t_new[n]      likewise (GBP_F_TNEW_SET)
+ *   flags[n]      GBP_F_* word
+ *   counts[n]     G | V << 16                                               */
+int gbp_validate_pairs_dev(gbp_terrain *t, int64_t n, const double *s, const double *a,
+                           const uint8_t *direction, int direction_all, int adaptive,
+                           uint8_t *valid, double *s_new, double *t_new, uint32_t *flags,
+                           uint32_t *counts, gbp_stream stream);
+int gbp_validate_pairs_host(gbp_terrain *t, int64_t n, const double *s, const double *a,
+                            const uint8_t *direction, int direction_all, int adaptive,
+                            uint8_t *valid, double *s_new, double *t_new, uint32_t *flags,
+                            uint32_t *counts);
+
+/* ---- counter-based samplers (Philox4x32-10, keyed (seed, stream, index)) ---
+ * Identical draws regardless of batching / device count.  The distributions
+ * are the reference's; its unseeded rand() / clock-seeded engines
+ * (planning_utils.cpp:435, planner_class.cpp:51) are not reproducible, so the
+ * engine defines its own reproducible streams.
+ *
+ * PlannerClass::randomState (planner_class.cpp:38-76), index i of stream.
+ * If require_phase >= 0 the draw is repeated (k = 0..max_tries-1) until
+ * isValidState(state, require_phase) holds; tries[i] = k+1 (or -1 if none). */
+int gbp_sample_states_dev(gbp_terrain *t, int64_t n, uint64_t seed, uint64_t stream_id,
+                          int64_t index_base, int require_phase, int max_tries,
+                          double *states, int32_t *tries, gbp_stream stream);
+/* getRandomAction(surf_norm) (planning_utils.cpp:392-442) with rotate_grf
+ * (:198-231): actions[n][10] from normals[n][3]; draw (stream_id, index_base+i). */
+int gbp_sample_actions_dev(int64_t n, const double *normals, uint64_t seed,
+                           uint64_t stream_id, int64_t index_base, double *actions,
+                           gbp_stream stream);
+
+/* ---- batched extend (RRTClass::newConfig + the acceptance half of
+ *      RRTClass::extend, rrt.cpp:20-102) --------------------------------------
+ * For extend i: s_near[i] (the nearest vertex, found by gbp_nearest_batch),
+ * target[i] (the state the tree is extended towards).  Candidate action j
+ * (j = 0..5) is getRandomAction(getSurfaceNormal(target)) drawn from stream
+ * (seed, extend_base + i, j); candidates are checked (forward or reverse by
+ * direction) and the LOWEST valid j is taken — the sequential newConfig.
+ * result[i] = TRAPPED / ADVANCED / REACHED (isWithinBounds(s_new, target));
+ * chosen[i] = j or -1; s_new[i], a_new[i] written when result != TRAPPED.   */
+int gbp_extend_batch_dev(gbp_terrain *t, int64_t n, const double *s_near,
+                         const double *target, const uint8_t *direction,
+                         int direction_all, int adaptive, uint64_t seed,
+                         int64_t extend_base, int32_t *result, int32_t *chosen,
+                         double *s_new, double *a_new, uint32_t *counts,
+                         gbp_stream stream);
+int gbp_extend_batch_host(gbp_terrain *t, int64_t n, const double *s_near,
+                          const double *target, const uint8_t *direction,
+                          int direction_all, int adaptive, uint64_t seed,
+                          int64_t extend_base, int32_t *result, int32_t *chosen,
+                          double *s_new, double *a_new, uint32_t *counts);
+
+/* ---- nearest neighbour (PlannerClass::getNearestNeighbor,
+ *      planner_class.cpp:185-200) ----------------------------------------------
+ * vertices[n_vert][8] (device-resident SoA-free flat tree), queries[n_q][8];
+ * index[i] = argmin_v stateDistance(query_i, v) with ties to the LOWEST index
+ * (the reference ties to unordered_map iteration order). */
+int gbp_nearest_batch_dev(int64_t n_query, const double *queries, int64_t n_vert,
+                          const double *vertices, int32_t *index, double *dist,
+                          gbp_stream stream);
+int gbp_nearest_batch_host(int64_t n_query, const double *queries, int64_t n_vert,
+                           const double *vertices, int32_t *index, double *dist);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GBP_H */

@@ -1,0 +1,293 @@
+"""ctypes binding of the CPU restatement (oracle/gbp_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product package
+(global_body_planner_amd/), which must fail loudly without its HIP library.
+
+Parity status: the reference's tests pin nothing and the reference cannot be
+compiled in this image (its headers include ROS / grid_map / Eigen), so
+bit-level parity against reference OUTPUTS is unpinned; see DESIGN.md and
+tests/test_oracle_pins.py for the survey-recorded reference outputs this
+restatement is pinned to.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+FORWARD, REVERSE = 0, 1
+FLIGHT, STANCE = 0, 1
+TRAPPED, ADVANCED, REACHED = 0, 1, 2
+
+
+def build(force=False):
+    """Compile liboracle.so with the committed Makefile (gcc only)."""
+    src = os.path.join(_HERE, "gbp_oracle.c")
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.run(["make", "-C", _HERE, "-s"], check=True)
+    return _LIB_PATH
+
+
+class _Terrain(ctypes.Structure):
+    _fields_ = [
+        ("nx", ctypes.c_int),
+        ("ny", ctypes.c_int),
+        ("x", ctypes.c_void_p),
+        ("y", ctypes.c_void_p),
+        ("z", ctypes.c_void_p),
+        ("dx", ctypes.c_void_p),
+        ("dy", ctypes.c_void_p),
+        ("dz", ctypes.c_void_p),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P, I, D, U64, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_uint64, ctypes.c_int64
+        sig = {
+            "orc_set_scan_mode": (None, [I]),
+            "orc_get_scan_mode": (I, []),
+            "orc_ground_height": (D, [P, D, D, P]),
+            "orc_height_is_nan": (I, [P, D, D, P]),
+            "orc_surface_normal": (None, [P, D, D, P, P]),
+            "orc_apply_stance": (None, [P, P, D, P]),
+            "orc_apply_flight": (None, [P, D, P]),
+            "orc_apply_stance_reverse": (None, [P, P, D, P]),
+            "orc_is_valid_action": (I, [P]),
+            "orc_is_valid_pair": (I, [P, P, P, I, I, P, P, P, P]),
+            "orc_pose_distance": (D, [P, P]),
+            "orc_state_distance": (D, [P, P]),
+            "orc_state_yaw_distance": (D, [P, P]),
+            "orc_attempt_connect": (I, [P, P, P, D, P, P, I, I]),
+            "orc_validate_pairs": (None, [P, I64, P, P, P, I, I, P, P, P, P, P, I]),
+            "orc_valid_states": (None, [P, I64, P, P, I, P, P, P, I]),
+            "orc_height_batch": (None, [P, I64, P, P, P, P, I]),
+            "orc_normal_batch": (None, [P, I64, P, P, P, I]),
+            "orc_extend_batch": (None, [P, I64, P, P, P, P, I, I, P, P, P, P, P, I]),
+            "orc_nearest_batch": (None, [I64, P, I, P, P, P, I]),
+            "orc_sample_states": (None, [P, I64, U64, U64, I64, I, I, P, P, I]),
+            "orc_sample_actions": (None, [I64, P, U64, U64, I64, P, I]),
+            "orc_philox4x32_10": (None, [P, P, P]),
+            "orc_uniform2": (None, [U64, U64, ctypes.c_uint32, I64, ctypes.c_uint32, P]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+class OracleTerrain:
+    """A FastTerrainMap restated on the CPU (x-major arrays, float64)."""
+
+    def __init__(self, x, y, z, dx=None, dy=None, dz=None):
+        self.x = _c(x, np.float64)
+        self.y = _c(y, np.float64)
+        self.z = _c(z, np.float64)
+        self.nx, self.ny = self.x.size, self.y.size
+        assert self.z.shape == (self.nx, self.ny)
+        self.dx = None if dx is None else _c(dx, np.float64)
+        self.dy = None if dy is None else _c(dy, np.float64)
+        self.dz = None if dz is None else _c(dz, np.float64)
+        self._s = _Terrain(self.nx, self.ny, self.x.ctypes.data, self.y.ctypes.data,
+                           self.z.ctypes.data,
+                           None if self.dx is None else self.dx.ctypes.data,
+                           None if self.dy is None else self.dy.ctypes.data,
+                           None if self.dz is None else self.dz.ctypes.data)
+
+    @classmethod
+    def from_data(cls, td):
+        return cls(td.x, td.y, td.z, td.dx, td.dy, td.dz)
+
+    @property
+    def ref(self):
+        return ctypes.byref(self._s)
+
+    # scalar reference calls -------------------------------------------------
+    def ground_height(self, x, y):
+        o = ctypes.c_int(0)
+        h = lib().orc_ground_height(self.ref, x, y, ctypes.byref(o))
+        return h, bool(o.value)
+
+    def height_is_nan(self, x, y):
+        o = ctypes.c_int(0)
+        r = lib().orc_height_is_nan(self.ref, x, y, ctypes.byref(o))
+        return bool(r), bool(o.value)
+
+    # batches ------------------------------------------------------------------
+    def height_batch(self, xy, nthreads=1):
+        xy = _c(xy, np.float64).reshape(-1, 2)
+        n = xy.shape[0]
+        h = np.empty(n)
+        nan = np.empty(n, np.uint8)
+        ood = np.empty(n, np.uint8)
+        lib().orc_height_batch(self.ref, n, _p(xy), _p(h), _p(nan), _p(ood), nthreads)
+        return h, nan, ood
+
+    def normal_batch(self, xy, nthreads=1):
+        xy = _c(xy, np.float64).reshape(-1, 2)
+        n = xy.shape[0]
+        nrm = np.empty((n, 3))
+        ood = np.empty(n, np.uint8)
+        lib().orc_normal_batch(self.ref, n, _p(xy), _p(nrm), _p(ood), nthreads)
+        return nrm, ood
+
+    def valid_states(self, states, phase, nthreads=1):
+        states = _c(states, np.float64).reshape(-1, 8)
+        n = states.shape[0]
+        valid = np.empty(n, np.uint8)
+        flags = np.empty(n, np.uint32)
+        counts = np.empty(n, np.uint32)
+        ph = None
+        pall = 0
+        if np.ndim(phase) == 0:
+            pall = int(phase)
+        else:
+            ph = _c(phase, np.uint8)
+        lib().orc_valid_states(self.ref, n, _p(states), _p(ph), pall, _p(valid), _p(flags),
+                               _p(counts), nthreads)
+        return valid, flags, counts
+
+    def validate_pairs(self, s, a, direction, adaptive=False, s_new_init=None, t_new_init=None,
+                       nthreads=1):
+        s = _c(s, np.float64).reshape(-1, 8)
+        a = _c(a, np.float64).reshape(-1, 10)
+        n = s.shape[0]
+        valid = np.empty(n, np.uint8)
+        s_new = np.full((n, 8), np.nan) if s_new_init is None else _c(s_new_init, np.float64).copy()
+        t_new = np.full(n, np.nan) if t_new_init is None else _c(t_new_init, np.float64).copy()
+        flags = np.empty(n, np.uint32)
+        counts = np.empty(n, np.uint32)
+        d = None
+        dall = 0
+        if np.ndim(direction) == 0:
+            dall = int(direction)
+        else:
+            d = _c(direction, np.uint8)
+        lib().orc_validate_pairs(self.ref, n, _p(s), _p(a), _p(d), dall, int(bool(adaptive)),
+                                 _p(valid), _p(s_new), _p(t_new), _p(flags), _p(counts), nthreads)
+        return valid, s_new, t_new, flags, counts
+
+    def extend_batch(self, s_near, target, actions, direction, adaptive=False, nthreads=1):
+        s_near = _c(s_near, np.float64).reshape(-1, 8)
+        target = _c(target, np.float64).reshape(-1, 8)
+        n = s_near.shape[0]
+        actions = _c(actions, np.float64).reshape(n, 6, 10)
+        result = np.empty(n, np.int32)
+        chosen = np.empty(n, np.int32)
+        s_new = np.full((n, 8), np.nan)
+        a_new = np.full((n, 10), np.nan)
+        counts = np.empty(n, np.uint32)
+        d = None
+        dall = 0
+        if np.ndim(direction) == 0:
+            dall = int(direction)
+        else:
+            d = _c(direction, np.uint8)
+        lib().orc_extend_batch(self.ref, n, _p(s_near), _p(target), _p(actions), _p(d), dall,
+                               int(bool(adaptive)), _p(result), _p(chosen), _p(s_new), _p(a_new),
+                               _p(counts), nthreads)
+        return result, chosen, s_new, a_new, counts
+
+    def sample_states(self, n, seed, stream_id, index_base=0, require_phase=-1, max_tries=1,
+                      nthreads=1):
+        st = np.empty((n, 8))
+        tries = np.empty(n, np.int32)
+        lib().orc_sample_states(self.ref, n, seed, stream_id, index_base, require_phase,
+                                max_tries, _p(st), _p(tries), nthreads)
+        return st, tries
+
+    def attempt_connect(self, s_existing, s, direction, t_s=0.0, adaptive=False):
+        s_existing = _c(s_existing, np.float64)
+        s = _c(s, np.float64)
+        s_new = np.full(8, np.nan)
+        a_new = np.full(10, np.nan)
+        r = lib().orc_attempt_connect(self.ref, _p(s_existing), _p(s), float(t_s), _p(s_new),
+                                      _p(a_new), int(direction), int(bool(adaptive)))
+        return r, s_new, a_new
+
+
+def sample_actions(normals, seed, stream_id, index_base=0, nthreads=1):
+    normals = _c(normals, np.float64).reshape(-1, 3)
+    n = normals.shape[0]
+    out = np.empty((n, 10))
+    lib().orc_sample_actions(n, _p(normals), seed, stream_id, index_base, _p(out), nthreads)
+    return out
+
+
+def nearest_batch(queries, verts, nthreads=1):
+    q = _c(queries, np.float64).reshape(-1, 8)
+    v = _c(verts, np.float64).reshape(-1, 8)
+    idx = np.empty(q.shape[0], np.int32)
+    dist = np.empty(q.shape[0])
+    lib().orc_nearest_batch(q.shape[0], _p(q), v.shape[0], _p(v), _p(idx), _p(dist), nthreads)
+    return idx, dist
+
+
+def apply_stance(s, a, t):
+    o = np.empty(8)
+    lib().orc_apply_stance(_p(_c(s, np.float64)), _p(_c(a, np.float64)), float(t), _p(o))
+    return o
+
+
+def apply_flight(s, t):
+    o = np.empty(8)
+    lib().orc_apply_flight(_p(_c(s, np.float64)), float(t), _p(o))
+    return o
+
+
+def apply_stance_reverse(s, a, t):
+    o = np.empty(8)
+    lib().orc_apply_stance_reverse(_p(_c(s, np.float64)), _p(_c(a, np.float64)), float(t), _p(o))
+    return o
+
+
+def is_valid_action(a):
+    return bool(lib().orc_is_valid_action(_p(_c(a, np.float64))))
+
+
+def state_distance(q1, q2):
+    return lib().orc_state_distance(_p(_c(q1, np.float64)), _p(_c(q2, np.float64)))
+
+
+def pose_distance(q1, q2):
+    return lib().orc_pose_distance(_p(_c(q1, np.float64)), _p(_c(q2, np.float64)))
+
+
+def state_yaw_distance(q1, q2):
+    return lib().orc_state_yaw_distance(_p(_c(q1, np.float64)), _p(_c(q2, np.float64)))
+
+
+def philox(ctr, key):
+    c = np.ascontiguousarray(ctr, np.uint32)
+    k = np.ascontiguousarray(key, np.uint32)
+    o = np.empty(4, np.uint32)
+    lib().orc_philox4x32_10(_p(c), _p(k), _p(o))
+    return o
+
+
+def set_scan_mode(mode):
+    lib().orc_set_scan_mode(int(mode))
+
+
+def get_scan_mode():
+    return lib().orc_get_scan_mode()

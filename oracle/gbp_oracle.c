@@ -1,0 +1,867 @@
+/*
+ * gbp_oracle.c — CPU restatement of the global_body_planner hot path.
+ * TEST INFRASTRUCTURE ONLY (see gbp_oracle.h).  Every function cites the
+ * reference file:line it restates; expressions keep the reference's
+ * left-to-right evaluation order and are compiled with -ffp-contract=off.
+ */
+#include "gbp_oracle.h"
+
+#include <math.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ---- constants: include/global_body_planner/planning_utils.h:21-66 ------ */
+#define H_MAX 0.4
+#define H_MIN 0.075
+#define V_MAX 2.0
+#define V_NOM 0.75
+#define P_MAX 1.0
+#define ANG_ACC_MAX 7.0
+#define ROBOT_L 0.3
+#define ROBOT_W 0.3
+#define ROBOT_H 0.05
+#define M_CONST 13.0
+#define G_CONST 9.81
+#define F_MAX 637.0
+#define MU 1.0
+#define T_F_MAX 0.5
+#define T_F_MIN 0.0
+#define KINEMATICS_RES 0.05
+#define BACKUP_RATIO 0.5
+#define NUM_GEN_STATES 6
+#define GOAL_BOUNDS 0.5
+#define MY_PI 3.14159
+#define FRAGILE_EPS 1e-12
+
+#define PURPOSE_STATE 1u
+#define PURPOSE_ACTION 2u
+
+/* std::min / std::max semantics (NaN behaviour included) */
+static inline double std_min(double a, double b) { return (b < a) ? b : a; }
+static inline double std_max(double a, double b) { return (a < b) ? b : a; }
+
+static int g_scan_mode = 0;
+void orc_set_scan_mode(int mode) { g_scan_mode = mode; }
+int orc_get_scan_mode(void) { return g_scan_mode; }
+
+/* ---- bracket search: fast_terrain_map.cpp:101-117 ----------------------
+ * The reference scans i < size for d[i] <= v && v < d[i+1] (first match) and
+ * leaves the index at its default 0 when nothing matches.  Outcomes:
+ *   i >= 0          a bracket;
+ *   BR_LOW  (-1)    v is NaN or v < d[0]: no match, and the short-circuit of
+ *                   `d[i] <= v` never reads d[size]: well defined, index 0
+ *                   (heightIsNan then tests cell 0; getGroundHeight's x1/x2
+ *                   stay uninitialised -> UB unless v is NaN, which makes the
+ *                   height NaN whatever they hold);
+ *   BR_HIGH (-2)    v >= d[size-1]: the last step reads d[size] -> UB. */
+#define BR_LOW (-1)
+#define BR_HIGH (-2)
+static int bracket(const double *d, int n, double v) {
+  if (g_scan_mode == 0) {
+    for (int i = 0; i < n - 1; i++)
+      if (d[i] <= v && v < d[i + 1]) return i;
+  } else if (d[0] <= v && v < d[n - 1]) {
+    int lo = 0, hi = n - 1; /* d[lo] <= v < d[hi] */
+    while (hi - lo > 1) {
+      int mid = lo + (hi - lo) / 2;
+      if (d[mid] <= v) lo = mid; else hi = mid;
+    }
+    return lo;
+  }
+  return (d[n - 1] <= v) ? BR_HIGH : BR_LOW;
+}
+
+/* bilinear blend, fast_terrain_map.cpp:120-126 (same expression for :191-211) */
+static double bilinear(const double *f, int ny, int ix, int iy, double x1, double x2,
+                       double y1, double y2, double x, double y) {
+  double fx1y1 = f[(long)ix * ny + iy];
+  double fx1y2 = f[(long)ix * ny + iy + 1];
+  double fx2y1 = f[(long)(ix + 1) * ny + iy];
+  double fx2y2 = f[(long)(ix + 1) * ny + iy + 1];
+  return 1.0 / ((x2 - x1) * (y2 - y1)) *
+         (fx1y1 * (x2 - x) * (y2 - y) + fx2y1 * (x - x1) * (y2 - y) +
+          fx1y2 * (x2 - x) * (y - y1) + fx2y2 * (x - x1) * (y - y1));
+}
+
+/* fast_terrain_map.cpp:94-132.  NaN coordinate -> NaN (deterministic);
+ * any other missing bracket -> *ood = 1 (UB), NaN returned. */
+double orc_ground_height(const orc_terrain *T, double x, double y, int *ood) {
+  int ix = bracket(T->x, T->nx, x), iy = bracket(T->y, T->ny, y);
+  if (ood) *ood = 0;
+  if (isnan(x) || isnan(y)) return NAN;
+  if (ix < 0 || iy < 0) { if (ood) *ood = 1; return NAN; }
+  return bilinear(T->z, T->ny, ix, iy, T->x[ix], T->x[ix + 1], T->y[iy], T->y[iy + 1], x, y);
+}
+
+static int cell_has_nan(const orc_terrain *T, int ix, int iy) {
+  const double *z = T->z;
+  long ny = T->ny;
+  return isnan(z[ix * ny + iy]) || isnan(z[ix * ny + iy + 1]) || isnan(z[(ix + 1) * ny + iy]) ||
+         isnan(z[(ix + 1) * ny + iy + 1]);
+}
+
+/* fast_terrain_map.cpp:135-157.  BR_HIGH on either axis -> *ood = 1 (UB),
+ * returns 1; BR_LOW -> index 0 on that axis (the reference default). */
+int orc_height_is_nan(const orc_terrain *T, double x, double y, int *ood) {
+  int ix = bracket(T->x, T->nx, x), iy = bracket(T->y, T->ny, y);
+  if (ood) *ood = 0;
+  if (ix == BR_HIGH || iy == BR_HIGH) { if (ood) *ood = 1; return 1; }
+  return cell_has_nan(T, ix < 0 ? 0 : ix, iy < 0 ? 0 : iy);
+}
+
+/* fast_terrain_map.cpp:160-213 (same bracket rules as getGroundHeight) */
+void orc_surface_normal(const orc_terrain *T, double x, double y, double n[3], int *ood) {
+  int ix = bracket(T->x, T->nx, x), iy = bracket(T->y, T->ny, y);
+  if (ood) *ood = 0;
+  if (isnan(x) || isnan(y) || ix < 0 || iy < 0) {
+    if (ood && !(isnan(x) || isnan(y))) *ood = 1;
+    n[0] = n[1] = n[2] = NAN;
+    return;
+  }
+  if (!T->dx) { n[0] = 0.0; n[1] = 0.0; n[2] = 1.0; return; }
+  double x1 = T->x[ix], x2 = T->x[ix + 1], y1 = T->y[iy], y2 = T->y[iy + 1];
+  n[0] = bilinear(T->dx, T->ny, ix, iy, x1, x2, y1, y2, x, y);
+  n[1] = bilinear(T->dy, T->ny, ix, iy, x1, x2, y1, y2, x, y);
+  n[2] = bilinear(T->dz, T->ny, ix, iy, x1, x2, y1, y2, x, y);
+}
+
+/* ---- propagation -------------------------------------------------------- */
+/* planning_utils.cpp:237-274 */
+void orc_apply_stance(const double *s, const double *a, double t, double *o) {
+  double a_x_td = a[0], a_y_td = a[1], a_z_td = a[2];
+  double a_x_to = a[3], a_y_to = a[4], a_z_to = a[5];
+  double t_s = a[6], a_p_td = a[8], a_p_to = a[9];
+  double x_td = s[0], y_td = s[1], z_td = s[2], dx_td = s[3], dy_td = s[4], dz_td = s[5];
+  double p_td = s[6], dp_td = s[7];
+  double r[8];
+  r[0] = x_td + dx_td * t + 0.5 * a_x_td * t * t + (a_x_to - a_x_td) * (t * t * t) / (6.0 * t_s);
+  r[1] = y_td + dy_td * t + 0.5 * a_y_td * t * t + (a_y_to - a_y_td) * (t * t * t) / (6.0 * t_s);
+  r[2] = z_td + dz_td * t + 0.5 * a_z_td * t * t + (a_z_to - a_z_td) * (t * t * t) / (6.0 * t_s);
+  r[3] = dx_td + a_x_td * t + (a_x_to - a_x_td) * t * t / (2.0 * t_s);
+  r[4] = dy_td + a_y_td * t + (a_y_to - a_y_td) * t * t / (2.0 * t_s);
+  r[5] = dz_td + a_z_td * t + (a_z_to - a_z_td) * t * t / (2.0 * t_s);
+  r[6] = p_td + dp_td * t + 0.5 * a_p_td * t * t + (a_p_to - a_p_td) * (t * t * t) / (6.0 * t_s);
+  r[7] = dp_td + a_p_td * t + (a_p_to - a_p_td) * t * t / (2.0 * t_s);
+  memcpy(o, r, sizeof r);
+}
+
+/* planning_utils.cpp:282-306 (g is the literal 9.81, :283) */
+void orc_apply_flight(const double *s, double t_f, double *o) {
+  double g = 9.81;
+  double r[8];
+  r[0] = s[0] + s[3] * t_f;
+  r[1] = s[1] + s[4] * t_f;
+  r[2] = s[2] + s[5] * t_f - 0.5 * g * t_f * t_f;
+  r[3] = s[3];
+  r[4] = s[4];
+  r[5] = s[5] - g * t_f;
+  r[6] = s[6] + s[7] * t_f;
+  r[7] = s[7];
+  memcpy(o, r, sizeof r);
+}
+
+/* planning_utils.cpp:324-367 */
+void orc_apply_stance_reverse(const double *s, const double *a, double t, double *o) {
+  double a_x_td = a[0], a_y_td = a[1], a_z_td = a[2];
+  double a_x_to = a[3], a_y_to = a[4], a_z_to = a[5];
+  double t_s = a[6], a_p_td = a[8], a_p_to = a[9];
+  double x_to = s[0], y_to = s[1], z_to = s[2], dx_to = s[3], dy_to = s[4], dz_to = s[5];
+  double p_to = s[6], dp_to = s[7];
+  double cx = dx_to - a_x_td * t_s - 0.5 * (a_x_to - a_x_td) * t_s;
+  double cy = dy_to - a_y_td * t_s - 0.5 * (a_y_to - a_y_td) * t_s;
+  double cz = dz_to - a_z_td * t_s - 0.5 * (a_z_to - a_z_td) * t_s;
+  double cp = dp_to - a_p_td * t_s - 0.5 * (a_p_to - a_p_td) * t_s;
+  double r[8];
+  r[0] = x_to - cx * (t_s - t) - 0.5 * a_x_td * (t_s * t_s - t * t) -
+         (a_x_to - a_x_td) * (t_s * t_s * t_s - t * t * t) / (6.0 * t_s);
+  r[1] = y_to - cy * (t_s - t) - 0.5 * a_y_td * (t_s * t_s - t * t) -
+         (a_y_to - a_y_td) * (t_s * t_s * t_s - t * t * t) / (6.0 * t_s);
+  r[2] = z_to - cz * (t_s - t) - 0.5 * a_z_td * (t_s * t_s - t * t) -
+         (a_z_to - a_z_td) * (t_s * t_s * t_s - t * t * t) / (6.0 * t_s);
+  r[3] = dx_to - a_x_td * (t_s - t) - (a_x_to - a_x_td) * (t_s * t_s - t * t) / (2.0 * t_s);
+  r[4] = dy_to - a_y_td * (t_s - t) - (a_y_to - a_y_td) * (t_s * t_s - t * t) / (2.0 * t_s);
+  r[5] = dz_to - a_z_td * (t_s - t) - (a_z_to - a_z_td) * (t_s * t_s - t * t) / (2.0 * t_s);
+  r[7] = dp_to - a_p_td * (t_s - t) - (a_p_to - a_p_td) * (t_s * t_s - t * t) / (2.0 * t_s);
+  r[6] = p_to - cp * (t_s - t) - 0.5 * a_p_td * (t_s * t_s - t * t) -
+         (a_p_to - a_p_td) * (t_s * t_s * t_s - t * t * t) / (6.0 * t_s);
+  memcpy(o, r, sizeof r);
+}
+
+/* planning_utils.cpp:519-556 */
+int orc_is_valid_action(const double *a) {
+  if ((a[6] <= 0) || (a[7] < 0)) return 0;
+  double m = M_CONST, g = G_CONST, mu = MU;
+  double f_x_td = m * a[0], f_y_td = m * a[1], f_z_td = m * (a[2] + g);
+  double f_x_to = m * a[3], f_y_to = m * a[4], f_z_to = m * (a[5] + g);
+  double a_p_td = a[8], a_p_to = a[9];
+  if ((sqrt(f_x_td * f_x_td + f_y_td * f_y_td + f_z_td * f_z_td) >= F_MAX) ||
+      (sqrt(f_x_to * f_x_to + f_y_to * f_y_to + f_z_to * f_z_to) >= F_MAX) || (f_z_td < 0) ||
+      (f_z_to < 0) || (a_p_td >= F_MAX) || (a_p_to >= F_MAX))
+    return 0;
+  if ((sqrt(f_x_td * f_x_td + f_y_td * f_y_td) >= mu * f_z_td) ||
+      (sqrt(f_x_to * f_x_to + f_y_to * f_y_to) >= mu * f_z_to))
+    return 0;
+  return 1;
+}
+
+/* does a lookup point sit within FRAGILE_EPS of a grid line (bracket could
+ * move under a last-ulp trig difference)? */
+static int near_grid_line(const double *d, int n, int i, double v) {
+  if (i < 0) return 0;
+  return fabs(v - d[i]) < FRAGILE_EPS || (i + 1 < n && fabs(d[i + 1] - v) < FRAGILE_EPS);
+}
+
+static double cell_height(const orc_terrain *T, int ix, int iy, double x, double y) {
+  return bilinear(T->z, T->ny, ix, iy, T->x[ix], T->x[ix + 1], T->y[iy], T->y[iy + 1], x, y);
+}
+
+/* getGroundHeight inside isValidState: 0 = UB (no bracket, finite coords),
+ * 1 = value in *h (NaN for NaN coordinates) */
+static int height_at(const orc_terrain *T, double x, double y, double *h, orc_stats *st) {
+  if (isnan(x) || isnan(y)) { *h = NAN; return 1; }
+  int ix = bracket(T->x, T->nx, x), iy = bracket(T->y, T->ny, y);
+  if (ix < 0 || iy < 0) return 0;
+  if (near_grid_line(T->x, T->nx, ix, x) || near_grid_line(T->y, T->ny, iy, y))
+    st->flags |= GBP_F_FRAGILE;
+  *h = cell_height(T, ix, iy, x, y);
+  return 1;
+}
+
+/* heightIsNan inside isValidState: -1 = UB, else the reference's bool */
+static int nan_at(const orc_terrain *T, double x, double y) {
+  int ix = bracket(T->x, T->nx, x), iy = bracket(T->y, T->ny, y);
+  if (ix == BR_HIGH || iy == BR_HIGH) return -1;
+  return cell_has_nan(T, ix < 0 ? 0 : ix, iy < 0 ? 0 : iy);
+}
+
+/* planning_utils.cpp:562-635.  Out-of-domain convention: where
+ * the reference's result depends on an undefined read (a lookup point with
+ * no bracket and finite coordinates), the state is invalid and GBP_F_OOD is
+ * set when that UB could change the decision.  Every well-defined case
+ * (NaN coordinates, points below the first coordinate in heightIsNan) is
+ * restated exactly. */
+int orc_is_valid_state(const orc_terrain *T, const double *s, int phase, orc_stats *st) {
+  if (st->V >= GBP_MAX_SAMPLES) { st->flags |= GBP_F_LIMIT; return 0; } /* engine guard */
+  st->V++;
+  const double x0 = T->x[0], xN = T->x[T->nx - 1], y0 = T->y[0], yN = T->y[T->ny - 1];
+  /* (1) heightIsNan(centre) :564 */
+  int r = nan_at(T, s[0], s[1]);
+  if (r < 0) {
+    /* x or y >= the last coordinate: rejected by (2) unless exactly equal */
+    int in_closed = !(s[0] < x0 || s[0] > xN || s[1] < y0 || s[1] > yN);
+    if (in_closed) st->flags |= GBP_F_OOD;
+    return 0;
+  }
+  if (r) { st->flags |= GBP_F_NAN; return 0; }
+  /* (2) bounds + pitch :568-571 (abs() resolves to the double overload) */
+  if ((s[0] < x0) || (s[0] > xN) || (s[1] < y0) || (s[1] > yN) || (fabs(s[6]) >= P_MAX)) return 0;
+  /* (3) horizontal speed :574 */
+  if (sqrt(s[3] * s[3] + s[4] * s[4]) > V_MAX) return 0;
+  /* (4) rotation :578-594 */
+  double yaw = atan2(s[4], s[3]);
+  double cy = cos(yaw), sy = sin(yaw);
+  double pitch = s[6];
+  double cp = cos(pitch), sp = sin(pitch);
+  double R_11 = cy * cp, R_12 = -sy, R_13 = cy * sp;
+  double R_21 = sy * cp, R_22 = cy, R_23 = sy * sp;
+  double R_31 = -sp, R_32 = 0, R_33 = cp;
+  const double test_x[2] = {-0.5 * ROBOT_L, 0.5 * ROBOT_L};
+  const double test_y[2] = {-0.5 * ROBOT_W, 0.5 * ROBOT_W};
+  double z_body = -ROBOT_H;
+  /* (5) four corners :601-627 */
+  for (int bx = 0; bx < 2; bx++) {
+    for (int by = 0; by < 2; by++) {
+      double x_body = test_x[bx], y_body = test_y[by];
+      double x_leg = s[0] + R_11 * x_body + R_12 * y_body;
+      double y_leg = s[1] + R_21 * x_body + R_22 * y_body;
+      double z_leg = s[2] + R_31 * x_body + R_32 * y_body;
+      double x_corner = x_leg + R_13 * z_body;
+      double y_corner = y_leg + R_23 * z_body;
+      double z_corner = z_leg + R_33 * z_body;
+      /* heightIsNan(leg) :614 */
+      int rl = nan_at(T, x_leg, y_leg);
+      if (rl < 0) { st->flags |= GBP_F_OOD; return 0; }
+      if (rl) { st->flags |= GBP_F_NAN; return 0; }
+      /* both heights before the test :618-619 */
+      st->G += 2;
+      double gl, gc;
+      if (!height_at(T, x_leg, y_leg, &gl, st)) { st->flags |= GBP_F_OOD; return 0; }
+      if (!height_at(T, x_corner, y_corner, &gc, st)) { st->flags |= GBP_F_OOD; return 0; }
+      double leg_height = z_leg - gl;
+      double corner_height = z_corner - gc;
+      if (fabs(corner_height - H_MIN) < FRAGILE_EPS ||
+          (phase == GBP_STANCE && fabs(leg_height - H_MAX) < FRAGILE_EPS))
+        st->flags |= GBP_F_FRAGILE;
+      /* :624 */
+      if ((corner_height < H_MIN) || ((phase == GBP_STANCE) && (leg_height > H_MAX))) return 0;
+    }
+  }
+  /* (6) underside centre :630-632 */
+  st->G++;
+  double gu;
+  if (!height_at(T, s[0] + R_13 * z_body, s[1] + R_23 * z_body, &gu, st)) {
+    st->flags |= GBP_F_OOD;
+    return 0;
+  }
+  double height = (s[2] + R_33 * z_body) - gu;
+  if (fabs(height - H_MIN) < FRAGILE_EPS) st->flags |= GBP_F_FRAGILE;
+  if (height < H_MIN) return 0;
+  return 1;
+}
+
+#define STAGE(f, k) ((f) = ((f) & ~GBP_F_STAGE_MASK) | ((uint32_t)(k) << GBP_F_STAGE_SHIFT))
+
+/* planning_utils.cpp:713-753 */
+static int pair_fwd(const orc_terrain *T, const double *s, const double *a, double *s_new,
+                    double *t_new, orc_stats *st, uint32_t *f) {
+  double t_s = a[6], t_f = a[7], sc[8];
+  STAGE(*f, GBP_STAGE_FWD_STANCE);
+  for (double t = 0; t <= t_s; t += KINEMATICS_RES) {
+    orc_apply_stance(s, a, t, sc);
+    if (orc_is_valid_state(T, sc, GBP_STANCE, st) == 0) {
+      if (st->flags & GBP_F_LIMIT) return 0;
+      orc_apply_stance(s, a, (1.0 - BACKUP_RATIO) * t, s_new);
+      *f |= GBP_F_SNEW_SET;
+      return 0;
+    }
+    memcpy(s_new, sc, sizeof sc);
+    *t_new = t;
+    *f |= GBP_F_SNEW_SET | GBP_F_TNEW_SET;
+  }
+  double s_takeoff[8];
+  orc_apply_stance(s, a, a[6], s_takeoff);
+  STAGE(*f, GBP_STAGE_FWD_FLIGHT);
+  for (double t = 0; t < t_f; t += KINEMATICS_RES) {
+    orc_apply_flight(s_takeoff, t, sc);
+    if (orc_is_valid_state(T, sc, GBP_FLIGHT, st) == 0) return 0;
+  }
+  STAGE(*f, GBP_STAGE_FWD_LAND);
+  double s_land[8];
+  orc_apply_flight(s_takeoff, t_f, s_land);
+  if (orc_is_valid_state(T, s_land, GBP_STANCE, st) == 0) return 0;
+  memcpy(s_new, s_land, sizeof s_land);
+  *t_new = t_s + t_f;
+  *f |= GBP_F_SNEW_SET | GBP_F_TNEW_SET;
+  return 1;
+}
+
+/* planning_utils.cpp:651-712 */
+static int pair_fwd_adaptive(const orc_terrain *T, const double *s, const double *a,
+                             double *s_new, double *t_new, orc_stats *st, uint32_t *f) {
+  double t_s = a[6], t_f = a[7], sc[8];
+  double time_step = KINEMATICS_RES, t_pre_success = 0;
+  STAGE(*f, GBP_STAGE_FWD_STANCE);
+  for (double t = 0; t <= t_s; t += time_step) {
+    orc_apply_stance(s, a, t, sc);
+    if (orc_is_valid_state(T, sc, GBP_STANCE, st) == 0) {
+      if (st->flags & GBP_F_LIMIT) return 0;
+      if (KINEMATICS_RES - 0.01 <= time_step && time_step <= KINEMATICS_RES + 0.01) {
+        orc_apply_stance(s, a, (1.0 - BACKUP_RATIO) * t, s_new);
+        *f |= GBP_F_SNEW_SET;
+        return 0;
+      } else {
+        time_step = KINEMATICS_RES;
+        t = t_pre_success;
+      }
+    } else {
+      memcpy(s_new, sc, sizeof sc);
+      *t_new = t;
+      *f |= GBP_F_SNEW_SET | GBP_F_TNEW_SET;
+      time_step += KINEMATICS_RES;
+      t_pre_success = t;
+    }
+  }
+  double s_takeoff[8];
+  orc_apply_stance(s, a, a[6], s_takeoff);
+  time_step = KINEMATICS_RES;
+  t_pre_success = 0;
+  STAGE(*f, GBP_STAGE_FWD_FLIGHT);
+  for (double t = 0; t < t_f; t += time_step) {
+    orc_apply_flight(s_takeoff, t, sc);
+    if (orc_is_valid_state(T, sc, GBP_FLIGHT, st) == 0) return 0;
+    time_step += KINEMATICS_RES;
+    t_pre_success = t;
+  }
+  (void)t_pre_success;
+  STAGE(*f, GBP_STAGE_FWD_LAND);
+  double s_land[8];
+  orc_apply_flight(s_takeoff, t_f, s_land);
+  if (orc_is_valid_state(T, s_land, GBP_STANCE, st) == 0) return 0;
+  memcpy(s_new, s_land, sizeof s_land);
+  *t_new = t_s + t_f;
+  *f |= GBP_F_SNEW_SET | GBP_F_TNEW_SET;
+  return 1;
+}
+
+/* planning_utils.cpp:837-876 */
+static int pair_rev(const orc_terrain *T, const double *s, const double *a, double *s_new,
+                    double *t_new, orc_stats *st, uint32_t *f) {
+  double t_s = a[6], t_f = a[7], sc[8];
+  STAGE(*f, GBP_STAGE_REV_FLIGHT);
+  for (double t = 0; t < t_f; t += KINEMATICS_RES) {
+    orc_apply_flight(s, -t, sc);
+    if (orc_is_valid_state(T, sc, GBP_FLIGHT, st) == 0) return 0;
+  }
+  double s_takeoff[8];
+  orc_apply_flight(s, -t_f, s_takeoff);
+  STAGE(*f, GBP_STAGE_REV_STANCE);
+  for (double t = t_s; t >= 0; t -= KINEMATICS_RES) {
+    orc_apply_stance_reverse(s_takeoff, a, t, sc);
+    if (orc_is_valid_state(T, sc, GBP_STANCE, st) == 0) {
+      if (st->flags & GBP_F_LIMIT) return 0;
+      /* a FORWARD stance applied to the end state, as written (:857) */
+      orc_apply_stance(s, a, t + BACKUP_RATIO * (t_s - t), s_new);
+      *f |= GBP_F_SNEW_SET;
+      return 0;
+    }
+    memcpy(s_new, sc, sizeof sc);
+    *t_new = t_s - t;
+    *f |= GBP_F_SNEW_SET | GBP_F_TNEW_SET;
+  }
+  STAGE(*f, GBP_STAGE_REV_START);
+  double s_start[8];
+  orc_apply_stance_reverse(s_takeoff, a, 0, s_start);
+  if (orc_is_valid_state(T, s_start, GBP_STANCE, st) == 0) return 0;
+  memcpy(s_new, s_start, sizeof s_start);
+  *t_new = t_s;
+  *f |= GBP_F_SNEW_SET | GBP_F_TNEW_SET;
+  return 1;
+}
+
+/* planning_utils.cpp:774-836 */
+static int pair_rev_adaptive(const orc_terrain *T, const double *s, const double *a,
+                             double *s_new, double *t_new, orc_stats *st, uint32_t *f) {
+  double t_s = a[6], t_f = a[7], sc[8];
+  double time_step = KINEMATICS_RES, t_pre_success = 0;
+  STAGE(*f, GBP_STAGE_REV_FLIGHT);
+  for (double t = 0; t < t_f; t += time_step) {
+    orc_apply_flight(s, -t, sc);
+    if (orc_is_valid_state(T, sc, GBP_FLIGHT, st) == 0) return 0;
+    time_step += KINEMATICS_RES;
+    t_pre_success = t;
+  }
+  double s_takeoff[8];
+  orc_apply_flight(s, -t_f, s_takeoff);
+  time_step = KINEMATICS_RES;
+  t_pre_success = 0;
+  STAGE(*f, GBP_STAGE_REV_STANCE);
+  for (double t = t_s; t >= 0; t -= time_step) {
+    orc_apply_stance_reverse(s_takeoff, a, t, sc);
+    if (orc_is_valid_state(T, sc, GBP_STANCE, st) == 0) {
+      if (st->flags & GBP_F_LIMIT) return 0;
+      if (KINEMATICS_RES - 0.01 <= time_step && time_step <= KINEMATICS_RES + 0.01) {
+        orc_apply_stance(s, a, t + BACKUP_RATIO * (t_s - t), s_new);
+        *f |= GBP_F_SNEW_SET;
+        return 0;
+      } else {
+        time_step = KINEMATICS_RES;
+        t = t_pre_success;
+      }
+    } else {
+      memcpy(s_new, sc, sizeof sc);
+      *t_new = t_s - t;
+      *f |= GBP_F_SNEW_SET | GBP_F_TNEW_SET;
+      time_step += KINEMATICS_RES;
+      t_pre_success = t;
+    }
+  }
+  STAGE(*f, GBP_STAGE_REV_START);
+  double s_start[8];
+  orc_apply_stance_reverse(s_takeoff, a, 0, s_start);
+  if (orc_is_valid_state(T, s_start, GBP_STANCE, st) == 0) return 0;
+  memcpy(s_new, s_start, sizeof s_start);
+  *t_new = t_s;
+  *f |= GBP_F_SNEW_SET | GBP_F_TNEW_SET;
+  return 1;
+}
+
+int orc_is_valid_pair(const orc_terrain *T, const double *s, const double *a, int direction,
+                      int adaptive, double *s_new, double *t_new, uint32_t *flags,
+                      uint32_t *counts) {
+  orc_stats st = {0, 0, 0};
+  uint32_t f = 0;
+  int v;
+  if (direction == GBP_FORWARD)
+    v = adaptive ? pair_fwd_adaptive(T, s, a, s_new, t_new, &st, &f)
+                 : pair_fwd(T, s, a, s_new, t_new, &st, &f);
+  else
+    v = adaptive ? pair_rev_adaptive(T, s, a, s_new, t_new, &st, &f)
+                 : pair_rev(T, s, a, s_new, t_new, &st, &f);
+  f |= st.flags | (v ? GBP_F_VALID : 0u);
+  if (flags) *flags = f;
+  if (counts) *counts = (st.G & 0xFFFFu) | (st.V << 16);
+  return v;
+}
+
+/* ---- distances: planning_utils.cpp:106-132, planning_utils.h:133-145 ---- */
+double orc_pose_distance(const double *q1, const double *q2) {
+  double sum = 0;
+  for (int i = 0; i < 3; i++) sum = sum + (q2[i] - q1[i]) * (q2[i] - q1[i]);
+  return sqrt(sum);
+}
+
+double orc_state_distance(const double *q1, const double *q2) {
+  double sum = 0;
+  for (int i = 0; i < 8; i++) sum = sum + 1.0 * (q2[i] - q1[i]) * (q2[i] - q1[i]);
+  return sqrt(sum);
+}
+
+double orc_state_yaw_distance(const double *q1, const double *q2) {
+  double yaw1 = atan2(q1[4], q1[3]);
+  double yaw2 = atan2(q2[4], q2[3]);
+  double yaw_min = std_min(yaw1, yaw2);
+  double yaw_max = std_max(yaw1, yaw2);
+  return std_min(yaw_max - yaw_min, yaw_min + 2 * MY_PI - yaw_max);
+}
+
+/* planner_class.cpp:185-200 */
+int orc_nearest(const double *verts, int n_vert, const double *q, double *dist) {
+  int nearest = 0;
+  double best = INFINITY;
+  for (int v = 0; v < n_vert; v++) {
+    double c = orc_state_distance(q, verts + (long)v * 8);
+    if (c < best) { best = c; nearest = v; }
+  }
+  if (dist) *dist = best;
+  return nearest;
+}
+
+/* rrt.cpp:20-70 + :84-101 */
+int orc_extend(const orc_terrain *T, const double *s_near, const double *target,
+               const double *actions, int direction, int adaptive, double *s_new,
+               double *a_new, int *chosen, uint32_t *counts) {
+  double best_so_far = orc_state_distance(s_near, target);
+  uint32_t G = 0, V = 0;
+  double s_test[8];
+  double t_new;
+  int found = -1;
+  for (int j = 0; j < NUM_GEN_STATES; ++j) {
+    uint32_t f, c;
+    int v = orc_is_valid_pair(T, s_near, actions + 10 * j, direction, adaptive, s_test, &t_new,
+                              &f, &c);
+    G += GBP_COUNT_G(c);
+    V += GBP_COUNT_V(c);
+    if (v) { found = j; break; }
+  }
+  if (counts) *counts = (G & 0xFFFFu) | (V << 16);
+  if (chosen) *chosen = found;
+  if (found >= 0) {
+    double current_dist = orc_state_distance(s_test, target);
+    if (current_dist < best_so_far) {
+      best_so_far = current_dist;
+      memcpy(s_new, s_test, sizeof s_test);
+      memcpy(a_new, actions + 10 * found, 10 * sizeof(double));
+    }
+  }
+  if (best_so_far == orc_state_distance(s_near, target)) return GBP_TRAPPED;
+  return (orc_state_distance(s_new, target) <= GOAL_BOUNDS) ? GBP_REACHED : GBP_ADVANCED;
+}
+
+/* rrt_connect.cpp:20-84 (recursive attemptConnect) */
+static int attempt_connect_ts(const orc_terrain *T, const double *s_existing, const double *s,
+                              double t_s, double *s_new, double *a_new, int direction,
+                              int adaptive, int depth) {
+  if (t_s <= KINEMATICS_RES) return GBP_TRAPPED;
+  if (depth > 64) return GBP_TRAPPED; /* guard; the reference recursion is unbounded */
+  const double *s_start = (direction == GBP_FORWARD) ? s_existing : s;
+  const double *s_goal = (direction == GBP_FORWARD) ? s : s_existing;
+  double t_new = NAN; /* reference: uninitialised */
+  double t_f = 0;
+  double x_td = s_start[0], y_td = s_start[1], z_td = s_start[2];
+  double dx_td = s_start[3], dy_td = s_start[4], dz_td = s_start[5];
+  double x_to = s_goal[0], y_to = s_goal[1], z_to = s_goal[2];
+  double dx_to = s_goal[3], dy_to = s_goal[4], dz_to = s_goal[5];
+  double p_td = s_start[6], dp_td = s_start[7], p_to = s_goal[6], dp_to = s_goal[7];
+  double a[10];
+  a[0] = -(2.0 * (3.0 * x_td - 3.0 * x_to + 2.0 * dx_td * t_s + dx_to * t_s)) / (t_s * t_s);
+  a[1] = -(2.0 * (3.0 * y_td - 3.0 * y_to + 2.0 * dy_td * t_s + dy_to * t_s)) / (t_s * t_s);
+  a[2] = -(2.0 * (3.0 * z_td - 3.0 * z_to + 2.0 * dz_td * t_s + dz_to * t_s)) / (t_s * t_s);
+  a[3] = (2.0 * (3.0 * x_td - 3.0 * x_to + dx_td * t_s + 2.0 * dx_to * t_s)) / (t_s * t_s);
+  a[4] = (2.0 * (3.0 * y_td - 3.0 * y_to + dy_td * t_s + 2.0 * dy_to * t_s)) / (t_s * t_s);
+  a[5] = (2.0 * (3.0 * z_td - 3.0 * z_to + dz_td * t_s + 2.0 * dz_to * t_s)) / (t_s * t_s);
+  a[6] = t_s;
+  a[7] = t_f;
+  a[8] = -(2.0 * (3.0 * p_td - 3.0 * p_to + 2.0 * dp_td * t_s + dp_to * t_s)) / (t_s * t_s);
+  a[9] = (2.0 * (3.0 * p_td - 3.0 * p_to + dp_td * t_s + 2.0 * dp_to * t_s)) / (t_s * t_s);
+  memcpy(a_new, a, sizeof a);
+  if (orc_is_valid_action(a_new)) {
+    uint32_t f;
+    int ok = (direction == GBP_FORWARD)
+                 ? orc_is_valid_pair(T, s_start, a_new, GBP_FORWARD, adaptive, s_new, &t_new, &f, 0)
+                 : orc_is_valid_pair(T, s_goal, a_new, GBP_REVERSE, adaptive, s_new, &t_new, &f, 0);
+    if (ok) return GBP_REACHED;
+    /* The reference recurses with t_new / s_new even when the failed check
+     * never assigned them (uninitialised locals: UB).
+     * Convention shared with the engine: that case is TRAPPED. */
+    if (!(f & GBP_F_TNEW_SET) || !(f & GBP_F_SNEW_SET)) return GBP_TRAPPED;
+    double s_mid[8];
+    memcpy(s_mid, s_new, sizeof s_mid);
+    if (attempt_connect_ts(T, s_existing, s_mid, t_new, s_new, a_new, direction, adaptive,
+                           depth + 1) == GBP_TRAPPED)
+      return GBP_TRAPPED;
+    return GBP_ADVANCED;
+  }
+  return GBP_TRAPPED;
+}
+
+int orc_attempt_connect(const orc_terrain *T, const double *s_existing, const double *s,
+                        double t_s, double *s_new, double *a_new, int direction, int adaptive) {
+  if (!(t_s > 0)) t_s = orc_pose_distance(s, s_existing) / V_NOM; /* rrt_connect.cpp:89 */
+  return attempt_connect_ts(T, s_existing, s, t_s, s_new, a_new, direction, adaptive, 0);
+}
+
+/* ---- batch helpers ------------------------------------------------------ */
+#ifdef _OPENMP
+#define OMP_FOR _Pragma("omp parallel for schedule(dynamic, 256) num_threads(nthreads)")
+#else
+#define OMP_FOR
+#endif
+
+void orc_validate_pairs(const orc_terrain *T, int64_t n, const double *s, const double *a,
+                        const uint8_t *direction, int direction_all, int adaptive,
+                        uint8_t *valid, double *s_new, double *t_new, uint32_t *flags,
+                        uint32_t *counts, int nthreads) {
+  if (nthreads <= 0) nthreads = 1;
+  OMP_FOR
+  for (int64_t i = 0; i < n; i++) {
+    double sn[8], tn;
+    uint32_t f, c;
+    int dir = direction ? direction[i] : direction_all;
+    int v = orc_is_valid_pair(T, s + 8 * i, a + 10 * i, dir, adaptive, sn, &tn, &f, &c);
+    if (valid) valid[i] = (uint8_t)v;
+    if (s_new && (f & GBP_F_SNEW_SET)) memcpy(s_new + 8 * i, sn, sizeof sn);
+    if (t_new && (f & GBP_F_TNEW_SET)) t_new[i] = tn;
+    if (flags) flags[i] = f;
+    if (counts) counts[i] = c;
+  }
+}
+
+void orc_valid_states(const orc_terrain *T, int64_t n, const double *states,
+                      const uint8_t *phase, int phase_all, uint8_t *valid, uint32_t *flags,
+                      uint32_t *counts, int nthreads) {
+  if (nthreads <= 0) nthreads = 1;
+  OMP_FOR
+  for (int64_t i = 0; i < n; i++) {
+    orc_stats st = {0, 0, 0};
+    int v = orc_is_valid_state(T, states + 8 * i, phase ? phase[i] : phase_all, &st);
+    if (valid) valid[i] = (uint8_t)v;
+    if (flags) flags[i] = st.flags | (v ? GBP_F_VALID : 0u);
+    if (counts) counts[i] = (st.G & 0xFFFFu) | (st.V << 16);
+  }
+}
+
+void orc_height_batch(const orc_terrain *T, int64_t n, const double *xy, double *h,
+                      uint8_t *is_nan, uint8_t *ood, int nthreads) {
+  if (nthreads <= 0) nthreads = 1;
+  OMP_FOR
+  for (int64_t i = 0; i < n; i++) {
+    int o1 = 0, o2 = 0;
+    double v = orc_ground_height(T, xy[2 * i], xy[2 * i + 1], &o1);
+    int nn = orc_height_is_nan(T, xy[2 * i], xy[2 * i + 1], &o2);
+    if (h) h[i] = v;
+    if (is_nan) is_nan[i] = (uint8_t)nn;
+    if (ood) ood[i] = (uint8_t)(o1 | o2);
+  }
+}
+
+void orc_normal_batch(const orc_terrain *T, int64_t n, const double *xy, double *nrm,
+                      uint8_t *ood, int nthreads) {
+  if (nthreads <= 0) nthreads = 1;
+  OMP_FOR
+  for (int64_t i = 0; i < n; i++) {
+    int o = 0;
+    orc_surface_normal(T, xy[2 * i], xy[2 * i + 1], nrm + 3 * i, &o);
+    if (ood) ood[i] = (uint8_t)o;
+  }
+}
+
+void orc_extend_batch(const orc_terrain *T, int64_t n, const double *s_near,
+                      const double *target, const double *actions, const uint8_t *direction,
+                      int direction_all, int adaptive, int32_t *result, int32_t *chosen,
+                      double *s_new, double *a_new, uint32_t *counts, int nthreads) {
+  if (nthreads <= 0) nthreads = 1;
+  OMP_FOR
+  for (int64_t i = 0; i < n; i++) {
+    double sn[8], an[10];
+    int ch;
+    uint32_t c;
+    int dir = direction ? direction[i] : direction_all;
+    int r = orc_extend(T, s_near + 8 * i, target + 8 * i, actions + 60 * i, dir, adaptive, sn,
+                       an, &ch, &c);
+    if (result) result[i] = r;
+    if (chosen) chosen[i] = ch;
+    if (r != GBP_TRAPPED) {
+      if (s_new) memcpy(s_new + 8 * i, sn, sizeof sn);
+      if (a_new) memcpy(a_new + 10 * i, an, sizeof an);
+    }
+    if (counts) counts[i] = c;
+  }
+}
+
+void orc_nearest_batch(int64_t n_q, const double *q, int n_vert, const double *verts,
+                       int32_t *idx, double *dist, int nthreads) {
+  if (nthreads <= 0) nthreads = 1;
+  OMP_FOR
+  for (int64_t i = 0; i < n_q; i++) {
+    double d;
+    int k = orc_nearest(verts, n_vert, q + 8 * i, &d);
+    if (idx) idx[i] = k;
+    if (dist) dist[i] = d;
+  }
+}
+
+/* ---- Philox4x32-10 (Salmon et al., SC'11) ------------------------------- */
+static inline void mulhilo32(uint32_t a, uint32_t b, uint32_t *hi, uint32_t *lo) {
+  uint64_t p = (uint64_t)a * b;
+  *hi = (uint32_t)(p >> 32);
+  *lo = (uint32_t)p;
+}
+
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+  uint32_t k0 = key[0], k1 = key[1];
+  for (int r = 0; r < 10; r++) {
+    uint32_t hi0, lo0, hi1, lo1;
+    mulhilo32(0xD2511F53u, c0, &hi0, &lo0);
+    mulhilo32(0xCD9E8D57u, c2, &hi1, &lo1);
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+void orc_uniform2(uint64_t seed, uint64_t stream_id, uint32_t purpose, int64_t index,
+                  uint32_t draw, double u[2]) {
+  uint32_t ctr[4] = {draw, (uint32_t)(uint64_t)index, (uint32_t)((uint64_t)index >> 32),
+                     (uint32_t)stream_id ^ (purpose << 24)};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(stream_id >> 32)};
+  uint32_t o[4];
+  orc_philox4x32_10(ctr, key, o);
+  uint64_t w0 = ((uint64_t)o[1] << 32) | o[0];
+  uint64_t w1 = ((uint64_t)o[3] << 32) | o[2];
+  u[0] = (double)(w0 >> 11) * 0x1p-53;
+  u[1] = (double)(w1 >> 11) * 0x1p-53;
+}
+
+/* Box-Muller pair (the reference's libstdc++ polar method yields a pair too:
+ * a[9] is its cached second value) */
+static void box_muller(double u1, double u2, double *z0, double *z1) {
+  double r = sqrt(-2.0 * log(1.0 - u1));
+  double th = 6.283185307179586 * u2;
+  *z0 = r * cos(th);
+  *z1 = r * sin(th);
+}
+
+/* planner_class.cpp:38-76 */
+int orc_sample_state(const orc_terrain *T, uint64_t seed, uint64_t stream_id, int64_t index,
+                     int require_phase, int max_tries, double *q) {
+  double x_min = T->x[0], x_max = T->x[T->nx - 1];
+  double y_min = T->y[0], y_max = T->y[T->ny - 1];
+  double z_min_rel = H_MIN + ROBOT_H, z_max_rel = H_MAX + ROBOT_H;
+  double mean = 0.5 * (z_max_rel + z_min_rel);
+  double sd = (z_max_rel - z_min_rel) * (1.0 / (2 * 3.0));
+  if (max_tries <= 0) max_tries = 1;
+  for (int k = 0; k < max_tries; k++) {
+    double u0[2], u1[2], u2[2], u3[2];
+    orc_uniform2(seed, stream_id, PURPOSE_STATE, index, 4u * k + 0, u0);
+    orc_uniform2(seed, stream_id, PURPOSE_STATE, index, 4u * k + 1, u1);
+    orc_uniform2(seed, stream_id, PURPOSE_STATE, index, 4u * k + 2, u2);
+    orc_uniform2(seed, stream_id, PURPOSE_STATE, index, 4u * k + 3, u3);
+    double z0, z1;
+    box_muller(u1[0], u1[1], &z0, &z1);
+    double hz = z0 * sd + mean;
+    q[0] = (x_max - x_min) * u0[0] + x_min;
+    q[1] = (y_max - y_min) * u0[1] + y_min;
+    q[2] = std_max(std_min(hz, z_max_rel), z_min_rel) + orc_ground_height(T, q[0], q[1], 0);
+    double phi = (2.0 * MY_PI) * u2[0];
+    double cos_theta = 2.0 * u2[1] - 1.0;
+    double theta = acos(cos_theta);
+    double v = u3[0] * V_MAX;
+    q[3] = v * sin(theta) * cos(phi);
+    q[4] = v * sin(theta) * sin(phi);
+    q[5] = v * cos(theta);
+    q[6] = 2 * P_MAX * u3[1] - P_MAX;
+    q[7] = 0.0;
+    if (require_phase < 0) return k + 1;
+    orc_stats st = {0, 0, 0};
+    if (orc_is_valid_state(T, q, require_phase, &st)) return k + 1;
+  }
+  return -1;
+}
+
+/* planning_utils.cpp:198-231 */
+void orc_rotate_grf(const double *n, const double *f, double *out) {
+  double v0 = n[1] * 1.0 - n[2] * 0.0;
+  double v1 = n[2] * 0.0 - n[0] * 1.0;
+  double v2 = n[0] * 0.0 - n[1] * 0.0;
+  double s = sqrt(v0 * v0 + v1 * v1 + v2 * v2);
+  double c = n[0] * 0.0 + n[1] * 0.0 + n[2] * 1.0;
+  if (s < 0.000001) {
+    out[0] = f[0]; out[1] = f[1]; out[2] = f[2];
+    return;
+  }
+  double K[3][3] = {{0, -v2, v1}, {v2, 0, -v0}, {-v1, v0, 0}};
+  double R[3][3];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) {
+      double kk = K[i][0] * K[0][j] + K[i][1] * K[1][j] + K[i][2] * K[2][j];
+      R[i][j] = (i == j ? 1.0 : 0.0) + K[i][j] + kk * (1 - c) / (s * s);
+    }
+  for (int i = 0; i < 3; i++) out[i] = R[i][0] * f[0] + R[i][1] * f[1] + R[i][2] * f[2];
+}
+
+/* planning_utils.cpp:392-442 */
+void orc_sample_action(const double *nrm, uint64_t seed, uint64_t stream_id, int64_t index,
+                       double *a) {
+  double u[5][2];
+  for (uint32_t d = 0; d < 5; d++) orc_uniform2(seed, stream_id, PURPOSE_ACTION, index, d, u[d]);
+  double f_z_td = F_MAX * u[0][0];
+  double f_z_to = F_MAX * u[0][1];
+  double f_x_td = 2 * MU * f_z_td * u[1][0] - MU * f_z_td;
+  double f_x_to = 2 * MU * f_z_to * u[1][1] - MU * f_z_to;
+  double f_y_td = 2 * MU * f_z_td * u[2][0] - MU * f_z_td;
+  double f_y_to = 2 * MU * f_z_to * u[2][1] - MU * f_z_to;
+  double f_td[3] = {f_x_td, f_y_td, f_z_td}, f_to[3] = {f_x_to, f_y_to, f_z_to};
+  double r_td[3], r_to[3];
+  orc_rotate_grf(nrm, f_td, r_td);
+  orc_rotate_grf(nrm, f_to, r_to);
+  double t_s = 0.3;
+  double t_f = (T_F_MAX - T_F_MIN) * u[3][0] + T_F_MIN;
+  a[0] = r_td[0] / M_CONST;
+  a[1] = r_td[1] / M_CONST;
+  a[2] = r_td[2] / M_CONST - G_CONST;
+  a[3] = r_to[0] / M_CONST;
+  a[4] = r_to[1] / M_CONST;
+  a[5] = r_to[2] / M_CONST - G_CONST;
+  a[6] = t_s;
+  a[7] = t_f;
+  double z0, z1;
+  box_muller(u[4][0], u[4][1], &z0, &z1);
+  double n0 = z0 * (ANG_ACC_MAX / 4.0) + 0.0, n1 = z1 * (ANG_ACC_MAX / 4.0) + 0.0;
+  a[8] = std_max(std_min(n0, ANG_ACC_MAX), -ANG_ACC_MAX);
+  a[9] = std_max(std_min(n1, ANG_ACC_MAX), -ANG_ACC_MAX);
+}
+
+void orc_sample_states(const orc_terrain *T, int64_t n, uint64_t seed, uint64_t stream_id,
+                       int64_t index_base, int require_phase, int max_tries, double *states,
+                       int32_t *tries, int nthreads) {
+  if (nthreads <= 0) nthreads = 1;
+  OMP_FOR
+  for (int64_t i = 0; i < n; i++) {
+    int k = orc_sample_state(T, seed, stream_id, index_base + i, require_phase, max_tries,
+                             states + 8 * i);
+    if (tries) tries[i] = k;
+  }
+}
+
+void orc_sample_actions(int64_t n, const double *normals, uint64_t seed, uint64_t stream_id,
+                        int64_t index_base, double *actions, int nthreads) {
+  if (nthreads <= 0) nthreads = 1;
+  OMP_FOR
+  for (int64_t i = 0; i < n; i++)
+    orc_sample_action(normals + 3 * i, seed, stream_id, index_base + i, actions + 10 * i);
+}

@@ -1,0 +1,140 @@
+/*
+ * gbp_oracle.h — CPU restatement of the global_body_planner hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the checker the HIP engine is compared
+ * against; nothing in the product (global_body_planner_amd/, include/gbp.h's
+ * implementation) may link, import or call it.  Only tests/, the smoke() of
+ * __graft_entry__.py and bench.py's cpu_baseline leg use it.
+ *
+ * It restates, in plain C99 (FP64, no FMA contraction, glibc libm for
+ * atan2/sin/cos/sqrt exactly like the reference's host build), the reference
+ * functions cited on each declaration.  The bracket search is the reference's
+ * O(N) linear scan (fast_terrain_map.cpp:101-117) so the CPU baseline timed
+ * from it has the reference's cost model; orc_set_scan_mode(1) switches to a
+ * bisection that returns the identical bracket (used only to make big parity
+ * runs finish quickly).
+ *
+ * Parity status: the reference's own tests pin nothing (test/
+ * test_global_body_planner.cpp asserts 1+1==2) and the reference cannot be
+ * compiled here (its headers need ROS / grid_map / Eigen, absent from the
+ * image), so bit-level parity against reference *outputs* is UNPINNED; the
+ * restatement is pinned against the survey-recorded outputs of the compiled
+ * reference in tests/test_oracle_pins.py.  See DESIGN.md.
+ */
+#ifndef GBP_ORACLE_H
+#define GBP_ORACLE_H
+
+#include <stdint.h>
+#include "../include/gbp.h" /* flag / enum values only (the ABI contract) */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  int nx, ny;
+  const double *x, *y;          /* ascending coordinates               */
+  const double *z;              /* x-major [nx][ny]: z[ix*ny+iy]       */
+  const double *dx, *dy, *dz;   /* x-major, may be NULL => (0,0,1)     */
+} orc_terrain;
+
+/* per-check accumulator */
+typedef struct {
+  uint32_t G;      /* executed getGroundHeight calls  */
+  uint32_t V;      /* executed isValidState calls     */
+  uint32_t flags;  /* GBP_F_OOD / GBP_F_NAN / GBP_F_FRAGILE */
+} orc_stats;
+
+void orc_set_scan_mode(int mode); /* 0 = linear scan (reference), 1 = bisection */
+int  orc_get_scan_mode(void);
+
+/* fast_terrain_map.cpp:94-132.  *ood = 1 if no bracket exists (reference UB). */
+double orc_ground_height(const orc_terrain *T, double x, double y, int *ood);
+/* fast_terrain_map.cpp:135-157 */
+int orc_height_is_nan(const orc_terrain *T, double x, double y, int *ood);
+/* fast_terrain_map.cpp:160-213 */
+void orc_surface_normal(const orc_terrain *T, double x, double y, double n[3], int *ood);
+
+/* planning_utils.cpp:237-277 */
+void orc_apply_stance(const double *s, const double *a, double t, double *out);
+/* planning_utils.cpp:282-306 */
+void orc_apply_flight(const double *s, double t_f, double *out);
+/* planning_utils.cpp:324-370 */
+void orc_apply_stance_reverse(const double *s, const double *a, double t, double *out);
+/* planning_utils.cpp:519-556 */
+int orc_is_valid_action(const double *a);
+/* planning_utils.cpp:562-635 */
+int orc_is_valid_state(const orc_terrain *T, const double *s, int phase, orc_stats *st);
+
+/* planning_utils.cpp:645-881 (direction FORWARD -> isValidStateActionPair,
+ * REVERSE -> isValidStateActionPairReverse; adaptive -> *AdaptiveStepSize).
+ * s_new / t_new are only written where the reference writes them; the return
+ * value is the reference's bool; *flags receives GBP_F_* bits. */
+int orc_is_valid_pair(const orc_terrain *T, const double *s, const double *a, int direction,
+                      int adaptive, double *s_new, double *t_new, uint32_t *flags,
+                      uint32_t *counts);
+
+/* planning_utils.cpp:106-132, planning_utils.h:133-145 */
+double orc_pose_distance(const double *q1, const double *q2);
+double orc_state_distance(const double *q1, const double *q2);
+double orc_state_yaw_distance(const double *q1, const double *q2);
+
+/* planner_class.cpp:185-200 (ties -> lowest index) */
+int orc_nearest(const double *verts, int n_vert, const double *q, double *dist);
+
+/* rrt.cpp:20-70 (newConfig) + rrt.cpp:84-101 (acceptance): candidate actions
+ * are given explicitly (actions[6][10]).  Returns TRAPPED/ADVANCED/REACHED;
+ * *chosen = index of the first valid candidate or -1. */
+int orc_extend(const orc_terrain *T, const double *s_near, const double *target,
+               const double *actions, int direction, int adaptive, double *s_new,
+               double *a_new, int *chosen, uint32_t *counts);
+
+/* rrt_connect.cpp:20-91 (attemptConnect, recursive).  Returns TRAPPED/ADVANCED/
+ * REACHED; t_s <= 0 means "compute from poseDistance / V_NOM" (:85-91). */
+int orc_attempt_connect(const orc_terrain *T, const double *s_existing, const double *s,
+                        double t_s, double *s_new, double *a_new, int direction,
+                        int adaptive);
+
+/* ---- batch helpers (OpenMP over independent items, nthreads <= 0 => 1) --- */
+void orc_validate_pairs(const orc_terrain *T, int64_t n, const double *s, const double *a,
+                        const uint8_t *direction, int direction_all, int adaptive,
+                        uint8_t *valid, double *s_new, double *t_new, uint32_t *flags,
+                        uint32_t *counts, int nthreads);
+void orc_valid_states(const orc_terrain *T, int64_t n, const double *states,
+                      const uint8_t *phase, int phase_all, uint8_t *valid, uint32_t *flags,
+                      uint32_t *counts, int nthreads);
+void orc_height_batch(const orc_terrain *T, int64_t n, const double *xy, double *h,
+                      uint8_t *is_nan, uint8_t *ood, int nthreads);
+void orc_normal_batch(const orc_terrain *T, int64_t n, const double *xy, double *nrm,
+                      uint8_t *ood, int nthreads);
+void orc_extend_batch(const orc_terrain *T, int64_t n, const double *s_near,
+                      const double *target, const double *actions /* n*6*10 */,
+                      const uint8_t *direction, int direction_all, int adaptive,
+                      int32_t *result, int32_t *chosen, double *s_new, double *a_new,
+                      uint32_t *counts, int nthreads);
+void orc_nearest_batch(int64_t n_q, const double *q, int n_vert, const double *verts,
+                       int32_t *idx, double *dist, int nthreads);
+
+/* ---- counter-based samplers (Philox4x32-10), same keys as the engine ---- */
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+/* uniform in [0,1): (hi:lo >> 11) * 2^-53 for each of the two 64-bit halves */
+void orc_uniform2(uint64_t seed, uint64_t stream_id, uint32_t purpose, int64_t index,
+                  uint32_t draw, double u[2]);
+/* planner_class.cpp:38-76; returns number of tries (k+1) or -1 */
+int orc_sample_state(const orc_terrain *T, uint64_t seed, uint64_t stream_id, int64_t index,
+                     int require_phase, int max_tries, double *state);
+/* planning_utils.cpp:392-442 */
+void orc_sample_action(const double *normal, uint64_t seed, uint64_t stream_id, int64_t index,
+                       double *action);
+/* planning_utils.cpp:198-231 */
+void orc_rotate_grf(const double *n, const double *f, double *out);
+void orc_sample_states(const orc_terrain *T, int64_t n, uint64_t seed, uint64_t stream_id,
+                       int64_t index_base, int require_phase, int max_tries, double *states,
+                       int32_t *tries, int nthreads);
+void orc_sample_actions(int64_t n, const double *normals, uint64_t seed, uint64_t stream_id,
+                        int64_t index_base, double *actions, int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,279 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU restatement.
+
+Bar: bit-exact for decisions, flags, lookup counts, s_new and t_new (all FP64
+arithmetic is restated in the reference's order without FMA); attempts whose
+trig-dependent margin is within 1e-12 (GBP_F_FRAGILE) are counted and
+excluded from the decision comparison.  Samplers use device log/sin/cos/acos
+and are compared with an explicit relative tolerance (1e-12).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from global_body_planner_amd import _lib as L
+from global_body_planner_amd import terrain_data as td
+from tests.helpers import assert_pairs_equal, attempts_oracle, bits, same_f64, u32
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+TERRAINS = ["synth-rough-256", "slope-gridmap", "rough_terrain-gridmap", "rough_terrain-direct"]
+_cache = {}
+
+
+def terrain_pair(name, **kw):
+    import global_body_planner_amd as gbp
+    key = (name, tuple(sorted(kw.items())))
+    if key not in _cache:
+        data = td.by_name(name)
+        _cache[key] = (data, gbp.Terrain.from_data(data, device=0, **kw),
+                       oracle.OracleTerrain.from_data(data))
+    return _cache[key]
+
+
+@pytest.fixture(autouse=True)
+def _bisect():
+    oracle.set_scan_mode(1)  # same brackets as the linear scan, faster
+    yield
+    oracle.set_scan_mode(0)
+
+
+def np_(t):
+    return t.cpu().numpy()
+
+
+# ---- K1 ----------------------------------------------------------------------
+@pytest.mark.parametrize("name", TERRAINS)
+def test_height_and_normal_parity(gpu, name):
+    data, T, O = terrain_pair(name)
+    rng = np.random.default_rng(1)
+    x0, xN, y0, yN = data.bounds
+    n = 20000
+    xy = np.stack([rng.uniform(x0 - 0.3, xN + 0.3, n), rng.uniform(y0 - 0.3, yN + 0.3, n)], 1)
+    # grid lines, +-1 ulp around them, and the exact upper edges (reference UB)
+    gx = data.x[rng.integers(0, data.x.size, 500)]
+    gy = data.y[rng.integers(0, data.y.size, 500)]
+    extra = [np.stack([gx, gy], 1), np.stack([np.nextafter(gx, -np.inf), gy], 1),
+             np.stack([np.nextafter(gx, np.inf), np.nextafter(gy, np.inf)], 1),
+             np.array([[xN, y0], [x0, yN], [xN, yN], [x0, y0]])]
+    xy = np.concatenate([xy] + extra)
+    h, nan, ood = T.height(torch.from_numpy(xy))
+    rh, rnan, rood = O.height_batch(xy, nthreads=8)
+    assert np.array_equal(np_(ood), rood)
+    assert np.array_equal(np_(nan), rnan)
+    assert np.array_equal(bits(np_(h)), bits(rh)) or np.array_equal(
+        np.isnan(np_(h)), np.isnan(rh)) and np.array_equal(bits(np_(h)[~np.isnan(rh)]),
+                                                           bits(rh[~np.isnan(rh)]))
+    nrm, nood = T.normal(torch.from_numpy(xy))
+    rn, rnood = O.normal_batch(xy, nthreads=8)
+    assert np.array_equal(np_(nood), rnood)
+    ok = rnood == 0
+    assert np.array_equal(bits(np_(nrm)[ok]), bits(rn[ok]))
+
+
+def test_height_nan_cells(gpu):
+    import global_body_planner_amd as gbp
+    data = td.synth_rough(64)
+    z = data.z.copy()
+    z[10:13, 20:22] = np.nan
+    z[40, 5] = np.nan
+    T = gbp.Terrain(data.x, data.y, z, data.dx, data.dy, data.dz, device=0)
+    O = oracle.OracleTerrain(data.x, data.y, z, data.dx, data.dy, data.dz)
+    rng = np.random.default_rng(2)
+    xy = np.stack([rng.uniform(0, data.x[-1], 20000), rng.uniform(0, data.y[-1], 20000)], 1)
+    h, nan, ood = T.height(torch.from_numpy(xy))
+    rh, rnan, rood = O.height_batch(xy)
+    assert rnan.sum() > 0
+    assert np.array_equal(np_(nan), rnan) and np.array_equal(np_(ood), rood)
+    assert np.array_equal(np.isnan(np_(h)), np.isnan(rh))
+    ok = ~np.isnan(rh)
+    assert np.array_equal(bits(np_(h)[ok]), bits(rh[ok]))
+    # validity on the NaN map
+    st, _ = O.sample_states(20000, 5, 9, 0, -1, 1, nthreads=8)
+    for phase in (L.STANCE, L.FLIGHT):
+        v, f, c = T.valid_states(torch.from_numpy(st), phase)
+        rv, rf, rc = O.valid_states(st, phase, nthreads=8)
+        assert np.array_equal(np_(v), rv)
+        assert np.array_equal(u32(f), rf)
+        assert np.array_equal(u32(c), rc)
+    assert ((rf & L.F_NAN) != 0).sum() > 0
+
+
+# ---- isValidState ------------------------------------------------------------
+@pytest.mark.parametrize("name", TERRAINS)
+def test_valid_states_parity(gpu, name):
+    data, T, O = terrain_pair(name)
+    st, _ = O.sample_states(30000, 11, 7, 0, -1, 1, nthreads=8)
+    for phase in (L.STANCE, L.FLIGHT):
+        v, f, c = T.valid_states(torch.from_numpy(st), phase)
+        rv, rf, rc = O.valid_states(st, phase, nthreads=8)
+        frag = ((u32(f) | rf) & L.F_FRAGILE) != 0
+        assert np.array_equal(np_(v)[~frag], rv[~frag])
+        assert np.array_equal(u32(f)[~frag], rf[~frag])
+        assert np.array_equal(u32(c)[~frag], rc[~frag])
+
+
+# ---- K2: the hot path ------------------------------------------------------------
+@pytest.mark.parametrize("kernel", [L.KERNEL_DIRECT, L.KERNEL_PERSISTENT])
+@pytest.mark.parametrize("adaptive", [False, True])
+@pytest.mark.parametrize("name", TERRAINS)
+def test_validate_pairs_parity(gpu, name, kernel, adaptive):
+    data, T, O = terrain_pair(name)
+    T.set_option(L.OPT_KERNEL, kernel)
+    n = 20000
+    s, a, d, _, _ = attempts_oracle(O, n, seed=123 + len(name))
+    res = T.validate_pairs(torch.from_numpy(s), torch.from_numpy(a), torch.from_numpy(d),
+                           adaptive=adaptive)
+    gpu_t = (np_(res.valid), np_(res.s_new), np_(res.t_new), u32(res.flags), u32(res.counts))
+    ref = O.validate_pairs(s, a, d, adaptive=adaptive, nthreads=8)
+    nfrag = assert_pairs_equal(gpu_t, ref, f"{name}/k{kernel}/ad{adaptive}")
+    assert nfrag <= n * 1e-3
+    assert ref[0].sum() > 0 or name.startswith("slope")  # some valid pairs are exercised
+
+
+@pytest.mark.parametrize("kernel", [L.KERNEL_DIRECT, L.KERNEL_PERSISTENT])
+@pytest.mark.parametrize("waves", [1, 2, 4])
+def test_validate_pairs_register_variants(gpu, kernel, waves):
+    data, T, O = terrain_pair("synth-rough-256")
+    T.set_option(L.OPT_KERNEL, kernel)
+    T.set_option(L.OPT_WAVES, waves)
+    try:
+        s, a, d, _, _ = attempts_oracle(O, 8192, seed=77)
+        res = T.validate_pairs(torch.from_numpy(s), torch.from_numpy(a), torch.from_numpy(d))
+        gpu_t = (np_(res.valid), np_(res.s_new), np_(res.t_new), u32(res.flags), u32(res.counts))
+        assert_pairs_equal(gpu_t, O.validate_pairs(s, a, d, nthreads=8), f"w{waves}")
+    finally:
+        T.set_option(L.OPT_WAVES, 2)
+
+
+@pytest.mark.parametrize("kernel", [L.KERNEL_DIRECT, L.KERNEL_PERSISTENT])
+def test_validate_pairs_edge_cases(gpu, kernel):
+    """Empty batch, untouched outputs, degenerate stance/flight times, edges."""
+    data, T, O = terrain_pair("synth-rough-256")
+    T.set_option(L.OPT_KERNEL, kernel)
+    empty = T.validate_pairs(torch.empty((0, 8), dtype=torch.float64),
+                             torch.empty((0, 10), dtype=torch.float64), L.FORWARD)
+    assert empty.valid.numel() == 0
+    s, a, d, _, _ = attempts_oracle(O, 4000, seed=5)
+    a = a.copy()
+    s = s.copy()
+    k = np.arange(4000)
+    a[k % 7 == 0, 7] = 0.0          # no flight phase
+    a[k % 7 == 1, 6] = -0.1         # stance loop never runs (t_s < 0)
+    a[k % 7 == 2, 6] = np.nan       # NaN stance time
+    a[k % 7 == 3, 7] = 0.05         # exactly one flight sample boundary
+    a[k % 7 == 4, 7] = 1e-300       # denormal-ish flight time
+    a[k % 13 == 5, 6] = np.inf      # the reference never terminates: engine sample cap
+    a[k % 13 == 6, 7] = np.inf
+    xN, yN = data.x[-1], data.y[-1]
+    s[k % 11 == 0, 0] = xN          # centre exactly at the map edge (UB lookup)
+    s[k % 11 == 1, 1] = yN
+    s[k % 11 == 2, 0] = data.x[10]  # centre exactly on a grid line
+    sentinel = np.full((4000, 8), 12345.0)
+    tsent = np.full(4000, -7.0)
+    for adaptive in (False, True):
+        res = T.validate_pairs(torch.from_numpy(s), torch.from_numpy(a), torch.from_numpy(d),
+                               adaptive=adaptive, s_new=torch.from_numpy(sentinel),
+                               t_new=torch.from_numpy(tsent))
+        ref = O.validate_pairs(s, a, d, adaptive=adaptive, s_new_init=sentinel,
+                               t_new_init=tsent, nthreads=8)
+        gpu_t = (np_(res.valid), np_(res.s_new), np_(res.t_new), u32(res.flags), u32(res.counts))
+        assert_pairs_equal(gpu_t, ref, f"edge/ad{adaptive}")
+        # rows the reference never assigns keep the caller's contents, bit for bit
+        assert np.all(same_f64(gpu_t[1], ref[1]))
+        assert np.all(same_f64(gpu_t[2], ref[2]))
+
+
+def test_validate_pairs_host_entry(gpu):
+    data, T, O = terrain_pair("synth-rough-256")
+    s, a, d, _, _ = attempts_oracle(O, 3000, seed=9)
+    out = T.validate_pairs_host(s, a, d)
+    assert_pairs_equal(out, O.validate_pairs(s, a, d, nthreads=8), "host")
+
+
+# ---- samplers ---------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["synth-rough-256", "slope-gridmap"])
+def test_samplers_match_oracle(gpu, name):
+    data, T, O = terrain_pair(name)
+    n = 20000
+    g, gt = T.sample_states(n, 31, 1, 0, require_phase=L.STANCE, max_tries=256)
+    r, rt = O.sample_states(n, 31, 1, 0, L.STANCE, 256, nthreads=8)
+    assert np.array_equal(np_(gt), rt)  # same accepted draw for every index
+    np.testing.assert_allclose(np_(g), r, rtol=1e-12, atol=1e-12)
+    nrm = O.normal_batch(r[:, :2])[0]
+    ga = T.sample_actions(torch.from_numpy(nrm), 31, 3)
+    ra = oracle.sample_actions(nrm, 31, 3)
+    np.testing.assert_allclose(np_(ga), ra, rtol=1e-12, atol=1e-12)
+    assert np.array_equal(np_(ga)[:, 6], ra[:, 6]) and np.array_equal(np_(ga)[:, 7], ra[:, 7])
+
+
+# ---- extend -------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["synth-rough-256", "rough_terrain-gridmap"])
+def test_extend_parity(gpu, name):
+    data, T, O = terrain_pair(name)
+    n = 6000
+    s_near, _, d, target, _ = attempts_oracle(O, n, seed=41)
+    base = 1000
+    r = T.extend(torch.from_numpy(s_near), torch.from_numpy(target), torch.from_numpy(d),
+                 seed=41, extend_base=base)
+    # the engine's candidate actions, regenerated through the public sampler:
+    # candidate j of extend i is stream EXTD (0x45585444), index (base+i)*8+j
+    nrm = O.normal_batch(target[:, :2])[0]
+    dense = np_(T.sample_actions(torch.from_numpy(np.repeat(nrm, 8, axis=0)), 41, 0x45585444,
+                                 base * 8)).reshape(n, 8, 10)
+    cand = np.ascontiguousarray(dense[:, :6])
+    rr, rch, rsn, ran, rc = O.extend_batch(s_near, target, cand, d, nthreads=8)
+    assert np.array_equal(np_(r.result), rr)
+    assert np.array_equal(np_(r.chosen), rch)
+    assert np.array_equal(u32(r.counts), rc)
+    acc = rr != L.TRAPPED
+    assert np.array_equal(bits(np_(r.s_new)[acc]), bits(rsn[acc]))
+    assert np.array_equal(bits(np_(r.a_new)[acc]), bits(ran[acc]))
+    assert (rch >= 0).sum() > 0
+
+
+# ---- nearest neighbour ------------------------------------------------------------------
+def test_nearest_parity(gpu):
+    import global_body_planner_amd as gbp
+    rng = np.random.default_rng(3)
+    verts = rng.normal(size=(5000, 8))
+    verts[100] = verts[7]          # exact duplicate: tie -> lowest index
+    q = np.concatenate([rng.normal(size=(2000, 8)), verts[[7, 100, 4999]]])
+    idx, dist = gbp.nearest(torch.from_numpy(q).cuda(), torch.from_numpy(verts).cuda())
+    ri, rd = oracle.nearest_batch(q, verts)
+    assert np.array_equal(np_(idx), ri)
+    assert np.array_equal(bits(np_(dist)), bits(rd))
+    assert np_(idx)[-3] == 7 and np_(idx)[-2] == 7
+    # empty tree keeps index 0 with +inf, like the reference's initial values
+    idx0, d0 = gbp.nearest(torch.from_numpy(q[:4]).cuda(), torch.empty((0, 8), dtype=torch.float64).cuda())
+    assert np.all(np_(idx0) == 0) and np.all(np.isinf(np_(d0)))
+
+
+# ---- full-size, size-independent properties --------------------------------------------
+def test_full_size_batch_properties(gpu):
+    """BASELINE config 3 size (256k attempts, synth-rough-1024): direct == persistent
+    bit for bit, determinism, slice independence, and parity with the oracle."""
+    import global_body_planner_amd as gbp
+    from global_body_planner_amd import workload as W
+    data = td.synth_rough(1024)
+    T = gbp.Terrain.from_data(data, device=0)
+    O = oracle.OracleTerrain.from_data(data)
+    n = 262144
+    s, a, d, tgt, tries = W.make_attempts(T, n, W.CONFIG_SEEDS[3])
+    assert int((tries < 0).sum()) == 0
+    outs = []
+    for kernel in (L.KERNEL_DIRECT, L.KERNEL_PERSISTENT, L.KERNEL_PERSISTENT):
+        T.set_option(L.OPT_KERNEL, kernel)
+        r = T.validate_pairs(s, a, d)
+        outs.append((np_(r.valid), np_(r.s_new), np_(r.t_new), u32(r.flags), u32(r.counts)))
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+    # slice independence: the second half generated on its own equals the full batch's half
+    s2, a2, d2, _, _ = W.make_attempts(T, n // 2, W.CONFIG_SEEDS[3], index_base=n // 2)
+    assert torch.equal(s2, s[n // 2:]) and torch.equal(a2, a[n // 2:]) and torch.equal(d2, d[n // 2:])
+    ref = O.validate_pairs(np_(s), np_(a), np_(d), nthreads=16)
+    nfrag = assert_pairs_equal(outs[0], ref, "full")
+    assert nfrag < 50
+    assert 0 < ref[0].sum() < n
