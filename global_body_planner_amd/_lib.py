@@ -22,7 +22,7 @@ MAX_SAMPLES = 4096
 F_STAGE_SHIFT = 8
 F_STAGE_MASK = 0xF << F_STAGE_SHIFT
 STORAGE_AUTO, STORAGE_F32, STORAGE_F64 = 0, 1, 2
-OPT_KERNEL, OPT_BLOCK, OPT_GRID_PER_CU, OPT_WAVES = 1, 2, 3, 4
+OPT_KERNEL, OPT_BLOCK, OPT_GRID_PER_CU, OPT_WAVES, OPT_LDS_COORDS = 1, 2, 3, 4, 5
 KERNEL_DIRECT, KERNEL_PERSISTENT = 0, 1
 
 EXPORTS = [
@@ -50,16 +50,20 @@ class GbpError(RuntimeError):
 _lib = None
 
 
-def load():
-    """Load libgbp.so (raises OSError / FileNotFoundError if it is not built)."""
+def load(path=None):
+    """Load libgbp.so (raises OSError / FileNotFoundError if it is not built).
+
+    `path` loads another build of the same ABI (diagnostic timing builds) as a
+    separate handle; the default library is cached."""
     global _lib
-    if _lib is not None:
+    if path is None and _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    p = path or LIB_PATH
+    if not os.path.exists(p):
         raise FileNotFoundError(
-            f"{LIB_PATH} is missing: build the HIP engine first "
+            f"{p} is missing: build the HIP engine first "
             "(python -c 'import __graft_entry__ as g; g.build()')")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(p)
     P, I, I64, U64, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t
     sig = {
         "gbp_version": (I, []),
@@ -94,8 +98,9 @@ def load():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    _lib = L
-    return _lib
+    if path is None:
+        _lib = L
+    return L
 
 
 def check(status, what=""):

@@ -53,6 +53,9 @@ struct TerrainView {
   int nx, ny;
   double x0, xN, y0, yN;         // x[0], x[nx-1], y[0], y[ny-1]
   double inv_hx, inv_hy;         // 1 / mean spacing (bracket guess only)
+  int one_x, one_y;              // host-verified: the guess is within one cell of the
+                                 // bracket for every v (gbp_terrain_create), so a single
+                                 // branch-free correction step is exact
 };
 
 // First i with d[i] <= v < d[i+1] (fast_terrain_map.cpp:101-117).  O(1): a
@@ -64,14 +67,23 @@ struct TerrainView {
 constexpr int BR_LOW = -1;
 constexpr int BR_HIGH = -2;
 
+__device__ __forceinline__ int bracket_guess(int n, double d0, double inv, double v) {
+  const int i = (int)((v - d0) * inv);
+  return i < 0 ? 0 : (i > n - 2 ? n - 2 : i);
+}
+
 __device__ __forceinline__ int bracket(const double *__restrict__ d, int n, double d0,
-                                       double dN, double inv, double v) {
+                                       double dN, double inv, int one, double v) {
   if (!(v >= d0 && v < dN)) return (v >= dN) ? BR_HIGH : BR_LOW;
-  const double g = (v - d0) * inv;
-  int i = (int)g;
-  i = i < 0 ? 0 : (i > n - 2 ? n - 2 : i);
-  while (i > 0 && v < d[i]) --i;
-  while (i < n - 2 && v >= d[i + 1]) ++i;
+  int i = bracket_guess(n, d0, inv, v);
+#ifndef GBP_EXPERIMENT_FAST_BRACKET  // diagnostic timing build only (results may differ)
+  if (one) {
+    i += (v >= d[i + 1] ? 1 : 0) - (v < d[i] ? 1 : 0);
+  } else {
+    while (i > 0 && v < d[i]) --i;
+    while (i < n - 2 && v >= d[i + 1]) ++i;
+  }
+#endif
   return i;
 }
 
@@ -89,8 +101,8 @@ __device__ __forceinline__ void load_quad(const TerrainView<ZT> &T, int ix, int 
 // (BR_HIGH on an axis), else the reference's bool (BR_LOW -> index 0)
 template <class ZT>
 __device__ __forceinline__ int nan_at(const TerrainView<ZT> &T, double x, double y) {
-  const int ix = bracket(T.x, T.nx, T.x0, T.xN, T.inv_hx, x);
-  const int iy = bracket(T.y, T.ny, T.y0, T.yN, T.inv_hy, y);
+  const int ix = bracket(T.x, T.nx, T.x0, T.xN, T.inv_hx, T.one_x, x);
+  const int iy = bracket(T.y, T.ny, T.y0, T.yN, T.inv_hy, T.one_y, y);
   if (ix == BR_HIGH || iy == BR_HIGH) return -1;
   double f11, f12, f21, f22;
   load_quad(T, ix < 0 ? 0 : ix, iy < 0 ? 0 : iy, f11, f12, f21, f22);
@@ -117,8 +129,8 @@ __device__ __forceinline__ bool height_at(const TerrainView<ZT> &T, double x, do
     h = __builtin_nan("");
     return true;
   }
-  const int ix = bracket(T.x, T.nx, T.x0, T.xN, T.inv_hx, x);
-  const int iy = bracket(T.y, T.ny, T.y0, T.yN, T.inv_hy, y);
+  const int ix = bracket(T.x, T.nx, T.x0, T.xN, T.inv_hx, T.one_x, x);
+  const int iy = bracket(T.y, T.ny, T.y0, T.yN, T.inv_hy, T.one_y, y);
   if (ix < 0 || iy < 0) return false;
   const double x1 = T.x[ix], x2 = T.x[ix + 1], y1 = T.y[iy], y2 = T.y[iy + 1];
   double f11, f12, f21, f22;
@@ -129,12 +141,60 @@ __device__ __forceinline__ bool height_at(const TerrainView<ZT> &T, double x, do
   return true;
 }
 
+// ---- batched lookups ------------------------------------------------------------
+// A probe = one lookup point's bracket plus its four heights, fetched
+// UNCONDITIONALLY from a clamped (always valid) cell so that every fetch of a
+// state check can be in flight at once; the reference's sequential logic and
+// early exits are then replayed on the fetched values (is_valid_state below).
+template <class ZT>
+struct Probe {
+  int ix, iy;   // bracket codes: >= 0, BR_LOW or BR_HIGH
+  ZT q[4];      // z[cx][cy], z[cx][cy+1], z[cx+1][cy], z[cx+1][cy+1] of the clamped cell
+};
+
+template <class ZT>
+__device__ __forceinline__ void probe(const TerrainView<ZT> &T, double x, double y, Probe<ZT> &p) {
+  p.ix = bracket(T.x, T.nx, T.x0, T.xN, T.inv_hx, T.one_x, x);
+  p.iy = bracket(T.y, T.ny, T.y0, T.yN, T.inv_hy, T.one_y, y);
+  const int cx = p.ix < 0 ? 0 : p.ix, cy = p.iy < 0 ? 0 : p.iy;
+  const ZT *z = T.z + (size_t)cx * T.ny + cy;
+  p.q[0] = z[0];
+  p.q[1] = z[1];
+  p.q[2] = z[T.ny];
+  p.q[3] = z[T.ny + 1];
+}
+
+// heightIsNan on a probe: -1 = UB (BR_HIGH), else the reference's bool
+template <class ZT>
+__device__ __forceinline__ int probe_nan(const Probe<ZT> &p) {
+  if (p.ix == BR_HIGH || p.iy == BR_HIGH) return -1;
+  return (isnan((double)p.q[0]) || isnan((double)p.q[1]) || isnan((double)p.q[2]) ||
+          isnan((double)p.q[3])) ? 1 : 0;
+}
+
+// getGroundHeight on a probe (same contract as height_at)
+template <class ZT>
+__device__ __forceinline__ bool probe_height(const TerrainView<ZT> &T, const Probe<ZT> &p,
+                                             double x, double y, double &h, bool &near) {
+  if (isnan(x) || isnan(y)) {
+    h = __builtin_nan("");
+    return true;
+  }
+  if (p.ix < 0 || p.iy < 0) return false;
+  const double x1 = T.x[p.ix], x2 = T.x[p.ix + 1], y1 = T.y[p.iy], y2 = T.y[p.iy + 1];
+  near = near || fabs(x - x1) < FRAGILE_EPS || fabs(x2 - x) < FRAGILE_EPS ||
+         fabs(y - y1) < FRAGILE_EPS || fabs(y2 - y) < FRAGILE_EPS;
+  h = bilinear((double)p.q[0], (double)p.q[1], (double)p.q[2], (double)p.q[3], x1, x2, y1, y2, x,
+               y);
+  return true;
+}
+
 // fast_terrain_map.cpp:160-213
 template <class ZT>
 __device__ __forceinline__ bool surface_normal(const TerrainView<ZT> &T, double x, double y,
                                                double n[3]) {
-  const int ix = bracket(T.x, T.nx, T.x0, T.xN, T.inv_hx, x);
-  const int iy = bracket(T.y, T.ny, T.y0, T.yN, T.inv_hy, y);
+  const int ix = bracket(T.x, T.nx, T.x0, T.xN, T.inv_hx, T.one_x, x);
+  const int iy = bracket(T.y, T.ny, T.y0, T.yN, T.inv_hy, T.one_y, y);
   if (isnan(x) || isnan(y) || ix < 0 || iy < 0) {
     n[0] = n[1] = n[2] = __builtin_nan("");
     return isnan(x) || isnan(y);  // NaN coordinates: deterministic NaN, not UB
@@ -235,8 +295,11 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
     return false;
   }
   acc.V++;
+  // centre cell fetched first: its latency hides under the checks and trig below
+  Probe<ZT> pc;
+  probe(T, s[0], s[1], pc);
   // (1) heightIsNan(centre) :564
-  const int r = nan_at(T, s[0], s[1]);
+  const int r = probe_nan(pc);
   if (r < 0) {  // x or y >= the last coordinate: rejected by (2) unless exactly equal
     const bool in_closed = !(s[0] < T.x0 || s[0] > T.xN || s[1] < T.y0 || s[1] > T.yN);
     if (in_closed) acc.flags |= GBP_F_OOD;
@@ -267,9 +330,21 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
   const double R_21 = sy * cp, R_22 = cy, R_23 = sy * sp;
   const double R_31 = -sp, R_32 = 0, R_33 = cp;
   const double z_body = -ROBOT_H;
-  // (5) four corners :601-627, x_body outer, y_body inner (not unrolled: keeps
-  // one corner's cells live at a time)
-#pragma unroll 1
+  // all nine remaining lookups of this state are fetched before any is tested
+  Probe<ZT> pl[4], pk[4], pu;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const double x_body = (k < 2) ? -0.5 * ROBOT_L : 0.5 * ROBOT_L;
+    const double y_body = (k & 1) ? 0.5 * ROBOT_W : -0.5 * ROBOT_W;
+    const double x_leg = s[0] + R_11 * x_body + R_12 * y_body;
+    const double y_leg = s[1] + R_21 * x_body + R_22 * y_body;
+    probe(T, x_leg, y_leg, pl[k]);
+    probe(T, x_leg + R_13 * z_body, y_leg + R_23 * z_body, pk[k]);
+  }
+  const double ux = s[0] + R_13 * z_body, uy = s[1] + R_23 * z_body;
+  probe(T, ux, uy, pu);
+  // (5) four corners :601-627, x_body outer, y_body inner, in reference order
+#pragma unroll
   for (int k = 0; k < 4; k++) {
     const double x_body = (k < 2) ? -0.5 * ROBOT_L : 0.5 * ROBOT_L;
     const double y_body = (k & 1) ? 0.5 * ROBOT_W : -0.5 * ROBOT_W;
@@ -279,7 +354,7 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
     const double x_corner = x_leg + R_13 * z_body;
     const double y_corner = y_leg + R_23 * z_body;
     const double z_corner = z_leg + R_33 * z_body;
-    const int rl = nan_at(T, x_leg, y_leg);  // heightIsNan(leg) :614
+    const int rl = probe_nan(pl[k]);  // heightIsNan(leg) :614
     if (rl < 0) {
       acc.flags |= GBP_F_OOD;
       return false;
@@ -291,13 +366,13 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
     acc.G += 2;  // both heights computed before the test :618-619
     double gl, gc;
     bool near = false;
-    const bool okl = height_at(T, x_leg, y_leg, gl, near);
+    const bool okl = probe_height(T, pl[k], x_leg, y_leg, gl, near);
     if (near) acc.flags |= GBP_F_FRAGILE;
     if (!okl) {
       acc.flags |= GBP_F_OOD;
       return false;
     }
-    const bool okc = height_at(T, x_corner, y_corner, gc, near);
+    const bool okc = probe_height(T, pk[k], x_corner, y_corner, gc, near);
     if (near) acc.flags |= GBP_F_FRAGILE;
     if (!okc) {
       acc.flags |= GBP_F_OOD;
@@ -314,7 +389,7 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
   acc.G++;
   double gu;
   bool near = false;
-  const bool oku = height_at(T, s[0] + R_13 * z_body, s[1] + R_23 * z_body, gu, near);
+  const bool oku = probe_height(T, pu, ux, uy, gu, near);
   if (near) acc.flags |= GBP_F_FRAGILE;
   if (!oku) {
     acc.flags |= GBP_F_OOD;

@@ -92,12 +92,28 @@ __global__ void k_valid_states(TerrainView<ZT> T, int64_t n, const double *__res
 // ============================================================================
 // W = minimum waves per SIMD requested from the register allocator
 // (__launch_bounds__ 2nd argument): 1 -> up to 512 VGPR+AGPR, 2 -> 256, 4 -> 128.
-template <class ZT, bool ADAPTIVE, int W>
+// LDSC: the coordinate vectors are staged in LDS (bracket fix-up and the
+// bilinear x1/x2/y1/y2 then never touch global memory)
+template <class ZT>
+__device__ __forceinline__ TerrainView<ZT> stage_coords(const TerrainView<ZT> &T0, double *smem) {
+  for (int i = threadIdx.x; i < T0.nx; i += blockDim.x) smem[i] = T0.x[i];
+  for (int i = threadIdx.x; i < T0.ny; i += blockDim.x) smem[T0.nx + i] = T0.y[i];
+  __syncthreads();
+  TerrainView<ZT> T = T0;
+  T.x = smem;
+  T.y = smem + T0.nx;
+  return T;
+}
+
+extern __shared__ double gbp_smem[];
+
+template <class ZT, bool ADAPTIVE, int W, bool LDSC>
 __global__ __launch_bounds__(256, W) void k_validate_direct(
-    TerrainView<ZT> T, int64_t n, const double *__restrict__ S, const double *__restrict__ A,
+    TerrainView<ZT> T0, int64_t n, const double *__restrict__ S, const double *__restrict__ A,
     const uint8_t *__restrict__ dir, int dir_all, uint8_t *__restrict__ valid,
     double *__restrict__ s_new, double *__restrict__ t_new, uint32_t *__restrict__ flags,
     uint32_t *__restrict__ counts) {
+  const TerrainView<ZT> T = LDSC ? stage_coords(T0, gbp_smem) : T0;
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   double s[8], a[10], sn[8];
@@ -139,7 +155,9 @@ enum : int {
 enum : int { SN_NONE = 0, SN_STANCE_S = 1, SN_FLIGHT_B = 2, SN_STANCE_REV_B = 3 };
 
 struct Lane {
-  double s[8], a[10], b[8];  // input state, action, take-off state of the phase
+  double s[8], a[10];        // input state and action (the take-off state of the
+                             // flight / reverse-stance phases is recomputed per
+                             // sample: cheaper than 16 more live VGPRs)
   double t, ts, tpre;        // sample time, adaptive step, last success time
   double snew_p, tnew;
   int stage, snew_kind;
@@ -162,7 +180,6 @@ __device__ __forceinline__ void enter_stage(Lane &L, int st) {
         st = ST_FWD_FLIGHT;
         break;
       case ST_FWD_FLIGHT:  // :732-735
-        apply_stance(L.s, L.a, L.a[6], L.b);
         L.t = 0;
         if (L.t < L.a[7]) return;
         st = ST_FWD_LAND;
@@ -173,7 +190,6 @@ __device__ __forceinline__ void enter_stage(Lane &L, int st) {
         st = ST_REV_STANCE;
         break;
       case ST_REV_STANCE:  // :849-852
-        apply_flight(L.s, -L.a[7], L.b);
         L.t = L.a[6];
         if (L.t >= 0) return;
         st = ST_REV_START;
@@ -181,6 +197,26 @@ __device__ __forceinline__ void enter_stage(Lane &L, int st) {
       default:  // FWD_LAND, REV_START: exactly one sample
         return;
     }
+  }
+}
+
+// the state the reference evaluates at time t of a stage (the take-off state
+// s_takeoff of :732 / :849 recomputed from (s, a): the same closed form and
+// operands, hence the same bits)
+__device__ __forceinline__ void sample_state(const Lane &L, int stage, double t, double *o) {
+  double b[8];
+  switch (stage) {
+    case ST_FWD_STANCE: apply_stance(L.s, L.a, t, o); return;
+    case ST_REV_FLIGHT: apply_flight(L.s, -t, o); return;
+    case ST_FWD_FLIGHT:
+    case ST_FWD_LAND:  // applyFlight(applyStance(s, a), t)
+      apply_stance(L.s, L.a, L.a[6], b);
+      apply_flight(b, t, o);
+      return;
+    default:  // ST_REV_STANCE / ST_REV_START: applyStanceReverse(applyFlight(s, -t_f), a, t)
+      apply_flight(L.s, -L.a[7], b);
+      apply_stance_reverse(b, L.a, t, o);
+      return;
   }
 }
 
@@ -193,15 +229,9 @@ __device__ __forceinline__ bool small_step(double ts) {
 template <class ZT, bool ADAPTIVE>
 __device__ __forceinline__ bool step_lane(const TerrainView<ZT> &T, Lane &L) {
   double sc[8];
-  int phase = GBP_STANCE;
-  switch (L.stage) {
-    case ST_FWD_STANCE: apply_stance(L.s, L.a, L.t, sc); break;
-    case ST_FWD_FLIGHT: apply_flight(L.b, L.t, sc); phase = GBP_FLIGHT; break;
-    case ST_FWD_LAND: apply_flight(L.b, L.a[7], sc); break;
-    case ST_REV_FLIGHT: apply_flight(L.s, -L.t, sc); phase = GBP_FLIGHT; break;
-    case ST_REV_STANCE: apply_stance_reverse(L.b, L.a, L.t, sc); break;
-    default: apply_stance_reverse(L.b, L.a, 0, sc); break;  // ST_REV_START
-  }
+  const int phase = (L.stage == ST_FWD_FLIGHT || L.stage == ST_REV_FLIGHT) ? GBP_FLIGHT : GBP_STANCE;
+  sample_state(L, L.stage,
+               L.stage == ST_FWD_LAND ? L.a[7] : (L.stage == ST_REV_START ? 0.0 : L.t), sc);
   const bool ok = is_valid_state(T, sc, phase, L.acc);
   if (L.acc.flags & GBP_F_LIMIT) return true;  // stopped: reported invalid
   const double step = ADAPTIVE ? 0.0 : KINEMATICS_RES;  // plain loops: constant increment
@@ -297,12 +327,13 @@ __device__ __forceinline__ bool step_lane(const TerrainView<ZT> &T, Lane &L) {
   }
 }
 
-template <class ZT, bool ADAPTIVE, int W>
+template <class ZT, bool ADAPTIVE, int W, bool LDSC>
 __global__ __launch_bounds__(256, W) void k_validate_persistent(
-    TerrainView<ZT> T, int n, const double *__restrict__ S, const double *__restrict__ A,
+    TerrainView<ZT> T0, int n, const double *__restrict__ S, const double *__restrict__ A,
     const uint8_t *__restrict__ dir, int dir_all, uint8_t *__restrict__ valid,
     double *__restrict__ s_new, double *__restrict__ t_new, uint32_t *__restrict__ flags,
     uint32_t *__restrict__ counts, unsigned int *__restrict__ head) {
+  const TerrainView<ZT> T = LDSC ? stage_coords(T0, gbp_smem) : T0;
   const int lane = threadIdx.x & (WAVE - 1);
   Lane L;
   L.stage = ST_IDLE;
@@ -345,8 +376,8 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
         if (s_new && L.snew_kind != SN_NONE) {
           double o[8];
           if (L.snew_kind == SN_STANCE_S) apply_stance(L.s, L.a, L.snew_p, o);
-          else if (L.snew_kind == SN_FLIGHT_B) apply_flight(L.b, L.snew_p, o);
-          else apply_stance_reverse(L.b, L.a, L.snew_p, o);
+          else if (L.snew_kind == SN_FLIGHT_B) sample_state(L, ST_FWD_LAND, L.snew_p, o);
+          else sample_state(L, ST_REV_STANCE, L.snew_p, o);
 #pragma unroll
           for (int k = 0; k < 8; k++) s_new[8 * i + k] = o[k];
         }
@@ -540,6 +571,7 @@ struct gbp_terrain {
   int storage = GBP_STORAGE_F64;
   double bounds[4] = {0, 0, 0, 0};
   double inv_hx = 0, inv_hy = 0;
+  int one_x = 0, one_y = 0;         // one-step bracket correction is exact (verified)
   double *d_x = nullptr, *d_y = nullptr;
   void *d_z = nullptr;
   double *d_dx = nullptr, *d_dy = nullptr, *d_dz = nullptr;
@@ -548,6 +580,7 @@ struct gbp_terrain {
   int64_t opt_block = 256;
   int64_t opt_grid_per_cu = 8;
   int64_t opt_waves = 2;            // register budget of the validate kernels (waves/SIMD)
+  int64_t opt_lds_coords = 1;       // stage the coordinate vectors in LDS when they fit
   unsigned int *d_head = nullptr;   // persistent-kernel work counter (zeroed per launch)
   hipStream_t host_stream = nullptr;
   void *ws = nullptr;               // grow-only device workspace
@@ -592,6 +625,8 @@ TerrainView<ZT> view(const gbp_terrain *t) {
   v.yN = t->bounds[3];
   v.inv_hx = t->inv_hx;
   v.inv_hy = t->inv_hy;
+  v.one_x = t->one_x;
+  v.one_y = t->one_y;
   return v;
 }
 
@@ -616,12 +651,13 @@ int ensure_ws(gbp_terrain *t, void **ws, size_t *have, size_t need) {
   return GBP_OK;
 }
 
-template <class ZT, bool AD, int W>
+template <class ZT, bool AD, int W, bool LDSC>
 int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *a,
                       const uint8_t *dir, int dir_all, uint8_t *valid, double *s_new,
                       double *t_new, uint32_t *flags, uint32_t *counts, hipStream_t st) {
   const TerrainView<ZT> T = view<ZT>(t);
   const int block = (int)t->opt_block;
+  const size_t lds = LDSC ? sizeof(double) * (size_t)(t->nx + t->ny) : 0;
   const int64_t chunk = (int64_t)1 << 30;
   const int64_t want = (int64_t)t->num_cus * t->opt_grid_per_cu;
   for (int64_t off = 0; off < n; off += chunk) {
@@ -632,15 +668,17 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
     double *tn = t_new ? t_new + off : nullptr;
     uint32_t *c = counts ? counts + off : nullptr;
     if (t->opt_kernel == GBP_KERNEL_DIRECT) {
+      // the direct form inlines the state check at five call sites: it gets the
+      // whole register file (W = 1) whatever the persistent kernel's budget is
       const unsigned g = (unsigned)((m + block - 1) / block);
-      hipLaunchKernelGGL((k_validate_direct<ZT, AD, W>), dim3(g), dim3(block), 0, st, T, m,
+      hipLaunchKernelGGL((k_validate_direct<ZT, AD, 1, LDSC>), dim3(g), dim3(block), lds, st, T, m,
                          s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn, flags + off, c);
     } else {
       // persistent: grid sized to residency; the work counter is zeroed per launch
       const int64_t g = std::max<int64_t>(1, std::min<int64_t>(want, (m + block - 1) / block));
       HIPCHK(hipMemsetAsync(t->d_head, 0, sizeof(unsigned int), st));
-      hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W>), dim3((unsigned)g), dim3(block), 0,
-                         st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
+      hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, LDSC>), dim3((unsigned)g), dim3(block),
+                         lds, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
                          flags + off, c, t->d_head);
     }
     HIPCHK(hipGetLastError());
@@ -653,15 +691,39 @@ int launch_validate(gbp_terrain *t, int64_t n, const double *s, const double *a,
                     const uint8_t *dir, int dir_all, int adaptive, uint8_t *valid,
                     double *s_new, double *t_new, uint32_t *flags, uint32_t *counts,
                     hipStream_t st) {
-#define GBP_LV(AD, W) \
-  launch_validate_w<ZT, AD, W>(t, n, s, a, dir, dir_all, valid, s_new, t_new, flags, counts, st)
+#define GBP_LV(AD, W)                                                                         \
+  (lds_ok ? launch_validate_w<ZT, AD, W, true>(t, n, s, a, dir, dir_all, valid, s_new, t_new,  \
+                                               flags, counts, st)                              \
+          : launch_validate_w<ZT, AD, W, false>(t, n, s, a, dir, dir_all, valid, s_new, t_new, \
+                                                flags, counts, st))
   const int64_t w = t->opt_waves;
+  const bool lds_ok = t->opt_lds_coords && sizeof(double) * (size_t)(t->nx + t->ny) <= 65536;
   if (adaptive) return w >= 4 ? GBP_LV(true, 4) : (w >= 2 ? GBP_LV(true, 2) : GBP_LV(true, 1));
   return w >= 4 ? GBP_LV(false, 4) : (w >= 2 ? GBP_LV(false, 2) : GBP_LV(false, 1));
 #undef GBP_LV
 }
 
 bool valid_handle(const gbp_terrain *t) { return t != nullptr && t->d_z != nullptr; }
+
+// The device guesses a bracket as (int)((v - d[0]) * inv) clamped to [0, n-2]
+// (gbp_device.h bracket_guess); this host copy uses the same IEEE operations
+// (no contraction in this TU).  The guess is monotone in v, so checking both
+// ends of every cell [d[i], d[i+1]) proves |guess - bracket| <= 1 everywhere.
+int guess_host(int n, double d0, double inv, double v) {
+  const int i = (int)((v - d0) * inv);
+  return i < 0 ? 0 : (i > n - 2 ? n - 2 : i);
+}
+
+int one_step_exact(const double *d, int n, double inv) {
+  if (!(inv > 0) || !std::isfinite(inv)) return 0;
+  for (int i = 0; i + 1 < n; i++) {
+    if (!(d[i] < d[i + 1])) return 0;  // empty cells: keep the general search
+    const int lo = guess_host(n, d[0], inv, d[i]);
+    const int hi = guess_host(n, d[0], inv, std::nextafter(d[i + 1], -INFINITY));
+    if (lo < i - 1 || hi > i + 1) return 0;
+  }
+  return 1;
+}
 
 // host-pointer entry points: one synchronous staging round trip through the
 // handle's workspace on its private stream (used by the C++ adapters that
@@ -776,6 +838,8 @@ int gbp_terrain_create(int device, int nx, int ny, const double *x, const double
   t->bounds[3] = y[ny - 1];
   t->inv_hx = (x[nx - 1] > x[0]) ? (double)(nx - 1) / (x[nx - 1] - x[0]) : 0.0;
   t->inv_hy = (y[ny - 1] > y[0]) ? (double)(ny - 1) / (y[ny - 1] - y[0]) : 0.0;
+  t->one_x = one_step_exact(x, nx, t->inv_hx);
+  t->one_y = one_step_exact(y, ny, t->inv_hy);
   (void)hipDeviceGetAttribute(&t->num_cus, hipDeviceAttributeMultiprocessorCount, device);
   if (t->num_cus <= 0) t->num_cus = 256;
   int rc = GBP_OK;
@@ -860,6 +924,9 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
       if (value != 1 && value != 2 && value != 4) return GBP_E_INVALID_ARG;
       t->opt_waves = value;
       return GBP_OK;
+    case GBP_OPT_LDS_COORDS:
+      t->opt_lds_coords = value ? 1 : 0;
+      return GBP_OK;
     default:
       return GBP_E_INVALID_ARG;
   }
@@ -873,6 +940,7 @@ int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value) {
     case GBP_OPT_BLOCK: *value = t->opt_block; return GBP_OK;
     case GBP_OPT_GRID_PER_CU: *value = t->opt_grid_per_cu; return GBP_OK;
     case GBP_OPT_WAVES: *value = t->opt_waves; return GBP_OK;
+    case GBP_OPT_LDS_COORDS: *value = t->opt_lds_coords; return GBP_OK;
     default: return GBP_E_INVALID_ARG;
   }
 }

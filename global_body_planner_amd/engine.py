@@ -51,8 +51,8 @@ class Terrain:
     """A FastTerrainMap resident in HBM (x-major heights, fp32 when lossless)."""
 
     def __init__(self, x, y, z, dx=None, dy=None, dz=None, device=0,
-                 storage=L.STORAGE_AUTO, kernel=None):
-        self._lib = L.load()
+                 storage=L.STORAGE_AUTO, kernel=None, lib=None):
+        self._lib = lib if lib is not None else L.load()
         self.device = int(device)
         self.torch_device = torch.device("cuda", self.device)
         x = np.ascontiguousarray(x, np.float64)

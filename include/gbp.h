@@ -120,6 +120,7 @@ int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage,
 #define GBP_OPT_BLOCK         2  /* threads per workgroup (multiple of 64)            */
 #define GBP_OPT_GRID_PER_CU   3  /* persistent kernel: workgroups per CU              */
 #define GBP_OPT_WAVES         4  /* register budget: min waves per SIMD (1, 2 or 4)   */
+#define GBP_OPT_LDS_COORDS    5  /* 1: stage coordinate vectors in LDS when they fit  */
 #define GBP_KERNEL_DIRECT     0  /* one lane per attempt                              */
 #define GBP_KERNEL_PERSISTENT 1  /* persistent waves, lanes re-packed per sample      */
 int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value);

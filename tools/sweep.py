@@ -1,0 +1,91 @@
+"""Interleaved A/B sweep of validate-kernel variants in ONE process
+(cdna_hip_programming.md §5.4 rule 24): every variant is timed in each of R
+rounds, rounds interleaved; prints median/min ms per launch and checks that
+every variant returns bit-identical outputs."""
+import argparse
+import itertools
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import global_body_planner_amd as gbp  # noqa: E402
+from global_body_planner_amd import _lib as L  # noqa: E402
+from global_body_planner_amd import terrain_data as td  # noqa: E402
+from global_body_planner_amd import workload as W  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--terrain", default="synth-rough-1024")
+    p.add_argument("--batch", type=int, default=262144)
+    p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--launches", type=int, default=10)
+    p.add_argument("--kernels", default="direct,persistent")
+    p.add_argument("--waves", default="1,2,4")
+    p.add_argument("--grid", default="4,8,16")
+    p.add_argument("--block", default="256")
+    p.add_argument("--lds", default="1")
+    p.add_argument("--adaptive", action="store_true")
+    p.add_argument("--out", default=None)
+    a = p.parse_args()
+    data = td.by_name(a.terrain)
+    T = gbp.Terrain.from_data(data, device=0)
+    s, act, d, _, _ = W.make_attempts(T, a.batch, W.CONFIG_SEEDS[3])
+    variants = []
+    for k in a.kernels.split(","):
+        for w in (map(int, a.waves.split(",")) if k == "persistent" else [1]):
+            for b in map(int, a.block.split(",")):
+                grids = map(int, a.grid.split(",")) if k == "persistent" else [0]
+                for g in grids:
+                    for lds in map(int, a.lds.split(",")):
+                        variants.append((k, w, b, g, lds))
+    times = {v: [] for v in variants}
+    ref = None
+    st = torch.cuda.current_stream()
+    for r in range(a.rounds):
+        for v in variants:
+            k, w, b, g, lds = v
+            T.set_option(L.OPT_KERNEL, L.KERNEL_PERSISTENT if k == "persistent" else L.KERNEL_DIRECT)
+            T.set_option(L.OPT_WAVES, w)
+            T.set_option(L.OPT_LDS_COORDS, lds)
+            T.set_option(L.OPT_BLOCK, b)
+            if g:
+                T.set_option(L.OPT_GRID_PER_CU, g)
+            out = T.validate_pairs(s, act, d, adaptive=a.adaptive)
+            if r == 0:
+                sig = (out.valid.cpu().numpy().tobytes(), out.flags.cpu().numpy().tobytes(),
+                       out.counts.cpu().numpy().tobytes(), out.s_new.cpu().numpy().tobytes())
+                if ref is None:
+                    ref = sig
+                elif sig != ref:
+                    print(f"MISMATCH in variant {v}", flush=True)
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(a.launches)]
+            for e0, e1 in ev:
+                e0.record(st)
+                T.validate_pairs(s, act, d, adaptive=a.adaptive, out=out)
+                e1.record(st)
+            torch.cuda.synchronize()
+            times[v].extend(e0.elapsed_time(e1) for e0, e1 in ev)
+    rows = []
+    for v in variants:
+        t = np.array(times[v])
+        rows.append({"kernel": v[0], "waves": v[1], "block": v[2], "grid_per_cu": v[3], "lds": v[4],
+                     "median_ms": float(np.median(t)), "min_ms": float(t.min()),
+                     "attempts_per_s": a.batch / (np.median(t) * 1e-3)})
+    rows.sort(key=lambda r: r["median_ms"])
+    for r in rows:
+        print(f"{r['kernel']:10s} w={r['waves']} b={r['block']} g={r['grid_per_cu']:2d} lds={r['lds']} "
+              f"median {r['median_ms']:.4f} ms  min {r['min_ms']:.4f} ms  "
+              f"{r['attempts_per_s'] / 1e6:.1f} M attempts/s")
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump({"terrain": a.terrain, "batch": a.batch, "rows": rows}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
