@@ -113,6 +113,11 @@ __device__ __forceinline__ int nan_at(const TerrainView<ZT> &T, double x, double
 __device__ __forceinline__ double bilinear(double f11, double f12, double f21, double f22,
                                            double x1, double x2, double y1, double y2,
                                            double x, double y) {
+#ifdef GBP_EXPERIMENT_NO_DIV
+  return 2500.0 * ((x2 - x1) * (y2 - y1)) *
+         (f11 * (x2 - x) * (y2 - y) + f21 * (x - x1) * (y2 - y) + f12 * (x2 - x) * (y - y1) +
+          f22 * (x - x1) * (y - y1));
+#endif
   return 1.0 / ((x2 - x1) * (y2 - y1)) *
          (f11 * (x2 - x) * (y2 - y) + f21 * (x - x1) * (y2 - y) + f12 * (x2 - x) * (y - y1) +
           f22 * (x - x1) * (y - y1));
@@ -157,6 +162,10 @@ __device__ __forceinline__ void probe(const TerrainView<ZT> &T, double x, double
   p.ix = bracket(T.x, T.nx, T.x0, T.xN, T.inv_hx, T.one_x, x);
   p.iy = bracket(T.y, T.ny, T.y0, T.yN, T.inv_hy, T.one_y, y);
   const int cx = p.ix < 0 ? 0 : p.ix, cy = p.iy < 0 ? 0 : p.iy;
+#ifdef GBP_EXPERIMENT_NO_ZLOAD
+  p.q[0] = (ZT)(cx * 1e-4); p.q[1] = (ZT)(cy * 1e-4); p.q[2] = (ZT)0.1; p.q[3] = (ZT)0.2;
+  return;
+#endif
   const ZT *z = T.z + (size_t)cx * T.ny + cy;
   p.q[0] = z[0];
   p.q[1] = z[1];
@@ -182,8 +191,10 @@ __device__ __forceinline__ bool probe_height(const TerrainView<ZT> &T, const Pro
   }
   if (p.ix < 0 || p.iy < 0) return false;
   const double x1 = T.x[p.ix], x2 = T.x[p.ix + 1], y1 = T.y[p.iy], y2 = T.y[p.iy + 1];
+#ifndef GBP_EXPERIMENT_NO_FRAGILE
   near = near || fabs(x - x1) < FRAGILE_EPS || fabs(x2 - x) < FRAGILE_EPS ||
          fabs(y - y1) < FRAGILE_EPS || fabs(y2 - y) < FRAGILE_EPS;
+#endif
   h = bilinear((double)p.q[0], (double)p.q[1], (double)p.q[2], (double)p.q[3], x1, x2, y1, y2, x,
                y);
   return true;

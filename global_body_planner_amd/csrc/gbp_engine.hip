@@ -35,22 +35,43 @@ namespace {
 constexpr uint64_t EXTEND_STREAM = 0x45585444ull;  // "EXTD"
 constexpr int WAVE = 64;
 
+// LDSC: the coordinate vectors are staged in LDS (bracket fix-up and the
+// bilinear x1/x2/y1/y2 then never touch global memory)
+template <class ZT>
+__device__ __forceinline__ TerrainView<ZT> stage_coords(const TerrainView<ZT> &T0, double *smem) {
+  for (int i = threadIdx.x; i < T0.nx; i += blockDim.x) smem[i] = T0.x[i];
+  for (int i = threadIdx.x; i < T0.ny; i += blockDim.x) smem[T0.nx + i] = T0.y[i];
+  __syncthreads();
+  TerrainView<ZT> T = T0;
+  T.x = smem;
+  T.y = smem + T0.nx;
+  return T;
+}
+
 // ============================================================================
 // K1: batched terrain queries
 // ============================================================================
-template <class ZT>
-__global__ void k_height(TerrainView<ZT> T, int64_t n, const double *__restrict__ xy,
-                         double *__restrict__ h, uint8_t *__restrict__ is_nan,
-                         uint8_t *__restrict__ ood) {
+// one probe per point: a single bracket pair and one cell fetch serve both
+// getGroundHeight and heightIsNan; coordinates come from LDS when LDSC.
+template <class ZT, bool LDSC>
+__global__ __launch_bounds__(256) void k_height(TerrainView<ZT> T0, int64_t n,
+                                                const double2 *__restrict__ xy,
+                                                double *__restrict__ h,
+                                                uint8_t *__restrict__ is_nan,
+                                                uint8_t *__restrict__ ood) {
+  extern __shared__ double k1_smem[];
+  const TerrainView<ZT> T = LDSC ? stage_coords(T0, k1_smem) : T0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const double x = xy[2 * i], y = xy[2 * i + 1];
+    const double2 p = xy[i];
+    Probe<ZT> pr;
+    probe(T, p.x, p.y, pr);
     double v;
     bool near = false;
-    const bool ok = height_at(T, x, y, v, near);      // getGroundHeight
-    const int r = nan_at(T, x, y);                     // heightIsNan
+    const bool ok = probe_height(T, pr, p.x, p.y, v, near);  // getGroundHeight
+    const int r = probe_nan(pr);                              // heightIsNan
     if (h) h[i] = ok ? v : __builtin_nan("");
-    if (is_nan) is_nan[i] = r != 0 ? 1 : 0;            // UB (-1) reported as 1, like ood
+    if (is_nan) is_nan[i] = r != 0 ? 1 : 0;                   // UB (-1) reported as 1, like ood
     if (ood) ood[i] = (!ok || r < 0) ? 1 : 0;
   }
 }
@@ -92,19 +113,6 @@ __global__ void k_valid_states(TerrainView<ZT> T, int64_t n, const double *__res
 // ============================================================================
 // W = minimum waves per SIMD requested from the register allocator
 // (__launch_bounds__ 2nd argument): 1 -> up to 512 VGPR+AGPR, 2 -> 256, 4 -> 128.
-// LDSC: the coordinate vectors are staged in LDS (bracket fix-up and the
-// bilinear x1/x2/y1/y2 then never touch global memory)
-template <class ZT>
-__device__ __forceinline__ TerrainView<ZT> stage_coords(const TerrainView<ZT> &T0, double *smem) {
-  for (int i = threadIdx.x; i < T0.nx; i += blockDim.x) smem[i] = T0.x[i];
-  for (int i = threadIdx.x; i < T0.ny; i += blockDim.x) smem[T0.nx + i] = T0.y[i];
-  __syncthreads();
-  TerrainView<ZT> T = T0;
-  T.x = smem;
-  T.y = smem + T0.nx;
-  return T;
-}
-
 extern __shared__ double gbp_smem[];
 
 template <class ZT, bool ADAPTIVE, int W, bool LDSC>
@@ -332,38 +340,62 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
     TerrainView<ZT> T0, int n, const double *__restrict__ S, const double *__restrict__ A,
     const uint8_t *__restrict__ dir, int dir_all, uint8_t *__restrict__ valid,
     double *__restrict__ s_new, double *__restrict__ t_new, uint32_t *__restrict__ flags,
-    uint32_t *__restrict__ counts, unsigned int *__restrict__ head) {
+    uint32_t *__restrict__ counts, unsigned int *__restrict__ head, int sched, int chunk) {
   const TerrainView<ZT> T = LDSC ? stage_coords(T0, gbp_smem) : T0;
   const int lane = threadIdx.x & (WAVE - 1);
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
   Lane L;
   L.stage = ST_IDLE;
   bool exhausted = false;
+  // work source (wave-uniform): [cur, end) is the range this wave hands out
+  // to its idle lanes.  sched 1: a fixed per-wave slice, no atomics at all;
+  // sched 0 / 2: slices of `chunk` (0 = exactly the lanes that need one)
+  // dequeued from one device-scope counter (MI355X_MICROARCH.md 'dequeue').
+  unsigned int cur = 0, end = 0;
+  if (sched == 1) {
+    const unsigned int waves = gridDim.x * (blockDim.x / WAVE);
+    const unsigned int wid = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+    cur = (unsigned int)(((unsigned long long)n * wid) / waves);
+    end = (unsigned int)(((unsigned long long)n * (wid + 1)) / waves);
+  }
   for (;;) {
     const bool need = (L.stage == ST_IDLE) && !exhausted;
-    const unsigned long long m = __ballot(need);
-    if (m) {
-      const int leader = __ffsll((long long)m) - 1;
-      unsigned int base = 0;
-      if (lane == leader) base = atomicAdd(head, (unsigned int)__popcll(m));
-      base = __shfl(base, leader);
-      if (need) {
-        const unsigned int i = base + (unsigned int)__popcll(m & ((1ull << lane) - 1ull));
-        if (i < (unsigned int)n) {
-          L.idx = (int)i;
-#pragma unroll
-          for (int k = 0; k < 8; k++) L.s[k] = S[8 * (size_t)i + k];
-#pragma unroll
-          for (int k = 0; k < 10; k++) L.a[k] = A[10 * (size_t)i + k];
-          L.f = 0;
-          L.acc = Acc{0, 0, 0};
-          L.snew_kind = SN_NONE;
-          L.tnew_set = 0;
-          const int d = dir ? dir[i] : dir_all;
-          enter_stage(L, d == GBP_FORWARD ? ST_FWD_STANCE : ST_REV_FLIGHT);
-        } else {
-          exhausted = true;
+    unsigned long long m = __ballot(need);
+    while (m) {
+      if (cur >= end) {
+        unsigned int base = 0xFFFFFFFFu;
+        const unsigned int grab = chunk > 0 ? (unsigned int)chunk : (unsigned int)__popcll(m);
+        if (sched != 1) {
+          const int leader = __ffsll((long long)m) - 1;
+          if (lane == leader) base = atomicAdd(head, grab);
+          base = __shfl(base, leader);
         }
+        if (sched == 1 || base >= (unsigned int)n) {
+          if (need) exhausted = true;
+          break;
+        }
+        cur = base;
+        end = min(base + grab, (unsigned int)n);
       }
+      const unsigned int take = min(end - cur, (unsigned int)__popcll(m));
+      const unsigned int rank = (unsigned int)__popcll(m & lt_mask);
+      const bool mine = ((m >> lane) & 1ull) && rank < take;
+      if (mine) {
+        const unsigned int i = cur + rank;
+        L.idx = (int)i;
+#pragma unroll
+        for (int k = 0; k < 8; k++) L.s[k] = S[8 * (size_t)i + k];
+#pragma unroll
+        for (int k = 0; k < 10; k++) L.a[k] = A[10 * (size_t)i + k];
+        L.f = 0;
+        L.acc = Acc{0, 0, 0};
+        L.snew_kind = SN_NONE;
+        L.tnew_set = 0;
+        const int d = dir ? dir[i] : dir_all;
+        enter_stage(L, d == GBP_FORWARD ? ST_FWD_STANCE : ST_REV_FLIGHT);
+      }
+      cur += take;
+      m &= ~__ballot(mine);
     }
     if (!__any(L.stage != ST_IDLE)) break;
     if (L.stage != ST_IDLE) {
@@ -581,6 +613,8 @@ struct gbp_terrain {
   int64_t opt_grid_per_cu = 8;
   int64_t opt_waves = 2;            // register budget of the validate kernels (waves/SIMD)
   int64_t opt_lds_coords = 1;       // stage the coordinate vectors in LDS when they fit
+  int64_t opt_sched = 1;            // persistent work source: 0 atomic, 1 static, 2 chunked
+  int64_t opt_chunk = 0;            // dequeue granularity for sched 0/2 (0 = per need)
   unsigned int *d_head = nullptr;   // persistent-kernel work counter (zeroed per launch)
   hipStream_t host_stream = nullptr;
   void *ws = nullptr;               // grow-only device workspace
@@ -675,11 +709,13 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
                          s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn, flags + off, c);
     } else {
       // persistent: grid sized to residency; the work counter is zeroed per launch
-      const int64_t g = std::max<int64_t>(1, std::min<int64_t>(want, (m + block - 1) / block));
-      HIPCHK(hipMemsetAsync(t->d_head, 0, sizeof(unsigned int), st));
+      const int64_t resident = (int64_t)t->num_cus * std::max<int64_t>(1, W * 256 / block);
+      const int64_t g = std::max<int64_t>(
+          1, std::min<int64_t>(t->opt_sched == 1 ? resident : want, (m + block - 1) / block));
+      if (t->opt_sched != 1) HIPCHK(hipMemsetAsync(t->d_head, 0, sizeof(unsigned int), st));
       hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, LDSC>), dim3((unsigned)g), dim3(block),
                          lds, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
-                         flags + off, c, t->d_head);
+                         flags + off, c, t->d_head, (int)t->opt_sched, (int)t->opt_chunk);
     }
     HIPCHK(hipGetLastError());
   }
@@ -927,6 +963,14 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
     case GBP_OPT_LDS_COORDS:
       t->opt_lds_coords = value ? 1 : 0;
       return GBP_OK;
+    case GBP_OPT_SCHED:
+      if (value < 0 || value > 2) return GBP_E_INVALID_ARG;
+      t->opt_sched = value;
+      return GBP_OK;
+    case GBP_OPT_CHUNK:
+      if (value < 0 || value > 65536) return GBP_E_INVALID_ARG;
+      t->opt_chunk = value;
+      return GBP_OK;
     default:
       return GBP_E_INVALID_ARG;
   }
@@ -941,6 +985,8 @@ int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value) {
     case GBP_OPT_GRID_PER_CU: *value = t->opt_grid_per_cu; return GBP_OK;
     case GBP_OPT_WAVES: *value = t->opt_waves; return GBP_OK;
     case GBP_OPT_LDS_COORDS: *value = t->opt_lds_coords; return GBP_OK;
+    case GBP_OPT_SCHED: *value = t->opt_sched; return GBP_OK;
+    case GBP_OPT_CHUNK: *value = t->opt_chunk; return GBP_OK;
     default: return GBP_E_INVALID_ARG;
   }
 }
@@ -952,13 +998,28 @@ int gbp_height_batch_dev(gbp_terrain *t, int64_t n, const double *xy, double *he
   if (n < 0 || (n > 0 && !xy)) return GBP_E_INVALID_ARG;
   if (n == 0) return GBP_OK;
   DeviceGuard g(t->device);
-  const unsigned grid = grid_for(n, 256, t->num_cus * 16);
-  if (t->storage == GBP_STORAGE_F32)
-    hipLaunchKernelGGL(k_height<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                       view<float>(t), n, xy, height, is_nan, ood);
-  else
-    hipLaunchKernelGGL(k_height<double>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                       view<double>(t), n, xy, height, is_nan, ood);
+  if (((uintptr_t)xy) % 16) return GBP_E_INVALID_ARG;  // xy is read as double2
+  const size_t cbytes = sizeof(double) * (size_t)(t->nx + t->ny);
+  const bool lds = t->opt_lds_coords && cbytes <= 65536;
+  // enough workgroups to cover the LDS staging cost many times over
+  const unsigned grid = grid_for(n, 256, t->num_cus * 8);
+  const double2 *p = (const double2 *)xy;
+  hipStream_t st = (hipStream_t)stream;
+  if (t->storage == GBP_STORAGE_F32) {
+    if (lds)
+      hipLaunchKernelGGL((k_height<float, true>), dim3(grid), dim3(256), cbytes, st,
+                         view<float>(t), n, p, height, is_nan, ood);
+    else
+      hipLaunchKernelGGL((k_height<float, false>), dim3(grid), dim3(256), 0, st, view<float>(t),
+                         n, p, height, is_nan, ood);
+  } else {
+    if (lds)
+      hipLaunchKernelGGL((k_height<double, true>), dim3(grid), dim3(256), cbytes, st,
+                         view<double>(t), n, p, height, is_nan, ood);
+    else
+      hipLaunchKernelGGL((k_height<double, false>), dim3(grid), dim3(256), 0, st,
+                         view<double>(t), n, p, height, is_nan, ood);
+  }
   HIPCHK(hipGetLastError());
   return GBP_OK;
 }

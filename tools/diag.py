@@ -29,7 +29,9 @@ Ts = {k: gbp.Terrain.from_data(data, device=0, lib=v) for k, v in libs.items()}
 for T in Ts.values():
     T.set_option(L.OPT_WAVES, a.waves)
 s, act, d, _, _ = W.make_attempts(Ts["real"], 262144, W.CONFIG_SEEDS[3])
+st_states, _ = Ts["real"].sample_states(1 << 20, 3, 11, 0)
 times = {k: [] for k in Ts}
+vtimes = {k: [] for k in Ts}
 st = torch.cuda.current_stream()
 for r in range(a.rounds):
     for k, T in Ts.items():
@@ -42,8 +44,17 @@ for r in range(a.rounds):
             e1.record(st)
         torch.cuda.synchronize()
         times[k] += [e0.elapsed_time(e1) for e0, e1 in ev]
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(a.launches)]
+        for e0, e1 in ev:
+            e0.record(st)
+            T.valid_states(st_states, 1)
+            e1.record(st)
+        torch.cuda.synchronize()
+        vtimes[k] += [e0.elapsed_time(e1) for e0, e1 in ev]
         if r == 0:
             c = out.counts.to(torch.int64) & 0xFFFFFFFF
             print(f"{k:16s} valid={int(out.valid.sum())} V={int((c >> 16).sum())}", flush=True)
 for k, t in times.items():
-    print(f"{k:16s} median {np.median(t):.4f} ms  min {np.min(t):.4f} ms")
+    print(f"{k:16s} pairs median {np.median(t):.4f} ms  min {np.min(t):.4f} ms   "
+          f"valid_states(1M) median {np.median(vtimes[k]):.4f} ms")

@@ -29,6 +29,7 @@ def main():
     p.add_argument("--grid", default="4,8,16")
     p.add_argument("--block", default="256")
     p.add_argument("--lds", default="1")
+    p.add_argument("--sched", default="0", help="comma list of sched:chunk, e.g. 0:0,1:0,2:64")
     p.add_argument("--adaptive", action="store_true")
     p.add_argument("--out", default=None)
     a = p.parse_args()
@@ -42,13 +43,16 @@ def main():
                 grids = map(int, a.grid.split(",")) if k == "persistent" else [0]
                 for g in grids:
                     for lds in map(int, a.lds.split(",")):
-                        variants.append((k, w, b, g, lds))
+                        for sc in (a.sched.split(",") if k == "persistent" else ["0:0"]):
+                            variants.append((k, w, b, g, lds, sc if ":" in sc else sc + ":0"))
     times = {v: [] for v in variants}
     ref = None
     st = torch.cuda.current_stream()
     for r in range(a.rounds):
         for v in variants:
-            k, w, b, g, lds = v
+            k, w, b, g, lds, sc = v
+            T.set_option(L.OPT_SCHED, int(sc.split(":")[0]))
+            T.set_option(L.OPT_CHUNK, int(sc.split(":")[1]))
             T.set_option(L.OPT_KERNEL, L.KERNEL_PERSISTENT if k == "persistent" else L.KERNEL_DIRECT)
             T.set_option(L.OPT_WAVES, w)
             T.set_option(L.OPT_LDS_COORDS, lds)
@@ -74,12 +78,12 @@ def main():
     rows = []
     for v in variants:
         t = np.array(times[v])
-        rows.append({"kernel": v[0], "waves": v[1], "block": v[2], "grid_per_cu": v[3], "lds": v[4],
+        rows.append({"kernel": v[0], "waves": v[1], "block": v[2], "grid_per_cu": v[3], "lds": v[4], "sched": v[5],
                      "median_ms": float(np.median(t)), "min_ms": float(t.min()),
                      "attempts_per_s": a.batch / (np.median(t) * 1e-3)})
     rows.sort(key=lambda r: r["median_ms"])
     for r in rows:
-        print(f"{r['kernel']:10s} w={r['waves']} b={r['block']} g={r['grid_per_cu']:2d} lds={r['lds']} "
+        print(f"{r['kernel']:10s} w={r['waves']} b={r['block']} g={r['grid_per_cu']:2d} lds={r['lds']} sched={r['sched']:5s} "
               f"median {r['median_ms']:.4f} ms  min {r['min_ms']:.4f} ms  "
               f"{r['attempts_per_s'] / 1e6:.1f} M attempts/s")
     if a.out:
