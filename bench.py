@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 import global_body_planner_amd as gbp  # noqa: E402
 from global_body_planner_amd import _lib as L  # noqa: E402
 from global_body_planner_amd import terrain_data as td  # noqa: E402
+from global_body_planner_amd import sharding  # noqa: E402
 from global_body_planner_amd import workload as W  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md chip table)
@@ -108,7 +109,8 @@ def main():
     T.set_option(L.OPT_WAVES, args.waves)
     T.set_option(L.OPT_GRID_PER_CU, args.grid_per_cu)
     B = args.batch
-    s, a, d, _, tries = W.make_attempts(T, B, args.seed, index_base=rank * B)
+    base, _ = sharding.weak_shard(rank, B)   # rank r: attempts [r*B, (r+1)*B) of one global stream
+    s, a, d, _, tries = W.make_attempts(T, B, args.seed, index_base=base)
     res = T.validate_pairs(s, a, d, adaptive=args.adaptive)
     torch.cuda.synchronize()
     # per-launch algorithmic bytes from the kernel's own G/V counters
@@ -152,12 +154,8 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
 
-    tm = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    sums = torch.tensor([B, n_valid, n_ood, n_frag, gv], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-    elapsed = float(tm.item())
+    elapsed, sums = sharding.reduce_run(elapsed, [B, n_valid, n_ood, n_frag, gv], dev)
+    sums = torch.tensor(sums, dtype=torch.float64)
     tot_attempts = float(sums[0].item()) * args.steps
     value = tot_attempts / elapsed
 

@@ -1,0 +1,78 @@
+"""Multi-GPU plumbing: one process per GPU, torch.distributed (RCCL over xGMI
+for "nccl", gloo on CPU for tests).
+
+The extend/validity workload shards with NO data-path collective (SURVEY
+§8(e)): attempts are independent given the read-only terrain, which every
+rank holds in its own HBM, and the Philox-keyed inputs of rank r's slice are
+identical wherever they are generated.  Only the end-of-run timing (MAX) and
+counters (SUM) cross ranks.  The multi-restart configuration (config 4) adds
+one fixed-size all_gather of each rank's best-path record.
+"""
+import torch
+import torch.distributed as dist
+
+PATH_MAX = 256          # states per best-path record
+REC_HEADER = 4          # cost, length, yaw, n_states
+REC_SIZE = REC_HEADER + PATH_MAX * 8 + PATH_MAX * 10   # 4612 doubles = 36.9 KB
+
+
+def weak_shard(rank, per_rank):
+    """Rank r owns attempts [r * per_rank, (r + 1) * per_rank) of the global stream."""
+    return rank * per_rank, per_rank
+
+
+def strong_shard(rank, world, n_total):
+    lo = n_total * rank // world
+    hi = n_total * (rank + 1) // world
+    return lo, hi - lo
+
+
+def reduce_run(elapsed_s, counters, device):
+    """(max elapsed over ranks, per-counter sums) — the only cross-rank traffic."""
+    t = torch.tensor([float(elapsed_s)], dtype=torch.float64, device=device)
+    c = torch.tensor([float(v) for v in counters], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    return float(t.item()), [float(v) for v in c.tolist()]
+
+
+def pack_path(cost, length, yaw, states, actions, device="cpu"):
+    """Fixed-size best-path record (states [k, 8], actions [k-1, 10], k <= PATH_MAX)."""
+    rec = torch.full((REC_SIZE,), float("nan"), dtype=torch.float64, device=device)
+    k = 0 if states is None else int(len(states))
+    if k > PATH_MAX:
+        raise ValueError(f"path of {k} states exceeds PATH_MAX={PATH_MAX}")
+    rec[0], rec[1], rec[2], rec[3] = float(cost), float(length), float(yaw), float(k)
+    if k:
+        rec[REC_HEADER:REC_HEADER + 8 * k] = torch.as_tensor(states, dtype=torch.float64).reshape(-1)
+        if actions is not None and len(actions):
+            a = torch.as_tensor(actions, dtype=torch.float64).reshape(-1)
+            off = REC_HEADER + PATH_MAX * 8
+            rec[off:off + a.numel()] = a
+    return rec
+
+
+def unpack_path(rec):
+    k = int(rec[3].item()) if rec[3] == rec[3] else 0
+    states = rec[REC_HEADER:REC_HEADER + 8 * k].reshape(k, 8)
+    off = REC_HEADER + PATH_MAX * 8
+    actions = rec[off:off + 10 * max(k - 1, 0)].reshape(max(k - 1, 0), 10)
+    return {"cost": float(rec[0]), "length": float(rec[1]), "yaw": float(rec[2]),
+            "states": states, "actions": actions}
+
+
+def allgather_best_path(rec):
+    """all_gather every rank's record; every rank picks argmin(cost), ties to the
+    lowest rank.  NaN cost = no solution."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return 0, rec
+    world = dist.get_world_size()
+    out = [torch.empty_like(rec) for _ in range(world)]
+    dist.all_gather(out, rec)
+    best, best_cost = 0, float("inf")
+    for r, o in enumerate(out):
+        c = float(o[0].item())
+        if c == c and c < best_cost:
+            best, best_cost = r, c
+    return best, out[best]

@@ -1,0 +1,92 @@
+"""The C-ABI boundary: libgbp.so loads, exports every entry point that
+include/gbp.h declares, and validates arguments before touching a device
+(no compute here — the CPU container has no GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from global_body_planner_amd import _lib as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gbp.h")
+
+
+def declared():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(gbp_\w+)\s*\(", txt)) - {"gbp_terrain"})
+
+
+def test_library_exports_every_declared_symbol():
+    names = declared()
+    assert len(names) >= 25
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (gbp_\w+)", out))
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    assert sorted(L.EXPORTS) == names  # the Python binding covers the same surface
+
+
+def test_exports_are_plain_c():
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    # no mangled C++ symbol leaks through the boundary except HIP's runtime glue
+    assert "gbp_" not in "".join(l for l in out.splitlines() if "_Z" in l and "gbp" in l)
+
+
+def test_load_version_and_status_strings():
+    lib = L.load()
+    assert lib.gbp_version() == 100
+    assert lib.gbp_status_string(0) == b"ok"
+    assert lib.gbp_status_string(-6) == b"no HIP device"
+    assert lib.gbp_status_string(12345) == b"unknown status"
+
+
+def test_argument_validation_without_device():
+    lib = L.load()
+    h = ctypes.c_void_p()
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    x = np.arange(4.0)
+    z = np.zeros((4, 4))
+    assert lib.gbp_terrain_create(0, 1, 4, P(x), P(x), P(z), None, None, None, 0, ctypes.byref(h)) \
+        == -5  # GBP_E_SHAPE
+    bad = np.array([0.0, 2.0, 1.0, 3.0])
+    assert lib.gbp_terrain_create(0, 4, 4, P(bad), P(x), P(z), None, None, None, 0,
+                                  ctypes.byref(h)) == -1  # non-ascending coordinates
+    assert lib.gbp_terrain_create(0, 4, 4, P(x), P(x), None, None, None, None, 0,
+                                  ctypes.byref(h)) == -1  # no heights
+    assert lib.gbp_terrain_create(0, 4, 4, P(x), P(x), P(z), P(z), None, None, 0,
+                                  ctypes.byref(h)) == -1  # partial slope layers
+    assert lib.gbp_terrain_destroy(None) == -2
+    assert lib.gbp_validate_pairs_dev(None, 1, None, None, None, 0, 0, None, None, None, None,
+                                      None, None) == -2
+    assert lib.gbp_nearest_batch_dev(-1, None, 0, None, None, None, None) == -1
+    c = ctypes.c_int(7)
+    rc = lib.gbp_device_count(ctypes.byref(c))
+    import torch
+    if not torch.cuda.is_available():
+        assert rc == -6 and c.value == 0
+        assert lib.gbp_terrain_create(0, 4, 4, P(x), P(x), P(z), None, None, None, 0,
+                                      ctypes.byref(h)) == -6
+
+
+def test_product_has_no_cpu_fallback(monkeypatch, tmp_path):
+    """Without libgbp.so the engine raises instead of computing on the CPU."""
+    monkeypatch.setattr(L, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(L, "_lib", None)
+    with pytest.raises(FileNotFoundError):
+        L.load()
+
+
+def test_product_never_imports_the_oracle():
+    pkg = os.path.join(ROOT, "global_body_planner_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h", ".cpp")):
+                txt = open(os.path.join(dirpath, f)).read()
+                assert "import oracle" not in txt and "gbp_oracle" not in txt, f

@@ -298,3 +298,24 @@ def test_validate_pairs_schedulers(gpu, sched, chunk, lds):
         T.set_option(L.OPT_SCHED, 0)
         T.set_option(L.OPT_CHUNK, 0)
         T.set_option(L.OPT_LDS_COORDS, 1)
+
+
+def test_engine_matches_golden_vectors(gpu):
+    """The engine against the committed oracle vectors (tests/golden)."""
+    import os
+    from tests.helpers import same_f64
+    path = os.path.join(os.path.dirname(__file__), "golden", "oracle_vectors.npz")
+    g = np.load(path)
+    for name in ["slope-gridmap", "rough_terrain-gridmap", "synth-rough-256"]:
+        data, T, O = terrain_pair(name)
+        T.set_option(L.OPT_KERNEL, L.KERNEL_PERSISTENT)
+        p = name + "/"
+        h, isn, ood = T.height(torch.from_numpy(g[p + "xy"]))
+        assert np.all(same_f64(np_(h), g[p + "h"]))
+        assert np.array_equal(np_(isn), g[p + "is_nan"]) and np.array_equal(np_(ood), g[p + "ood"])
+        for ad in (0, 1):
+            res = T.validate_pairs(torch.from_numpy(g[p + "pair_s"]), torch.from_numpy(g[p + "pair_a"]),
+                                   torch.from_numpy(g[p + "pair_dir"]), adaptive=bool(ad))
+            out = (np_(res.valid), np_(res.s_new), np_(res.t_new), u32(res.flags), u32(res.counts))
+            ref = tuple(g[p + f"pair_{k}_{ad}"] for k in ("valid", "s_new", "t_new", "flags", "counts"))
+            assert_pairs_equal(out, ref, f"golden-gpu {name} ad{ad}")
