@@ -57,6 +57,10 @@ def parse():
                    help="bounded CPU-baseline sample (0 disables)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--out", default=None, help="also write the JSON line here")
+    p.add_argument("--ttfs-runs", type=int, default=3,
+                   help="batched RRT-Connect runs for time-to-first-solution (0 disables)")
+    p.add_argument("--plan-batch", type=int, default=256, help="targets per half-iteration")
+    p.add_argument("--plan-max-time", type=float, default=30.0, help="seconds per planner run")
     return p.parse_args()
 
 
@@ -80,6 +84,51 @@ def cpu_baseline(data, s, a, d, seconds):
             "sample": f"first {done} attempts of the same batch on the host CPU "
                       f"({dt:.1f} s, 1 thread, oracle/gbp_oracle.c linear-scan brackets)",
             "host_cpu": _cpu_model(), "host_threads_available": os.cpu_count()}
+
+
+def time_to_first_solution(data, args, rank, world, dev):
+    """Config 3: synth-rough-1024, start (1.0, 10.23) -> goal
+    (19.42, 10.23), z = 0.375 + ground, v = (1, 0, 0), batch-synchronous
+    RRT-Connect (include/gbp_planner.h).  With N ranks each run is config 4:
+    one independent tree pair per GPU (seed + rank), first solution = min over
+    ranks, best path shared by one all_gather of the fixed-size record."""
+    from global_body_planner_amd import planner
+    T = gbp.Terrain.from_data(data, device=dev.index)
+    L = data.x[-1]
+    xy = torch.tensor([[1.0, L / 2], [19.42 if L > 20 else L - 1.0, L / 2]], dtype=torch.float64,
+                      device=dev)
+    h = T.height(xy)[0]
+    h = h.cpu().numpy()
+    xy = xy.cpu().numpy()
+    start = planner.start_goal_state(h[0], xy[0, 0], xy[0, 1])
+    goal = planner.start_goal_state(h[1], xy[1, 0], xy[1, 1])
+    runs = []
+    best = None
+    for k in range(args.ttfs_runs):
+        out = planner.plan_rrt_connect(data, start, goal, batch=args.plan_batch,
+                                       max_time=args.plan_max_time,
+                                       seed=args.seed + 7919 * k + rank, device=dev.index)
+        ttf = out["time_to_first"] if out["found"] else float("inf")
+        t = torch.tensor([ttf], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        runs.append({"ttfs_s": float(t.item()), "rank0_iterations": out["iterations"],
+                     "rank0_extends": out["extends"], "rank0_attempts": out["attempts_checked"],
+                     "rank0_vertices": out["vertices_a"] + out["vertices_b"]})
+        if k == args.ttfs_runs - 1:
+            cost = out["path_length"] if out["found"] else float("nan")
+            rec = sharding.pack_path(cost, out["path_length"], 0.0,
+                                     out["states"] if out["found"] else None,
+                                     out["actions"] if out["found"] else None, device=dev)
+            who, rec = sharding.allgather_best_path(rec)
+            best = {"rank": who, "cost": sharding.unpack_path(rec)["cost"]}
+    solved = [r["ttfs_s"] for r in runs if np.isfinite(r["ttfs_s"])]
+    return {"value": float(np.median(solved)) if solved else None, "unit": "s",
+            "solved": f"{len(solved)}/{len(runs)}", "runs": runs, "best_path": best,
+            "batch": args.plan_batch, "max_time_s": args.plan_max_time,
+            "start": [float(v) for v in start[:3]], "goal": [float(v) for v in goal[:3]],
+            "definition": "wall seconds from buildRRTConnectBatched start to the first REACHED "
+                          "connect (min over ranks), median over runs"}
 
 
 def _cpu_model():
@@ -159,6 +208,8 @@ def main():
     tot_attempts = float(sums[0].item()) * args.steps
     value = tot_attempts / elapsed
 
+    ttfs = time_to_first_solution(data, args, rank, world, dev) if args.ttfs_runs > 0 else None
+
     if rank == 0:
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
         traffic = None
@@ -203,7 +254,7 @@ def main():
                 "kernel": "k_validate_persistent" if args.kernel == "persistent" else "k_validate_direct",
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },
-            "time_to_first_solution": None,
+            "time_to_first_solution": ttfs,
         }
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(data, s.cpu().numpy(), a.cpu().numpy(),

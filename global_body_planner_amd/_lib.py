@@ -35,7 +35,8 @@ EXPORTS = [
     "gbp_normal_batch_dev", "gbp_normal_batch_host",
     "gbp_valid_states_dev", "gbp_valid_states_host",
     "gbp_validate_pairs_dev", "gbp_validate_pairs_host",
-    "gbp_sample_states_dev", "gbp_sample_actions_dev",
+    "gbp_sample_states_dev", "gbp_sample_states_host", "gbp_sample_actions_dev",
+    "gbp_sample_actions_host",
     "gbp_extend_batch_dev", "gbp_extend_batch_host",
     "gbp_nearest_batch_dev", "gbp_nearest_batch_host",
 ]
@@ -90,6 +91,8 @@ def load(path=None):
         "gbp_validate_pairs_host": (I, [P, I64, P, P, P, I, I, P, P, P, P, P]),
         "gbp_sample_states_dev": (I, [P, I64, U64, U64, I64, I, I, P, P, P]),
         "gbp_sample_actions_dev": (I, [I64, P, U64, U64, I64, P, P]),
+        "gbp_sample_states_host": (I, [P, I64, U64, U64, I64, I, I, P, P]),
+        "gbp_sample_actions_host": (I, [P, I64, P, U64, U64, I64, P]),
         "gbp_extend_batch_dev": (I, [P, I64, P, P, P, I, I, U64, I64, P, P, P, P, P, P]),
         "gbp_extend_batch_host": (I, [P, I64, P, P, P, I, I, U64, I64, P, P, P, P, P]),
         "gbp_nearest_batch_dev": (I, [I64, P, I64, P, P, P, P]),

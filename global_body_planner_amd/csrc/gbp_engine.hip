@@ -1304,6 +1304,47 @@ int gbp_extend_batch_host(gbp_terrain *t, int64_t n, const double *s_near, const
   return GBP_OK;
 }
 
+int gbp_sample_states_host(gbp_terrain *t, int64_t n, uint64_t seed, uint64_t stream_id,
+                           int64_t index_base, int require_phase, int max_tries, double *states,
+                           int32_t *tries) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n <= 0) return n == 0 ? GBP_OK : GBP_E_INVALID_ARG;
+  if (!states) return GBP_E_INVALID_ARG;
+  DeviceGuard g(t->device);
+  hipStream_t st = t->host_stream;
+  int rc = ensure_ws(t, &t->ws, &t->ws_bytes, rnd(64 * n) + rnd(4 * n) + 1024);
+  if (rc) return rc;
+  Stage S{t, (char *)t->ws};
+  double *ds = S.take<double>(8 * n);
+  int32_t *dt = S.take<int32_t>(n);
+  rc = gbp_sample_states_dev(t, n, seed, stream_id, index_base, require_phase, max_tries, ds, dt,
+                             st);
+  if (rc) return rc;
+  D2H(states, ds, 64 * n);
+  if (tries) D2H(tries, dt, 4 * n);
+  HIPCHK(hipStreamSynchronize(st));
+  return GBP_OK;
+}
+
+int gbp_sample_actions_host(gbp_terrain *t, int64_t n, const double *normals, uint64_t seed,
+                            uint64_t stream_id, int64_t index_base, double *actions) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n <= 0) return n == 0 ? GBP_OK : GBP_E_INVALID_ARG;
+  if (!normals || !actions) return GBP_E_INVALID_ARG;
+  DeviceGuard g(t->device);
+  hipStream_t st = t->host_stream;
+  int rc = ensure_ws(t, &t->ws, &t->ws_bytes, rnd(24 * n) + rnd(80 * n) + 1024);
+  if (rc) return rc;
+  Stage S{t, (char *)t->ws};
+  double *dn = S.take<double>(3 * n), *da = S.take<double>(10 * n);
+  H2D(dn, normals, 24 * n);
+  rc = gbp_sample_actions_dev(n, dn, seed, stream_id, index_base, da, st);
+  if (rc) return rc;
+  D2H(actions, da, 80 * n);
+  HIPCHK(hipStreamSynchronize(st));
+  return GBP_OK;
+}
+
 int gbp_nearest_batch_host(int64_t n_query, const double *queries, int64_t n_vert,
                            const double *vertices, int32_t *index, double *dist) {
   if (n_query <= 0) return n_query == 0 ? GBP_OK : GBP_E_INVALID_ARG;

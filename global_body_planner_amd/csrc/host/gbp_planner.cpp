@@ -1,0 +1,1102 @@
+// gbp_planner.cpp — C++ host mirror of the reference planner over the C ABI.
+// Compiled without FMA contraction (-ffp-contract=off) so the host arithmetic
+// (propagation closed forms, isValidAction, distances, connect actions) is
+// the reference's.  Every terrain query / state check / NN scan / candidate
+// sampling goes through include/gbp.h (the HIP engine): there is no CPU
+// evaluation of the validity path here.
+#include "gbp_planner.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+
+namespace gbp_amd {
+
+EngineError::EngineError(int s, const std::string &what)
+    : std::runtime_error(what + ": " + gbp_status_string(s)), status(s) {}
+
+static void chk(int rc, const char *what) {
+  if (rc != GBP_OK) throw EngineError(rc, what);
+}
+
+static inline double std_min(double a, double b) { return (b < a) ? b : a; }
+static inline double std_max(double a, double b) { return (a < b) ? b : a; }
+
+// ============================================================================
+// FastTerrainMap
+// ============================================================================
+FastTerrainMap::FastTerrainMap(int device) : device_(device) {}
+
+FastTerrainMap::~FastTerrainMap() {
+  if (handle_) gbp_terrain_destroy(handle_);
+}
+
+void FastTerrainMap::loadData(int x_size, int y_size, std::vector<double> x_data,
+                              std::vector<double> y_data, std::vector<std::vector<double>> z_data,
+                              std::vector<std::vector<double>> dx_data,
+                              std::vector<std::vector<double>> dy_data,
+                              std::vector<std::vector<double>> dz_data) {
+  const size_t cells = (size_t)x_size * y_size;
+  std::vector<double> z(cells), dx, dy, dz;
+  const bool slopes = dx_data.size() == (size_t)x_size && dy_data.size() == (size_t)x_size &&
+                      dz_data.size() == (size_t)x_size;
+  if (slopes) {
+    dx.resize(cells);
+    dy.resize(cells);
+    dz.resize(cells);
+  }
+  for (int i = 0; i < x_size; i++)
+    for (int j = 0; j < y_size; j++) {
+      const size_t k = (size_t)i * y_size + j;
+      z[k] = z_data[i][j];
+      if (slopes) {
+        dx[k] = dx_data[i][j];
+        dy[k] = dy_data[i][j];
+        dz[k] = dz_data[i][j];
+      }
+    }
+  loadDataFlat(x_size, y_size, x_data.data(), y_data.data(), z.data(),
+               slopes ? dx.data() : nullptr, slopes ? dy.data() : nullptr,
+               slopes ? dz.data() : nullptr);
+}
+
+void FastTerrainMap::loadDataFlat(int x_size, int y_size, const double *x, const double *y,
+                                  const double *z, const double *dx, const double *dy,
+                                  const double *dz) {
+  gbp_terrain *h = nullptr;
+  chk(gbp_terrain_create(device_, x_size, y_size, x, y, z, dx, dy, dz, GBP_STORAGE_AUTO, &h),
+      "gbp_terrain_create");
+  if (handle_) gbp_terrain_destroy(handle_);
+  handle_ = h;
+  x_size_ = x_size;
+  y_size_ = y_size;
+  x_data_.assign(x, x + x_size);
+  y_data_.assign(y, y + y_size);
+}
+
+double FastTerrainMap::getGroundHeight(const double x, const double y) {
+  const double xy[2] = {x, y};
+  double h;
+  chk(gbp_height_batch_host(handle_, 1, xy, &h, nullptr, nullptr), "getGroundHeight");
+  return h;
+}
+
+bool FastTerrainMap::heightIsNan(const double x, const double y) {
+  const double xy[2] = {x, y};
+  uint8_t n;
+  chk(gbp_height_batch_host(handle_, 1, xy, nullptr, &n, nullptr), "heightIsNan");
+  return n != 0;
+}
+
+std::array<double, 3> FastTerrainMap::getSurfaceNormal(const double x, const double y) {
+  const double xy[2] = {x, y};
+  std::array<double, 3> n;
+  chk(gbp_normal_batch_host(handle_, 1, xy, n.data(), nullptr), "getSurfaceNormal");
+  return n;
+}
+
+void FastTerrainMap::getGroundHeightBatch(int64_t n, const double *xy, double *h,
+                                          uint8_t *is_nan) {
+  chk(gbp_height_batch_host(handle_, n, xy, h, is_nan, nullptr), "getGroundHeightBatch");
+}
+
+void FastTerrainMap::getSurfaceNormalBatch(int64_t n, const double *xy, double *normal) {
+  chk(gbp_normal_batch_host(handle_, n, xy, normal, nullptr), "getSurfaceNormalBatch");
+}
+
+// ============================================================================
+// planning_utils
+// ============================================================================
+namespace planning_utils {
+
+static uint64_t g_seed = 20251018;
+static int64_t g_action_draws = 0;
+
+void setRandomSeed(uint64_t seed) {
+  g_seed = seed;
+  g_action_draws = 0;
+}
+
+State interp(State q1, State q2, double x) {  // planning_utils.cpp:97-103
+  State q;
+  for (int d = 0; d < 8; d++) q[d] = (q2[d] - q1[d]) * x + q1[d];
+  return q;
+}
+
+double poseDistance(const State &q1, const State &q2) {  // :106-115
+  double sum = 0;
+  for (int i = 0; i < POSEDIM; i++) sum = sum + (q2[i] - q1[i]) * (q2[i] - q1[i]);
+  return std::sqrt(sum);
+}
+
+double stateDistance(const State &q1, const State &q2) {  // :116-127
+  double sum = 0;
+  for (int i = 0; i < 8; i++) sum = sum + 1.0 * (q2[i] - q1[i]) * (q2[i] - q1[i]);
+  return std::sqrt(sum);
+}
+
+double stateYawDistance(const State &q1, const State &q2) {  // planning_utils.h:133-145
+  const double yaw1 = std::atan2(q1[4], q1[3]);
+  const double yaw2 = std::atan2(q2[4], q2[3]);
+  const double yaw_min = std_min(yaw1, yaw2), yaw_max = std_max(yaw1, yaw2);
+  return std_min(yaw_max - yaw_min, yaw_min + 2 * MY_PI - yaw_max);
+}
+
+double stateDistance(const State &q1, const State &q2, bool f, double lw, double yw) {
+  if (f) return poseDistance(q1, q2) * lw + stateYawDistance(q1, q2) * yw;
+  return stateDistance(q1, q2);
+}
+
+bool isWithinBounds(State s1, State s2) { return stateDistance(s1, s2) <= GOAL_BOUNDS; }
+
+State applyStance(State s, Action a, double t) {  // :237-274
+  const double a_x_td = a[0], a_y_td = a[1], a_z_td = a[2];
+  const double a_x_to = a[3], a_y_to = a[4], a_z_to = a[5];
+  const double t_s = a[6], a_p_td = a[8], a_p_to = a[9];
+  State o;
+  o[0] = s[0] + s[3] * t + 0.5 * a_x_td * t * t + (a_x_to - a_x_td) * (t * t * t) / (6.0 * t_s);
+  o[1] = s[1] + s[4] * t + 0.5 * a_y_td * t * t + (a_y_to - a_y_td) * (t * t * t) / (6.0 * t_s);
+  o[2] = s[2] + s[5] * t + 0.5 * a_z_td * t * t + (a_z_to - a_z_td) * (t * t * t) / (6.0 * t_s);
+  o[3] = s[3] + a_x_td * t + (a_x_to - a_x_td) * t * t / (2.0 * t_s);
+  o[4] = s[4] + a_y_td * t + (a_y_to - a_y_td) * t * t / (2.0 * t_s);
+  o[5] = s[5] + a_z_td * t + (a_z_to - a_z_td) * t * t / (2.0 * t_s);
+  o[6] = s[6] + s[7] * t + 0.5 * a_p_td * t * t + (a_p_to - a_p_td) * (t * t * t) / (6.0 * t_s);
+  o[7] = s[7] + a_p_td * t + (a_p_to - a_p_td) * t * t / (2.0 * t_s);
+  return o;
+}
+
+State applyStance(State s, Action a) { return applyStance(s, a, a[6]); }
+
+State applyFlight(State s, double t_f) {  // :282-306
+  const double g = 9.81;
+  State o;
+  o[0] = s[0] + s[3] * t_f;
+  o[1] = s[1] + s[4] * t_f;
+  o[2] = s[2] + s[5] * t_f - 0.5 * g * t_f * t_f;
+  o[3] = s[3];
+  o[4] = s[4];
+  o[5] = s[5] - g * t_f;
+  o[6] = s[6] + s[7] * t_f;
+  o[7] = s[7];
+  return o;
+}
+
+State applyAction(State s, Action a) { return applyFlight(applyStance(s, a), a[7]); }
+
+State applyStanceReverse(State s, Action a, double t) {  // :324-367
+  const double a_x_td = a[0], a_y_td = a[1], a_z_td = a[2];
+  const double a_x_to = a[3], a_y_to = a[4], a_z_to = a[5];
+  const double t_s = a[6], a_p_td = a[8], a_p_to = a[9];
+  const double cx = s[3] - a_x_td * t_s - 0.5 * (a_x_to - a_x_td) * t_s;
+  const double cy = s[4] - a_y_td * t_s - 0.5 * (a_y_to - a_y_td) * t_s;
+  const double cz = s[5] - a_z_td * t_s - 0.5 * (a_z_to - a_z_td) * t_s;
+  const double cp = s[7] - a_p_td * t_s - 0.5 * (a_p_to - a_p_td) * t_s;
+  State o;
+  o[0] = s[0] - cx * (t_s - t) - 0.5 * a_x_td * (t_s * t_s - t * t) -
+         (a_x_to - a_x_td) * (t_s * t_s * t_s - t * t * t) / (6.0 * t_s);
+  o[1] = s[1] - cy * (t_s - t) - 0.5 * a_y_td * (t_s * t_s - t * t) -
+         (a_y_to - a_y_td) * (t_s * t_s * t_s - t * t * t) / (6.0 * t_s);
+  o[2] = s[2] - cz * (t_s - t) - 0.5 * a_z_td * (t_s * t_s - t * t) -
+         (a_z_to - a_z_td) * (t_s * t_s * t_s - t * t * t) / (6.0 * t_s);
+  o[3] = s[3] - a_x_td * (t_s - t) - (a_x_to - a_x_td) * (t_s * t_s - t * t) / (2.0 * t_s);
+  o[4] = s[4] - a_y_td * (t_s - t) - (a_y_to - a_y_td) * (t_s * t_s - t * t) / (2.0 * t_s);
+  o[5] = s[5] - a_z_td * (t_s - t) - (a_z_to - a_z_td) * (t_s * t_s - t * t) / (2.0 * t_s);
+  o[7] = s[7] - a_p_td * (t_s - t) - (a_p_to - a_p_td) * (t_s * t_s - t * t) / (2.0 * t_s);
+  o[6] = s[6] - cp * (t_s - t) - 0.5 * a_p_td * (t_s * t_s - t * t) -
+         (a_p_to - a_p_td) * (t_s * t_s * t_s - t * t * t) / (6.0 * t_s);
+  return o;
+}
+
+State applyStanceReverse(State s, Action a) { return applyStanceReverse(s, a, 0); }
+
+std::array<double, 3> rotate_grf(std::array<double, 3> n, std::array<double, 3> f) {  // :198-231
+  const double v0 = n[1] * 1.0 - n[2] * 0.0, v1 = n[2] * 0.0 - n[0] * 1.0,
+               v2 = n[0] * 0.0 - n[1] * 0.0;
+  const double s = std::sqrt(v0 * v0 + v1 * v1 + v2 * v2);
+  const double c = n[0] * 0.0 + n[1] * 0.0 + n[2] * 1.0;
+  if (s < 0.000001) return f;
+  const double K[3][3] = {{0, -v2, v1}, {v2, 0, -v0}, {-v1, v0, 0}};
+  std::array<double, 3> out;
+  for (int i = 0; i < 3; i++) {
+    double acc = 0;
+    for (int j = 0; j < 3; j++) {
+      const double kk = K[i][0] * K[0][j] + K[i][1] * K[1][j] + K[i][2] * K[2][j];
+      const double r = (i == j ? 1.0 : 0.0) + K[i][j] + kk * (1 - c) / (s * s);
+      acc = j == 0 ? r * f[0] : acc + r * f[j];
+    }
+    out[i] = acc;
+  }
+  return out;
+}
+
+bool isValidAction(Action a) {  // :519-556
+  if ((a[6] <= 0) || (a[7] < 0)) return false;
+  const double m = M_CONST, g = G_CONST, mu = MU;
+  const double f_x_td = m * a[0], f_y_td = m * a[1], f_z_td = m * (a[2] + g);
+  const double f_x_to = m * a[3], f_y_to = m * a[4], f_z_to = m * (a[5] + g);
+  if ((std::sqrt(f_x_td * f_x_td + f_y_td * f_y_td + f_z_td * f_z_td) >= F_MAX) ||
+      (std::sqrt(f_x_to * f_x_to + f_y_to * f_y_to + f_z_to * f_z_to) >= F_MAX) || (f_z_td < 0) ||
+      (f_z_to < 0) || (a[8] >= F_MAX) || (a[9] >= F_MAX))
+    return false;
+  if ((std::sqrt(f_x_td * f_x_td + f_y_td * f_y_td) >= mu * f_z_td) ||
+      (std::sqrt(f_x_to * f_x_to + f_y_to * f_y_to) >= mu * f_z_to))
+    return false;
+  return true;
+}
+
+bool isValidState(State s, FastTerrainMap &terrain, int phase) {
+  uint8_t v;
+  chk(gbp_valid_states_host(terrain.handle(), 1, s.data(), nullptr, phase, &v, nullptr, nullptr),
+      "isValidState");
+  return v != 0;
+}
+
+static bool pair1(State &s, Action &a, FastTerrainMap &terrain, State &s_new, double &t_new,
+                  int direction, bool adaptive) {
+  uint8_t v;
+  uint32_t f;
+  chk(gbp_validate_pairs_host(terrain.handle(), 1, s.data(), a.data(), nullptr, direction,
+                              adaptive ? 1 : 0, &v, s_new.data(), &t_new, &f, nullptr),
+      "isValidStateActionPair");
+  return v != 0;
+}
+
+bool isValidStateActionPair(State s, Action a, FastTerrainMap &terrain, State &s_new, double &t_new,
+                            bool adaptive) {
+  return pair1(s, a, terrain, s_new, t_new, FORWARD, adaptive);
+}
+bool isValidStateActionPair(State s, Action a, FastTerrainMap &terrain, State &s_new,
+                            double &t_new) {
+  return pair1(s, a, terrain, s_new, t_new, FORWARD, false);
+}
+bool isValidStateActionPair(State s, Action a, FastTerrainMap &terrain) {
+  State d{};
+  double t = 0;
+  return pair1(s, a, terrain, d, t, FORWARD, false);
+}
+bool isValidStateActionPairAdaptiveStepSize(State s, Action a, FastTerrainMap &terrain,
+                                            State &s_new, double &t_new) {
+  return pair1(s, a, terrain, s_new, t_new, FORWARD, true);
+}
+bool isValidStateActionPairReverse(State s, Action a, FastTerrainMap &terrain, State &s_new,
+                                   double &t_new, bool adaptive) {
+  return pair1(s, a, terrain, s_new, t_new, REVERSE, adaptive);
+}
+bool isValidStateActionPairReverse(State s, Action a, FastTerrainMap &terrain, State &s_new,
+                                   double &t_new) {
+  return pair1(s, a, terrain, s_new, t_new, REVERSE, false);
+}
+bool isValidStateActionPairReverse(State s, Action a, FastTerrainMap &terrain) {
+  State d{};
+  double t = 0;
+  return pair1(s, a, terrain, d, t, REVERSE, false);
+}
+bool isValidStateActionPairReverseAdaptiveStepSize(State s, Action a, FastTerrainMap &terrain,
+                                                   State &s_new, double &t_new) {
+  return pair1(s, a, terrain, s_new, t_new, REVERSE, true);
+}
+
+void isValidStateActionPairBatch(const std::vector<State> &s, const std::vector<Action> &a,
+                                 const std::vector<uint8_t> &direction, FastTerrainMap &terrain,
+                                 bool adaptive, std::vector<uint8_t> &valid,
+                                 std::vector<State> &s_new, std::vector<double> &t_new,
+                                 std::vector<uint32_t> *flags) {
+  const int64_t n = (int64_t)s.size();
+  valid.resize(n);
+  s_new.resize(n);
+  t_new.resize(n);
+  std::vector<uint32_t> f(n);
+  if (n == 0) return;
+  chk(gbp_validate_pairs_host(terrain.handle(), n, s[0].data(), a[0].data(),
+                              direction.empty() ? nullptr : direction.data(), FORWARD,
+                              adaptive ? 1 : 0, valid.data(), s_new[0].data(), t_new.data(),
+                              f.data(), nullptr),
+      "isValidStateActionPairBatch");
+  if (flags) flags->swap(f);
+}
+
+Action getRandomAction(std::array<double, 3> surf_norm) {
+  throw std::logic_error("getRandomAction(surf_norm) needs a terrain handle: use "
+                         "RRTClass::newConfig (engine-sampled candidates)");
+  (void)surf_norm;
+}
+
+void interpStateActionPair(State s, Action a, double t0, double dt, std::vector<State> &path,
+                           std::vector<double> &ts, std::vector<int> &phase) {  // :142-173
+  const double t_s = a[6], t_f = a[7];
+  for (double t = 0; t < t_s; t += dt) {
+    ts.push_back(t + t0);
+    path.push_back(applyStance(s, a, t));
+    phase.push_back(t_f == 0 ? CONNECT_STANCE : STANCE);
+  }
+  const State s_takeoff = applyStance(s, a);
+  for (double t = 0; t < t_f; t += dt) {
+    ts.push_back(t_s + t + t0);
+    path.push_back(applyFlight(s_takeoff, t));
+    phase.push_back(FLIGHT);
+  }
+  if (t_f > 0) {
+    ts.push_back(t0 + t_s + t_f);
+    path.push_back(applyFlight(s_takeoff, t_f));
+    phase.push_back(STANCE);
+  }
+}
+
+void getInterpPath(std::vector<State> states, std::vector<Action> actions, double dt,
+                   std::vector<State> &path, std::vector<double> &ts,
+                   std::vector<int> &phase) {  // :182-193
+  double t0 = 0;
+  for (size_t i = 0; i < actions.size(); i++) {
+    interpStateActionPair(states[i], actions[i], t0, dt, path, ts, phase);
+    t0 += (actions[i][6] + actions[i][7]);
+  }
+  ts.push_back(t0);
+  path.push_back(states.back());
+}
+
+}  // namespace planning_utils
+
+using namespace planning_utils;
+
+// ============================================================================
+// PlannerClass
+// ============================================================================
+PlannerClass::PlannerClass(int device) : device_(device) {}
+
+PlannerClass::~PlannerClass() {
+  if (d_vertices_) gbp_device_free(d_vertices_);
+  if (d_scratch_) gbp_device_free(d_scratch_);
+}
+
+PlannerClass::PlannerClass(const PlannerClass &o)
+    : device_(o.device_), vertices_(o.vertices_), actions_(o.actions_), parent_(o.parent_),
+      successors_(o.successors_), g_(o.g_), y_(o.y_), cost_add_yaw_flag_(o.cost_add_yaw_flag_),
+      cost_add_yaw_length_weight_(o.cost_add_yaw_length_weight_),
+      cost_add_yaw_yaw_weight_(o.cost_add_yaw_yaw_weight_), seed_(o.seed_),
+      stream_id_(o.stream_id_), draws_(o.draws_) {}
+
+PlannerClass &PlannerClass::operator=(const PlannerClass &o) {
+  if (this == &o) return *this;
+  if (d_vertices_) gbp_device_free(d_vertices_);
+  if (d_scratch_) gbp_device_free(d_scratch_);
+  d_vertices_ = nullptr;
+  d_scratch_ = nullptr;
+  d_capacity_ = d_count_ = d_scratch_cap_ = 0;
+  device_ = o.device_;
+  vertices_ = o.vertices_;
+  actions_ = o.actions_;
+  parent_ = o.parent_;
+  successors_ = o.successors_;
+  g_ = o.g_;
+  y_ = o.y_;
+  cost_add_yaw_flag_ = o.cost_add_yaw_flag_;
+  cost_add_yaw_length_weight_ = o.cost_add_yaw_length_weight_;
+  cost_add_yaw_yaw_weight_ = o.cost_add_yaw_yaw_weight_;
+  seed_ = o.seed_;
+  stream_id_ = o.stream_id_;
+  draws_ = o.draws_;
+  return *this;
+}
+
+void PlannerClass::init(State s, bool f, double lw, double yw) {  // graph_class.cpp:141-152
+  vertices_.clear();
+  actions_.clear();
+  parent_.clear();
+  successors_.clear();
+  g_.clear();
+  y_.clear();
+  d_count_ = 0;
+  addVertex(0, s);
+  g_[0] = 0;
+  y_[0] = 0;
+  cost_add_yaw_flag_ = f;
+  cost_add_yaw_length_weight_ = lw;
+  cost_add_yaw_yaw_weight_ = yw;
+}
+
+void PlannerClass::addVertex(int idx, State s) {
+  if (idx >= (int)vertices_.size()) {
+    vertices_.resize(idx + 1);
+    actions_.resize(idx + 1);
+    parent_.resize(idx + 1, -1);
+    successors_.resize(idx + 1);
+    g_.resize(idx + 1, 0);
+    y_.resize(idx + 1, 0);
+  }
+  vertices_[idx] = s;
+  if (idx < d_count_) d_count_ = idx;  // re-upload from here
+}
+
+void PlannerClass::addEdge(int idx1, int idx2) {  // graph_class.cpp:36-42
+  parent_[idx2] = idx1;
+  successors_[idx1].push_back(idx2);
+  g_[idx2] = g_[idx1] + poseDistance(vertices_[idx1], vertices_[idx2]);
+  y_[idx2] = y_[idx1] + stateYawDistance(vertices_[idx1], vertices_[idx2]);
+}
+
+int PlannerClass::getPredecessor(int idx) const { return parent_[idx]; }
+
+void PlannerClass::updateGYValue(int idx, double g_val, double y_val) {  // :131-138
+  g_[idx] = g_val;
+  y_[idx] = y_val;
+  for (int succ : successors_[idx])
+    updateGYValue(succ, g_[idx] + poseDistance(vertices_[idx], vertices_[succ]),
+                  y_[idx] + stateYawDistance(vertices_[idx], vertices_[succ]));
+}
+
+void PlannerClass::sync_device() {
+  const int64_t V = (int64_t)vertices_.size();
+  if (V > d_capacity_) {
+    int64_t cap = std::max<int64_t>(1024, d_capacity_);
+    while (cap < V) cap *= 2;
+    void *p = nullptr;
+    chk(gbp_device_alloc(device_, (size_t)cap * sizeof(State), &p), "tree alloc");
+    if (d_vertices_) gbp_device_free(d_vertices_);
+    d_vertices_ = (double *)p;
+    d_capacity_ = cap;
+    d_count_ = 0;
+  }
+  if (d_count_ < V) {
+    chk(gbp_memcpy_h2d(d_vertices_ + 8 * d_count_, vertices_[d_count_].data(),
+                       (size_t)(V - d_count_) * sizeof(State), nullptr),
+        "tree upload");
+    chk(gbp_stream_synchronize(nullptr), "tree upload");  // pageable source
+    d_count_ = V;
+  }
+}
+
+State PlannerClass::randomState(FastTerrainMap &terrain) {  // planner_class.cpp:38-76
+  State q;
+  int32_t tries;
+  chk(gbp_sample_states_host(terrain.handle(), 1, seed_, stream_id_, draws_++, -1, 1, q.data(),
+                             &tries),
+      "randomState");
+  return q;
+}
+
+std::vector<State> PlannerClass::randomStateBatch(FastTerrainMap &terrain, int n) {
+  std::vector<State> q(n);
+  if (n <= 0) return q;
+  std::vector<int32_t> tries(n);
+  chk(gbp_sample_states_host(terrain.handle(), n, seed_, stream_id_, draws_, -1, 1, q[0].data(),
+                             tries.data()),
+      "randomStateBatch");
+  draws_ += n;
+  return q;
+}
+
+std::vector<int> PlannerClass::getNearestNeighborBatch(const std::vector<State> &q) {
+  std::vector<int> idx(q.size(), 0);
+  if (q.empty()) return idx;
+  sync_device();
+  const int64_t nq = (int64_t)q.size();
+  if (nq > d_scratch_cap_) {
+    int64_t cap = std::max<int64_t>(256, d_scratch_cap_);
+    while (cap < nq) cap *= 2;
+    void *p = nullptr;
+    chk(gbp_device_alloc(device_, (size_t)cap * (sizeof(State) + sizeof(int32_t)), &p),
+        "nn scratch alloc");
+    if (d_scratch_) gbp_device_free(d_scratch_);
+    d_scratch_ = p;
+    d_scratch_cap_ = cap;
+  }
+  double *dq = (double *)d_scratch_;
+  int32_t *di = (int32_t *)(dq + 8 * d_scratch_cap_);
+  std::vector<int32_t> out(nq);
+  chk(gbp_memcpy_h2d(dq, q[0].data(), (size_t)nq * sizeof(State), nullptr), "nn upload");
+  chk(gbp_nearest_batch_dev(nq, dq, (int64_t)vertices_.size(), d_vertices_, di, nullptr, nullptr),
+      "getNearestNeighbor");
+  chk(gbp_memcpy_d2h(out.data(), di, (size_t)nq * sizeof(int32_t), nullptr), "nn download");
+  chk(gbp_stream_synchronize(nullptr), "nn sync");
+  for (int64_t i = 0; i < nq; i++) idx[i] = out[i];
+  return idx;
+}
+
+int PlannerClass::getNearestNeighbor(State q) { return getNearestNeighborBatch({q})[0]; }
+
+std::vector<int> PlannerClass::neighborhoodDist(State q, double dist) {  // :173-182
+  std::vector<int> out;
+  for (int i = 0; i < (int)vertices_.size(); i++) {
+    const double d = stateDistance(q, vertices_[i]);
+    if (d <= dist && d > 0) out.push_back(i);
+  }
+  return out;
+}
+
+std::vector<int> PlannerClass::neighborhoodN(State q, int N) {  // :151-171
+  std::vector<std::pair<double, int>> d;
+  for (int i = 0; i < (int)vertices_.size(); i++)
+    d.push_back({stateDistance(q, vertices_[i], cost_add_yaw_flag_, cost_add_yaw_length_weight_,
+                               cost_add_yaw_yaw_weight_),
+                 i});
+  std::sort(d.begin(), d.end());
+  std::vector<int> out;
+  for (int i = 0; i < std::min<int>(N, (int)d.size()); i++) out.push_back(d[i].second);
+  return out;
+}
+
+// ============================================================================
+// RRTClass
+// ============================================================================
+bool RRTClass::newConfig(State s, State s_near, State &s_new, Action &a_new, FastTerrainMap &terrain,
+                         int direction) {  // rrt.cpp:20-70 on the engine (6 candidates, one launch)
+  int32_t result, chosen;
+  uint32_t counts;
+  State sn = s_new;
+  Action an = a_new;
+  const uint8_t dir = (uint8_t)direction;
+  chk(gbp_extend_batch_host(terrain.handle(), 1, s_near.data(), s.data(), &dir, direction,
+                            state_action_pair_check_adaptive_step_size_flag_ ? 1 : 0, seed_,
+                            extend_counter_++, &result, &chosen, sn.data(), an.data(), &counts),
+      "newConfig");
+  if (result == GBP_TRAPPED) return false;
+  s_new = sn;
+  a_new = an;
+  return true;
+}
+
+int RRTClass::extend(PlannerClass &T, State s, FastTerrainMap &terrain, int direction) {
+  const int s_near_index = T.getNearestNeighbor(s);  // rrt.cpp:78-102
+  const State s_near = T.getVertex(s_near_index);
+  State s_new{};
+  Action a_new{};
+  if (newConfig(s, s_near, s_new, a_new, terrain, direction)) {
+    const int s_new_index = T.getNumVertices();
+    T.addVertex(s_new_index, s_new);
+    T.addEdge(s_near_index, s_new_index);
+    T.addAction(s_new_index, a_new);
+    T.updateGYValue(s_new_index, T.getGValue(s_near_index) + poseDistance(s_near, s_new),
+                    T.getYValue(s_near_index) + stateYawDistance(s_near, s_new));
+    return isWithinBounds(s_new, s) ? GBP_PLANNER_REACHED : GBP_PLANNER_ADVANCED;
+  }
+  return GBP_PLANNER_TRAPPED;
+}
+
+std::vector<int> RRTClass::pathFromStart(PlannerClass &T, int s) {  // rrt.cpp:107-118
+  std::vector<int> path{s};
+  while (s != 0) {
+    s = T.getPredecessor(s);
+    path.push_back(s);
+  }
+  std::reverse(path.begin(), path.end());
+  return path;
+}
+
+std::vector<State> RRTClass::getStateSequence(PlannerClass &T, std::vector<int> path) {
+  std::vector<State> out;
+  for (int i : path) out.push_back(T.getVertex(i));
+  return out;
+}
+
+std::vector<Action> RRTClass::getActionSequence(PlannerClass &T, std::vector<int> path) {
+  std::vector<Action> out;
+  for (size_t i = 1; i < path.size(); ++i) out.push_back(T.getAction(path[i]));
+  return out;
+}
+
+void RRTClass::getStatistics(double &plan_time, int &success_var, int &vertices_generated,
+                             double &time_to_first_solve, std::vector<double> &cost_vector,
+                             std::vector<double> &cost_vector_times, double &path_duration) {
+  plan_time = elapsed_total.count();
+  success_var = success_;
+  vertices_generated = num_vertices;
+  time_to_first_solve = elapsed_to_first.count();
+  cost_vector = cost_vector_;
+  cost_vector_times = cost_vector_times_;
+  path_duration = path_duration_;
+}
+
+// ============================================================================
+// RRTConnectClass
+// ============================================================================
+static Action connect_action(const State &s_start, const State &s_goal, double t_s) {
+  // rrt_connect.cpp:53-63 (cubic-Hermite stance action, t_f = 0)
+  const double x_td = s_start[0], y_td = s_start[1], z_td = s_start[2];
+  const double dx_td = s_start[3], dy_td = s_start[4], dz_td = s_start[5];
+  const double x_to = s_goal[0], y_to = s_goal[1], z_to = s_goal[2];
+  const double dx_to = s_goal[3], dy_to = s_goal[4], dz_to = s_goal[5];
+  const double p_td = s_start[6], dp_td = s_start[7], p_to = s_goal[6], dp_to = s_goal[7];
+  Action a;
+  a[0] = -(2.0 * (3.0 * x_td - 3.0 * x_to + 2.0 * dx_td * t_s + dx_to * t_s)) / (t_s * t_s);
+  a[1] = -(2.0 * (3.0 * y_td - 3.0 * y_to + 2.0 * dy_td * t_s + dy_to * t_s)) / (t_s * t_s);
+  a[2] = -(2.0 * (3.0 * z_td - 3.0 * z_to + 2.0 * dz_td * t_s + dz_to * t_s)) / (t_s * t_s);
+  a[3] = (2.0 * (3.0 * x_td - 3.0 * x_to + dx_td * t_s + 2.0 * dx_to * t_s)) / (t_s * t_s);
+  a[4] = (2.0 * (3.0 * y_td - 3.0 * y_to + dy_td * t_s + 2.0 * dy_to * t_s)) / (t_s * t_s);
+  a[5] = (2.0 * (3.0 * z_td - 3.0 * z_to + dz_td * t_s + 2.0 * dz_to * t_s)) / (t_s * t_s);
+  a[6] = t_s;
+  a[7] = 0;
+  a[8] = -(2.0 * (3.0 * p_td - 3.0 * p_to + 2.0 * dp_td * t_s + dp_to * t_s)) / (t_s * t_s);
+  a[9] = (2.0 * (3.0 * p_td - 3.0 * p_to + dp_td * t_s + 2.0 * dp_to * t_s)) / (t_s * t_s);
+  return a;
+}
+
+int RRTConnectClass::attemptConnect(State s_existing, State s, double t_s, State &s_new,
+                                    Action &a_new, FastTerrainMap &terrain, int direction) {
+  std::vector<int> r;
+  std::vector<State> sn{s_new};
+  std::vector<Action> an{a_new};
+  attemptConnectBatch({s_existing}, {s}, {t_s}, terrain, direction, r, sn, an, nullptr);
+  if (r[0] != GBP_PLANNER_TRAPPED || sn[0] != s_new) {
+    s_new = sn[0];
+    a_new = an[0];
+  }
+  return r[0];
+}
+
+int RRTConnectClass::attemptConnect(State s_existing, State s, State &s_new, Action &a_new,
+                                    FastTerrainMap &terrain, int direction) {
+  const double t_s = poseDistance(s, s_existing) / V_NOM;  // rrt_connect.cpp:89
+  return attemptConnect(s_existing, s, t_s, s_new, a_new, terrain, direction);
+}
+
+// The recursive attemptConnect (rrt_connect.cpp:20-84) for many independent
+// connections, run as lock-step rounds: round d evaluates recursion depth d of
+// every still-open connection in ONE engine launch.  Per connection:
+//   REACHED  if its depth-0 pair check is valid,
+//   ADVANCED if a deeper level's check is valid,
+//   TRAPPED  if t_s <= KINEMATICS_RES, isValidAction fails, or (engine
+//            convention) the failed check left t_new / s_new
+//            unassigned — the reference would recurse on uninitialised values.
+void RRTConnectClass::attemptConnectBatch(const std::vector<State> &s_existing,
+                                          const std::vector<State> &s0, std::vector<double> t_s,
+                                          FastTerrainMap &terrain, int direction,
+                                          std::vector<int> &result, std::vector<State> &s_new,
+                                          std::vector<Action> &a_new, BatchStats *stats) {
+  const size_t n = s_existing.size();
+  result.assign(n, GBP_PLANNER_TRAPPED);
+  s_new.resize(n);
+  a_new.resize(n);
+  std::vector<State> s = s0;
+  std::vector<int> open(n);
+  std::iota(open.begin(), open.end(), 0);
+  for (int depth = 0; !open.empty() && depth < 64; depth++) {
+    std::vector<int> chk_idx;
+    std::vector<State> cs;
+    std::vector<Action> ca;
+    for (int k : open) {
+      if (t_s[k] <= KINEMATICS_RES) continue;  // TRAPPED (:23-24)
+      const State &start = (direction == FORWARD) ? s_existing[k] : s[k];
+      const State &goal = (direction == FORWARD) ? s[k] : s_existing[k];
+      const Action a = connect_action(start, goal, t_s[k]);
+      a_new[k] = a;
+      if (!isValidAction(a)) continue;  // TRAPPED (:66, :83)
+      chk_idx.push_back(k);
+      cs.push_back(direction == FORWARD ? start : goal);
+      ca.push_back(a);
+    }
+    open.clear();
+    if (chk_idx.empty()) break;
+    std::vector<uint8_t> valid;
+    std::vector<State> sn(chk_idx.size());
+    std::vector<double> tn(chk_idx.size(), 0.0);
+    std::vector<uint32_t> fl(chk_idx.size());
+    for (size_t j = 0; j < chk_idx.size(); j++) sn[j] = s_new[chk_idx[j]];
+    const int64_t m = (int64_t)chk_idx.size();
+    chk(gbp_validate_pairs_host(terrain.handle(), m, cs[0].data(), ca[0].data(), nullptr,
+                                direction, state_action_pair_check_adaptive_step_size_flag_ ? 1 : 0,
+                                nullptr, sn[0].data(), tn.data(), fl.data(), nullptr),
+        "attemptConnect");
+    if (stats) stats->attempts_checked += m;
+    for (size_t j = 0; j < chk_idx.size(); j++) {
+      const int k = chk_idx[j];
+      if (fl[j] & GBP_F_SNEW_SET) s_new[k] = sn[j];
+      if (fl[j] & GBP_F_VALID) {
+        result[k] = depth == 0 ? GBP_PLANNER_REACHED : GBP_PLANNER_ADVANCED;
+      } else if ((fl[j] & GBP_F_TNEW_SET) && (fl[j] & GBP_F_SNEW_SET)) {
+        s[k] = sn[j];  // :77 recurse toward the returned state with t_s = t_new
+        t_s[k] = tn[j];
+        open.push_back(k);
+      }
+    }
+  }
+}
+
+int RRTConnectClass::connect(PlannerClass &T, State s, FastTerrainMap &terrain, int direction) {
+  const int s_near_index = T.getNearestNeighbor(s);  // rrt_connect.cpp:98-120
+  const State s_near = T.getVertex(s_near_index);
+  State s_new{};
+  Action a_new{};
+  const int result = attemptConnect(s_near, s, s_new, a_new, terrain, direction);
+  if (result != GBP_PLANNER_TRAPPED) {
+    const int s_new_index = T.getNumVertices();
+    T.addVertex(s_new_index, s_new);
+    T.addEdge(s_near_index, s_new_index);
+    T.addAction(s_new_index, a_new);
+    T.updateGYValue(s_new_index, T.getGValue(s_near_index) + poseDistance(s_near, s_new),
+                    T.getYValue(s_near_index) + stateYawDistance(s_near, s_new));
+  }
+  return result;
+}
+
+std::vector<Action> RRTConnectClass::getActionSequenceReverse(PlannerClass &T,
+                                                              std::vector<int> path) {
+  std::vector<Action> out;
+  for (size_t i = 0; i + 1 < path.size(); ++i) out.push_back(T.getAction(path[i]));
+  return out;
+}
+
+void RRTConnectClass::postProcessPath(std::vector<State> &state_sequence,
+                                      std::vector<Action> &action_sequence,
+                                      FastTerrainMap &terrain) {  // rrt_connect.cpp:139-227
+  State s = state_sequence.front();
+  const State s_goal = state_sequence.back();
+  State dummy{};
+  Action a_new{};
+  std::vector<State> new_states{s};
+  std::vector<Action> new_actions;
+  path_length_ = 0;
+  path_yaw_ = 0;
+  path_cost_ = 0;
+  while (s != s_goal) {
+    std::vector<State> sc = state_sequence;
+    std::vector<Action> ac = action_sequence;
+    State s_next = sc.back();
+    Action a_next = ac.back();
+    State old_state{};
+    Action old_action{};
+    while ((attemptConnect(s, s_next, dummy, a_new, terrain, FORWARD) != GBP_PLANNER_REACHED) &&
+           (s != s_next)) {
+      old_state = s_next;
+      old_action = a_next;
+      sc.pop_back();
+      ac.pop_back();
+      s_next = sc.back();
+      a_next = ac.back();
+    }
+    if (s != s_next) {
+      new_states.push_back(s_next);
+      new_actions.push_back(a_new);
+      const double dl = poseDistance(s, s_next), dy = stateYawDistance(s, s_next);
+      path_length_ += dl;
+      path_yaw_ += dy;
+      path_cost_ += cost_add_yaw_flag_ ? dl * cost_add_yaw_length_weight_ + dy * cost_add_yaw_yaw_weight_
+                                       : dl;
+      s = s_next;
+    } else {
+      // the reference adds to path_cost_ but not path_length_ here (:210-215)
+      new_states.push_back(old_state);
+      new_actions.push_back(old_action);
+      const double dl = poseDistance(s, old_state), dy = stateYawDistance(s, old_state);
+      path_cost_ += cost_add_yaw_flag_ ? dl * cost_add_yaw_length_weight_ + dy * cost_add_yaw_yaw_weight_
+                                       : dl;
+      s = old_state;
+    }
+  }
+  state_sequence = new_states;
+  action_sequence = new_actions;
+}
+
+void RRTConnectClass::runRRTConnect(PlannerClass &Ta, PlannerClass &Tb,
+                                    FastTerrainMap &terrain) {  // rrt_connect.cpp:230-314
+  const auto t_start = std::chrono::high_resolution_clock::now();
+  while (true) {
+    std::chrono::duration<double> el = std::chrono::high_resolution_clock::now() - t_start;
+    if (el.count() >= anytime_horizon) {
+      anytime_horizon = anytime_horizon * horizon_expansion_factor;
+      return;
+    }
+    State s_rand = Ta.randomState(terrain);
+    if (isValidState(s_rand, terrain, STANCE)) {
+      if (extend(Ta, s_rand, terrain, FORWARD) != GBP_PLANNER_TRAPPED) {
+        const State s_new = Ta.getVertex(Ta.getNumVertices() - 1);
+        if (connect(Tb, s_new, terrain, REVERSE) == GBP_PLANNER_REACHED) {
+          goal_found = true;
+          elapsed_to_first = std::chrono::high_resolution_clock::now() - t_start;
+          break;
+        }
+      }
+    }
+    s_rand = Tb.randomState(terrain);
+    if (isValidState(s_rand, terrain, STANCE)) {
+      if (extend(Tb, s_rand, terrain, REVERSE) != GBP_PLANNER_TRAPPED) {
+        const State s_new = Tb.getVertex(Tb.getNumVertices() - 1);
+        if (connect(Ta, s_new, terrain, FORWARD) == GBP_PLANNER_REACHED) {
+          goal_found = true;
+          elapsed_to_first = std::chrono::high_resolution_clock::now() - t_start;
+          break;
+        }
+      }
+    }
+  }
+  path_length_ = Ta.getGValue(Ta.getNumVertices() - 1) + Tb.getGValue(Tb.getNumVertices() - 1);
+  path_yaw_ = Ta.getYValue(Ta.getNumVertices() - 1) + Tb.getYValue(Tb.getNumVertices() - 1);
+  path_cost_ = cost_add_yaw_flag_ ? path_length_ * cost_add_yaw_length_weight_ +
+                                        path_yaw_ * cost_add_yaw_yaw_weight_
+                                  : path_length_;
+}
+
+void RRTConnectClass::buildRRTConnect(FastTerrainMap &terrain, State s_start, State s_goal,
+                                      std::vector<State> &state_sequence,
+                                      std::vector<Action> &action_sequence,
+                                      double max_time_opt) {  // rrt_connect.cpp:323-467
+  const auto t_start = std::chrono::high_resolution_clock::now();
+  success_ = 0;
+  cost_vector_.clear();
+  cost_vector_times_.clear();
+  wall_to_first_ = -1;
+  goal_found = false;
+  PlannerClass Ta(terrain.device()), Tb(terrain.device()), Ta_best(terrain.device()),
+      Tb_best(terrain.device());
+  anytime_horizon = poseDistance(s_start, s_goal) / planning_rate_estimate;
+  num_vertices = 0;
+  double cost_so_far = INFTY;
+  int restart = 0;
+  std::chrono::duration<double> el{0};
+  while (true) {
+    Ta = PlannerClass(terrain.device());
+    Tb = PlannerClass(terrain.device());
+    Ta.setStream(seed_, 1000 + 2 * restart);
+    Tb.setStream(seed_, 1001 + 2 * restart);
+    restart++;
+    Ta.init(s_start, cost_add_yaw_flag_, cost_add_yaw_length_weight_, cost_add_yaw_yaw_weight_);
+    Tb.init(s_goal, cost_add_yaw_flag_, cost_add_yaw_length_weight_, cost_add_yaw_yaw_weight_);
+    goal_found = false;
+    runRRTConnect(Ta, Tb, terrain);
+    num_vertices += Ta.getNumVertices() + Tb.getNumVertices();
+    el = std::chrono::high_resolution_clock::now() - t_start;
+    if (el.count() >= max_time_solve) {
+      elapsed_total = el;
+      elapsed_to_first = el;
+      success_ = 0;
+      return;
+    }
+    if (goal_found) {
+      if (wall_to_first_ < 0) wall_to_first_ = el.count();
+      std::vector<int> path_a = pathFromStart(Ta, Ta.getNumVertices() - 1);
+      std::vector<int> path_b = pathFromStart(Tb, Tb.getNumVertices() - 1);
+      std::reverse(path_b.begin(), path_b.end());
+      std::vector<Action> action_sequence_b = getActionSequenceReverse(Tb, path_b);
+      path_b.erase(path_b.begin());
+      state_sequence = getStateSequence(Ta, path_a);
+      std::vector<State> sb = getStateSequence(Tb, path_b);
+      state_sequence.insert(state_sequence.end(), sb.begin(), sb.end());
+      action_sequence = getActionSequence(Ta, path_a);
+      action_sequence.insert(action_sequence.end(), action_sequence_b.begin(),
+                             action_sequence_b.end());
+      postProcessPath(state_sequence, action_sequence, terrain);
+      if (path_cost_ < cost_so_far) {
+        cost_so_far = path_cost_;
+        Ta_best = Ta;
+        Tb_best = Tb;
+        el = std::chrono::high_resolution_clock::now() - t_start;
+        cost_vector_.push_back(cost_so_far);
+        cost_vector_times_.push_back(el.count());
+      }
+    }
+    if (goal_found && el.count() >= max_time_opt) break;
+  }
+  Ta = Ta_best;
+  Tb = Tb_best;
+  {
+    std::vector<int> path_a = pathFromStart(Ta, Ta.getNumVertices() - 1);
+    std::vector<int> path_b = pathFromStart(Tb, Tb.getNumVertices() - 1);
+    std::reverse(path_b.begin(), path_b.end());
+    std::vector<Action> action_sequence_b = getActionSequenceReverse(Tb, path_b);
+    path_b.erase(path_b.begin());
+    state_sequence = getStateSequence(Ta, path_a);
+    std::vector<State> sb = getStateSequence(Tb, path_b);
+    state_sequence.insert(state_sequence.end(), sb.begin(), sb.end());
+    action_sequence = getActionSequence(Ta, path_a);
+    action_sequence.insert(action_sequence.end(), action_sequence_b.begin(),
+                           action_sequence_b.end());
+  }
+  postProcessPath(state_sequence, action_sequence, terrain);
+  elapsed_total = std::chrono::high_resolution_clock::now() - t_start;
+  if (elapsed_total.count() <= 5.0) success_ = 1;
+  path_duration_ = 0.0;
+  for (const Action &a : action_sequence) path_duration_ += (a[6] + a[7]);
+}
+
+// one batch-synchronous half-iteration: extend T toward `batch` targets, then
+// connect every new vertex to O (direction of the connect = opposite of dir)
+int RRTConnectClass::halfIterationBatched(PlannerClass &T, PlannerClass &O, FastTerrainMap &terrain,
+                                          int dir, int batch, int &meet_t, int &meet_o,
+                                          BatchStats *stats) {
+  // targets: randomState + isValidState(STANCE) (rrt_connect.cpp:249-254)
+  std::vector<State> cand = T.randomStateBatch(terrain, batch);
+  std::vector<uint8_t> ok(batch);
+  chk(gbp_valid_states_host(terrain.handle(), batch, cand[0].data(), nullptr, STANCE, ok.data(),
+                            nullptr, nullptr),
+      "target validity");
+  std::vector<State> targets;
+  for (int i = 0; i < batch; i++)
+    if (ok[i]) targets.push_back(cand[i]);
+  if (stats) stats->targets += (int64_t)targets.size();
+  if (targets.empty()) return 0;
+  const int64_t n = (int64_t)targets.size();
+  // extend (rrt.cpp:77-102), all targets against the current tree snapshot
+  std::vector<int> nn = T.getNearestNeighborBatch(targets);
+  std::vector<State> s_near(n), s_new(n);
+  std::vector<Action> a_new(n);
+  for (int64_t i = 0; i < n; i++) s_near[i] = T.getVertex(nn[i]);
+  std::vector<int32_t> res(n), chosen(n);
+  chk(gbp_extend_batch_host(terrain.handle(), n, s_near[0].data(), targets[0].data(), nullptr, dir,
+                            state_action_pair_check_adaptive_step_size_flag_ ? 1 : 0, seed_,
+                            extend_counter_, res.data(), chosen.data(), s_new[0].data(),
+                            a_new[0].data(), nullptr),
+      "extend batch");
+  extend_counter_ += n;
+  if (stats) {
+    stats->extends += n;
+    stats->attempts_checked += 6 * n;
+  }
+  std::vector<int> added;
+  for (int64_t i = 0; i < n; i++) {
+    if (res[i] == GBP_TRAPPED) continue;
+    const int idx = T.getNumVertices();
+    T.addVertex(idx, s_new[i]);
+    T.addEdge(nn[i], idx);
+    T.addAction(idx, a_new[i]);
+    T.updateGYValue(idx, T.getGValue(nn[i]) + poseDistance(s_near[i], s_new[i]),
+                    T.getYValue(nn[i]) + stateYawDistance(s_near[i], s_new[i]));
+    added.push_back(idx);
+  }
+  if (added.empty()) return 0;
+  // connect every new vertex to the other tree (rrt_connect.cpp:98-120)
+  std::vector<State> q;
+  for (int idx : added) q.push_back(T.getVertex(idx));
+  std::vector<int> nno = O.getNearestNeighborBatch(q);
+  std::vector<State> s_ex(q.size());
+  std::vector<double> t_s(q.size());
+  for (size_t k = 0; k < q.size(); k++) {
+    s_ex[k] = O.getVertex(nno[k]);
+    t_s[k] = poseDistance(q[k], s_ex[k]) / V_NOM;
+  }
+  const int cdir = (dir == FORWARD) ? REVERSE : FORWARD;
+  std::vector<int> cres;
+  std::vector<State> csn(q.size(), State{});
+  std::vector<Action> can(q.size(), Action{});
+  attemptConnectBatch(s_ex, q, t_s, terrain, cdir, cres, csn, can, stats);
+  if (stats) stats->connects += (int64_t)q.size();
+  int found = 0;
+  for (size_t k = 0; k < q.size(); k++) {
+    if (cres[k] == GBP_PLANNER_TRAPPED) continue;
+    const int idx = O.getNumVertices();
+    O.addVertex(idx, csn[k]);
+    O.addEdge(nno[k], idx);
+    O.addAction(idx, can[k]);
+    O.updateGYValue(idx, O.getGValue(nno[k]) + poseDistance(s_ex[k], csn[k]),
+                    O.getYValue(nno[k]) + stateYawDistance(s_ex[k], csn[k]));
+    if (cres[k] == GBP_PLANNER_REACHED && !found) {
+      found = 1;
+      meet_t = added[k];
+      meet_o = idx;
+    }
+  }
+  return found;
+}
+
+bool RRTConnectClass::buildRRTConnectBatched(FastTerrainMap &terrain, State s_start, State s_goal,
+                                             int batch, double max_time,
+                                             std::vector<State> &state_sequence,
+                                             std::vector<Action> &action_sequence,
+                                             BatchStats *stats) {
+  const auto t_start = std::chrono::high_resolution_clock::now();
+  goal_found = false;
+  wall_to_first_ = -1;
+  PlannerClass Ta(terrain.device()), Tb(terrain.device());
+  Ta.setStream(seed_, 101);
+  Tb.setStream(seed_, 102);
+  Ta.init(s_start, cost_add_yaw_flag_, cost_add_yaw_length_weight_, cost_add_yaw_yaw_weight_);
+  Tb.init(s_goal, cost_add_yaw_flag_, cost_add_yaw_length_weight_, cost_add_yaw_yaw_weight_);
+  BatchStats local;
+  BatchStats &st = stats ? *stats : local;
+  int ia = -1, ib = -1;
+  while (true) {
+    std::chrono::duration<double> el = std::chrono::high_resolution_clock::now() - t_start;
+    if (el.count() >= max_time) break;
+    st.iterations++;
+    if (halfIterationBatched(Ta, Tb, terrain, FORWARD, batch, ia, ib, &st)) {
+      goal_found = true;
+      break;
+    }
+    if (halfIterationBatched(Tb, Ta, terrain, REVERSE, batch, ib, ia, &st)) {
+      goal_found = true;
+      break;
+    }
+  }
+  elapsed_to_first = std::chrono::high_resolution_clock::now() - t_start;
+  st.vertices_a = Ta.getNumVertices();
+  st.vertices_b = Tb.getNumVertices();
+  num_vertices = Ta.getNumVertices() + Tb.getNumVertices();
+  if (!goal_found) return false;
+  wall_to_first_ = elapsed_to_first.count();
+  // rrt_connect.cpp:386-401 with the meeting vertices (ia in Ta, ib in Tb)
+  std::vector<int> path_a = pathFromStart(Ta, ia);
+  std::vector<int> path_b = pathFromStart(Tb, ib);
+  std::reverse(path_b.begin(), path_b.end());
+  std::vector<Action> action_sequence_b = getActionSequenceReverse(Tb, path_b);
+  path_b.erase(path_b.begin());
+  state_sequence = getStateSequence(Ta, path_a);
+  std::vector<State> sb = getStateSequence(Tb, path_b);
+  state_sequence.insert(state_sequence.end(), sb.begin(), sb.end());
+  action_sequence = getActionSequence(Ta, path_a);
+  action_sequence.insert(action_sequence.end(), action_sequence_b.begin(), action_sequence_b.end());
+  path_length_ = Ta.getGValue(ia) + Tb.getGValue(ib);
+  path_yaw_ = Ta.getYValue(ia) + Tb.getYValue(ib);
+  path_cost_ = path_length_;
+  path_duration_ = 0;
+  for (const Action &a : action_sequence) path_duration_ += a[6] + a[7];
+  return true;
+}
+
+}  // namespace gbp_amd
+
+// ============================================================================
+// flat C entry point
+// ============================================================================
+extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r,
+                                    double *path_states, double *path_actions, int capacity) {
+  using namespace gbp_amd;
+  if (!p || !r || p->batch < 1) return GBP_E_INVALID_ARG;
+  try {
+    FastTerrainMap terrain(p->device);
+    terrain.loadDataFlat(p->nx, p->ny, p->x, p->y, p->z, p->dx, p->dy, p->dz);
+    RRTConnectClass planner;
+    planner.setSeed(p->seed);
+    State s0, s1;
+    std::copy(p->start, p->start + 8, s0.begin());
+    std::copy(p->goal, p->goal + 8, s1.begin());
+    std::vector<State> states;
+    std::vector<Action> actions;
+    BatchStats st;
+    const auto t0 = std::chrono::high_resolution_clock::now();
+    const bool found =
+        planner.buildRRTConnectBatched(terrain, s0, s1, p->batch, p->max_time, states, actions, &st);
+    double ttf = planner.wallTimeToFirst();
+    if (found && p->post_process) planner.postProcessPath(states, actions, terrain);
+    const std::chrono::duration<double> tot = std::chrono::high_resolution_clock::now() - t0;
+    memset(r, 0, sizeof(*r));
+    r->found = found ? 1 : 0;
+    r->time_to_first = found ? ttf : -1.0;
+    r->total_time = tot.count();
+    r->iterations = st.iterations;
+    r->targets = st.targets;
+    r->extends = st.extends;
+    r->attempts_checked = st.attempts_checked;
+    r->connects = st.connects;
+    r->vertices_a = st.vertices_a;
+    r->vertices_b = st.vertices_b;
+    r->n_states = found ? (int)states.size() : 0;
+    if (found) {
+      double len = 0;
+      for (size_t i = 1; i < states.size(); i++) len += planning_utils::poseDistance(states[i - 1], states[i]);
+      r->path_length = len;
+      r->path_cost = len;
+      double dur = 0;
+      for (const Action &a : actions) dur += a[6] + a[7];
+      r->path_duration = dur;
+      for (int i = 0; i < std::min<int>(capacity, (int)states.size()); i++) {
+        if (path_states) std::copy(states[i].begin(), states[i].end(), path_states + 8 * i);
+        if (path_actions && i < (int)actions.size())
+          std::copy(actions[i].begin(), actions[i].end(), path_actions + 10 * i);
+      }
+    }
+    return GBP_OK;
+  } catch (const EngineError &e) {
+    return e.status;
+  } catch (...) {
+    return GBP_E_INVALID_ARG;
+  }
+}

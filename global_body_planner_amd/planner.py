@@ -1,0 +1,94 @@
+"""Python binding of the batched RRT-Connect planner (lib/libgbp_planner.so).
+
+The planner itself is C++ (csrc/host/gbp_planner.cpp, declared in
+include/gbp_planner.h): a host mirror of the reference's FastTerrainMap /
+planning_utils / PlannerClass / RRTConnectClass whose every validity check,
+terrain query, nearest-neighbour scan and candidate draw runs on the HIP engine.
+This module only marshals `gbp_plan_rrt_connect` (the flat C entry) — the call
+the reference's GlobalBodyPlanner::callPlanner makes
+(global_body_planner.cpp:89-131 -> RRTConnectClass::buildRRTConnect).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib
+
+PLANNER_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libgbp_planner.so")
+
+_D = ctypes.c_double
+_P = ctypes.c_void_p
+
+
+class PlanParams(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("nx", ctypes.c_int), ("ny", ctypes.c_int),
+                ("x", _P), ("y", _P), ("z", _P), ("dx", _P), ("dy", _P), ("dz", _P),
+                ("start", _D * 8), ("goal", _D * 8), ("batch", ctypes.c_int),
+                ("max_time", _D), ("seed", ctypes.c_uint64), ("post_process", ctypes.c_int)]
+
+
+class PlanResult(ctypes.Structure):
+    _fields_ = [("found", ctypes.c_int), ("time_to_first", _D), ("total_time", _D),
+                ("iterations", ctypes.c_int64), ("targets", ctypes.c_int64),
+                ("extends", ctypes.c_int64), ("attempts_checked", ctypes.c_int64),
+                ("connects", ctypes.c_int64), ("vertices_a", ctypes.c_int64),
+                ("vertices_b", ctypes.c_int64), ("n_states", ctypes.c_int),
+                ("path_length", _D), ("path_cost", _D), ("path_duration", _D)]
+
+
+_planner = None
+
+
+def load():
+    """Load libgbp_planner.so (raises if it is not built: no fallback)."""
+    global _planner
+    if _planner is None:
+        _lib.load()   # libgbp.so first (the planner links it by rpath)
+        if not os.path.exists(PLANNER_PATH):
+            raise FileNotFoundError(f"{PLANNER_PATH} is missing: run __graft_entry__.build()")
+        L = ctypes.CDLL(PLANNER_PATH)
+        L.gbp_plan_rrt_connect.restype = ctypes.c_int
+        L.gbp_plan_rrt_connect.argtypes = [ctypes.POINTER(PlanParams), ctypes.POINTER(PlanResult),
+                                           _P, _P, ctypes.c_int]
+        _planner = L
+    return _planner
+
+
+def start_goal_state(height, x, y):
+    """GlobalBodyPlanner::setStartAndGoalStates (global_body_planner.cpp:219-264):
+    z = 0.375 + ground height, v = (1, 0, 0), pitch and pitch rate 0."""
+    return np.array([x, y, 0.375 + height, 1.0, 0.0, 0.0, 0.0, 0.0], dtype=np.float64)
+
+
+def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018,
+                     post_process=False, device=0, capacity=4096):
+    """Plan start -> goal on terrain `data` (terrain_data.TerrainData).
+
+    Returns a dict with the C result fields plus `states` [n][8] and
+    `actions` [n-1][10] (the found path; empty if none)."""
+    L = load()
+    x = np.ascontiguousarray(data.x, dtype=np.float64)
+    y = np.ascontiguousarray(data.y, dtype=np.float64)
+    z = np.ascontiguousarray(data.z, dtype=np.float64)
+    slopes = [None if getattr(data, k, None) is None else
+              np.ascontiguousarray(getattr(data, k), dtype=np.float64) for k in ("dx", "dy", "dz")]
+    p = PlanParams()
+    p.device, p.nx, p.ny = device, x.size, y.size
+    p.x, p.y, p.z = x.ctypes.data, y.ctypes.data, z.ctypes.data
+    p.dx, p.dy, p.dz = [None if s is None else s.ctypes.data for s in slopes]
+    p.start[:] = [float(v) for v in start]
+    p.goal[:] = [float(v) for v in goal]
+    p.batch, p.max_time, p.seed, p.post_process = int(batch), float(max_time), int(seed), int(post_process)
+    r = PlanResult()
+    states = np.zeros((capacity, 8))
+    actions = np.zeros((capacity, 10))
+    rc = L.gbp_plan_rrt_connect(ctypes.byref(p), ctypes.byref(r), states.ctypes.data,
+                                actions.ctypes.data, capacity)
+    if rc != 0:
+        raise _lib.GbpError(rc, "gbp_plan_rrt_connect")
+    out = {k: getattr(r, k) for k, _ in PlanResult._fields_}
+    n = r.n_states
+    out["states"] = states[:n].copy()
+    out["actions"] = actions[:max(n - 1, 0)].copy()
+    return out

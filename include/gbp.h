@@ -186,11 +186,16 @@ int gbp_validate_pairs_host(gbp_terrain *t, int64_t n, const double *s, const do
 int gbp_sample_states_dev(gbp_terrain *t, int64_t n, uint64_t seed, uint64_t stream_id,
                           int64_t index_base, int require_phase, int max_tries,
                           double *states, int32_t *tries, gbp_stream stream);
+int gbp_sample_states_host(gbp_terrain *t, int64_t n, uint64_t seed, uint64_t stream_id,
+                           int64_t index_base, int require_phase, int max_tries,
+                           double *states, int32_t *tries);
 /* getRandomAction(surf_norm) (planning_utils.cpp:392-442) with rotate_grf
  * (:198-231): actions[n][10] from normals[n][3]; draw (stream_id, index_base+i). */
 int gbp_sample_actions_dev(int64_t n, const double *normals, uint64_t seed,
                            uint64_t stream_id, int64_t index_base, double *actions,
                            gbp_stream stream);
+int gbp_sample_actions_host(gbp_terrain *t, int64_t n, const double *normals, uint64_t seed,
+                            uint64_t stream_id, int64_t index_base, double *actions);
 
 /* ---- batched extend (RRTClass::newConfig + the acceptance half of
  *      RRTClass::extend, rrt.cpp:20-102) --------------------------------------

@@ -1,0 +1,402 @@
+// gbp_planner.h — C++ host mirror of the reference planner API over the C ABI.
+//
+// Same class / function names, argument meanings and return conventions as
+// the reference (include/global_body_planner/{fast_terrain_map,planning_utils,
+// planner_class,rrt,rrt_connect}.h), with every state-validity evaluation,
+// terrain query, nearest-neighbour scan and candidate sampling executed by the
+// HIP engine (include/gbp.h).  Namespace gbp_amd; include gbp_planner_compat.h
+// for the reference's global names (the drop-in under the ROS node, see
+// INTEGRATION.md).  No ROS / grid_map / Eigen dependency.
+//
+// Extensions beyond the reference surface (all batch-synchronous, B = 1
+// reproduces the sequential algorithm on the engine's counter-based RNG):
+//   planning_utils::isValidStateActionPairBatch, FastTerrainMap::*Batch,
+//   PlannerClass::getNearestNeighborBatch, RRTConnectClass::buildRRTConnectBatched.
+#pragma once
+
+#include <array>
+#include <chrono>
+#include <stdexcept>
+#include <type_traits>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "gbp.h"
+
+namespace gbp_amd {
+
+namespace planning_utils {
+// include/global_body_planner/planning_utils.h:21-66
+const double H_MAX = 0.4;
+const double H_MIN = 0.075;
+const double V_MAX = 2.0;
+const double V_NOM = 0.75;
+const double P_MAX = 1.0;
+const double DP_MAX = 3.0;
+const double ANG_ACC_MAX = 7.0;
+const double ROBOT_L = 0.3;
+const double ROBOT_W = 0.3;
+const double ROBOT_H = 0.05;
+const double M_CONST = 13;
+const double G_CONST = 9.81;
+const double F_MAX = 637;
+const double MU = 1.0;
+const double T_S_MIN = 0.3;
+const double T_S_MAX = 0.3;
+const double T_F_MIN = 0.0;
+const double T_F_MAX = 0.5;
+const double KINEMATICS_RES = 0.05;
+const double BACKUP_TIME = 0.2;
+const double BACKUP_RATIO = 0.5;
+const int NUM_GEN_STATES = 6;
+const double GOAL_BOUNDS = 0.5;
+const int FLIGHT = 0;
+const int STANCE = 1;
+const int CONNECT_STANCE = 2;
+const int FORWARD = 0;
+const int REVERSE = 1;
+const int POSEDIM = 3;
+const int STATEDIM = 8;
+const int ACTIONDIM = 10;
+typedef std::array<double, STATEDIM> State;
+typedef std::array<double, ACTIONDIM> Action;
+typedef std::pair<State, Action> StateActionPair;
+const double INFTY = 1.7976931348623157e308;
+const double MY_PI = 3.14159;
+}  // namespace planning_utils
+
+using planning_utils::Action;
+using planning_utils::State;
+
+#define GBP_PLANNER_TRAPPED 0
+#define GBP_PLANNER_ADVANCED 1
+#define GBP_PLANNER_REACHED 2
+
+// Thrown only by constructors / loaders when the engine reports an error
+// (the reference's hot path has no error channel; the C ABI returns codes).
+struct EngineError : std::runtime_error {
+  int status;
+  EngineError(int s, const std::string &what);
+};
+
+// ---- FastTerrainMap (fast_terrain_map.h:14-120) ------------------------------
+class FastTerrainMap {
+ public:
+  explicit FastTerrainMap(int device = 0);
+  ~FastTerrainMap();
+  FastTerrainMap(const FastTerrainMap &) = delete;
+  FastTerrainMap &operator=(const FastTerrainMap &) = delete;
+
+  // fast_terrain_map.cpp:10-28 (x-major nested vectors, as the reference)
+  void loadData(int x_size, int y_size, std::vector<double> x_data, std::vector<double> y_data,
+                std::vector<std::vector<double>> z_data, std::vector<std::vector<double>> dx_data,
+                std::vector<std::vector<double>> dy_data, std::vector<std::vector<double>> dz_data);
+  // flat x-major variant (no nested-vector copies); dx/dy/dz may be null
+  void loadDataFlat(int x_size, int y_size, const double *x, const double *y, const double *z,
+                    const double *dx, const double *dy, const double *dz);
+  // fast_terrain_map.cpp:31-91 for any map type exposing the grid_map calls
+  // used there (getSize, getPosition, at, exists); see INTEGRATION.md
+  template <class GridMap>
+  void loadDataFromGridMap(const GridMap &map);
+
+  double getGroundHeight(const double x, const double y);               // :94-132
+  bool heightIsNan(const double x, const double y);                     // :135-157
+  std::array<double, 3> getSurfaceNormal(const double x, const double y);  // :160-213
+  const std::vector<double> &getXData() const { return x_data_; }       // :216-218
+  const std::vector<double> &getYData() const { return y_data_; }       // :221-223
+
+  // batched queries: xy[n][2]
+  void getGroundHeightBatch(int64_t n, const double *xy, double *h, uint8_t *is_nan);
+  void getSurfaceNormalBatch(int64_t n, const double *xy, double *normal);
+
+  gbp_terrain *handle() const { return handle_; }
+  int device() const { return device_; }
+
+ private:
+  int device_;
+  gbp_terrain *handle_ = nullptr;
+  int x_size_ = 0, y_size_ = 0;
+  std::vector<double> x_data_, y_data_;
+};
+
+namespace planning_utils {
+// planning_utils.cpp:97-132, planning_utils.h:133-155
+State interp(State q1, State q2, double x);
+double poseDistance(const State &q1, const State &q2);
+double stateDistance(const State &q1, const State &q2);
+double stateYawDistance(const State &q1, const State &q2);
+double stateDistance(const State &q1, const State &q2, bool cost_add_yaw_flag,
+                     double cost_add_yaw_length_weight, double cost_add_yaw_yaw_weight);
+bool isWithinBounds(State s1, State s2);
+// planning_utils.cpp:237-370 (host arithmetic, identical expressions)
+State applyStance(State s, Action a, double t);
+State applyStance(State s, Action a);
+State applyFlight(State s, double t_f);
+State applyAction(State s, Action a);
+State applyStanceReverse(State s, Action a, double t);
+State applyStanceReverse(State s, Action a);
+std::array<double, 3> rotate_grf(std::array<double, 3> surface_norm, std::array<double, 3> grf);
+// planning_utils.cpp:519-556 (host arithmetic)
+bool isValidAction(Action a);
+// planning_utils.cpp:562-635 — evaluated by the engine
+bool isValidState(State s, FastTerrainMap &terrain, int phase);
+// planning_utils.cpp:645-881 — evaluated by the engine; s_new / t_new are
+// written only where the reference writes them
+bool isValidStateActionPair(State s, Action a, FastTerrainMap &terrain, State &s_new, double &t_new,
+                            bool state_action_pair_check_adaptive_step_size_flag);
+bool isValidStateActionPair(State s, Action a, FastTerrainMap &terrain, State &s_new, double &t_new);
+bool isValidStateActionPair(State s, Action a, FastTerrainMap &terrain);
+bool isValidStateActionPairAdaptiveStepSize(State s, Action a, FastTerrainMap &terrain,
+                                            State &s_new, double &t_new);
+bool isValidStateActionPairReverse(State s, Action a, FastTerrainMap &terrain, State &s_new,
+                                   double &t_new, bool state_action_pair_check_adaptive_step_size_flag);
+bool isValidStateActionPairReverse(State s, Action a, FastTerrainMap &terrain, State &s_new,
+                                   double &t_new);
+bool isValidStateActionPairReverse(State s, Action a, FastTerrainMap &terrain);
+bool isValidStateActionPairReverseAdaptiveStepSize(State s, Action a, FastTerrainMap &terrain,
+                                                   State &s_new, double &t_new);
+// the hot path, batched: one engine launch for n pairs (direction per pair)
+void isValidStateActionPairBatch(const std::vector<State> &s, const std::vector<Action> &a,
+                                 const std::vector<uint8_t> &direction, FastTerrainMap &terrain,
+                                 bool adaptive, std::vector<uint8_t> &valid,
+                                 std::vector<State> &s_new, std::vector<double> &t_new,
+                                 std::vector<uint32_t> *flags = nullptr);
+// planning_utils.cpp:392-442 on the engine's counter-based stream
+// (the reference's rand() / clock-seeded engines are not reproducible)
+Action getRandomAction(std::array<double, 3> surf_norm);
+void setRandomSeed(uint64_t seed);
+// planning_utils.cpp:142-193
+void interpStateActionPair(State s, Action a, double t0, double dt,
+                           std::vector<State> &interp_path, std::vector<double> &interp_t,
+                           std::vector<int> &interp_phase);
+void getInterpPath(std::vector<State> state_sequence, std::vector<Action> action_sequence,
+                   double dt, std::vector<State> &interp_path, std::vector<double> &interp_t,
+                   std::vector<int> &interp_phase);
+}  // namespace planning_utils
+
+// ---- GraphClass + PlannerClass (graph_class.h, planner_class.h) --------------
+// Vertices live in host vectors AND in a device mirror (flat double[V][8]) that
+// the nearest-neighbour kernel scans.
+class PlannerClass {
+ public:
+  explicit PlannerClass(int device = 0);
+  ~PlannerClass();
+  PlannerClass(const PlannerClass &o);
+  PlannerClass &operator=(const PlannerClass &o);
+
+  void init(State s, bool cost_add_yaw_flag = false, double cost_add_yaw_length_weight = 1,
+            double cost_add_yaw_yaw_weight = 1);                           // graph_class.cpp:141-152
+  void addVertex(int index, State s);                                      // :28-31
+  State getVertex(int index) const { return vertices_[index]; }            // :18-20
+  int getNumVertices() const { return (int)vertices_.size(); }             // :23-25
+  void addEdge(int idx1, int idx2);                                        // :36-42
+  int getPredecessor(int idx) const;                                       // :62-68
+  std::vector<int> getSuccessors(int idx) const { return successors_[idx]; }
+  void addAction(int idx, Action a) { actions_[idx] = a; }                 // :75-77
+  Action getAction(int idx) const { return actions_[idx]; }
+  double getGValue(int idx) const { return g_[idx]; }
+  double getYValue(int idx) const { return y_[idx]; }
+  void updateGYValue(int idx, double g_val, double y_val);                 // :131-138
+
+  // planner_class.cpp:38-76 on the engine sampler (stream = this tree's id)
+  State randomState(FastTerrainMap &terrain);
+  // n consecutive randomState draws of this tree's stream in one launch
+  std::vector<State> randomStateBatch(FastTerrainMap &terrain, int n);
+  // planner_class.cpp:185-200 on the engine (ties -> lowest index)
+  int getNearestNeighbor(State q);
+  std::vector<int> getNearestNeighborBatch(const std::vector<State> &q);
+  std::vector<int> neighborhoodDist(State q, double dist);                 // :173-182
+  std::vector<int> neighborhoodN(State q, int N);                          // :151-171
+
+  void setStream(uint64_t seed, uint64_t stream_id) {
+    seed_ = seed;
+    stream_id_ = stream_id;
+  }
+  const std::vector<State> &vertices() const { return vertices_; }
+
+ private:
+  void sync_device();
+  int device_;
+  std::vector<State> vertices_;
+  std::vector<Action> actions_;
+  std::vector<int> parent_;
+  std::vector<std::vector<int>> successors_;
+  std::vector<double> g_, y_;
+  bool cost_add_yaw_flag_ = false;
+  double cost_add_yaw_length_weight_ = 1, cost_add_yaw_yaw_weight_ = 1;
+  double *d_vertices_ = nullptr;
+  int64_t d_capacity_ = 0, d_count_ = 0;
+  void *d_scratch_ = nullptr;   // nearest-neighbour queries [q][8] + indices [q]
+  int64_t d_scratch_cap_ = 0;
+  uint64_t seed_ = 1, stream_id_ = 100;
+  int64_t draws_ = 0;
+};
+
+// ---- RRTClass / RRTConnectClass (rrt.h, rrt_connect.h) -------------------------
+class RRTClass {
+ public:
+  RRTClass() = default;
+  virtual ~RRTClass() = default;
+  // rrt.cpp:20-70 (candidates drawn from the engine stream, checked in one launch)
+  bool newConfig(State s, State s_near, State &s_new, Action &a_new, FastTerrainMap &terrain,
+                 int direction);
+  // rrt.cpp:77-102
+  virtual int extend(PlannerClass &T, State s, FastTerrainMap &terrain, int direction);
+  std::vector<int> pathFromStart(PlannerClass &T, int idx);                // rrt.cpp:107-118
+  std::vector<State> getStateSequence(PlannerClass &T, std::vector<int> path);
+  std::vector<Action> getActionSequence(PlannerClass &T, std::vector<int> path);
+  void getStatistics(double &plan_time, int &success_var, int &vertices_generated,
+                     double &time_to_first_solve, std::vector<double> &cost_vector,
+                     std::vector<double> &cost_vector_times, double &path_duration);
+  void set_state_action_pair_check_adaptive_step_size_flag_(bool f) {
+    state_action_pair_check_adaptive_step_size_flag_ = f;
+  }
+  void set_cost_add_yaw(bool flag, double lw, double yw) {
+    cost_add_yaw_flag_ = flag;
+    cost_add_yaw_length_weight_ = lw;
+    cost_add_yaw_yaw_weight_ = yw;
+  }
+  void setSeed(uint64_t seed) { seed_ = seed; }
+  // wall clock from the start of the build call to the first goal (the
+  // reference's elapsed_to_first restarts with every tree pair)
+  double wallTimeToFirst() const { return wall_to_first_; }
+
+ protected:
+  bool goal_found = false;
+  std::chrono::duration<double> elapsed_total{0};
+  std::chrono::duration<double> elapsed_to_first{0};
+  double wall_to_first_ = -1;
+  int success_ = 0;
+  int num_vertices = 0;
+  double path_length_ = 0, path_yaw_ = 0, path_cost_ = 0;
+  std::vector<double> length_vector_, yaw_vector_, cost_vector_, cost_vector_times_;
+  double path_duration_ = 0;
+  bool state_action_pair_check_adaptive_step_size_flag_ = false;
+  bool cost_add_yaw_flag_ = false;
+  double cost_add_yaw_length_weight_ = 1, cost_add_yaw_yaw_weight_ = 1;
+  uint64_t seed_ = 20251018;
+  int64_t extend_counter_ = 0;
+};
+
+struct BatchStats {
+  int64_t iterations = 0, targets = 0, extends = 0, attempts_checked = 0, connects = 0;
+  int64_t vertices_a = 0, vertices_b = 0;
+};
+
+class RRTConnectClass : public RRTClass {
+ public:
+  // rrt_connect.cpp:20-84 (recursive; the pair checks run on the engine)
+  int attemptConnect(State s_existing, State s, double t_s, State &s_new, Action &a_new,
+                     FastTerrainMap &terrain, int direction);
+  // rrt_connect.cpp:85-91
+  int attemptConnect(State s_existing, State s, State &s_new, Action &a_new, FastTerrainMap &terrain,
+                     int direction);
+  int connect(PlannerClass &T, State s, FastTerrainMap &terrain, int direction);  // :98-120
+  std::vector<Action> getActionSequenceReverse(PlannerClass &T, std::vector<int> path);
+  void postProcessPath(std::vector<State> &state_sequence, std::vector<Action> &action_sequence,
+                       FastTerrainMap &terrain);                                    // :139-227
+  void runRRTConnect(PlannerClass &Ta, PlannerClass &Tb, FastTerrainMap &terrain);  // :230-314
+  void buildRRTConnect(FastTerrainMap &terrain, State s_start, State s_goal,
+                       std::vector<State> &state_sequence, std::vector<Action> &action_sequence,
+                       double max_time);                                            // :323-467
+
+  // Batch-synchronous RRT-Connect: each half-iteration draws `batch` targets,
+  // extends the tree toward all of them against the current snapshot (one
+  // engine launch, 6 candidates each), inserts the non-TRAPPED successors in
+  // target order, then connects every new vertex to the other tree with the
+  // recursive attemptConnect run as lock-step rounds (one launch per round).
+  // batch = 1 is runRRTConnect.  Stops at the first solution or max_time.
+  bool buildRRTConnectBatched(FastTerrainMap &terrain, State s_start, State s_goal, int batch,
+                              double max_time, std::vector<State> &state_sequence,
+                              std::vector<Action> &action_sequence, BatchStats *stats = nullptr);
+
+ protected:
+  double anytime_horizon = 0;
+  const double planning_rate_estimate = 16.0;
+  double horizon_expansion_factor = 1.2;
+  const int max_time_solve = 4000;
+
+ private:
+  // one lock-step round of attemptConnect for many (s_existing, s, t_s) triples
+  void attemptConnectBatch(const std::vector<State> &s_existing, const std::vector<State> &s,
+                           std::vector<double> t_s, FastTerrainMap &terrain, int direction,
+                           std::vector<int> &result, std::vector<State> &s_new,
+                           std::vector<Action> &a_new, BatchStats *stats);
+  int halfIterationBatched(PlannerClass &T, PlannerClass &O, FastTerrainMap &terrain, int dir,
+                           int batch, int &meet_t, int &meet_o, BatchStats *stats);
+};
+
+// ---- implementation of the grid_map adapter (fast_terrain_map.cpp:31-91) -------
+// Written against grid_map::GridMap's public API (getSize, getStartIndex,
+// getPosition(Index, Position&), at(layer, Index), exists(layer)); a template
+// so this header needs no grid_map build (not in this image; untested here).
+template <class GridMap>
+void FastTerrainMap::loadDataFromGridMap(const GridMap &map) {
+  using Index = typename std::decay<decltype(map.getStartIndex())>::type;
+  using Position = typename std::decay<decltype(map.getPosition())>::type;
+  const int x_size = map.getSize()(0);
+  const int y_size = map.getSize()(1);
+  std::vector<double> x(x_size), y(y_size), z((size_t)x_size * y_size);
+  const bool slopes = map.exists("dx");
+  std::vector<double> dx, dy, dz;
+  if (slopes) {
+    dx.resize(z.size());
+    dy.resize(z.size());
+    dz.resize(z.size());
+  }
+  for (int i = 0; i < x_size; i++) {
+    Index index((x_size - 1) - i, 0);
+    Position position;
+    map.getPosition(index, position);
+    x[i] = position.x();
+  }
+  for (int i = 0; i < y_size; i++) {
+    Index index(0, (y_size - 1) - i);
+    Position position;
+    map.getPosition(index, position);
+    y[i] = position.y();
+  }
+  for (int i = 0; i < x_size; i++)
+    for (int j = 0; j < y_size; j++) {
+      Index index((x_size - 1) - i, (y_size - 1) - j);
+      const size_t k = (size_t)i * y_size + j;
+      z[k] = (double)map.at("elevation", index);
+      if (slopes) {
+        dx[k] = (double)map.at("dx", index);
+        dy[k] = (double)map.at("dy", index);
+        dz[k] = (double)map.at("dz", index);
+      }
+    }
+  loadDataFlat(x_size, y_size, x.data(), y.data(), z.data(), slopes ? dx.data() : nullptr,
+               slopes ? dy.data() : nullptr, slopes ? dz.data() : nullptr);
+}
+
+}  // namespace gbp_amd
+
+// ---- flat C entry point of the batched planner (Python / bench) -------------
+extern "C" {
+typedef struct {
+  int device, nx, ny;
+  const double *x, *y, *z, *dx, *dy, *dz;  // x-major, dx/dy/dz may be NULL
+  double start[8], goal[8];
+  int batch;            // targets per half-iteration (1 = sequential runRRTConnect)
+  double max_time;      // seconds
+  uint64_t seed;
+  int post_process;     // run postProcessPath on the found path
+} gbp_plan_params;
+
+typedef struct {
+  int found;
+  double time_to_first;  // wall seconds, build start -> first goal
+  double total_time;
+  int64_t iterations, targets, extends, attempts_checked, connects, vertices_a, vertices_b;
+  int n_states;          // path states written (<= capacity)
+  double path_length, path_cost, path_duration;
+} gbp_plan_result;
+
+/* plans from start to goal; path_states[capacity][8] / path_actions[capacity][10]
+ * (may be NULL).  Returns GBP_OK or a negative status. */
+int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r, double *path_states,
+                         double *path_actions, int capacity);
+}

@@ -90,3 +90,25 @@ def test_product_never_imports_the_oracle():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 txt = open(os.path.join(dirpath, f)).read()
                 assert "import oracle" not in txt and "gbp_oracle" not in txt, f
+
+
+def test_planner_library_exports_and_fails_without_device():
+    """libgbp_planner.so (include/gbp_planner.h) exports the flat C entry
+    gbp_plan_rrt_connect, no other unmangled symbol, and reports the engine's
+    status instead of planning on the CPU when no device is present."""
+    from global_body_planner_amd import planner
+    out = subprocess.run(["nm", "-D", "--defined-only", planner.PLANNER_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    c_syms = set(re.findall(r"\bT (gbp_\w+)", out))
+    assert c_syms == {"gbp_plan_rrt_connect"}
+    txt = open(os.path.join(ROOT, "include", "gbp_planner.h")).read()
+    assert "int gbp_plan_rrt_connect(" in txt
+    # the C structs mirror the header layout
+    assert ctypes.sizeof(planner.PlanParams) == 4 * 3 + 4 + 8 * 6 + 8 * 16 + 8 + 8 + 8 + 8
+    import torch
+    if not torch.cuda.is_available():
+        from global_body_planner_amd import terrain_data as td
+        data = td.synth_rough(64)
+        with pytest.raises(L.GbpError) as e:
+            planner.plan_rrt_connect(data, np.zeros(8), np.zeros(8), batch=4, max_time=0.1)
+        assert e.value.status == -6

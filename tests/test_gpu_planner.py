@@ -1,0 +1,101 @@
+"""The batched RRT-Connect planner (include/gbp_planner.h, csrc/host/gbp_planner.cpp)
+on the GPU.  A planner run has no bit-level reference output (the reference's
+RNG is unseeded): these tests check what must hold for ANY
+reference-semantics path, edge by edge against the oracle:
+
+  * states[0] == start and states[-1] == goal exactly;
+  * every edge (states[i], actions[i]) was accepted by a pair check the oracle
+    reproduces bit-exactly: isValidStateActionPair(states[i], a_i) (edges grown
+    FORWARD, rrt.cpp:36 / rrt_connect.cpp:70) or
+    isValidStateActionPairReverse(states[i+1], a_i) (edges grown REVERSE,
+    rrt.cpp:39 / rrt_connect.cpp:71);
+  * the action is dynamically feasible (isValidAction, planning_utils.cpp:519)
+    and lands on the next state: applyAction(states[i], a_i) == states[i+1]
+    to 1e-9 (forward edges exactly, reverse edges up to the stance inversion);
+  * the run is deterministic for a fixed (seed, batch).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from global_body_planner_amd import planner
+from global_body_planner_amd import terrain_data as td
+
+pytestmark = pytest.mark.gpu
+
+
+def _start_goal(O, xs, ys, xg, yg):
+    hs, _ = O.ground_height(xs, ys)
+    hg, _ = O.ground_height(xg, yg)
+    return planner.start_goal_state(hs, xs, ys), planner.start_goal_state(hg, xg, yg)
+
+
+def check_path(O, out, start, goal):
+    S, A = out["states"], out["actions"]
+    assert out["found"] == 1 and S.shape[0] >= 2 and A.shape[0] == S.shape[0] - 1
+    assert np.array_equal(S[0], start) and np.array_equal(S[-1], goal)
+    fv, _, _, _, _ = O.validate_pairs(S[:-1], A, np.zeros(len(A), np.uint8))
+    rv, _, _, _, _ = O.validate_pairs(S[1:], A, np.ones(len(A), np.uint8))
+    ok = (fv != 0) | (rv != 0)
+    assert ok.all(), f"edges {np.nonzero(~ok)[0]} accepted by neither pair check"
+    for i in range(len(A)):
+        assert oracle.is_valid_action(A[i]), i
+        land = oracle.apply_flight(oracle.apply_stance(S[i], A[i], A[i][6]), A[i][7])
+        np.testing.assert_allclose(land, S[i + 1], rtol=1e-9, atol=1e-9, err_msg=f"edge {i}")
+    dur = float(np.sum(A[:, 6] + A[:, 7]))
+    assert out["path_duration"] == pytest.approx(dur, rel=1e-12)
+
+
+@pytest.mark.parametrize("batch", [1, 64])
+def test_plan_synth256(gpu, batch):
+    data = td.synth_rough(256)
+    O = oracle.OracleTerrain.from_data(data)
+    start, goal = _start_goal(O, 1.0, 2.55, 4.02, 2.55)   # SURVEY §8(d) config 2 pair
+    out = planner.plan_rrt_connect(data, start, goal, batch=batch, max_time=60.0, seed=11)
+    check_path(O, out, start, goal)
+    assert out["time_to_first"] > 0 and out["iterations"] >= 1
+    assert out["vertices_a"] >= 1 and out["vertices_b"] >= 1
+
+
+def test_plan_is_deterministic(gpu):
+    data = td.synth_rough(256)
+    O = oracle.OracleTerrain.from_data(data)
+    start, goal = _start_goal(O, 1.0, 2.55, 4.02, 2.55)
+    a = planner.plan_rrt_connect(data, start, goal, batch=32, max_time=60.0, seed=5)
+    b = planner.plan_rrt_connect(data, start, goal, batch=32, max_time=60.0, seed=5)
+    assert a["found"] and b["found"]
+    assert np.array_equal(a["states"], b["states"]) and np.array_equal(a["actions"], b["actions"])
+    assert a["iterations"] == b["iterations"] and a["vertices_a"] == b["vertices_a"]
+
+
+def test_plan_slope_config1_and_post_process(gpu):
+    """Config 1: slope CSV, start (1,0) -> goal (8,0); the
+    post-processed path (rrt_connect.cpp:139-227) keeps the same endpoints and
+    only edges accepted by a pair check."""
+    data = td.csv_gridmap("slope")
+    O = oracle.OracleTerrain.from_data(data)
+    start, goal = _start_goal(O, 1.0, 0.0, 8.0, 0.0)
+    out = planner.plan_rrt_connect(data, start, goal, batch=128, max_time=120.0, seed=3)
+    check_path(O, out, start, goal)
+    pp = planner.plan_rrt_connect(data, start, goal, batch=128, max_time=120.0, seed=3,
+                                  post_process=True)
+    assert pp["found"]
+    S, A = pp["states"], pp["actions"]
+    assert np.array_equal(S[0], start) and np.array_equal(S[-1], goal)
+    assert len(S) <= len(out["states"])
+    # shortcut edges are forward connects (rrt_connect.cpp:158); an edge kept
+    # from the tree (:205-215) may have been grown in reverse
+    fv, _, _, _, _ = O.validate_pairs(S[:-1], A, np.zeros(len(A), np.uint8))
+    rv, _, _, _, _ = O.validate_pairs(S[1:], A, np.ones(len(A), np.uint8))
+    assert ((fv != 0) | (rv != 0)).all()
+
+
+def test_plan_stance_invalid_start_never_solves(gpu):
+    """slope (0,0) is STANCE-invalid, so every forward attempt from the
+    root fails after one state check and the planner times out without a path."""
+    data = td.csv_gridmap("slope")
+    O = oracle.OracleTerrain.from_data(data)
+    start, goal = _start_goal(O, 0.0, 0.0, 8.0, 0.0)
+    out = planner.plan_rrt_connect(data, start, goal, batch=64, max_time=3.0, seed=1)
+    assert out["found"] == 0 and out["n_states"] == 0 and out["time_to_first"] == -1.0
+    assert out["vertices_a"] == 1   # the root never gets a successor
