@@ -28,8 +28,31 @@ static inline double std_max(double a, double b) { return (a < b) ? b : a; }
 // ============================================================================
 FastTerrainMap::FastTerrainMap(int device) : device_(device) {}
 
+FastTerrainMap FastTerrainMap::borrow(gbp_terrain *handle) {
+  FastTerrainMap m;
+  int nx = 0, ny = 0, storage = 0, dev = 0;
+  double b[4];
+  chk(gbp_terrain_info(handle, &nx, &ny, &storage, b, &dev), "FastTerrainMap::borrow");
+  m.device_ = dev;
+  m.handle_ = handle;
+  m.owned_ = false;
+  m.x_size_ = nx;
+  m.y_size_ = ny;
+  // coordinate copies are not needed by the engine-backed queries; keep the
+  // bounds so getXData().front()/back() hold the map edges
+  m.x_data_ = {b[0], b[1]};
+  m.y_data_ = {b[2], b[3]};
+  return m;
+}
+
+FastTerrainMap::FastTerrainMap(FastTerrainMap &&o) noexcept
+    : device_(o.device_), handle_(o.handle_), owned_(o.owned_), x_size_(o.x_size_),
+      y_size_(o.y_size_), x_data_(std::move(o.x_data_)), y_data_(std::move(o.y_data_)) {
+  o.handle_ = nullptr;
+}
+
 FastTerrainMap::~FastTerrainMap() {
-  if (handle_) gbp_terrain_destroy(handle_);
+  if (handle_ && owned_) gbp_terrain_destroy(handle_);
 }
 
 void FastTerrainMap::loadData(int x_size, int y_size, std::vector<double> x_data,
@@ -67,8 +90,9 @@ void FastTerrainMap::loadDataFlat(int x_size, int y_size, const double *x, const
   gbp_terrain *h = nullptr;
   chk(gbp_terrain_create(device_, x_size, y_size, x, y, z, dx, dy, dz, GBP_STORAGE_AUTO, &h),
       "gbp_terrain_create");
-  if (handle_) gbp_terrain_destroy(handle_);
+  if (handle_ && owned_) gbp_terrain_destroy(handle_);
   handle_ = h;
+  owned_ = true;
   x_size_ = x_size;
   y_size_ = y_size;
   x_data_.assign(x, x + x_size);
@@ -670,7 +694,7 @@ void RRTConnectClass::attemptConnectBatch(const std::vector<State> &s_existing,
   std::vector<State> s = s0;
   std::vector<int> open(n);
   std::iota(open.begin(), open.end(), 0);
-  for (int depth = 0; !open.empty() && depth < 64; depth++) {
+  for (int depth = 0; !open.empty() && depth <= 64; depth++) {  // oracle's depth guard
     std::vector<int> chk_idx;
     std::vector<State> cs;
     std::vector<Action> ca;
@@ -1092,6 +1116,46 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
         if (path_actions && i < (int)actions.size())
           std::copy(actions[i].begin(), actions[i].end(), path_actions + 10 * i);
       }
+    }
+    return GBP_OK;
+  } catch (const EngineError &e) {
+    return e.status;
+  } catch (...) {
+    return GBP_E_INVALID_ARG;
+  }
+}
+
+extern "C" int gbp_attempt_connect_batch(gbp_terrain *t, int64_t n, const double *s_existing,
+                                         const double *s, const double *t_s, int direction,
+                                         int adaptive, int32_t *result, double *s_new,
+                                         double *a_new) {
+  using namespace gbp_amd;
+  if (!t) return GBP_E_BAD_HANDLE;
+  if (n < 0 || (n > 0 && (!s_existing || !s || !result || !s_new || !a_new)) ||
+      (direction != GBP_FORWARD && direction != GBP_REVERSE))
+    return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  try {
+    FastTerrainMap terrain = FastTerrainMap::borrow(t);
+    RRTConnectClass rc;
+    rc.set_state_action_pair_check_adaptive_step_size_flag_(adaptive != 0);
+    std::vector<State> se(n), sq(n), sn(n);
+    std::vector<Action> an(n);
+    std::vector<double> ts(n);
+    for (int64_t i = 0; i < n; i++) {
+      std::copy(s_existing + 8 * i, s_existing + 8 * i + 8, se[i].begin());
+      std::copy(s + 8 * i, s + 8 * i + 8, sq[i].begin());
+      std::copy(s_new + 8 * i, s_new + 8 * i + 8, sn[i].begin());
+      std::copy(a_new + 10 * i, a_new + 10 * i + 10, an[i].begin());
+      const double v = t_s ? t_s[i] : 0.0;
+      ts[i] = (v > 0) ? v : planning_utils::poseDistance(sq[i], se[i]) / planning_utils::V_NOM;
+    }
+    std::vector<int> r;
+    rc.attemptConnectBatchPublic(se, sq, ts, terrain, direction, r, sn, an);
+    for (int64_t i = 0; i < n; i++) {
+      result[i] = r[i];
+      std::copy(sn[i].begin(), sn[i].end(), s_new + 8 * i);
+      std::copy(an[i].begin(), an[i].end(), a_new + 10 * i);
     }
     return GBP_OK;
   } catch (const EngineError &e) {

@@ -51,6 +51,9 @@ def load():
         L.gbp_plan_rrt_connect.restype = ctypes.c_int
         L.gbp_plan_rrt_connect.argtypes = [ctypes.POINTER(PlanParams), ctypes.POINTER(PlanResult),
                                            _P, _P, ctypes.c_int]
+        L.gbp_attempt_connect_batch.restype = ctypes.c_int
+        L.gbp_attempt_connect_batch.argtypes = [_P, ctypes.c_int64, _P, _P, _P, ctypes.c_int,
+                                                ctypes.c_int, _P, _P, _P]
         _planner = L
     return _planner
 
@@ -92,3 +95,26 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     out["states"] = states[:n].copy()
     out["actions"] = actions[:max(n - 1, 0)].copy()
     return out
+
+
+def attempt_connect(terrain, s_existing, s, direction, t_s=None, adaptive=False, s_new=None,
+                    a_new=None):
+    """RRTConnectClass::attemptConnect (rrt_connect.cpp:20-91) for n pairs on an
+    engine Terrain (engine.Terrain).  Returns (result[n], s_new[n][8], a_new[n][10]);
+    s_new / a_new start as the given arrays (NaN if None) and are written only
+    where the reference writes them."""
+    L = load()
+    se = np.ascontiguousarray(s_existing, np.float64).reshape(-1, 8)
+    sq = np.ascontiguousarray(s, np.float64).reshape(-1, 8)
+    n = se.shape[0]
+    ts = None if t_s is None else np.ascontiguousarray(t_s, np.float64).reshape(n)
+    sn = np.full((n, 8), np.nan) if s_new is None else np.array(s_new, np.float64).reshape(n, 8)
+    an = np.full((n, 10), np.nan) if a_new is None else np.array(a_new, np.float64).reshape(n, 10)
+    res = np.empty(n, np.int32)
+    rc = L.gbp_attempt_connect_batch(terrain._h, n, se.ctypes.data, sq.ctypes.data,
+                                     None if ts is None else ts.ctypes.data, int(direction),
+                                     int(bool(adaptive)), res.ctypes.data, sn.ctypes.data,
+                                     an.ctypes.data)
+    if rc != 0:
+        raise _lib.GbpError(rc, "gbp_attempt_connect_batch")
+    return res, sn, an

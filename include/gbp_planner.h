@@ -84,6 +84,9 @@ struct EngineError : std::runtime_error {
 class FastTerrainMap {
  public:
   explicit FastTerrainMap(int device = 0);
+  // wrap an existing engine handle (not owned: the caller destroys it)
+  static FastTerrainMap borrow(gbp_terrain *handle);
+  FastTerrainMap(FastTerrainMap &&o) noexcept;
   ~FastTerrainMap();
   FastTerrainMap(const FastTerrainMap &) = delete;
   FastTerrainMap &operator=(const FastTerrainMap &) = delete;
@@ -116,6 +119,7 @@ class FastTerrainMap {
  private:
   int device_;
   gbp_terrain *handle_ = nullptr;
+  bool owned_ = true;
   int x_size_ = 0, y_size_ = 0;
   std::vector<double> x_data_, y_data_;
 };
@@ -311,6 +315,16 @@ class RRTConnectClass : public RRTClass {
                               double max_time, std::vector<State> &state_sequence,
                               std::vector<Action> &action_sequence, BatchStats *stats = nullptr);
 
+  // attemptConnect for many independent pairs (lock-step rounds, one engine
+  // launch per recursion depth); s_new / a_new are in/out per pair
+  void attemptConnectBatchPublic(const std::vector<State> &s_existing, const std::vector<State> &s,
+                                 std::vector<double> t_s, FastTerrainMap &terrain, int direction,
+                                 std::vector<int> &result, std::vector<State> &s_new,
+                                 std::vector<Action> &a_new) {
+    attemptConnectBatch(s_existing, s, std::move(t_s), terrain, direction, result, s_new, a_new,
+                        nullptr);
+  }
+
  protected:
   double anytime_horizon = 0;
   const double planning_rate_estimate = 16.0;
@@ -399,4 +413,14 @@ typedef struct {
  * (may be NULL).  Returns GBP_OK or a negative status. */
 int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r, double *path_states,
                          double *path_actions, int capacity);
+
+/* RRTConnectClass::attemptConnect (rrt_connect.cpp:20-91) for n independent
+ * (s_existing, s) pairs on an engine terrain handle, lock-step batched.
+ * t_s[i] <= 0 (or t_s NULL) => poseDistance(s, s_existing) / V_NOM (:89).
+ * s_new[n][8] / a_new[n][10] are in/out like the reference's references:
+ * written only where the reference writes them.  result[i] = TRAPPED /
+ * ADVANCED / REACHED. */
+int gbp_attempt_connect_batch(gbp_terrain *t, int64_t n, const double *s_existing,
+                              const double *s, const double *t_s, int direction, int adaptive,
+                              int32_t *result, double *s_new, double *a_new);
 }

@@ -100,9 +100,10 @@ def test_planner_library_exports_and_fails_without_device():
     out = subprocess.run(["nm", "-D", "--defined-only", planner.PLANNER_PATH], capture_output=True,
                          text=True, check=True).stdout
     c_syms = set(re.findall(r"\bT (gbp_\w+)", out))
-    assert c_syms == {"gbp_plan_rrt_connect"}
+    assert c_syms == {"gbp_plan_rrt_connect", "gbp_attempt_connect_batch"}
     txt = open(os.path.join(ROOT, "include", "gbp_planner.h")).read()
-    assert "int gbp_plan_rrt_connect(" in txt
+    for name in c_syms:
+        assert f"int {name}(" in txt
     # the C structs mirror the header layout
     assert ctypes.sizeof(planner.PlanParams) == 4 * 3 + 4 + 8 * 6 + 8 * 16 + 8 + 8 + 8 + 8
     import torch

@@ -9,8 +9,9 @@ reference-semantics path, edge by edge against the oracle:
     FORWARD, rrt.cpp:36 / rrt_connect.cpp:70) or
     isValidStateActionPairReverse(states[i+1], a_i) (edges grown REVERSE,
     rrt.cpp:39 / rrt_connect.cpp:71);
-  * the action is dynamically feasible (isValidAction, planning_utils.cpp:519)
-    and lands on the next state: applyAction(states[i], a_i) == states[i+1]
+  * connect actions (t_f = 0, rrt_connect.cpp:53-66) are dynamically feasible
+    (isValidAction, planning_utils.cpp:519 — extend actions are never checked
+    by the reference, rrt.cpp:33) and every action lands on the next state: applyAction(states[i], a_i) == states[i+1]
     to 1e-9 (forward edges exactly, reverse edges up to the stance inversion);
   * the run is deterministic for a fixed (seed, batch).
 """
@@ -39,7 +40,8 @@ def check_path(O, out, start, goal):
     ok = (fv != 0) | (rv != 0)
     assert ok.all(), f"edges {np.nonzero(~ok)[0]} accepted by neither pair check"
     for i in range(len(A)):
-        assert oracle.is_valid_action(A[i]), i
+        if A[i][7] == 0:
+            assert oracle.is_valid_action(A[i]), i
         land = oracle.apply_flight(oracle.apply_stance(S[i], A[i], A[i][6]), A[i][7])
         np.testing.assert_allclose(land, S[i + 1], rtol=1e-9, atol=1e-9, err_msg=f"edge {i}")
     dur = float(np.sum(A[:, 6] + A[:, 7]))
@@ -99,3 +101,35 @@ def test_plan_stance_invalid_start_never_solves(gpu):
     out = planner.plan_rrt_connect(data, start, goal, batch=64, max_time=3.0, seed=1)
     assert out["found"] == 0 and out["n_states"] == 0 and out["time_to_first"] == -1.0
     assert out["vertices_a"] == 1   # the root never gets a successor
+
+
+@pytest.mark.parametrize("name", ["synth-rough-256", "slope-gridmap"])
+@pytest.mark.parametrize("direction", [0, 1])
+def test_attempt_connect_parity(gpu, name, direction):
+    """RRTConnectClass::attemptConnect (rrt_connect.cpp:20-91) through the C++
+    host planner on the engine vs the oracle's recursive restatement: result
+    code, s_new and a_new bit-exact (in/out semantics: NaN where unwritten)."""
+    import global_body_planner_amd as gbp
+    from tests.helpers import same_f64
+    data = td.by_name(name)
+    O = oracle.OracleTerrain.from_data(data)
+    T = gbp.Terrain.from_data(data, device=0)
+    n = 1500
+    se, _ = O.sample_states(n, 31, 1, require_phase=1, max_tries=256, nthreads=8)
+    rng = np.random.default_rng(direction)
+    s = se.copy()
+    near = rng.uniform(size=n) < 0.7        # 70% short hops (REACHED / ADVANCED), 30% far targets
+    s[near, :3] += rng.normal(scale=0.15, size=(near.sum(), 3))
+    s[near, 3:6] += rng.normal(scale=0.3, size=(near.sum(), 3))
+    far, _ = O.sample_states(n, 32, 2, require_phase=1, max_tries=256, nthreads=8)
+    s[~near] = far[~near]
+    hs = O.height_batch(s[:, :2])[0]
+    s[near, 2] = np.where(np.isfinite(hs[near]), hs[near] + 0.3, s[near, 2])
+    r, sn, an = planner.attempt_connect(T, se, s, direction)
+    for i in range(n):
+        ro, sno, ano = O.attempt_connect(se[i], s[i], direction)
+        assert r[i] == ro, (i, r[i], ro)
+        assert np.all(same_f64(sn[i], sno)), i
+        assert np.all(same_f64(an[i], ano)), i
+    counts = np.bincount(r, minlength=3)
+    assert counts[2] > 0 and counts[0] > 0, counts   # both REACHED and TRAPPED occur
