@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <numeric>
 
@@ -565,6 +566,8 @@ std::vector<int> PlannerClass::neighborhoodN(State q, int N) {  // :151-171
 // ============================================================================
 bool RRTClass::newConfig(State s, State s_near, State &s_new, Action &a_new, FastTerrainMap &terrain,
                          int direction) {  // rrt.cpp:20-70 on the engine (6 candidates, one launch)
+  if (action_direction_sampling_flag_ || state_direction_sampling_flag_)
+    throw std::logic_error("direction sampling (planning_utils.cpp:445-515) is not implemented");
   int32_t result, chosen;
   uint32_t counts;
   State sn = s_new;
@@ -620,15 +623,51 @@ std::vector<Action> RRTClass::getActionSequence(PlannerClass &T, std::vector<int
 }
 
 void RRTClass::getStatistics(double &plan_time, int &success_var, int &vertices_generated,
-                             double &time_to_first_solve, std::vector<double> &cost_vector,
-                             std::vector<double> &cost_vector_times, double &path_duration) {
+                             double &time_to_first_solve, std::vector<double> &length_vector,
+                             std::vector<double> &yaw_vector, std::vector<double> &cost_vector,
+                             std::vector<double> &cost_vector_times, double &path_duration,
+                             std::vector<std::vector<double>> &allStatePosition) {
   plan_time = elapsed_total.count();
   success_var = success_;
   vertices_generated = num_vertices;
   time_to_first_solve = elapsed_to_first.count();
+  length_vector = length_vector_;
+  yaw_vector = yaw_vector_;
   cost_vector = cost_vector_;
   cost_vector_times = cost_vector_times_;
   path_duration = path_duration_;
+  allStatePosition = allStatePosition_;
+}
+
+void RRTClass::printPath(PlannerClass &T, std::vector<int> path) {
+  std::printf("Printing path:");
+  for (int idx : path) {
+    const State s = T.getVertex(idx);
+    std::printf("\n%d or {", idx);
+    for (int d = 0; d < 8; d++) std::printf(d ? ", %g" : "%g", s[d]);
+    std::printf("} ->");
+  }
+  std::printf("\b\b  \n");
+}
+
+void RRTClass::saveStateSequence(PlannerClass &T) {
+  for (int i = 0; i < T.getNumVertices(); ++i) {
+    const State s = T.getVertex(i);
+    allStatePosition_.push_back({s[0], s[1], s[2]});
+  }
+}
+
+void RRTClass::print_setting_parameters() {
+  std::printf("state_action_pair_check_adaptive_step_size_flag: %d\n",
+              (int)state_action_pair_check_adaptive_step_size_flag_);
+  std::printf("cost_add_yaw: %d %g %g\n", (int)cost_add_yaw_flag_, cost_add_yaw_length_weight_,
+              cost_add_yaw_yaw_weight_);
+  std::printf("action_direction_sampling: %d %g\n", (int)action_direction_sampling_flag_,
+              action_direction_sampling_probability_threshold_);
+  std::printf("state_direction_sampling: %d %g %d\n", (int)state_direction_sampling_flag_,
+              state_direction_sampling_probability_threshold_,
+              (int)state_direction_sampling_speed_direction_flag_);
+  std::printf("engine seed: %llu\n", (unsigned long long)seed_);
 }
 
 // ============================================================================
@@ -856,6 +895,8 @@ void RRTConnectClass::buildRRTConnect(FastTerrainMap &terrain, State s_start, St
                                       double max_time_opt) {  // rrt_connect.cpp:323-467
   const auto t_start = std::chrono::high_resolution_clock::now();
   success_ = 0;
+  length_vector_.clear();
+  yaw_vector_.clear();
   cost_vector_.clear();
   cost_vector_times_.clear();
   wall_to_first_ = -1;
@@ -864,7 +905,7 @@ void RRTConnectClass::buildRRTConnect(FastTerrainMap &terrain, State s_start, St
       Tb_best(terrain.device());
   anytime_horizon = poseDistance(s_start, s_goal) / planning_rate_estimate;
   num_vertices = 0;
-  double cost_so_far = INFTY;
+  double length_so_far = INFTY, yaw_so_far = INFTY, cost_so_far = INFTY;
   int restart = 0;
   std::chrono::duration<double> el{0};
   while (true) {
@@ -883,6 +924,7 @@ void RRTConnectClass::buildRRTConnect(FastTerrainMap &terrain, State s_start, St
       elapsed_total = el;
       elapsed_to_first = el;
       success_ = 0;
+      num_vertices += Ta.getNumVertices() + Tb.getNumVertices();  // counted twice, as :366
       return;
     }
     if (goal_found) {
@@ -900,10 +942,14 @@ void RRTConnectClass::buildRRTConnect(FastTerrainMap &terrain, State s_start, St
                              action_sequence_b.end());
       postProcessPath(state_sequence, action_sequence, terrain);
       if (path_cost_ < cost_so_far) {
+        length_so_far = path_length_;
+        yaw_so_far = path_yaw_;
         cost_so_far = path_cost_;
         Ta_best = Ta;
         Tb_best = Tb;
         el = std::chrono::high_resolution_clock::now() - t_start;
+        length_vector_.push_back(length_so_far);
+        yaw_vector_.push_back(yaw_so_far);
         cost_vector_.push_back(cost_so_far);
         cost_vector_times_.push_back(el.count());
       }
@@ -912,7 +958,7 @@ void RRTConnectClass::buildRRTConnect(FastTerrainMap &terrain, State s_start, St
   }
   Ta = Ta_best;
   Tb = Tb_best;
-  {
+  if (goal_found) {
     std::vector<int> path_a = pathFromStart(Ta, Ta.getNumVertices() - 1);
     std::vector<int> path_b = pathFromStart(Tb, Tb.getNumVertices() - 1);
     std::reverse(path_b.begin(), path_b.end());

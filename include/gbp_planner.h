@@ -250,9 +250,27 @@ class RRTClass {
   std::vector<int> pathFromStart(PlannerClass &T, int idx);                // rrt.cpp:107-118
   std::vector<State> getStateSequence(PlannerClass &T, std::vector<int> path);
   std::vector<Action> getActionSequence(PlannerClass &T, std::vector<int> path);
+  // rrt.cpp:154-169 (same 10 outputs)
   void getStatistics(double &plan_time, int &success_var, int &vertices_generated,
-                     double &time_to_first_solve, std::vector<double> &cost_vector,
-                     std::vector<double> &cost_vector_times, double &path_duration);
+                     double &time_to_first_solve, std::vector<double> &length_vector,
+                     std::vector<double> &yaw_vector, std::vector<double> &cost_vector,
+                     std::vector<double> &cost_vector_times, double &path_duration,
+                     std::vector<std::vector<double>> &allStatePosition);
+  void printPath(PlannerClass &T, std::vector<int> path);                  // rrt.cpp:143-152
+  void saveStateSequence(PlannerClass &T);                                 // rrt.cpp:253-265
+  // rrt.cpp:268-280: stored like the reference; direction sampling (default
+  // off, params.yaml:25-27) is not implemented by the engine samplers, so
+  // newConfig throws std::logic_error when a flag is on
+  void set_action_direction_sampling(bool flag, double threshold) {
+    action_direction_sampling_flag_ = flag;
+    action_direction_sampling_probability_threshold_ = threshold;
+  }
+  void set_state_direction_sampling(bool flag, double threshold, bool speed_direction_flag) {
+    state_direction_sampling_flag_ = flag;
+    state_direction_sampling_probability_threshold_ = threshold;
+    state_direction_sampling_speed_direction_flag_ = speed_direction_flag;
+  }
+  void print_setting_parameters();
   void set_state_action_pair_check_adaptive_step_size_flag_(bool f) {
     state_action_pair_check_adaptive_step_size_flag_ = f;
   }
@@ -276,6 +294,12 @@ class RRTClass {
   double path_length_ = 0, path_yaw_ = 0, path_cost_ = 0;
   std::vector<double> length_vector_, yaw_vector_, cost_vector_, cost_vector_times_;
   double path_duration_ = 0;
+  std::vector<std::vector<double>> allStatePosition_;
+  bool action_direction_sampling_flag_ = false;
+  double action_direction_sampling_probability_threshold_ = 0.15;
+  bool state_direction_sampling_flag_ = false;
+  double state_direction_sampling_probability_threshold_ = 0.05;
+  bool state_direction_sampling_speed_direction_flag_ = false;
   bool state_action_pair_check_adaptive_step_size_flag_ = false;
   bool cost_add_yaw_flag_ = false;
   double cost_add_yaw_length_weight_ = 1, cost_add_yaw_yaw_weight_ = 1;

@@ -1,0 +1,86 @@
+// Compile/link check of the drop-in: the calls GlobalBodyPlanner makes on the
+// planner classes (global_body_planner.cpp:43, :88-119, :178-195, :263-264,
+// :131 getInterpPath), written against the reference's global names through
+// gbp_planner_compat.h.  Built and linked by tests/test_abi.py; run on the
+// GPU box by tests/test_gpu_planner.py (argv: nothing; exit 0 = plan found).
+#include <cstdio>
+#include <vector>
+
+#include "gbp_planner_compat.h"
+
+// a minimal grid_map-shaped type (getSize, getStartIndex, getPosition, at, exists)
+namespace fake_grid_map {
+struct Vec2i {
+  int v[2];
+  Vec2i(int a = 0, int b = 0) : v{a, b} {}
+  int operator()(int i) const { return v[i]; }
+};
+struct Pos {
+  double px = 0, py = 0;
+  double x() const { return px; }
+  double y() const { return py; }
+};
+struct GridMap {
+  int nx, ny;
+  double res;
+  std::vector<float> z;  // grid_map index (i, j) -> z[i*ny + j]
+  Vec2i getSize() const { return Vec2i(nx, ny); }
+  Vec2i getStartIndex() const { return Vec2i(0, 0); }
+  Pos getPosition() const { return Pos(); }
+  void getPosition(const Vec2i &idx, Pos &p) const {
+    // grid_map: index (0,0) is the max corner (fast_terrain_map.cpp:44-54 reverses it)
+    p.px = (nx - 1 - idx(0)) * res;
+    p.py = (ny - 1 - idx(1)) * res;
+  }
+  float at(const char *layer, const Vec2i &idx) const {
+    (void)layer;
+    return z[(size_t)idx(0) * ny + idx(1)];
+  }
+  bool exists(const char *layer) const {
+    (void)layer;
+    return false;
+  }
+};
+}  // namespace fake_grid_map
+
+int main() {
+  fake_grid_map::GridMap map{120, 60, 0.05, {}};
+  map.z.assign((size_t)map.nx * map.ny, 0.0f);  // flat ground
+  FastTerrainMap terrain_;
+  terrain_.loadDataFromGridMap(map);  // global_body_planner.cpp:43
+
+  State robot_start_ = {0.5, 1.5, 0.375, 1, 0, 0, 0, 0};
+  State robot_goal_ = {4.5, 1.5, 0.375, 1, 0, 0, 0, 0};
+  robot_start_[2] += terrain_.getGroundHeight(robot_start_[0], robot_start_[1]);  // :263
+  robot_goal_[2] += terrain_.getGroundHeight(robot_goal_[0], robot_goal_[1]);     // :264
+
+  RRTConnectClass rrt_connect_obj;                                    // :89
+  rrt_connect_obj.set_state_action_pair_check_adaptive_step_size_flag_(false);  // :182
+  rrt_connect_obj.set_cost_add_yaw(false, 1.0, 1.0);                  // :190
+  rrt_connect_obj.set_action_direction_sampling(false, 0.15);
+  rrt_connect_obj.set_state_direction_sampling(false, 0.05, false);
+
+  std::vector<State> state_sequence_;
+  std::vector<Action> action_sequence_;
+  rrt_connect_obj.buildRRTConnect(terrain_, robot_start_, robot_goal_, state_sequence_,
+                                  action_sequence_, 0.0);             // :115
+  double plan_time, time_to_first_solve, path_duration;
+  int success, vertices_generated;
+  std::vector<double> length_vector, yaw_vector, cost_vector, cost_vector_times;
+  std::vector<std::vector<double>> allStatePosition;
+  rrt_connect_obj.getStatistics(plan_time, success, vertices_generated, time_to_first_solve,
+                                length_vector, yaw_vector, cost_vector, cost_vector_times,
+                                path_duration, allStatePosition);     // :118
+  std::vector<State> body_plan_;
+  std::vector<double> t_plan_;
+  std::vector<int> interp_phase;
+  getInterpPath(state_sequence_, action_sequence_, 0.05, body_plan_, t_plan_, interp_phase);  // :131
+  std::printf("states %zu actions %zu vertices %d plan_time %.3f path_duration %.3f interp %zu\n",
+              state_sequence_.size(), action_sequence_.size(), vertices_generated, plan_time,
+              path_duration, body_plan_.size());
+  const bool ok = state_sequence_.size() >= 2 && state_sequence_.front() == robot_start_ &&
+                  state_sequence_.back() == robot_goal_ &&
+                  action_sequence_.size() + 1 == state_sequence_.size() &&
+                  body_plan_.size() == t_plan_.size();
+  return ok ? 0 : 1;
+}

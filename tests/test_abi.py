@@ -113,3 +113,23 @@ def test_planner_library_exports_and_fails_without_device():
         with pytest.raises(L.GbpError) as e:
             planner.plan_rrt_connect(data, np.zeros(8), np.zeros(8), batch=4, max_time=0.1)
         assert e.value.status == -6
+
+
+def build_node_callsite(out):
+    """g++ the ROS-node call-site check against the reference's global names."""
+    lib = os.path.join(ROOT, "global_body_planner_amd", "lib")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "integration", "node_callsite.cpp"), "-L", lib,
+                    "-lgbp_planner", "-lgbp", f"-Wl,-rpath,{lib}", "-o", str(out)], check=True)
+    return str(out)
+
+
+def test_node_callsite_compiles_links_and_refuses_cpu(tmp_path):
+    """The call sites of global_body_planner.cpp compile unchanged against
+    gbp_planner_compat.h and link against libgbp_planner.so; without a GPU the
+    planner raises the engine's error instead of planning on the CPU."""
+    exe = build_node_callsite(tmp_path / "node_callsite")
+    import torch
+    if not torch.cuda.is_available():
+        r = subprocess.run([exe], capture_output=True, text=True)
+        assert r.returncode != 0 and "no HIP device" in r.stderr

@@ -133,3 +133,15 @@ def test_attempt_connect_parity(gpu, name, direction):
         assert np.all(same_f64(an[i], ano)), i
     counts = np.bincount(r, minlength=3)
     assert counts[2] > 0 and counts[0] > 0, counts   # both REACHED and TRAPPED occur
+
+
+def test_node_callsite_plans_on_gpu(gpu, tmp_path):
+    """The ROS-node call sequence (tests/integration/node_callsite.cpp: grid_map
+    ingest, start/goal heights, buildRRTConnect, getStatistics, getInterpPath)
+    through the reference's global names runs to a path on the engine."""
+    import subprocess
+    from tests.test_abi import build_node_callsite
+    exe = build_node_callsite(tmp_path / "node_callsite")
+    r = subprocess.run(["timeout", "-k", "10", "120", exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("states ")
