@@ -24,6 +24,7 @@ F_STAGE_MASK = 0xF << F_STAGE_SHIFT
 STORAGE_AUTO, STORAGE_F32, STORAGE_F64 = 0, 1, 2
 OPT_KERNEL, OPT_BLOCK, OPT_GRID_PER_CU, OPT_WAVES, OPT_LDS_COORDS, OPT_SCHED, OPT_CHUNK = \
     1, 2, 3, 4, 5, 6, 7
+OPT_HELPERS = 8
 KERNEL_DIRECT, KERNEL_PERSISTENT = 0, 1
 
 EXPORTS = [

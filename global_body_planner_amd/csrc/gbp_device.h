@@ -224,6 +224,16 @@ __device__ __forceinline__ bool surface_normal(const TerrainView<ZT> &T, double 
   return true;
 }
 
+// stance divisions x / (6 t_s), x / (2 t_s) (Markstein with a constant
+// reciprocal was measured: no faster than the hardware-assisted sequence)
+__device__ __forceinline__ double pdiv(double x, double d) {
+#ifdef GBP_EXPERIMENT_NO_PROPDIV  // diagnostic timing build only (results differ)
+  return x * 0.5;
+#endif
+  return x / d;
+}
+#define PDIV6(x) pdiv((x), 6.0 * t_s)
+#define PDIV2(x) pdiv((x), 2.0 * t_s)
 // ---- propagation --------------------------------------------------------------
 // planning_utils.cpp:237-274
 __device__ __forceinline__ void apply_stance(const double *s, const double *a, double t,
@@ -231,14 +241,14 @@ __device__ __forceinline__ void apply_stance(const double *s, const double *a, d
   const double a_x_td = a[0], a_y_td = a[1], a_z_td = a[2];
   const double a_x_to = a[3], a_y_to = a[4], a_z_to = a[5];
   const double t_s = a[6], a_p_td = a[8], a_p_to = a[9];
-  o[0] = s[0] + s[3] * t + 0.5 * a_x_td * t * t + (a_x_to - a_x_td) * (t * t * t) / (6.0 * t_s);
-  o[1] = s[1] + s[4] * t + 0.5 * a_y_td * t * t + (a_y_to - a_y_td) * (t * t * t) / (6.0 * t_s);
-  o[2] = s[2] + s[5] * t + 0.5 * a_z_td * t * t + (a_z_to - a_z_td) * (t * t * t) / (6.0 * t_s);
-  o[3] = s[3] + a_x_td * t + (a_x_to - a_x_td) * t * t / (2.0 * t_s);
-  o[4] = s[4] + a_y_td * t + (a_y_to - a_y_td) * t * t / (2.0 * t_s);
-  o[5] = s[5] + a_z_td * t + (a_z_to - a_z_td) * t * t / (2.0 * t_s);
-  o[6] = s[6] + s[7] * t + 0.5 * a_p_td * t * t + (a_p_to - a_p_td) * (t * t * t) / (6.0 * t_s);
-  o[7] = s[7] + a_p_td * t + (a_p_to - a_p_td) * t * t / (2.0 * t_s);
+  o[0] = s[0] + s[3] * t + 0.5 * a_x_td * t * t + PDIV6((a_x_to - a_x_td) * (t * t * t));
+  o[1] = s[1] + s[4] * t + 0.5 * a_y_td * t * t + PDIV6((a_y_to - a_y_td) * (t * t * t));
+  o[2] = s[2] + s[5] * t + 0.5 * a_z_td * t * t + PDIV6((a_z_to - a_z_td) * (t * t * t));
+  o[3] = s[3] + a_x_td * t + PDIV2((a_x_to - a_x_td) * t * t);
+  o[4] = s[4] + a_y_td * t + PDIV2((a_y_to - a_y_td) * t * t);
+  o[5] = s[5] + a_z_td * t + PDIV2((a_z_to - a_z_td) * t * t);
+  o[6] = s[6] + s[7] * t + 0.5 * a_p_td * t * t + PDIV6((a_p_to - a_p_td) * (t * t * t));
+  o[7] = s[7] + a_p_td * t + PDIV2((a_p_to - a_p_td) * t * t);
 }
 
 // planning_utils.cpp:282-306 (g is the literal 9.81)
@@ -265,14 +275,14 @@ __device__ __forceinline__ void apply_stance_reverse(const double *s, const doub
   const double cz = s[5] - a_z_td * t_s - 0.5 * (a_z_to - a_z_td) * t_s;
   const double cp = s[7] - a_p_td * t_s - 0.5 * (a_p_to - a_p_td) * t_s;
   const double d1 = t_s - t, d2 = t_s * t_s - t * t, d3 = t_s * t_s * t_s - t * t * t;
-  o[0] = s[0] - cx * d1 - 0.5 * a_x_td * d2 - (a_x_to - a_x_td) * d3 / (6.0 * t_s);
-  o[1] = s[1] - cy * d1 - 0.5 * a_y_td * d2 - (a_y_to - a_y_td) * d3 / (6.0 * t_s);
-  o[2] = s[2] - cz * d1 - 0.5 * a_z_td * d2 - (a_z_to - a_z_td) * d3 / (6.0 * t_s);
-  o[3] = s[3] - a_x_td * d1 - (a_x_to - a_x_td) * d2 / (2.0 * t_s);
-  o[4] = s[4] - a_y_td * d1 - (a_y_to - a_y_td) * d2 / (2.0 * t_s);
-  o[5] = s[5] - a_z_td * d1 - (a_z_to - a_z_td) * d2 / (2.0 * t_s);
-  o[7] = s[7] - a_p_td * d1 - (a_p_to - a_p_td) * d2 / (2.0 * t_s);
-  o[6] = s[6] - cp * d1 - 0.5 * a_p_td * d2 - (a_p_to - a_p_td) * d3 / (6.0 * t_s);
+  o[0] = s[0] - cx * d1 - 0.5 * a_x_td * d2 - PDIV6((a_x_to - a_x_td) * d3);
+  o[1] = s[1] - cy * d1 - 0.5 * a_y_td * d2 - PDIV6((a_y_to - a_y_td) * d3);
+  o[2] = s[2] - cz * d1 - 0.5 * a_z_td * d2 - PDIV6((a_z_to - a_z_td) * d3);
+  o[3] = s[3] - a_x_td * d1 - PDIV2((a_x_to - a_x_td) * d2);
+  o[4] = s[4] - a_y_td * d1 - PDIV2((a_y_to - a_y_td) * d2);
+  o[5] = s[5] - a_z_td * d1 - PDIV2((a_z_to - a_z_td) * d2);
+  o[7] = s[7] - a_p_td * d1 - PDIV2((a_p_to - a_p_td) * d2);
+  o[6] = s[6] - cp * d1 - 0.5 * a_p_td * d2 - PDIV6((a_p_to - a_p_td) * d3);
 }
 
 // planning_utils.cpp:519-556
@@ -289,6 +299,57 @@ __device__ __forceinline__ bool is_valid_action(const double *a) {
       (sqrt(f_x_to * f_x_to + f_y_to * f_y_to) >= mu * f_z_to))
     return false;
   return true;
+}
+
+// ---- rotation trig of isValidState (planning_utils.cpp:578-594) ---------------
+// The reference forms cos/sin(atan2(dy, dx)) and cos/sin(p) with glibc; the
+// device's libm differs from glibc by ulps anyway, which is why decisions
+// within FRAGILE_EPS of a threshold are flagged.  Within that contract the
+// same values are computed more cheaply:
+//  * yaw: cos(atan2(dy,dx)) = dx/|v|, sin(atan2(dy,dx)) = dy/|v| (|v| is the
+//    speed already computed for check (3)); error <= 2 ulp.  |v| = 0, tiny,
+//    huge or non-finite take the libm path (atan2(+-0, -0) = +-pi etc.).
+//  * pitch: |p| < P_MAX = 1 here (check (2)), so sin/cos are their Taylor
+//    series to p^19 / p^20 (truncation < 5e-20) in Horner form with fma;
+//    NaN propagates as with libm.
+// Position error from either is ~1e-16 m, far below FRAGILE_EPS = 1e-12.
+__device__ __forceinline__ void rotation_trig(double dx, double dy, double speed, double p,
+                                              double &cy, double &sy, double &cp, double &sp) {
+  if (speed > 1e-150 && speed < 1e150) {
+    cy = dx / speed;
+    sy = dy / speed;
+  } else {
+    const double yaw = atan2(dy, dx);
+    cy = cos(yaw);
+    sy = sin(yaw);
+  }
+  if (fabs(p) < 1.0) {
+    const double z = p * p;
+    double ps = -1.0 / 121645100408832000.0;                  // -1/19!
+    ps = __builtin_fma(ps, z, 1.0 / 355687428096000.0);       //  1/17!
+    ps = __builtin_fma(ps, z, -1.0 / 1307674368000.0);        // -1/15!
+    ps = __builtin_fma(ps, z, 1.0 / 6227020800.0);            //  1/13!
+    ps = __builtin_fma(ps, z, -1.0 / 39916800.0);             // -1/11!
+    ps = __builtin_fma(ps, z, 1.0 / 362880.0);                //  1/9!
+    ps = __builtin_fma(ps, z, -1.0 / 5040.0);                 // -1/7!
+    ps = __builtin_fma(ps, z, 1.0 / 120.0);                   //  1/5!
+    ps = __builtin_fma(ps, z, -1.0 / 6.0);                    // -1/3!
+    sp = __builtin_fma(p * z, ps, p);
+    double pc = 1.0 / 2432902008176640000.0;                  //  1/20!
+    pc = __builtin_fma(pc, z, -1.0 / 6402373705728000.0);     // -1/18!
+    pc = __builtin_fma(pc, z, 1.0 / 20922789888000.0);        //  1/16!
+    pc = __builtin_fma(pc, z, -1.0 / 87178291200.0);          // -1/14!
+    pc = __builtin_fma(pc, z, 1.0 / 479001600.0);             //  1/12!
+    pc = __builtin_fma(pc, z, -1.0 / 3628800.0);              // -1/10!
+    pc = __builtin_fma(pc, z, 1.0 / 40320.0);                 //  1/8!
+    pc = __builtin_fma(pc, z, -1.0 / 720.0);                  // -1/6!
+    pc = __builtin_fma(pc, z, 1.0 / 24.0);                    //  1/4!
+    pc = __builtin_fma(pc, z, -0.5);                          // -1/2!
+    cp = __builtin_fma(z, pc, 1.0);
+  } else {
+    cp = cos(p);
+    sp = sin(p);
+  }
 }
 
 // ---- state validity: planning_utils.cpp:562-635 ------------------------------
@@ -324,7 +385,8 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
   if ((s[0] < T.x0) || (s[0] > T.xN) || (s[1] < T.y0) || (s[1] > T.yN) || (fabs(s[6]) >= P_MAX))
     return false;
   // (3) horizontal speed :574
-  if (sqrt(s[3] * s[3] + s[4] * s[4]) > V_MAX) return false;
+  const double speed = sqrt(s[3] * s[3] + s[4] * s[4]);
+  if (speed > V_MAX) return false;
   // (4) rotation :578-594
 #ifdef GBP_EXPERIMENT_NO_TRIG
   const double yaw = s[4] * s[3];
@@ -332,10 +394,8 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
   const double pitch = s[6];
   const double cp = pitch * 0.5, sp = pitch * 0.25;
 #else
-  const double yaw = atan2(s[4], s[3]);
-  const double cy = cos(yaw), sy = sin(yaw);
-  const double pitch = s[6];
-  const double cp = cos(pitch), sp = sin(pitch);
+  double cy, sy, cp, sp;
+  rotation_trig(s[3], s[4], speed, s[6], cy, sy, cp, sp);
 #endif
   const double R_11 = cy * cp, R_12 = -sy, R_13 = cy * sp;
   const double R_21 = sy * cp, R_22 = cy, R_23 = sy * sp;

@@ -19,6 +19,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <cstring>
+
 #include <algorithm>
 #include <cmath>
 #include <mutex>
@@ -41,12 +43,15 @@ template <class ZT>
 __device__ __forceinline__ TerrainView<ZT> stage_coords(const TerrainView<ZT> &T0, double *smem) {
   for (int i = threadIdx.x; i < T0.nx; i += blockDim.x) smem[i] = T0.x[i];
   for (int i = threadIdx.x; i < T0.ny; i += blockDim.x) smem[T0.nx + i] = T0.y[i];
-  __syncthreads();
   TerrainView<ZT> T = T0;
   T.x = smem;
   T.y = smem + T0.nx;
+  __syncthreads();
   return T;
 }
+
+// LDS bytes of stage_coords for this terrain
+inline size_t stage_bytes(int nx, int ny) { return sizeof(double) * (size_t)(nx + ny); }
 
 // ============================================================================
 // K1: batched terrain queries
@@ -233,15 +238,40 @@ __device__ __forceinline__ bool small_step(double ts) {
   return !ADAPTIVE || (KINEMATICS_RES - 0.01 <= ts && ts <= KINEMATICS_RES + 0.01);
 }
 
-// returns true when the pair is decided (L.f has VALID set or not)
-template <class ZT, bool ADAPTIVE>
-__device__ __forceinline__ bool step_lane(const TerrainView<ZT> &T, Lane &L) {
-  double sc[8];
-  const int phase = (L.stage == ST_FWD_FLIGHT || L.stage == ST_REV_FLIGHT) ? GBP_FLIGHT : GBP_STANCE;
-  sample_state(L, L.stage,
-               L.stage == ST_FWD_LAND ? L.a[7] : (L.stage == ST_REV_START ? 0.0 : L.t), sc);
-  const bool ok = is_valid_state(T, sc, phase, L.acc);
-  if (L.acc.flags & GBP_F_LIMIT) return true;  // stopped: reported invalid
+__device__ __forceinline__ int stage_phase(int st) {
+  return (st == ST_FWD_FLIGHT || st == ST_REV_FLIGHT) ? GBP_FLIGHT : GBP_STANCE;
+}
+// the sample time of a lane's current stage
+__device__ __forceinline__ double stage_time(const Lane &L) {
+  return L.stage == ST_FWD_LAND ? L.a[7] : (L.stage == ST_REV_START ? 0.0 : L.t);
+}
+
+// Advance (t, ts) the way a SUCCESSFUL sample of loop stage `st` does in
+// transition() below, and test the loop condition: the time of the next
+// sample if the current one passes.  false: the loop ends (or a one-sample
+// stage).  Used by tail helpers to evaluate an owner's future samples.
+template <bool ADAPTIVE>
+__device__ __forceinline__ bool advance_on_success(int st, const double *a, double &t, double &ts) {
+  switch (st) {
+    case ST_FWD_STANCE:
+      if (ADAPTIVE) { ts += KINEMATICS_RES; t += ts; } else { t += KINEMATICS_RES; }
+      return t <= a[6];
+    case ST_FWD_FLIGHT:
+    case ST_REV_FLIGHT:
+      if (ADAPTIVE) { ts += KINEMATICS_RES; t += ts; } else { t += KINEMATICS_RES; }
+      return t < a[7];
+    case ST_REV_STANCE:
+      if (ADAPTIVE) { ts += KINEMATICS_RES; t -= ts; } else { t -= KINEMATICS_RES; }
+      return t >= 0;
+    default:
+      return false;
+  }
+}
+
+// the reference's control flow after one isValidState result `ok` of the
+// lane's current stage; returns true when the pair is decided
+template <bool ADAPTIVE>
+__device__ __forceinline__ bool transition(Lane &L, bool ok) {
   const double step = ADAPTIVE ? 0.0 : KINEMATICS_RES;  // plain loops: constant increment
   switch (L.stage) {
     case ST_FWD_STANCE:
@@ -335,28 +365,81 @@ __device__ __forceinline__ bool step_lane(const TerrainView<ZT> &T, Lane &L) {
   }
 }
 
+// index of the n-th (0-based) set bit of m; requires n < popcount(m)
+__device__ __forceinline__ int nth_set_bit(unsigned long long m, int n) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const unsigned long long low = (1ull << w) - 1ull;
+    const int c = __popcll(m & low);
+    if (n >= c) {
+      n -= c;
+      m >>= w;
+      pos += w;
+    } else {
+      m &= low;
+    }
+  }
+  return pos;
+}
+
+// one sample of the lane's own attempt (the non-helper path)
+template <class ZT, bool ADAPTIVE>
+__device__ __forceinline__ bool step_lane(const TerrainView<ZT> &T, Lane &L) {
+  double sc[8];
+  sample_state(L, L.stage, stage_time(L), sc);
+  const bool ok = is_valid_state(T, sc, stage_phase(L.stage), L.acc);
+  if (L.acc.flags & GBP_F_LIMIT) return true;  // stopped: reported invalid
+  return transition<ADAPTIVE>(L, ok);
+}
+
+#ifdef GBP_DIAG_UTIL
+__device__ unsigned long long gbp_diag[4];
+extern "C" int gbp_diag_read(unsigned long long *out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gbp_diag), sizeof(unsigned long long) * 4) != hipSuccess)
+    return -4;
+  if (reset) {
+    unsigned long long z[4] = {0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(gbp_diag), z, sizeof z) != hipSuccess) return -4;
+  }
+  return 0;
+}
+#endif
+
 template <class ZT, bool ADAPTIVE, int W, bool LDSC>
 __global__ __launch_bounds__(256, W) void k_validate_persistent(
     TerrainView<ZT> T0, int n, const double *__restrict__ S, const double *__restrict__ A,
     const uint8_t *__restrict__ dir, int dir_all, uint8_t *__restrict__ valid,
     double *__restrict__ s_new, double *__restrict__ t_new, uint32_t *__restrict__ flags,
-    uint32_t *__restrict__ counts, unsigned int *__restrict__ head, int sched, int chunk) {
+    uint32_t *__restrict__ counts, unsigned int *__restrict__ head, int sched, int chunk,
+    int helpers) {
   const TerrainView<ZT> T = LDSC ? stage_coords(T0, gbp_smem) : T0;
   const int lane = threadIdx.x & (WAVE - 1);
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
+#ifdef GBP_DIAG_UTIL
+  const unsigned long long t_begin = wall_clock64();
+#endif
   Lane L;
   L.stage = ST_IDLE;
   bool exhausted = false;
   // work source (wave-uniform): [cur, end) is the range this wave hands out
   // to its idle lanes.  sched 1: a fixed per-wave slice, no atomics at all;
   // sched 0 / 2: slices of `chunk` (0 = exactly the lanes that need one)
-  // dequeued from one device-scope counter (MI355X_MICROARCH.md 'dequeue').
+  // dequeued from one device-scope counter (MI355X_MICROARCH.md 'dequeue');
+  // sched 3: the first half of the attempts as fixed per-wave slices, the
+  // second half in chunks of `chunk` from the counter, each dequeue issued one
+  // refill AHEAD so its latency hides under the samples (balances the waves'
+  // unequal sample totals without stalling on the atomic).
   unsigned int cur = 0, end = 0;
-  if (sched == 1) {
+  const unsigned int n_static = sched == 3 ? (unsigned int)n / 2u : (unsigned int)n;
+  const unsigned int csz = chunk > 0 ? (unsigned int)chunk : 32u;
+  unsigned int nxt = 0xFFFFFFFFu;  // prefetched dynamic chunk (sched 3, lane 0)
+  if (sched == 1 || sched == 3) {
     const unsigned int waves = gridDim.x * (blockDim.x / WAVE);
     const unsigned int wid = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
-    cur = (unsigned int)(((unsigned long long)n * wid) / waves);
-    end = (unsigned int)(((unsigned long long)n * (wid + 1)) / waves);
+    cur = (unsigned int)(((unsigned long long)n_static * wid) / waves);
+    end = (unsigned int)(((unsigned long long)n_static * (wid + 1)) / waves);
+    if (sched == 3 && lane == 0) nxt = n_static + atomicAdd(head, csz);
   }
   for (;;) {
     const bool need = (L.stage == ST_IDLE) && !exhausted;
@@ -364,8 +447,12 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
     while (m) {
       if (cur >= end) {
         unsigned int base = 0xFFFFFFFFu;
-        const unsigned int grab = chunk > 0 ? (unsigned int)chunk : (unsigned int)__popcll(m);
-        if (sched != 1) {
+        const unsigned int grab = sched == 3 ? csz
+                                  : (chunk > 0 ? (unsigned int)chunk : (unsigned int)__popcll(m));
+        if (sched == 3) {
+          base = __shfl(nxt, 0);
+          if (lane == 0 && base < (unsigned int)n) nxt = n_static + atomicAdd(head, csz);
+        } else if (sched != 1) {
           const int leader = __ffsll((long long)m) - 1;
           if (lane == leader) base = atomicAdd(head, grab);
           base = __shfl(base, leader);
@@ -377,7 +464,7 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
         cur = base;
         end = min(base + grab, (unsigned int)n);
       }
-      const unsigned int take = min(end - cur, (unsigned int)__popcll(m));
+    const unsigned int take = min(end - cur, (unsigned int)__popcll(m));
       const unsigned int rank = (unsigned int)__popcll(m & lt_mask);
       const bool mine = ((m >> lane) & 1ull) && rank < take;
       if (mine) {
@@ -397,9 +484,91 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
       cur += take;
       m &= ~__ballot(mine);
     }
-    if (!__any(L.stage != ST_IDLE)) break;
-    if (L.stage != ST_IDLE) {
-      if (step_lane<ZT, ADAPTIVE>(T, L)) {
+    const unsigned long long act = __ballot(L.stage != ST_IDLE);
+    if (!act) break;
+    const bool owner = L.stage != ST_IDLE;
+    // ---- the sample each lane evaluates this step --------------------------
+    // Normally a lane evaluates its own attempt's next sample.  In a wave's
+    // tail (no work left to refill idle lanes) the idle lanes become helpers:
+    // helper j of owner r evaluates the owner's sample `slot` steps ahead,
+    // assuming the samples in between pass (advance_on_success); the owner
+    // then consumes the results in order and stops at the first failure or
+    // stage change, so exactly the reference's samples are counted.
+    const int n_act = __popcll(act);
+    const bool tail = helpers && n_act < WAVE;  // every idle lane is exhausted here
+    int st = L.stage, slot = 0;
+    double t_eval = owner ? stage_time(L) : 0.0;
+    uint32_t vbase = L.acc.V;
+    bool has = owner;
+    if (tail) {
+      const unsigned long long idle = ~act;
+      const int j = __popcll(idle & lt_mask);
+      const int src = owner ? lane : nth_set_bit(act, j % n_act);
+      slot = owner ? 0 : 1 + j / n_act;
+#pragma unroll
+      for (int k = 0; k < 8; k++) L.s[k] = __shfl(L.s[k], src);
+#pragma unroll
+      for (int k = 0; k < 10; k++) L.a[k] = __shfl(L.a[k], src);
+      st = __shfl(L.stage, src);
+      double t = __shfl(L.t, src), ts = __shfl(L.ts, src);
+      vbase = __shfl(L.acc.V, src);
+      if (!owner) {
+        has = true;
+        for (int k = 0; k < slot && has; k++) has = advance_on_success<ADAPTIVE>(st, L.a, t, ts);
+        t_eval = t;
+      }
+    }
+#ifdef GBP_DIAG_UTIL  // diagnostic build: lane utilisation of the sample steps
+    {
+      const unsigned long long busy = __ballot(has);
+      if (lane == 0) {
+        atomicAdd(&gbp_diag[0], 1ull);
+        atomicAdd(&gbp_diag[1], (unsigned long long)__popcll(busy));
+      }
+    }
+#endif
+    Acc acc_s{0, vbase + (uint32_t)slot, 0};
+    bool ok = false;
+    if (has) {
+      double sc[8];
+      sample_state(L, st, t_eval, sc);
+      ok = is_valid_state(T, sc, stage_phase(st), acc_s);
+    }
+    bool decided = false;
+    if (owner) {  // the lane's own sample
+      L.acc.G += acc_s.G;
+      L.acc.V = acc_s.V;
+      L.acc.flags |= acc_s.flags;
+      decided = (acc_s.flags & GBP_F_LIMIT) ? true : transition<ADAPTIVE>(L, ok);
+    }
+    if (tail) {  // consume helper results in slot order
+      const unsigned long long idle = ~act;
+      const int n_idle = WAVE - n_act;
+      const uint32_t w0 = (acc_s.flags & 0xFFFFu) | (ok ? 1u << 16 : 0u) | (has ? 1u << 17 : 0u) |
+                          ((acc_s.V - (vbase + (uint32_t)slot)) << 18);
+      const uint32_t w1 = acc_s.G;
+      const int my_rank = __popcll(act & lt_mask);
+      bool chain = owner && !decided && ok && L.stage == st;
+      const int kmax = (n_idle + n_act - 1) / n_act;
+      for (int k = 1; k <= kmax; k++) {
+        const int j = (k - 1) * n_act + my_rank;
+        const bool exists = owner && j < n_idle;
+        const int src = exists ? nth_set_bit(idle, j) : lane;
+        const uint32_t r0 = __shfl(w0, src), r1 = __shfl(w1, src);
+        if (chain && exists && ((r0 >> 17) & 1u)) {
+          L.acc.G += r1;
+          L.acc.V += (r0 >> 18) & 1u;
+          L.acc.flags |= r0 & 0xFFFFu;
+          const bool okk = (r0 >> 16) & 1u;
+          decided = (r0 & GBP_F_LIMIT) ? true : transition<ADAPTIVE>(L, okk);
+          chain = !decided && okk && L.stage == st;
+        } else {
+          chain = false;
+        }
+      }
+    }
+    if (owner) {
+      if (decided) {
         const size_t i = (size_t)L.idx;
         uint32_t f = L.f | L.acc.flags;
         if (L.snew_kind != SN_NONE) f |= GBP_F_SNEW_SET;
@@ -420,6 +589,13 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
       }
     }
   }
+#ifdef GBP_DIAG_UTIL
+  if (lane == 0) {
+    const unsigned long long dt = wall_clock64() - t_begin;
+    atomicAdd(&gbp_diag[2], dt);
+    atomicMax(&gbp_diag[3], dt);
+  }
+#endif
 }
 
 // ============================================================================
@@ -615,7 +791,9 @@ struct gbp_terrain {
   int64_t opt_lds_coords = 1;       // stage the coordinate vectors in LDS when they fit
   int64_t opt_sched = 1;            // persistent work source: 0 atomic, 1 static, 2 chunked
   int64_t opt_chunk = 0;            // dequeue granularity for sched 0/2 (0 = per need)
+  int64_t opt_helpers = 1;          // idle lanes of a drained wave evaluate owners' next samples
   unsigned int *d_head = nullptr;   // persistent-kernel work counter (zeroed per launch)
+  size_t lds_max = 65536;           // LDS bytes a workgroup may use
   hipStream_t host_stream = nullptr;
   void *ws = nullptr;               // grow-only device workspace
   size_t ws_bytes = 0;
@@ -691,7 +869,7 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
                       double *t_new, uint32_t *flags, uint32_t *counts, hipStream_t st) {
   const TerrainView<ZT> T = view<ZT>(t);
   const int block = (int)t->opt_block;
-  const size_t lds = LDSC ? sizeof(double) * (size_t)(t->nx + t->ny) : 0;
+  const size_t lds = LDSC ? stage_bytes(t->nx, t->ny) : 0;
   const int64_t chunk = (int64_t)1 << 30;
   const int64_t want = (int64_t)t->num_cus * t->opt_grid_per_cu;
   for (int64_t off = 0; off < n; off += chunk) {
@@ -711,11 +889,13 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
       // persistent: grid sized to residency; the work counter is zeroed per launch
       const int64_t resident = (int64_t)t->num_cus * std::max<int64_t>(1, W * 256 / block);
       const int64_t g = std::max<int64_t>(
-          1, std::min<int64_t>(t->opt_sched == 1 ? resident : want, (m + block - 1) / block));
+          1, std::min<int64_t>(t->opt_sched == 1 || t->opt_sched == 3 ? resident : want,
+                               (m + block - 1) / block));
       if (t->opt_sched != 1) HIPCHK(hipMemsetAsync(t->d_head, 0, sizeof(unsigned int), st));
       hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, LDSC>), dim3((unsigned)g), dim3(block),
                          lds, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
-                         flags + off, c, t->d_head, (int)t->opt_sched, (int)t->opt_chunk);
+                         flags + off, c, t->d_head, (int)t->opt_sched, (int)t->opt_chunk,
+                         (int)t->opt_helpers);
     }
     HIPCHK(hipGetLastError());
   }
@@ -733,7 +913,7 @@ int launch_validate(gbp_terrain *t, int64_t n, const double *s, const double *a,
           : launch_validate_w<ZT, AD, W, false>(t, n, s, a, dir, dir_all, valid, s_new, t_new, \
                                                 flags, counts, st))
   const int64_t w = t->opt_waves;
-  const bool lds_ok = t->opt_lds_coords && sizeof(double) * (size_t)(t->nx + t->ny) <= 65536;
+  const bool lds_ok = t->opt_lds_coords && stage_bytes(t->nx, t->ny) <= t->lds_max;
   if (adaptive) return w >= 4 ? GBP_LV(true, 4) : (w >= 2 ? GBP_LV(true, 2) : GBP_LV(true, 1));
   return w >= 4 ? GBP_LV(false, 4) : (w >= 2 ? GBP_LV(false, 2) : GBP_LV(false, 1));
 #undef GBP_LV
@@ -911,6 +1091,12 @@ int gbp_terrain_create(int device, int nx, int ny, const double *x, const double
     }
   }
   if (hipMalloc((void **)&t->d_head, 256) != hipSuccess) return fail(GBP_E_ALLOC);
+  {
+    int lm = 0;
+    if (hipDeviceGetAttribute(&lm, hipDeviceAttributeMaxSharedMemoryPerBlock, device) ==
+            hipSuccess && lm > 0)
+      t->lds_max = (size_t)lm;
+  }
   if (hipStreamCreateWithFlags(&t->host_stream, hipStreamNonBlocking) != hipSuccess)
     return fail(GBP_E_HIP);
   (void)rc;
@@ -964,12 +1150,15 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
       t->opt_lds_coords = value ? 1 : 0;
       return GBP_OK;
     case GBP_OPT_SCHED:
-      if (value < 0 || value > 2) return GBP_E_INVALID_ARG;
+      if (value < 0 || value > 3) return GBP_E_INVALID_ARG;
       t->opt_sched = value;
       return GBP_OK;
     case GBP_OPT_CHUNK:
       if (value < 0 || value > 65536) return GBP_E_INVALID_ARG;
       t->opt_chunk = value;
+      return GBP_OK;
+    case GBP_OPT_HELPERS:
+      t->opt_helpers = value ? 1 : 0;
       return GBP_OK;
     default:
       return GBP_E_INVALID_ARG;
@@ -987,6 +1176,7 @@ int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value) {
     case GBP_OPT_LDS_COORDS: *value = t->opt_lds_coords; return GBP_OK;
     case GBP_OPT_SCHED: *value = t->opt_sched; return GBP_OK;
     case GBP_OPT_CHUNK: *value = t->opt_chunk; return GBP_OK;
+    case GBP_OPT_HELPERS: *value = t->opt_helpers; return GBP_OK;
     default: return GBP_E_INVALID_ARG;
   }
 }
@@ -999,8 +1189,8 @@ int gbp_height_batch_dev(gbp_terrain *t, int64_t n, const double *xy, double *he
   if (n == 0) return GBP_OK;
   DeviceGuard g(t->device);
   if (((uintptr_t)xy) % 16) return GBP_E_INVALID_ARG;  // xy is read as double2
-  const size_t cbytes = sizeof(double) * (size_t)(t->nx + t->ny);
-  const bool lds = t->opt_lds_coords && cbytes <= 65536;
+  const size_t cbytes = stage_bytes(t->nx, t->ny);
+  const bool lds = t->opt_lds_coords && cbytes <= t->lds_max;
   // enough workgroups to cover the LDS staging cost many times over
   const unsigned grid = grid_for(n, 256, t->num_cus * 8);
   const double2 *p = (const double2 *)xy;

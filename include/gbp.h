@@ -122,8 +122,11 @@ int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage,
 #define GBP_OPT_WAVES         4  /* register budget: min waves per SIMD (1, 2 or 4)   */
 #define GBP_OPT_LDS_COORDS    5  /* 1: stage coordinate vectors in LDS when they fit  */
 #define GBP_OPT_SCHED         6  /* persistent work source: 0 one atomic counter,
-                                    1 static per-wave slices, 2 chunked counter      */
+                                    1 static per-wave slices, 2 chunked counter,
+                                    3 half static + prefetched counter chunks        */
 #define GBP_OPT_CHUNK         7  /* attempts per dequeue for sched 0 / 2 (0 = per need) */
+#define GBP_OPT_HELPERS       8  /* 1: a drained wave's idle lanes evaluate the remaining
+                                    attempts' next samples ahead (default 1)          */
 #define GBP_KERNEL_DIRECT     0  /* one lane per attempt                              */
 #define GBP_KERNEL_PERSISTENT 1  /* persistent waves, lanes re-packed per sample      */
 int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value);
