@@ -215,21 +215,82 @@ __device__ __forceinline__ void enter_stage(Lane &L, int st) {
 
 // the state the reference evaluates at time t of a stage (the take-off state
 // s_takeoff of :732 / :849 recomputed from (s, a): the same closed form and
-// operands, hence the same bits)
+// operands, hence the same bits).
+//
+// Every stage but the reverse flight needs one stance closed form
+// (applyStance at t or t_s, or applyStanceReverse at t) and each of those has
+// eight divisions by 6 t_s / 2 t_s.  Lanes of one wave sit in different
+// stages, so the numerators are formed per stage (divergent, cheap), the
+// eight divisions run ONCE for the whole wave (converged), and the stage's
+// own sums finish the state — the expression trees of apply_stance /
+// apply_stance_reverse (gbp_device.h), split at the quotient.
 __device__ __forceinline__ void sample_state(const Lane &L, int stage, double t, double *o) {
-  double b[8];
-  switch (stage) {
-    case ST_FWD_STANCE: apply_stance(L.s, L.a, t, o); return;
-    case ST_REV_FLIGHT: apply_flight(L.s, -t, o); return;
-    case ST_FWD_FLIGHT:
-    case ST_FWD_LAND:  // applyFlight(applyStance(s, a), t)
-      apply_stance(L.s, L.a, L.a[6], b);
-      apply_flight(b, t, o);
-      return;
-    default:  // ST_REV_STANCE / ST_REV_START: applyStanceReverse(applyFlight(s, -t_f), a, t)
-      apply_flight(L.s, -L.a[7], b);
-      apply_stance_reverse(b, L.a, t, o);
-      return;
+  const double *a = L.a;
+  if (stage == ST_REV_FLIGHT) {  // applyFlight(s, -t)
+    apply_flight(L.s, -t, o);
+    return;
+  }
+  const bool rev = (stage == ST_REV_STANCE || stage == ST_REV_START);
+  const double t_s = a[6];
+  double b[8];  // the state the stance form starts from
+  double tt;    // its time argument
+  if (rev) {
+    apply_flight(L.s, -a[7], b);  // s_to = applyFlight(s, -t_f)
+    tt = t;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; k++) b[k] = L.s[k];
+    tt = (stage == ST_FWD_STANCE) ? t : t_s;
+  }
+  // numerators: applyStance (a_to - a_td) * (t*t*t) and (a_to - a_td) * t * t;
+  // applyStanceReverse (a_to - a_td) * d3 and (a_to - a_td) * d2
+  const double d1 = t_s - tt, d2 = t_s * t_s - tt * tt, d3 = t_s * t_s * t_s - tt * tt * tt;
+  const double t3 = tt * tt * tt;
+  const int ax[4] = {0, 1, 2, 8}, ao[4] = {3, 4, 5, 9};
+  double n6[4], n2[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const double da = a[ao[k]] - a[ax[k]];
+    n6[k] = rev ? da * d3 : da * t3;
+    n2[k] = rev ? da * d2 : da * tt * tt;
+  }
+  // the eight divisions, once per wave
+  double q6[4], q2[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    q6[k] = n6[k] / (6.0 * t_s);
+    q2[k] = n2[k] / (2.0 * t_s);
+  }
+  if (rev) {  // planning_utils.cpp:348-364
+    const double cx = b[3] - a[0] * t_s - 0.5 * (a[3] - a[0]) * t_s;
+    const double cy = b[4] - a[1] * t_s - 0.5 * (a[4] - a[1]) * t_s;
+    const double cz = b[5] - a[2] * t_s - 0.5 * (a[5] - a[2]) * t_s;
+    const double cp = b[7] - a[8] * t_s - 0.5 * (a[9] - a[8]) * t_s;
+    o[0] = b[0] - cx * d1 - 0.5 * a[0] * d2 - q6[0];
+    o[1] = b[1] - cy * d1 - 0.5 * a[1] * d2 - q6[1];
+    o[2] = b[2] - cz * d1 - 0.5 * a[2] * d2 - q6[2];
+    o[3] = b[3] - a[0] * d1 - q2[0];
+    o[4] = b[4] - a[1] * d1 - q2[1];
+    o[5] = b[5] - a[2] * d1 - q2[2];
+    o[7] = b[7] - a[8] * d1 - q2[3];
+    o[6] = b[6] - cp * d1 - 0.5 * a[8] * d2 - q6[3];
+    return;
+  }
+  // planning_utils.cpp:262-271
+  double c[8];
+  c[0] = b[0] + b[3] * tt + 0.5 * a[0] * tt * tt + q6[0];
+  c[1] = b[1] + b[4] * tt + 0.5 * a[1] * tt * tt + q6[1];
+  c[2] = b[2] + b[5] * tt + 0.5 * a[2] * tt * tt + q6[2];
+  c[3] = b[3] + a[0] * tt + q2[0];
+  c[4] = b[4] + a[1] * tt + q2[1];
+  c[5] = b[5] + a[2] * tt + q2[2];
+  c[6] = b[6] + b[7] * tt + 0.5 * a[8] * tt * tt + q6[3];
+  c[7] = b[7] + a[8] * tt + q2[3];
+  if (stage == ST_FWD_STANCE) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) o[k] = c[k];
+  } else {  // ST_FWD_FLIGHT / ST_FWD_LAND: applyFlight(applyStance(s, a), t)
+    apply_flight(c, t, o);
   }
 }
 
