@@ -1,10 +1,7 @@
 #!/bin/bash
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest -m gpu -q -x tests > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
-case $rc in 0|1) ;; *) exit $rc;; esac
-timeout -k 10 600 python tools/sweep.py --kernels persistent --waves 2,1 --grid 8 --block 256 --sched 1:0 --rounds 5 > gpurun_out/sweep.txt 2>&1; rc=$?
-cat gpurun_out/sweep.txt
-timeout -k 10 300 python tools/micro.py > gpurun_out/micro.log 2>&1; grep -E "lookups_per_s|states_per_s|median" gpurun_out/micro.log
+PROF_TAG=r01c bash tools/profile.sh || exit $?
+timeout -k 10 600 python bench.py --steps 20 --warmup 3 --cpu-seconds 15 --ttfs-runs 1 --plan-max-time 20 > gpurun_out/bench_full.log 2>&1; rc=$?
+tail -1 gpurun_out/bench_full.log
 exit $rc
