@@ -40,6 +40,7 @@ EXPORTS = [
     "gbp_sample_actions_host",
     "gbp_extend_batch_dev", "gbp_extend_batch_host",
     "gbp_nearest_batch_dev", "gbp_nearest_batch_host",
+    "gbp_neighbors_batch_dev", "gbp_neighbors_batch_host",
 ]
 
 
@@ -98,6 +99,8 @@ def load(path=None):
         "gbp_extend_batch_host": (I, [P, I64, P, P, P, I, I, U64, I64, P, P, P, P, P]),
         "gbp_nearest_batch_dev": (I, [I64, P, I64, P, P, P, P]),
         "gbp_nearest_batch_host": (I, [I64, P, I64, P, P, P]),
+        "gbp_neighbors_batch_dev": (I, [I64, P, I64, P, ctypes.c_double, I, P, P, P]),
+        "gbp_neighbors_batch_host": (I, [I64, P, I64, P, ctypes.c_double, I, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -829,6 +829,88 @@ __global__ __launch_bounds__(256) void k_nearest(int64_t n_query, const double *
   }
 }
 
+// Many queries against a large tree: 256 queries per workgroup (one per
+// thread, held in registers) and the vertices streamed through LDS in tiles
+// of 256, so each vertex is read from L2 once per 256 queries instead of once
+// per query.  Same distance, same strict-< scan in ascending index order.
+__global__ __launch_bounds__(256) void k_nearest_tiled(int64_t n_query,
+                                                       const double *__restrict__ q,
+                                                       int64_t n_vert,
+                                                       const double *__restrict__ v,
+                                                       int32_t *__restrict__ idx,
+                                                       double *__restrict__ dist) {
+  __shared__ double tile[256 * 8];
+  const int64_t qi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const bool live = qi < n_query;
+  double qq[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) qq[k] = live ? q[8 * qi + k] : 0.0;
+  double best = INFINITY;
+  int bi = 0;  // nothing < INFINITY: the reference keeps index 0
+  for (int64_t j0 = 0; j0 < n_vert; j0 += 256) {
+    const int cnt = (int)min<int64_t>(256, n_vert - j0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < cnt * 8; e += blockDim.x) tile[e] = v[8 * j0 + e];
+    __syncthreads();
+    for (int j = 0; j < cnt; j++) {
+      const double c = state_distance(qq, tile + 8 * j);
+      if (c < best) {
+        best = c;
+        bi = (int)(j0 + j);
+      }
+    }
+  }
+  if (live) {
+    idx[qi] = bi;
+    if (dist) dist[qi] = best;
+  }
+}
+
+// PlannerClass::neighborhoodDist (planner_class.cpp:173-182): the vertices
+// with 0 < stateDistance(q, v) <= radius, in ascending vertex index (the
+// reference iterates an unordered_map; the engine fixes index order, H9).
+// One workgroup per query; out[q][0..max_out) holds the first max_out
+// neighbours, count[q] the total (may exceed max_out).
+__global__ __launch_bounds__(256) void k_neighbors(int64_t n_query, const double *__restrict__ q,
+                                                   int64_t n_vert, const double *__restrict__ v,
+                                                   double radius, int max_out,
+                                                   int32_t *__restrict__ out,
+                                                   int32_t *__restrict__ count) {
+  __shared__ int wave_cnt[256 / WAVE];
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int64_t qi = blockIdx.x; qi < n_query; qi += gridDim.x) {
+    double qq[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) qq[k] = q[8 * qi + k];
+    int base = 0;
+    for (int64_t j0 = 0; j0 < n_vert; j0 += blockDim.x) {
+      const int64_t j = j0 + threadIdx.x;
+      bool hit = false;
+      if (j < n_vert) {
+        const double d = state_distance(qq, v + 8 * j);
+        hit = (d <= radius) && (d > 0);
+      }
+      const unsigned long long m = __ballot(hit);
+      if (lane == 0) wave_cnt[w] = __popcll(m);
+      __syncthreads();
+      int off = base;
+      int total = 0;
+      for (int k = 0; k < (int)(blockDim.x / WAVE); k++) {
+        if (k < w) off += wave_cnt[k];
+        total += wave_cnt[k];
+      }
+      if (hit) {
+        const int pos = off + __popcll(m & lt);
+        if (pos < max_out) out[qi * (int64_t)max_out + pos] = (int32_t)j;
+      }
+      base += total;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) count[qi] = base;
+  }
+}
+
 }  // namespace
 
 // ============================================================================
@@ -1406,9 +1488,31 @@ int gbp_nearest_batch_dev(int64_t n_query, const double *queries, int64_t n_vert
   if (n_vert > 0x7FFFFFFE) return GBP_E_SHAPE;
   if (n_query == 0) return GBP_OK;
   if (n_vert > 0 && !vertices) return GBP_E_INVALID_ARG;
+  if (n_query >= 512 && n_vert >= 256) {  // many queries: vertex tiles shared through LDS
+    const unsigned grid = (unsigned)((n_query + 255) / 256);
+    hipLaunchKernelGGL(k_nearest_tiled, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_query,
+                       queries, n_vert, vertices, index, dist);
+  } else {  // few queries: one workgroup scans the tree per query
+    const unsigned grid = (unsigned)std::min<int64_t>(n_query, 65535);
+    hipLaunchKernelGGL(k_nearest, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_query,
+                       queries, n_vert, vertices, index, dist);
+  }
+  HIPCHK(hipGetLastError());
+  return GBP_OK;
+}
+
+int gbp_neighbors_batch_dev(int64_t n_query, const double *queries, int64_t n_vert,
+                            const double *vertices, double radius, int max_out, int32_t *out,
+                            int32_t *count, gbp_stream stream) {
+  if (n_query < 0 || n_vert < 0 || max_out < 0 || (n_query > 0 && (!queries || !count)) ||
+      (max_out > 0 && n_query > 0 && !out))
+    return GBP_E_INVALID_ARG;
+  if (n_vert > 0x7FFFFFFE) return GBP_E_SHAPE;
+  if (n_query == 0) return GBP_OK;
+  if (n_vert > 0 && !vertices) return GBP_E_INVALID_ARG;
   const unsigned grid = (unsigned)std::min<int64_t>(n_query, 65535);
-  hipLaunchKernelGGL(k_nearest, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_query, queries,
-                     n_vert, vertices, index, dist);
+  hipLaunchKernelGGL(k_neighbors, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_query, queries,
+                     n_vert, vertices, radius, max_out, out, count);
   HIPCHK(hipGetLastError());
   return GBP_OK;
 }
@@ -1619,6 +1723,36 @@ int gbp_nearest_batch_host(int64_t n_query, const double *queries, int64_t n_ver
   if (!rc && hipMemcpy(index, di, 4 * n_query, hipMemcpyDeviceToHost) != hipSuccess)
     rc = GBP_E_HIP;
   if (!rc && dist && hipMemcpy(dist, dd, 8 * n_query, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = GBP_E_HIP;
+  (void)hipFree(buf);
+  return rc;
+}
+
+int gbp_neighbors_batch_host(int64_t n_query, const double *queries, int64_t n_vert,
+                             const double *vertices, double radius, int max_out, int32_t *out,
+                             int32_t *count) {
+  if (n_query <= 0) return n_query == 0 ? GBP_OK : GBP_E_INVALID_ARG;
+  if (!queries || !count || max_out < 0 || (max_out > 0 && !out) || (n_vert > 0 && !vertices))
+    return GBP_E_INVALID_ARG;
+  void *buf = nullptr;
+  const size_t nout = (size_t)n_query * (size_t)max_out;
+  const size_t need = rnd(64 * n_query) + rnd(64 * (n_vert > 0 ? n_vert : 1)) +
+                      rnd(4 * (nout > 0 ? nout : 1)) + rnd(4 * n_query) + 1024;
+  if (hipMalloc(&buf, need) != hipSuccess) return GBP_E_ALLOC;
+  char *p = (char *)buf;
+  double *dq = (double *)p; p += rnd(64 * n_query);
+  double *dv = (double *)p; p += rnd(64 * (n_vert > 0 ? n_vert : 1));
+  int32_t *dout = (int32_t *)p; p += rnd(4 * (nout > 0 ? nout : 1));
+  int32_t *dc = (int32_t *)p;
+  int rc = GBP_OK;
+  if (hipMemcpy(dq, queries, 64 * n_query, hipMemcpyHostToDevice) != hipSuccess) rc = GBP_E_HIP;
+  if (!rc && n_vert > 0 &&
+      hipMemcpy(dv, vertices, 64 * n_vert, hipMemcpyHostToDevice) != hipSuccess)
+    rc = GBP_E_HIP;
+  if (!rc) rc = gbp_neighbors_batch_dev(n_query, dq, n_vert, dv, radius, max_out, dout, dc, nullptr);
+  if (!rc && nout > 0 && hipMemcpy(out, dout, 4 * nout, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = GBP_E_HIP;
+  if (!rc && hipMemcpy(count, dc, 4 * n_query, hipMemcpyDeviceToHost) != hipSuccess)
     rc = GBP_E_HIP;
   (void)hipFree(buf);
   return rc;

@@ -266,6 +266,21 @@ def nearest(queries, vertices):
     return idx, dist
 
 
+def neighbors(queries, vertices, radius, max_out=256):
+    """Batched PlannerClass::neighborhoodDist (planner_class.cpp:173-182):
+    (idx [n, max_out] int32, -1 padded, ascending vertex index; count [n])."""
+    lib = L.load()
+    q = queries.contiguous()
+    v = vertices.contiguous()
+    n = q.shape[0]
+    out = torch.full((n, max_out), -1, dtype=torch.int32, device=q.device)
+    cnt = torch.empty(n, dtype=torch.int32, device=q.device)
+    check(lib.gbp_neighbors_batch_dev(n, _ptr(q), v.shape[0], _ptr(v), float(radius), max_out,
+                                      _ptr(out), _ptr(cnt), _stream(q.device.index or 0)),
+          "neighbors")
+    return out, cnt
+
+
 def device_count():
     lib = L.load()
     c = ctypes.c_int(0)

@@ -232,6 +232,18 @@ int gbp_nearest_batch_dev(int64_t n_query, const double *queries, int64_t n_vert
 int gbp_nearest_batch_host(int64_t n_query, const double *queries, int64_t n_vert,
                            const double *vertices, int32_t *index, double *dist);
 
+/* ---- radius neighbourhood (PlannerClass::neighborhoodDist,
+ *      planner_class.cpp:173-182; used by RRT*-Connect, rrt_star_connect.cpp:28)
+ * out[i][0..max_out): the vertices with 0 < stateDistance(query_i, v) <= radius
+ * in ascending index (the reference: unordered_map order);
+ * count[i] = how many there are (entries beyond max_out are not written). */
+int gbp_neighbors_batch_dev(int64_t n_query, const double *queries, int64_t n_vert,
+                            const double *vertices, double radius, int max_out, int32_t *out,
+                            int32_t *count, gbp_stream stream);
+int gbp_neighbors_batch_host(int64_t n_query, const double *queries, int64_t n_vert,
+                             const double *vertices, double radius, int max_out, int32_t *out,
+                             int32_t *count);
+
 #ifdef __cplusplus
 }
 #endif

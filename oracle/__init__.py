@@ -75,6 +75,7 @@ def lib():
             "orc_normal_batch": (None, [P, I64, P, P, P, I]),
             "orc_extend_batch": (None, [P, I64, P, P, P, P, I, I, P, P, P, P, P, I]),
             "orc_nearest_batch": (None, [I64, P, I, P, P, P, I]),
+            "orc_neighbors_batch": (None, [I64, P, I, P, D, I, P, P, I]),
             "orc_sample_states": (None, [P, I64, U64, U64, I64, I, I, P, P, I]),
             "orc_sample_actions": (None, [I64, P, U64, U64, I64, P, I]),
             "orc_philox4x32_10": (None, [P, P, P]),
@@ -241,6 +242,17 @@ def nearest_batch(queries, verts, nthreads=1):
     dist = np.empty(q.shape[0])
     lib().orc_nearest_batch(q.shape[0], _p(q), v.shape[0], _p(v), _p(idx), _p(dist), nthreads)
     return idx, dist
+
+
+def neighbors_batch(queries, verts, radius, max_out=256, nthreads=1):
+    """planner_class.cpp:173-182, ascending index: (out [n, max_out] -1 padded, count [n])."""
+    q = _c(queries, np.float64).reshape(-1, 8)
+    v = _c(verts, np.float64).reshape(-1, 8)
+    out = np.full((q.shape[0], max_out), -1, np.int32)
+    cnt = np.empty(q.shape[0], np.int32)
+    lib().orc_neighbors_batch(q.shape[0], _p(q), v.shape[0], _p(v), float(radius), int(max_out),
+                              _p(out), _p(cnt), nthreads)
+    return out, cnt
 
 
 def apply_stance(s, a, t):

@@ -712,6 +712,26 @@ void orc_nearest_batch(int64_t n_q, const double *q, int n_vert, const double *v
   }
 }
 
+/* PlannerClass::neighborhoodDist (planner_class.cpp:173-182): vertices with
+ * stateDistance <= dist and > 0, in ascending index (the engine's order; the
+ * reference iterates an unordered_map) */
+void orc_neighbors_batch(int64_t n_q, const double *q, int n_vert, const double *verts,
+                         double radius, int max_out, int32_t *out, int32_t *count, int nthreads) {
+  if (nthreads <= 0) nthreads = 1;
+  OMP_FOR
+  for (int64_t i = 0; i < n_q; i++) {
+    int c = 0;
+    for (int v = 0; v < n_vert; v++) {
+      if ((orc_state_distance(q + 8 * i, verts + (long)v * 8) <= radius) &&
+          orc_state_distance(q + 8 * i, verts + (long)v * 8) > 0) {
+        if (c < max_out) out[i * (int64_t)max_out + c] = v;
+        c++;
+      }
+    }
+    count[i] = c;
+  }
+}
+
 /* ---- Philox4x32-10 (Salmon et al., SC'11) ------------------------------- */
 static inline void mulhilo32(uint32_t a, uint32_t b, uint32_t *hi, uint32_t *lo) {
   uint64_t p = (uint64_t)a * b;

@@ -114,6 +114,8 @@ void orc_extend_batch(const orc_terrain *T, int64_t n, const double *s_near,
                       uint32_t *counts, int nthreads);
 void orc_nearest_batch(int64_t n_q, const double *q, int n_vert, const double *verts,
                        int32_t *idx, double *dist, int nthreads);
+void orc_neighbors_batch(int64_t n_q, const double *q, int n_vert, const double *verts,
+                         double radius, int max_out, int32_t *out, int32_t *count, int nthreads);
 
 /* ---- counter-based samplers (Philox4x32-10), same keys as the engine ---- */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

@@ -245,9 +245,34 @@ def test_nearest_parity(gpu):
     assert np.array_equal(np_(idx), ri)
     assert np.array_equal(bits(np_(dist)), bits(rd))
     assert np_(idx)[-3] == 7 and np_(idx)[-2] == 7
+    # few queries take the one-workgroup-per-query kernel, many the LDS-tiled one
+    i2, d2 = gbp.nearest(torch.from_numpy(q[:100]).cuda(), torch.from_numpy(verts).cuda())
+    assert np.array_equal(np_(i2), ri[:100]) and np.array_equal(bits(np_(d2)), bits(rd[:100]))
+    qn = q[:600].copy()
+    qn[5] = np.nan                 # NaN query: no distance is < inf -> index 0
+    i3, _ = gbp.nearest(torch.from_numpy(qn).cuda(), torch.from_numpy(verts[:300]).cuda())
+    r3, _ = oracle.nearest_batch(qn, verts[:300])
+    assert np.array_equal(np_(i3), r3) and np_(i3)[5] == 0
     # empty tree keeps index 0 with +inf, like the reference's initial values
     idx0, d0 = gbp.nearest(torch.from_numpy(q[:4]).cuda(), torch.empty((0, 8), dtype=torch.float64).cuda())
     assert np.all(np_(idx0) == 0) and np.all(np.isinf(np_(d0)))
+
+
+def test_neighbors_parity(gpu):
+    """PlannerClass::neighborhoodDist (planner_class.cpp:173-182) on the engine
+    vs the oracle: same members, ascending index, self (distance 0) excluded,
+    counts beyond max_out reported."""
+    import global_body_planner_amd as gbp
+    rng = np.random.default_rng(4)
+    verts = rng.normal(size=(3000, 8)) * 0.8
+    q = np.concatenate([rng.normal(size=(700, 8)) * 0.8, verts[[0, 17, 2999]]])
+    for radius, max_out in ((3.0, 512), (1.5, 16), (0.0, 8)):
+        out, cnt = gbp.neighbors(torch.from_numpy(q).cuda(), torch.from_numpy(verts).cuda(),
+                                 radius, max_out)
+        ro, rc = oracle.neighbors_batch(q, verts, radius, max_out)
+        assert np.array_equal(np_(cnt), rc)
+        assert np.array_equal(np_(out), ro)
+    assert rc.max() <= 3000 and (np_(cnt) > 16).any()   # truncation exercised at max_out 16
 
 
 # ---- full-size, size-independent properties --------------------------------------------
