@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <climits>
 #include <numeric>
 
 namespace gbp_amd {
@@ -392,6 +393,7 @@ PlannerClass::PlannerClass(int device) : device_(device) {}
 PlannerClass::~PlannerClass() {
   if (d_vertices_) gbp_device_free(d_vertices_);
   if (d_scratch_) gbp_device_free(d_scratch_);
+  if (d_nbr_) gbp_device_free(d_nbr_);
 }
 
 PlannerClass::PlannerClass(const PlannerClass &o)
@@ -405,9 +407,12 @@ PlannerClass &PlannerClass::operator=(const PlannerClass &o) {
   if (this == &o) return *this;
   if (d_vertices_) gbp_device_free(d_vertices_);
   if (d_scratch_) gbp_device_free(d_scratch_);
+  if (d_nbr_) gbp_device_free(d_nbr_);
   d_vertices_ = nullptr;
   d_scratch_ = nullptr;
+  d_nbr_ = nullptr;
   d_capacity_ = d_count_ = d_scratch_cap_ = 0;
+  d_nbr_bytes_ = 0;
   device_ = o.device_;
   vertices_ = o.vertices_;
   actions_ = o.actions_;
@@ -458,6 +463,16 @@ void PlannerClass::addEdge(int idx1, int idx2) {  // graph_class.cpp:36-42
   successors_[idx1].push_back(idx2);
   g_[idx2] = g_[idx1] + poseDistance(vertices_[idx1], vertices_[idx2]);
   y_[idx2] = y_[idx1] + stateYawDistance(vertices_[idx1], vertices_[idx2]);
+}
+
+void PlannerClass::removeEdge(int idx1, int idx2) {  // graph_class.cpp:44-58
+  if (parent_[idx2] == idx1) parent_[idx2] = -1;
+  std::vector<int> &succ = successors_[idx1];
+  for (auto it = succ.begin(); it != succ.end(); ++it)
+    if (*it == idx2) {
+      succ.erase(it);
+      break;
+    }
 }
 
 int PlannerClass::getPredecessor(int idx) const { return parent_[idx]; }
@@ -540,11 +555,52 @@ std::vector<int> PlannerClass::getNearestNeighborBatch(const std::vector<State> 
 
 int PlannerClass::getNearestNeighbor(State q) { return getNearestNeighborBatch({q})[0]; }
 
-std::vector<int> PlannerClass::neighborhoodDist(State q, double dist) {  // :173-182
-  std::vector<int> out;
-  for (int i = 0; i < (int)vertices_.size(); i++) {
-    const double d = stateDistance(q, vertices_[i]);
-    if (d <= dist && d > 0) out.push_back(i);
+std::vector<int> PlannerClass::neighborhoodDist(State q, double dist) {  // :173-182 on the engine
+  return neighborhoodDistBatch({q}, dist)[0];
+}
+
+std::vector<std::vector<int>> PlannerClass::neighborhoodDistBatch(const std::vector<State> &q,
+                                                                  double dist,
+                                                                  const std::vector<int> &limit) {
+  std::vector<std::vector<int>> out(q.size());
+  if (q.empty() || vertices_.empty()) return out;
+  sync_device();
+  const int64_t nq = (int64_t)q.size();
+  int max_out = 256;
+  for (int pass = 0; pass < 2; pass++) {
+    const size_t bytes = (size_t)nq * (sizeof(State) + sizeof(int32_t) * (max_out + 1)) + 256;
+    if (bytes > d_nbr_bytes_) {
+      if (d_nbr_) gbp_device_free(d_nbr_);
+      d_nbr_ = nullptr;
+      d_nbr_bytes_ = 0;
+      chk(gbp_device_alloc(device_, bytes, &d_nbr_), "neighbourhood scratch");
+      d_nbr_bytes_ = bytes;
+    }
+    double *dq = (double *)d_nbr_;
+    int32_t *dcnt = (int32_t *)(dq + 8 * nq);
+    int32_t *dout = dcnt + nq;
+    std::vector<int32_t> cnt(nq), lst((size_t)nq * max_out);
+    chk(gbp_memcpy_h2d(dq, q[0].data(), (size_t)nq * sizeof(State), nullptr), "nbr upload");
+    chk(gbp_neighbors_batch_dev(nq, dq, (int64_t)vertices_.size(), d_vertices_, dist, max_out, dout,
+                                dcnt, nullptr),
+        "neighborhoodDist");
+    chk(gbp_memcpy_d2h(cnt.data(), dcnt, (size_t)nq * sizeof(int32_t), nullptr), "nbr count");
+    chk(gbp_memcpy_d2h(lst.data(), dout, lst.size() * sizeof(int32_t), nullptr), "nbr list");
+    chk(gbp_stream_synchronize(nullptr), "nbr sync");
+    int need = 0;
+    for (int64_t i = 0; i < nq; i++) need = std::max(need, (int)cnt[i]);
+    if (need > max_out && pass == 0) {  // a list overflowed: once more with room for all
+      max_out = need;
+      continue;
+    }
+    for (int64_t i = 0; i < nq; i++) {
+      const int lim = limit.empty() ? INT32_MAX : limit[i];
+      for (int k = 0; k < std::min<int>(cnt[i], max_out); k++) {
+        const int v = lst[(size_t)i * max_out + k];
+        if (v < lim) out[i].push_back(v);
+      }
+    }
+    break;
   }
   return out;
 }
@@ -725,7 +781,8 @@ void RRTConnectClass::attemptConnectBatch(const std::vector<State> &s_existing,
                                           const std::vector<State> &s0, std::vector<double> t_s,
                                           FastTerrainMap &terrain, int direction,
                                           std::vector<int> &result, std::vector<State> &s_new,
-                                          std::vector<Action> &a_new, BatchStats *stats) {
+                                          std::vector<Action> &a_new, BatchStats *stats,
+                                          int max_depth) {
   const size_t n = s_existing.size();
   result.assign(n, GBP_PLANNER_TRAPPED);
   s_new.resize(n);
@@ -733,7 +790,7 @@ void RRTConnectClass::attemptConnectBatch(const std::vector<State> &s_existing,
   std::vector<State> s = s0;
   std::vector<int> open(n);
   std::iota(open.begin(), open.end(), 0);
-  for (int depth = 0; !open.empty() && depth <= 64; depth++) {  // oracle's depth guard
+  for (int depth = 0; !open.empty() && depth <= max_depth; depth++) {  // 64: oracle's guard
     std::vector<int> chk_idx;
     std::vector<State> cs;
     std::vector<Action> ca;
@@ -980,9 +1037,12 @@ void RRTConnectClass::buildRRTConnect(FastTerrainMap &terrain, State s_start, St
 
 // one batch-synchronous half-iteration: extend T toward `batch` targets, then
 // connect every new vertex to O (direction of the connect = opposite of dir)
-int RRTConnectClass::halfIterationBatched(PlannerClass &T, PlannerClass &O, FastTerrainMap &terrain,
-                                          int dir, int batch, int &meet_t, int &meet_o,
-                                          BatchStats *stats) {
+void RRTConnectClass::extendBatch(PlannerClass &T, FastTerrainMap &terrain, int dir, int batch,
+                                  std::vector<int> &added, std::vector<int> &nearest,
+                                  std::vector<Action> &a_out, bool insert, BatchStats *stats) {
+  added.clear();
+  nearest.clear();
+  a_out.clear();
   // targets: randomState + isValidState(STANCE) (rrt_connect.cpp:249-254)
   std::vector<State> cand = T.randomStateBatch(terrain, batch);
   std::vector<uint8_t> ok(batch);
@@ -993,7 +1053,7 @@ int RRTConnectClass::halfIterationBatched(PlannerClass &T, PlannerClass &O, Fast
   for (int i = 0; i < batch; i++)
     if (ok[i]) targets.push_back(cand[i]);
   if (stats) stats->targets += (int64_t)targets.size();
-  if (targets.empty()) return 0;
+  if (targets.empty()) return;
   const int64_t n = (int64_t)targets.size();
   // extend (rrt.cpp:77-102), all targets against the current tree snapshot
   std::vector<int> nn = T.getNearestNeighborBatch(targets);
@@ -1011,18 +1071,28 @@ int RRTConnectClass::halfIterationBatched(PlannerClass &T, PlannerClass &O, Fast
     stats->extends += n;
     stats->attempts_checked += 6 * n;
   }
-  std::vector<int> added;
   for (int64_t i = 0; i < n; i++) {
     if (res[i] == GBP_TRAPPED) continue;
     const int idx = T.getNumVertices();
     T.addVertex(idx, s_new[i]);
-    T.addEdge(nn[i], idx);
-    T.addAction(idx, a_new[i]);
-    T.updateGYValue(idx, T.getGValue(nn[i]) + poseDistance(s_near[i], s_new[i]),
-                    T.getYValue(nn[i]) + stateYawDistance(s_near[i], s_new[i]));
+    if (insert) {  // rrt.cpp:86-92
+      T.addEdge(nn[i], idx);
+      T.addAction(idx, a_new[i]);
+      T.updateGYValue(idx, T.getGValue(nn[i]) + poseDistance(s_near[i], s_new[i]),
+                      T.getYValue(nn[i]) + stateYawDistance(s_near[i], s_new[i]));
+    }
     added.push_back(idx);
+    nearest.push_back(nn[i]);
+    a_out.push_back(a_new[i]);
   }
-  if (added.empty()) return 0;
+}
+
+std::vector<std::pair<int, int>> RRTConnectClass::connectBatch(PlannerClass &T, PlannerClass &O,
+                                                               FastTerrainMap &terrain, int dir,
+                                                               const std::vector<int> &added,
+                                                               BatchStats *stats) {
+  std::vector<std::pair<int, int>> reached;
+  if (added.empty()) return reached;
   // connect every new vertex to the other tree (rrt_connect.cpp:98-120)
   std::vector<State> q;
   for (int idx : added) q.push_back(T.getVertex(idx));
@@ -1039,7 +1109,6 @@ int RRTConnectClass::halfIterationBatched(PlannerClass &T, PlannerClass &O, Fast
   std::vector<Action> can(q.size(), Action{});
   attemptConnectBatch(s_ex, q, t_s, terrain, cdir, cres, csn, can, stats);
   if (stats) stats->connects += (int64_t)q.size();
-  int found = 0;
   for (size_t k = 0; k < q.size(); k++) {
     if (cres[k] == GBP_PLANNER_TRAPPED) continue;
     const int idx = O.getNumVertices();
@@ -1048,13 +1117,22 @@ int RRTConnectClass::halfIterationBatched(PlannerClass &T, PlannerClass &O, Fast
     O.addAction(idx, can[k]);
     O.updateGYValue(idx, O.getGValue(nno[k]) + poseDistance(s_ex[k], csn[k]),
                     O.getYValue(nno[k]) + stateYawDistance(s_ex[k], csn[k]));
-    if (cres[k] == GBP_PLANNER_REACHED && !found) {
-      found = 1;
-      meet_t = added[k];
-      meet_o = idx;
-    }
+    if (cres[k] == GBP_PLANNER_REACHED) reached.push_back({added[k], idx});
   }
-  return found;
+  return reached;
+}
+
+int RRTConnectClass::halfIterationBatched(PlannerClass &T, PlannerClass &O, FastTerrainMap &terrain,
+                                          int dir, int batch, int &meet_t, int &meet_o,
+                                          BatchStats *stats) {
+  std::vector<int> added, nearest;
+  std::vector<Action> a_new;
+  extendBatch(T, terrain, dir, batch, added, nearest, a_new, true, stats);
+  const std::vector<std::pair<int, int>> reached = connectBatch(T, O, terrain, dir, added, stats);
+  if (reached.empty()) return 0;
+  meet_t = reached.front().first;
+  meet_o = reached.front().second;
+  return 1;
 }
 
 bool RRTConnectClass::buildRRTConnectBatched(FastTerrainMap &terrain, State s_start, State s_goal,
@@ -1111,6 +1189,276 @@ bool RRTConnectClass::buildRRTConnectBatched(FastTerrainMap &terrain, State s_st
   return true;
 }
 
+// ============================================================================
+// RRTStarConnectClass
+// ============================================================================
+void RRTStarConnectClass::insertStar(PlannerClass &T, FastTerrainMap &terrain, int dir,
+                                     const std::vector<int> &added,
+                                     const std::vector<int> &nearest,
+                                     const std::vector<Action> &a_new, BatchStats *stats) {
+  if (added.empty()) return;
+  // neighbourhoods (rrt_star_connect.cpp:28): vertex k sees the vertices
+  // before it, exactly the tree a sequential insertion would scan
+  std::vector<State> q;
+  for (int idx : added) q.push_back(T.getVertex(idx));
+  const std::vector<std::vector<int>> nb = T.neighborhoodDistBatch(q, delta, added);
+  // every connect the insertion may need, in one lock-step batch: choose-parent
+  // attemptConnect(s_near, s_new) (:36) and rewire attemptConnect(s_new, s_near) (:59)
+  std::vector<State> se, ss;
+  std::vector<double> ts;
+  std::vector<size_t> first(added.size() + 1, 0);
+  for (size_t k = 0; k < added.size(); k++) {
+    first[k] = se.size();
+    for (int j : nb[k]) {
+      const State sn = T.getVertex(j);
+      se.push_back(sn);  // choose-parent
+      ss.push_back(q[k]);
+      ts.push_back(poseDistance(q[k], sn) / V_NOM);
+      se.push_back(q[k]);  // rewire
+      ss.push_back(sn);
+      ts.push_back(poseDistance(sn, q[k]) / V_NOM);
+    }
+  }
+  first[added.size()] = se.size();
+  std::vector<int> res;
+  std::vector<State> dummy(se.size(), State{});
+  std::vector<Action> act(se.size(), Action{});
+  if (!se.empty())
+    attemptConnectBatch(se, ss, ts, terrain, dir, res, dummy, act, stats, /*max_depth=*/0);
+  if (stats) stats->connects += (int64_t)se.size();
+  // sequential replay of rrt_star_connect.cpp:18-66 for each new vertex in order
+  for (size_t k = 0; k < added.size(); k++) {
+    const int s_new_idx = added[k];
+    const State s_new = q[k];
+    const int s_nearest_index = nearest[k];
+    const State s_nearest = T.getVertex(s_nearest_index);
+    int s_min_idx = s_nearest_index;
+    Action a_sel = a_new[k];
+    double g_s_new = T.getGValue(s_nearest_index) + poseDistance(s_new, s_nearest);
+    double y_s_new = T.getYValue(s_nearest_index) + stateYawDistance(s_new, s_nearest);
+    for (size_t i = 0; i < nb[k].size(); i++) {  // choose parent (:31-44)
+      const size_t c = first[k] + 2 * i;
+      if (res[c] != GBP_PLANNER_REACHED) continue;
+      const int j = nb[k][i];
+      const State s_near = T.getVertex(j);
+      const double g_s_near = T.getGValue(j) + poseDistance(s_near, s_new);
+      const double y_s_near = T.getYValue(j) + stateYawDistance(s_near, s_new);
+      if (g_s_near < g_s_new) {
+        a_sel = act[c];
+        s_min_idx = j;
+        g_s_new = g_s_near;
+        y_s_new = y_s_near;
+      }
+    }
+    T.addEdge(s_min_idx, s_new_idx);  // :47-49
+    T.updateGYValue(s_new_idx, g_s_new, y_s_new);
+    T.addAction(s_new_idx, a_sel);
+    for (size_t i = 0; i < nb[k].size(); i++) {  // rewire (:51-66)
+      const int j = nb[k][i];
+      if (j == s_min_idx) continue;
+      const size_t c = first[k] + 2 * i + 1;
+      const State s_near = T.getVertex(j);
+      if (res[c] == GBP_PLANNER_REACHED &&
+          T.getGValue(j) > (T.getGValue(s_new_idx) + poseDistance(s_near, s_new))) {
+        const int s_parent = T.getPredecessor(j);
+        T.removeEdge(s_parent, j);
+        T.addEdge(s_new_idx, j);
+        T.updateGYValue(j, T.getGValue(s_new_idx) + poseDistance(s_near, s_new),
+                        T.getYValue(s_new_idx) + stateYawDistance(s_near, s_new));
+        T.addAction(j, act[c]);
+        rewires_++;
+        if (stats) stats->rewires++;
+      }
+    }
+  }
+}
+
+int RRTStarConnectClass::extend(PlannerClass &T, State s, FastTerrainMap &terrain, int direction) {
+  const int s_nearest_index = T.getNearestNeighbor(s);  // rrt_star_connect.cpp:12-19
+  const State s_nearest = T.getVertex(s_nearest_index);
+  State s_new{};
+  Action a_new{};
+  if (!newConfig(s, s_nearest, s_new, a_new, terrain, direction)) return GBP_PLANNER_TRAPPED;
+  const int s_new_idx = T.getNumVertices();
+  T.addVertex(s_new_idx, s_new);
+  insertStar(T, terrain, direction, {s_new_idx}, {s_nearest_index}, {a_new}, nullptr);
+  return isWithinBounds(s_new, s) ? GBP_PLANNER_REACHED : GBP_PLANNER_ADVANCED;
+}
+
+void RRTStarConnectClass::getStateAndActionSequences(PlannerClass &Ta, PlannerClass &Tb,
+                                                     int shared_a_idx, int shared_b_idx,
+                                                     std::vector<State> &state_sequence,
+                                                     std::vector<Action> &action_sequence) {
+  state_sequence.clear();  // rrt_star_connect.cpp:70-89
+  action_sequence.clear();
+  std::vector<int> path_a = pathFromStart(Ta, shared_a_idx);
+  std::vector<int> path_b = pathFromStart(Tb, shared_b_idx);
+  std::reverse(path_b.begin(), path_b.end());
+  std::vector<Action> action_sequence_b = getActionSequenceReverse(Tb, path_b);
+  path_b.erase(path_b.begin());
+  state_sequence = getStateSequence(Ta, path_a);
+  std::vector<State> sb = getStateSequence(Tb, path_b);
+  state_sequence.insert(state_sequence.end(), sb.begin(), sb.end());
+  action_sequence = getActionSequence(Ta, path_a);
+  action_sequence.insert(action_sequence.end(), action_sequence_b.begin(), action_sequence_b.end());
+}
+
+void RRTStarConnectClass::buildRRTStarConnect(FastTerrainMap &terrain, State s_start, State s_goal,
+                                              std::vector<State> &state_sequence,
+                                              std::vector<Action> &action_sequence,
+                                              double max_time) {  // rrt_star_connect.cpp:91-205
+  const auto t_start = std::chrono::high_resolution_clock::now();
+  success_ = 0;
+  length_vector_.clear();
+  yaw_vector_.clear();
+  cost_vector_.clear();
+  cost_vector_times_.clear();
+  PlannerClass Ta(terrain.device()), Tb(terrain.device());
+  Ta.setStream(seed_, 301);
+  Tb.setStream(seed_, 302);
+  Ta.init(s_start, cost_add_yaw_flag_, cost_add_yaw_length_weight_, cost_add_yaw_yaw_weight_);
+  Tb.init(s_goal, cost_add_yaw_flag_, cost_add_yaw_length_weight_, cost_add_yaw_yaw_weight_);
+  int shared_a_idx = -1, shared_b_idx = -1;
+  std::vector<int> shared_a, shared_b;
+  goal_found = false;
+  wall_to_first_ = -1;
+  const double length_so_far = INFTY, yaw_so_far = INFTY;  // never updated by the reference
+  double cost_so_far = INFTY;
+  while (true) {
+    State s_rand = Ta.randomState(terrain);
+    if (isValidState(s_rand, terrain, STANCE)) {
+      if (extend(Ta, s_rand, terrain, FORWARD) != GBP_PLANNER_TRAPPED) {
+        const State s_new = Ta.getVertex(Ta.getNumVertices() - 1);
+        if (connect(Tb, s_new, terrain, REVERSE) == GBP_PLANNER_REACHED) {
+          if (!goal_found) {
+            elapsed_to_first = std::chrono::high_resolution_clock::now() - t_start;
+            wall_to_first_ = elapsed_to_first.count();
+          }
+          goal_found = true;
+          shared_a.push_back(Ta.getNumVertices() - 1);
+          shared_b.push_back(Tb.getNumVertices() - 1);
+        }
+      }
+    }
+    s_rand = Tb.randomState(terrain);
+    if (isValidState(s_rand, terrain, STANCE)) {
+      if (extend(Tb, s_rand, terrain, REVERSE) != GBP_PLANNER_TRAPPED) {
+        const State s_new = Tb.getVertex(Tb.getNumVertices() - 1);
+        if (connect(Ta, s_new, terrain, FORWARD) == GBP_PLANNER_REACHED) {
+          if (!goal_found) {
+            elapsed_to_first = std::chrono::high_resolution_clock::now() - t_start;
+            wall_to_first_ = elapsed_to_first.count();
+          }
+          goal_found = true;
+          shared_a.push_back(Ta.getNumVertices() - 1);
+          shared_b.push_back(Tb.getNumVertices() - 1);
+        }
+      }
+    }
+    const std::chrono::duration<double> el = std::chrono::high_resolution_clock::now() - t_start;
+    if (goal_found && el.count() >= max_time) break;
+    for (size_t i = 0; i < shared_a.size(); ++i) {
+      const double cost = Ta.getGValue(shared_a[i]) + Tb.getGValue(shared_b[i]);
+      if (cost < cost_so_far) {
+        cost_so_far = cost;
+        shared_a_idx = shared_a[i];
+        shared_b_idx = shared_b[i];
+        length_vector_.push_back(length_so_far);
+        yaw_vector_.push_back(yaw_so_far);
+        cost_vector_.push_back(cost_so_far);
+        cost_vector_times_.push_back(
+            std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t_start)
+                .count());
+      }
+    }
+  }
+  num_vertices = Ta.getNumVertices() + Tb.getNumVertices();
+  if (goal_found && shared_a_idx >= 0)
+    getStateAndActionSequences(Ta, Tb, shared_a_idx, shared_b_idx, state_sequence, action_sequence);
+  elapsed_total = std::chrono::high_resolution_clock::now() - t_start;
+  length_vector_.push_back(length_so_far);
+  yaw_vector_.push_back(yaw_so_far);
+  cost_vector_.push_back(cost_so_far);
+  cost_vector_times_.push_back(elapsed_total.count());
+  best_cost_ = cost_so_far;
+  if (!state_sequence.empty()) postProcessPath(state_sequence, action_sequence, terrain);
+  if (elapsed_total.count() <= 5.0) success_ = 1;
+  path_duration_ = 0.0;
+  for (const Action &a : action_sequence) path_duration_ += a[6] + a[7];
+}
+
+bool RRTStarConnectClass::buildRRTStarConnectBatched(FastTerrainMap &terrain, State s_start,
+                                                     State s_goal, int batch, double max_time,
+                                                     std::vector<State> &state_sequence,
+                                                     std::vector<Action> &action_sequence,
+                                                     BatchStats *stats) {
+  const auto t_start = std::chrono::high_resolution_clock::now();
+  goal_found = false;
+  wall_to_first_ = -1;
+  rewires_ = 0;
+  cost_vector_.clear();
+  cost_vector_times_.clear();
+  PlannerClass Ta(terrain.device()), Tb(terrain.device());
+  Ta.setStream(seed_, 401);
+  Tb.setStream(seed_, 402);
+  Ta.init(s_start, cost_add_yaw_flag_, cost_add_yaw_length_weight_, cost_add_yaw_yaw_weight_);
+  Tb.init(s_goal, cost_add_yaw_flag_, cost_add_yaw_length_weight_, cost_add_yaw_yaw_weight_);
+  BatchStats local;
+  BatchStats &st = stats ? *stats : local;
+  std::vector<int> shared_a, shared_b;
+  int best_a = -1, best_b = -1;
+  double cost_so_far = INFTY;
+  while (true) {
+    const double el =
+        std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t_start).count();
+    if (el >= max_time) break;
+    st.iterations++;
+    for (int half = 0; half < 2; half++) {
+      PlannerClass &T = half == 0 ? Ta : Tb;
+      PlannerClass &O = half == 0 ? Tb : Ta;
+      const int dir = half == 0 ? FORWARD : REVERSE;
+      std::vector<int> added, nearest;
+      std::vector<Action> a_new;
+      extendBatch(T, terrain, dir, batch, added, nearest, a_new, /*insert=*/false, &st);
+      insertStar(T, terrain, dir, added, nearest, a_new, &st);
+      for (const auto &pr : connectBatch(T, O, terrain, dir, added, &st)) {
+        if (!goal_found) {
+          elapsed_to_first = std::chrono::high_resolution_clock::now() - t_start;
+          wall_to_first_ = elapsed_to_first.count();
+        }
+        goal_found = true;
+        shared_a.push_back(half == 0 ? pr.first : pr.second);
+        shared_b.push_back(half == 0 ? pr.second : pr.first);
+        st.solutions++;
+      }
+    }
+    for (size_t i = 0; i < shared_a.size(); ++i) {  // rewiring keeps lowering g
+      const double cost = Ta.getGValue(shared_a[i]) + Tb.getGValue(shared_b[i]);
+      if (cost < cost_so_far) {
+        cost_so_far = cost;
+        best_a = shared_a[i];
+        best_b = shared_b[i];
+        cost_vector_.push_back(cost_so_far);
+        cost_vector_times_.push_back(
+            std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t_start)
+                .count());
+      }
+    }
+  }
+  st.vertices_a = Ta.getNumVertices();
+  st.vertices_b = Tb.getNumVertices();
+  num_vertices = Ta.getNumVertices() + Tb.getNumVertices();
+  best_cost_ = cost_so_far;
+  if (!goal_found) return false;
+  getStateAndActionSequences(Ta, Tb, best_a, best_b, state_sequence, action_sequence);
+  path_length_ = Ta.getGValue(best_a) + Tb.getGValue(best_b);
+  path_yaw_ = Ta.getYValue(best_a) + Tb.getYValue(best_b);
+  path_cost_ = path_length_;
+  path_duration_ = 0;
+  for (const Action &a : action_sequence) path_duration_ += a[6] + a[7];
+  return true;
+}
+
 }  // namespace gbp_amd
 
 // ============================================================================
@@ -1119,11 +1467,11 @@ bool RRTConnectClass::buildRRTConnectBatched(FastTerrainMap &terrain, State s_st
 extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r,
                                     double *path_states, double *path_actions, int capacity) {
   using namespace gbp_amd;
-  if (!p || !r || p->batch < 1) return GBP_E_INVALID_ARG;
+  if (!p || !r || p->batch < 1 || p->algorithm < 0 || p->algorithm > 1) return GBP_E_INVALID_ARG;
   try {
     FastTerrainMap terrain(p->device);
     terrain.loadDataFlat(p->nx, p->ny, p->x, p->y, p->z, p->dx, p->dy, p->dz);
-    RRTConnectClass planner;
+    RRTStarConnectClass planner;  // is-a RRTConnectClass: algorithm 0 uses the plain build
     planner.setSeed(p->seed);
     State s0, s1;
     std::copy(p->start, p->start + 8, s0.begin());
@@ -1133,7 +1481,11 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     BatchStats st;
     const auto t0 = std::chrono::high_resolution_clock::now();
     const bool found =
-        planner.buildRRTConnectBatched(terrain, s0, s1, p->batch, p->max_time, states, actions, &st);
+        p->algorithm == 1
+            ? planner.buildRRTStarConnectBatched(terrain, s0, s1, p->batch, p->max_time, states,
+                                                 actions, &st)
+            : planner.buildRRTConnectBatched(terrain, s0, s1, p->batch, p->max_time, states,
+                                             actions, &st);
     double ttf = planner.wallTimeToFirst();
     if (found && p->post_process) planner.postProcessPath(states, actions, terrain);
     const std::chrono::duration<double> tot = std::chrono::high_resolution_clock::now() - t0;
@@ -1149,11 +1501,13 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     r->vertices_a = st.vertices_a;
     r->vertices_b = st.vertices_b;
     r->n_states = found ? (int)states.size() : 0;
+    r->rewires = st.rewires;
+    r->solutions = st.solutions;
     if (found) {
       double len = 0;
       for (size_t i = 1; i < states.size(); i++) len += planning_utils::poseDistance(states[i - 1], states[i]);
       r->path_length = len;
-      r->path_cost = len;
+      r->path_cost = p->algorithm == 1 ? planner.bestCost() : len;
       double dur = 0;
       for (const Action &a : actions) dur += a[6] + a[7];
       r->path_duration = dur;

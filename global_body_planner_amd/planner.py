@@ -25,7 +25,8 @@ class PlanParams(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("nx", ctypes.c_int), ("ny", ctypes.c_int),
                 ("x", _P), ("y", _P), ("z", _P), ("dx", _P), ("dy", _P), ("dz", _P),
                 ("start", _D * 8), ("goal", _D * 8), ("batch", ctypes.c_int),
-                ("max_time", _D), ("seed", ctypes.c_uint64), ("post_process", ctypes.c_int)]
+                ("max_time", _D), ("seed", ctypes.c_uint64), ("post_process", ctypes.c_int),
+                ("algorithm", ctypes.c_int)]
 
 
 class PlanResult(ctypes.Structure):
@@ -34,7 +35,8 @@ class PlanResult(ctypes.Structure):
                 ("extends", ctypes.c_int64), ("attempts_checked", ctypes.c_int64),
                 ("connects", ctypes.c_int64), ("vertices_a", ctypes.c_int64),
                 ("vertices_b", ctypes.c_int64), ("n_states", ctypes.c_int),
-                ("path_length", _D), ("path_cost", _D), ("path_duration", _D)]
+                ("path_length", _D), ("path_cost", _D), ("path_duration", _D),
+                ("rewires", ctypes.c_int64), ("solutions", ctypes.c_int64)]
 
 
 _planner = None
@@ -65,9 +67,11 @@ def start_goal_state(height, x, y):
 
 
 def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018,
-                     post_process=False, device=0, capacity=4096):
+                     post_process=False, device=0, capacity=4096, algorithm=0):
     """Plan start -> goal on terrain `data` (terrain_data.TerrainData).
 
+    algorithm 0: batch-synchronous RRT-Connect, stops at the first solution;
+    algorithm 1: batch-synchronous RRT*-Connect, anytime until max_time.
     Returns a dict with the C result fields plus `states` [n][8] and
     `actions` [n-1][10] (the found path; empty if none)."""
     L = load()
@@ -83,6 +87,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     p.start[:] = [float(v) for v in start]
     p.goal[:] = [float(v) for v in goal]
     p.batch, p.max_time, p.seed, p.post_process = int(batch), float(max_time), int(seed), int(post_process)
+    p.algorithm = int(algorithm)
     r = PlanResult()
     states = np.zeros((capacity, 8))
     actions = np.zeros((capacity, 10))
@@ -95,6 +100,11 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     out["states"] = states[:n].copy()
     out["actions"] = actions[:max(n - 1, 0)].copy()
     return out
+
+
+def plan_rrt_star_connect(data, start, goal, **kw):
+    """RRTStarConnectClass::buildRRTStarConnect, batch-synchronous (algorithm 1)."""
+    return plan_rrt_connect(data, start, goal, algorithm=1, **kw)
 
 
 def attempt_connect(terrain, s_existing, s, direction, t_s=None, adaptive=False, s_new=None,

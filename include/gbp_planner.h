@@ -195,6 +195,7 @@ class PlannerClass {
   State getVertex(int index) const { return vertices_[index]; }            // :18-20
   int getNumVertices() const { return (int)vertices_.size(); }             // :23-25
   void addEdge(int idx1, int idx2);                                        // :36-42
+  void removeEdge(int idx1, int idx2);                                     // :44-58
   int getPredecessor(int idx) const;                                       // :62-68
   std::vector<int> getSuccessors(int idx) const { return successors_[idx]; }
   void addAction(int idx, Action a) { actions_[idx] = a; }                 // :75-77
@@ -211,6 +212,10 @@ class PlannerClass {
   int getNearestNeighbor(State q);
   std::vector<int> getNearestNeighborBatch(const std::vector<State> &q);
   std::vector<int> neighborhoodDist(State q, double dist);                 // :173-182
+  // neighborhoodDist for many queries in one launch; query k only sees
+  // vertices with index < limit[k] (limit empty: all), ascending index
+  std::vector<std::vector<int>> neighborhoodDistBatch(const std::vector<State> &q, double dist,
+                                                      const std::vector<int> &limit = {});
   std::vector<int> neighborhoodN(State q, int N);                          // :151-171
 
   void setStream(uint64_t seed, uint64_t stream_id) {
@@ -233,6 +238,8 @@ class PlannerClass {
   int64_t d_capacity_ = 0, d_count_ = 0;
   void *d_scratch_ = nullptr;   // nearest-neighbour queries [q][8] + indices [q]
   int64_t d_scratch_cap_ = 0;
+  void *d_nbr_ = nullptr;       // neighbourhood queries + output lists
+  size_t d_nbr_bytes_ = 0;
   uint64_t seed_ = 1, stream_id_ = 100;
   int64_t draws_ = 0;
 };
@@ -310,6 +317,7 @@ class RRTClass {
 struct BatchStats {
   int64_t iterations = 0, targets = 0, extends = 0, attempts_checked = 0, connects = 0;
   int64_t vertices_a = 0, vertices_b = 0;
+  int64_t rewires = 0, solutions = 0;
 };
 
 class RRTConnectClass : public RRTClass {
@@ -355,14 +363,65 @@ class RRTConnectClass : public RRTClass {
   double horizon_expansion_factor = 1.2;
   const int max_time_solve = 4000;
 
- private:
-  // one lock-step round of attemptConnect for many (s_existing, s, t_s) triples
+  // lock-step attemptConnect for many (s_existing, s, t_s) triples; with
+  // max_depth = 0 only REACHED is decided (callers that test == REACHED)
   void attemptConnectBatch(const std::vector<State> &s_existing, const std::vector<State> &s,
                            std::vector<double> t_s, FastTerrainMap &terrain, int direction,
                            std::vector<int> &result, std::vector<State> &s_new,
-                           std::vector<Action> &a_new, BatchStats *stats);
+                           std::vector<Action> &a_new, BatchStats *stats, int max_depth = 64);
+  // connect each vertex `added` of T to the other tree O (rrt_connect.cpp:98-120,
+  // in order, NN against O's snapshot); returns the (T vertex, O vertex) pairs
+  // whose connect REACHED
+  std::vector<std::pair<int, int>> connectBatch(PlannerClass &T, PlannerClass &O,
+                                                FastTerrainMap &terrain, int dir,
+                                                const std::vector<int> &added, BatchStats *stats);
+  // draw `batch` targets, keep the STANCE-valid ones, extend T toward all of
+  // them against T's snapshot; returns the inserted vertices (in target order),
+  // their nearest vertices and actions
+  void extendBatch(PlannerClass &T, FastTerrainMap &terrain, int dir, int batch,
+                   std::vector<int> &added, std::vector<int> &nearest, std::vector<Action> &a_new,
+                   bool insert, BatchStats *stats);
   int halfIterationBatched(PlannerClass &T, PlannerClass &O, FastTerrainMap &terrain, int dir,
                            int batch, int &meet_t, int &meet_o, BatchStats *stats);
+};
+
+// ---- RRTStarConnectClass (rrt_star_connect.h, rrt_star_connect.cpp) ------------
+class RRTStarConnectClass : public RRTConnectClass {
+ public:
+  // rrt_star_connect.cpp:11-67: newConfig, then choose-parent among the
+  // vertices within delta and rewire them through s_new (connects on the engine)
+  int extend(PlannerClass &T, State s, FastTerrainMap &terrain, int direction) override;
+  // rrt_star_connect.cpp:70-89
+  void getStateAndActionSequences(PlannerClass &Ta, PlannerClass &Tb, int shared_a_idx,
+                                  int shared_b_idx, std::vector<State> &state_sequence,
+                                  std::vector<Action> &action_sequence);
+  // rrt_star_connect.cpp:91-205
+  void buildRRTStarConnect(FastTerrainMap &terrain, State s_start, State s_goal,
+                           std::vector<State> &state_sequence,
+                           std::vector<Action> &action_sequence, double max_time);
+  // Batch-synchronous RRT*-Connect: as buildRRTConnectBatched, with every new
+  // vertex inserted by choose-parent + rewire (its neighbourhood = the vertices
+  // within delta that precede it, as in the sequential algorithm); all
+  // neighbourhood scans of a batch run in one launch and all their connects in
+  // one pair-check launch, the tree updates then replay sequentially in order.
+  // Runs until max_time after the first solution (anytime), keeping the best.
+  bool buildRRTStarConnectBatched(FastTerrainMap &terrain, State s_start, State s_goal, int batch,
+                                  double max_time, std::vector<State> &state_sequence,
+                                  std::vector<Action> &action_sequence, BatchStats *stats = nullptr);
+  double bestCost() const { return best_cost_; }
+  int64_t rewires() const { return rewires_; }
+
+ protected:
+  const double delta = 3.0;  // rrt_star_connect.h:59
+  double best_cost_ = INFINITY_COST;
+  int64_t rewires_ = 0;
+  static constexpr double INFINITY_COST = 1.7976931348623157e308;
+
+ private:
+  // choose-parent + rewire for the new vertices `added` of T (in order)
+  void insertStar(PlannerClass &T, FastTerrainMap &terrain, int dir, const std::vector<int> &added,
+                  const std::vector<int> &nearest, const std::vector<Action> &a_new,
+                  BatchStats *stats);
 };
 
 // ---- implementation of the grid_map adapter (fast_terrain_map.cpp:31-91) -------
@@ -422,6 +481,7 @@ typedef struct {
   double max_time;      // seconds
   uint64_t seed;
   int post_process;     // run postProcessPath on the found path
+  int algorithm;        // 0 rrt-connect, 1 rrt-star-connect (anytime until max_time)
 } gbp_plan_params;
 
 typedef struct {
@@ -431,6 +491,7 @@ typedef struct {
   int64_t iterations, targets, extends, attempts_checked, connects, vertices_a, vertices_b;
   int n_states;          // path states written (<= capacity)
   double path_length, path_cost, path_duration;
+  int64_t rewires, solutions;  // RRT*: edges rewired, tree connections found
 } gbp_plan_result;
 
 /* plans from start to goal; path_states[capacity][8] / path_actions[capacity][10]

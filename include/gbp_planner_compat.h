@@ -6,6 +6,7 @@
 // compiles unchanged against include/gbp_planner.h.
 //
 // Names exported: FastTerrainMap, PlannerClass, RRTClass, RRTConnectClass,
+// RRTStarConnectClass,
 // namespace planning_utils (State, Action, constants, apply*/isValid*/...),
 // and the TRAPPED / ADVANCED / REACHED macros of rrt.h:7-9.
 #pragma once
@@ -16,6 +17,7 @@ using gbp_amd::FastTerrainMap;
 using gbp_amd::PlannerClass;
 using gbp_amd::RRTClass;
 using gbp_amd::RRTConnectClass;
+using gbp_amd::RRTStarConnectClass;
 namespace planning_utils = gbp_amd::planning_utils;
 using namespace gbp_amd::planning_utils;  // the reference's headers do the same (planning_utils.h)
 

@@ -4,6 +4,7 @@
 // gbp_planner_compat.h.  Built and linked by tests/test_abi.py; run on the
 // GPU box by tests/test_gpu_planner.py (argv: nothing; exit 0 = plan found).
 #include <cstdio>
+#include <string>
 #include <vector>
 
 #include "gbp_planner_compat.h"
@@ -43,7 +44,8 @@ struct GridMap {
 };
 }  // namespace fake_grid_map
 
-int main() {
+int main(int argc, char **argv) {
+  const bool star = argc > 1 && std::string(argv[1]) == "star";  // algorithm: rrt-star-connect
   fake_grid_map::GridMap map{120, 60, 0.05, {}};
   map.z.assign((size_t)map.nx * map.ny, 0.0f);  // flat ground
   FastTerrainMap terrain_;
@@ -55,20 +57,28 @@ int main() {
   robot_goal_[2] += terrain_.getGroundHeight(robot_goal_[0], robot_goal_[1]);     // :264
 
   RRTConnectClass rrt_connect_obj;                                    // :89
-  rrt_connect_obj.set_state_action_pair_check_adaptive_step_size_flag_(false);  // :182
-  rrt_connect_obj.set_cost_add_yaw(false, 1.0, 1.0);                  // :190
-  rrt_connect_obj.set_action_direction_sampling(false, 0.15);
-  rrt_connect_obj.set_state_direction_sampling(false, 0.05, false);
+  RRTStarConnectClass rrt_star_connect_obj;                           // :90
+  for (RRTClass *o : {(RRTClass *)&rrt_connect_obj, (RRTClass *)&rrt_star_connect_obj}) {
+    o->set_state_action_pair_check_adaptive_step_size_flag_(false);   // :182 setPlannerParameter
+    o->set_cost_add_yaw(false, 1.0, 1.0);                             // :190
+    o->set_action_direction_sampling(false, 0.15);
+    o->set_state_direction_sampling(false, 0.05, false);
+  }
 
   std::vector<State> state_sequence_;
   std::vector<Action> action_sequence_;
-  rrt_connect_obj.buildRRTConnect(terrain_, robot_start_, robot_goal_, state_sequence_,
-                                  action_sequence_, 0.0);             // :115
+  if (!star)
+    rrt_connect_obj.buildRRTConnect(terrain_, robot_start_, robot_goal_, state_sequence_,
+                                    action_sequence_, 0.0);           // :115
+  else
+    rrt_star_connect_obj.buildRRTStarConnect(terrain_, robot_start_, robot_goal_, state_sequence_,
+                                             action_sequence_, 1.0);  // :121
+  RRTConnectClass &rrt_stats = star ? rrt_star_connect_obj : rrt_connect_obj;
   double plan_time, time_to_first_solve, path_duration;
   int success, vertices_generated;
   std::vector<double> length_vector, yaw_vector, cost_vector, cost_vector_times;
   std::vector<std::vector<double>> allStatePosition;
-  rrt_connect_obj.getStatistics(plan_time, success, vertices_generated, time_to_first_solve,
+  rrt_stats.getStatistics(plan_time, success, vertices_generated, time_to_first_solve,
                                 length_vector, yaw_vector, cost_vector, cost_vector_times,
                                 path_duration, allStatePosition);     // :118
   std::vector<State> body_plan_;

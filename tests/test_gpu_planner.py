@@ -145,3 +145,29 @@ def test_node_callsite_plans_on_gpu(gpu, tmp_path):
     r = subprocess.run(["timeout", "-k", "10", "120", exe], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.startswith("states ")
+
+
+def test_node_callsite_rrt_star_on_gpu(gpu, tmp_path):
+    """The node's rrt-star-connect branch (global_body_planner.cpp:120-124):
+    RRTStarConnectClass::buildRRTStarConnect with its choose-parent / rewire
+    extend, engine-backed, reaches a path."""
+    import subprocess
+    from tests.test_abi import build_node_callsite
+    exe = build_node_callsite(tmp_path / "node_callsite")
+    r = subprocess.run(["timeout", "-k", "10", "120", exe, "star"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_plan_rrt_star_synth256(gpu):
+    """Batch-synchronous RRT*-Connect (config 5's algorithm) on the config-2
+    pair: a valid path, rewiring happened, and the reported cost is the tree
+    cost of the returned path (sum of pose distances along it)."""
+    data = td.synth_rough(256)
+    O = oracle.OracleTerrain.from_data(data)
+    start, goal = _start_goal(O, 1.0, 2.55, 4.02, 2.55)
+    out = planner.plan_rrt_star_connect(data, start, goal, batch=64, max_time=8.0, seed=21)
+    check_path(O, out, start, goal)
+    assert out["rewires"] > 0 and out["solutions"] >= 1
+    S = out["states"]
+    length = sum(oracle.pose_distance(S[i], S[i + 1]) for i in range(len(S) - 1))
+    assert out["path_cost"] == pytest.approx(length, rel=1e-9)
