@@ -882,7 +882,9 @@ void RRTConnectClass::postProcessPath(std::vector<State> &state_sequence,
       sc.pop_back();
       ac.pop_back();
       s_next = sc.back();
-      a_next = ac.back();
+      // the reference reads back() of the now-empty action copy when it pops
+      // down to s itself (UB, never used afterwards): keep the last value
+      if (!ac.empty()) a_next = ac.back();
     }
     if (s != s_next) {
       new_states.push_back(s_next);
@@ -1370,6 +1372,16 @@ void RRTStarConnectClass::buildRRTStarConnect(FastTerrainMap &terrain, State s_s
             std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t_start)
                 .count());
       }
+    }
+  }
+  // the reference leaves the loop before ranking a connection found in its last
+  // iteration (shared_a_idx may then be uninitialised): rank once more
+  for (size_t i = 0; i < shared_a.size(); ++i) {
+    const double cost = Ta.getGValue(shared_a[i]) + Tb.getGValue(shared_b[i]);
+    if (cost < cost_so_far) {
+      cost_so_far = cost;
+      shared_a_idx = shared_a[i];
+      shared_b_idx = shared_b[i];
     }
   }
   num_vertices = Ta.getNumVertices() + Tb.getNumVertices();

@@ -266,13 +266,16 @@ def test_neighbors_parity(gpu):
     rng = np.random.default_rng(4)
     verts = rng.normal(size=(3000, 8)) * 0.8
     q = np.concatenate([rng.normal(size=(700, 8)) * 0.8, verts[[0, 17, 2999]]])
+    counts = {}
     for radius, max_out in ((3.0, 512), (1.5, 16), (0.0, 8)):
         out, cnt = gbp.neighbors(torch.from_numpy(q).cuda(), torch.from_numpy(verts).cuda(),
                                  radius, max_out)
         ro, rc = oracle.neighbors_batch(q, verts, radius, max_out)
         assert np.array_equal(np_(cnt), rc)
         assert np.array_equal(np_(out), ro)
-    assert rc.max() <= 3000 and (np_(cnt) > 16).any()   # truncation exercised at max_out 16
+        counts[radius] = rc
+    assert (counts[1.5] > 16).any()      # truncation exercised at max_out 16
+    assert not counts[0.0].any()         # distance 0 (the vertex itself) is excluded
 
 
 # ---- full-size, size-independent properties --------------------------------------------
