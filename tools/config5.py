@@ -1,0 +1,105 @@
+"""BASELINE config 5: RRT*-Connect on synth-fractal-4096 (one tree pair per GPU).
+
+  python tools/config5.py --max-time 20 --batch 256 [--out profiles/r01_config5.json]
+  torchrun --nproc-per-node N tools/config5.py ...   (N independent restarts, best path
+                                                       shared by one all_gather)
+
+Start (1.0, L/2) and goal 8 m further along +x (the first STANCE-valid points
+scanning outward / inward in 0.02 m steps; z = 0.375 + ground, v = (1,0,0)).
+Reports time to first solution, best tree cost over time, rewires, and the
+engine work rate (pair checks / s) of the anytime RRT*-Connect.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import global_body_planner_amd as gbp  # noqa: E402
+from global_body_planner_amd import planner, sharding  # noqa: E402
+from global_body_planner_amd import terrain_data as td  # noqa: E402
+
+
+def first_valid(T, x, y, step, n=400):
+    xs = x + step * np.arange(n)
+    xy = np.stack([xs, np.full(n, y)], 1)
+    h = T.height_host(xy)[0]
+    st = np.zeros((n, 8))
+    st[:, 0], st[:, 1], st[:, 2], st[:, 3] = xs, y, 0.375 + h, 1.0
+    v, _, _ = T.valid_states(torch.from_numpy(st), gbp.STANCE)
+    k = int(np.argmax(v.cpu().numpy() > 0))
+    return st[k]
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--terrain", default="synth-fractal-4096")
+    p.add_argument("--batch", type=int, default=256)
+    p.add_argument("--max-time", type=float, default=20.0)
+    p.add_argument("--seed", type=int, default=20251020)
+    p.add_argument("--span", type=float, default=8.0)
+    p.add_argument("--out", default=None)
+    a = p.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    t0 = time.perf_counter()
+    data = td.by_name(a.terrain)
+    t_gen = time.perf_counter() - t0
+    T = gbp.Terrain.from_data(data, device=local)
+    L = data.x[-1]
+    start = first_valid(T, 1.0, L / 2, 0.02)
+    goal = first_valid(T, 1.0 + a.span, L / 2, -0.02)
+    out = planner.plan_rrt_star_connect(data, start, goal, batch=a.batch, max_time=a.max_time,
+                                        seed=a.seed + rank, device=local)
+    found = bool(out["found"])
+    cost = out["path_cost"] if found else float("nan")
+    rec = sharding.pack_path(cost, out["path_length"], 0.0, out["states"] if found else None,
+                             out["actions"] if found else None, device=dev)
+    who, best = sharding.allgather_best_path(rec)
+    ttf = torch.tensor([out["time_to_first"] if found else float("inf")], dtype=torch.float64,
+                       device=dev)
+    work = torch.tensor([float(out["attempts_checked"]), float(out["rewires"]),
+                         float(out["connects"]), float(out["extends"])], dtype=torch.float64,
+                        device=dev)
+    if world > 1:
+        dist.all_reduce(ttf, op=dist.ReduceOp.MIN)
+        dist.all_reduce(work, op=dist.ReduceOp.SUM)
+    if rank == 0:
+        b = sharding.unpack_path(best)
+        res = {
+            "config": "5: RRT*-Connect, %s, %d GPU(s), batch %d, %.1f s anytime" % (
+                a.terrain, world, a.batch, a.max_time),
+            "terrain_gen_s": round(t_gen, 2),
+            "start": start[:3].tolist(), "goal": goal[:3].tolist(),
+            "time_to_first_solution_s": float(ttf.item()),
+            "best_cost": b["cost"], "best_rank": who, "best_path_states": int(b["states"].shape[0]),
+            "pair_checks_per_s": float(work[0].item()) / out["total_time"],
+            "rewires": int(work[1].item()), "connect_checks": int(work[2].item()),
+            "extends": int(work[3].item()),
+            "rank0": {k: out[k] for k in ("iterations", "targets", "extends", "attempts_checked",
+                                          "connects", "vertices_a", "vertices_b", "rewires",
+                                          "solutions", "total_time", "time_to_first")},
+        }
+        line = json.dumps(res)
+        print(line, flush=True)
+        if a.out:
+            with open(a.out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
