@@ -487,20 +487,21 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
   // to its idle lanes.  sched 1: a fixed per-wave slice, no atomics at all;
   // sched 0 / 2: slices of `chunk` (0 = exactly the lanes that need one)
   // dequeued from one device-scope counter (MI355X_MICROARCH.md 'dequeue');
-  // sched 3: the first half of the attempts as fixed per-wave slices, the
-  // second half in chunks of `chunk` from the counter, each dequeue issued one
-  // refill AHEAD so its latency hides under the samples (balances the waves'
-  // unequal sample totals without stalling on the atomic).
-  unsigned int cur = 0, end = 0;
-  const unsigned int n_static = sched == 3 ? (unsigned int)n / 2u : (unsigned int)n;
-  const unsigned int csz = chunk > 0 ? (unsigned int)chunk : 32u;
-  unsigned int nxt = 0xFFFFFFFFu;  // prefetched dynamic chunk (sched 3, lane 0)
-  if (sched == 1 || sched == 3) {
+  // sched 3: a fixed slice per WORKGROUP, dealt to its waves on demand from
+  // an LDS counter (an LDS atomic costs ~100 cycles, a device atomic ~1 us), so
+  // the waves of a workgroup even out their unequal sample totals.
+  __shared__ unsigned int wg_head;
+  unsigned int cur = 0, end = 0, wg_begin = 0, wg_end = 0;
+  if (sched == 1) {
     const unsigned int waves = gridDim.x * (blockDim.x / WAVE);
     const unsigned int wid = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
-    cur = (unsigned int)(((unsigned long long)n_static * wid) / waves);
-    end = (unsigned int)(((unsigned long long)n_static * (wid + 1)) / waves);
-    if (sched == 3 && lane == 0) nxt = n_static + atomicAdd(head, csz);
+    cur = (unsigned int)(((unsigned long long)n * wid) / waves);
+    end = (unsigned int)(((unsigned long long)n * (wid + 1)) / waves);
+  } else if (sched == 3) {
+    wg_begin = (unsigned int)(((unsigned long long)n * blockIdx.x) / gridDim.x);
+    wg_end = (unsigned int)(((unsigned long long)n * (blockIdx.x + 1)) / gridDim.x);
+    if (threadIdx.x == 0) wg_head = 0;
+    __syncthreads();
   }
   for (;;) {
     const bool need = (L.stage == ST_IDLE) && !exhausted;
@@ -508,13 +509,13 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
     while (m) {
       if (cur >= end) {
         unsigned int base = 0xFFFFFFFFu;
-        const unsigned int grab = sched == 3 ? csz
-                                  : (chunk > 0 ? (unsigned int)chunk : (unsigned int)__popcll(m));
+        const unsigned int grab = chunk > 0 ? (unsigned int)chunk : (unsigned int)__popcll(m);
+        const int leader = __ffsll((long long)m) - 1;
         if (sched == 3) {
-          base = __shfl(nxt, 0);
-          if (lane == 0 && base < (unsigned int)n) nxt = n_static + atomicAdd(head, csz);
+          if (lane == leader) base = wg_begin + atomicAdd(&wg_head, grab);
+          base = __shfl(base, leader);
+          if (base >= wg_end) base = 0xFFFFFFFFu;
         } else if (sched != 1) {
-          const int leader = __ffsll((long long)m) - 1;
           if (lane == leader) base = atomicAdd(head, grab);
           base = __shfl(base, leader);
         }
@@ -523,7 +524,7 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
           break;
         }
         cur = base;
-        end = min(base + grab, (unsigned int)n);
+        end = min(base + grab, sched == 3 ? wg_end : (unsigned int)n);
       }
     const unsigned int take = min(end - cur, (unsigned int)__popcll(m));
       const unsigned int rank = (unsigned int)__popcll(m & lt_mask);
@@ -1034,7 +1035,8 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
       const int64_t g = std::max<int64_t>(
           1, std::min<int64_t>(t->opt_sched == 1 || t->opt_sched == 3 ? resident : want,
                                (m + block - 1) / block));
-      if (t->opt_sched != 1) HIPCHK(hipMemsetAsync(t->d_head, 0, sizeof(unsigned int), st));
+      if (t->opt_sched == 0 || t->opt_sched == 2)
+        HIPCHK(hipMemsetAsync(t->d_head, 0, sizeof(unsigned int), st));
       hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, LDSC>), dim3((unsigned)g), dim3(block),
                          lds, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
                          flags + off, c, t->d_head, (int)t->opt_sched, (int)t->opt_chunk,

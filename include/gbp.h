@@ -123,7 +123,7 @@ int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage,
 #define GBP_OPT_LDS_COORDS    5  /* 1: stage coordinate vectors in LDS when they fit  */
 #define GBP_OPT_SCHED         6  /* persistent work source: 0 one atomic counter,
                                     1 static per-wave slices, 2 chunked counter,
-                                    3 half static + prefetched counter chunks        */
+                                    3 per-workgroup slices dealt from an LDS counter */
 #define GBP_OPT_CHUNK         7  /* attempts per dequeue for sched 0 / 2 (0 = per need) */
 #define GBP_OPT_HELPERS       8  /* 1: a drained wave's idle lanes evaluate the remaining
                                     attempts' next samples ahead (default 1)          */

@@ -307,15 +307,18 @@ def test_full_size_batch_properties(gpu):
     assert 0 < ref[0].sum() < n
 
 
-@pytest.mark.parametrize("sched,chunk", [(0, 0), (1, 0), (2, 64), (2, 7)])
+@pytest.mark.parametrize("sched,chunk", [(0, 0), (1, 0), (2, 64), (2, 7), (3, 0), (3, 16)])
 @pytest.mark.parametrize("lds", [0, 1])
-def test_validate_pairs_schedulers(gpu, sched, chunk, lds):
-    """Every work-distribution mode of the persistent kernel computes the same answers."""
+@pytest.mark.parametrize("helpers", [0, 1])
+def test_validate_pairs_schedulers(gpu, sched, chunk, lds, helpers):
+    """Every work-distribution mode of the persistent kernel, with and without
+    tail helper lanes, computes the same answers."""
     data, T, O = terrain_pair("synth-rough-256")
     T.set_option(L.OPT_KERNEL, L.KERNEL_PERSISTENT)
     T.set_option(L.OPT_SCHED, sched)
     T.set_option(L.OPT_CHUNK, chunk)
     T.set_option(L.OPT_LDS_COORDS, lds)
+    T.set_option(L.OPT_HELPERS, helpers)
     try:
         for n in (1, 63, 5000):
             s, a, d, _, _ = attempts_oracle(O, n, seed=1000 + n)
@@ -323,9 +326,10 @@ def test_validate_pairs_schedulers(gpu, sched, chunk, lds):
             gpu_t = (np_(res.valid), np_(res.s_new), np_(res.t_new), u32(res.flags), u32(res.counts))
             assert_pairs_equal(gpu_t, O.validate_pairs(s, a, d, nthreads=8), f"s{sched}c{chunk}n{n}")
     finally:
-        T.set_option(L.OPT_SCHED, 0)
+        T.set_option(L.OPT_SCHED, 1)
         T.set_option(L.OPT_CHUNK, 0)
         T.set_option(L.OPT_LDS_COORDS, 1)
+        T.set_option(L.OPT_HELPERS, 1)
 
 
 def test_engine_matches_golden_vectors(gpu):

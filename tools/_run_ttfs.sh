@@ -1,6 +1,9 @@
 #!/bin/bash
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 300 python tools/config5.py --max-time 20 --batch 256 --out gpurun_out/config5.json > gpurun_out/config5.log 2>&1; rc=$?
-tail -3 gpurun_out/config5.log
+timeout -k 10 600 python -m pytest -m gpu -q -x tests/test_gpu_parity.py -k "schedul or full_size" > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
+case $rc in 0|1|5) ;; *) exit $rc;; esac
+timeout -k 10 600 python tools/sweep.py --kernels persistent --waves 2 --grid 8 --block 256,128 --sched 1:0,3:0,3:8,3:32 --rounds 5 > gpurun_out/sweep.txt 2>&1; rc=$?
+cat gpurun_out/sweep.txt
 exit $rc
