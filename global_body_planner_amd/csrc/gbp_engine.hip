@@ -167,10 +167,16 @@ enum : int {
 // closed form and the same operands the reference assigned it from
 enum : int { SN_NONE = 0, SN_STANCE_S = 1, SN_FLIGHT_B = 2, SN_STANCE_REV_B = 3 };
 
+// Each lane's attempt (s[8], a[10]) lives in LDS, not in VGPRs: a row of
+// SA_ROW doubles per thread (odd stride: the 64 lanes' 8-byte reads hit
+// distinct bank pairs).  Freed registers keep the state check's in-flight
+// lookups out of scratch; tail helpers read their owner's row directly.
+constexpr int SA_ROW = 19;
+
 struct Lane {
-  double s[8], a[10];        // input state and action (the take-off state of the
-                             // flight / reverse-stance phases is recomputed per
-                             // sample: cheaper than 16 more live VGPRs)
+  double *s, *a;             // this lane's LDS row: input state and action (the
+                             // take-off state of the flight / reverse-stance
+                             // phases is recomputed per sample)
   double t, ts, tpre;        // sample time, adaptive step, last success time
   double snew_p, tnew;
   int stage, snew_kind;
@@ -224,10 +230,15 @@ __device__ __forceinline__ void enter_stage(Lane &L, int st) {
 // eight divisions run ONCE for the whole wave (converged), and the stage's
 // own sums finish the state — the expression trees of apply_stance /
 // apply_stance_reverse (gbp_device.h), split at the quotient.
-__device__ __forceinline__ void sample_state(const Lane &L, int stage, double t, double *o) {
-  const double *a = L.a;
+__device__ __forceinline__ void sample_state(const double *s_in, const double *a_in, int stage,
+                                             double t, double *o) {
+  double sv[8], a[10];
+#pragma unroll
+  for (int k = 0; k < 8; k++) sv[k] = s_in[k];
+#pragma unroll
+  for (int k = 0; k < 10; k++) a[k] = a_in[k];
   if (stage == ST_REV_FLIGHT) {  // applyFlight(s, -t)
-    apply_flight(L.s, -t, o);
+    apply_flight(sv, -t, o);
     return;
   }
   const bool rev = (stage == ST_REV_STANCE || stage == ST_REV_START);
@@ -235,11 +246,11 @@ __device__ __forceinline__ void sample_state(const Lane &L, int stage, double t,
   double b[8];  // the state the stance form starts from
   double tt;    // its time argument
   if (rev) {
-    apply_flight(L.s, -a[7], b);  // s_to = applyFlight(s, -t_f)
+    apply_flight(sv, -a[7], b);  // s_to = applyFlight(s, -t_f)
     tt = t;
   } else {
 #pragma unroll
-    for (int k = 0; k < 8; k++) b[k] = L.s[k];
+    for (int k = 0; k < 8; k++) b[k] = sv[k];
     tt = (stage == ST_FWD_STANCE) ? t : t_s;
   }
   // numerators: applyStance (a_to - a_td) * (t*t*t) and (a_to - a_td) * t * t;
@@ -448,7 +459,7 @@ __device__ __forceinline__ int nth_set_bit(unsigned long long m, int n) {
 template <class ZT, bool ADAPTIVE>
 __device__ __forceinline__ bool step_lane(const TerrainView<ZT> &T, Lane &L) {
   double sc[8];
-  sample_state(L, L.stage, stage_time(L), sc);
+  sample_state(L.s, L.a, L.stage, stage_time(L), sc);
   const bool ok = is_valid_state(T, sc, stage_phase(L.stage), L.acc);
   if (L.acc.flags & GBP_F_LIMIT) return true;  // stopped: reported invalid
   return transition<ADAPTIVE>(L, ok);
@@ -477,10 +488,14 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
   const TerrainView<ZT> T = LDSC ? stage_coords(T0, gbp_smem) : T0;
   const int lane = threadIdx.x & (WAVE - 1);
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  double *const SA = gbp_smem + (LDSC ? T0.nx + T0.ny : 0);   // attempt rows
+  double *const wave_rows = SA + (size_t)(threadIdx.x & ~(WAVE - 1)) * SA_ROW;
 #ifdef GBP_DIAG_UTIL
   const unsigned long long t_begin = wall_clock64();
 #endif
   Lane L;
+  L.s = SA + (size_t)threadIdx.x * SA_ROW;
+  L.a = L.s + 8;
   L.stage = ST_IDLE;
   bool exhausted = false;
   // work source (wave-uniform): [cur, end) is the range this wave hands out
@@ -549,6 +564,7 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
     const unsigned long long act = __ballot(L.stage != ST_IDLE);
     if (!act) break;
     const bool owner = L.stage != ST_IDLE;
+    asm volatile("" ::: "memory");  // re-read attempt rows per step (no long live ranges)
     // ---- the sample each lane evaluates this step --------------------------
     // Normally a lane evaluates its own attempt's next sample.  In a wave's
     // tail (no work left to refill idle lanes) the idle lanes become helpers:
@@ -559,6 +575,7 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
     const int n_act = __popcll(act);
     const bool tail = helpers && n_act < WAVE;  // every idle lane is exhausted here
     int st = L.stage, slot = 0;
+    const double *ps = L.s;  // the attempt row this lane samples
     double t_eval = owner ? stage_time(L) : 0.0;
     uint32_t vbase = L.acc.V;
     bool has = owner;
@@ -567,16 +584,13 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
       const int j = __popcll(idle & lt_mask);
       const int src = owner ? lane : nth_set_bit(act, j % n_act);
       slot = owner ? 0 : 1 + j / n_act;
-#pragma unroll
-      for (int k = 0; k < 8; k++) L.s[k] = __shfl(L.s[k], src);
-#pragma unroll
-      for (int k = 0; k < 10; k++) L.a[k] = __shfl(L.a[k], src);
+      ps = wave_rows + src * SA_ROW;  // the owner's attempt row
       st = __shfl(L.stage, src);
       double t = __shfl(L.t, src), ts = __shfl(L.ts, src);
       vbase = __shfl(L.acc.V, src);
       if (!owner) {
         has = true;
-        for (int k = 0; k < slot && has; k++) has = advance_on_success<ADAPTIVE>(st, L.a, t, ts);
+        for (int k = 0; k < slot && has; k++) has = advance_on_success<ADAPTIVE>(st, ps + 8, t, ts);
         t_eval = t;
       }
     }
@@ -593,7 +607,7 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
     bool ok = false;
     if (has) {
       double sc[8];
-      sample_state(L, st, t_eval, sc);
+      sample_state(ps, ps + 8, st, t_eval, sc);
       ok = is_valid_state(T, sc, stage_phase(st), acc_s);
     }
     bool decided = false;
@@ -629,6 +643,7 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
         }
       }
     }
+    asm volatile("" ::: "memory");
     if (owner) {
       if (decided) {
         const size_t i = (size_t)L.idx;
@@ -638,9 +653,14 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
         if (valid) valid[i] = (f & GBP_F_VALID) ? 1 : 0;
         if (s_new && L.snew_kind != SN_NONE) {
           double o[8];
-          if (L.snew_kind == SN_STANCE_S) apply_stance(L.s, L.a, L.snew_p, o);
-          else if (L.snew_kind == SN_FLIGHT_B) sample_state(L, ST_FWD_LAND, L.snew_p, o);
-          else sample_state(L, ST_REV_STANCE, L.snew_p, o);
+          double sv[8], av[10];
+#pragma unroll
+          for (int k = 0; k < 8; k++) sv[k] = L.s[k];
+#pragma unroll
+          for (int k = 0; k < 10; k++) av[k] = L.a[k];
+          if (L.snew_kind == SN_STANCE_S) apply_stance(sv, av, L.snew_p, o);
+          else if (L.snew_kind == SN_FLIGHT_B) sample_state(sv, av, ST_FWD_LAND, L.snew_p, o);
+          else sample_state(sv, av, ST_REV_STANCE, L.snew_p, o);
 #pragma unroll
           for (int k = 0; k < 8; k++) s_new[8 * i + k] = o[k];
         }
@@ -1013,7 +1033,8 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
                       double *t_new, uint32_t *flags, uint32_t *counts, hipStream_t st) {
   const TerrainView<ZT> T = view<ZT>(t);
   const int block = (int)t->opt_block;
-  const size_t lds = LDSC ? stage_bytes(t->nx, t->ny) : 0;
+  const size_t coords = LDSC ? stage_bytes(t->nx, t->ny) : 0;
+  const size_t rows = sizeof(double) * SA_ROW * (size_t)block;  // persistent kernel only
   const int64_t chunk = (int64_t)1 << 30;
   const int64_t want = (int64_t)t->num_cus * t->opt_grid_per_cu;
   for (int64_t off = 0; off < n; off += chunk) {
@@ -1027,7 +1048,7 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
       // the direct form inlines the state check at five call sites: it gets the
       // whole register file (W = 1) whatever the persistent kernel's budget is
       const unsigned g = (unsigned)((m + block - 1) / block);
-      hipLaunchKernelGGL((k_validate_direct<ZT, AD, 1, LDSC>), dim3(g), dim3(block), lds, st, T, m,
+      hipLaunchKernelGGL((k_validate_direct<ZT, AD, 1, LDSC>), dim3(g), dim3(block), coords, st, T, m,
                          s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn, flags + off, c);
     } else {
       // persistent: grid sized to residency; the work counter is zeroed per launch
@@ -1038,7 +1059,7 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
       if (t->opt_sched == 0 || t->opt_sched == 2)
         HIPCHK(hipMemsetAsync(t->d_head, 0, sizeof(unsigned int), st));
       hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, LDSC>), dim3((unsigned)g), dim3(block),
-                         lds, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
+                         coords + rows, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
                          flags + off, c, t->d_head, (int)t->opt_sched, (int)t->opt_chunk,
                          (int)t->opt_helpers);
     }
@@ -1058,7 +1079,13 @@ int launch_validate(gbp_terrain *t, int64_t n, const double *s, const double *a,
           : launch_validate_w<ZT, AD, W, false>(t, n, s, a, dir, dir_all, valid, s_new, t_new, \
                                                 flags, counts, st))
   const int64_t w = t->opt_waves;
-  const bool lds_ok = t->opt_lds_coords && stage_bytes(t->nx, t->ny) <= t->lds_max;
+  // coordinates in LDS only if they fit next to the attempt rows, with room
+  // for the W workgroups of 256 lanes that share a CU (160 KB per CU)
+  const size_t rows = sizeof(double) * SA_ROW * (size_t)t->opt_block;
+  const size_t per_cu = std::max<int64_t>(1, (int64_t)w * 256 / t->opt_block) *
+                        (stage_bytes(t->nx, t->ny) + rows);
+  const bool lds_ok = t->opt_lds_coords && stage_bytes(t->nx, t->ny) + rows <= t->lds_max &&
+                      (t->opt_kernel == GBP_KERNEL_DIRECT || per_cu <= 160 * 1024);
   if (adaptive) return w >= 4 ? GBP_LV(true, 4) : (w >= 2 ? GBP_LV(true, 2) : GBP_LV(true, 1));
   return w >= 4 ? GBP_LV(false, 4) : (w >= 2 ? GBP_LV(false, 2) : GBP_LV(false, 1));
 #undef GBP_LV
