@@ -729,6 +729,17 @@ void RRTClass::print_setting_parameters() {
 // ============================================================================
 // RRTConnectClass
 // ============================================================================
+static void tree_extent(const PlannerClass &T, double e[4]) {
+  e[0] = e[2] = INFINITY;
+  e[1] = e[3] = -INFINITY;
+  for (const State &v : T.vertices()) {
+    e[0] = std::min(e[0], v[0]);
+    e[1] = std::max(e[1], v[0]);
+    e[2] = std::min(e[2], v[1]);
+    e[3] = std::max(e[3], v[1]);
+  }
+}
+
 static Action connect_action(const State &s_start, const State &s_goal, double t_s) {
   // rrt_connect.cpp:53-63 (cubic-Hermite stance action, t_f = 0)
   const double x_td = s_start[0], y_td = s_start[1], z_td = s_start[2];
@@ -1167,6 +1178,8 @@ bool RRTConnectClass::buildRRTConnectBatched(FastTerrainMap &terrain, State s_st
     }
   }
   elapsed_to_first = std::chrono::high_resolution_clock::now() - t_start;
+  tree_extent(Ta, st.extent_a);
+  tree_extent(Tb, st.extent_b);
   st.vertices_a = Ta.getNumVertices();
   st.vertices_b = Tb.getNumVertices();
   num_vertices = Ta.getNumVertices() + Tb.getNumVertices();
@@ -1457,6 +1470,8 @@ bool RRTStarConnectClass::buildRRTStarConnectBatched(FastTerrainMap &terrain, St
       }
     }
   }
+  tree_extent(Ta, st.extent_a);
+  tree_extent(Tb, st.extent_b);
   st.vertices_a = Ta.getNumVertices();
   st.vertices_b = Tb.getNumVertices();
   num_vertices = Ta.getNumVertices() + Tb.getNumVertices();
@@ -1515,6 +1530,10 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     r->n_states = found ? (int)states.size() : 0;
     r->rewires = st.rewires;
     r->solutions = st.solutions;
+    for (int k = 0; k < 4; k++) {
+      r->extent_a[k] = st.extent_a[k];
+      r->extent_b[k] = st.extent_b[k];
+    }
     if (found) {
       double len = 0;
       for (size_t i = 1; i < states.size(); i++) len += planning_utils::poseDistance(states[i - 1], states[i]);

@@ -36,7 +36,8 @@ class PlanResult(ctypes.Structure):
                 ("connects", ctypes.c_int64), ("vertices_a", ctypes.c_int64),
                 ("vertices_b", ctypes.c_int64), ("n_states", ctypes.c_int),
                 ("path_length", _D), ("path_cost", _D), ("path_duration", _D),
-                ("rewires", ctypes.c_int64), ("solutions", ctypes.c_int64)]
+                ("rewires", ctypes.c_int64), ("solutions", ctypes.c_int64),
+                ("extent_a", _D * 4), ("extent_b", _D * 4)]
 
 
 _planner = None
@@ -96,6 +97,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     if rc != 0:
         raise _lib.GbpError(rc, "gbp_plan_rrt_connect")
     out = {k: getattr(r, k) for k, _ in PlanResult._fields_}
+    out["extent_a"], out["extent_b"] = list(r.extent_a), list(r.extent_b)
     n = r.n_states
     out["states"] = states[:n].copy()
     out["actions"] = actions[:max(n - 1, 0)].copy()

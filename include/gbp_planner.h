@@ -318,6 +318,7 @@ struct BatchStats {
   int64_t iterations = 0, targets = 0, extends = 0, attempts_checked = 0, connects = 0;
   int64_t vertices_a = 0, vertices_b = 0;
   int64_t rewires = 0, solutions = 0;
+  double extent_a[4] = {0, 0, 0, 0}, extent_b[4] = {0, 0, 0, 0};  // x_min x_max y_min y_max
 };
 
 class RRTConnectClass : public RRTClass {
@@ -492,6 +493,7 @@ typedef struct {
   int n_states;          // path states written (<= capacity)
   double path_length, path_cost, path_duration;
   int64_t rewires, solutions;  // RRT*: edges rewired, tree connections found
+  double extent_a[4], extent_b[4];  // x_min, x_max, y_min, y_max of each tree's vertices
 } gbp_plan_result;
 
 /* plans from start to goal; path_states[capacity][8] / path_actions[capacity][10]

@@ -50,7 +50,9 @@ def main():
                    "targets": out["targets"], "extends": out["extends"],
                    "attempts": out["attempts_checked"], "connects": out["connects"],
                    "va": out["vertices_a"], "vb": out["vertices_b"],
-                   "n_states": out["n_states"], "path_length": out["path_length"]}
+                   "n_states": out["n_states"], "path_length": out["path_length"],
+                   "extent_a": [round(v, 3) for v in out["extent_a"]],
+                   "extent_b": [round(v, 3) for v in out["extent_b"]]}
             print(json.dumps(row), flush=True)
             if f:
                 f.write(json.dumps(row) + "\n")
