@@ -43,12 +43,23 @@ __device__ __forceinline__ double std_min(double a, double b) { return (b < a) ?
 __device__ __forceinline__ double std_max(double a, double b) { return (a < b) ? b : a; }
 
 // ---- device terrain view ----------------------------------------------------
-// x-major height grid z[ix*ny + iy] (== FastTerrainMap::z_data_[ix][iy]) in
-// fp32 (lossless for grid_map maps, whose layers are float) or fp64.
+// Heights FastTerrainMap::z_data_[ix][iy] in fp32 (lossless for grid_map maps,
+// whose layers are float) or fp64, stored as CELL QUADS: cell (ix, iy),
+// 0 <= ix < nx-1, 0 <= iy < ny-1, holds its four corners
+//   zq[4*(ix*(ny-1) + iy) + {0,1,2,3}] = z[ix][iy], z[ix][iy+1], z[ix+1][iy], z[ix+1][iy+1]
+// so one bilinear lookup is ONE aligned 16-B (fp32) / 2 x 16-B (fp64) load
+// from one cache line instead of four 4-B gathers from two rows.  Every
+// lookup's cell is clamped into that range, so no other z is ever read.
+// (-DGBP_ZROWS: the plain x-major z[ix*ny + iy] layout, diagnostic builds.)
+template <class ZT>
+struct alignas(4 * sizeof(ZT)) ZQuad {
+  ZT q[4];
+};
+
 template <class ZT>
 struct TerrainView {
   const double *x, *y;           // coordinates (ascending)
-  const ZT *z;                   // heights, x-major
+  const ZT *z;                   // heights: cell quads (or x-major rows with GBP_ZROWS)
   const double *dx, *dy, *dz;    // slope layers, x-major fp64, may be null
   int nx, ny;
   double x0, xN, y0, yN;         // x[0], x[nx-1], y[0], y[ny-1]
@@ -56,7 +67,26 @@ struct TerrainView {
   int one_x, one_y;              // host-verified: the guess is within one cell of the
                                  // bracket for every v (gbp_terrain_create), so a single
                                  // branch-free correction step is exact
+  // host-verified affine coordinates (gbp_terrain_create): x[i] is bit-for-bit
+  // ax + hx * (double)(i - bx) for every i (likewise y), e.g. x[i] = i * 0.02
+  // (synthetic maps) or grid_map's reversed cell centres, so CM == 2 kernels
+  // compute coordinates instead of reading them
+  int affine;
+  int bx, by;
+  double ax, hx, ay, hy;
 };
+
+// Coordinate modes of the hot kernels (template CM): 0 = coordinate vectors
+// read from global memory, 1 = staged in LDS (the pointers in the view point
+// there), 2 = computed from the verified affine form.
+template <int CM, int AX, class ZT>
+__device__ __forceinline__ double coord(const TerrainView<ZT> &T, int i) {
+  if constexpr (CM == 2) {
+    return AX == 0 ? T.ax + T.hx * (double)(i - T.bx) : T.ay + T.hy * (double)(i - T.by);
+  } else {
+    return AX == 0 ? T.x[i] : T.y[i];
+  }
+}
 
 // First i with d[i] <= v < d[i+1] (fast_terrain_map.cpp:101-117).  O(1): a
 // guess from the mean spacing, then a fix-up against the actual coordinates,
@@ -87,14 +117,51 @@ __device__ __forceinline__ int bracket(const double *__restrict__ d, int n, doub
   return i;
 }
 
+// the four corners of cell (ix, iy), ix <= nx-2, iy <= ny-2, in Probe::q order
+template <class ZT>
+__device__ __forceinline__ void fetch_cell(const TerrainView<ZT> &T, int ix, int iy, ZT q[4]) {
+#ifdef GBP_ZROWS
+  const ZT *p = T.z + (size_t)ix * T.ny + iy;
+  q[0] = p[0];
+  q[1] = p[1];
+  q[2] = p[T.ny];
+  q[3] = p[T.ny + 1];
+#else
+  const ZQuad<ZT> c = ((const ZQuad<ZT> *)T.z)[(size_t)ix * (T.ny - 1) + iy];
+  q[0] = c.q[0];
+  q[1] = c.q[1];
+  q[2] = c.q[2];
+  q[3] = c.q[3];
+#endif
+}
+
+// bracket() of axis AX of the view, coordinates per CM
+template <int CM, int AX, class ZT>
+__device__ __forceinline__ int bracket_ax(const TerrainView<ZT> &T, double v) {
+  const double d0 = AX == 0 ? T.x0 : T.y0, dN = AX == 0 ? T.xN : T.yN;
+  const int n = AX == 0 ? T.nx : T.ny;
+  if (!(v >= d0 && v < dN)) return (v >= dN) ? BR_HIGH : BR_LOW;
+  int i = bracket_guess(n, d0, AX == 0 ? T.inv_hx : T.inv_hy, v);
+#ifndef GBP_EXPERIMENT_FAST_BRACKET  // diagnostic timing build only (results may differ)
+  if (AX == 0 ? T.one_x : T.one_y) {
+    i += (v >= coord<CM, AX>(T, i + 1) ? 1 : 0) - (v < coord<CM, AX>(T, i) ? 1 : 0);
+  } else {
+    while (i > 0 && v < coord<CM, AX>(T, i)) --i;
+    while (i < n - 2 && v >= coord<CM, AX>(T, i + 1)) ++i;
+  }
+#endif
+  return i;
+}
+
 template <class ZT>
 __device__ __forceinline__ void load_quad(const TerrainView<ZT> &T, int ix, int iy, double &f11,
                                           double &f12, double &f21, double &f22) {
-  const ZT *p = T.z + (size_t)ix * T.ny + iy;
-  f11 = (double)p[0];
-  f12 = (double)p[1];
-  f21 = (double)p[T.ny];
-  f22 = (double)p[T.ny + 1];
+  ZT q[4];
+  fetch_cell(T, ix, iy, q);
+  f11 = (double)q[0];
+  f12 = (double)q[1];
+  f21 = (double)q[2];
+  f22 = (double)q[3];
 }
 
 // FastTerrainMap::heightIsNan (fast_terrain_map.cpp:135-157): -1 = UB
@@ -157,20 +224,16 @@ struct Probe {
   ZT q[4];      // z[cx][cy], z[cx][cy+1], z[cx+1][cy], z[cx+1][cy+1] of the clamped cell
 };
 
-template <class ZT>
+template <class ZT, int CM = 0>
 __device__ __forceinline__ void probe(const TerrainView<ZT> &T, double x, double y, Probe<ZT> &p) {
-  p.ix = bracket(T.x, T.nx, T.x0, T.xN, T.inv_hx, T.one_x, x);
-  p.iy = bracket(T.y, T.ny, T.y0, T.yN, T.inv_hy, T.one_y, y);
+  p.ix = bracket_ax<CM, 0>(T, x);
+  p.iy = bracket_ax<CM, 1>(T, y);
   const int cx = p.ix < 0 ? 0 : p.ix, cy = p.iy < 0 ? 0 : p.iy;
 #ifdef GBP_EXPERIMENT_NO_ZLOAD
   p.q[0] = (ZT)(cx * 1e-4); p.q[1] = (ZT)(cy * 1e-4); p.q[2] = (ZT)0.1; p.q[3] = (ZT)0.2;
   return;
 #endif
-  const ZT *z = T.z + (size_t)cx * T.ny + cy;
-  p.q[0] = z[0];
-  p.q[1] = z[1];
-  p.q[2] = z[T.ny];
-  p.q[3] = z[T.ny + 1];
+  fetch_cell(T, cx, cy, p.q);
 }
 
 // heightIsNan on a probe: -1 = UB (BR_HIGH), else the reference's bool
@@ -182,7 +245,7 @@ __device__ __forceinline__ int probe_nan(const Probe<ZT> &p) {
 }
 
 // getGroundHeight on a probe (same contract as height_at)
-template <class ZT>
+template <class ZT, int CM = 0>
 __device__ __forceinline__ bool probe_height(const TerrainView<ZT> &T, const Probe<ZT> &p,
                                              double x, double y, double &h, bool &near) {
   if (isnan(x) || isnan(y)) {
@@ -190,7 +253,8 @@ __device__ __forceinline__ bool probe_height(const TerrainView<ZT> &T, const Pro
     return true;
   }
   if (p.ix < 0 || p.iy < 0) return false;
-  const double x1 = T.x[p.ix], x2 = T.x[p.ix + 1], y1 = T.y[p.iy], y2 = T.y[p.iy + 1];
+  const double x1 = coord<CM, 0>(T, p.ix), x2 = coord<CM, 0>(T, p.ix + 1);
+  const double y1 = coord<CM, 1>(T, p.iy), y2 = coord<CM, 1>(T, p.iy + 1);
 #ifndef GBP_EXPERIMENT_NO_FRAGILE
   near = near || fabs(x - x1) < FRAGILE_EPS || fabs(x2 - x) < FRAGILE_EPS ||
          fabs(y - y1) < FRAGILE_EPS || fabs(y2 - y) < FRAGILE_EPS;
@@ -314,8 +378,9 @@ __device__ __forceinline__ bool is_valid_action(const double *a) {
 //    NaN propagates as with libm.
 // Position error from either is ~1e-16 m, far below FRAGILE_EPS = 1e-12.
 __device__ __forceinline__ void rotation_trig(double dx, double dy, double speed, double p,
-                                              double &cy, double &sy, double &cp, double &sp) {
-  if (speed > 1e-150 && speed < 1e150) {
+                                              double &cy, double &sy, double &cp, double &sp,
+                                              bool live = true) {
+  if (!live || (speed > 1e-150 && speed < 1e150)) {
     cy = dx / speed;
     sy = dy / speed;
   } else {
@@ -323,7 +388,7 @@ __device__ __forceinline__ void rotation_trig(double dx, double dy, double speed
     cy = cos(yaw);
     sy = sin(yaw);
   }
-  if (fabs(p) < 1.0) {
+  if (!live || fabs(p) < 1.0) {
     const double z = p * p;
     double ps = -1.0 / 121645100408832000.0;                  // -1/19!
     ps = __builtin_fma(ps, z, 1.0 / 355687428096000.0);       //  1/17!
@@ -352,6 +417,70 @@ __device__ __forceinline__ void rotation_trig(double dx, double dy, double speed
   }
 }
 
+// A 64-bit constant materialised at its use, in an SGPR pair: left to itself
+// the compiler hoists every polynomial coefficient of the state check out of
+// the persistent loop into VGPRs that stay live for the whole kernel (with
+// libm's atan2/sin/cos tables, ~80 VGPRs: what held the validate kernel at
+// 2 waves per SIMD).
+__device__ __forceinline__ double kc(double v) {
+  uint64_t u = __builtin_bit_cast(uint64_t, v);
+  asm volatile("" : "+s"(u));
+  return __builtin_bit_cast(double, u);
+}
+
+// isValidState's rotation (planning_utils.cpp:578-594) for a state that passed
+// checks (2)-(3), i.e. |p| < P_MAX = 1 and speed = |(dx, dy)| <= V_MAX (or
+// NaN), without libm, whose constant tables would stay resident for the whole
+// persistent loop.  Same contract as rotation_trig (decisions within
+// FRAGILE_EPS of a threshold are flagged):
+//  * yaw: cos/sin(atan2(dy, dx)) = dx/|v|, dy/|v| (<= 2 ulp).  Below 1e-150
+//    the components are first scaled by 2^600 (exact) so dx^2 + dy^2 cannot
+//    underflow; |v| = 0 takes atan2's signed-zero results, atan2(+-0, +0) =
+//    +-0 -> (1, +-0) and atan2(+-0, -0) = +-pi -> (-1, +-1.2246467991473532e-16)
+//    (the correctly rounded cos/sin of the double nearest pi).  NaN propagates.
+//  * pitch: Taylor series to p^19 / p^20 (truncation < 5e-20); NaN propagates.
+// Lanes that already failed a check run the same code on values nobody reads.
+__device__ __forceinline__ void rotation_trig_nolibm(double dx, double dy, double speed, double p,
+                                                     double &cy, double &sy, double &cp,
+                                                     double &sp) {
+  cy = dx / speed;
+  sy = dy / speed;
+  if (speed < 1e-150) {  // rare; false for NaN (the quotients are NaN, as atan2 is)
+    if (speed == 0) {
+      const bool west = signbit(dx);
+      cy = west ? -1.0 : 1.0;
+      sy = west ? copysign(1.2246467991473532e-16, dy) : dy;
+    } else {
+      const double xs = dx * 0x1p600, ys = dy * 0x1p600;
+      const double r = sqrt(xs * xs + ys * ys);
+      cy = xs / r;
+      sy = ys / r;
+    }
+  }
+  const double z = p * p;
+  double ps = kc(-1.0 / 121645100408832000.0);              // -1/19!
+  ps = __builtin_fma(ps, z, kc(1.0 / 355687428096000.0));   //  1/17!
+  ps = __builtin_fma(ps, z, kc(-1.0 / 1307674368000.0));    // -1/15!
+  ps = __builtin_fma(ps, z, kc(1.0 / 6227020800.0));        //  1/13!
+  ps = __builtin_fma(ps, z, kc(-1.0 / 39916800.0));         // -1/11!
+  ps = __builtin_fma(ps, z, kc(1.0 / 362880.0));            //  1/9!
+  ps = __builtin_fma(ps, z, kc(-1.0 / 5040.0));             // -1/7!
+  ps = __builtin_fma(ps, z, kc(1.0 / 120.0));               //  1/5!
+  ps = __builtin_fma(ps, z, kc(-1.0 / 6.0));                // -1/3!
+  sp = __builtin_fma(p * z, ps, p);
+  double pc = kc(1.0 / 2432902008176640000.0);              //  1/20!
+  pc = __builtin_fma(pc, z, kc(-1.0 / 6402373705728000.0)); // -1/18!
+  pc = __builtin_fma(pc, z, kc(1.0 / 20922789888000.0));    //  1/16!
+  pc = __builtin_fma(pc, z, kc(-1.0 / 87178291200.0));      // -1/14!
+  pc = __builtin_fma(pc, z, kc(1.0 / 479001600.0));         //  1/12!
+  pc = __builtin_fma(pc, z, kc(-1.0 / 3628800.0));          // -1/10!
+  pc = __builtin_fma(pc, z, kc(1.0 / 40320.0));             //  1/8!
+  pc = __builtin_fma(pc, z, kc(-1.0 / 720.0));              // -1/6!
+  pc = __builtin_fma(pc, z, kc(1.0 / 24.0));                //  1/4!
+  pc = __builtin_fma(pc, z, -0.5);                          // -1/2!
+  cp = __builtin_fma(z, pc, 1.0);
+}
+
 // ---- state validity: planning_utils.cpp:562-635 ------------------------------
 // Out-of-domain convention: a reached lookup with no bracket makes
 // the state invalid; GBP_F_OOD marks the cases where the reference's decision
@@ -360,8 +489,135 @@ struct Acc {
   uint32_t G, V, flags;
 };
 
-template <class ZT>
+// getGroundHeight on a probe, evaluated unconditionally (branch-free form):
+// the bilinear value of the clamped cell, `ok` = the reference's call would not
+// be UB, `near` = in-domain point within FRAGILE_EPS of a grid line
+template <class ZT, int CM>
+__device__ __forceinline__ double probe_height_bf(const TerrainView<ZT> &T, const Probe<ZT> &p,
+                                                  double x, double y, bool &ok, bool &near) {
+  const bool nanxy = isnan(x) || isnan(y);
+  const bool br = p.ix >= 0 && p.iy >= 0;
+  const int cx = br ? p.ix : 0, cy = br ? p.iy : 0;
+  const double x1 = coord<CM, 0>(T, cx), x2 = coord<CM, 0>(T, cx + 1);
+  const double y1 = coord<CM, 1>(T, cy), y2 = coord<CM, 1>(T, cy + 1);
+  ok = br || nanxy;
+#ifndef GBP_EXPERIMENT_NO_FRAGILE
+  near = br && !nanxy &&
+         (fabs(x - x1) < FRAGILE_EPS || fabs(x2 - x) < FRAGILE_EPS || fabs(y - y1) < FRAGILE_EPS ||
+          fabs(y2 - y) < FRAGILE_EPS);
+#else
+  near = false;
+#endif
+  const double h = bilinear((double)p.q[0], (double)p.q[1], (double)p.q[2], (double)p.q[3], x1, x2,
+                            y1, y2, x, y);
+  return nanxy ? __builtin_nan("") : h;
+}
+
+#ifndef GBP_BRANCHY
+// isValidState as ONE straight-line pass: every lookup, height and test is
+// evaluated for every lane, and the reference's sequence of early returns is
+// replayed as a predicate `alive` (a test only counts, sets flags or rejects
+// while every earlier test has passed).  Lanes of a wave hold unrelated
+// states, so the early-return form executes nearly every branch per wave
+// anyway and pays the exec-mask bookkeeping on top; here the wave issues one
+// path.  Same values, same decisions, same G/V and flags as the reference's
+// executed calls.
+template <class ZT, int CM = 0>
 __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int phase, Acc &acc) {
+  if (acc.V >= GBP_MAX_SAMPLES) {  // engine guard: the reference loop would not terminate
+    acc.flags |= GBP_F_LIMIT;
+    return false;
+  }
+  acc.V++;
+  Probe<ZT> pc;
+  probe<ZT, CM>(T, s[0], s[1], pc);
+  const bool outside = (s[0] < T.x0) || (s[0] > T.xN) || (s[1] < T.y0) || (s[1] > T.yN);
+  const double speed = sqrt(s[3] * s[3] + s[4] * s[4]);
+  uint32_t fl = 0;
+  // (1) heightIsNan(centre) :564 (x or y >= the last coordinate: UB, rejected
+  //     by (2) unless exactly equal)
+  const int r = probe_nan(pc);
+  if (r < 0 && !outside) fl |= GBP_F_OOD;
+  if (r > 0) fl |= GBP_F_NAN;
+  // (2) bounds + |pitch| :568-571, (3) horizontal speed :574
+  bool alive = r == 0 && !(outside || (fabs(s[6]) >= P_MAX)) && !(speed > V_MAX);
+  // (4) rotation :578-594
+#ifdef GBP_EXPERIMENT_NO_TRIG
+  const double yaw = s[4] * s[3];
+  const double cy = yaw * 0.5, sy = yaw * 0.25;
+  const double pitch = s[6];
+  const double cp = pitch * 0.5, sp = pitch * 0.25;
+#else
+  double cy, sy, cp, sp;
+  rotation_trig_nolibm(s[3], s[4], speed, s[6], cy, sy, cp, sp);
+#endif
+  const double R_11 = cy * cp, R_12 = -sy, R_13 = cy * sp;
+  const double R_21 = sy * cp, R_22 = cy, R_23 = sy * sp;
+  const double R_31 = -sp, R_32 = 0, R_33 = cp;
+  const double z_body = -ROBOT_H;
+  Probe<ZT> pl[4], pk[4], pu;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const double x_body = (k < 2) ? -0.5 * ROBOT_L : 0.5 * ROBOT_L;
+    const double y_body = (k & 1) ? 0.5 * ROBOT_W : -0.5 * ROBOT_W;
+    const double x_leg = s[0] + R_11 * x_body + R_12 * y_body;
+    const double y_leg = s[1] + R_21 * x_body + R_22 * y_body;
+    probe<ZT, CM>(T, x_leg, y_leg, pl[k]);
+    probe<ZT, CM>(T, x_leg + R_13 * z_body, y_leg + R_23 * z_body, pk[k]);
+  }
+  const double ux = s[0] + R_13 * z_body, uy = s[1] + R_23 * z_body;
+  probe<ZT, CM>(T, ux, uy, pu);
+  uint32_t G = 0;
+  // (5) four corners :601-627, x_body outer, y_body inner, in reference order
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const double x_body = (k < 2) ? -0.5 * ROBOT_L : 0.5 * ROBOT_L;
+    const double y_body = (k & 1) ? 0.5 * ROBOT_W : -0.5 * ROBOT_W;
+    const double x_leg = s[0] + R_11 * x_body + R_12 * y_body;
+    const double y_leg = s[1] + R_21 * x_body + R_22 * y_body;
+    const double z_leg = s[2] + R_31 * x_body + R_32 * y_body;
+    const double x_corner = x_leg + R_13 * z_body;
+    const double y_corner = y_leg + R_23 * z_body;
+    const double z_corner = z_leg + R_33 * z_body;
+    const int rl = probe_nan(pl[k]);  // heightIsNan(leg) :614
+    if (alive && rl < 0) fl |= GBP_F_OOD;
+    if (alive && rl > 0) fl |= GBP_F_NAN;
+    alive = alive && rl == 0;
+    G += alive ? 2u : 0u;  // both heights computed before the test :618-619
+    bool okl, okc, nl, nc;
+    const double gl = probe_height_bf<ZT, CM>(T, pl[k], x_leg, y_leg, okl, nl);
+    const double gc = probe_height_bf<ZT, CM>(T, pk[k], x_corner, y_corner, okc, nc);
+    if (alive && nl) fl |= GBP_F_FRAGILE;
+    if (alive && !okl) fl |= GBP_F_OOD;
+    alive = alive && okl;
+    if (alive && nc) fl |= GBP_F_FRAGILE;
+    if (alive && !okc) fl |= GBP_F_OOD;
+    alive = alive && okc;
+    const double leg_height = z_leg - gl;
+    const double corner_height = z_corner - gc;
+    if (alive && (fabs(corner_height - H_MIN) < FRAGILE_EPS ||
+                  (phase == GBP_STANCE && fabs(leg_height - H_MAX) < FRAGILE_EPS)))
+      fl |= GBP_F_FRAGILE;
+    alive = alive && !((corner_height < H_MIN) || ((phase == GBP_STANCE) && (leg_height > H_MAX)));
+  }
+  // (6) underside centre :630-632
+  G += alive ? 1u : 0u;
+  bool oku, nu;
+  const double gu = probe_height_bf<ZT, CM>(T, pu, ux, uy, oku, nu);
+  if (alive && nu) fl |= GBP_F_FRAGILE;
+  if (alive && !oku) fl |= GBP_F_OOD;
+  alive = alive && oku;
+  const double height = (s[2] + R_33 * z_body) - gu;
+  if (alive && fabs(height - H_MIN) < FRAGILE_EPS) fl |= GBP_F_FRAGILE;
+  alive = alive && !(height < H_MIN);
+  acc.G += G;
+  acc.flags |= fl;
+  return alive;
+}
+#else
+template <class ZT, int CM = 0>
+__device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int phase, Acc &acc) {
+  // (reads the coordinate vectors whatever CM is: they stay valid in every mode)
   if (acc.V >= GBP_MAX_SAMPLES) {  // engine guard: the reference loop would not terminate
     acc.flags |= GBP_F_LIMIT;
     return false;
@@ -471,6 +727,7 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
   if (height < H_MIN) return false;
   return true;
 }
+#endif  // GBP_BRANCHY
 
 __device__ __forceinline__ uint32_t stage_bits(uint32_t k) { return k << GBP_F_STAGE_SHIFT; }
 

@@ -37,8 +37,9 @@ namespace {
 constexpr uint64_t EXTEND_STREAM = 0x45585444ull;  // "EXTD"
 constexpr int WAVE = 64;
 
-// LDSC: the coordinate vectors are staged in LDS (bracket fix-up and the
-// bilinear x1/x2/y1/y2 then never touch global memory)
+// CM == 1: the coordinate vectors are staged in LDS (bracket fix-up and the
+// bilinear x1/x2/y1/y2 then never touch global memory); CM == 2 computes
+// them (gbp_device.h coord)
 template <class ZT>
 __device__ __forceinline__ TerrainView<ZT> stage_coords(const TerrainView<ZT> &T0, double *smem) {
   for (int i = threadIdx.x; i < T0.nx; i += blockDim.x) smem[i] = T0.x[i];
@@ -51,29 +52,30 @@ __device__ __forceinline__ TerrainView<ZT> stage_coords(const TerrainView<ZT> &T
 }
 
 // LDS bytes of stage_coords for this terrain
-inline size_t stage_bytes(int nx, int ny) { return sizeof(double) * (size_t)(nx + ny); }
+// (rounded up to 16 B so the attempt rows behind it stay 16-B aligned)
+inline size_t stage_bytes(int nx, int ny) { return sizeof(double) * (size_t)((nx + ny + 1) & ~1); }
 
 // ============================================================================
 // K1: batched terrain queries
 // ============================================================================
 // one probe per point: a single bracket pair and one cell fetch serve both
-// getGroundHeight and heightIsNan; coordinates come from LDS when LDSC.
-template <class ZT, bool LDSC>
+// getGroundHeight and heightIsNan; coordinates per CM (gbp_device.h coord).
+template <class ZT, int CM>
 __global__ __launch_bounds__(256) void k_height(TerrainView<ZT> T0, int64_t n,
                                                 const double2 *__restrict__ xy,
                                                 double *__restrict__ h,
                                                 uint8_t *__restrict__ is_nan,
                                                 uint8_t *__restrict__ ood) {
   extern __shared__ double k1_smem[];
-  const TerrainView<ZT> T = LDSC ? stage_coords(T0, k1_smem) : T0;
+  const TerrainView<ZT> T = CM == 1 ? stage_coords(T0, k1_smem) : T0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const double2 p = xy[i];
     Probe<ZT> pr;
-    probe(T, p.x, p.y, pr);
+    probe<ZT, CM>(T, p.x, p.y, pr);
     double v;
     bool near = false;
-    const bool ok = probe_height(T, pr, p.x, p.y, v, near);  // getGroundHeight
+    const bool ok = probe_height<ZT, CM>(T, pr, p.x, p.y, v, near);  // getGroundHeight
     const int r = probe_nan(pr);                              // heightIsNan
     if (h) h[i] = ok ? v : __builtin_nan("");
     if (is_nan) is_nan[i] = r != 0 ? 1 : 0;                   // UB (-1) reported as 1, like ood
@@ -120,13 +122,13 @@ __global__ void k_valid_states(TerrainView<ZT> T, int64_t n, const double *__res
 // (__launch_bounds__ 2nd argument): 1 -> up to 512 VGPR+AGPR, 2 -> 256, 4 -> 128.
 extern __shared__ double gbp_smem[];
 
-template <class ZT, bool ADAPTIVE, int W, bool LDSC>
+template <class ZT, bool ADAPTIVE, int W, int CM>
 __global__ __launch_bounds__(256, W) void k_validate_direct(
     TerrainView<ZT> T0, int64_t n, const double *__restrict__ S, const double *__restrict__ A,
     const uint8_t *__restrict__ dir, int dir_all, uint8_t *__restrict__ valid,
     double *__restrict__ s_new, double *__restrict__ t_new, uint32_t *__restrict__ flags,
     uint32_t *__restrict__ counts) {
-  const TerrainView<ZT> T = LDSC ? stage_coords(T0, gbp_smem) : T0;
+  const TerrainView<ZT> T = CM == 1 ? stage_coords(T0, gbp_smem) : T0;
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   double s[8], a[10], sn[8];
@@ -467,6 +469,15 @@ __device__ __forceinline__ bool step_lane(const TerrainView<ZT> &T, Lane &L) {
 
 #ifdef GBP_DIAG_UTIL
 __device__ unsigned long long gbp_diag[4];
+// per-wave timeline of the last launch: begin, end (wall_clock64), steps, CU id
+__device__ unsigned long long gbp_diag_wave[16384][4];
+extern "C" int gbp_diag_waves(unsigned long long *out, int n) {
+  if (n > 16384) n = 16384;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gbp_diag_wave), sizeof(unsigned long long) * 4 * n) !=
+      hipSuccess)
+    return -4;
+  return 0;
+}
 extern "C" int gbp_diag_read(unsigned long long *out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gbp_diag), sizeof(unsigned long long) * 4) != hipSuccess)
     return -4;
@@ -478,20 +489,21 @@ extern "C" int gbp_diag_read(unsigned long long *out, int reset) {
 }
 #endif
 
-template <class ZT, bool ADAPTIVE, int W, bool LDSC>
+template <class ZT, bool ADAPTIVE, int W, int CM>
 __global__ __launch_bounds__(256, W) void k_validate_persistent(
     TerrainView<ZT> T0, int n, const double *__restrict__ S, const double *__restrict__ A,
     const uint8_t *__restrict__ dir, int dir_all, uint8_t *__restrict__ valid,
     double *__restrict__ s_new, double *__restrict__ t_new, uint32_t *__restrict__ flags,
     uint32_t *__restrict__ counts, unsigned int *__restrict__ head, int sched, int chunk,
-    int helpers) {
-  const TerrainView<ZT> T = LDSC ? stage_coords(T0, gbp_smem) : T0;
+    int helpers, int prefix) {
+  const TerrainView<ZT> T = CM == 1 ? stage_coords(T0, gbp_smem) : T0;
   const int lane = threadIdx.x & (WAVE - 1);
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
-  double *const SA = gbp_smem + (LDSC ? T0.nx + T0.ny : 0);   // attempt rows
+  double *const SA = gbp_smem + (CM == 1 ? (T0.nx + T0.ny + 1) & ~1 : 0);  // attempt rows
   double *const wave_rows = SA + (size_t)(threadIdx.x & ~(WAVE - 1)) * SA_ROW;
 #ifdef GBP_DIAG_UTIL
   const unsigned long long t_begin = wall_clock64();
+  unsigned long long n_steps = 0, n_busy = 0;
 #endif
   Lane L;
   L.s = SA + (size_t)threadIdx.x * SA_ROW;
@@ -505,9 +517,25 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
   // sched 3: a fixed slice per WORKGROUP, dealt to its waves on demand from
   // an LDS counter (an LDS atomic costs ~100 cycles, a device atomic ~1 us), so
   // the waves of a workgroup even out their unequal sample totals.
+  // sched 4: a static per-wave prefix (prefix/1024 of the batch), then chunks
+  // of the rest dequeued from 8 heads, one per XCD (MI355X_MICROARCH.md
+  // 'dequeue': one head saturates near 88 dequeues/us), a wave starting at its
+  // workgroup's XCD shard and moving on to the next shard when one runs dry.
+  // The XCDs of one launch run at visibly different speeds (tools/timeline.py),
+  // so fixed slices leave the fast ones idle for the kernel's last third.
   __shared__ unsigned int wg_head;
   unsigned int cur = 0, end = 0, wg_begin = 0, wg_end = 0;
-  if (sched == 1) {
+  unsigned int dyn0 = 0;  // sched 4: first dynamically dealt attempt
+  int shard = 0, shards_left = 8;
+  if (sched == 4) {
+    const unsigned int waves = gridDim.x * (blockDim.x / WAVE);
+    const unsigned int wid = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+    const unsigned int per = (unsigned int)(((unsigned long long)n * (unsigned)prefix / 1024u) / waves);
+    cur = per * wid;
+    end = cur + per;
+    dyn0 = per * waves;
+    shard = blockIdx.x & 7;
+  } else if (sched == 1) {
     const unsigned int waves = gridDim.x * (blockDim.x / WAVE);
     const unsigned int wid = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
     cur = (unsigned int)(((unsigned long long)n * wid) / waves);
@@ -526,7 +554,24 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
         unsigned int base = 0xFFFFFFFFu;
         const unsigned int grab = chunk > 0 ? (unsigned int)chunk : (unsigned int)__popcll(m);
         const int leader = __ffsll((long long)m) - 1;
-        if (sched == 3) {
+        unsigned int lim = (unsigned int)n;
+        if (sched == 4) {
+          while (shards_left > 0) {  // wave-uniform
+            const unsigned long long rest = (unsigned long long)((unsigned int)n - dyn0);
+            const unsigned int lo = dyn0 + (unsigned int)(rest * (unsigned)shard / 8u);
+            const unsigned int hi = dyn0 + (unsigned int)(rest * (unsigned)(shard + 1) / 8u);
+            unsigned int b = 0xFFFFFFFFu;
+            if (lane == leader) b = lo + atomicAdd(head + 32 * shard, grab);
+            b = __shfl(b, leader);
+            if (b < hi) {
+              base = b;
+              lim = hi;
+              break;
+            }
+            shard = (shard + 1) & 7;
+            shards_left--;
+          }
+        } else if (sched == 3) {
           if (lane == leader) base = wg_begin + atomicAdd(&wg_head, grab);
           base = __shfl(base, leader);
           if (base >= wg_end) base = 0xFFFFFFFFu;
@@ -539,7 +584,7 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
           break;
         }
         cur = base;
-        end = min(base + grab, sched == 3 ? wg_end : (unsigned int)n);
+        end = min(base + grab, sched == 3 ? wg_end : lim);
       }
     const unsigned int take = min(end - cur, (unsigned int)__popcll(m));
       const unsigned int rank = (unsigned int)__popcll(m & lt_mask);
@@ -547,10 +592,15 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
       if (mine) {
         const unsigned int i = cur + rank;
         L.idx = (int)i;
+#ifdef GBP_EXPERIMENT_HOT_INPUTS  // diagnostic timing build only: rows from an L2-hot subset
+        const unsigned int ii = i & 4095u;
+#else
+        const unsigned int ii = i;
+#endif
 #pragma unroll
-        for (int k = 0; k < 8; k++) L.s[k] = S[8 * (size_t)i + k];
+        for (int k = 0; k < 8; k++) L.s[k] = S[8 * (size_t)ii + k];
 #pragma unroll
-        for (int k = 0; k < 10; k++) L.a[k] = A[10 * (size_t)i + k];
+        for (int k = 0; k < 10; k++) L.a[k] = A[10 * (size_t)ii + k];
         L.f = 0;
         L.acc = Acc{0, 0, 0};
         L.snew_kind = SN_NONE;
@@ -597,10 +647,8 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
 #ifdef GBP_DIAG_UTIL  // diagnostic build: lane utilisation of the sample steps
     {
       const unsigned long long busy = __ballot(has);
-      if (lane == 0) {
-        atomicAdd(&gbp_diag[0], 1ull);
-        atomicAdd(&gbp_diag[1], (unsigned long long)__popcll(busy));
-      }
+      n_busy += (unsigned long long)__popcll(busy);  // one atomic per wave at the end:
+      n_steps++;                                      // per-step atomics distort timing
     }
 #endif
     Acc acc_s{0, vbase + (uint32_t)slot, 0};
@@ -608,7 +656,7 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
     if (has) {
       double sc[8];
       sample_state(ps, ps + 8, st, t_eval, sc);
-      ok = is_valid_state(T, sc, stage_phase(st), acc_s);
+      ok = is_valid_state<ZT, CM>(T, sc, stage_phase(st), acc_s);
     }
     bool decided = false;
     if (owner) {  // the lane's own sample
@@ -651,16 +699,24 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
         if (L.snew_kind != SN_NONE) f |= GBP_F_SNEW_SET;
         if (L.tnew_set) f |= GBP_F_TNEW_SET;
         if (valid) valid[i] = (f & GBP_F_VALID) ? 1 : 0;
+#ifdef GBP_EXPERIMENT_NO_SNEW  // diagnostic timing build only (s_new not written)
+        if (false) {
+#else
         if (s_new && L.snew_kind != SN_NONE) {
+#endif
           double o[8];
           double sv[8], av[10];
 #pragma unroll
           for (int k = 0; k < 8; k++) sv[k] = L.s[k];
 #pragma unroll
           for (int k = 0; k < 10; k++) av[k] = L.a[k];
-          if (L.snew_kind == SN_STANCE_S) apply_stance(sv, av, L.snew_p, o);
-          else if (L.snew_kind == SN_FLIGHT_B) sample_state(sv, av, ST_FWD_LAND, L.snew_p, o);
-          else sample_state(sv, av, ST_REV_STANCE, L.snew_p, o);
+          // one closed form for every kind: sample_state at FWD_STANCE is
+          // apply_stance's expression tree (same operands, same bits)
+          sample_state(sv, av,
+                       L.snew_kind == SN_STANCE_S
+                           ? ST_FWD_STANCE
+                           : (L.snew_kind == SN_FLIGHT_B ? ST_FWD_LAND : ST_REV_STANCE),
+                       L.snew_p, o);
 #pragma unroll
           for (int k = 0; k < 8; k++) s_new[8 * i + k] = o[k];
         }
@@ -673,9 +729,19 @@ __global__ __launch_bounds__(256, W) void k_validate_persistent(
   }
 #ifdef GBP_DIAG_UTIL
   if (lane == 0) {
-    const unsigned long long dt = wall_clock64() - t_begin;
+    const unsigned long long t_end = wall_clock64();
+    const unsigned long long dt = t_end - t_begin;
+    atomicAdd(&gbp_diag[0], n_steps);
+    atomicAdd(&gbp_diag[1], n_busy);
     atomicAdd(&gbp_diag[2], dt);
     atomicMax(&gbp_diag[3], dt);
+    const unsigned int wid = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+    if (wid < 16384) {
+      gbp_diag_wave[wid][0] = t_begin;
+      gbp_diag_wave[wid][1] = t_end;
+      gbp_diag_wave[wid][2] = n_steps;
+      gbp_diag_wave[wid][3] = (unsigned long long)__smid();
+    }
   }
 #endif
 }
@@ -956,6 +1022,11 @@ struct gbp_terrain {
   int64_t opt_sched = 1;            // persistent work source: 0 atomic, 1 static, 2 chunked
   int64_t opt_chunk = 0;            // dequeue granularity for sched 0/2 (0 = per need)
   int64_t opt_helpers = 1;          // idle lanes of a drained wave evaluate owners' next samples
+  int64_t opt_prefix = 512;         // sched 4: statically dealt share of a batch (1/1024)
+  int64_t opt_affine = 1;           // compute coordinates when the affine form is exact
+  int affine = 0;                   // host-verified affine coordinates (both axes)
+  int bx = 0, by = 0;
+  double ax = 0, hx = 0, ay = 0, hy = 0;
   unsigned int *d_head = nullptr;   // persistent-kernel work counter (zeroed per launch)
   size_t lds_max = 65536;           // LDS bytes a workgroup may use
   hipStream_t host_stream = nullptr;
@@ -1003,6 +1074,13 @@ TerrainView<ZT> view(const gbp_terrain *t) {
   v.inv_hy = t->inv_hy;
   v.one_x = t->one_x;
   v.one_y = t->one_y;
+  v.affine = t->affine;
+  v.bx = t->bx;
+  v.by = t->by;
+  v.ax = t->ax;
+  v.hx = t->hx;
+  v.ay = t->ay;
+  v.hy = t->hy;
   return v;
 }
 
@@ -1027,13 +1105,22 @@ int ensure_ws(gbp_terrain *t, void **ws, size_t *have, size_t need) {
   return GBP_OK;
 }
 
-template <class ZT, bool AD, int W, bool LDSC>
+// coordinate mode of the hot kernels (gbp_device.h coord): LDS-staged vectors
+// when they fit (measured 1-2 % ahead of computing them at 1024^2), else the
+// verified affine form (e.g. 4096^2, whose vectors leave no LDS for the
+// attempt rows), else global memory
+int coord_mode(const gbp_terrain *t, bool lds_ok) {
+  if (lds_ok) return 1;
+  return (t->opt_affine && t->affine) ? 2 : 0;
+}
+
+template <class ZT, bool AD, int W, int CM>
 int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *a,
                       const uint8_t *dir, int dir_all, uint8_t *valid, double *s_new,
                       double *t_new, uint32_t *flags, uint32_t *counts, hipStream_t st) {
   const TerrainView<ZT> T = view<ZT>(t);
   const int block = (int)t->opt_block;
-  const size_t coords = LDSC ? stage_bytes(t->nx, t->ny) : 0;
+  const size_t coords = CM == 1 ? stage_bytes(t->nx, t->ny) : 0;
   const size_t rows = sizeof(double) * SA_ROW * (size_t)block;  // persistent kernel only
   const int64_t chunk = (int64_t)1 << 30;
   const int64_t want = (int64_t)t->num_cus * t->opt_grid_per_cu;
@@ -1048,20 +1135,22 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
       // the direct form inlines the state check at five call sites: it gets the
       // whole register file (W = 1) whatever the persistent kernel's budget is
       const unsigned g = (unsigned)((m + block - 1) / block);
-      hipLaunchKernelGGL((k_validate_direct<ZT, AD, 1, LDSC>), dim3(g), dim3(block), coords, st, T, m,
+      hipLaunchKernelGGL((k_validate_direct<ZT, AD, 1, CM == 2 ? 0 : CM>), dim3(g), dim3(block), coords, st, T, m,
                          s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn, flags + off, c);
     } else {
       // persistent: grid sized to residency; the work counter is zeroed per launch
       const int64_t resident = (int64_t)t->num_cus * std::max<int64_t>(1, W * 256 / block);
-      const int64_t g = std::max<int64_t>(
-          1, std::min<int64_t>(t->opt_sched == 1 || t->opt_sched == 3 ? resident : want,
-                               (m + block - 1) / block));
+      const bool fixed_grid = t->opt_sched == 1 || t->opt_sched >= 3;
+      const int64_t g =
+          std::max<int64_t>(1, std::min<int64_t>(fixed_grid ? resident : want, (m + block - 1) / block));
       if (t->opt_sched == 0 || t->opt_sched == 2)
         HIPCHK(hipMemsetAsync(t->d_head, 0, sizeof(unsigned int), st));
-      hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, LDSC>), dim3((unsigned)g), dim3(block),
+      if (t->opt_sched == 4) HIPCHK(hipMemsetAsync(t->d_head, 0, 8 * 128, st));
+      hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, CM>), dim3((unsigned)g), dim3(block),
                          coords + rows, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
-                         flags + off, c, t->d_head, (int)t->opt_sched, (int)t->opt_chunk,
-                         (int)t->opt_helpers);
+                         flags + off, c, t->d_head, (int)t->opt_sched,
+                         (int)(t->opt_sched == 4 && t->opt_chunk == 0 ? 32 : t->opt_chunk),
+                         (int)t->opt_helpers, (int)t->opt_prefix);
     }
     HIPCHK(hipGetLastError());
   }
@@ -1073,21 +1162,26 @@ int launch_validate(gbp_terrain *t, int64_t n, const double *s, const double *a,
                     const uint8_t *dir, int dir_all, int adaptive, uint8_t *valid,
                     double *s_new, double *t_new, uint32_t *flags, uint32_t *counts,
                     hipStream_t st) {
-#define GBP_LV(AD, W)                                                                         \
-  (lds_ok ? launch_validate_w<ZT, AD, W, true>(t, n, s, a, dir, dir_all, valid, s_new, t_new,  \
-                                               flags, counts, st)                              \
-          : launch_validate_w<ZT, AD, W, false>(t, n, s, a, dir, dir_all, valid, s_new, t_new, \
-                                                flags, counts, st))
+#define GBP_LV(AD, W)                                                                       \
+  (cm == 2 ? launch_validate_w<ZT, AD, W, 2>(t, n, s, a, dir, dir_all, valid, s_new, t_new,  \
+                                             flags, counts, st)                              \
+   : cm == 1 ? launch_validate_w<ZT, AD, W, 1>(t, n, s, a, dir, dir_all, valid, s_new, t_new, \
+                                               flags, counts, st)                            \
+             : launch_validate_w<ZT, AD, W, 0>(t, n, s, a, dir, dir_all, valid, s_new, t_new, \
+                                               flags, counts, st))
   const int64_t w = t->opt_waves;
-  // coordinates in LDS only if they fit next to the attempt rows, with room
-  // for the W workgroups of 256 lanes that share a CU (160 KB per CU)
+  // coordinates computed when the affine form is exact; else in LDS only if
+  // they fit next to the attempt rows, with room for the W workgroups of 256
+  // lanes that share a CU (160 KB per CU); else read from global memory
   const size_t rows = sizeof(double) * SA_ROW * (size_t)t->opt_block;
   const size_t per_cu = std::max<int64_t>(1, (int64_t)w * 256 / t->opt_block) *
                         (stage_bytes(t->nx, t->ny) + rows);
   const bool lds_ok = t->opt_lds_coords && stage_bytes(t->nx, t->ny) + rows <= t->lds_max &&
                       (t->opt_kernel == GBP_KERNEL_DIRECT || per_cu <= 160 * 1024);
-  if (adaptive) return w >= 4 ? GBP_LV(true, 4) : (w >= 2 ? GBP_LV(true, 2) : GBP_LV(true, 1));
-  return w >= 4 ? GBP_LV(false, 4) : (w >= 2 ? GBP_LV(false, 2) : GBP_LV(false, 1));
+  const int cm = coord_mode(t, lds_ok);
+  // W = 1 and 2 give the same allocation (the kernel needs < 256 VGPRs)
+  if (adaptive) return w >= 4 ? GBP_LV(true, 4) : (w == 3 ? GBP_LV(true, 3) : GBP_LV(true, 2));
+  return w >= 4 ? GBP_LV(false, 4) : (w == 3 ? GBP_LV(false, 3) : GBP_LV(false, 2));
 #undef GBP_LV
 }
 
@@ -1111,6 +1205,41 @@ int one_step_exact(const double *d, int n, double inv) {
     if (lo < i - 1 || hi > i + 1) return 0;
   }
   return 1;
+}
+
+// Is d[i] == a + h * (double)(i - base) bit for bit for every i?  Tried with
+// base 0 (a = d[0]) and base n-1 (a = d[n-1], grid_map's reversed cell
+// centres) and h within a few ulps of the end-to-end and first/last spacings.
+// The device evaluates the same expression (no contraction in either TU).
+bool affine_exact(const double *d, int n, double a, double h, int base) {
+  for (int i = 0; i < n; i++) {
+    const double v = a + h * (double)(i - base);
+    if (memcmp(&v, &d[i], sizeof v) != 0) return false;
+  }
+  return true;
+}
+
+bool affine_fit(const double *d, int n, double *a, double *h, int *base) {
+  if (n < 2) return false;
+  const double cands[3] = {(d[n - 1] - d[0]) / (double)(n - 1), d[1] - d[0], d[n - 1] - d[n - 2]};
+  for (int b = 0; b < 2; b++) {
+    const int bs = b ? n - 1 : 0;
+    const double av = d[bs];
+    for (double c : cands) {
+      if (!(c > 0) || !std::isfinite(c)) continue;
+      double hv = c;
+      for (int k = 0; k < 4; k++) hv = std::nextafter(hv, -INFINITY);
+      for (int k = 0; k < 9; k++, hv = std::nextafter(hv, INFINITY)) {
+        if (affine_exact(d, n, av, hv, bs)) {
+          *a = av;
+          *h = hv;
+          *base = bs;
+          return true;
+        }
+      }
+    }
+  }
+  return false;
 }
 
 // host-pointer entry points: one synchronous staging round trip through the
@@ -1228,6 +1357,7 @@ int gbp_terrain_create(int device, int nx, int ny, const double *x, const double
   t->inv_hy = (y[ny - 1] > y[0]) ? (double)(ny - 1) / (y[ny - 1] - y[0]) : 0.0;
   t->one_x = one_step_exact(x, nx, t->inv_hx);
   t->one_y = one_step_exact(y, ny, t->inv_hy);
+  t->affine = affine_fit(x, nx, &t->ax, &t->hx, &t->bx) && affine_fit(y, ny, &t->ay, &t->hy, &t->by);
   (void)hipDeviceGetAttribute(&t->num_cus, hipDeviceAttributeMultiprocessorCount, device);
   if (t->num_cus <= 0) t->num_cus = 256;
   int rc = GBP_OK;
@@ -1241,15 +1371,28 @@ int gbp_terrain_create(int device, int nx, int ny, const double *x, const double
     return fail(GBP_E_HIP);
   if (hipMemcpy(t->d_y, y, sizeof(double) * ny, hipMemcpyHostToDevice) != hipSuccess)
     return fail(GBP_E_HIP);
+  // heights as cell quads (gbp_device.h TerrainView), or rows with GBP_ZROWS
+#ifdef GBP_ZROWS
+  const size_t zcount = cells;
+  auto zsrc = [&](size_t k) { return z[k]; };
+#else
+  const size_t qx = (size_t)nx - 1, qy = (size_t)ny - 1, zcount = 4 * qx * qy;
+  auto zsrc = [&](size_t k) {
+    const size_t c = k >> 2, ix = c / qy, iy = c % qy, corner = k & 3;
+    return z[(ix + (corner >> 1)) * (size_t)ny + iy + (corner & 1)];
+  };
+#endif
   if (storage == GBP_STORAGE_F32) {
-    std::vector<float> zf(cells);
-    for (size_t i = 0; i < cells; i++) zf[i] = (float)z[i];
-    if (hipMalloc(&t->d_z, sizeof(float) * cells) != hipSuccess) return fail(GBP_E_ALLOC);
-    if (hipMemcpy(t->d_z, zf.data(), sizeof(float) * cells, hipMemcpyHostToDevice) != hipSuccess)
+    std::vector<float> zf(zcount);
+    for (size_t i = 0; i < zcount; i++) zf[i] = (float)zsrc(i);
+    if (hipMalloc(&t->d_z, sizeof(float) * zcount) != hipSuccess) return fail(GBP_E_ALLOC);
+    if (hipMemcpy(t->d_z, zf.data(), sizeof(float) * zcount, hipMemcpyHostToDevice) != hipSuccess)
       return fail(GBP_E_HIP);
   } else {
-    if (hipMalloc(&t->d_z, sizeof(double) * cells) != hipSuccess) return fail(GBP_E_ALLOC);
-    if (hipMemcpy(t->d_z, z, sizeof(double) * cells, hipMemcpyHostToDevice) != hipSuccess)
+    std::vector<double> zd(zcount);
+    for (size_t i = 0; i < zcount; i++) zd[i] = zsrc(i);
+    if (hipMalloc(&t->d_z, sizeof(double) * zcount) != hipSuccess) return fail(GBP_E_ALLOC);
+    if (hipMemcpy(t->d_z, zd.data(), sizeof(double) * zcount, hipMemcpyHostToDevice) != hipSuccess)
       return fail(GBP_E_HIP);
   }
   if (dx) {
@@ -1262,7 +1405,7 @@ int gbp_terrain_create(int device, int nx, int ny, const double *x, const double
         return fail(GBP_E_HIP);
     }
   }
-  if (hipMalloc((void **)&t->d_head, 256) != hipSuccess) return fail(GBP_E_ALLOC);
+  if (hipMalloc((void **)&t->d_head, 8 * 128) != hipSuccess) return fail(GBP_E_ALLOC);
   {
     int lm = 0;
     if (hipDeviceGetAttribute(&lm, hipDeviceAttributeMaxSharedMemoryPerBlock, device) ==
@@ -1315,14 +1458,14 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
       t->opt_grid_per_cu = value;
       return GBP_OK;
     case GBP_OPT_WAVES:
-      if (value != 1 && value != 2 && value != 4) return GBP_E_INVALID_ARG;
+      if (value < 1 || value > 4) return GBP_E_INVALID_ARG;
       t->opt_waves = value;
       return GBP_OK;
     case GBP_OPT_LDS_COORDS:
       t->opt_lds_coords = value ? 1 : 0;
       return GBP_OK;
     case GBP_OPT_SCHED:
-      if (value < 0 || value > 3) return GBP_E_INVALID_ARG;
+      if (value < 0 || value > 4) return GBP_E_INVALID_ARG;
       t->opt_sched = value;
       return GBP_OK;
     case GBP_OPT_CHUNK:
@@ -1331,6 +1474,13 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
       return GBP_OK;
     case GBP_OPT_HELPERS:
       t->opt_helpers = value ? 1 : 0;
+      return GBP_OK;
+    case GBP_OPT_AFFINE_COORDS:
+      t->opt_affine = value ? 1 : 0;
+      return GBP_OK;
+    case GBP_OPT_PREFIX:
+      if (value < 0 || value > 1024) return GBP_E_INVALID_ARG;
+      t->opt_prefix = value;
       return GBP_OK;
     default:
       return GBP_E_INVALID_ARG;
@@ -1349,6 +1499,9 @@ int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value) {
     case GBP_OPT_SCHED: *value = t->opt_sched; return GBP_OK;
     case GBP_OPT_CHUNK: *value = t->opt_chunk; return GBP_OK;
     case GBP_OPT_HELPERS: *value = t->opt_helpers; return GBP_OK;
+    case GBP_OPT_AFFINE_COORDS: *value = t->opt_affine; return GBP_OK;
+    case GBP_OPT_PREFIX: *value = t->opt_prefix; return GBP_OK;
+    case GBP_OPT_COORD_MODE: *value = coord_mode(t, t->opt_lds_coords != 0); return GBP_OK;
     default: return GBP_E_INVALID_ARG;
   }
 }
@@ -1367,21 +1520,20 @@ int gbp_height_batch_dev(gbp_terrain *t, int64_t n, const double *xy, double *he
   const unsigned grid = grid_for(n, 256, t->num_cus * 8);
   const double2 *p = (const double2 *)xy;
   hipStream_t st = (hipStream_t)stream;
+  const int cm = coord_mode(t, lds);
+#define GBP_K1(ZT, CM)                                                                      \
+  hipLaunchKernelGGL((k_height<ZT, CM>), dim3(grid), dim3(256), CM == 1 ? cbytes : 0, st, \
+                     view<ZT>(t), n, p, height, is_nan, ood)
   if (t->storage == GBP_STORAGE_F32) {
-    if (lds)
-      hipLaunchKernelGGL((k_height<float, true>), dim3(grid), dim3(256), cbytes, st,
-                         view<float>(t), n, p, height, is_nan, ood);
-    else
-      hipLaunchKernelGGL((k_height<float, false>), dim3(grid), dim3(256), 0, st, view<float>(t),
-                         n, p, height, is_nan, ood);
+    if (cm == 2) GBP_K1(float, 2);
+    else if (cm == 1) GBP_K1(float, 1);
+    else GBP_K1(float, 0);
   } else {
-    if (lds)
-      hipLaunchKernelGGL((k_height<double, true>), dim3(grid), dim3(256), cbytes, st,
-                         view<double>(t), n, p, height, is_nan, ood);
-    else
-      hipLaunchKernelGGL((k_height<double, false>), dim3(grid), dim3(256), 0, st,
-                         view<double>(t), n, p, height, is_nan, ood);
+    if (cm == 2) GBP_K1(double, 2);
+    else if (cm == 1) GBP_K1(double, 1);
+    else GBP_K1(double, 0);
   }
+#undef GBP_K1
   HIPCHK(hipGetLastError());
   return GBP_OK;
 }

@@ -119,14 +119,19 @@ int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage,
 #define GBP_OPT_KERNEL        1  /* GBP_KERNEL_* for the validate/extend entry points */
 #define GBP_OPT_BLOCK         2  /* threads per workgroup (multiple of 64)            */
 #define GBP_OPT_GRID_PER_CU   3  /* persistent kernel: workgroups per CU              */
-#define GBP_OPT_WAVES         4  /* register budget: min waves per SIMD (1, 2 or 4)   */
+#define GBP_OPT_WAVES         4  /* register budget: min waves per SIMD (1..4)        */
 #define GBP_OPT_LDS_COORDS    5  /* 1: stage coordinate vectors in LDS when they fit  */
 #define GBP_OPT_SCHED         6  /* persistent work source: 0 one atomic counter,
                                     1 static per-wave slices, 2 chunked counter,
-                                    3 per-workgroup slices dealt from an LDS counter */
+                                    3 per-workgroup slices dealt from an LDS counter,
+                                    4 static per-wave prefix + chunks from 8 per-XCD heads */
 #define GBP_OPT_CHUNK         7  /* attempts per dequeue for sched 0 / 2 (0 = per need) */
 #define GBP_OPT_HELPERS       8  /* 1: a drained wave's idle lanes evaluate the remaining
                                     attempts' next samples ahead (default 1)          */
+#define GBP_OPT_AFFINE_COORDS 9  /* 1 (default): compute grid coordinates when the host
+                                    verified x[i] == a + h*(i - b) bit for bit         */
+#define GBP_OPT_COORD_MODE   10  /* read-only: 2 computed, 1 LDS-staged, 0 global      */
+#define GBP_OPT_PREFIX       11  /* sched 4: statically dealt share, 1/1024 (def. 512) */
 #define GBP_KERNEL_DIRECT     0  /* one lane per attempt                              */
 #define GBP_KERNEL_PERSISTENT 1  /* persistent waves, lanes re-packed per sample      */
 int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value);

@@ -44,9 +44,12 @@ def np_(t):
 
 
 # ---- K1 ----------------------------------------------------------------------
+@pytest.mark.parametrize("coords", [1, 2, 0])
 @pytest.mark.parametrize("name", TERRAINS)
-def test_height_and_normal_parity(gpu, name):
+def test_height_and_normal_parity(gpu, name, coords):
     data, T, O = terrain_pair(name)
+    T.set_option(L.OPT_LDS_COORDS, 1 if coords == 1 else 0)
+    T.set_option(L.OPT_AFFINE_COORDS, 1 if coords == 2 else 0)
     rng = np.random.default_rng(1)
     x0, xN, y0, yN = data.bounds
     n = 20000
@@ -70,6 +73,8 @@ def test_height_and_normal_parity(gpu, name):
     assert np.array_equal(np_(nood), rnood)
     ok = rnood == 0
     assert np.array_equal(bits(np_(nrm)[ok]), bits(rn[ok]))
+    T.set_option(L.OPT_LDS_COORDS, 1)
+    T.set_option(L.OPT_AFFINE_COORDS, 1)
 
 
 def test_height_nan_cells(gpu):
@@ -133,7 +138,7 @@ def test_validate_pairs_parity(gpu, name, kernel, adaptive):
 
 
 @pytest.mark.parametrize("kernel", [L.KERNEL_DIRECT, L.KERNEL_PERSISTENT])
-@pytest.mark.parametrize("waves", [1, 2, 4])
+@pytest.mark.parametrize("waves", [1, 2, 3, 4])
 def test_validate_pairs_register_variants(gpu, kernel, waves):
     data, T, O = terrain_pair("synth-rough-256")
     T.set_option(L.OPT_KERNEL, kernel)
@@ -307,18 +312,23 @@ def test_full_size_batch_properties(gpu):
     assert 0 < ref[0].sum() < n
 
 
-@pytest.mark.parametrize("sched,chunk", [(0, 0), (1, 0), (2, 64), (2, 7), (3, 0), (3, 16)])
-@pytest.mark.parametrize("lds", [0, 1])
+@pytest.mark.parametrize("sched,chunk", [(0, 0), (1, 0), (2, 64), (2, 7), (3, 0), (3, 16),
+                                         (4, 0), (4, 5)])
+@pytest.mark.parametrize("coords", [0, 1, 2])
 @pytest.mark.parametrize("helpers", [0, 1])
-def test_validate_pairs_schedulers(gpu, sched, chunk, lds, helpers):
-    """Every work-distribution mode of the persistent kernel, with and without
-    tail helper lanes, computes the same answers."""
+def test_validate_pairs_schedulers(gpu, sched, chunk, coords, helpers):
+    """Every work-distribution mode of the persistent kernel, every coordinate
+    source (0 global vectors, 1 LDS-staged, 2 computed from the verified affine
+    form), with and without tail helper lanes, computes the same answers."""
     data, T, O = terrain_pair("synth-rough-256")
     T.set_option(L.OPT_KERNEL, L.KERNEL_PERSISTENT)
     T.set_option(L.OPT_SCHED, sched)
     T.set_option(L.OPT_CHUNK, chunk)
-    T.set_option(L.OPT_LDS_COORDS, lds)
+    T.set_option(L.OPT_PREFIX, 300)
+    T.set_option(L.OPT_LDS_COORDS, 1 if coords == 1 else 0)
+    T.set_option(L.OPT_AFFINE_COORDS, 1 if coords == 2 else 0)
     T.set_option(L.OPT_HELPERS, helpers)
+    assert T.get_option(L.OPT_COORD_MODE) == coords
     try:
         for n in (1, 63, 5000):
             s, a, d, _, _ = attempts_oracle(O, n, seed=1000 + n)
@@ -328,7 +338,9 @@ def test_validate_pairs_schedulers(gpu, sched, chunk, lds, helpers):
     finally:
         T.set_option(L.OPT_SCHED, 1)
         T.set_option(L.OPT_CHUNK, 0)
+        T.set_option(L.OPT_PREFIX, 512)
         T.set_option(L.OPT_LDS_COORDS, 1)
+        T.set_option(L.OPT_AFFINE_COORDS, 1)
         T.set_option(L.OPT_HELPERS, 1)
 
 

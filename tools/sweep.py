@@ -28,8 +28,8 @@ def main():
     p.add_argument("--waves", default="1,2,4")
     p.add_argument("--grid", default="4,8,16")
     p.add_argument("--block", default="256")
-    p.add_argument("--lds", default="1")
-    p.add_argument("--sched", default="0", help="comma list of sched:chunk, e.g. 0:0,1:0,2:64")
+    p.add_argument("--lds", default="2", help="coordinates: 0 global, 1 LDS, 2 computed (affine)")
+    p.add_argument("--sched", default="0", help="comma list of sched:chunk[:prefix], e.g. 0:0,1:0,2:64,4:32:512")
     p.add_argument("--adaptive", action="store_true")
     p.add_argument("--out", default=None)
     a = p.parse_args()
@@ -53,9 +53,11 @@ def main():
             k, w, b, g, lds, sc = v
             T.set_option(L.OPT_SCHED, int(sc.split(":")[0]))
             T.set_option(L.OPT_CHUNK, int(sc.split(":")[1]))
+            T.set_option(L.OPT_PREFIX, int(sc.split(":")[2]) if sc.count(":") >= 2 else 512)
             T.set_option(L.OPT_KERNEL, L.KERNEL_PERSISTENT if k == "persistent" else L.KERNEL_DIRECT)
             T.set_option(L.OPT_WAVES, w)
-            T.set_option(L.OPT_LDS_COORDS, lds)
+            T.set_option(L.OPT_LDS_COORDS, 1 if lds >= 1 else 0)
+            T.set_option(L.OPT_AFFINE_COORDS, 1 if lds == 2 else 0)
             T.set_option(L.OPT_BLOCK, b)
             if g:
                 T.set_option(L.OPT_GRID_PER_CU, g)
