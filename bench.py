@@ -11,11 +11,17 @@ Multi-GPU: one process per GPU (torchrun), each rank its own contiguous shard,
 no data-path collective ("scaling": "weak"); only the timing max and the
 counter sums cross ranks.
 
+The timed region is K back-to-back launches (no events inside); a second
+pass of K launches bracketed by HIP events on the launch stream gives the
+kernel's own duration for the roofline.
+
 Extra fields: `roofline` for the validate kernel (algorithmic bytes per
 SURVEY §8(d): 144 B in + 76 B out + 32 B x (G + V) per attempt, G/V = the
 executed getGroundHeight / isValidState calls reported by the kernel itself,
 over the HIP-event-timed kernel duration), `cpu_baseline` (the CPU
-restatement with the reference's O(N) scans, one host thread, rank 0, N=1).
+restatement with the reference's O(N) scans, one host thread, rank 0, N=1),
+`cpu_baseline_all_cores` (same, OpenMP over the job's host threads),
+`terrain_lookup` (the K1 lookup microbenchmark with its own roofline).
 """
 import argparse
 import json
@@ -57,6 +63,8 @@ def parse():
                    help="bounded CPU-baseline sample (0 disables)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--out", default=None, help="also write the JSON line here")
+    p.add_argument("--lookup-micro", type=int, default=1,
+                   help="also run the K1 terrain-lookup microbenchmark (rank 0)")
     p.add_argument("--ttfs-runs", type=int, default=3,
                    help="batched RRT-Connect runs for time-to-first-solution (0 disables)")
     p.add_argument("--plan-batch", type=int, default=256, help="targets per half-iteration")
@@ -64,26 +72,65 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(data, s, a, d, seconds):
-    """The oracle (reference algorithm, O(N) scans) on this host, 1 thread."""
+def cpu_baseline(data, s, a, d, seconds, threads=1):
+    """The oracle (reference algorithm, O(N) scans) on this host: 1 thread (the
+    reference's execution model) or `threads` OpenMP threads over attempts."""
     try:
         import oracle
     except Exception as e:  # pragma: no cover
         return {"value": None, "error": f"oracle unavailable: {e}"}
     O = oracle.OracleTerrain.from_data(data)
     oracle.set_scan_mode(0)
-    n_total, done, chunk = s.shape[0], 0, 256
+    n_total, done, chunk = s.shape[0], 0, 256 * threads
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds and done < n_total:
         hi = min(n_total, done + chunk)
-        O.validate_pairs(s[done:hi], a[done:hi], d[done:hi], nthreads=1)
+        O.validate_pairs(s[done:hi], a[done:hi], d[done:hi], nthreads=threads)
         done = hi
     dt = time.perf_counter() - t0
-    return {"value": round(done / dt, 1), "unit": "extend-attempts/s", "cores": 1,
+    return {"value": round(done / dt, 1), "unit": "extend-attempts/s", "cores": threads,
             "kind": "port",
             "sample": f"first {done} attempts of the same batch on the host CPU "
-                      f"({dt:.1f} s, 1 thread, oracle/gbp_oracle.c linear-scan brackets)",
+                      f"({dt:.1f} s, {threads} thread(s), oracle/gbp_oracle.c linear-scan brackets)",
             "host_cpu": _cpu_model(), "host_threads_available": os.cpu_count()}
+
+
+def terrain_lookup_micro(T, data, dev, points=1 << 24, launches=10):
+    """K1 (SURVEY §8(d) 'terrain-lookup microbenchmark', target >= 40 % of HBM
+    roofline): 2^24 uniform in-domain points on the bench terrain, 56 algorithmic
+    bytes per lookup (16 B xy in, 32 B of z cells, 8 B height out), HIP events
+    on the launch stream."""
+    import ctypes
+    g = torch.Generator(device=dev).manual_seed(5)
+    x0, xN, y0, yN = data.bounds
+    xy = torch.empty((points, 2), dtype=torch.float64, device=dev)
+    xy[:, 0].uniform_(x0, xN, generator=g)
+    xy[:, 1].uniform_(y0, yN, generator=g)
+    h = torch.empty(points, dtype=torch.float64, device=dev)
+    st = torch.cuda.current_stream(dev)
+    VP = ctypes.c_void_p
+
+    def k1():
+        rc = T._lib.gbp_height_batch_dev(T._h, points, VP(xy.data_ptr()), VP(h.data_ptr()), None,
+                                         None, VP(st.cuda_stream))
+        if rc != 0:
+            raise gbp.GbpError(rc, "height_batch")
+
+    k1()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(launches)]
+    for e0, e1 in ev:
+        e0.record(st)
+        k1()
+        e1.record(st)
+    torch.cuda.synchronize()
+    ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
+    achieved = 56.0 * points / (ms * 1e-3) / 1e9
+    return {"kernel": "k_height", "points": points, "ms_per_launch": round(ms, 4),
+            "lookups_per_s": round(points / (ms * 1e-3), 1), "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "bytes_per_lookup": 56, "z_storage": ["auto", "f32", "f64"][T.info()["storage"]]}
 
 
 def time_to_first_solution(data, args, rank, world, dev):
@@ -189,18 +236,23 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for e0, e1 in ev:
-        e0.record(stream)
+    for _ in range(args.steps):  # the timed region: K launches back to back
         step()
-        e1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # the validate kernel's own duration for the roofline: HIP events around
+    # each launch on the launch stream, in a separate pass of K launches
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    for e0, e1 in ev:
+        e0.record(stream)
+        step()
+        e1.record(stream)
+    torch.cuda.synchronize()
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
 
     elapsed, sums = sharding.reduce_run(elapsed, [B, n_valid, n_ood, n_frag, gv], dev)
@@ -256,9 +308,16 @@ def main():
             },
             "time_to_first_solution": ttfs,
         }
+        if args.lookup_micro:
+            out["terrain_lookup"] = terrain_lookup_micro(T, data, dev)
         if world == 1 and args.cpu_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(data, s.cpu().numpy(), a.cpu().numpy(),
-                                               d.cpu().numpy(), args.cpu_seconds)
+            s_h, a_h, d_h = s.cpu().numpy(), a.cpu().numpy(), d.cpu().numpy()
+            out["cpu_baseline"] = cpu_baseline(data, s_h, a_h, d_h, args.cpu_seconds)
+            # all host cores the box gives this job (OMP_NUM_THREADS there), OpenMP
+            # over attempts (SURVEY §8(d) CPU baseline (ii))
+            nt = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+            out["cpu_baseline_all_cores"] = cpu_baseline(data, s_h, a_h, d_h,
+                                                         min(args.cpu_seconds, 5.0), nt)
         line = json.dumps(out)
         print(line, flush=True)
         if args.out:

@@ -44,13 +44,17 @@ __device__ __forceinline__ double std_max(double a, double b) { return (a < b) ?
 
 // ---- device terrain view ----------------------------------------------------
 // Heights FastTerrainMap::z_data_[ix][iy] in fp32 (lossless for grid_map maps,
-// whose layers are float) or fp64, stored as CELL QUADS: cell (ix, iy),
-// 0 <= ix < nx-1, 0 <= iy < ny-1, holds its four corners
-//   zq[4*(ix*(ny-1) + iy) + {0,1,2,3}] = z[ix][iy], z[ix][iy+1], z[ix+1][iy], z[ix+1][iy+1]
-// so one bilinear lookup is ONE aligned 16-B (fp32) / 2 x 16-B (fp64) load
-// from one cache line instead of four 4-B gathers from two rows.  Every
-// lookup's cell is clamped into that range, so no other z is ever read.
-// (-DGBP_ZROWS: the plain x-major z[ix*ny + iy] layout, diagnostic builds.)
+// whose layers are float) or fp64, stored as X-PAIRS: for 0 <= ix < nx-1,
+//   zp[2*(ix*ny + iy) + {0,1}] = z[ix][iy], z[ix+1][iy]
+// so the four corners of cell (ix, iy) are the two adjacent pairs at iy and
+// iy+1: one 16-B (fp32) load from one cache line (15 lines in 16) instead of
+// four 4-B gathers from two rows, at twice the rows' footprint (8 MB at
+// 1024^2, fp32).  Measured against the alternatives (tools/diag.py, synth-
+// rough-1024): x-major rows (4 MB, 4 loads) and cell quads (16 B per cell,
+// 16 MB, 1 aligned load) are 7-8 % slower on the validate kernel and 8-24 %
+// slower on lookups: the quads' footprint drops the L2 hit rate from 86 % to
+// 39 %.  Every lookup's cell is clamped into range, so no other z is read.
+// (-DGBP_ZROWS / -DGBP_ZQUADS: the other layouts, diagnostic builds.)
 template <class ZT>
 struct alignas(4 * sizeof(ZT)) ZQuad {
   ZT q[4];
@@ -59,7 +63,7 @@ struct alignas(4 * sizeof(ZT)) ZQuad {
 template <class ZT>
 struct TerrainView {
   const double *x, *y;           // coordinates (ascending)
-  const ZT *z;                   // heights: cell quads (or x-major rows with GBP_ZROWS)
+  const ZT *z;                   // heights: x-pairs (rows / quads in diagnostic builds)
   const double *dx, *dy, *dz;    // slope layers, x-major fp64, may be null
   int nx, ny;
   double x0, xN, y0, yN;         // x[0], x[nx-1], y[0], y[ny-1]
@@ -120,18 +124,25 @@ __device__ __forceinline__ int bracket(const double *__restrict__ d, int n, doub
 // the four corners of cell (ix, iy), ix <= nx-2, iy <= ny-2, in Probe::q order
 template <class ZT>
 __device__ __forceinline__ void fetch_cell(const TerrainView<ZT> &T, int ix, int iy, ZT q[4]) {
-#ifdef GBP_ZROWS
+#if defined(GBP_ZROWS)
   const ZT *p = T.z + (size_t)ix * T.ny + iy;
   q[0] = p[0];
   q[1] = p[1];
   q[2] = p[T.ny];
   q[3] = p[T.ny + 1];
-#else
+#elif defined(GBP_ZQUADS)  // cell quads: zq[ix*(ny-1) + iy] = the cell's four corners
   const ZQuad<ZT> c = ((const ZQuad<ZT> *)T.z)[(size_t)ix * (T.ny - 1) + iy];
   q[0] = c.q[0];
   q[1] = c.q[1];
   q[2] = c.q[2];
   q[3] = c.q[3];
+#else  // x-pairs: zp[ix*ny + iy] = {z[ix][iy], z[ix+1][iy]}; the cell is 2 adjacent pairs
+  typedef ZT pair4 __attribute__((ext_vector_type(4), aligned(2 * sizeof(ZT))));
+  const pair4 c = *(const pair4 *)(T.z + 2 * ((size_t)ix * T.ny + iy));
+  q[0] = c[0];
+  q[2] = c[1];
+  q[1] = c[2];
+  q[3] = c[3];
 #endif
 }
 

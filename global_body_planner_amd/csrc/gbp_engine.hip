@@ -1371,15 +1371,21 @@ int gbp_terrain_create(int device, int nx, int ny, const double *x, const double
     return fail(GBP_E_HIP);
   if (hipMemcpy(t->d_y, y, sizeof(double) * ny, hipMemcpyHostToDevice) != hipSuccess)
     return fail(GBP_E_HIP);
-  // heights as cell quads (gbp_device.h TerrainView), or rows with GBP_ZROWS
-#ifdef GBP_ZROWS
+  // heights as x-pairs (gbp_device.h TerrainView); rows / quads: diagnostic builds
+#if defined(GBP_ZROWS)
   const size_t zcount = cells;
   auto zsrc = [&](size_t k) { return z[k]; };
-#else
+#elif defined(GBP_ZQUADS)
   const size_t qx = (size_t)nx - 1, qy = (size_t)ny - 1, zcount = 4 * qx * qy;
   auto zsrc = [&](size_t k) {
     const size_t c = k >> 2, ix = c / qy, iy = c % qy, corner = k & 3;
     return z[(ix + (corner >> 1)) * (size_t)ny + iy + (corner & 1)];
+  };
+#else
+  const size_t zcount = 2 * ((size_t)nx - 1) * (size_t)ny;
+  auto zsrc = [&](size_t k) {
+    const size_t c = k >> 1, ix = c / (size_t)ny, iy = c % (size_t)ny;
+    return z[(ix + (k & 1)) * (size_t)ny + iy];
   };
 #endif
   if (storage == GBP_STORAGE_F32) {

@@ -32,6 +32,12 @@ s, act, d, _, _ = W.make_attempts(Ts["real"], 262144, W.CONFIG_SEEDS[3])
 st_states, _ = Ts["real"].sample_states(1 << 20, 3, 11, 0)
 times = {k: [] for k in Ts}
 vtimes = {k: [] for k in Ts}
+htimes = {k: [] for k in Ts}
+g = torch.Generator(device="cuda").manual_seed(5)
+npts = 1 << 24
+xy = torch.empty((npts, 2), dtype=torch.float64, device="cuda")
+xy[:, 0].uniform_(data.bounds[0], data.bounds[1], generator=g)
+xy[:, 1].uniform_(data.bounds[2], data.bounds[3], generator=g)
 st = torch.cuda.current_stream()
 for r in range(a.rounds):
     for k, T in Ts.items():
@@ -52,9 +58,18 @@ for r in range(a.rounds):
             e1.record(st)
         torch.cuda.synchronize()
         vtimes[k] += [e0.elapsed_time(e1) for e0, e1 in ev]
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(a.launches)]
+        for e0, e1 in ev:
+            e0.record(st)
+            T.height(xy)
+            e1.record(st)
+        torch.cuda.synchronize()
+        htimes[k] += [e0.elapsed_time(e1) for e0, e1 in ev]
         if r == 0:
             c = out.counts.to(torch.int64) & 0xFFFFFFFF
             print(f"{k:16s} valid={int(out.valid.sum())} V={int((c >> 16).sum())}", flush=True)
 for k, t in times.items():
     print(f"{k:16s} pairs median {np.median(t):.4f} ms  min {np.min(t):.4f} ms   "
-          f"valid_states(1M) median {np.median(vtimes[k]):.4f} ms")
+          f"valid_states(1M) median {np.median(vtimes[k]):.4f} ms   "
+          f"height(16M) median {np.median(htimes[k]):.4f} ms")

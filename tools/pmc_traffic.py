@@ -53,6 +53,20 @@ def main(d):
             summary["validate_l2_hit_rate"] = hit / (hit + miss)
     with open(os.path.join(d, "summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
+    if "validate_hbm_bytes_per_launch" in summary:  # what bench.py reads (profiles/pmc_traffic.json)
+        k = [n for n in summary["kernels"] if "k_validate" in n]
+        with open(os.path.join(d, "pmc_traffic.json"), "w") as f:
+            json.dump({"terrain": os.environ.get("PMC_TERRAIN", "synth-rough-1024"),
+                       "batch": int(os.environ.get("PMC_BATCH", "262144")),
+                       "kernel": k[0].split("(")[0] if k else None,
+                       "avg_ns_trace": summary["kernels"][k[0]]["avg_ns"] if k else None,
+                       "hbm_bytes_per_launch": summary["validate_hbm_bytes_per_launch"],
+                       "fetch_kib_raw": summary.get("validate_fetch_kib_raw"),
+                       "write_kib_raw": summary.get("validate_write_kib_raw"),
+                       "l2_hit_rate": summary.get("validate_l2_hit_rate"),
+                       "correction": "(2*FETCH_SIZE + WRITE_SIZE)*1024, MI355X_MICROARCH.md §HBM",
+                       "source": "tools/profile.sh: rocprofv3 --kernel-trace --stats, then separate "
+                                 "--pmc FETCH_SIZE / WRITE_SIZE / TCC_HIT,TCC_MISS runs"}, f, indent=1)
     for k, v in sorted(summary["kernels"].items(), key=lambda kv: -kv[1]["total_ns"]):
         print(f"{v['calls']:6d} calls  avg {v['avg_ns'] / 1e3:10.2f} us  {v['pct']:6.2f}%  {k[:90]}")
     for k in ("validate_hbm_bytes_per_launch", "validate_fetch_kib_raw", "validate_write_kib_raw",
