@@ -490,7 +490,9 @@ extern "C" int gbp_diag_read(unsigned long long *out, int reset) {
 #endif
 
 template <class ZT, bool ADAPTIVE, int W, int CM>
-__global__ __launch_bounds__(256, W) void k_validate_persistent(
+// up to 512 threads: one 8-wave workgroup per CU at W = 2 lets sched 3's LDS
+// queue balance all the CU's waves, including the two that share a SIMD
+__global__ __launch_bounds__(512, W) void k_validate_persistent(
     TerrainView<ZT> T0, int n, const double *__restrict__ S, const double *__restrict__ A,
     const uint8_t *__restrict__ dir, int dir_all, uint8_t *__restrict__ valid,
     double *__restrict__ s_new, double *__restrict__ t_new, uint32_t *__restrict__ flags,
@@ -1134,8 +1136,9 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
     if (t->opt_kernel == GBP_KERNEL_DIRECT) {
       // the direct form inlines the state check at five call sites: it gets the
       // whole register file (W = 1) whatever the persistent kernel's budget is
-      const unsigned g = (unsigned)((m + block - 1) / block);
-      hipLaunchKernelGGL((k_validate_direct<ZT, AD, 1, CM == 2 ? 0 : CM>), dim3(g), dim3(block), coords, st, T, m,
+      const int db = std::min(block, 256);  // k_validate_direct: __launch_bounds__(256)
+      const unsigned g = (unsigned)((m + db - 1) / db);
+      hipLaunchKernelGGL((k_validate_direct<ZT, AD, 1, CM == 2 ? 0 : CM>), dim3(g), dim3(db), coords, st, T, m,
                          s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn, flags + off, c);
     } else {
       // persistent: grid sized to residency; the work counter is zeroed per launch
@@ -1456,7 +1459,7 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
       t->opt_kernel = value;
       return GBP_OK;
     case GBP_OPT_BLOCK:
-      if (value < 64 || value > 256 || value % 64) return GBP_E_INVALID_ARG;
+      if (value < 64 || value > 512 || value % 64) return GBP_E_INVALID_ARG;
       t->opt_block = value;
       return GBP_OK;
     case GBP_OPT_GRID_PER_CU:

@@ -117,7 +117,8 @@ int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage,
 
 /* engine options (per handle) */
 #define GBP_OPT_KERNEL        1  /* GBP_KERNEL_* for the validate/extend entry points */
-#define GBP_OPT_BLOCK         2  /* threads per workgroup (multiple of 64)            */
+#define GBP_OPT_BLOCK         2  /* threads per workgroup (multiple of 64, <= 512; the
+                                    direct kernel uses min(block, 256))               */
 #define GBP_OPT_GRID_PER_CU   3  /* persistent kernel: workgroups per CU              */
 #define GBP_OPT_WAVES         4  /* register budget: min waves per SIMD (1..4)        */
 #define GBP_OPT_LDS_COORDS    5  /* 1: stage coordinate vectors in LDS when they fit  */
