@@ -58,7 +58,7 @@ def main(d):
         with open(os.path.join(d, "pmc_traffic.json"), "w") as f:
             json.dump({"terrain": os.environ.get("PMC_TERRAIN", "synth-rough-1024"),
                        "batch": int(os.environ.get("PMC_BATCH", "262144")),
-                       "kernel": k[0].split("::")[-1].split("(")[0] if k else None,
+                       "kernel": k[0][k[0].index("k_validate"):k[0].index("(gbp::")] if k else None,
                        "avg_ns_trace": summary["kernels"][k[0]]["avg_ns"] if k else None,
                        "hbm_bytes_per_launch": summary["validate_hbm_bytes_per_launch"],
                        "fetch_kib_raw": summary.get("validate_fetch_kib_raw"),
