@@ -133,49 +133,66 @@ def terrain_lookup_micro(T, data, dev, points=1 << 24, launches=10):
             "bytes_per_lookup": 56, "z_storage": ["auto", "f32", "f64"][T.info()["storage"]]}
 
 
-def time_to_first_solution(data, args, rank, world, dev):
-    """Config 3: synth-rough-1024, start (1.0, 10.23) -> goal
-    (19.42, 10.23), z = 0.375 + ground, v = (1, 0, 0), batch-synchronous
-    RRT-Connect (include/gbp_planner.h).  With N ranks each run is config 4:
-    one independent tree pair per GPU (seed + rank), first solution = min over
-    ranks, best path shared by one all_gather of the fixed-size record."""
+# start (1.0, L/2), goal = the first STANCE-valid point scanning
+# down from L - 1 along y = L/2; reference wall times (its own
+# CPU build, 3 seeds) where it solved
+TTFS_PAIRS = {
+    "synth-rough-1024": {"start": (1.0, 10.23), "goal": (19.42, 10.23), "reference_s": None,
+                         "reference_note": "no solution within 1700 s (BASELINE §2.1)"},
+    "synth-rough-256": {"start": (1.0, 2.55), "goal": (4.02, 2.55),
+                        "reference_s": [0.05, 1.19, 2.64]},
+}
+
+
+def time_to_first_solution(data, name, runs, max_time, args, rank, world, dev):
+    """Batch-synchronous RRT-Connect (include/gbp_planner.h) from the pair's
+    start to its goal, z = 0.375 + ground, v = (1, 0, 0).  With N ranks each run
+    is config 4: one independent tree pair per GPU (seed + rank), first solution
+    = min over ranks, best path shared by one all_gather of the fixed-size record."""
     from global_body_planner_amd import planner
     T = gbp.Terrain.from_data(data, device=dev.index)
-    L = data.x[-1]
-    xy = torch.tensor([[1.0, L / 2], [19.42 if L > 20 else L - 1.0, L / 2]], dtype=torch.float64,
-                      device=dev)
-    h = T.height(xy)[0]
-    h = h.cpu().numpy()
+    pair = TTFS_PAIRS[name]
+    xy = torch.tensor([pair["start"], pair["goal"]], dtype=torch.float64, device=dev)
+    h = T.height(xy)[0].cpu().numpy()
     xy = xy.cpu().numpy()
     start = planner.start_goal_state(h[0], xy[0, 0], xy[0, 1])
     goal = planner.start_goal_state(h[1], xy[1, 0], xy[1, 1])
-    runs = []
+    out_runs = []
     best = None
-    for k in range(args.ttfs_runs):
+    for k in range(runs):
         out = planner.plan_rrt_connect(data, start, goal, batch=args.plan_batch,
-                                       max_time=args.plan_max_time,
+                                       max_time=max_time,
                                        seed=args.seed + 7919 * k + rank, device=dev.index)
         ttf = out["time_to_first"] if out["found"] else float("inf")
         t = torch.tensor([ttf], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        runs.append({"ttfs_s": float(t.item()), "rank0_iterations": out["iterations"],
-                     "rank0_extends": out["extends"], "rank0_attempts": out["attempts_checked"],
-                     "rank0_vertices": out["vertices_a"] + out["vertices_b"]})
-        if k == args.ttfs_runs - 1:
+        out_runs.append({"ttfs_s": float(t.item()), "rank0_iterations": out["iterations"],
+                         "rank0_extends": out["extends"],
+                         "rank0_attempts": out["attempts_checked"],
+                         "rank0_vertices": out["vertices_a"] + out["vertices_b"],
+                         "rank0_tree_x_extent": [round(out["extent_a"][0], 2),
+                                                 round(out["extent_a"][1], 2),
+                                                 round(out["extent_b"][0], 2),
+                                                 round(out["extent_b"][1], 2)]})
+        if k == runs - 1:
             cost = out["path_length"] if out["found"] else float("nan")
             rec = sharding.pack_path(cost, out["path_length"], 0.0,
                                      out["states"] if out["found"] else None,
                                      out["actions"] if out["found"] else None, device=dev)
             who, rec = sharding.allgather_best_path(rec)
             best = {"rank": who, "cost": sharding.unpack_path(rec)["cost"]}
-    solved = [r["ttfs_s"] for r in runs if np.isfinite(r["ttfs_s"])]
-    return {"value": float(np.median(solved)) if solved else None, "unit": "s",
-            "solved": f"{len(solved)}/{len(runs)}", "runs": runs, "best_path": best,
-            "batch": args.plan_batch, "max_time_s": args.plan_max_time,
-            "start": [float(v) for v in start[:3]], "goal": [float(v) for v in goal[:3]],
-            "definition": "wall seconds from buildRRTConnectBatched start to the first REACHED "
-                          "connect (min over ranks), median over runs"}
+    solved = [r["ttfs_s"] for r in out_runs if np.isfinite(r["ttfs_s"])]
+    res = {"terrain": name, "value": float(np.median(solved)) if solved else None, "unit": "s",
+           "solved": f"{len(solved)}/{len(out_runs)}", "runs": out_runs, "best_path": best,
+           "batch": args.plan_batch, "max_time_s": max_time,
+           "start": [float(v) for v in start[:3]], "goal": [float(v) for v in goal[:3]],
+           "reference_s": pair["reference_s"],
+           "definition": "wall seconds from buildRRTConnectBatched start to the first REACHED "
+                         "connect (min over ranks), median over solved runs"}
+    if pair.get("reference_note"):
+        res["reference_note"] = pair["reference_note"]
+    return res
 
 
 def _cpu_model():
@@ -260,7 +277,13 @@ def main():
     tot_attempts = float(sums[0].item()) * args.steps
     value = tot_attempts / elapsed
 
-    ttfs = time_to_first_solution(data, args, rank, world, dev) if args.ttfs_runs > 0 else None
+    ttfs = ttfs2 = None
+    if args.ttfs_runs > 0:
+        ttfs = time_to_first_solution(data, args.terrain, args.ttfs_runs, args.plan_max_time, args,
+                                      rank, world, dev) if args.terrain in TTFS_PAIRS else None
+        # config 2 (synth-rough-256), where the reference has wall times to compare with
+        ttfs2 = time_to_first_solution(td.by_name("synth-rough-256"), "synth-rough-256", 3, 20.0,
+                                       args, rank, world, dev)
 
     if rank == 0:
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
@@ -307,6 +330,7 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },
             "time_to_first_solution": ttfs,
+            "time_to_first_solution_config2": ttfs2,
         }
         if args.lookup_micro:
             out["terrain_lookup"] = terrain_lookup_micro(T, data, dev)
