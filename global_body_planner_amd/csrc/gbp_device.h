@@ -428,16 +428,20 @@ __device__ __forceinline__ void rotation_trig(double dx, double dy, double speed
   }
 }
 
-// A 64-bit constant materialised at its use, in an SGPR pair: left to itself
-// the compiler hoists every polynomial coefficient of the state check out of
-// the persistent loop into VGPRs that stay live for the whole kernel (with
-// libm's atan2/sin/cos tables, ~80 VGPRs: what held the validate kernel at
-// 2 waves per SIMD).
-__device__ __forceinline__ double kc(double v) {
-  uint64_t u = __builtin_bit_cast(uint64_t, v);
-  asm volatile("" : "+s"(u));
-  return __builtin_bit_cast(double, u);
+// A 64-bit constant materialised AT ITS USE (two s_mov_b32 inside the loop
+// body, an SGPR pair that lives for one instruction): left to itself the
+// compiler hoists every polynomial coefficient out of the persistent loop and
+// keeps it for the whole kernel, in VGPRs (with libm's atan2/sin/cos tables,
+// ~80 of them: what held the validate kernel at 2 waves per SIMD) or, short
+// of SGPRs, in VGPR spill lanes read back with v_readlane at every use.
+template <uint64_t BITS>
+__device__ __forceinline__ double kc() {
+  uint32_t lo, hi;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "i"((uint32_t)(BITS & 0xFFFFFFFFu)));
+  asm volatile("s_mov_b32 %0, %1" : "=s"(hi) : "i"((uint32_t)(BITS >> 32)));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
+#define KC(v) kc<__builtin_bit_cast(uint64_t, (double)(v))>()
 
 // isValidState's rotation (planning_utils.cpp:578-594) for a state that passed
 // checks (2)-(3), i.e. |p| < P_MAX = 1 and speed = |(dx, dy)| <= V_MAX (or
@@ -469,25 +473,25 @@ __device__ __forceinline__ void rotation_trig_nolibm(double dx, double dy, doubl
     }
   }
   const double z = p * p;
-  double ps = kc(-1.0 / 121645100408832000.0);              // -1/19!
-  ps = __builtin_fma(ps, z, kc(1.0 / 355687428096000.0));   //  1/17!
-  ps = __builtin_fma(ps, z, kc(-1.0 / 1307674368000.0));    // -1/15!
-  ps = __builtin_fma(ps, z, kc(1.0 / 6227020800.0));        //  1/13!
-  ps = __builtin_fma(ps, z, kc(-1.0 / 39916800.0));         // -1/11!
-  ps = __builtin_fma(ps, z, kc(1.0 / 362880.0));            //  1/9!
-  ps = __builtin_fma(ps, z, kc(-1.0 / 5040.0));             // -1/7!
-  ps = __builtin_fma(ps, z, kc(1.0 / 120.0));               //  1/5!
-  ps = __builtin_fma(ps, z, kc(-1.0 / 6.0));                // -1/3!
+  double ps = KC(-1.0 / 121645100408832000.0);              // -1/19!
+  ps = __builtin_fma(ps, z, KC(1.0 / 355687428096000.0));   //  1/17!
+  ps = __builtin_fma(ps, z, KC(-1.0 / 1307674368000.0));    // -1/15!
+  ps = __builtin_fma(ps, z, KC(1.0 / 6227020800.0));        //  1/13!
+  ps = __builtin_fma(ps, z, KC(-1.0 / 39916800.0));         // -1/11!
+  ps = __builtin_fma(ps, z, KC(1.0 / 362880.0));            //  1/9!
+  ps = __builtin_fma(ps, z, KC(-1.0 / 5040.0));             // -1/7!
+  ps = __builtin_fma(ps, z, KC(1.0 / 120.0));               //  1/5!
+  ps = __builtin_fma(ps, z, KC(-1.0 / 6.0));                // -1/3!
   sp = __builtin_fma(p * z, ps, p);
-  double pc = kc(1.0 / 2432902008176640000.0);              //  1/20!
-  pc = __builtin_fma(pc, z, kc(-1.0 / 6402373705728000.0)); // -1/18!
-  pc = __builtin_fma(pc, z, kc(1.0 / 20922789888000.0));    //  1/16!
-  pc = __builtin_fma(pc, z, kc(-1.0 / 87178291200.0));      // -1/14!
-  pc = __builtin_fma(pc, z, kc(1.0 / 479001600.0));         //  1/12!
-  pc = __builtin_fma(pc, z, kc(-1.0 / 3628800.0));          // -1/10!
-  pc = __builtin_fma(pc, z, kc(1.0 / 40320.0));             //  1/8!
-  pc = __builtin_fma(pc, z, kc(-1.0 / 720.0));              // -1/6!
-  pc = __builtin_fma(pc, z, kc(1.0 / 24.0));                //  1/4!
+  double pc = KC(1.0 / 2432902008176640000.0);              //  1/20!
+  pc = __builtin_fma(pc, z, KC(-1.0 / 6402373705728000.0)); // -1/18!
+  pc = __builtin_fma(pc, z, KC(1.0 / 20922789888000.0));    //  1/16!
+  pc = __builtin_fma(pc, z, KC(-1.0 / 87178291200.0));      // -1/14!
+  pc = __builtin_fma(pc, z, KC(1.0 / 479001600.0));         //  1/12!
+  pc = __builtin_fma(pc, z, KC(-1.0 / 3628800.0));          // -1/10!
+  pc = __builtin_fma(pc, z, KC(1.0 / 40320.0));             //  1/8!
+  pc = __builtin_fma(pc, z, KC(-1.0 / 720.0));              // -1/6!
+  pc = __builtin_fma(pc, z, KC(1.0 / 24.0));                //  1/4!
   pc = __builtin_fma(pc, z, -0.5);                          // -1/2!
   cp = __builtin_fma(z, pc, 1.0);
 }
@@ -505,7 +509,8 @@ struct Acc {
 // be UB, `near` = in-domain point within FRAGILE_EPS of a grid line
 template <class ZT, int CM>
 __device__ __forceinline__ double probe_height_bf(const TerrainView<ZT> &T, const Probe<ZT> &p,
-                                                  double x, double y, bool &ok, bool &near) {
+                                                  double x, double y, double eps, bool &ok,
+                                                  bool &near) {
   const bool nanxy = isnan(x) || isnan(y);
   const bool br = p.ix >= 0 && p.iy >= 0;
   const int cx = br ? p.ix : 0, cy = br ? p.iy : 0;
@@ -514,8 +519,7 @@ __device__ __forceinline__ double probe_height_bf(const TerrainView<ZT> &T, cons
   ok = br || nanxy;
 #ifndef GBP_EXPERIMENT_NO_FRAGILE
   near = br && !nanxy &&
-         (fabs(x - x1) < FRAGILE_EPS || fabs(x2 - x) < FRAGILE_EPS || fabs(y - y1) < FRAGILE_EPS ||
-          fabs(y2 - y) < FRAGILE_EPS);
+         (fabs(x - x1) < eps || fabs(x2 - x) < eps || fabs(y - y1) < eps || fabs(y2 - y) < eps);
 #else
   near = false;
 #endif
@@ -540,6 +544,7 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
     return false;
   }
   acc.V++;
+  const double eps = FRAGILE_EPS, hmin = H_MIN, hmax = H_MAX, hl = 0.5 * ROBOT_L, hw = 0.5 * ROBOT_W;
   Probe<ZT> pc;
   probe<ZT, CM>(T, s[0], s[1], pc);
   const bool outside = (s[0] < T.x0) || (s[0] > T.xN) || (s[1] < T.y0) || (s[1] > T.yN);
@@ -569,8 +574,8 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
   Probe<ZT> pl[4], pk[4], pu;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const double x_body = (k < 2) ? -0.5 * ROBOT_L : 0.5 * ROBOT_L;
-    const double y_body = (k & 1) ? 0.5 * ROBOT_W : -0.5 * ROBOT_W;
+    const double x_body = (k < 2) ? -hl : hl;
+    const double y_body = (k & 1) ? hw : -hw;
     const double x_leg = s[0] + R_11 * x_body + R_12 * y_body;
     const double y_leg = s[1] + R_21 * x_body + R_22 * y_body;
     probe<ZT, CM>(T, x_leg, y_leg, pl[k]);
@@ -582,8 +587,8 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
   // (5) four corners :601-627, x_body outer, y_body inner, in reference order
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const double x_body = (k < 2) ? -0.5 * ROBOT_L : 0.5 * ROBOT_L;
-    const double y_body = (k & 1) ? 0.5 * ROBOT_W : -0.5 * ROBOT_W;
+    const double x_body = (k < 2) ? -hl : hl;
+    const double y_body = (k & 1) ? hw : -hw;
     const double x_leg = s[0] + R_11 * x_body + R_12 * y_body;
     const double y_leg = s[1] + R_21 * x_body + R_22 * y_body;
     const double z_leg = s[2] + R_31 * x_body + R_32 * y_body;
@@ -596,8 +601,8 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
     alive = alive && rl == 0;
     G += alive ? 2u : 0u;  // both heights computed before the test :618-619
     bool okl, okc, nl, nc;
-    const double gl = probe_height_bf<ZT, CM>(T, pl[k], x_leg, y_leg, okl, nl);
-    const double gc = probe_height_bf<ZT, CM>(T, pk[k], x_corner, y_corner, okc, nc);
+    const double gl = probe_height_bf<ZT, CM>(T, pl[k], x_leg, y_leg, eps, okl, nl);
+    const double gc = probe_height_bf<ZT, CM>(T, pk[k], x_corner, y_corner, eps, okc, nc);
     if (alive && nl) fl |= GBP_F_FRAGILE;
     if (alive && !okl) fl |= GBP_F_OOD;
     alive = alive && okl;
@@ -606,21 +611,21 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
     alive = alive && okc;
     const double leg_height = z_leg - gl;
     const double corner_height = z_corner - gc;
-    if (alive && (fabs(corner_height - H_MIN) < FRAGILE_EPS ||
-                  (phase == GBP_STANCE && fabs(leg_height - H_MAX) < FRAGILE_EPS)))
+    if (alive && (fabs(corner_height - hmin) < eps ||
+                  (phase == GBP_STANCE && fabs(leg_height - hmax) < eps)))
       fl |= GBP_F_FRAGILE;
-    alive = alive && !((corner_height < H_MIN) || ((phase == GBP_STANCE) && (leg_height > H_MAX)));
+    alive = alive && !((corner_height < hmin) || ((phase == GBP_STANCE) && (leg_height > hmax)));
   }
   // (6) underside centre :630-632
   G += alive ? 1u : 0u;
   bool oku, nu;
-  const double gu = probe_height_bf<ZT, CM>(T, pu, ux, uy, oku, nu);
+  const double gu = probe_height_bf<ZT, CM>(T, pu, ux, uy, eps, oku, nu);
   if (alive && nu) fl |= GBP_F_FRAGILE;
   if (alive && !oku) fl |= GBP_F_OOD;
   alive = alive && oku;
   const double height = (s[2] + R_33 * z_body) - gu;
-  if (alive && fabs(height - H_MIN) < FRAGILE_EPS) fl |= GBP_F_FRAGILE;
-  alive = alive && !(height < H_MIN);
+  if (alive && fabs(height - hmin) < eps) fl |= GBP_F_FRAGILE;
+  alive = alive && !(height < hmin);
   acc.G += G;
   acc.flags |= fl;
   return alive;
