@@ -529,6 +529,10 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
   unsigned int cur = 0, end = 0, wg_begin = 0, wg_end = 0;
   unsigned int dyn0 = 0;  // sched 4: first dynamically dealt attempt
   int shard = 0, shards_left = 8;
+  // sched 4 keeps one dequeue in flight: the next chunk is claimed when the
+  // current one starts, so a refill never waits on a device-scope atomic
+  unsigned int rsv_val = 0;
+  int rsv_leader = -1;
   if (sched == 4) {
     const unsigned int waves = gridDim.x * (blockDim.x / WAVE);
     const unsigned int wid = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
@@ -558,13 +562,18 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
         const int leader = __ffsll((long long)m) - 1;
         unsigned int lim = (unsigned int)n;
         if (sched == 4) {
+          const unsigned long long rest = (unsigned long long)((unsigned int)n - dyn0);
           while (shards_left > 0) {  // wave-uniform
-            const unsigned long long rest = (unsigned long long)((unsigned int)n - dyn0);
             const unsigned int lo = dyn0 + (unsigned int)(rest * (unsigned)shard / 8u);
             const unsigned int hi = dyn0 + (unsigned int)(rest * (unsigned)(shard + 1) / 8u);
             unsigned int b = 0xFFFFFFFFu;
-            if (lane == leader) b = lo + atomicAdd(head + 32 * shard, grab);
-            b = __shfl(b, leader);
+            if (rsv_leader >= 0) {  // the chunk claimed one refill ago
+              b = lo + __shfl(rsv_val, rsv_leader);
+              rsv_leader = -1;
+            } else {
+              if (lane == leader) b = lo + atomicAdd(head + 32 * shard, grab);
+              b = __shfl(b, leader);
+            }
             if (b < hi) {
               base = b;
               lim = hi;
@@ -572,6 +581,10 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
             }
             shard = (shard + 1) & 7;
             shards_left--;
+          }
+          if (base != 0xFFFFFFFFu) {  // claim the next chunk of this shard now
+            if (lane == leader) rsv_val = atomicAdd(head + 32 * shard, grab);
+            rsv_leader = leader;
           }
         } else if (sched == 3) {
           if (lane == leader) base = wg_begin + atomicAdd(&wg_head, grab);
