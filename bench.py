@@ -67,7 +67,9 @@ def parse():
                    help="also run the K1 terrain-lookup microbenchmark (rank 0)")
     p.add_argument("--ttfs-runs", type=int, default=3,
                    help="batched RRT-Connect runs for time-to-first-solution (0 disables)")
-    p.add_argument("--plan-batch", type=int, default=256, help="targets per half-iteration")
+    p.add_argument("--plan-batch", type=int, default=0,
+                   help="targets per half-iteration (0: SURVEY §8(d), the config's attempt batch / 6 "
+                        "candidates: 43,690 at 1024^2 (256k), 10,923 at 256^2 (64k))")
     p.add_argument("--plan-max-time", type=float, default=30.0, help="seconds per planner run")
     return p.parse_args()
 
@@ -138,9 +140,10 @@ def terrain_lookup_micro(T, data, dev, points=1 << 24, launches=10):
 # CPU build, 3 seeds) where it solved
 TTFS_PAIRS = {
     "synth-rough-1024": {"start": (1.0, 10.23), "goal": (19.42, 10.23), "reference_s": None,
-                         "reference_note": "no solution within 1700 s (BASELINE §2.1)"},
+                         "reference_note": "no solution within 1700 s (BASELINE §2.1)",
+                         "batch": 262144 // 6},
     "synth-rough-256": {"start": (1.0, 2.55), "goal": (4.02, 2.55),
-                        "reference_s": [0.05, 1.19, 2.64]},
+                        "reference_s": [0.05, 1.19, 2.64], "batch": 65536 // 6},
 }
 
 
@@ -159,8 +162,9 @@ def time_to_first_solution(data, name, runs, max_time, args, rank, world, dev):
     goal = planner.start_goal_state(h[1], xy[1, 0], xy[1, 1])
     out_runs = []
     best = None
+    batch = args.plan_batch or pair["batch"]
     for k in range(runs):
-        out = planner.plan_rrt_connect(data, start, goal, batch=args.plan_batch,
+        out = planner.plan_rrt_connect(data, start, goal, batch=batch,
                                        max_time=max_time,
                                        seed=args.seed + 7919 * k + rank, device=dev.index)
         ttf = out["time_to_first"] if out["found"] else float("inf")
@@ -185,7 +189,7 @@ def time_to_first_solution(data, name, runs, max_time, args, rank, world, dev):
     solved = [r["ttfs_s"] for r in out_runs if np.isfinite(r["ttfs_s"])]
     res = {"terrain": name, "value": float(np.median(solved)) if solved else None, "unit": "s",
            "solved": f"{len(solved)}/{len(out_runs)}", "runs": out_runs, "best_path": best,
-           "batch": args.plan_batch, "max_time_s": max_time,
+           "batch": batch, "max_time_s": max_time,
            "start": [float(v) for v in start[:3]], "goal": [float(v) for v in goal[:3]],
            "reference_s": pair["reference_s"],
            "definition": "wall seconds from buildRRTConnectBatched start to the first REACHED "
