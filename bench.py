@@ -199,6 +199,49 @@ def time_to_first_solution(data, name, runs, max_time, args, rank, world, dev):
     return res
 
 
+def extend_micro(T, s, tgt, d, seed, launches=10):
+    """RRTClass::newConfig + extend acceptance (rrt.cpp:20-102) for B/6 extends
+    per launch (config 3: 256k attempts = 43,690 extends of up to 6 candidates):
+    candidate actions drawn at the target's surface normal, checked, the closest
+    valid one selected (gbp_extend_batch_dev, HIP events on the launch stream)."""
+    import ctypes
+    n = s.shape[0] // 6
+    dev = s.device
+    VP = ctypes.c_void_p
+    res = torch.empty(n, dtype=torch.int32, device=dev)
+    cho = torch.empty(n, dtype=torch.int32, device=dev)
+    sn = torch.empty((n, 8), dtype=torch.float64, device=dev)
+    an = torch.empty((n, 10), dtype=torch.float64, device=dev)
+    cnt = torch.empty(n, dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream(dev)
+    sv, tv, dv = s[:n].contiguous(), tgt[:n].contiguous(), d[:n].contiguous()
+
+    def ext():
+        rc = T._lib.gbp_extend_batch_dev(T._h, n, VP(sv.data_ptr()), VP(tv.data_ptr()),
+                                         VP(dv.data_ptr()), 0, 0, seed, 0, VP(res.data_ptr()),
+                                         VP(cho.data_ptr()), VP(sn.data_ptr()), VP(an.data_ptr()),
+                                         VP(cnt.data_ptr()), VP(st.cuda_stream))
+        if rc != 0:
+            raise gbp.GbpError(rc, "extend_batch")
+
+    ext()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(launches)]
+    for e0, e1 in ev:
+        e0.record(st)
+        ext()
+        e1.record(st)
+    torch.cuda.synchronize()
+    ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
+    adv = int((res != 0).sum().item())
+    return {"extends_per_launch": n, "ms_per_launch": round(ms, 4),
+            "extends_per_s": round(n / (ms * 1e-3), 1),
+            "non_trapped_fraction": round(adv / n, 5),
+            "definition": "newConfig (<= 6 candidates, first valid in index order) + the "
+                          "closer-than-s_near acceptance, per extend"}
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -227,7 +270,7 @@ def main():
     T.set_option(L.OPT_GRID_PER_CU, args.grid_per_cu)
     B = args.batch
     base, _ = sharding.weak_shard(rank, B)   # rank r: attempts [r*B, (r+1)*B) of one global stream
-    s, a, d, _, tries = W.make_attempts(T, B, args.seed, index_base=base)
+    s, a, d, tgt, tries = W.make_attempts(T, B, args.seed, index_base=base)
     res = T.validate_pairs(s, a, d, adaptive=args.adaptive)
     torch.cuda.synchronize()
     # per-launch algorithmic bytes from the kernel's own G/V counters
@@ -338,6 +381,7 @@ def main():
         }
         if args.lookup_micro:
             out["terrain_lookup"] = terrain_lookup_micro(T, data, dev)
+            out["extend_batch"] = extend_micro(T, s, tgt, d, args.seed)
         if world == 1 and args.cpu_seconds > 0:
             s_h, a_h, d_h = s.cpu().numpy(), a.cpu().numpy(), d.cpu().numpy()
             out["cpu_baseline"] = cpu_baseline(data, s_h, a_h, d_h, args.cpu_seconds)
