@@ -1037,6 +1037,7 @@ struct gbp_terrain {
   int64_t opt_sched = 1;            // persistent work source: 0 atomic, 1 static, 2 chunked
   int64_t opt_chunk = 0;            // dequeue granularity for sched 0/2 (0 = per need)
   int64_t opt_helpers = 1;          // idle lanes of a drained wave evaluate owners' next samples
+  int64_t opt_oversub = 1;          // fixed-grid schedules: workgroups = oversub x resident
   int64_t opt_prefix = 512;         // sched 4: statically dealt share of a batch (1/1024)
   int64_t opt_affine = 1;           // compute coordinates when the affine form is exact
   int affine = 0;                   // host-verified affine coordinates (both axes)
@@ -1156,9 +1157,13 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
     } else {
       // persistent: grid sized to residency; the work counter is zeroed per launch
       const int64_t resident = (int64_t)t->num_cus * std::max<int64_t>(1, W * 256 / block);
+      // fixed-grid schedules launch `oversub` x the resident workgroups: a
+      // workgroup that finishes its slice early frees its slot to one that has
+      // not started (the hardware dispatcher's work queue), so a wave's
+      // ragged end overlaps another's full start
       const bool fixed_grid = t->opt_sched == 1 || t->opt_sched >= 3;
-      const int64_t g =
-          std::max<int64_t>(1, std::min<int64_t>(fixed_grid ? resident : want, (m + block - 1) / block));
+      const int64_t g = std::max<int64_t>(
+          1, std::min<int64_t>(fixed_grid ? resident * t->opt_oversub : want, (m + block - 1) / block));
       if (t->opt_sched == 0 || t->opt_sched == 2)
         HIPCHK(hipMemsetAsync(t->d_head, 0, sizeof(unsigned int), st));
       if (t->opt_sched == 4) HIPCHK(hipMemsetAsync(t->d_head, 0, 8 * 128, st));
@@ -1504,6 +1509,10 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
       if (value < 0 || value > 1024) return GBP_E_INVALID_ARG;
       t->opt_prefix = value;
       return GBP_OK;
+    case GBP_OPT_OVERSUB:
+      if (value < 1 || value > 64) return GBP_E_INVALID_ARG;
+      t->opt_oversub = value;
+      return GBP_OK;
     default:
       return GBP_E_INVALID_ARG;
   }
@@ -1523,6 +1532,7 @@ int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value) {
     case GBP_OPT_HELPERS: *value = t->opt_helpers; return GBP_OK;
     case GBP_OPT_AFFINE_COORDS: *value = t->opt_affine; return GBP_OK;
     case GBP_OPT_PREFIX: *value = t->opt_prefix; return GBP_OK;
+    case GBP_OPT_OVERSUB: *value = t->opt_oversub; return GBP_OK;
     case GBP_OPT_COORD_MODE: *value = coord_mode(t, t->opt_lds_coords != 0); return GBP_OK;
     default: return GBP_E_INVALID_ARG;
   }

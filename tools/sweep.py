@@ -30,6 +30,7 @@ def main():
     p.add_argument("--block", default="256")
     p.add_argument("--lds", default="2", help="coordinates: 0 global, 1 LDS, 2 computed (affine)")
     p.add_argument("--sched", default="0", help="comma list of sched:chunk[:prefix], e.g. 0:0,1:0,2:64,4:32:512")
+    p.add_argument("--oversub", default="1", help="comma list of workgroup oversubscription factors")
     p.add_argument("--adaptive", action="store_true")
     p.add_argument("--out", default=None)
     a = p.parse_args()
@@ -44,13 +45,14 @@ def main():
                 for g in grids:
                     for lds in map(int, a.lds.split(",")):
                         for sc in (a.sched.split(",") if k == "persistent" else ["0:0"]):
-                            variants.append((k, w, b, g, lds, sc if ":" in sc else sc + ":0"))
+                            for ov in map(int, a.oversub.split(",")):
+                                variants.append((k, w, b, g, lds, sc if ":" in sc else sc + ":0", ov))
     times = {v: [] for v in variants}
     ref = None
     st = torch.cuda.current_stream()
     for r in range(a.rounds):
         for v in variants:
-            k, w, b, g, lds, sc = v
+            k, w, b, g, lds, sc, ov = v
             T.set_option(L.OPT_SCHED, int(sc.split(":")[0]))
             T.set_option(L.OPT_CHUNK, int(sc.split(":")[1]))
             T.set_option(L.OPT_PREFIX, int(sc.split(":")[2]) if sc.count(":") >= 2 else 512)
@@ -61,6 +63,7 @@ def main():
             T.set_option(L.OPT_BLOCK, b)
             if g:
                 T.set_option(L.OPT_GRID_PER_CU, g)
+            T.set_option(L.OPT_OVERSUB, ov)
             out = T.validate_pairs(s, act, d, adaptive=a.adaptive)
             if r == 0:
                 sig = (out.valid.cpu().numpy().tobytes(), out.flags.cpu().numpy().tobytes(),
@@ -80,12 +83,12 @@ def main():
     rows = []
     for v in variants:
         t = np.array(times[v])
-        rows.append({"kernel": v[0], "waves": v[1], "block": v[2], "grid_per_cu": v[3], "lds": v[4], "sched": v[5],
+        rows.append({"kernel": v[0], "waves": v[1], "block": v[2], "grid_per_cu": v[3], "lds": v[4], "sched": v[5], "oversub": v[6],
                      "median_ms": float(np.median(t)), "min_ms": float(t.min()),
                      "attempts_per_s": a.batch / (np.median(t) * 1e-3)})
     rows.sort(key=lambda r: r["median_ms"])
     for r in rows:
-        print(f"{r['kernel']:10s} w={r['waves']} b={r['block']} g={r['grid_per_cu']:2d} lds={r['lds']} sched={r['sched']:5s} "
+        print(f"{r['kernel']:10s} w={r['waves']} b={r['block']} g={r['grid_per_cu']:2d} lds={r['lds']} sched={r['sched']:5s} ov={r['oversub']} "
               f"median {r['median_ms']:.4f} ms  min {r['min_ms']:.4f} ms  "
               f"{r['attempts_per_s'] / 1e6:.1f} M attempts/s")
     if a.out:
