@@ -20,6 +20,7 @@ PAIRS = {  # first STANCE-valid goal scanning down from L-1 along
     "synth-rough-256": ((1.0, 2.55), (4.02, 2.55)),
     "synth-rough-1024": ((1.0, 10.23), (19.42, 10.23)),
     "slope-gridmap": ((1.0, 0.0), (8.0, 0.0)),
+    "rough_terrain-gridmap": ((0.0, 0.0), (10.0, 0.0)),  # the launch defaults (BASELINE §2)
 }
 
 
