@@ -497,7 +497,7 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
     const uint8_t *__restrict__ dir, int dir_all, uint8_t *__restrict__ valid,
     double *__restrict__ s_new, double *__restrict__ t_new, uint32_t *__restrict__ flags,
     uint32_t *__restrict__ counts, unsigned int *__restrict__ head, int sched, int chunk,
-    int helpers, int prefix) {
+    int helpers, int prefix, int xcd_map) {
   const TerrainView<ZT> T = CM == 1 ? stage_coords(T0, gbp_smem) : T0;
   const int lane = threadIdx.x & (WAVE - 1);
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
@@ -543,7 +543,13 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
     shard = blockIdx.x & 7;
   } else if (sched == 1) {
     const unsigned int waves = gridDim.x * (blockDim.x / WAVE);
-    const unsigned int wid = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+    // xcd_map: workgroup b runs on XCD b % 8 (round-robin dispatch); numbering
+    // the slices XCD-major gives each XCD one contiguous eighth of the batch,
+    // so a batch ordered by position keeps each XCD's L2 on its own stripe
+    const unsigned int wg = (xcd_map && (gridDim.x & 7u) == 0)
+                                ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)
+                                : blockIdx.x;
+    const unsigned int wid = wg * (blockDim.x / WAVE) + threadIdx.x / WAVE;
     cur = (unsigned int)(((unsigned long long)n * wid) / waves);
     end = (unsigned int)(((unsigned long long)n * (wid + 1)) / waves);
   } else if (sched == 3) {
@@ -1040,6 +1046,7 @@ struct gbp_terrain {
   int64_t opt_oversub = 1;          // fixed-grid schedules: workgroups = oversub x resident
   int64_t opt_prefix = 512;         // sched 4: statically dealt share of a batch (1/1024)
   int64_t opt_affine = 1;           // compute coordinates when the affine form is exact
+  int64_t opt_xcd_map = 0;          // sched 1: slices numbered XCD-major
   int affine = 0;                   // host-verified affine coordinates (both axes)
   int bx = 0, by = 0;
   double ax = 0, hx = 0, ay = 0, hy = 0;
@@ -1171,7 +1178,7 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
                          coords + rows, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
                          flags + off, c, t->d_head, (int)t->opt_sched,
                          (int)(t->opt_sched == 4 && t->opt_chunk == 0 ? 32 : t->opt_chunk),
-                         (int)t->opt_helpers, (int)t->opt_prefix);
+                         (int)t->opt_helpers, (int)t->opt_prefix, (int)t->opt_xcd_map);
     }
     HIPCHK(hipGetLastError());
   }
@@ -1513,6 +1520,9 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
       if (value < 1 || value > 64) return GBP_E_INVALID_ARG;
       t->opt_oversub = value;
       return GBP_OK;
+    case GBP_OPT_XCD_MAP:
+      t->opt_xcd_map = value ? 1 : 0;
+      return GBP_OK;
     default:
       return GBP_E_INVALID_ARG;
   }
@@ -1533,6 +1543,7 @@ int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value) {
     case GBP_OPT_AFFINE_COORDS: *value = t->opt_affine; return GBP_OK;
     case GBP_OPT_PREFIX: *value = t->opt_prefix; return GBP_OK;
     case GBP_OPT_OVERSUB: *value = t->opt_oversub; return GBP_OK;
+    case GBP_OPT_XCD_MAP: *value = t->opt_xcd_map; return GBP_OK;
     case GBP_OPT_COORD_MODE: *value = coord_mode(t, t->opt_lds_coords != 0); return GBP_OK;
     default: return GBP_E_INVALID_ARG;
   }

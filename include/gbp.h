@@ -134,6 +134,8 @@ int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage,
 #define GBP_OPT_COORD_MODE   10  /* read-only: 2 computed, 1 LDS-staged, 0 global      */
 #define GBP_OPT_PREFIX       11  /* sched 4: statically dealt share, 1/1024 (def. 512) */
 #define GBP_OPT_OVERSUB      12  /* sched 1/3/4: launch oversub x the resident workgroups */
+#define GBP_OPT_XCD_MAP      13  /* sched 1: 1 = each XCD takes one contiguous eighth of
+                                    the batch (workgroup b runs on XCD b % 8)           */
 #define GBP_KERNEL_DIRECT     0  /* one lane per attempt                              */
 #define GBP_KERNEL_PERSISTENT 1  /* persistent waves, lanes re-packed per sample      */
 int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value);

@@ -344,6 +344,33 @@ def test_validate_pairs_schedulers(gpu, sched, chunk, coords, helpers):
         T.set_option(L.OPT_HELPERS, 1)
 
 
+@pytest.mark.parametrize("name", ["synth-rough-256", "rough_terrain-gridmap"])
+def test_validate_pairs_xcd_map(gpu, name):
+    """XCD-major slice numbering (GBP_OPT_XCD_MAP) only changes which wave
+    evaluates an attempt: outputs are bit-identical to the default numbering and
+    to the oracle, on a batch ordered by position (the case it is for) and on
+    grids that are not a multiple of 8 workgroups (identity numbering)."""
+    data, T, O = terrain_pair(name)
+    T.set_option(L.OPT_KERNEL, L.KERNEL_PERSISTENT)
+    try:
+        for n in (9000, 20011, 700):
+            s, a, d, _, _ = attempts_oracle(O, n, seed=4242 + n)
+            order = np.argsort(s[:, 0], kind="stable")
+            s, a, d = s[order].copy(), a[order].copy(), d[order].copy()
+            outs = []
+            for xm in (0, 1):
+                T.set_option(L.OPT_XCD_MAP, xm)
+                assert T.get_option(L.OPT_XCD_MAP) == xm
+                res = T.validate_pairs(torch.from_numpy(s), torch.from_numpy(a), torch.from_numpy(d))
+                outs.append((np_(res.valid), np_(res.s_new), np_(res.t_new), u32(res.flags),
+                             u32(res.counts)))
+            for x, y in zip(outs[0], outs[1]):
+                assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+            assert_pairs_equal(outs[1], O.validate_pairs(s, a, d, nthreads=16), f"xcd n{n}")
+    finally:
+        T.set_option(L.OPT_XCD_MAP, 0)
+
+
 def test_engine_matches_golden_vectors(gpu):
     """The engine against the committed oracle vectors (tests/golden)."""
     import os

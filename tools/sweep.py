@@ -31,12 +31,34 @@ def main():
     p.add_argument("--lds", default="2", help="coordinates: 0 global, 1 LDS, 2 computed (affine)")
     p.add_argument("--sched", default="0", help="comma list of sched:chunk[:prefix], e.g. 0:0,1:0,2:64,4:32:512")
     p.add_argument("--oversub", default="1", help="comma list of workgroup oversubscription factors")
+    p.add_argument("--set", action="append", default=[],
+                   help="extra option axis KEY=v1,v2 (KEY: an OPT_* name such as PREFETCH, or its id)")
+    p.add_argument("--order", default="batch",
+                   help="attempt order: batch (as generated), x (sorted by s_near x), xy "
+                        "(x-stripes, then y), binsXxY (X x-stripes x Y y-bands, random within)")
     p.add_argument("--adaptive", action="store_true")
     p.add_argument("--out", default=None)
     a = p.parse_args()
     data = td.by_name(a.terrain)
     T = gbp.Terrain.from_data(data, device=0)
     s, act, d, _, _ = W.make_attempts(T, a.batch, W.CONFIG_SEEDS[3])
+    if a.order != "batch":  # diagnostic: a position-ordered batch (L2 locality per XCD)
+        ext = [float(data.x[0]), float(data.x[-1]), float(data.y[0]), float(data.y[-1])]
+        if a.order == "rand":  # a random permutation (scattered rows and outputs)
+            g = torch.Generator(device="cpu").manual_seed(7)
+            key = torch.randperm(s.shape[0], generator=g).to(s.device).double()
+        elif a.order == "x":
+            key = s[:, 0]
+        elif a.order == "xy":
+            key = torch.floor(s[:, 0] / 2.56) * 64 + s[:, 1]
+        else:
+            bx, by = map(int, a.order[4:].split("x"))
+            ix = ((s[:, 0] - ext[0]) / (ext[1] - ext[0]) * bx).floor().clamp(0, bx - 1)
+            iy = ((s[:, 1] - ext[2]) / (ext[3] - ext[2]) * by).floor().clamp(0, by - 1)
+            key = ix * by + iy
+        perm = torch.argsort(key, stable=True)
+        s, act = s[perm].contiguous(), act[perm].contiguous()
+        d = d[perm].contiguous() if d is not None else d
     variants = []
     for k in a.kernels.split(","):
         for w in (map(int, a.waves.split(",")) if k == "persistent" else [1]):
@@ -47,12 +69,20 @@ def main():
                         for sc in (a.sched.split(",") if k == "persistent" else ["0:0"]):
                             for ov in map(int, a.oversub.split(",")):
                                 variants.append((k, w, b, g, lds, sc if ":" in sc else sc + ":0", ov))
+    extra_keys, extra_vals = [], []
+    for spec in a.set:
+        k, vals = spec.split("=")
+        extra_keys.append((k, int(k) if k.isdigit() else getattr(L, "OPT_" + k.upper())))
+        extra_vals.append([int(x) for x in vals.split(",")])
+    variants = [v + (ex,) for v in variants for ex in itertools.product(*extra_vals)]
     times = {v: [] for v in variants}
     ref = None
     st = torch.cuda.current_stream()
     for r in range(a.rounds):
         for v in variants:
-            k, w, b, g, lds, sc, ov = v
+            k, w, b, g, lds, sc, ov, ex = v
+            for (_, key), val in zip(extra_keys, ex):
+                T.set_option(key, val)
             T.set_option(L.OPT_SCHED, int(sc.split(":")[0]))
             T.set_option(L.OPT_CHUNK, int(sc.split(":")[1]))
             T.set_option(L.OPT_PREFIX, int(sc.split(":")[2]) if sc.count(":") >= 2 else 512)
@@ -84,11 +114,12 @@ def main():
     for v in variants:
         t = np.array(times[v])
         rows.append({"kernel": v[0], "waves": v[1], "block": v[2], "grid_per_cu": v[3], "lds": v[4], "sched": v[5], "oversub": v[6],
+                     "set": {name: val for (name, _), val in zip(extra_keys, v[7])},
                      "median_ms": float(np.median(t)), "min_ms": float(t.min()),
                      "attempts_per_s": a.batch / (np.median(t) * 1e-3)})
     rows.sort(key=lambda r: r["median_ms"])
     for r in rows:
-        print(f"{r['kernel']:10s} w={r['waves']} b={r['block']} g={r['grid_per_cu']:2d} lds={r['lds']} sched={r['sched']:5s} ov={r['oversub']} "
+        print(f"{r['kernel']:10s} w={r['waves']} b={r['block']} g={r['grid_per_cu']:2d} lds={r['lds']} sched={r['sched']:5s} ov={r['oversub']} {r['set']} "
               f"median {r['median_ms']:.4f} ms  min {r['min_ms']:.4f} ms  "
               f"{r['attempts_per_s'] / 1e6:.1f} M attempts/s")
     if a.out:
