@@ -25,7 +25,7 @@ STORAGE_AUTO, STORAGE_F32, STORAGE_F64 = 0, 1, 2
 OPT_KERNEL, OPT_BLOCK, OPT_GRID_PER_CU, OPT_WAVES, OPT_LDS_COORDS, OPT_SCHED, OPT_CHUNK = \
     1, 2, 3, 4, 5, 6, 7
 OPT_HELPERS = 8
-OPT_AFFINE_COORDS, OPT_COORD_MODE, OPT_PREFIX, OPT_OVERSUB, OPT_XCD_MAP = 9, 10, 11, 12, 13
+OPT_AFFINE_COORDS, OPT_COORD_MODE, OPT_PREFIX, OPT_OVERSUB, OPT_XCD_MAP, OPT_FAST_RCP = 9, 10, 11, 12, 13, 14
 KERNEL_DIRECT, KERNEL_PERSISTENT = 0, 1
 
 EXPORTS = [

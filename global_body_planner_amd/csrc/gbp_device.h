@@ -78,6 +78,10 @@ struct TerrainView {
   int affine;
   int bx, by;
   double ax, hx, ay, hy;
+  // host-verified cell-area reciprocal (gbp_terrain_create): when nonzero, two
+  // Newton steps from this seed give exactly 1.0 / ((x2-x1)*(y2-y1)) for every
+  // pair of grid spacings of the terrain (recip_area)
+  double rcp_seed;
 };
 
 // Coordinate modes of the hot kernels (template CM): 0 = coordinate vectors
@@ -187,16 +191,32 @@ __device__ __forceinline__ int nan_at(const TerrainView<ZT> &T, double x, double
   return (isnan(f11) || isnan(f12) || isnan(f21) || isnan(f22)) ? 1 : 0;
 }
 
+// 1.0 / d for a cell area d = (x2 - x1) * (y2 - y1) (fast_terrain_map.cpp:124):
+// the IEEE quotient, or, when the host has checked bit-for-bit that it equals
+// the quotient for every (x-spacing, y-spacing) pair of the terrain, two
+// Newton steps from the terrain's uniform seed 1 / (mean area) — four FMAs
+// instead of the scaled division sequence (v_rcp + v_div_scale/fmas/fixup).
+// `seed` is wave-uniform, so the branch is too.
+__host__ __device__ __forceinline__ double recip_newton(double d, double seed) {
+  const double e0 = __builtin_fma(-d, seed, 1.0);
+  const double y1 = __builtin_fma(seed, e0, seed);
+  const double e1 = __builtin_fma(-d, y1, 1.0);
+  return __builtin_fma(y1, e1, y1);
+}
+__device__ __forceinline__ double recip_area(double d, double seed) {
+  return seed != 0.0 ? recip_newton(d, seed) : 1.0 / d;
+}
+
 // fast_terrain_map.cpp:124-126 (left-to-right evaluation, no contraction)
 __device__ __forceinline__ double bilinear(double f11, double f12, double f21, double f22,
                                            double x1, double x2, double y1, double y2,
-                                           double x, double y) {
+                                           double x, double y, double seed = 0.0) {
 #ifdef GBP_EXPERIMENT_NO_DIV
   return 2500.0 * ((x2 - x1) * (y2 - y1)) *
          (f11 * (x2 - x) * (y2 - y) + f21 * (x - x1) * (y2 - y) + f12 * (x2 - x) * (y - y1) +
           f22 * (x - x1) * (y - y1));
 #endif
-  return 1.0 / ((x2 - x1) * (y2 - y1)) *
+  return recip_area((x2 - x1) * (y2 - y1), seed) *
          (f11 * (x2 - x) * (y2 - y) + f21 * (x - x1) * (y2 - y) + f12 * (x2 - x) * (y - y1) +
           f22 * (x - x1) * (y - y1));
 }
@@ -220,7 +240,7 @@ __device__ __forceinline__ bool height_at(const TerrainView<ZT> &T, double x, do
   load_quad(T, ix, iy, f11, f12, f21, f22);
   near = near || fabs(x - x1) < FRAGILE_EPS || fabs(x2 - x) < FRAGILE_EPS ||
          fabs(y - y1) < FRAGILE_EPS || fabs(y2 - y) < FRAGILE_EPS;
-  h = bilinear(f11, f12, f21, f22, x1, x2, y1, y2, x, y);
+  h = bilinear(f11, f12, f21, f22, x1, x2, y1, y2, x, y, T.rcp_seed);
   return true;
 }
 
@@ -270,8 +290,8 @@ __device__ __forceinline__ bool probe_height(const TerrainView<ZT> &T, const Pro
   near = near || fabs(x - x1) < FRAGILE_EPS || fabs(x2 - x) < FRAGILE_EPS ||
          fabs(y - y1) < FRAGILE_EPS || fabs(y2 - y) < FRAGILE_EPS;
 #endif
-  h = bilinear((double)p.q[0], (double)p.q[1], (double)p.q[2], (double)p.q[3], x1, x2, y1, y2, x,
-               y);
+  h = bilinear((double)p.q[0], (double)p.q[1], (double)p.q[2], (double)p.q[3], x1, x2, y1, y2, x, y,
+               T.rcp_seed);
   return true;
 }
 
@@ -295,7 +315,7 @@ __device__ __forceinline__ bool surface_normal(const TerrainView<ZT> &T, double 
 #pragma unroll
   for (int k = 0; k < 3; k++)
     n[k] = bilinear(L[k][b], L[k][b + 1], L[k][b + T.ny], L[k][b + T.ny + 1], x1, x2, y1, y2, x,
-                    y);
+                    y, T.rcp_seed);
   return true;
 }
 
@@ -524,7 +544,7 @@ __device__ __forceinline__ double probe_height_bf(const TerrainView<ZT> &T, cons
   near = false;
 #endif
   const double h = bilinear((double)p.q[0], (double)p.q[1], (double)p.q[2], (double)p.q[3], x1, x2,
-                            y1, y2, x, y);
+                            y1, y2, x, y, T.rcp_seed);
   return nanxy ? __builtin_nan("") : h;
 }
 

@@ -1046,6 +1046,8 @@ struct gbp_terrain {
   int64_t opt_oversub = 1;          // fixed-grid schedules: workgroups = oversub x resident
   int64_t opt_prefix = 512;         // sched 4: statically dealt share of a batch (1/1024)
   int64_t opt_affine = 1;           // compute coordinates when the affine form is exact
+  int64_t opt_fast_rcp = 1;         // cell-area reciprocal by verified Newton steps
+  double rcp_seed = 0;              // verified_rcp_seed (0: every spacing pair not exact)
   int64_t opt_xcd_map = 0;          // sched 1: slices numbered XCD-major
   int affine = 0;                   // host-verified affine coordinates (both axes)
   int bx = 0, by = 0;
@@ -1104,6 +1106,7 @@ TerrainView<ZT> view(const gbp_terrain *t) {
   v.hx = t->hx;
   v.ay = t->ay;
   v.hy = t->hy;
+  v.rcp_seed = t->opt_fast_rcp ? t->rcp_seed : 0.0;
   return v;
 }
 
@@ -1247,6 +1250,35 @@ bool affine_exact(const double *d, int n, double a, double h, int base) {
   return true;
 }
 
+// The seed of recip_area: 1 / (mean cell area), adopted only if two Newton
+// steps from it reproduce 1.0 / (dx * dy) bit for bit for EVERY pair of the
+// distinct x and y spacings of the terrain (the device evaluates the same
+// FMAs; products and differences are uncontracted in both TUs).  0 = divide.
+double verified_rcp_seed(const double *x, int nx, const double *y, int ny) {
+  if (nx < 2 || ny < 2) return 0.0;
+  auto spacings = [](const double *d, int n) {
+    std::vector<double> v;
+    for (int i = 0; i + 1 < n; i++) v.push_back(d[i + 1] - d[i]);
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end(), [](double a, double b) {
+              return memcmp(&a, &b, sizeof a) == 0;
+            }), v.end());
+    return v;
+  };
+  const std::vector<double> sx = spacings(x, nx), sy = spacings(y, ny);
+  if ((double)sx.size() * (double)sy.size() > 4e6) return 0.0;
+  const double seed = 1.0 / (((x[nx - 1] - x[0]) / (double)(nx - 1)) *
+                             ((y[ny - 1] - y[0]) / (double)(ny - 1)));
+  if (!std::isfinite(seed) || !(seed > 0)) return 0.0;
+  for (double dx : sx)
+    for (double dy : sy) {
+      const double d = dx * dy;
+      const double q = 1.0 / d, r = recip_newton(d, seed);
+      if (memcmp(&q, &r, sizeof q) != 0) return 0.0;
+    }
+  return seed;
+}
+
 bool affine_fit(const double *d, int n, double *a, double *h, int *base) {
   if (n < 2) return false;
   const double cands[3] = {(d[n - 1] - d[0]) / (double)(n - 1), d[1] - d[0], d[n - 1] - d[n - 2]};
@@ -1386,6 +1418,7 @@ int gbp_terrain_create(int device, int nx, int ny, const double *x, const double
   t->one_x = one_step_exact(x, nx, t->inv_hx);
   t->one_y = one_step_exact(y, ny, t->inv_hy);
   t->affine = affine_fit(x, nx, &t->ax, &t->hx, &t->bx) && affine_fit(y, ny, &t->ay, &t->hy, &t->by);
+  t->rcp_seed = verified_rcp_seed(x, nx, y, ny);
   (void)hipDeviceGetAttribute(&t->num_cus, hipDeviceAttributeMultiprocessorCount, device);
   if (t->num_cus <= 0) t->num_cus = 256;
   int rc = GBP_OK;
@@ -1523,6 +1556,9 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
     case GBP_OPT_XCD_MAP:
       t->opt_xcd_map = value ? 1 : 0;
       return GBP_OK;
+    case GBP_OPT_FAST_RCP:
+      t->opt_fast_rcp = value ? 1 : 0;
+      return GBP_OK;
     default:
       return GBP_E_INVALID_ARG;
   }
@@ -1544,6 +1580,7 @@ int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value) {
     case GBP_OPT_PREFIX: *value = t->opt_prefix; return GBP_OK;
     case GBP_OPT_OVERSUB: *value = t->opt_oversub; return GBP_OK;
     case GBP_OPT_XCD_MAP: *value = t->opt_xcd_map; return GBP_OK;
+    case GBP_OPT_FAST_RCP: *value = t->opt_fast_rcp ? (t->rcp_seed != 0.0 ? 1 : 0) : 0; return GBP_OK;
     case GBP_OPT_COORD_MODE: *value = coord_mode(t, t->opt_lds_coords != 0); return GBP_OK;
     default: return GBP_E_INVALID_ARG;
   }

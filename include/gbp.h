@@ -136,6 +136,9 @@ int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage,
 #define GBP_OPT_OVERSUB      12  /* sched 1/3/4: launch oversub x the resident workgroups */
 #define GBP_OPT_XCD_MAP      13  /* sched 1: 1 = each XCD takes one contiguous eighth of
                                     the batch (workgroup b runs on XCD b % 8)           */
+#define GBP_OPT_FAST_RCP     14  /* 1 (default): the bilinear 1/((x2-x1)(y2-y1)) by two
+                                    Newton steps when gbp_terrain_create verified them
+                                    bit-exact for every spacing pair; get: 1 = in use   */
 #define GBP_KERNEL_DIRECT     0  /* one lane per attempt                              */
 #define GBP_KERNEL_PERSISTENT 1  /* persistent waves, lanes re-packed per sample      */
 int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value);

@@ -371,6 +371,36 @@ def test_validate_pairs_xcd_map(gpu, name):
         T.set_option(L.OPT_XCD_MAP, 0)
 
 
+@pytest.mark.parametrize("name", TERRAINS)
+def test_fast_reciprocal_bit_exact(gpu, name):
+    """The bilinear 1/((x2-x1)(y2-y1)) by two Newton steps (GBP_OPT_FAST_RCP,
+    enabled by gbp_terrain_create only after checking every spacing pair
+    bit-for-bit) gives the same heights, pair results and flags as the IEEE
+    division, and the oracle."""
+    data, T, O = terrain_pair(name)
+    used = T.get_option(L.OPT_FAST_RCP)
+    print(name, "fast reciprocal in use:", used)
+    if name.startswith("synth") or name.endswith("gridmap"):
+        assert used == 1  # affine / grid_map geometry: a handful of spacings
+    n = 6000
+    s, a, d, _, _ = attempts_oracle(O, n, seed=777)
+    rng = np.random.default_rng(5)
+    xy = np.stack([rng.uniform(data.x[0], data.x[-1], 20000), rng.uniform(data.y[0], data.y[-1], 20000)], 1)
+    outs = []
+    try:
+        for f in (0, 1):
+            T.set_option(L.OPT_FAST_RCP, f)
+            h, _, _ = T.height(torch.from_numpy(xy))
+            res = T.validate_pairs(torch.from_numpy(s), torch.from_numpy(a), torch.from_numpy(d))
+            outs.append((np_(h), np_(res.valid), np_(res.s_new), np_(res.t_new), u32(res.flags),
+                         u32(res.counts)))
+    finally:
+        T.set_option(L.OPT_FAST_RCP, 1)
+    for x, y in zip(outs[0], outs[1]):
+        assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+    assert_pairs_equal(outs[1][1:], O.validate_pairs(s, a, d, nthreads=16), f"rcp {name}")
+
+
 def test_engine_matches_golden_vectors(gpu):
     """The engine against the committed oracle vectors (tests/golden)."""
     import os
