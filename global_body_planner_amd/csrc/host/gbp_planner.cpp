@@ -1204,6 +1204,103 @@ bool RRTConnectClass::buildRRTConnectBatched(FastTerrainMap &terrain, State s_st
   return true;
 }
 
+bool RRTConnectClass::buildRRTConnectBatchedAnytime(FastTerrainMap &terrain, State s_start,
+                                                    State s_goal, int batch, double max_time,
+                                                    double max_time_opt,
+                                                    std::vector<State> &state_sequence,
+                                                    std::vector<Action> &action_sequence,
+                                                    BatchStats *stats) {
+  const auto t_start = std::chrono::high_resolution_clock::now();
+  auto since = [](std::chrono::high_resolution_clock::time_point t0) {
+    return std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t0).count();
+  };
+  BatchStats local;
+  BatchStats &st = stats ? *stats : local;
+  wall_to_first_ = -1;
+  goal_found = false;
+  cost_vector_.clear();
+  cost_vector_times_.clear();
+  length_vector_.clear();
+  yaw_vector_.clear();
+  anytime_horizon = poseDistance(s_start, s_goal) / planning_rate_estimate;  // :345
+  num_vertices = 0;
+  double cost_so_far = INFTY;
+  std::vector<State> best_states;
+  std::vector<Action> best_actions;
+  double best_length = 0, best_yaw = 0;
+  for (int restart = 0;; restart++) {  // :350-420, one pair of fresh trees per restart
+    PlannerClass Ta(terrain.device()), Tb(terrain.device());
+    Ta.setStream(seed_, 2000 + 2 * restart);
+    Tb.setStream(seed_, 2001 + 2 * restart);
+    Ta.init(s_start, cost_add_yaw_flag_, cost_add_yaw_length_weight_, cost_add_yaw_yaw_weight_);
+    Tb.init(s_goal, cost_add_yaw_flag_, cost_add_yaw_length_weight_, cost_add_yaw_yaw_weight_);
+    const auto t_run = std::chrono::high_resolution_clock::now();
+    bool found = false;
+    int ia = -1, ib = -1;
+    while (true) {  // runRRTConnect (:228-318) at batch granularity
+      if (since(t_run) >= anytime_horizon) {
+        anytime_horizon *= horizon_expansion_factor;
+        break;
+      }
+      st.iterations++;
+      if (halfIterationBatched(Ta, Tb, terrain, FORWARD, batch, ia, ib, &st) ||
+          halfIterationBatched(Tb, Ta, terrain, REVERSE, batch, ib, ia, &st)) {
+        found = true;
+        break;
+      }
+      if (since(t_start) >= max_time) break;
+    }
+    num_vertices += Ta.getNumVertices() + Tb.getNumVertices();
+    st.vertices_a = Ta.getNumVertices();
+    st.vertices_b = Tb.getNumVertices();
+    tree_extent(Ta, st.extent_a);
+    tree_extent(Tb, st.extent_b);
+    double el = since(t_start);
+    if (found) {
+      st.solutions++;
+      if (wall_to_first_ < 0) wall_to_first_ = el;
+      std::vector<int> path_a = pathFromStart(Ta, ia);
+      std::vector<int> path_b = pathFromStart(Tb, ib);
+      std::reverse(path_b.begin(), path_b.end());
+      std::vector<Action> action_b = getActionSequenceReverse(Tb, path_b);
+      path_b.erase(path_b.begin());
+      std::vector<State> states = getStateSequence(Ta, path_a);
+      std::vector<State> sb = getStateSequence(Tb, path_b);
+      states.insert(states.end(), sb.begin(), sb.end());
+      std::vector<Action> actions = getActionSequence(Ta, path_a);
+      actions.insert(actions.end(), action_b.begin(), action_b.end());
+      path_length_ = Ta.getGValue(ia) + Tb.getGValue(ib);
+      path_yaw_ = Ta.getYValue(ia) + Tb.getYValue(ib);
+      postProcessPath(states, actions, terrain);  // :398, sets path_length_/path_cost_
+      if (path_cost_ < cost_so_far) {  // :401-414
+        cost_so_far = path_cost_;
+        best_length = path_length_;
+        best_yaw = path_yaw_;
+        best_states = states;
+        best_actions = actions;
+        el = since(t_start);
+        length_vector_.push_back(best_length);
+        yaw_vector_.push_back(best_yaw);
+        cost_vector_.push_back(cost_so_far);
+        cost_vector_times_.push_back(el);
+      }
+      goal_found = true;
+    }
+    if (goal_found && el >= max_time_opt) break;  // :417
+    if (el >= max_time) break;                     // no (further) time: the best so far
+  }
+  elapsed_total = std::chrono::high_resolution_clock::now() - t_start;
+  if (!goal_found) return false;
+  state_sequence = best_states;
+  action_sequence = best_actions;
+  path_length_ = best_length;
+  path_yaw_ = best_yaw;
+  path_cost_ = cost_so_far;
+  path_duration_ = 0;
+  for (const Action &a : action_sequence) path_duration_ += a[6] + a[7];
+  return true;
+}
+
 // ============================================================================
 // RRTStarConnectClass
 // ============================================================================
@@ -1494,7 +1591,7 @@ bool RRTStarConnectClass::buildRRTStarConnectBatched(FastTerrainMap &terrain, St
 extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r,
                                     double *path_states, double *path_actions, int capacity) {
   using namespace gbp_amd;
-  if (!p || !r || p->batch < 1 || p->algorithm < 0 || p->algorithm > 1) return GBP_E_INVALID_ARG;
+  if (!p || !r || p->batch < 1 || p->algorithm < 0 || p->algorithm > 2) return GBP_E_INVALID_ARG;
   try {
     FastTerrainMap terrain(p->device);
     terrain.loadDataFlat(p->nx, p->ny, p->x, p->y, p->z, p->dx, p->dy, p->dz);
@@ -1511,10 +1608,14 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
         p->algorithm == 1
             ? planner.buildRRTStarConnectBatched(terrain, s0, s1, p->batch, p->max_time, states,
                                                  actions, &st)
+        : p->algorithm == 2
+            ? planner.buildRRTConnectBatchedAnytime(terrain, s0, s1, p->batch, p->max_time,
+                                                    p->max_time_opt, states, actions, &st)
             : planner.buildRRTConnectBatched(terrain, s0, s1, p->batch, p->max_time, states,
                                              actions, &st);
     double ttf = planner.wallTimeToFirst();
-    if (found && p->post_process) planner.postProcessPath(states, actions, terrain);
+    // algorithm 2's paths are post-processed inside the restarts (as buildRRTConnect)
+    if (found && p->post_process && p->algorithm != 2) planner.postProcessPath(states, actions, terrain);
     const std::chrono::duration<double> tot = std::chrono::high_resolution_clock::now() - t0;
     memset(r, 0, sizeof(*r));
     r->found = found ? 1 : 0;
@@ -1538,7 +1639,7 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
       double len = 0;
       for (size_t i = 1; i < states.size(); i++) len += planning_utils::poseDistance(states[i - 1], states[i]);
       r->path_length = len;
-      r->path_cost = p->algorithm == 1 ? planner.bestCost() : len;
+      r->path_cost = p->algorithm == 1 ? planner.bestCost() : (p->algorithm == 2 ? planner.pathCost() : len);
       double dur = 0;
       for (const Action &a : actions) dur += a[6] + a[7];
       r->path_duration = dur;

@@ -26,7 +26,7 @@ class PlanParams(ctypes.Structure):
                 ("x", _P), ("y", _P), ("z", _P), ("dx", _P), ("dy", _P), ("dz", _P),
                 ("start", _D * 8), ("goal", _D * 8), ("batch", ctypes.c_int),
                 ("max_time", _D), ("seed", ctypes.c_uint64), ("post_process", ctypes.c_int),
-                ("algorithm", ctypes.c_int)]
+                ("algorithm", ctypes.c_int), ("max_time_opt", _D)]
 
 
 class PlanResult(ctypes.Structure):
@@ -68,11 +68,15 @@ def start_goal_state(height, x, y):
 
 
 def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018,
-                     post_process=False, device=0, capacity=4096, algorithm=0):
+                     post_process=False, device=0, capacity=4096, algorithm=0, max_time_opt=0.0):
     """Plan start -> goal on terrain `data` (terrain_data.TerrainData).
 
     algorithm 0: batch-synchronous RRT-Connect, stops at the first solution;
-    algorithm 1: batch-synchronous RRT*-Connect, anytime until max_time.
+    algorithm 1: batch-synchronous RRT*-Connect, anytime until max_time;
+    algorithm 2: RRTConnectClass::buildRRTConnect's anytime restarts
+      (rrt_connect.cpp:323-467) on batch-synchronous trees: restart on the
+      growing horizon, post-process every solution, keep the cheapest, stop
+      once a solution exists and `max_time_opt` seconds have passed.
     Returns a dict with the C result fields plus `states` [n][8] and
     `actions` [n-1][10] (the found path; empty if none)."""
     L = load()
@@ -89,6 +93,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     p.goal[:] = [float(v) for v in goal]
     p.batch, p.max_time, p.seed, p.post_process = int(batch), float(max_time), int(seed), int(post_process)
     p.algorithm = int(algorithm)
+    p.max_time_opt = float(max_time_opt)
     r = PlanResult()
     states = np.zeros((capacity, 8))
     actions = np.zeros((capacity, 10))
@@ -107,6 +112,13 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
 def plan_rrt_star_connect(data, start, goal, **kw):
     """RRTStarConnectClass::buildRRTStarConnect, batch-synchronous (algorithm 1)."""
     return plan_rrt_connect(data, start, goal, algorithm=1, **kw)
+
+
+def plan_rrt_connect_anytime(data, start, goal, max_time_opt=1.0, **kw):
+    """RRTConnectClass::buildRRTConnect's anytime restarts, batch-synchronous
+    (algorithm 2); `cost_history` is not returned, `solutions` counts the
+    restarts that reached the goal."""
+    return plan_rrt_connect(data, start, goal, algorithm=2, max_time_opt=max_time_opt, **kw)
 
 
 def attempt_connect(terrain, s_existing, s, direction, t_s=None, adaptive=False, s_new=None,

@@ -290,6 +290,9 @@ class RRTClass {
   // wall clock from the start of the build call to the first goal (the
   // reference's elapsed_to_first restarts with every tree pair)
   double wallTimeToFirst() const { return wall_to_first_; }
+  // the last build's path cost / its history (rrt_connect.h getters' data)
+  double pathCost() const { return path_cost_; }
+  const std::vector<double> &costHistory() const { return cost_vector_; }
 
  protected:
   bool goal_found = false;
@@ -347,6 +350,19 @@ class RRTConnectClass : public RRTClass {
   bool buildRRTConnectBatched(FastTerrainMap &terrain, State s_start, State s_goal, int batch,
                               double max_time, std::vector<State> &state_sequence,
                               std::vector<Action> &action_sequence, BatchStats *stats = nullptr);
+
+  // buildRRTConnect's anytime restarts (rrt_connect.cpp:323-467) on the
+  // batch-synchronous half-iterations: fresh trees every restart, a restart
+  // ends after anytime_horizon seconds (poseDistance(start, goal) /
+  // planning_rate_estimate, x horizon_expansion_factor per restart) or at its
+  // first REACHED connect; every solution is post-processed and the cheapest
+  // (path_cost_) kept.  Stops once a solution exists and max_time_opt has
+  // passed, or at max_time without one.  Returns the best path.
+  bool buildRRTConnectBatchedAnytime(FastTerrainMap &terrain, State s_start, State s_goal,
+                                     int batch, double max_time, double max_time_opt,
+                                     std::vector<State> &state_sequence,
+                                     std::vector<Action> &action_sequence,
+                                     BatchStats *stats = nullptr);
 
   // attemptConnect for many independent pairs (lock-step rounds, one engine
   // launch per recursion depth); s_new / a_new are in/out per pair
@@ -482,7 +498,11 @@ typedef struct {
   double max_time;      // seconds
   uint64_t seed;
   int post_process;     // run postProcessPath on the found path
-  int algorithm;        // 0 rrt-connect, 1 rrt-star-connect (anytime until max_time)
+  int algorithm;        // 0 rrt-connect (first solution), 1 rrt-star-connect (anytime
+                        // until max_time), 2 rrt-connect with the reference's anytime
+                        // restarts (best post-processed path after max_time_opt)
+  double max_time_opt;  // algorithm 2: keep restarting until a solution exists and this
+                        // many seconds have passed (buildRRTConnect's max_time_opt)
 } gbp_plan_params;
 
 typedef struct {

@@ -105,7 +105,8 @@ def test_planner_library_exports_and_fails_without_device():
     for name in c_syms:
         assert f"int {name}(" in txt
     # the C structs mirror the header layout
-    assert ctypes.sizeof(planner.PlanParams) == 4 * 3 + 4 + 8 * 6 + 8 * 16 + 8 + 8 + 8 + 8
+    # ... + max_time_opt (double)
+    assert ctypes.sizeof(planner.PlanParams) == 4 * 3 + 4 + 8 * 6 + 8 * 16 + 8 + 8 + 8 + 8 + 8
     import torch
     if not torch.cuda.is_available():
         from global_body_planner_amd import terrain_data as td

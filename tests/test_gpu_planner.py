@@ -171,3 +171,28 @@ def test_plan_rrt_star_synth256(gpu):
     S = out["states"]
     length = sum(oracle.pose_distance(S[i], S[i + 1]) for i in range(len(S) - 1))
     assert out["path_cost"] == pytest.approx(length, rel=1e-9)
+
+
+def test_plan_anytime_restarts_synth256(gpu):
+    """buildRRTConnect's anytime restarts (rrt_connect.cpp:323-467) on the
+    batched trees (algorithm 2): keeps restarting until a solution exists and
+    max_time_opt has passed; the returned (post-processed) path is the cheapest
+    found, with the reference's endpoints and only pair-check-accepted edges."""
+    data = td.synth_rough(256)
+    O = oracle.OracleTerrain.from_data(data)
+    start, goal = _start_goal(O, 1.0, 2.55, 4.02, 2.55)
+    out = planner.plan_rrt_connect_anytime(data, start, goal, max_time_opt=0.6, batch=256,
+                                           max_time=30.0, seed=9)
+    assert out["found"] == 1 and out["solutions"] >= 1
+    assert out["total_time"] >= 0.6 and 0 < out["time_to_first"] <= out["total_time"]
+    S, A = out["states"], out["actions"]
+    assert np.array_equal(S[0], start) and np.array_equal(S[-1], goal)
+    fv, _, _, _, _ = O.validate_pairs(S[:-1], A, np.zeros(len(A), np.uint8))
+    rv, _, _, _, _ = O.validate_pairs(S[1:], A, np.ones(len(A), np.uint8))
+    assert ((fv != 0) | (rv != 0)).all()
+    assert np.isfinite(out["path_cost"]) and out["path_cost"] > 0
+    # one restart only (max_time_opt 0): the first solution, post-processed
+    one = planner.plan_rrt_connect_anytime(data, start, goal, max_time_opt=0.0, batch=256,
+                                           max_time=30.0, seed=9)
+    assert one["found"] == 1 and one["solutions"] == 1
+    assert out["path_cost"] <= one["path_cost"] + 1e-12  # same first restart, then only improvements
