@@ -149,6 +149,10 @@ TTFS_PAIRS = {
                          "batch": 262144 // 6},
     "synth-rough-256": {"start": (1.0, 2.55), "goal": (4.02, 2.55),
                         "reference_s": [0.05, 1.19, 2.64], "batch": 65536 // 6},
+    # config 1: the slope CSV through the grid_map geometry; the
+    # reference's own CPU build took 12.0 / 27.0 / 28.8 s (BASELINE §2)
+    "slope-gridmap": {"start": (1.0, 0.0), "goal": (8.0, 0.0),
+                      "reference_s": [12.0, 27.0, 28.8], "batch": 65536 // 6},
 }
 
 
@@ -351,12 +355,14 @@ def main():
     tot_attempts = float(sums[0].item()) * args.steps
     value = tot_attempts / elapsed
 
-    ttfs = ttfs2 = None
+    ttfs = ttfs2 = ttfs1 = None
     if args.ttfs_runs > 0:
         ttfs = time_to_first_solution(data, args.terrain, args.ttfs_runs, args.plan_max_time, args,
                                       rank, world, dev) if args.terrain in TTFS_PAIRS else None
         # config 2 (synth-rough-256), where the reference has wall times to compare with
         ttfs2 = time_to_first_solution(td.by_name("synth-rough-256"), "synth-rough-256", 3, 20.0,
+                                       args, rank, world, dev)
+        ttfs1 = time_to_first_solution(td.by_name("slope-gridmap"), "slope-gridmap", 3, 20.0,
                                        args, rank, world, dev)
 
     if rank == 0:
@@ -410,6 +416,7 @@ def main():
             },
             "time_to_first_solution": ttfs,
             "time_to_first_solution_config2": ttfs2,
+            "time_to_first_solution_config1": ttfs1,
         }
         if args.lookup_micro:
             out["terrain_lookup"] = terrain_lookup_micro(T, data, dev)
