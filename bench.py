@@ -60,7 +60,6 @@ def parse():
     p.add_argument("--seed", type=int, default=W.CONFIG_SEEDS[3])
     p.add_argument("--kernel", choices=["persistent", "direct"], default="persistent")
     p.add_argument("--waves", type=int, default=2)
-    p.add_argument("--grid-per-cu", type=int, default=8)
     p.add_argument("--streams", type=int, default=4,
                    help="HIP streams the K independent steps are issued on round-robin (1: serial)")
     p.add_argument("--adaptive", action="store_true")
@@ -276,7 +275,6 @@ def main():
     T = gbp.Terrain.from_data(data, device=local)
     T.set_option(L.OPT_KERNEL, L.KERNEL_PERSISTENT if args.kernel == "persistent" else L.KERNEL_DIRECT)
     T.set_option(L.OPT_WAVES, args.waves)
-    T.set_option(L.OPT_GRID_PER_CU, args.grid_per_cu)
     B = args.batch
     base, _ = sharding.weak_shard(rank, B)   # rank r: attempts [r*B, (r+1)*B) of one global stream
     s, a, d, tgt, tries = W.make_attempts(T, B, args.seed, index_base=base)

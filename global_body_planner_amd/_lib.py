@@ -17,15 +17,13 @@ FLIGHT, STANCE, CONNECT_STANCE = 0, 1, 2
 FORWARD, REVERSE = 0, 1
 TRAPPED, ADVANCED, REACHED = 0, 1, 2
 NUM_GEN_STATES = 6
-F_VALID, F_OOD, F_NAN, F_SNEW_SET, F_TNEW_SET, F_FRAGILE, F_LIMIT = 1, 2, 4, 8, 16, 32, 64
-MAX_SAMPLES = 4096
+F_VALID, F_OOD, F_NAN, F_SNEW_SET, F_TNEW_SET, F_FRAGILE, F_LIMIT, F_RESOLVED = 1, 2, 4, 8, 16, 32, 64, 128
+MAX_SAMPLES = 7000
 F_STAGE_SHIFT = 8
 F_STAGE_MASK = 0xF << F_STAGE_SHIFT
 STORAGE_AUTO, STORAGE_F32, STORAGE_F64 = 0, 1, 2
-OPT_KERNEL, OPT_BLOCK, OPT_GRID_PER_CU, OPT_WAVES, OPT_LDS_COORDS, OPT_SCHED, OPT_CHUNK = \
-    1, 2, 3, 4, 5, 6, 7
-OPT_HELPERS = 8
-OPT_AFFINE_COORDS, OPT_COORD_MODE, OPT_PREFIX, OPT_OVERSUB, OPT_XCD_MAP, OPT_FAST_RCP = 9, 10, 11, 12, 13, 14
+OPT_KERNEL, OPT_BLOCK, OPT_WAVES, OPT_LDS_COORDS, OPT_HELPERS = 1, 2, 4, 5, 8
+OPT_AFFINE_COORDS, OPT_COORD_MODE, OPT_XCD_MAP, OPT_FAST_RCP = 9, 10, 13, 14
 KERNEL_DIRECT, KERNEL_PERSISTENT = 0, 1
 
 EXPORTS = [

@@ -54,16 +54,11 @@ __device__ __forceinline__ double std_max(double a, double b) { return (a < b) ?
 // 16 MB, 1 aligned load) are 7-8 % slower on the validate kernel and 8-24 %
 // slower on lookups: the quads' footprint drops the L2 hit rate from 86 % to
 // 39 %.  Every lookup's cell is clamped into range, so no other z is read.
-// (-DGBP_ZROWS / -DGBP_ZQUADS: the other layouts, diagnostic builds.)
-template <class ZT>
-struct alignas(4 * sizeof(ZT)) ZQuad {
-  ZT q[4];
-};
 
 template <class ZT>
 struct TerrainView {
   const double *x, *y;           // coordinates (ascending)
-  const ZT *z;                   // heights: x-pairs (rows / quads in diagnostic builds)
+  const ZT *z;                   // heights: x-pairs
   const double *dx, *dy, *dz;    // slope layers, x-major fp64, may be null
   int nx, ny;
   double x0, xN, y0, yN;         // x[0], x[nx-1], y[0], y[ny-1]
@@ -114,40 +109,25 @@ __device__ __forceinline__ int bracket(const double *__restrict__ d, int n, doub
                                        double dN, double inv, int one, double v) {
   if (!(v >= d0 && v < dN)) return (v >= dN) ? BR_HIGH : BR_LOW;
   int i = bracket_guess(n, d0, inv, v);
-#ifndef GBP_EXPERIMENT_FAST_BRACKET  // diagnostic timing build only (results may differ)
   if (one) {
     i += (v >= d[i + 1] ? 1 : 0) - (v < d[i] ? 1 : 0);
   } else {
     while (i > 0 && v < d[i]) --i;
     while (i < n - 2 && v >= d[i + 1]) ++i;
   }
-#endif
   return i;
 }
 
 // the four corners of cell (ix, iy), ix <= nx-2, iy <= ny-2, in Probe::q order
 template <class ZT>
 __device__ __forceinline__ void fetch_cell(const TerrainView<ZT> &T, int ix, int iy, ZT q[4]) {
-#if defined(GBP_ZROWS)
-  const ZT *p = T.z + (size_t)ix * T.ny + iy;
-  q[0] = p[0];
-  q[1] = p[1];
-  q[2] = p[T.ny];
-  q[3] = p[T.ny + 1];
-#elif defined(GBP_ZQUADS)  // cell quads: zq[ix*(ny-1) + iy] = the cell's four corners
-  const ZQuad<ZT> c = ((const ZQuad<ZT> *)T.z)[(size_t)ix * (T.ny - 1) + iy];
-  q[0] = c.q[0];
-  q[1] = c.q[1];
-  q[2] = c.q[2];
-  q[3] = c.q[3];
-#else  // x-pairs: zp[ix*ny + iy] = {z[ix][iy], z[ix+1][iy]}; the cell is 2 adjacent pairs
+  // x-pairs: zp[ix*ny + iy] = {z[ix][iy], z[ix+1][iy]}; the cell is 2 adjacent pairs
   typedef ZT pair4 __attribute__((ext_vector_type(4), aligned(2 * sizeof(ZT))));
   const pair4 c = *(const pair4 *)(T.z + 2 * ((size_t)ix * T.ny + iy));
   q[0] = c[0];
   q[2] = c[1];
   q[1] = c[2];
   q[3] = c[3];
-#endif
 }
 
 // bracket() of axis AX of the view, coordinates per CM
@@ -157,14 +137,12 @@ __device__ __forceinline__ int bracket_ax(const TerrainView<ZT> &T, double v) {
   const int n = AX == 0 ? T.nx : T.ny;
   if (!(v >= d0 && v < dN)) return (v >= dN) ? BR_HIGH : BR_LOW;
   int i = bracket_guess(n, d0, AX == 0 ? T.inv_hx : T.inv_hy, v);
-#ifndef GBP_EXPERIMENT_FAST_BRACKET  // diagnostic timing build only (results may differ)
   if (AX == 0 ? T.one_x : T.one_y) {
     i += (v >= coord<CM, AX>(T, i + 1) ? 1 : 0) - (v < coord<CM, AX>(T, i) ? 1 : 0);
   } else {
     while (i > 0 && v < coord<CM, AX>(T, i)) --i;
     while (i < n - 2 && v >= coord<CM, AX>(T, i + 1)) ++i;
   }
-#endif
   return i;
 }
 
@@ -211,11 +189,6 @@ __device__ __forceinline__ double recip_area(double d, double seed) {
 __device__ __forceinline__ double bilinear(double f11, double f12, double f21, double f22,
                                            double x1, double x2, double y1, double y2,
                                            double x, double y, double seed = 0.0) {
-#ifdef GBP_EXPERIMENT_NO_DIV
-  return 2500.0 * ((x2 - x1) * (y2 - y1)) *
-         (f11 * (x2 - x) * (y2 - y) + f21 * (x - x1) * (y2 - y) + f12 * (x2 - x) * (y - y1) +
-          f22 * (x - x1) * (y - y1));
-#endif
   return recip_area((x2 - x1) * (y2 - y1), seed) *
          (f11 * (x2 - x) * (y2 - y) + f21 * (x - x1) * (y2 - y) + f12 * (x2 - x) * (y - y1) +
           f22 * (x - x1) * (y - y1));
@@ -260,10 +233,6 @@ __device__ __forceinline__ void probe(const TerrainView<ZT> &T, double x, double
   p.ix = bracket_ax<CM, 0>(T, x);
   p.iy = bracket_ax<CM, 1>(T, y);
   const int cx = p.ix < 0 ? 0 : p.ix, cy = p.iy < 0 ? 0 : p.iy;
-#ifdef GBP_EXPERIMENT_NO_ZLOAD
-  p.q[0] = (ZT)(cx * 1e-4); p.q[1] = (ZT)(cy * 1e-4); p.q[2] = (ZT)0.1; p.q[3] = (ZT)0.2;
-  return;
-#endif
   fetch_cell(T, cx, cy, p.q);
 }
 
@@ -286,10 +255,8 @@ __device__ __forceinline__ bool probe_height(const TerrainView<ZT> &T, const Pro
   if (p.ix < 0 || p.iy < 0) return false;
   const double x1 = coord<CM, 0>(T, p.ix), x2 = coord<CM, 0>(T, p.ix + 1);
   const double y1 = coord<CM, 1>(T, p.iy), y2 = coord<CM, 1>(T, p.iy + 1);
-#ifndef GBP_EXPERIMENT_NO_FRAGILE
   near = near || fabs(x - x1) < FRAGILE_EPS || fabs(x2 - x) < FRAGILE_EPS ||
          fabs(y - y1) < FRAGILE_EPS || fabs(y2 - y) < FRAGILE_EPS;
-#endif
   h = bilinear((double)p.q[0], (double)p.q[1], (double)p.q[2], (double)p.q[3], x1, x2, y1, y2, x, y,
                T.rcp_seed);
   return true;
@@ -322,9 +289,6 @@ __device__ __forceinline__ bool surface_normal(const TerrainView<ZT> &T, double 
 // stance divisions x / (6 t_s), x / (2 t_s) (Markstein with a constant
 // reciprocal was measured: no faster than the hardware-assisted sequence)
 __device__ __forceinline__ double pdiv(double x, double d) {
-#ifdef GBP_EXPERIMENT_NO_PROPDIV  // diagnostic timing build only (results differ)
-  return x * 0.5;
-#endif
   return x / d;
 }
 #define PDIV6(x) pdiv((x), 6.0 * t_s)
@@ -396,58 +360,6 @@ __device__ __forceinline__ bool is_valid_action(const double *a) {
   return true;
 }
 
-// ---- rotation trig of isValidState (planning_utils.cpp:578-594) ---------------
-// The reference forms cos/sin(atan2(dy, dx)) and cos/sin(p) with glibc; the
-// device's libm differs from glibc by ulps anyway, which is why decisions
-// within FRAGILE_EPS of a threshold are flagged.  Within that contract the
-// same values are computed more cheaply:
-//  * yaw: cos(atan2(dy,dx)) = dx/|v|, sin(atan2(dy,dx)) = dy/|v| (|v| is the
-//    speed already computed for check (3)); error <= 2 ulp.  |v| = 0, tiny,
-//    huge or non-finite take the libm path (atan2(+-0, -0) = +-pi etc.).
-//  * pitch: |p| < P_MAX = 1 here (check (2)), so sin/cos are their Taylor
-//    series to p^19 / p^20 (truncation < 5e-20) in Horner form with fma;
-//    NaN propagates as with libm.
-// Position error from either is ~1e-16 m, far below FRAGILE_EPS = 1e-12.
-__device__ __forceinline__ void rotation_trig(double dx, double dy, double speed, double p,
-                                              double &cy, double &sy, double &cp, double &sp,
-                                              bool live = true) {
-  if (!live || (speed > 1e-150 && speed < 1e150)) {
-    cy = dx / speed;
-    sy = dy / speed;
-  } else {
-    const double yaw = atan2(dy, dx);
-    cy = cos(yaw);
-    sy = sin(yaw);
-  }
-  if (!live || fabs(p) < 1.0) {
-    const double z = p * p;
-    double ps = -1.0 / 121645100408832000.0;                  // -1/19!
-    ps = __builtin_fma(ps, z, 1.0 / 355687428096000.0);       //  1/17!
-    ps = __builtin_fma(ps, z, -1.0 / 1307674368000.0);        // -1/15!
-    ps = __builtin_fma(ps, z, 1.0 / 6227020800.0);            //  1/13!
-    ps = __builtin_fma(ps, z, -1.0 / 39916800.0);             // -1/11!
-    ps = __builtin_fma(ps, z, 1.0 / 362880.0);                //  1/9!
-    ps = __builtin_fma(ps, z, -1.0 / 5040.0);                 // -1/7!
-    ps = __builtin_fma(ps, z, 1.0 / 120.0);                   //  1/5!
-    ps = __builtin_fma(ps, z, -1.0 / 6.0);                    // -1/3!
-    sp = __builtin_fma(p * z, ps, p);
-    double pc = 1.0 / 2432902008176640000.0;                  //  1/20!
-    pc = __builtin_fma(pc, z, -1.0 / 6402373705728000.0);     // -1/18!
-    pc = __builtin_fma(pc, z, 1.0 / 20922789888000.0);        //  1/16!
-    pc = __builtin_fma(pc, z, -1.0 / 87178291200.0);          // -1/14!
-    pc = __builtin_fma(pc, z, 1.0 / 479001600.0);             //  1/12!
-    pc = __builtin_fma(pc, z, -1.0 / 3628800.0);              // -1/10!
-    pc = __builtin_fma(pc, z, 1.0 / 40320.0);                 //  1/8!
-    pc = __builtin_fma(pc, z, -1.0 / 720.0);                  // -1/6!
-    pc = __builtin_fma(pc, z, 1.0 / 24.0);                    //  1/4!
-    pc = __builtin_fma(pc, z, -0.5);                          // -1/2!
-    cp = __builtin_fma(z, pc, 1.0);
-  } else {
-    cp = cos(p);
-    sp = sin(p);
-  }
-}
-
 // A 64-bit constant materialised AT ITS USE (two s_mov_b32 inside the loop
 // body, an SGPR pair that lives for one instruction): left to itself the
 // compiler hoists every polynomial coefficient out of the persistent loop and
@@ -466,8 +378,10 @@ __device__ __forceinline__ double kc() {
 // isValidState's rotation (planning_utils.cpp:578-594) for a state that passed
 // checks (2)-(3), i.e. |p| < P_MAX = 1 and speed = |(dx, dy)| <= V_MAX (or
 // NaN), without libm, whose constant tables would stay resident for the whole
-// persistent loop.  Same contract as rotation_trig (decisions within
-// FRAGILE_EPS of a threshold are flagged):
+// persistent loop.  The reference forms these values with glibc's atan2 /
+// cos / sin, which no device libm reproduces bit for bit either; decisions
+// within FRAGILE_EPS of a threshold are therefore flagged GBP_F_FRAGILE and
+// re-decided on the host with glibc (gbp_host_check.cpp):
 //  * yaw: cos/sin(atan2(dy, dx)) = dx/|v|, dy/|v| (<= 2 ulp).  Below 1e-150
 //    the components are first scaled by 2^600 (exact) so dx^2 + dy^2 cannot
 //    underflow; |v| = 0 takes atan2's signed-zero results, atan2(+-0, +0) =
@@ -537,18 +451,13 @@ __device__ __forceinline__ double probe_height_bf(const TerrainView<ZT> &T, cons
   const double x1 = coord<CM, 0>(T, cx), x2 = coord<CM, 0>(T, cx + 1);
   const double y1 = coord<CM, 1>(T, cy), y2 = coord<CM, 1>(T, cy + 1);
   ok = br || nanxy;
-#ifndef GBP_EXPERIMENT_NO_FRAGILE
   near = br && !nanxy &&
          (fabs(x - x1) < eps || fabs(x2 - x) < eps || fabs(y - y1) < eps || fabs(y2 - y) < eps);
-#else
-  near = false;
-#endif
   const double h = bilinear((double)p.q[0], (double)p.q[1], (double)p.q[2], (double)p.q[3], x1, x2,
                             y1, y2, x, y, T.rcp_seed);
   return nanxy ? __builtin_nan("") : h;
 }
 
-#ifndef GBP_BRANCHY
 // isValidState as ONE straight-line pass: every lookup, height and test is
 // evaluated for every lane, and the reference's sequence of early returns is
 // replayed as a predicate `alive` (a test only counts, sets flags or rejects
@@ -578,15 +487,8 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
   // (2) bounds + |pitch| :568-571, (3) horizontal speed :574
   bool alive = r == 0 && !(outside || (fabs(s[6]) >= P_MAX)) && !(speed > V_MAX);
   // (4) rotation :578-594
-#ifdef GBP_EXPERIMENT_NO_TRIG
-  const double yaw = s[4] * s[3];
-  const double cy = yaw * 0.5, sy = yaw * 0.25;
-  const double pitch = s[6];
-  const double cp = pitch * 0.5, sp = pitch * 0.25;
-#else
   double cy, sy, cp, sp;
   rotation_trig_nolibm(s[3], s[4], speed, s[6], cy, sy, cp, sp);
-#endif
   const double R_11 = cy * cp, R_12 = -sy, R_13 = cy * sp;
   const double R_21 = sy * cp, R_22 = cy, R_23 = sy * sp;
   const double R_31 = -sp, R_32 = 0, R_33 = cp;
@@ -650,120 +552,6 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
   acc.flags |= fl;
   return alive;
 }
-#else
-template <class ZT, int CM = 0>
-__device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int phase, Acc &acc) {
-  // (reads the coordinate vectors whatever CM is: they stay valid in every mode)
-  if (acc.V >= GBP_MAX_SAMPLES) {  // engine guard: the reference loop would not terminate
-    acc.flags |= GBP_F_LIMIT;
-    return false;
-  }
-  acc.V++;
-  // centre cell fetched first: its latency hides under the checks and trig below
-  Probe<ZT> pc;
-  probe(T, s[0], s[1], pc);
-  // (1) heightIsNan(centre) :564
-  const int r = probe_nan(pc);
-  if (r < 0) {  // x or y >= the last coordinate: rejected by (2) unless exactly equal
-    const bool in_closed = !(s[0] < T.x0 || s[0] > T.xN || s[1] < T.y0 || s[1] > T.yN);
-    if (in_closed) acc.flags |= GBP_F_OOD;
-    return false;
-  }
-  if (r) {
-    acc.flags |= GBP_F_NAN;
-    return false;
-  }
-  // (2) bounds + |pitch| :568-571
-  if ((s[0] < T.x0) || (s[0] > T.xN) || (s[1] < T.y0) || (s[1] > T.yN) || (fabs(s[6]) >= P_MAX))
-    return false;
-  // (3) horizontal speed :574
-  const double speed = sqrt(s[3] * s[3] + s[4] * s[4]);
-  if (speed > V_MAX) return false;
-  // (4) rotation :578-594
-#ifdef GBP_EXPERIMENT_NO_TRIG
-  const double yaw = s[4] * s[3];
-  const double cy = yaw * 0.5, sy = yaw * 0.25;
-  const double pitch = s[6];
-  const double cp = pitch * 0.5, sp = pitch * 0.25;
-#else
-  double cy, sy, cp, sp;
-  rotation_trig(s[3], s[4], speed, s[6], cy, sy, cp, sp);
-#endif
-  const double R_11 = cy * cp, R_12 = -sy, R_13 = cy * sp;
-  const double R_21 = sy * cp, R_22 = cy, R_23 = sy * sp;
-  const double R_31 = -sp, R_32 = 0, R_33 = cp;
-  const double z_body = -ROBOT_H;
-  // all nine remaining lookups of this state are fetched before any is tested
-  Probe<ZT> pl[4], pk[4], pu;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const double x_body = (k < 2) ? -0.5 * ROBOT_L : 0.5 * ROBOT_L;
-    const double y_body = (k & 1) ? 0.5 * ROBOT_W : -0.5 * ROBOT_W;
-    const double x_leg = s[0] + R_11 * x_body + R_12 * y_body;
-    const double y_leg = s[1] + R_21 * x_body + R_22 * y_body;
-    probe(T, x_leg, y_leg, pl[k]);
-    probe(T, x_leg + R_13 * z_body, y_leg + R_23 * z_body, pk[k]);
-  }
-  const double ux = s[0] + R_13 * z_body, uy = s[1] + R_23 * z_body;
-  probe(T, ux, uy, pu);
-  // (5) four corners :601-627, x_body outer, y_body inner, in reference order
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const double x_body = (k < 2) ? -0.5 * ROBOT_L : 0.5 * ROBOT_L;
-    const double y_body = (k & 1) ? 0.5 * ROBOT_W : -0.5 * ROBOT_W;
-    const double x_leg = s[0] + R_11 * x_body + R_12 * y_body;
-    const double y_leg = s[1] + R_21 * x_body + R_22 * y_body;
-    const double z_leg = s[2] + R_31 * x_body + R_32 * y_body;
-    const double x_corner = x_leg + R_13 * z_body;
-    const double y_corner = y_leg + R_23 * z_body;
-    const double z_corner = z_leg + R_33 * z_body;
-    const int rl = probe_nan(pl[k]);  // heightIsNan(leg) :614
-    if (rl < 0) {
-      acc.flags |= GBP_F_OOD;
-      return false;
-    }
-    if (rl) {
-      acc.flags |= GBP_F_NAN;
-      return false;
-    }
-    acc.G += 2;  // both heights computed before the test :618-619
-    double gl, gc;
-    bool near = false;
-    const bool okl = probe_height(T, pl[k], x_leg, y_leg, gl, near);
-    if (near) acc.flags |= GBP_F_FRAGILE;
-    if (!okl) {
-      acc.flags |= GBP_F_OOD;
-      return false;
-    }
-    const bool okc = probe_height(T, pk[k], x_corner, y_corner, gc, near);
-    if (near) acc.flags |= GBP_F_FRAGILE;
-    if (!okc) {
-      acc.flags |= GBP_F_OOD;
-      return false;
-    }
-    const double leg_height = z_leg - gl;
-    const double corner_height = z_corner - gc;
-    if (fabs(corner_height - H_MIN) < FRAGILE_EPS ||
-        (phase == GBP_STANCE && fabs(leg_height - H_MAX) < FRAGILE_EPS))
-      acc.flags |= GBP_F_FRAGILE;
-    if ((corner_height < H_MIN) || ((phase == GBP_STANCE) && (leg_height > H_MAX))) return false;
-  }
-  // (6) underside centre :630-632
-  acc.G++;
-  double gu;
-  bool near = false;
-  const bool oku = probe_height(T, pu, ux, uy, gu, near);
-  if (near) acc.flags |= GBP_F_FRAGILE;
-  if (!oku) {
-    acc.flags |= GBP_F_OOD;
-    return false;
-  }
-  const double height = (s[2] + R_33 * z_body) - gu;
-  if (fabs(height - H_MIN) < FRAGILE_EPS) acc.flags |= GBP_F_FRAGILE;
-  if (height < H_MIN) return false;
-  return true;
-}
-#endif  // GBP_BRANCHY
 
 __device__ __forceinline__ uint32_t stage_bits(uint32_t k) { return k << GBP_F_STAGE_SHIFT; }
 

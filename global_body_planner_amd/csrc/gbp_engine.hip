@@ -467,81 +467,28 @@ __device__ __forceinline__ bool step_lane(const TerrainView<ZT> &T, Lane &L) {
   return transition<ADAPTIVE>(L, ok);
 }
 
-#ifdef GBP_DIAG_UTIL
-__device__ unsigned long long gbp_diag[4];
-// per-wave timeline of the last launch: begin, end (wall_clock64), steps, CU id
-__device__ unsigned long long gbp_diag_wave[16384][4];
-extern "C" int gbp_diag_waves(unsigned long long *out, int n) {
-  if (n > 16384) n = 16384;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gbp_diag_wave), sizeof(unsigned long long) * 4 * n) !=
-      hipSuccess)
-    return -4;
-  return 0;
-}
-extern "C" int gbp_diag_read(unsigned long long *out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gbp_diag), sizeof(unsigned long long) * 4) != hipSuccess)
-    return -4;
-  if (reset) {
-    unsigned long long z[4] = {0, 0, 0, 0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(gbp_diag), z, sizeof z) != hipSuccess) return -4;
-  }
-  return 0;
-}
-#endif
-
 template <class ZT, bool ADAPTIVE, int W, int CM>
-// up to 512 threads: one 8-wave workgroup per CU at W = 2 lets sched 3's LDS
-// queue balance all the CU's waves, including the two that share a SIMD
 __global__ __launch_bounds__(512, W) void k_validate_persistent(
     TerrainView<ZT> T0, int n, const double *__restrict__ S, const double *__restrict__ A,
     const uint8_t *__restrict__ dir, int dir_all, uint8_t *__restrict__ valid,
     double *__restrict__ s_new, double *__restrict__ t_new, uint32_t *__restrict__ flags,
-    uint32_t *__restrict__ counts, unsigned int *__restrict__ head, int sched, int chunk,
-    int helpers, int prefix, int xcd_map) {
+    uint32_t *__restrict__ counts, const int *__restrict__ n_dev, int helpers, int xcd_map) {
   const TerrainView<ZT> T = CM == 1 ? stage_coords(T0, gbp_smem) : T0;
+  if (n_dev) n = *n_dev;  // batch size produced on the device (planner loop)
   const int lane = threadIdx.x & (WAVE - 1);
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
   double *const SA = gbp_smem + (CM == 1 ? (T0.nx + T0.ny + 1) & ~1 : 0);  // attempt rows
   double *const wave_rows = SA + (size_t)(threadIdx.x & ~(WAVE - 1)) * SA_ROW;
-#ifdef GBP_DIAG_UTIL
-  const unsigned long long t_begin = wall_clock64();
-  unsigned long long n_steps = 0, n_busy = 0;
-#endif
   Lane L;
   L.s = SA + (size_t)threadIdx.x * SA_ROW;
   L.a = L.s + 8;
   L.stage = ST_IDLE;
-  bool exhausted = false;
-  // work source (wave-uniform): [cur, end) is the range this wave hands out
-  // to its idle lanes.  sched 1: a fixed per-wave slice, no atomics at all;
-  // sched 0 / 2: slices of `chunk` (0 = exactly the lanes that need one)
-  // dequeued from one device-scope counter (MI355X_MICROARCH.md 'dequeue');
-  // sched 3: a fixed slice per WORKGROUP, dealt to its waves on demand from
-  // an LDS counter (an LDS atomic costs ~100 cycles, a device atomic ~1 us), so
-  // the waves of a workgroup even out their unequal sample totals.
-  // sched 4: a static per-wave prefix (prefix/1024 of the batch), then chunks
-  // of the rest dequeued from 8 heads, one per XCD (MI355X_MICROARCH.md
-  // 'dequeue': one head saturates near 88 dequeues/us), a wave starting at its
-  // workgroup's XCD shard and moving on to the next shard when one runs dry.
-  // The XCDs of one launch run at visibly different speeds (tools/timeline.py),
-  // so fixed slices leave the fast ones idle for the kernel's last third.
-  __shared__ unsigned int wg_head;
-  unsigned int cur = 0, end = 0, wg_begin = 0, wg_end = 0;
-  unsigned int dyn0 = 0;  // sched 4: first dynamically dealt attempt
-  int shard = 0, shards_left = 8;
-  // sched 4 keeps one dequeue in flight: the next chunk is claimed when the
-  // current one starts, so a refill never waits on a device-scope atomic
-  unsigned int rsv_val = 0;
-  int rsv_leader = -1;
-  if (sched == 4) {
-    const unsigned int waves = gridDim.x * (blockDim.x / WAVE);
-    const unsigned int wid = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
-    const unsigned int per = (unsigned int)(((unsigned long long)n * (unsigned)prefix / 1024u) / waves);
-    cur = per * wid;
-    end = cur + per;
-    dyn0 = per * waves;
-    shard = blockIdx.x & 7;
-  } else if (sched == 1) {
+  // work source: a fixed contiguous slice [cur, end) per wave, handed out to
+  // the wave's idle lanes in order (no atomics).  Dynamic dequeues (one or
+  // eight device-scope heads, chunked, per-workgroup LDS queues) were
+  // measured slower and removed.
+  unsigned int cur, end;
+  {
     const unsigned int waves = gridDim.x * (blockDim.x / WAVE);
     // xcd_map: workgroup b runs on XCD b % 8 (round-robin dispatch); numbering
     // the slices XCD-major gives each XCD one contiguous eighth of the batch,
@@ -552,76 +499,21 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
     const unsigned int wid = wg * (blockDim.x / WAVE) + threadIdx.x / WAVE;
     cur = (unsigned int)(((unsigned long long)n * wid) / waves);
     end = (unsigned int)(((unsigned long long)n * (wid + 1)) / waves);
-  } else if (sched == 3) {
-    wg_begin = (unsigned int)(((unsigned long long)n * blockIdx.x) / gridDim.x);
-    wg_end = (unsigned int)(((unsigned long long)n * (blockIdx.x + 1)) / gridDim.x);
-    if (threadIdx.x == 0) wg_head = 0;
-    __syncthreads();
   }
   for (;;) {
-    const bool need = (L.stage == ST_IDLE) && !exhausted;
+    const bool need = L.stage == ST_IDLE;
     unsigned long long m = __ballot(need);
-    while (m) {
-      if (cur >= end) {
-        unsigned int base = 0xFFFFFFFFu;
-        const unsigned int grab = chunk > 0 ? (unsigned int)chunk : (unsigned int)__popcll(m);
-        const int leader = __ffsll((long long)m) - 1;
-        unsigned int lim = (unsigned int)n;
-        if (sched == 4) {
-          const unsigned long long rest = (unsigned long long)((unsigned int)n - dyn0);
-          while (shards_left > 0) {  // wave-uniform
-            const unsigned int lo = dyn0 + (unsigned int)(rest * (unsigned)shard / 8u);
-            const unsigned int hi = dyn0 + (unsigned int)(rest * (unsigned)(shard + 1) / 8u);
-            unsigned int b = 0xFFFFFFFFu;
-            if (rsv_leader >= 0) {  // the chunk claimed one refill ago
-              b = lo + __shfl(rsv_val, rsv_leader);
-              rsv_leader = -1;
-            } else {
-              if (lane == leader) b = lo + atomicAdd(head + 32 * shard, grab);
-              b = __shfl(b, leader);
-            }
-            if (b < hi) {
-              base = b;
-              lim = hi;
-              break;
-            }
-            shard = (shard + 1) & 7;
-            shards_left--;
-          }
-          if (base != 0xFFFFFFFFu) {  // claim the next chunk of this shard now
-            if (lane == leader) rsv_val = atomicAdd(head + 32 * shard, grab);
-            rsv_leader = leader;
-          }
-        } else if (sched == 3) {
-          if (lane == leader) base = wg_begin + atomicAdd(&wg_head, grab);
-          base = __shfl(base, leader);
-          if (base >= wg_end) base = 0xFFFFFFFFu;
-        } else if (sched != 1) {
-          if (lane == leader) base = atomicAdd(head, grab);
-          base = __shfl(base, leader);
-        }
-        if (sched == 1 || base >= (unsigned int)n) {
-          if (need) exhausted = true;
-          break;
-        }
-        cur = base;
-        end = min(base + grab, sched == 3 ? wg_end : lim);
-      }
-    const unsigned int take = min(end - cur, (unsigned int)__popcll(m));
+    if (m && cur < end) {
+      const unsigned int take = min(end - cur, (unsigned int)__popcll(m));
       const unsigned int rank = (unsigned int)__popcll(m & lt_mask);
-      const bool mine = ((m >> lane) & 1ull) && rank < take;
+      const bool mine = need && rank < take;
       if (mine) {
         const unsigned int i = cur + rank;
         L.idx = (int)i;
-#ifdef GBP_EXPERIMENT_HOT_INPUTS  // diagnostic timing build only: rows from an L2-hot subset
-        const unsigned int ii = i & 4095u;
-#else
-        const unsigned int ii = i;
-#endif
 #pragma unroll
-        for (int k = 0; k < 8; k++) L.s[k] = S[8 * (size_t)ii + k];
+        for (int k = 0; k < 8; k++) L.s[k] = S[8 * (size_t)i + k];
 #pragma unroll
-        for (int k = 0; k < 10; k++) L.a[k] = A[10 * (size_t)ii + k];
+        for (int k = 0; k < 10; k++) L.a[k] = A[10 * (size_t)i + k];
         L.f = 0;
         L.acc = Acc{0, 0, 0};
         L.snew_kind = SN_NONE;
@@ -630,7 +522,6 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
         enter_stage(L, d == GBP_FORWARD ? ST_FWD_STANCE : ST_REV_FLIGHT);
       }
       cur += take;
-      m &= ~__ballot(mine);
     }
     const unsigned long long act = __ballot(L.stage != ST_IDLE);
     if (!act) break;
@@ -665,13 +556,6 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
         t_eval = t;
       }
     }
-#ifdef GBP_DIAG_UTIL  // diagnostic build: lane utilisation of the sample steps
-    {
-      const unsigned long long busy = __ballot(has);
-      n_busy += (unsigned long long)__popcll(busy);  // one atomic per wave at the end:
-      n_steps++;                                      // per-step atomics distort timing
-    }
-#endif
     Acc acc_s{0, vbase + (uint32_t)slot, 0};
     bool ok = false;
     if (has) {
@@ -720,11 +604,7 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
         if (L.snew_kind != SN_NONE) f |= GBP_F_SNEW_SET;
         if (L.tnew_set) f |= GBP_F_TNEW_SET;
         if (valid) valid[i] = (f & GBP_F_VALID) ? 1 : 0;
-#ifdef GBP_EXPERIMENT_NO_SNEW  // diagnostic timing build only (s_new not written)
-        if (false) {
-#else
         if (s_new && L.snew_kind != SN_NONE) {
-#endif
           double o[8];
           double sv[8], av[10];
 #pragma unroll
@@ -748,23 +628,6 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
       }
     }
   }
-#ifdef GBP_DIAG_UTIL
-  if (lane == 0) {
-    const unsigned long long t_end = wall_clock64();
-    const unsigned long long dt = t_end - t_begin;
-    atomicAdd(&gbp_diag[0], n_steps);
-    atomicAdd(&gbp_diag[1], n_busy);
-    atomicAdd(&gbp_diag[2], dt);
-    atomicMax(&gbp_diag[3], dt);
-    const unsigned int wid = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
-    if (wid < 16384) {
-      gbp_diag_wave[wid][0] = t_begin;
-      gbp_diag_wave[wid][1] = t_end;
-      gbp_diag_wave[wid][2] = n_steps;
-      gbp_diag_wave[wid][3] = (unsigned long long)__smid();
-    }
-  }
-#endif
 }
 
 // ============================================================================
@@ -1037,28 +900,28 @@ struct gbp_terrain {
   int num_cus = 256;
   int64_t opt_kernel = GBP_KERNEL_PERSISTENT;
   int64_t opt_block = 256;
-  int64_t opt_grid_per_cu = 8;
   int64_t opt_waves = 2;            // register budget of the validate kernels (waves/SIMD)
   int64_t opt_lds_coords = 1;       // stage the coordinate vectors in LDS when they fit
-  int64_t opt_sched = 1;            // persistent work source: 0 atomic, 1 static, 2 chunked
-  int64_t opt_chunk = 0;            // dequeue granularity for sched 0/2 (0 = per need)
   int64_t opt_helpers = 1;          // idle lanes of a drained wave evaluate owners' next samples
-  int64_t opt_oversub = 1;          // fixed-grid schedules: workgroups = oversub x resident
-  int64_t opt_prefix = 512;         // sched 4: statically dealt share of a batch (1/1024)
   int64_t opt_affine = 1;           // compute coordinates when the affine form is exact
   int64_t opt_fast_rcp = 1;         // cell-area reciprocal by verified Newton steps
   double rcp_seed = 0;              // verified_rcp_seed (0: every spacing pair not exact)
-  int64_t opt_xcd_map = 0;          // sched 1: slices numbered XCD-major
+  int64_t opt_xcd_map = 0;          // persistent kernel: slices numbered XCD-major
   int affine = 0;                   // host-verified affine coordinates (both axes)
   int bx = 0, by = 0;
   double ax = 0, hx = 0, ay = 0, hy = 0;
-  unsigned int *d_head = nullptr;   // persistent-kernel work counter (zeroed per launch)
   size_t lds_max = 65536;           // LDS bytes a workgroup may use
   hipStream_t host_stream = nullptr;
   void *ws = nullptr;               // grow-only device workspace
   size_t ws_bytes = 0;
-  void *ws2 = nullptr;              // second workspace (extend candidates)
-  size_t ws2_bytes = 0;
+  // extend-candidate workspaces, one per stream: _dev calls on one handle may
+  // run concurrently on different streams without sharing scratch
+  struct StreamWs {
+    hipStream_t stream;
+    void *ptr;
+    size_t bytes;
+  };
+  std::vector<StreamWs> cand_ws;
 };
 
 namespace {
@@ -1149,7 +1012,6 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
   const size_t coords = CM == 1 ? stage_bytes(t->nx, t->ny) : 0;
   const size_t rows = sizeof(double) * SA_ROW * (size_t)block;  // persistent kernel only
   const int64_t chunk = (int64_t)1 << 30;
-  const int64_t want = (int64_t)t->num_cus * t->opt_grid_per_cu;
   for (int64_t off = 0; off < n; off += chunk) {
     const int64_t m = std::min<int64_t>(n - off, chunk);
     const uint8_t *d = dir ? dir + off : nullptr;
@@ -1165,23 +1027,13 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
       hipLaunchKernelGGL((k_validate_direct<ZT, AD, 1, CM == 2 ? 0 : CM>), dim3(g), dim3(db), coords, st, T, m,
                          s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn, flags + off, c);
     } else {
-      // persistent: grid sized to residency; the work counter is zeroed per launch
+      // persistent: one workgroup per resident slot (W waves per SIMD)
       const int64_t resident = (int64_t)t->num_cus * std::max<int64_t>(1, W * 256 / block);
-      // fixed-grid schedules launch `oversub` x the resident workgroups: a
-      // workgroup that finishes its slice early frees its slot to one that has
-      // not started (the hardware dispatcher's work queue), so a wave's
-      // ragged end overlaps another's full start
-      const bool fixed_grid = t->opt_sched == 1 || t->opt_sched >= 3;
-      const int64_t g = std::max<int64_t>(
-          1, std::min<int64_t>(fixed_grid ? resident * t->opt_oversub : want, (m + block - 1) / block));
-      if (t->opt_sched == 0 || t->opt_sched == 2)
-        HIPCHK(hipMemsetAsync(t->d_head, 0, sizeof(unsigned int), st));
-      if (t->opt_sched == 4) HIPCHK(hipMemsetAsync(t->d_head, 0, 8 * 128, st));
+      const int64_t g = std::max<int64_t>(1, std::min<int64_t>(resident, (m + block - 1) / block));
       hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, CM>), dim3((unsigned)g), dim3(block),
                          coords + rows, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
-                         flags + off, c, t->d_head, (int)t->opt_sched,
-                         (int)(t->opt_sched == 4 && t->opt_chunk == 0 ? 32 : t->opt_chunk),
-                         (int)t->opt_helpers, (int)t->opt_prefix, (int)t->opt_xcd_map);
+                         flags + off, c, (const int *)nullptr, (int)t->opt_helpers,
+                         (int)t->opt_xcd_map);
     }
     HIPCHK(hipGetLastError());
   }
@@ -1432,23 +1284,12 @@ int gbp_terrain_create(int device, int nx, int ny, const double *x, const double
     return fail(GBP_E_HIP);
   if (hipMemcpy(t->d_y, y, sizeof(double) * ny, hipMemcpyHostToDevice) != hipSuccess)
     return fail(GBP_E_HIP);
-  // heights as x-pairs (gbp_device.h TerrainView); rows / quads: diagnostic builds
-#if defined(GBP_ZROWS)
-  const size_t zcount = cells;
-  auto zsrc = [&](size_t k) { return z[k]; };
-#elif defined(GBP_ZQUADS)
-  const size_t qx = (size_t)nx - 1, qy = (size_t)ny - 1, zcount = 4 * qx * qy;
-  auto zsrc = [&](size_t k) {
-    const size_t c = k >> 2, ix = c / qy, iy = c % qy, corner = k & 3;
-    return z[(ix + (corner >> 1)) * (size_t)ny + iy + (corner & 1)];
-  };
-#else
+  // heights as x-pairs (gbp_device.h TerrainView)
   const size_t zcount = 2 * ((size_t)nx - 1) * (size_t)ny;
   auto zsrc = [&](size_t k) {
     const size_t c = k >> 1, ix = c / (size_t)ny, iy = c % (size_t)ny;
     return z[(ix + (k & 1)) * (size_t)ny + iy];
   };
-#endif
   if (storage == GBP_STORAGE_F32) {
     std::vector<float> zf(zcount);
     for (size_t i = 0; i < zcount; i++) zf[i] = (float)zsrc(i);
@@ -1472,7 +1313,6 @@ int gbp_terrain_create(int device, int nx, int ny, const double *x, const double
         return fail(GBP_E_HIP);
     }
   }
-  if (hipMalloc((void **)&t->d_head, 8 * 128) != hipSuccess) return fail(GBP_E_ALLOC);
   {
     int lm = 0;
     if (hipDeviceGetAttribute(&lm, hipDeviceAttributeMaxSharedMemoryPerBlock, device) ==
@@ -1490,9 +1330,12 @@ int gbp_terrain_destroy(gbp_terrain *t) {
   if (!t) return GBP_E_BAD_HANDLE;
   DeviceGuard g(t->device);
   if (t->host_stream) (void)hipStreamSynchronize(t->host_stream);
-  void *ptrs[] = {t->d_x, t->d_y, t->d_z, t->d_dx, t->d_dy, t->d_dz, t->d_head, t->ws, t->ws2};
+  (void)hipDeviceSynchronize();  // cand_ws may be in use on any caller stream
+  void *ptrs[] = {t->d_x, t->d_y, t->d_z, t->d_dx, t->d_dy, t->d_dz, t->ws};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
+  for (auto &w : t->cand_ws)
+    if (w.ptr) (void)hipFree(w.ptr);
   if (t->host_stream) (void)hipStreamDestroy(t->host_stream);
   delete t;
   return GBP_OK;
@@ -1520,10 +1363,6 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
       if (value < 64 || value > 512 || value % 64) return GBP_E_INVALID_ARG;
       t->opt_block = value;
       return GBP_OK;
-    case GBP_OPT_GRID_PER_CU:
-      if (value < 1 || value > 64) return GBP_E_INVALID_ARG;
-      t->opt_grid_per_cu = value;
-      return GBP_OK;
     case GBP_OPT_WAVES:
       if (value < 1 || value > 4) return GBP_E_INVALID_ARG;
       t->opt_waves = value;
@@ -1531,27 +1370,11 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
     case GBP_OPT_LDS_COORDS:
       t->opt_lds_coords = value ? 1 : 0;
       return GBP_OK;
-    case GBP_OPT_SCHED:
-      if (value < 0 || value > 4) return GBP_E_INVALID_ARG;
-      t->opt_sched = value;
-      return GBP_OK;
-    case GBP_OPT_CHUNK:
-      if (value < 0 || value > 65536) return GBP_E_INVALID_ARG;
-      t->opt_chunk = value;
-      return GBP_OK;
     case GBP_OPT_HELPERS:
       t->opt_helpers = value ? 1 : 0;
       return GBP_OK;
     case GBP_OPT_AFFINE_COORDS:
       t->opt_affine = value ? 1 : 0;
-      return GBP_OK;
-    case GBP_OPT_PREFIX:
-      if (value < 0 || value > 1024) return GBP_E_INVALID_ARG;
-      t->opt_prefix = value;
-      return GBP_OK;
-    case GBP_OPT_OVERSUB:
-      if (value < 1 || value > 64) return GBP_E_INVALID_ARG;
-      t->opt_oversub = value;
       return GBP_OK;
     case GBP_OPT_XCD_MAP:
       t->opt_xcd_map = value ? 1 : 0;
@@ -1570,15 +1393,10 @@ int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value) {
   switch (key) {
     case GBP_OPT_KERNEL: *value = t->opt_kernel; return GBP_OK;
     case GBP_OPT_BLOCK: *value = t->opt_block; return GBP_OK;
-    case GBP_OPT_GRID_PER_CU: *value = t->opt_grid_per_cu; return GBP_OK;
     case GBP_OPT_WAVES: *value = t->opt_waves; return GBP_OK;
     case GBP_OPT_LDS_COORDS: *value = t->opt_lds_coords; return GBP_OK;
-    case GBP_OPT_SCHED: *value = t->opt_sched; return GBP_OK;
-    case GBP_OPT_CHUNK: *value = t->opt_chunk; return GBP_OK;
     case GBP_OPT_HELPERS: *value = t->opt_helpers; return GBP_OK;
     case GBP_OPT_AFFINE_COORDS: *value = t->opt_affine; return GBP_OK;
-    case GBP_OPT_PREFIX: *value = t->opt_prefix; return GBP_OK;
-    case GBP_OPT_OVERSUB: *value = t->opt_oversub; return GBP_OK;
     case GBP_OPT_XCD_MAP: *value = t->opt_xcd_map; return GBP_OK;
     case GBP_OPT_FAST_RCP: *value = t->opt_fast_rcp ? (t->rcp_seed != 0.0 ? 1 : 0) : 0; return GBP_OK;
     case GBP_OPT_COORD_MODE: *value = coord_mode(t, t->opt_lds_coords != 0); return GBP_OK;
@@ -1715,9 +1533,19 @@ int gbp_extend_batch_dev(gbp_terrain *t, int64_t n, const double *s_near, const 
   const int64_t m = n * GBP_NUM_GEN_STATES;
   // candidate workspace: s (8) + a (10) + s_new (8) doubles, flags + counts u32, dir u8
   const size_t need = (size_t)m * (26 * sizeof(double) + 2 * sizeof(uint32_t) + 1) + 256;
-  int rc = ensure_ws(t, &t->ws2, &t->ws2_bytes, need);
+  gbp_terrain::StreamWs *w = nullptr;
+  for (auto &e : t->cand_ws)
+    if (e.stream == st) w = &e;
+  if (!w) {
+    t->cand_ws.push_back({st, nullptr, 0});
+    w = &t->cand_ws.back();
+  }
+  // a grown workspace may still be read by this stream's earlier launches:
+  // ensure_ws frees the old one only after the stream has drained it
+  if (w->bytes < need) HIPCHK(hipStreamSynchronize(st));
+  int rc = ensure_ws(t, &w->ptr, &w->bytes, need);
   if (rc) return rc;
-  char *p = (char *)t->ws2;
+  char *p = (char *)w->ptr;
   double *cs = (double *)p; p += (size_t)m * 8 * sizeof(double);
   double *ca = (double *)p; p += (size_t)m * 10 * sizeof(double);
   double *csn = (double *)p; p += (size_t)m * 8 * sizeof(double);

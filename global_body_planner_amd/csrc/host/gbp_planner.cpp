@@ -801,7 +801,7 @@ void RRTConnectClass::attemptConnectBatch(const std::vector<State> &s_existing,
   std::vector<State> s = s0;
   std::vector<int> open(n);
   std::iota(open.begin(), open.end(), 0);
-  for (int depth = 0; !open.empty() && depth <= max_depth; depth++) {  // 64: oracle's guard
+  for (int depth = 0; !open.empty() && depth <= max_depth; depth++) {
     std::vector<int> chk_idx;
     std::vector<State> cs;
     std::vector<Action> ca;
@@ -841,6 +841,9 @@ void RRTConnectClass::attemptConnectBatch(const std::vector<State> &s_existing,
       }
     }
   }
+  // still open after level max_depth: TRAPPED by the engine's cap (gbp.h
+  // GBP_CONNECT_MAX_DEPTH; with max_depth 0 only REACHED is asked for)
+  if (stats && max_depth > 0) stats->depth_capped += (int64_t)open.size();
 }
 
 int RRTConnectClass::connect(PlannerClass &T, State s, FastTerrainMap &terrain, int direction) {
@@ -903,16 +906,14 @@ void RRTConnectClass::postProcessPath(std::vector<State> &state_sequence,
       const double dl = poseDistance(s, s_next), dy = stateYawDistance(s, s_next);
       path_length_ += dl;
       path_yaw_ += dy;
-      path_cost_ += cost_add_yaw_flag_ ? dl * cost_add_yaw_length_weight_ + dy * cost_add_yaw_yaw_weight_
-                                       : dl;
+      path_cost_ += weightedCost(dl, dy);
       s = s_next;
     } else {
       // the reference adds to path_cost_ but not path_length_ here (:210-215)
       new_states.push_back(old_state);
       new_actions.push_back(old_action);
       const double dl = poseDistance(s, old_state), dy = stateYawDistance(s, old_state);
-      path_cost_ += cost_add_yaw_flag_ ? dl * cost_add_yaw_length_weight_ + dy * cost_add_yaw_yaw_weight_
-                                       : dl;
+      path_cost_ += weightedCost(dl, dy);
       s = old_state;
     }
   }
@@ -954,9 +955,7 @@ void RRTConnectClass::runRRTConnect(PlannerClass &Ta, PlannerClass &Tb,
   }
   path_length_ = Ta.getGValue(Ta.getNumVertices() - 1) + Tb.getGValue(Tb.getNumVertices() - 1);
   path_yaw_ = Ta.getYValue(Ta.getNumVertices() - 1) + Tb.getYValue(Tb.getNumVertices() - 1);
-  path_cost_ = cost_add_yaw_flag_ ? path_length_ * cost_add_yaw_length_weight_ +
-                                        path_yaw_ * cost_add_yaw_yaw_weight_
-                                  : path_length_;
+  path_cost_ = weightedCost(path_length_, path_yaw_);
 }
 
 void RRTConnectClass::buildRRTConnect(FastTerrainMap &terrain, State s_start, State s_goal,
@@ -1082,7 +1081,8 @@ void RRTConnectClass::extendBatch(PlannerClass &T, FastTerrainMap &terrain, int 
   extend_counter_ += n;
   if (stats) {
     stats->extends += n;
-    stats->attempts_checked += 6 * n;
+    // newConfig stops at the first valid candidate (rrt.cpp:36-50)
+    for (int64_t i = 0; i < n; i++) stats->attempts_checked += chosen[i] >= 0 ? chosen[i] + 1 : 6;
   }
   for (int64_t i = 0; i < n; i++) {
     if (res[i] == GBP_TRAPPED) continue;
@@ -1198,7 +1198,7 @@ bool RRTConnectClass::buildRRTConnectBatched(FastTerrainMap &terrain, State s_st
   action_sequence.insert(action_sequence.end(), action_sequence_b.begin(), action_sequence_b.end());
   path_length_ = Ta.getGValue(ia) + Tb.getGValue(ib);
   path_yaw_ = Ta.getYValue(ia) + Tb.getYValue(ib);
-  path_cost_ = path_length_;
+  path_cost_ = weightedCost(path_length_, path_yaw_);  // rrt_connect.cpp:304-313
   path_duration_ = 0;
   for (const Action &a : action_sequence) path_duration_ += a[6] + a[7];
   return true;
@@ -1577,7 +1577,7 @@ bool RRTStarConnectClass::buildRRTStarConnectBatched(FastTerrainMap &terrain, St
   getStateAndActionSequences(Ta, Tb, best_a, best_b, state_sequence, action_sequence);
   path_length_ = Ta.getGValue(best_a) + Tb.getGValue(best_b);
   path_yaw_ = Ta.getYValue(best_a) + Tb.getYValue(best_b);
-  path_cost_ = path_length_;
+  path_cost_ = weightedCost(path_length_, path_yaw_);
   path_duration_ = 0;
   for (const Action &a : action_sequence) path_duration_ += a[6] + a[7];
   return true;
@@ -1639,7 +1639,7 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
       double len = 0;
       for (size_t i = 1; i < states.size(); i++) len += planning_utils::poseDistance(states[i - 1], states[i]);
       r->path_length = len;
-      r->path_cost = p->algorithm == 1 ? planner.bestCost() : (p->algorithm == 2 ? planner.pathCost() : len);
+      r->path_cost = p->algorithm == 1 ? planner.bestCost() : planner.pathCost();
       double dur = 0;
       for (const Action &a : actions) dur += a[6] + a[7];
       r->path_duration = dur;

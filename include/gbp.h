@@ -54,6 +54,12 @@ extern "C" {
 #define GBP_STATE_DIM       8
 #define GBP_ACTION_DIM     10
 #define GBP_NUM_GEN_STATES  6   /* planning_utils.h:45 */
+/* attemptConnect (rrt_connect.cpp:20-84) recurses without a bound; the
+ * engine stops a connection after this many levels and reports it TRAPPED
+ * (counted as depth_capped).  Each level's stance time shrinks by >= one
+ * KINEMATICS_RES step except in degenerate reverse cases, so a cap of 1024
+ * covers t_s up to 51 s (a 38 m connect at V_NOM) without truncation.      */
+#define GBP_CONNECT_MAX_DEPTH 1024
 
 /* ---- per-attempt flag word (output of the validate/extend entry points) -- */
 #define GBP_F_VALID      (1u << 0)  /* the pair check returned true                      */
@@ -67,9 +73,13 @@ extern "C" {
 #define GBP_F_FRAGILE    (1u << 5)  /* a trig-dependent comparison was within 1e-12 of its
                                        threshold (decision could differ across libm builds) */
 #define GBP_F_LIMIT      (1u << 6)  /* the pair needed more than GBP_MAX_SAMPLES state checks
-                                       (e.g. t_s = inf: the reference never terminates); the
-                                       check is stopped and reported invalid                 */
-#define GBP_MAX_SAMPLES  4096u
+                                       (t_s + t_f > ~350 s, e.g. a connect longer than ~262 m at
+                                       V_NOM, or t_s = inf where the reference never
+                                       terminates); the check is stopped and reported invalid.
+                                       The cap keeps G = 9 V below the 16-bit counter field. */
+#define GBP_F_RESOLVED   (1u << 7)  /* a FRAGILE attempt whose outputs were re-decided on the
+                                       host with glibc trig (gbp_resolve_fragile_host)        */
+#define GBP_MAX_SAMPLES  7000u
 #define GBP_F_STAGE_SHIFT 8u        /* bits 8..11: stage in which the check ended          */
 #define GBP_F_STAGE_MASK  (0xFu << GBP_F_STAGE_SHIFT)
 #define GBP_STAGE_FWD_STANCE 1u     /* planning_utils.cpp:718-730 */
@@ -119,23 +129,18 @@ int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage,
 #define GBP_OPT_KERNEL        1  /* GBP_KERNEL_* for the validate/extend entry points */
 #define GBP_OPT_BLOCK         2  /* threads per workgroup (multiple of 64, <= 512; the
                                     direct kernel uses min(block, 256))               */
-#define GBP_OPT_GRID_PER_CU   3  /* persistent kernel: workgroups per CU              */
-#define GBP_OPT_WAVES         4  /* register budget: min waves per SIMD (1..4)        */
+/* keys 3, 6, 7, 11, 12 (grid size, dynamic work sources, chunking, prefix,
+   oversubscription) were measured slower than static per-wave slices and removed */
+#define GBP_OPT_WAVES         4  /* register budget: min waves per SIMD (2..4)        */
 #define GBP_OPT_LDS_COORDS    5  /* 1: stage coordinate vectors in LDS when they fit  */
-#define GBP_OPT_SCHED         6  /* persistent work source: 0 one atomic counter,
-                                    1 static per-wave slices, 2 chunked counter,
-                                    3 per-workgroup slices dealt from an LDS counter,
-                                    4 static per-wave prefix + chunks from 8 per-XCD heads */
-#define GBP_OPT_CHUNK         7  /* attempts per dequeue for sched 0 / 2 (0 = per need) */
 #define GBP_OPT_HELPERS       8  /* 1: a drained wave's idle lanes evaluate the remaining
                                     attempts' next samples ahead (default 1)          */
 #define GBP_OPT_AFFINE_COORDS 9  /* 1 (default): compute grid coordinates when the host
                                     verified x[i] == a + h*(i - b) bit for bit         */
 #define GBP_OPT_COORD_MODE   10  /* read-only: 2 computed, 1 LDS-staged, 0 global      */
-#define GBP_OPT_PREFIX       11  /* sched 4: statically dealt share, 1/1024 (def. 512) */
-#define GBP_OPT_OVERSUB      12  /* sched 1/3/4: launch oversub x the resident workgroups */
-#define GBP_OPT_XCD_MAP      13  /* sched 1: 1 = each XCD takes one contiguous eighth of
-                                    the batch (workgroup b runs on XCD b % 8)           */
+#define GBP_OPT_XCD_MAP      13  /* 1 = each XCD takes one contiguous eighth of the batch
+                                    (workgroup b runs on XCD b % 8): for batches the
+                                    caller ordered by position                         */
 #define GBP_OPT_FAST_RCP     14  /* 1 (default): the bilinear 1/((x2-x1)(y2-y1)) by two
                                     Newton steps when gbp_terrain_create verified them
                                     bit-exact for every spacing pair; get: 1 = in use   */

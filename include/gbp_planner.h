@@ -292,6 +292,12 @@ class RRTClass {
   double wallTimeToFirst() const { return wall_to_first_; }
   // the last build's path cost / its history (rrt_connect.h getters' data)
   double pathCost() const { return path_cost_; }
+  // the reference's path cost: length, or the cost_add_yaw weighted sum
+  // (rrt_connect.cpp:304-313, :193-215)
+  double weightedCost(double length, double yaw) const {
+    return cost_add_yaw_flag_ ? length * cost_add_yaw_length_weight_ + yaw * cost_add_yaw_yaw_weight_
+                              : length;
+  }
   const std::vector<double> &costHistory() const { return cost_vector_; }
 
  protected:
@@ -321,6 +327,8 @@ struct BatchStats {
   int64_t iterations = 0, targets = 0, extends = 0, attempts_checked = 0, connects = 0;
   int64_t vertices_a = 0, vertices_b = 0;
   int64_t rewires = 0, solutions = 0;
+  int64_t depth_capped = 0;   // connects stopped at GBP_CONNECT_MAX_DEPTH (TRAPPED)
+  int64_t fragile_resolved = 0;  // attempts re-decided on the host (GBP_F_RESOLVED)
   double extent_a[4] = {0, 0, 0, 0}, extent_b[4] = {0, 0, 0, 0};  // x_min x_max y_min y_max
 };
 
@@ -385,7 +393,8 @@ class RRTConnectClass : public RRTClass {
   void attemptConnectBatch(const std::vector<State> &s_existing, const std::vector<State> &s,
                            std::vector<double> t_s, FastTerrainMap &terrain, int direction,
                            std::vector<int> &result, std::vector<State> &s_new,
-                           std::vector<Action> &a_new, BatchStats *stats, int max_depth = 64);
+                           std::vector<Action> &a_new, BatchStats *stats,
+                           int max_depth = GBP_CONNECT_MAX_DEPTH);
   // connect each vertex `added` of T to the other tree O (rrt_connect.cpp:98-120,
   // in order, NN against O's snapshot); returns the (T vertex, O vertex) pairs
   // whose connect REACHED

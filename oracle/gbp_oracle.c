@@ -564,7 +564,8 @@ static int attempt_connect_ts(const orc_terrain *T, const double *s_existing, co
                               double t_s, double *s_new, double *a_new, int direction,
                               int adaptive, int depth) {
   if (t_s <= KINEMATICS_RES) return GBP_TRAPPED;
-  if (depth > 64) return GBP_TRAPPED; /* guard; the reference recursion is unbounded */
+  /* engine convention (gbp.h GBP_CONNECT_MAX_DEPTH): the reference recursion is unbounded */
+  if (depth > GBP_CONNECT_MAX_DEPTH) return GBP_TRAPPED;
   const double *s_start = (direction == GBP_FORWARD) ? s_existing : s;
   const double *s_goal = (direction == GBP_FORWARD) ? s : s_existing;
   double t_new = NAN; /* reference: uninitialised */

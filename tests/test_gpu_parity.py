@@ -312,36 +312,31 @@ def test_full_size_batch_properties(gpu):
     assert 0 < ref[0].sum() < n
 
 
-@pytest.mark.parametrize("sched,chunk", [(0, 0), (1, 0), (2, 64), (2, 7), (3, 0), (3, 16),
-                                         (4, 0), (4, 5)])
 @pytest.mark.parametrize("coords", [0, 1, 2])
 @pytest.mark.parametrize("helpers", [0, 1])
-def test_validate_pairs_schedulers(gpu, sched, chunk, coords, helpers):
-    """Every work-distribution mode of the persistent kernel, every coordinate
-    source (0 global vectors, 1 LDS-staged, 2 computed from the verified affine
-    form), with and without tail helper lanes, computes the same answers."""
+@pytest.mark.parametrize("waves", [2, 3, 4])
+def test_validate_pairs_variants(gpu, coords, helpers, waves):
+    """Every coordinate source of the persistent kernel (0 global vectors, 1
+    LDS-staged, 2 computed from the verified affine form), with and without
+    tail helper lanes, at every register budget, computes the same answers."""
     data, T, O = terrain_pair("synth-rough-256")
     T.set_option(L.OPT_KERNEL, L.KERNEL_PERSISTENT)
-    T.set_option(L.OPT_SCHED, sched)
-    T.set_option(L.OPT_CHUNK, chunk)
-    T.set_option(L.OPT_PREFIX, 300)
     T.set_option(L.OPT_LDS_COORDS, 1 if coords == 1 else 0)
     T.set_option(L.OPT_AFFINE_COORDS, 1 if coords == 2 else 0)
     T.set_option(L.OPT_HELPERS, helpers)
+    T.set_option(L.OPT_WAVES, waves)
     assert T.get_option(L.OPT_COORD_MODE) == coords
     try:
         for n in (1, 63, 5000):
             s, a, d, _, _ = attempts_oracle(O, n, seed=1000 + n)
             res = T.validate_pairs(torch.from_numpy(s), torch.from_numpy(a), torch.from_numpy(d))
             gpu_t = (np_(res.valid), np_(res.s_new), np_(res.t_new), u32(res.flags), u32(res.counts))
-            assert_pairs_equal(gpu_t, O.validate_pairs(s, a, d, nthreads=8), f"s{sched}c{chunk}n{n}")
+            assert_pairs_equal(gpu_t, O.validate_pairs(s, a, d, nthreads=8), f"c{coords}h{helpers}w{waves}n{n}")
     finally:
-        T.set_option(L.OPT_SCHED, 1)
-        T.set_option(L.OPT_CHUNK, 0)
-        T.set_option(L.OPT_PREFIX, 512)
         T.set_option(L.OPT_LDS_COORDS, 1)
         T.set_option(L.OPT_AFFINE_COORDS, 1)
         T.set_option(L.OPT_HELPERS, 1)
+        T.set_option(L.OPT_WAVES, 2)
 
 
 @pytest.mark.parametrize("name", ["synth-rough-256", "rough_terrain-gridmap"])

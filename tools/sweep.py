@@ -25,12 +25,9 @@ def main():
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--launches", type=int, default=10)
     p.add_argument("--kernels", default="direct,persistent")
-    p.add_argument("--waves", default="1,2,4")
-    p.add_argument("--grid", default="4,8,16")
+    p.add_argument("--waves", default="2,3,4")
     p.add_argument("--block", default="256")
     p.add_argument("--lds", default="2", help="coordinates: 0 global, 1 LDS, 2 computed (affine)")
-    p.add_argument("--sched", default="0", help="comma list of sched:chunk[:prefix], e.g. 0:0,1:0,2:64,4:32:512")
-    p.add_argument("--oversub", default="1", help="comma list of workgroup oversubscription factors")
     p.add_argument("--set", action="append", default=[],
                    help="extra option axis KEY=v1,v2 (KEY: an OPT_* name such as PREFETCH, or its id)")
     p.add_argument("--order", default="batch",
@@ -63,12 +60,8 @@ def main():
     for k in a.kernels.split(","):
         for w in (map(int, a.waves.split(",")) if k == "persistent" else [1]):
             for b in map(int, a.block.split(",")):
-                grids = map(int, a.grid.split(",")) if k == "persistent" else [0]
-                for g in grids:
-                    for lds in map(int, a.lds.split(",")):
-                        for sc in (a.sched.split(",") if k == "persistent" else ["0:0"]):
-                            for ov in map(int, a.oversub.split(",")):
-                                variants.append((k, w, b, g, lds, sc if ":" in sc else sc + ":0", ov))
+                for lds in map(int, a.lds.split(",")):
+                    variants.append((k, w, b, lds))
     extra_keys, extra_vals = [], []
     for spec in a.set:
         k, vals = spec.split("=")
@@ -80,20 +73,14 @@ def main():
     st = torch.cuda.current_stream()
     for r in range(a.rounds):
         for v in variants:
-            k, w, b, g, lds, sc, ov, ex = v
+            k, w, b, lds, ex = v
             for (_, key), val in zip(extra_keys, ex):
                 T.set_option(key, val)
-            T.set_option(L.OPT_SCHED, int(sc.split(":")[0]))
-            T.set_option(L.OPT_CHUNK, int(sc.split(":")[1]))
-            T.set_option(L.OPT_PREFIX, int(sc.split(":")[2]) if sc.count(":") >= 2 else 512)
             T.set_option(L.OPT_KERNEL, L.KERNEL_PERSISTENT if k == "persistent" else L.KERNEL_DIRECT)
             T.set_option(L.OPT_WAVES, w)
             T.set_option(L.OPT_LDS_COORDS, 1 if lds >= 1 else 0)
             T.set_option(L.OPT_AFFINE_COORDS, 1 if lds == 2 else 0)
             T.set_option(L.OPT_BLOCK, b)
-            if g:
-                T.set_option(L.OPT_GRID_PER_CU, g)
-            T.set_option(L.OPT_OVERSUB, ov)
             out = T.validate_pairs(s, act, d, adaptive=a.adaptive)
             if r == 0:
                 sig = (out.valid.cpu().numpy().tobytes(), out.flags.cpu().numpy().tobytes(),
@@ -113,13 +100,13 @@ def main():
     rows = []
     for v in variants:
         t = np.array(times[v])
-        rows.append({"kernel": v[0], "waves": v[1], "block": v[2], "grid_per_cu": v[3], "lds": v[4], "sched": v[5], "oversub": v[6],
-                     "set": {name: val for (name, _), val in zip(extra_keys, v[7])},
+        rows.append({"kernel": v[0], "waves": v[1], "block": v[2], "lds": v[3],
+                     "set": {name: val for (name, _), val in zip(extra_keys, v[4])},
                      "median_ms": float(np.median(t)), "min_ms": float(t.min()),
                      "attempts_per_s": a.batch / (np.median(t) * 1e-3)})
     rows.sort(key=lambda r: r["median_ms"])
     for r in rows:
-        print(f"{r['kernel']:10s} w={r['waves']} b={r['block']} g={r['grid_per_cu']:2d} lds={r['lds']} sched={r['sched']:5s} ov={r['oversub']} {r['set']} "
+        print(f"{r['kernel']:10s} w={r['waves']} b={r['block']} lds={r['lds']} {r['set']} "
               f"median {r['median_ms']:.4f} ms  min {r['min_ms']:.4f} ms  "
               f"{r['attempts_per_s'] / 1e6:.1f} M attempts/s")
     if a.out:
