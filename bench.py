@@ -221,6 +221,7 @@ def extend_micro(T, s, tgt, d, seed, launches=10):
     sn = torch.empty((n, 8), dtype=torch.float64, device=dev)
     an = torch.empty((n, 10), dtype=torch.float64, device=dev)
     cnt = torch.empty(n, dtype=torch.int32, device=dev)
+    efl = torch.empty(n, dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream(dev)
     sv, tv, dv = s[:n].contiguous(), tgt[:n].contiguous(), d[:n].contiguous()
 
@@ -228,7 +229,7 @@ def extend_micro(T, s, tgt, d, seed, launches=10):
         rc = T._lib.gbp_extend_batch_dev(T._h, n, VP(sv.data_ptr()), VP(tv.data_ptr()),
                                          VP(dv.data_ptr()), 0, 0, seed, 0, VP(res.data_ptr()),
                                          VP(cho.data_ptr()), VP(sn.data_ptr()), VP(an.data_ptr()),
-                                         VP(cnt.data_ptr()), VP(st.cuda_stream))
+                                         VP(cnt.data_ptr()), VP(efl.data_ptr()), VP(st.cuda_stream))
         if rc != 0:
             raise gbp.GbpError(rc, "extend_batch")
 

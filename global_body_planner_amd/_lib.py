@@ -40,6 +40,7 @@ EXPORTS = [
     "gbp_extend_batch_dev", "gbp_extend_batch_host",
     "gbp_nearest_batch_dev", "gbp_nearest_batch_host",
     "gbp_neighbors_batch_dev", "gbp_neighbors_batch_host",
+    "gbp_resolve_fragile_host", "gbp_resolve_fragile_states_host", "gbp_extend_resolve_host",
 ]
 
 
@@ -94,8 +95,11 @@ def load(path=None):
         "gbp_sample_actions_dev": (I, [I64, P, U64, U64, I64, P, P]),
         "gbp_sample_states_host": (I, [P, I64, U64, U64, I64, I, I, P, P]),
         "gbp_sample_actions_host": (I, [P, I64, P, U64, U64, I64, P]),
-        "gbp_extend_batch_dev": (I, [P, I64, P, P, P, I, I, U64, I64, P, P, P, P, P, P]),
-        "gbp_extend_batch_host": (I, [P, I64, P, P, P, I, I, U64, I64, P, P, P, P, P]),
+        "gbp_extend_batch_dev": (I, [P, I64, P, P, P, I, I, U64, I64, P, P, P, P, P, P, P]),
+        "gbp_extend_batch_host": (I, [P, I64, P, P, P, I, I, U64, I64, P, P, P, P, P, P]),
+        "gbp_resolve_fragile_host": (I, [P, I64, P, P, P, I, I, P, P, P, P, P, P]),
+        "gbp_resolve_fragile_states_host": (I, [P, I64, P, P, I, P, P, P, P]),
+        "gbp_extend_resolve_host": (I, [P, I64, P, P, P, I, I, U64, I64, P, P, P, P, P, P, P]),
         "gbp_nearest_batch_dev": (I, [I64, P, I64, P, P, P, P]),
         "gbp_nearest_batch_host": (I, [I64, P, I64, P, P, P]),
         "gbp_neighbors_batch_dev": (I, [I64, P, I64, P, ctypes.c_double, I, P, P, P]),

@@ -29,6 +29,7 @@
 
 #include "gbp.h"
 #include "gbp_device.h"
+#include "host/gbp_host_check.h"
 
 using namespace gbp;
 
@@ -701,7 +702,7 @@ __global__ void k_extend_select(int64_t n, const double *__restrict__ s_near,
                                 const uint32_t *__restrict__ cand_counts,
                                 int32_t *__restrict__ result, int32_t *__restrict__ chosen,
                                 double *__restrict__ s_new, double *__restrict__ a_new,
-                                uint32_t *__restrict__ counts) {
+                                uint32_t *__restrict__ counts, uint32_t *__restrict__ ext_flags) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     double sn[8], tg[8];
@@ -711,11 +712,12 @@ __global__ void k_extend_select(int64_t n, const double *__restrict__ s_near,
       tg[k] = target[8 * i + k];
     }
     int found = -1;
-    uint32_t G = 0, V = 0;
+    uint32_t G = 0, V = 0, ef = 0;
     for (int j = 0; j < GBP_NUM_GEN_STATES; j++) {
       const int64_t c = i * GBP_NUM_GEN_STATES + j;
       G += GBP_COUNT_G(cand_counts[c]);
       V += GBP_COUNT_V(cand_counts[c]);
+      ef |= cand_flags[c] & (GBP_F_VALID | GBP_F_OOD | GBP_F_NAN | GBP_F_FRAGILE | GBP_F_LIMIT);
       if (cand_flags[c] & GBP_F_VALID) {
         found = j;
         break;
@@ -743,6 +745,7 @@ __global__ void k_extend_select(int64_t n, const double *__restrict__ s_near,
     result[i] = r;
     if (chosen) chosen[i] = found;
     if (counts) counts[i] = (G & 0xFFFFu) | (V << 16);
+    if (ext_flags) ext_flags[i] = ef;
   }
 }
 
@@ -888,6 +891,8 @@ __global__ __launch_bounds__(256) void k_neighbors(int64_t n_query, const double
 // C ABI
 // ============================================================================
 struct gbp_terrain {
+  gbp_host::Terrain host;           // host copy (the values the device holds) for the
+                                    // glibc re-decision of FRAGILE attempts
   int device = 0;
   int nx = 0, ny = 0;
   int storage = GBP_STORAGE_F64;
@@ -1175,7 +1180,7 @@ size_t rnd(size_t b) { return (b + 255) & ~(size_t)255; }
 
 extern "C" {
 
-int gbp_version(void) { return 100; /* 0.1.0 */ }
+int gbp_version(void) { return 200; /* 0.2.0: extend flags, FRAGILE re-decision, trees */ }
 
 const char *gbp_status_string(int status) {
   switch (status) {
@@ -1271,6 +1276,13 @@ int gbp_terrain_create(int device, int nx, int ny, const double *x, const double
   t->one_y = one_step_exact(y, ny, t->inv_hy);
   t->affine = affine_fit(x, nx, &t->ax, &t->hx, &t->bx) && affine_fit(y, ny, &t->ay, &t->hy, &t->by);
   t->rcp_seed = verified_rcp_seed(x, nx, y, ny);
+  t->host.nx = nx;
+  t->host.ny = ny;
+  t->host.x.assign(x, x + nx);
+  t->host.y.assign(y, y + ny);
+  t->host.z.resize(cells);
+  for (size_t i = 0; i < cells; i++)  // exactly what the device holds
+    t->host.z[i] = storage == GBP_STORAGE_F32 ? (double)(float)z[i] : z[i];
   (void)hipDeviceGetAttribute(&t->num_cus, hipDeviceAttributeMultiprocessorCount, device);
   if (t->num_cus <= 0) t->num_cus = 256;
   int rc = GBP_OK;
@@ -1523,7 +1535,7 @@ int gbp_sample_actions_dev(int64_t n, const double *normals, uint64_t seed, uint
 int gbp_extend_batch_dev(gbp_terrain *t, int64_t n, const double *s_near, const double *target,
                          const uint8_t *direction, int direction_all, int adaptive, uint64_t seed,
                          int64_t extend_base, int32_t *result, int32_t *chosen, double *s_new,
-                         double *a_new, uint32_t *counts, gbp_stream stream) {
+                         double *a_new, uint32_t *counts, uint32_t *flags, gbp_stream stream) {
   if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
   if (n < 0 || (n > 0 && (!s_near || !target || !result || !s_new || !a_new)))
     return GBP_E_INVALID_ARG;
@@ -1564,7 +1576,7 @@ int gbp_extend_batch_dev(gbp_terrain *t, int64_t n, const double *s_near, const 
                               stream);
   if (rc) return rc;
   hipLaunchKernelGGL(k_extend_select, dim3(grid_for(n, 256, t->num_cus * 16)), dim3(256), 0, st,
-                     n, s_near, target, ca, csn, cf, cc, result, chosen, s_new, a_new, counts);
+                     n, s_near, target, ca, csn, cf, cc, result, chosen, s_new, a_new, counts, flags);
   HIPCHK(hipGetLastError());
   return GBP_OK;
 }
@@ -1670,11 +1682,14 @@ int gbp_valid_states_host(gbp_terrain *t, int64_t n, const double *states, const
   if (phase) H2D(dp, phase, n);
   rc = gbp_valid_states_dev(t, n, ds, phase ? dp : nullptr, phase_all, dv, df, dc, st);
   if (rc) return rc;
+  std::vector<uint32_t> fl(flags ? 0 : n);
+  uint32_t *flags_h = flags ? flags : fl.data();
   if (valid) D2H(valid, dv, n);
-  if (flags) D2H(flags, df, 4 * n);
+  D2H(flags_h, df, 4 * n);
   if (counts) D2H(counts, dc, 4 * n);
   HIPCHK(hipStreamSynchronize(st));
-  return GBP_OK;
+  return gbp_resolve_fragile_states_host(t, n, states, phase, phase_all, valid, flags_h, counts,
+                                         nullptr);
 }
 
 int gbp_validate_pairs_host(gbp_terrain *t, int64_t n, const double *s, const double *a,
@@ -1704,48 +1719,70 @@ int gbp_validate_pairs_host(gbp_terrain *t, int64_t n, const double *s, const do
   rc = gbp_validate_pairs_dev(t, n, ds, da, direction ? dd : nullptr, direction_all, adaptive,
                               dv, dsn, dtn, df, dc, st);
   if (rc) return rc;
+  std::vector<uint32_t> fl(flags ? 0 : n);
+  uint32_t *flags_h = flags ? flags : fl.data();
+  // the caller's s_new / t_new: a FRAGILE attempt the host re-decides gets
+  // back the caller's contents wherever the host check does not assign them
+  std::vector<double> sn0(s_new ? 8 * n : 0), tn0(t_new ? n : 0);
+  if (s_new) memcpy(sn0.data(), s_new, 64 * n);
+  if (t_new) memcpy(tn0.data(), t_new, 8 * n);
   if (valid) D2H(valid, dv, n);
   if (s_new) D2H(s_new, dsn, 64 * n);
   if (t_new) D2H(t_new, dtn, 8 * n);
-  if (flags) D2H(flags, df, 4 * n);
+  D2H(flags_h, df, 4 * n);
   if (counts) D2H(counts, dc, 4 * n);
   HIPCHK(hipStreamSynchronize(st));
-  return GBP_OK;
+  for (int64_t i = 0; i < n; i++) {
+    if (!(flags_h[i] & GBP_F_FRAGILE)) continue;
+    if (s_new) memcpy(s_new + 8 * i, sn0.data() + 8 * i, 64);
+    if (t_new) t_new[i] = tn0[i];
+  }
+  return gbp_resolve_fragile_host(t, n, s, a, direction, direction_all, adaptive, valid, s_new,
+                                  t_new, flags_h, counts, nullptr);
 }
 
 int gbp_extend_batch_host(gbp_terrain *t, int64_t n, const double *s_near, const double *target,
                           const uint8_t *direction, int direction_all, int adaptive,
                           uint64_t seed, int64_t extend_base, int32_t *result, int32_t *chosen,
-                          double *s_new, double *a_new, uint32_t *counts) {
+                          double *s_new, double *a_new, uint32_t *counts, uint32_t *flags) {
   if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
   if (n <= 0) return n == 0 ? GBP_OK : GBP_E_INVALID_ARG;
   if (!s_near || !target || !result || !s_new || !a_new) return GBP_E_INVALID_ARG;
   DeviceGuard g(t->device);
   hipStream_t st = t->host_stream;
   int rc = ensure_ws(t, &t->ws, &t->ws_bytes,
-                     3 * rnd(64 * n) + rnd(80 * n) + rnd(n) + 3 * rnd(4 * n) + 4096);
+                     3 * rnd(64 * n) + rnd(80 * n) + rnd(n) + 4 * rnd(4 * n) + 4096);
   if (rc) return rc;
   Stage S{t, (char *)t->ws};
   double *dsn = S.take<double>(8 * n), *dtg = S.take<double>(8 * n);
   double *dnew = S.take<double>(8 * n), *danew = S.take<double>(10 * n);
   uint8_t *dd = S.take<uint8_t>(n);
   int32_t *dr = S.take<int32_t>(n), *dch = S.take<int32_t>(n);
-  uint32_t *dc = S.take<uint32_t>(n);
+  uint32_t *dc = S.take<uint32_t>(n), *df = S.take<uint32_t>(n);
   H2D(dsn, s_near, 64 * n);
   H2D(dtg, target, 64 * n);
   H2D(dnew, s_new, 64 * n);
   H2D(danew, a_new, 80 * n);
   if (direction) H2D(dd, direction, n);
   rc = gbp_extend_batch_dev(t, n, dsn, dtg, direction ? dd : nullptr, direction_all, adaptive,
-                            seed, extend_base, dr, dch, dnew, danew, dc, st);
+                            seed, extend_base, dr, dch, dnew, danew, dc, df, st);
   if (rc) return rc;
+  std::vector<int32_t> ch(chosen ? 0 : n);
+  std::vector<uint32_t> cnt(counts ? 0 : n), fl(flags ? 0 : n);
+  int32_t *chosen_h = chosen ? chosen : ch.data();
+  uint32_t *counts_h = counts ? counts : cnt.data();
+  uint32_t *flags_h = flags ? flags : fl.data();
   D2H(result, dr, 4 * n);
-  if (chosen) D2H(chosen, dch, 4 * n);
+  D2H(chosen_h, dch, 4 * n);
   D2H(s_new, dnew, 64 * n);
   D2H(a_new, danew, 80 * n);
-  if (counts) D2H(counts, dc, 4 * n);
+  D2H(counts_h, dc, 4 * n);
+  D2H(flags_h, df, 4 * n);
   HIPCHK(hipStreamSynchronize(st));
-  return GBP_OK;
+  // decisions that hinge on a trig-sensitive margin: re-decided with glibc
+  return gbp_extend_resolve_host(t, n, s_near, target, direction, direction_all, adaptive, seed,
+                                 extend_base, result, chosen_h, s_new, a_new, counts_h, flags_h,
+                                 nullptr);
 }
 
 int gbp_sample_states_host(gbp_terrain *t, int64_t n, uint64_t seed, uint64_t stream_id,
@@ -1845,6 +1882,115 @@ int gbp_neighbors_batch_host(int64_t n_query, const double *queries, int64_t n_v
     rc = GBP_E_HIP;
   (void)hipFree(buf);
   return rc;
+}
+
+
+// ---- FRAGILE attempts: the glibc re-decision (host/gbp_host_check.cpp) ------------
+int gbp_resolve_fragile_host(gbp_terrain *t, int64_t n, const double *s, const double *a,
+                             const uint8_t *direction, int direction_all, int adaptive,
+                             uint8_t *valid, double *s_new, double *t_new, uint32_t *flags,
+                             uint32_t *counts, int64_t *n_resolved) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || (n > 0 && (!s || !a || !flags))) return GBP_E_INVALID_ARG;
+  if (!direction && direction_all != GBP_FORWARD && direction_all != GBP_REVERSE)
+    return GBP_E_INVALID_ARG;
+  int64_t k = 0;
+  for (int64_t i = 0; i < n; i++) {
+    if (!(flags[i] & GBP_F_FRAGILE)) continue;
+    double sn[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tn = 0;
+    uint32_t f = 0, c = 0;
+    const int d = direction ? direction[i] : direction_all;
+    const bool v = gbp_host::pair_check(t->host, s + 8 * i, a + 10 * i, d, adaptive, sn, &tn, &f, &c);
+    if (valid) valid[i] = v ? 1 : 0;
+    if (s_new && (f & GBP_F_SNEW_SET)) memcpy(s_new + 8 * i, sn, sizeof sn);
+    if (t_new && (f & GBP_F_TNEW_SET)) t_new[i] = tn;
+    flags[i] = f | GBP_F_RESOLVED;
+    if (counts) counts[i] = c;
+    k++;
+  }
+  if (n_resolved) *n_resolved = k;
+  return GBP_OK;
+}
+
+int gbp_resolve_fragile_states_host(gbp_terrain *t, int64_t n, const double *states,
+                                    const uint8_t *phase, int phase_all, uint8_t *valid,
+                                    uint32_t *flags, uint32_t *counts, int64_t *n_resolved) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || (n > 0 && (!states || !flags))) return GBP_E_INVALID_ARG;
+  int64_t k = 0;
+  for (int64_t i = 0; i < n; i++) {
+    if (!(flags[i] & GBP_F_FRAGILE)) continue;
+    gbp_host::Acc acc;
+    const bool v = gbp_host::is_valid_state(t->host, states + 8 * i, phase ? phase[i] : phase_all, acc);
+    if (valid) valid[i] = v ? 1 : 0;
+    flags[i] = acc.flags | (v ? GBP_F_VALID : 0u) | GBP_F_RESOLVED;
+    if (counts) counts[i] = (acc.G & 0xFFFFu) | (acc.V << 16);
+    k++;
+  }
+  if (n_resolved) *n_resolved = k;
+  return GBP_OK;
+}
+
+// RRTClass::newConfig + extend's acceptance (rrt.cpp:20-70, :84-101) on the
+// host for every extend whose executed candidates include a FRAGILE one.  The
+// candidate actions are regenerated on the device from the same Philox
+// stream (the engine's candidate sampler, not a host libm), then checked in
+// index order with the glibc pair check.
+int gbp_extend_resolve_host(gbp_terrain *t, int64_t n, const double *s_near, const double *target,
+                            const uint8_t *direction, int direction_all, int adaptive,
+                            uint64_t seed, int64_t extend_base, int32_t *result, int32_t *chosen,
+                            double *s_new, double *a_new, uint32_t *counts, uint32_t *flags,
+                            int64_t *n_resolved) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || (n > 0 && (!s_near || !target || !result || !s_new || !a_new || !flags)))
+    return GBP_E_INVALID_ARG;
+  int64_t k = 0;
+  for (int64_t i = 0; i < n; i++) {
+    if (!(flags[i] & GBP_F_FRAGILE)) continue;
+    const double *tg = target + 8 * i, *sn0 = s_near + 8 * i;
+    double nrm[3 * GBP_NUM_GEN_STATES], act[10 * GBP_NUM_GEN_STATES];
+    int rc = gbp_normal_batch_host(t, 1, tg, nrm, nullptr);  // rrt.cpp:25 (k_extend_prep)
+    if (rc) return rc;
+    for (int j = 1; j < GBP_NUM_GEN_STATES; j++) memcpy(nrm + 3 * j, nrm, 3 * sizeof(double));
+    rc = gbp_sample_actions_host(t, GBP_NUM_GEN_STATES, nrm, seed, EXTEND_STREAM,
+                                 (extend_base + i) * 8, act);
+    if (rc) return rc;
+    const int d = direction ? direction[i] : direction_all;
+    const double best0 = gbp_host::state_distance(sn0, tg);
+    double best = best0, s_test[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_test = 0;
+    uint32_t G = 0, V = 0, ef = 0;
+    int found = -1;
+    for (int j = 0; j < GBP_NUM_GEN_STATES; j++) {  // rrt.cpp:36-50
+      uint32_t f = 0, c = 0;
+      const bool v = gbp_host::pair_check(t->host, sn0, act + 10 * j, d, adaptive, s_test, &t_test, &f, &c);
+      G += GBP_COUNT_G(c);
+      V += GBP_COUNT_V(c);
+      ef |= f & (GBP_F_VALID | GBP_F_OOD | GBP_F_NAN | GBP_F_LIMIT);
+      if (v) {
+        found = j;
+        break;
+      }
+    }
+    if (found >= 0) {  // rrt.cpp:55-61
+      const double cur = gbp_host::state_distance(s_test, tg);
+      if (cur < best) {
+        best = cur;
+        memcpy(s_new + 8 * i, s_test, sizeof s_test);
+        memcpy(a_new + 10 * i, act + 10 * found, 10 * sizeof(double));
+      }
+    }
+    // rrt.cpp:65-68 / :84-101
+    result[i] = best == best0 ? GBP_TRAPPED
+                              : (gbp_host::state_distance(s_new + 8 * i, tg) <= GOAL_BOUNDS
+                                     ? GBP_REACHED
+                                     : GBP_ADVANCED);
+    if (chosen) chosen[i] = found;
+    if (counts) counts[i] = (G & 0xFFFFu) | (V << 16);
+    flags[i] = ef | GBP_F_RESOLVED;
+    k++;
+  }
+  if (n_resolved) *n_resolved = k;
+  return GBP_OK;
 }
 
 }  // extern "C"

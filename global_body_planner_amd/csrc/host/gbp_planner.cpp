@@ -631,7 +631,8 @@ bool RRTClass::newConfig(State s, State s_near, State &s_new, Action &a_new, Fas
   const uint8_t dir = (uint8_t)direction;
   chk(gbp_extend_batch_host(terrain.handle(), 1, s_near.data(), s.data(), &dir, direction,
                             state_action_pair_check_adaptive_step_size_flag_ ? 1 : 0, seed_,
-                            extend_counter_++, &result, &chosen, sn.data(), an.data(), &counts),
+                            extend_counter_++, &result, &chosen, sn.data(), an.data(), &counts,
+                            nullptr),
       "newConfig");
   if (result == GBP_TRAPPED) return false;
   s_new = sn;
@@ -1073,11 +1074,14 @@ void RRTConnectClass::extendBatch(PlannerClass &T, FastTerrainMap &terrain, int 
   std::vector<Action> a_new(n);
   for (int64_t i = 0; i < n; i++) s_near[i] = T.getVertex(nn[i]);
   std::vector<int32_t> res(n), chosen(n);
+  std::vector<uint32_t> eflags(n);
   chk(gbp_extend_batch_host(terrain.handle(), n, s_near[0].data(), targets[0].data(), nullptr, dir,
                             state_action_pair_check_adaptive_step_size_flag_ ? 1 : 0, seed_,
                             extend_counter_, res.data(), chosen.data(), s_new[0].data(),
-                            a_new[0].data(), nullptr),
+                            a_new[0].data(), nullptr, eflags.data()),
       "extend batch");
+  if (stats)
+    for (int64_t i = 0; i < n; i++) stats->fragile_resolved += (eflags[i] & GBP_F_RESOLVED) ? 1 : 0;
   extend_counter_ += n;
   if (stats) {
     stats->extends += n;

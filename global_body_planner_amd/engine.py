@@ -25,6 +25,10 @@ def _np_ptr(a):
     return None if a is None else a.ctypes.data_as(_VP)
 
 
+def _np(x):
+    return x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x)
+
+
 def _stream(device):
     return _VP(torch.cuda.current_stream(device).cuda_stream)
 
@@ -45,6 +49,7 @@ class ExtendResult:
     s_new: torch.Tensor
     a_new: torch.Tensor
     counts: torch.Tensor
+    flags: torch.Tensor     # int32 view: OR of the executed candidates' flags
 
 
 class Terrain:
@@ -215,11 +220,12 @@ class Terrain:
             result=self._empty(n, torch.int32), chosen=self._empty(n, torch.int32),
             s_new=torch.full((n, 8), float("nan"), dtype=torch.float64, device=self.torch_device),
             a_new=torch.full((n, 10), float("nan"), dtype=torch.float64, device=self.torch_device),
-            counts=self._empty(n, torch.int32))
+            counts=self._empty(n, torch.int32), flags=self._empty(n, torch.int32))
         check(self._lib.gbp_extend_batch_dev(self._h, n, _ptr(sn), _ptr(tg), _ptr(d), dall,
                                              int(bool(adaptive)), seed, extend_base, _ptr(r.result),
                                              _ptr(r.chosen), _ptr(r.s_new), _ptr(r.a_new),
-                                             _ptr(r.counts), _stream(self.device)), "extend")
+                                             _ptr(r.counts), _ptr(r.flags), _stream(self.device)),
+              "extend")
         return r
 
     # ---- host variants (numpy in/out) -------------------------------------------
@@ -241,6 +247,71 @@ class Terrain:
                                                 _np_ptr(s_new), _np_ptr(t_new), _np_ptr(flags),
                                                 _np_ptr(counts)), "validate_pairs_host")
         return valid, s_new, t_new, flags, counts
+
+    def resolve_fragile(self, s, a, direction, res, adaptive=False):
+        """gbp_resolve_fragile_host on a validate_pairs result: numpy copies
+        (valid, s_new, t_new, flags, counts) with every GBP_F_FRAGILE attempt
+        re-decided on the host with glibc trig; returns them and the number
+        re-decided."""
+        s = np.ascontiguousarray(_np(s), np.float64).reshape(-1, 8)
+        a = np.ascontiguousarray(_np(a), np.float64).reshape(-1, 10)
+        n = s.shape[0]
+        if np.ndim(direction) > 0 or isinstance(direction, torch.Tensor):
+            d, dall = np.ascontiguousarray(_np(direction), np.uint8), 0
+        else:
+            d, dall = None, int(direction)
+        valid = np.ascontiguousarray(_np(res.valid), np.uint8).copy()
+        s_new = np.ascontiguousarray(_np(res.s_new), np.float64).copy()
+        t_new = np.ascontiguousarray(_np(res.t_new), np.float64).copy()
+        flags = np.ascontiguousarray(_np(res.flags)).view(np.uint32).copy()
+        counts = np.ascontiguousarray(_np(res.counts)).view(np.uint32).copy()
+        k = ctypes.c_int64(0)
+        check(self._lib.gbp_resolve_fragile_host(self._h, n, _np_ptr(s), _np_ptr(a), _np_ptr(d),
+                                                 dall, int(bool(adaptive)), _np_ptr(valid),
+                                                 _np_ptr(s_new), _np_ptr(t_new), _np_ptr(flags),
+                                                 _np_ptr(counts), ctypes.byref(k)),
+              "resolve_fragile")
+        return (valid, s_new, t_new, flags, counts), k.value
+
+    def valid_states_host(self, states, phase):
+        """gbp_valid_states_host (FRAGILE states re-decided on the host):
+        (valid, flags, counts) numpy."""
+        st = np.ascontiguousarray(_np(states), np.float64).reshape(-1, 8)
+        n = st.shape[0]
+        if np.ndim(phase) > 0:
+            ph, pall = np.ascontiguousarray(_np(phase), np.uint8), 0
+        else:
+            ph, pall = None, int(phase)
+        valid = np.empty(n, np.uint8)
+        flags = np.empty(n, np.uint32)
+        counts = np.empty(n, np.uint32)
+        check(self._lib.gbp_valid_states_host(self._h, n, _np_ptr(st), _np_ptr(ph), pall,
+                                              _np_ptr(valid), _np_ptr(flags), _np_ptr(counts)),
+              "valid_states_host")
+        return valid, flags, counts
+
+    def extend_host(self, s_near, target, direction, seed, extend_base=0, adaptive=False):
+        """gbp_extend_batch_host (FRAGILE extends re-decided on the host):
+        (result, chosen, s_new, a_new, counts, flags) numpy; s_new / a_new NaN
+        where the extend is TRAPPED (written only where the reference writes)."""
+        sn = np.ascontiguousarray(_np(s_near), np.float64).reshape(-1, 8)
+        tg = np.ascontiguousarray(_np(target), np.float64).reshape(-1, 8)
+        n = sn.shape[0]
+        if np.ndim(direction) > 0 or isinstance(direction, torch.Tensor):
+            d, dall = np.ascontiguousarray(_np(direction), np.uint8), 0
+        else:
+            d, dall = None, int(direction)
+        res = np.empty(n, np.int32)
+        cho = np.empty(n, np.int32)
+        s_new = np.full((n, 8), np.nan)
+        a_new = np.full((n, 10), np.nan)
+        counts = np.empty(n, np.uint32)
+        flags = np.empty(n, np.uint32)
+        check(self._lib.gbp_extend_batch_host(self._h, n, _np_ptr(sn), _np_ptr(tg), _np_ptr(d), dall,
+                                              int(bool(adaptive)), seed, extend_base, _np_ptr(res),
+                                              _np_ptr(cho), _np_ptr(s_new), _np_ptr(a_new),
+                                              _np_ptr(counts), _np_ptr(flags)), "extend_host")
+        return res, cho, s_new, a_new, counts, flags
 
     def height_host(self, xy):
         xy = np.ascontiguousarray(xy, np.float64).reshape(-1, 2)

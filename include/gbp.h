@@ -231,12 +231,45 @@ int gbp_extend_batch_dev(gbp_terrain *t, int64_t n, const double *s_near,
                          int direction_all, int adaptive, uint64_t seed,
                          int64_t extend_base, int32_t *result, int32_t *chosen,
                          double *s_new, double *a_new, uint32_t *counts,
-                         gbp_stream stream);
+                         uint32_t *flags, gbp_stream stream);
+/* (flags[i]: OR of the executed candidates' VALID / OOD / NAN / FRAGILE / LIMIT
+ *  bits; a FRAGILE extend is re-decided by gbp_extend_resolve_host.  The _host
+ *  variant does that itself: its outputs are final.) */
 int gbp_extend_batch_host(gbp_terrain *t, int64_t n, const double *s_near,
                           const double *target, const uint8_t *direction,
                           int direction_all, int adaptive, uint64_t seed,
                           int64_t extend_base, int32_t *result, int32_t *chosen,
-                          double *s_new, double *a_new, uint32_t *counts);
+                          double *s_new, double *a_new, uint32_t *counts,
+                          uint32_t *flags);
+
+/* ---- FRAGILE attempts: the host re-decision ---------------------------------
+ * The kernels form isValidState's rotation without libm; where a decision's
+ * margin is below 1e-12 (a height within 1e-12 of H_MIN / H_MAX, a lookup
+ * point within 1e-12 of a grid line) the attempt is flagged GBP_F_FRAGILE,
+ * because glibc's atan2 / cos / sin (the reference's) could decide it the
+ * other way.  These entry points re-run exactly the flagged entries on the
+ * host with glibc and the reference's expressions (planning_utils.cpp
+ * :562-881, compiled without FMA like the reference) and overwrite their
+ * outputs; flags get GBP_F_RESOLVED (FRAGILE cleared).  Host pointers; the
+ * _host entry points above call them already, the _dev entry points leave it
+ * to the caller.  Entries the host check does not assign keep the buffer's
+ * contents.  n_resolved (may be NULL) = how many were re-decided. */
+int gbp_resolve_fragile_host(gbp_terrain *t, int64_t n, const double *s, const double *a,
+                             const uint8_t *direction, int direction_all, int adaptive,
+                             uint8_t *valid, double *s_new, double *t_new, uint32_t *flags,
+                             uint32_t *counts, int64_t *n_resolved);
+int gbp_resolve_fragile_states_host(gbp_terrain *t, int64_t n, const double *states,
+                                    const uint8_t *phase, int phase_all, uint8_t *valid,
+                                    uint32_t *flags, uint32_t *counts, int64_t *n_resolved);
+/* newConfig + acceptance (rrt.cpp:20-101) re-decided for every extend whose
+ * flags carry GBP_F_FRAGILE (same arguments as gbp_extend_batch_dev, host
+ * pointers): the six candidate actions are regenerated on the device from
+ * the same stream, then checked in order with the glibc pair check. */
+int gbp_extend_resolve_host(gbp_terrain *t, int64_t n, const double *s_near, const double *target,
+                            const uint8_t *direction, int direction_all, int adaptive,
+                            uint64_t seed, int64_t extend_base, int32_t *result, int32_t *chosen,
+                            double *s_new, double *a_new, uint32_t *counts, uint32_t *flags,
+                            int64_t *n_resolved);
 
 /* ---- nearest neighbour (PlannerClass::getNearestNeighbor,
  *      planner_class.cpp:185-200) ----------------------------------------------

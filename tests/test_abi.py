@@ -41,7 +41,7 @@ def test_exports_are_plain_c():
 
 def test_load_version_and_status_strings():
     lib = L.load()
-    assert lib.gbp_version() == 100
+    assert lib.gbp_version() == 200
     assert lib.gbp_status_string(0) == b"ok"
     assert lib.gbp_status_string(-6) == b"no HIP device"
     assert lib.gbp_status_string(12345) == b"unknown status"

@@ -1,0 +1,181 @@
+"""FRAGILE attempts: decisions within 1e-12 of a threshold, re-decided on the
+host with glibc (gbp_resolve_fragile_host / the _host entry points).
+
+The kernels form isValidState's rotation without libm (gbp_device.h
+rotation_trig_nolibm); glibc's atan2 / cos / sin (the reference's, and the
+oracle's) can differ from it by an ulp, which can flip a decision whose
+margin is that small.  These tests build states that sit within a few ulps /
+1e-13 of H_MIN (corners, underside), H_MAX (legs) and of grid lines, and
+check that
+
+  * the kernels flag every one of them GBP_F_FRAGILE,
+  * the product's final decision (host entry points, or _dev + resolve) equals
+    the oracle's on EVERY attempt, with no exclusion,
+  * the host re-decision itself equals the oracle on ordinary attempts too
+    (every attempt forced through it).
+
+Reference: planning_utils.cpp:562-635 (isValidState), :645-881 (pair checks),
+rrt.cpp:20-101 (newConfig / extend acceptance).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from global_body_planner_amd import _lib as L
+from global_body_planner_amd import terrain_data as td
+from tests.helpers import assert_pairs_equal, attempts_oracle, resolver, same_f64, u32
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+H_MIN, H_MAX, HL, HW, RH = 0.075, 0.4, 0.15, 0.15, 0.05
+MASK = np.uint32(~(L.F_FRAGILE | L.F_RESOLVED) & 0xFFFFFFFF)
+_cache = {}
+
+
+def pair_of(name):
+    import global_body_planner_amd as gbp
+    if name not in _cache:
+        data = td.by_name(name)
+        _cache[name] = (data, gbp.Terrain.from_data(data, device=0),
+                        oracle.OracleTerrain.from_data(data))
+    return _cache[name]
+
+
+def geometry(s):
+    """isValidState's lookup points (planning_utils.cpp:578-632) with numpy
+    trig: legs[4][3], corners[4][3], underside (x, y, z)."""
+    yaw = np.arctan2(s[4], s[3])
+    cy, sy, cp, sp = np.cos(yaw), np.sin(yaw), np.cos(s[6]), np.sin(s[6])
+    R = np.array([[cy * cp, -sy, cy * sp], [sy * cp, cy, sy * sp], [-sp, 0.0, cp]])
+    legs, corners = [], []
+    for xb in (-HL, HL):
+        for yb in (-HW, HW):
+            leg = s[:3] + R[:, 0] * xb + R[:, 1] * yb
+            legs.append(leg)
+            corners.append(leg + R[:, 2] * -RH)
+    under = s[:3] + R[:, 2] * -RH
+    return np.array(legs), np.array(corners), under
+
+
+def near_threshold_states(O, data, n_base, seed):
+    """Valid STANCE states moved onto a decision threshold: z shifted so the
+    binding H_MIN margin (a corner or the underside) or H_MAX margin (a leg)
+    is k ulps / +-1e-13 from zero, and x shifted so a leg lookup sits within
+    1e-13 of a grid line.  Returns (states, kind)."""
+    base, _ = O.sample_states(n_base, seed, 1, 0, L.STANCE, 256)
+    base = base[np.isfinite(base).all(1)]
+    out, kind = [], []
+    offsets = [k * 2.0 ** -53 for k in range(-6, 7)] + [-1e-13, 1e-13, -4e-13, 4e-13]
+    for s in base:
+        legs, corners, under = geometry(s)
+        pts = np.concatenate([legs[:, :2], corners[:, :2], under[None, :2]])
+        h, _ = O.height_batch(pts)
+        if not np.isfinite(h).all():
+            continue
+        m_min = min(np.min(corners[:, 2] - h[4:8] - H_MIN), under[2] - h[8] - H_MIN)
+        m_max = np.min(H_MAX - (legs[:, 2] - h[:4]))
+        for off in offsets:
+            a = s.copy()
+            a[2] = s[2] - m_min + off          # the lowest corner / underside onto H_MIN
+            out.append(a)
+            kind.append(0)
+            b = s.copy()
+            b[2] = s[2] + m_max + off          # the highest leg onto H_MAX (STANCE)
+            out.append(b)
+            kind.append(1)
+        # leg 0's x within 1e-13 of the grid line below it
+        i = int(np.searchsorted(data.x, legs[0, 0])) - 1
+        if 0 <= i < data.x.size - 1:
+            for eps in (-1e-13, 0.0, 1e-13):
+                c = s.copy()
+                c[0] = s[0] + (data.x[i] + eps - legs[0, 0])
+                out.append(c)
+                kind.append(2)
+    return np.array(out), np.array(kind)
+
+
+@pytest.mark.parametrize("name", ["synth-rough-256", "slope-gridmap"])
+def test_near_threshold_states(gpu, name):
+    data, T, O = pair_of(name)
+    st, kind = near_threshold_states(O, data, 60, 3)
+    assert st.shape[0] > 500
+    for phase in (L.STANCE, L.FLIGHT):
+        v, f, c = T.valid_states(torch.from_numpy(st), phase)
+        rv, rf, rc = O.valid_states(st, phase, nthreads=8)
+        gf = u32(f)
+        # every state whose binding margin the reference reaches is flagged
+        reach = (kind == 0) | ((kind == 1) & (phase == L.STANCE))
+        assert ((gf[reach] & L.F_FRAGILE) != 0).mean() > 0.95, (gf[reach] & L.F_FRAGILE).mean()
+        raw_diff = int((v.cpu().numpy() != rv).sum())
+        hv, hf, hc = T.valid_states_host(st, phase)
+        assert np.array_equal(hv, rv), np.flatnonzero(hv != rv)[:10]
+        assert np.array_equal(hf & MASK, rf & MASK)
+        assert np.array_equal(hc, rc)
+        nres = int(((hf & L.F_RESOLVED) != 0).sum())
+        assert nres >= int(((gf & L.F_FRAGILE) != 0).sum())
+        print(f"{name} phase {phase}: {st.shape[0]} near-threshold states, {nres} re-decided on the "
+              f"host, {raw_diff} raw kernel decisions differed from glibc, 0 after resolution")
+    # both sides of the threshold occur
+    rv, _, _ = O.valid_states(st, L.STANCE, nthreads=8)
+    assert 0 < rv[kind == 0].sum() < (kind == 0).sum()
+
+
+@pytest.mark.parametrize("name", ["synth-rough-256", "slope-gridmap"])
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_near_threshold_pairs_and_extends(gpu, name, adaptive):
+    """Pair checks whose first sample is a near-threshold state (a forward
+    stance sample at t = 0 and a reverse flight sample at t = -0 are the state
+    itself, H12), and extends from such states: the product's decisions
+    (host entries; _dev + resolve) equal the oracle's, no exclusion."""
+    data, T, O = pair_of(name)
+    st, _ = near_threshold_states(O, data, 40, 5)
+    n = st.shape[0]
+    s0, a, d, target, _ = attempts_oracle(O, n, seed=91)
+    ref = O.validate_pairs(st, a, d, adaptive=adaptive, nthreads=8)
+    host = T.validate_pairs_host(st, a, d, adaptive=adaptive)
+    nres = assert_pairs_equal(host, ref, "host", resolve=lambda g: g)
+    res = T.validate_pairs(torch.from_numpy(st), torch.from_numpy(a), torch.from_numpy(d),
+                           adaptive=adaptive)
+    gpu_t = (res.valid.cpu().numpy(), res.s_new.cpu().numpy(), res.t_new.cpu().numpy(),
+             u32(res.flags), u32(res.counts))
+    nres2 = assert_pairs_equal(gpu_t, ref, "dev+resolve", resolve=resolver(T, st, a, d, adaptive))
+    assert nres2 > n // 4, (nres2, n)
+    # extends from the near-threshold states (rrt.cpp:20-101), host entry
+    base = 77
+    rr_h, ch_h, sn_h, an_h, c_h, f_h = T.extend_host(st, target, d, seed=13, extend_base=base,
+                                                     adaptive=adaptive)
+    nrm = O.normal_batch(target[:, :2])[0]
+    dense = T.sample_actions(torch.from_numpy(np.repeat(nrm, 8, axis=0)), 13, 0x45585444,
+                             base * 8).cpu().numpy().reshape(n, 8, 10)
+    rr, rch, rsn, ran, rc = O.extend_batch(st, target, np.ascontiguousarray(dense[:, :6]), d,
+                                           adaptive=adaptive, nthreads=8)
+    assert np.array_equal(rr_h, rr) and np.array_equal(ch_h, rch) and np.array_equal(c_h, rc)
+    acc = rr != L.TRAPPED
+    assert np.all(same_f64(sn_h[acc], rsn[acc])) and np.all(same_f64(an_h[acc], ran[acc]))
+    assert ((f_h & L.F_RESOLVED) != 0).sum() > 0
+    print(f"{name} adaptive {adaptive}: {n} pairs ({nres} / {nres2} re-decided), "
+          f"{int(((f_h & L.F_RESOLVED) != 0).sum())} extends re-decided")
+
+
+@pytest.mark.parametrize("name", ["synth-rough-256", "rough_terrain-gridmap"])
+def test_host_recheck_equals_oracle_everywhere(gpu, name):
+    """The host re-decision pinned on ordinary attempts: every attempt of a
+    batch is marked FRAGILE and re-decided by gbp_resolve_fragile_host; all of
+    them must equal the oracle bit for bit (valid, s_new, t_new, flags, counts),
+    both directions, plain and adaptive."""
+    data, T, O = pair_of(name)
+    n = 12000
+    s, a, d, _, _ = attempts_oracle(O, n, seed=4321)
+    for adaptive in (False, True):
+        res = T.validate_pairs(torch.from_numpy(s), torch.from_numpy(a), torch.from_numpy(d),
+                               adaptive=adaptive)
+        gv = res.valid.cpu().numpy()
+        gsn = np.full((n, 8), np.nan)
+        gtn = np.full(n, np.nan)
+        gf = u32(res.flags) | np.uint32(L.F_FRAGILE)
+        gc = u32(res.counts)
+        ref = O.validate_pairs(s, a, d, adaptive=adaptive, nthreads=8)
+        k = assert_pairs_equal((gv, gsn, gtn, gf, gc), ref, f"all/ad{adaptive}",
+                               resolve=resolver(T, s, a, d, adaptive))
+        assert k == n

@@ -19,7 +19,7 @@ import oracle  # noqa: E402
 from global_body_planner_amd import _lib as L  # noqa: E402
 from global_body_planner_amd import terrain_data as td  # noqa: E402
 from global_body_planner_amd import workload as W  # noqa: E402
-from tests.helpers import assert_pairs_equal, u32  # noqa: E402
+from tests.helpers import assert_pairs_equal, resolver, u32  # noqa: E402
 
 
 def main():
@@ -53,7 +53,9 @@ def main():
                 ref = tuple(np.asarray(x)[keep] for x in ref)
                 label = f"{name} seed {seed} adaptive {int(adaptive)}"
                 try:
-                    nfrag = assert_pairs_equal(gpu_t, ref, label)
+                    sk, ak, dk = (x.cpu().numpy()[keep] for x in (s, act, d))
+                    nfrag = assert_pairs_equal(gpu_t, ref, label,
+                                               resolve=resolver(T, sk, ak, dk, adaptive))
                 except AssertionError as e:
                     print(f"MISMATCH {e}", flush=True)
                     sys.exit(1)
@@ -63,7 +65,7 @@ def main():
                 frag_total += nfrag
                 valid_total += nv
                 print(f"{label}: {m} attempts bit-exact, {nv} valid, {nfrag} fragile "
-                      f"(excluded from the decision compare) [{time.time() - t0:.0f} s]", flush=True)
+                      f"(re-decided on the host, then compared) [{time.time() - t0:.0f} s]", flush=True)
     print(f"TOTAL {total} attempts bit-exact vs oracle, {valid_total} valid, {frag_total} fragile",
           flush=True)
 
