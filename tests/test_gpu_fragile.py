@@ -70,7 +70,7 @@ def near_threshold_states(O, data, n_base, seed):
     for s in base:
         legs, corners, under = geometry(s)
         pts = np.concatenate([legs[:, :2], corners[:, :2], under[None, :2]])
-        h, _ = O.height_batch(pts)
+        h = O.height_batch(pts)[0]
         if not np.isfinite(h).all():
             continue
         m_min = min(np.min(corners[:, 2] - h[4:8] - H_MIN), under[2] - h[8] - H_MIN)
