@@ -29,13 +29,15 @@
 
 #include "gbp.h"
 #include "gbp_device.h"
+#include "gbp_lane.h"
+#include "gbp_internal.h"
 #include "host/gbp_host_check.h"
 
 using namespace gbp;
 
 namespace {
 
-constexpr uint64_t EXTEND_STREAM = 0x45585444ull;  // "EXTD"
+constexpr uint64_t EXTEND_STREAM = GBP_EXTEND_STREAM;
 constexpr int WAVE = 64;
 
 // CM == 1: the coordinate vectors are staged in LDS (bracket fix-up and the
@@ -157,316 +159,8 @@ __global__ __launch_bounds__(256, W) void k_validate_direct(
 // ============================================================================
 // K2 (persistent): per-sample state machine with lane re-packing
 // ============================================================================
-enum : int {
-  ST_IDLE = 0,
-  ST_FWD_STANCE = GBP_STAGE_FWD_STANCE,
-  ST_FWD_FLIGHT = GBP_STAGE_FWD_FLIGHT,
-  ST_FWD_LAND = GBP_STAGE_FWD_LAND,
-  ST_REV_FLIGHT = GBP_STAGE_REV_FLIGHT,
-  ST_REV_STANCE = GBP_STAGE_REV_STANCE,
-  ST_REV_START = GBP_STAGE_REV_START,
-};
-// deferred s_new: recomputed once at the end from (kind, param) — the same
-// closed form and the same operands the reference assigned it from
-enum : int { SN_NONE = 0, SN_STANCE_S = 1, SN_FLIGHT_B = 2, SN_STANCE_REV_B = 3 };
+// (lane state machine: gbp_lane.h)
 
-// Each lane's attempt (s[8], a[10]) lives in LDS, not in VGPRs: a row of
-// SA_ROW doubles per thread (odd stride: the 64 lanes' 8-byte reads hit
-// distinct bank pairs).  Freed registers keep the state check's in-flight
-// lookups out of scratch; tail helpers read their owner's row directly.
-constexpr int SA_ROW = 19;
-
-struct Lane {
-  double *s, *a;             // this lane's LDS row: input state and action (the
-                             // take-off state of the flight / reverse-stance
-                             // phases is recomputed per sample)
-  double t, ts, tpre;        // sample time, adaptive step, last success time
-  double snew_p, tnew;
-  int stage, snew_kind;
-  uint32_t f, tnew_set;
-  Acc acc;
-  int idx;
-};
-
-// enter a stage, skipping loops whose condition is false on entry
-__device__ __forceinline__ void enter_stage(Lane &L, int st) {
-  for (;;) {
-    L.f = (L.f & ~GBP_F_STAGE_MASK) | stage_bits((uint32_t)st);
-    L.stage = st;
-    L.ts = KINEMATICS_RES;
-    L.tpre = 0;
-    switch (st) {
-      case ST_FWD_STANCE:  // planning_utils.cpp:718
-        L.t = 0;
-        if (L.t <= L.a[6]) return;
-        st = ST_FWD_FLIGHT;
-        break;
-      case ST_FWD_FLIGHT:  // :732-735
-        L.t = 0;
-        if (L.t < L.a[7]) return;
-        st = ST_FWD_LAND;
-        break;
-      case ST_REV_FLIGHT:  // :842
-        L.t = 0;
-        if (L.t < L.a[7]) return;
-        st = ST_REV_STANCE;
-        break;
-      case ST_REV_STANCE:  // :849-852
-        L.t = L.a[6];
-        if (L.t >= 0) return;
-        st = ST_REV_START;
-        break;
-      default:  // FWD_LAND, REV_START: exactly one sample
-        return;
-    }
-  }
-}
-
-// the state the reference evaluates at time t of a stage (the take-off state
-// s_takeoff of :732 / :849 recomputed from (s, a): the same closed form and
-// operands, hence the same bits).
-//
-// Every stage but the reverse flight needs one stance closed form
-// (applyStance at t or t_s, or applyStanceReverse at t) and each of those has
-// eight divisions by 6 t_s / 2 t_s.  Lanes of one wave sit in different
-// stages, so the numerators are formed per stage (divergent, cheap), the
-// eight divisions run ONCE for the whole wave (converged), and the stage's
-// own sums finish the state — the expression trees of apply_stance /
-// apply_stance_reverse (gbp_device.h), split at the quotient.
-__device__ __forceinline__ void sample_state(const double *s_in, const double *a_in, int stage,
-                                             double t, double *o) {
-  double sv[8], a[10];
-#pragma unroll
-  for (int k = 0; k < 8; k++) sv[k] = s_in[k];
-#pragma unroll
-  for (int k = 0; k < 10; k++) a[k] = a_in[k];
-  if (stage == ST_REV_FLIGHT) {  // applyFlight(s, -t)
-    apply_flight(sv, -t, o);
-    return;
-  }
-  const bool rev = (stage == ST_REV_STANCE || stage == ST_REV_START);
-  const double t_s = a[6];
-  double b[8];  // the state the stance form starts from
-  double tt;    // its time argument
-  if (rev) {
-    apply_flight(sv, -a[7], b);  // s_to = applyFlight(s, -t_f)
-    tt = t;
-  } else {
-#pragma unroll
-    for (int k = 0; k < 8; k++) b[k] = sv[k];
-    tt = (stage == ST_FWD_STANCE) ? t : t_s;
-  }
-  // numerators: applyStance (a_to - a_td) * (t*t*t) and (a_to - a_td) * t * t;
-  // applyStanceReverse (a_to - a_td) * d3 and (a_to - a_td) * d2
-  const double d1 = t_s - tt, d2 = t_s * t_s - tt * tt, d3 = t_s * t_s * t_s - tt * tt * tt;
-  const double t3 = tt * tt * tt;
-  const int ax[4] = {0, 1, 2, 8}, ao[4] = {3, 4, 5, 9};
-  double n6[4], n2[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const double da = a[ao[k]] - a[ax[k]];
-    n6[k] = rev ? da * d3 : da * t3;
-    n2[k] = rev ? da * d2 : da * tt * tt;
-  }
-  // the eight divisions, once per wave
-  double q6[4], q2[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    q6[k] = n6[k] / (6.0 * t_s);
-    q2[k] = n2[k] / (2.0 * t_s);
-  }
-  if (rev) {  // planning_utils.cpp:348-364
-    const double cx = b[3] - a[0] * t_s - 0.5 * (a[3] - a[0]) * t_s;
-    const double cy = b[4] - a[1] * t_s - 0.5 * (a[4] - a[1]) * t_s;
-    const double cz = b[5] - a[2] * t_s - 0.5 * (a[5] - a[2]) * t_s;
-    const double cp = b[7] - a[8] * t_s - 0.5 * (a[9] - a[8]) * t_s;
-    o[0] = b[0] - cx * d1 - 0.5 * a[0] * d2 - q6[0];
-    o[1] = b[1] - cy * d1 - 0.5 * a[1] * d2 - q6[1];
-    o[2] = b[2] - cz * d1 - 0.5 * a[2] * d2 - q6[2];
-    o[3] = b[3] - a[0] * d1 - q2[0];
-    o[4] = b[4] - a[1] * d1 - q2[1];
-    o[5] = b[5] - a[2] * d1 - q2[2];
-    o[7] = b[7] - a[8] * d1 - q2[3];
-    o[6] = b[6] - cp * d1 - 0.5 * a[8] * d2 - q6[3];
-    return;
-  }
-  // planning_utils.cpp:262-271
-  double c[8];
-  c[0] = b[0] + b[3] * tt + 0.5 * a[0] * tt * tt + q6[0];
-  c[1] = b[1] + b[4] * tt + 0.5 * a[1] * tt * tt + q6[1];
-  c[2] = b[2] + b[5] * tt + 0.5 * a[2] * tt * tt + q6[2];
-  c[3] = b[3] + a[0] * tt + q2[0];
-  c[4] = b[4] + a[1] * tt + q2[1];
-  c[5] = b[5] + a[2] * tt + q2[2];
-  c[6] = b[6] + b[7] * tt + 0.5 * a[8] * tt * tt + q6[3];
-  c[7] = b[7] + a[8] * tt + q2[3];
-  if (stage == ST_FWD_STANCE) {
-#pragma unroll
-    for (int k = 0; k < 8; k++) o[k] = c[k];
-  } else {  // ST_FWD_FLIGHT / ST_FWD_LAND: applyFlight(applyStance(s, a), t)
-    apply_flight(c, t, o);
-  }
-}
-
-template <bool ADAPTIVE>
-__device__ __forceinline__ bool small_step(double ts) {
-  return !ADAPTIVE || (KINEMATICS_RES - 0.01 <= ts && ts <= KINEMATICS_RES + 0.01);
-}
-
-__device__ __forceinline__ int stage_phase(int st) {
-  return (st == ST_FWD_FLIGHT || st == ST_REV_FLIGHT) ? GBP_FLIGHT : GBP_STANCE;
-}
-// the sample time of a lane's current stage
-__device__ __forceinline__ double stage_time(const Lane &L) {
-  return L.stage == ST_FWD_LAND ? L.a[7] : (L.stage == ST_REV_START ? 0.0 : L.t);
-}
-
-// Advance (t, ts) the way a SUCCESSFUL sample of loop stage `st` does in
-// transition() below, and test the loop condition: the time of the next
-// sample if the current one passes.  false: the loop ends (or a one-sample
-// stage).  Used by tail helpers to evaluate an owner's future samples.
-template <bool ADAPTIVE>
-__device__ __forceinline__ bool advance_on_success(int st, const double *a, double &t, double &ts) {
-  switch (st) {
-    case ST_FWD_STANCE:
-      if (ADAPTIVE) { ts += KINEMATICS_RES; t += ts; } else { t += KINEMATICS_RES; }
-      return t <= a[6];
-    case ST_FWD_FLIGHT:
-    case ST_REV_FLIGHT:
-      if (ADAPTIVE) { ts += KINEMATICS_RES; t += ts; } else { t += KINEMATICS_RES; }
-      return t < a[7];
-    case ST_REV_STANCE:
-      if (ADAPTIVE) { ts += KINEMATICS_RES; t -= ts; } else { t -= KINEMATICS_RES; }
-      return t >= 0;
-    default:
-      return false;
-  }
-}
-
-// the reference's control flow after one isValidState result `ok` of the
-// lane's current stage; returns true when the pair is decided
-template <bool ADAPTIVE>
-__device__ __forceinline__ bool transition(Lane &L, bool ok) {
-  const double step = ADAPTIVE ? 0.0 : KINEMATICS_RES;  // plain loops: constant increment
-  switch (L.stage) {
-    case ST_FWD_STANCE:
-      if (!ok) {
-        if (small_step<ADAPTIVE>(L.ts)) {
-          L.snew_kind = SN_STANCE_S;
-          L.snew_p = (1.0 - BACKUP_RATIO) * L.t;
-          return true;
-        }
-        L.ts = KINEMATICS_RES;
-        L.t = L.tpre;
-        L.t += L.ts;
-      } else {
-        L.snew_kind = SN_STANCE_S;
-        L.snew_p = L.t;
-        L.tnew = L.t;
-        L.tnew_set = 1;
-        if (ADAPTIVE) {
-          L.ts += KINEMATICS_RES;
-          L.tpre = L.t;
-          L.t += L.ts;
-        } else {
-          L.t += step;
-        }
-      }
-      if (!(L.t <= L.a[6])) enter_stage(L, ST_FWD_FLIGHT);
-      return false;
-    case ST_FWD_FLIGHT:
-      if (!ok) return true;
-      if (ADAPTIVE) {
-        L.ts += KINEMATICS_RES;
-        L.tpre = L.t;
-        L.t += L.ts;
-      } else {
-        L.t += step;
-      }
-      if (!(L.t < L.a[7])) enter_stage(L, ST_FWD_LAND);
-      return false;
-    case ST_FWD_LAND:
-      if (!ok) return true;
-      L.snew_kind = SN_FLIGHT_B;
-      L.snew_p = L.a[7];
-      L.tnew = L.a[6] + L.a[7];
-      L.tnew_set = 1;
-      L.f |= GBP_F_VALID;
-      return true;
-    case ST_REV_FLIGHT:
-      if (!ok) return true;
-      if (ADAPTIVE) {
-        L.ts += KINEMATICS_RES;
-        L.tpre = L.t;
-        L.t += L.ts;
-      } else {
-        L.t += step;
-      }
-      if (!(L.t < L.a[7])) enter_stage(L, ST_REV_STANCE);
-      return false;
-    case ST_REV_STANCE:
-      if (!ok) {
-        if (small_step<ADAPTIVE>(L.ts)) {
-          L.snew_kind = SN_STANCE_S;  // forward stance on the end state (:857)
-          L.snew_p = L.t + BACKUP_RATIO * (L.a[6] - L.t);
-          return true;
-        }
-        L.ts = KINEMATICS_RES;
-        L.t = L.tpre;
-        L.t -= L.ts;
-      } else {
-        L.snew_kind = SN_STANCE_REV_B;
-        L.snew_p = L.t;
-        L.tnew = L.a[6] - L.t;
-        L.tnew_set = 1;
-        if (ADAPTIVE) {
-          L.ts += KINEMATICS_RES;
-          L.tpre = L.t;
-          L.t -= L.ts;
-        } else {
-          L.t -= step;
-        }
-      }
-      if (!(L.t >= 0)) enter_stage(L, ST_REV_START);
-      return false;
-    default:  // ST_REV_START
-      if (!ok) return true;
-      L.snew_kind = SN_STANCE_REV_B;
-      L.snew_p = 0;
-      L.tnew = L.a[6];
-      L.tnew_set = 1;
-      L.f |= GBP_F_VALID;
-      return true;
-  }
-}
-
-// index of the n-th (0-based) set bit of m; requires n < popcount(m)
-__device__ __forceinline__ int nth_set_bit(unsigned long long m, int n) {
-  int pos = 0;
-#pragma unroll
-  for (int w = 32; w >= 1; w >>= 1) {
-    const unsigned long long low = (1ull << w) - 1ull;
-    const int c = __popcll(m & low);
-    if (n >= c) {
-      n -= c;
-      m >>= w;
-      pos += w;
-    } else {
-      m &= low;
-    }
-  }
-  return pos;
-}
-
-// one sample of the lane's own attempt (the non-helper path)
-template <class ZT, bool ADAPTIVE>
-__device__ __forceinline__ bool step_lane(const TerrainView<ZT> &T, Lane &L) {
-  double sc[8];
-  sample_state(L.s, L.a, L.stage, stage_time(L), sc);
-  const bool ok = is_valid_state(T, sc, stage_phase(L.stage), L.acc);
-  if (L.acc.flags & GBP_F_LIMIT) return true;  // stopped: reported invalid
-  return transition<ADAPTIVE>(L, ok);
-}
 
 template <class ZT, bool ADAPTIVE, int W, int CM>
 __global__ __launch_bounds__(512, W) void k_validate_persistent(
@@ -890,114 +584,7 @@ __global__ __launch_bounds__(256) void k_neighbors(int64_t n_query, const double
 // ============================================================================
 // C ABI
 // ============================================================================
-struct gbp_terrain {
-  gbp_host::Terrain host;           // host copy (the values the device holds) for the
-                                    // glibc re-decision of FRAGILE attempts
-  int device = 0;
-  int nx = 0, ny = 0;
-  int storage = GBP_STORAGE_F64;
-  double bounds[4] = {0, 0, 0, 0};
-  double inv_hx = 0, inv_hy = 0;
-  int one_x = 0, one_y = 0;         // one-step bracket correction is exact (verified)
-  double *d_x = nullptr, *d_y = nullptr;
-  void *d_z = nullptr;
-  double *d_dx = nullptr, *d_dy = nullptr, *d_dz = nullptr;
-  int num_cus = 256;
-  int64_t opt_kernel = GBP_KERNEL_PERSISTENT;
-  int64_t opt_block = 256;
-  int64_t opt_waves = 2;            // register budget of the validate kernels (waves/SIMD)
-  int64_t opt_lds_coords = 1;       // stage the coordinate vectors in LDS when they fit
-  int64_t opt_helpers = 1;          // idle lanes of a drained wave evaluate owners' next samples
-  int64_t opt_affine = 1;           // compute coordinates when the affine form is exact
-  int64_t opt_fast_rcp = 1;         // cell-area reciprocal by verified Newton steps
-  double rcp_seed = 0;              // verified_rcp_seed (0: every spacing pair not exact)
-  int64_t opt_xcd_map = 0;          // persistent kernel: slices numbered XCD-major
-  int affine = 0;                   // host-verified affine coordinates (both axes)
-  int bx = 0, by = 0;
-  double ax = 0, hx = 0, ay = 0, hy = 0;
-  size_t lds_max = 65536;           // LDS bytes a workgroup may use
-  hipStream_t host_stream = nullptr;
-  void *ws = nullptr;               // grow-only device workspace
-  size_t ws_bytes = 0;
-  // extend-candidate workspaces, one per stream: _dev calls on one handle may
-  // run concurrently on different streams without sharing scratch
-  struct StreamWs {
-    hipStream_t stream;
-    void *ptr;
-    size_t bytes;
-  };
-  std::vector<StreamWs> cand_ws;
-};
-
 namespace {
-
-#define HIPCHK(expr)                      \
-  do {                                    \
-    hipError_t e_ = (expr);               \
-    if (e_ != hipSuccess) return GBP_E_HIP; \
-  } while (0)
-
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) (void)hipSetDevice(dev);
-  }
-  ~DeviceGuard() {
-    if (prev >= 0) (void)hipSetDevice(prev);
-  }
-};
-
-template <class ZT>
-TerrainView<ZT> view(const gbp_terrain *t) {
-  TerrainView<ZT> v;
-  v.x = t->d_x;
-  v.y = t->d_y;
-  v.z = (const ZT *)t->d_z;
-  v.dx = t->d_dx;
-  v.dy = t->d_dy;
-  v.dz = t->d_dz;
-  v.nx = t->nx;
-  v.ny = t->ny;
-  v.x0 = t->bounds[0];
-  v.xN = t->bounds[1];
-  v.y0 = t->bounds[2];
-  v.yN = t->bounds[3];
-  v.inv_hx = t->inv_hx;
-  v.inv_hy = t->inv_hy;
-  v.one_x = t->one_x;
-  v.one_y = t->one_y;
-  v.affine = t->affine;
-  v.bx = t->bx;
-  v.by = t->by;
-  v.ax = t->ax;
-  v.hx = t->hx;
-  v.ay = t->ay;
-  v.hy = t->hy;
-  v.rcp_seed = t->opt_fast_rcp ? t->rcp_seed : 0.0;
-  return v;
-}
-
-inline unsigned grid_for(int64_t n, int block, int cap = 65535 * 8) {
-  int64_t g = (n + block - 1) / block;
-  if (g < 1) g = 1;
-  if (g > cap) g = cap;
-  return (unsigned)g;
-}
-
-int ensure_ws(gbp_terrain *t, void **ws, size_t *have, size_t need) {
-  if (*have >= need) return GBP_OK;
-  if (*ws) (void)hipFree(*ws);
-  *ws = nullptr;
-  *have = 0;
-  size_t sz = std::max(need, (size_t)1 << 20);
-  if (hipMalloc(ws, sz) != hipSuccess) {
-    *ws = nullptr;
-    return GBP_E_ALLOC;
-  }
-  *have = sz;
-  return GBP_OK;
-}
 
 // coordinate mode of the hot kernels (gbp_device.h coord): LDS-staged vectors
 // when they fit (measured 1-2 % ahead of computing them at 1024^2), else the
@@ -1011,7 +598,8 @@ int coord_mode(const gbp_terrain *t, bool lds_ok) {
 template <class ZT, bool AD, int W, int CM>
 int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *a,
                       const uint8_t *dir, int dir_all, uint8_t *valid, double *s_new,
-                      double *t_new, uint32_t *flags, uint32_t *counts, hipStream_t st) {
+                      double *t_new, uint32_t *flags, uint32_t *counts, hipStream_t st,
+                      const int *n_dev) {
   const TerrainView<ZT> T = view<ZT>(t);
   const int block = (int)t->opt_block;
   const size_t coords = CM == 1 ? stage_bytes(t->nx, t->ny) : 0;
@@ -1024,7 +612,7 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
     double *sn = s_new ? s_new + 8 * off : nullptr;
     double *tn = t_new ? t_new + off : nullptr;
     uint32_t *c = counts ? counts + off : nullptr;
-    if (t->opt_kernel == GBP_KERNEL_DIRECT) {
+    if (t->opt_kernel == GBP_KERNEL_DIRECT && !n_dev) {
       // the direct form inlines the state check at five call sites: it gets the
       // whole register file (W = 1) whatever the persistent kernel's budget is
       const int db = std::min(block, 256);  // k_validate_direct: __launch_bounds__(256)
@@ -1037,7 +625,7 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
       const int64_t g = std::max<int64_t>(1, std::min<int64_t>(resident, (m + block - 1) / block));
       hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, CM>), dim3((unsigned)g), dim3(block),
                          coords + rows, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
-                         flags + off, c, (const int *)nullptr, (int)t->opt_helpers,
+                         flags + off, c, n_dev, (int)t->opt_helpers,
                          (int)t->opt_xcd_map);
     }
     HIPCHK(hipGetLastError());
@@ -1049,14 +637,14 @@ template <class ZT>
 int launch_validate(gbp_terrain *t, int64_t n, const double *s, const double *a,
                     const uint8_t *dir, int dir_all, int adaptive, uint8_t *valid,
                     double *s_new, double *t_new, uint32_t *flags, uint32_t *counts,
-                    hipStream_t st) {
+                    hipStream_t st, const int *n_dev = nullptr) {
 #define GBP_LV(AD, W)                                                                       \
   (cm == 2 ? launch_validate_w<ZT, AD, W, 2>(t, n, s, a, dir, dir_all, valid, s_new, t_new,  \
-                                             flags, counts, st)                              \
+                                             flags, counts, st, n_dev)                       \
    : cm == 1 ? launch_validate_w<ZT, AD, W, 1>(t, n, s, a, dir, dir_all, valid, s_new, t_new, \
-                                               flags, counts, st)                            \
+                                               flags, counts, st, n_dev)                     \
              : launch_validate_w<ZT, AD, W, 0>(t, n, s, a, dir, dir_all, valid, s_new, t_new, \
-                                               flags, counts, st))
+                                               flags, counts, st, n_dev))
   const int64_t w = t->opt_waves;
   // coordinates computed when the affine form is exact; else in LDS only if
   // they fit next to the attempt rows, with room for the W workgroups of 256
@@ -1065,7 +653,7 @@ int launch_validate(gbp_terrain *t, int64_t n, const double *s, const double *a,
   const size_t per_cu = std::max<int64_t>(1, (int64_t)w * 256 / t->opt_block) *
                         (stage_bytes(t->nx, t->ny) + rows);
   const bool lds_ok = t->opt_lds_coords && stage_bytes(t->nx, t->ny) + rows <= t->lds_max &&
-                      (t->opt_kernel == GBP_KERNEL_DIRECT || per_cu <= 160 * 1024);
+                      ((t->opt_kernel == GBP_KERNEL_DIRECT && !n_dev) || per_cu <= 160 * 1024);
   const int cm = coord_mode(t, lds_ok);
   // W = 1 and 2 give the same allocation (the kernel needs < 256 VGPRs)
   if (adaptive) return w >= 4 ? GBP_LV(true, 4) : (w == 3 ? GBP_LV(true, 3) : GBP_LV(true, 2));
@@ -1177,6 +765,18 @@ struct Stage {
 size_t rnd(size_t b) { return (b + 255) & ~(size_t)255; }
 
 }  // namespace
+
+__attribute__((visibility("hidden"))) int gbp_internal_validate_dev_n(
+    gbp_terrain *t, int64_t n_max, const int *n_dev, const double *s, const double *a,
+    const uint8_t *dir, int dir_all, int adaptive, uint8_t *valid, double *s_new, double *t_new,
+    uint32_t *flags, uint32_t *counts, hipStream_t st) {
+  if (n_max <= 0) return GBP_OK;
+  if (t->storage == GBP_STORAGE_F32)
+    return launch_validate<float>(t, n_max, s, a, dir, dir_all, adaptive, valid, s_new, t_new,
+                                  flags, counts, st, n_dev);
+  return launch_validate<double>(t, n_max, s, a, dir, dir_all, adaptive, valid, s_new, t_new,
+                                 flags, counts, st, n_dev);
+}
 
 extern "C" {
 
@@ -1555,7 +1155,7 @@ int gbp_extend_batch_dev(gbp_terrain *t, int64_t n, const double *s_near, const 
   // a grown workspace may still be read by this stream's earlier launches:
   // ensure_ws frees the old one only after the stream has drained it
   if (w->bytes < need) HIPCHK(hipStreamSynchronize(st));
-  int rc = ensure_ws(t, &w->ptr, &w->bytes, need);
+  int rc = ensure_ws(&w->ptr, &w->bytes, need);
   if (rc) return rc;
   char *p = (char *)w->ptr;
   double *cs = (double *)p; p += (size_t)m * 8 * sizeof(double);
@@ -1629,7 +1229,7 @@ int gbp_height_batch_host(gbp_terrain *t, int64_t n, const double *xy, double *h
   if (n <= 0) return n == 0 ? GBP_OK : GBP_E_INVALID_ARG;
   DeviceGuard g(t->device);
   hipStream_t st = t->host_stream;
-  int rc = ensure_ws(t, &t->ws, &t->ws_bytes, rnd(16 * n) + rnd(8 * n) + 2 * rnd(n) + 1024);
+  int rc = ensure_ws(&t->ws, &t->ws_bytes, rnd(16 * n) + rnd(8 * n) + 2 * rnd(n) + 1024);
   if (rc) return rc;
   Stage S{t, (char *)t->ws};
   double *dxy = S.take<double>(2 * n), *dh = S.take<double>(n);
@@ -1651,7 +1251,7 @@ int gbp_normal_batch_host(gbp_terrain *t, int64_t n, const double *xy, double *n
   if (!normal) return GBP_E_INVALID_ARG;
   DeviceGuard g(t->device);
   hipStream_t st = t->host_stream;
-  int rc = ensure_ws(t, &t->ws, &t->ws_bytes, rnd(16 * n) + rnd(24 * n) + rnd(n) + 1024);
+  int rc = ensure_ws(&t->ws, &t->ws_bytes, rnd(16 * n) + rnd(24 * n) + rnd(n) + 1024);
   if (rc) return rc;
   Stage S{t, (char *)t->ws};
   double *dxy = S.take<double>(2 * n), *dn = S.take<double>(3 * n);
@@ -1671,7 +1271,7 @@ int gbp_valid_states_host(gbp_terrain *t, int64_t n, const double *states, const
   if (n <= 0) return n == 0 ? GBP_OK : GBP_E_INVALID_ARG;
   DeviceGuard g(t->device);
   hipStream_t st = t->host_stream;
-  int rc = ensure_ws(t, &t->ws, &t->ws_bytes,
+  int rc = ensure_ws(&t->ws, &t->ws_bytes,
                      rnd(64 * n) + 2 * rnd(n) + 2 * rnd(4 * n) + 2048);
   if (rc) return rc;
   Stage S{t, (char *)t->ws};
@@ -1701,7 +1301,7 @@ int gbp_validate_pairs_host(gbp_terrain *t, int64_t n, const double *s, const do
   if (!s || !a) return GBP_E_INVALID_ARG;
   DeviceGuard g(t->device);
   hipStream_t st = t->host_stream;
-  int rc = ensure_ws(t, &t->ws, &t->ws_bytes,
+  int rc = ensure_ws(&t->ws, &t->ws_bytes,
                      rnd(64 * n) + rnd(80 * n) + rnd(64 * n) + rnd(8 * n) + 2 * rnd(n) +
                          2 * rnd(4 * n) + 4096);
   if (rc) return rc;
@@ -1750,7 +1350,7 @@ int gbp_extend_batch_host(gbp_terrain *t, int64_t n, const double *s_near, const
   if (!s_near || !target || !result || !s_new || !a_new) return GBP_E_INVALID_ARG;
   DeviceGuard g(t->device);
   hipStream_t st = t->host_stream;
-  int rc = ensure_ws(t, &t->ws, &t->ws_bytes,
+  int rc = ensure_ws(&t->ws, &t->ws_bytes,
                      3 * rnd(64 * n) + rnd(80 * n) + rnd(n) + 4 * rnd(4 * n) + 4096);
   if (rc) return rc;
   Stage S{t, (char *)t->ws};
@@ -1793,7 +1393,7 @@ int gbp_sample_states_host(gbp_terrain *t, int64_t n, uint64_t seed, uint64_t st
   if (!states) return GBP_E_INVALID_ARG;
   DeviceGuard g(t->device);
   hipStream_t st = t->host_stream;
-  int rc = ensure_ws(t, &t->ws, &t->ws_bytes, rnd(64 * n) + rnd(4 * n) + 1024);
+  int rc = ensure_ws(&t->ws, &t->ws_bytes, rnd(64 * n) + rnd(4 * n) + 1024);
   if (rc) return rc;
   Stage S{t, (char *)t->ws};
   double *ds = S.take<double>(8 * n);
@@ -1814,7 +1414,7 @@ int gbp_sample_actions_host(gbp_terrain *t, int64_t n, const double *normals, ui
   if (!normals || !actions) return GBP_E_INVALID_ARG;
   DeviceGuard g(t->device);
   hipStream_t st = t->host_stream;
-  int rc = ensure_ws(t, &t->ws, &t->ws_bytes, rnd(24 * n) + rnd(80 * n) + 1024);
+  int rc = ensure_ws(&t->ws, &t->ws_bytes, rnd(24 * n) + rnd(80 * n) + 1024);
   if (rc) return rc;
   Stage S{t, (char *)t->ws};
   double *dn = S.take<double>(3 * n), *da = S.take<double>(10 * n);
