@@ -14,12 +14,13 @@ from . import _lib
 from ._lib import (ADVANCED, FLIGHT, FORWARD, REACHED, REVERSE, STANCE, TRAPPED, GbpError,
                    KERNEL_DIRECT, KERNEL_PERSISTENT)
 from .terrain_data import TerrainData, csv_gridmap, csv_direct, synth_rough, synth_fractal
-from .engine import Terrain, PairResult, ExtendResult, nearest, neighbors, device_count
+from .engine import (Terrain, PairResult, ExtendResult, DeviceTree, PlanWorkspace, nearest,
+                     neighbors, device_count)
 
 __all__ = [
     "ADVANCED", "FLIGHT", "FORWARD", "REACHED", "REVERSE", "STANCE", "TRAPPED", "GbpError",
     "KERNEL_DIRECT", "KERNEL_PERSISTENT", "TerrainData", "csv_gridmap", "csv_direct",
-    "synth_rough", "synth_fractal", "Terrain", "PairResult", "ExtendResult", "nearest",
-    "neighbors", "device_count",
+    "synth_rough", "synth_fractal", "Terrain", "PairResult", "ExtendResult", "DeviceTree",
+    "PlanWorkspace", "nearest", "neighbors", "device_count",
 ]
-__version__ = "0.1.0"
+__version__ = "0.2.0"

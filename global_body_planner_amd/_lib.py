@@ -41,6 +41,12 @@ EXPORTS = [
     "gbp_nearest_batch_dev", "gbp_nearest_batch_host",
     "gbp_neighbors_batch_dev", "gbp_neighbors_batch_host",
     "gbp_resolve_fragile_host", "gbp_resolve_fragile_states_host", "gbp_extend_resolve_host",
+    "gbp_stream_create", "gbp_stream_destroy",
+    "gbp_tree_create", "gbp_tree_destroy", "gbp_tree_init", "gbp_tree_reserve", "gbp_tree_capacity",
+    "gbp_tree_size", "gbp_tree_read", "gbp_tree_append_host", "gbp_tree_device_ptrs",
+    "gbp_plan_ws_create", "gbp_plan_ws_destroy", "gbp_plan_reset", "gbp_plan_half_dev",
+    "gbp_plan_status_read", "gbp_plan_resolve_host", "gbp_extend_tree_dev",
+    "gbp_extend_tree_finish_dev", "gbp_extend_tree_host",
 ]
 
 
@@ -100,6 +106,26 @@ def load(path=None):
         "gbp_resolve_fragile_host": (I, [P, I64, P, P, P, I, I, P, P, P, P, P, P]),
         "gbp_resolve_fragile_states_host": (I, [P, I64, P, P, I, P, P, P, P]),
         "gbp_extend_resolve_host": (I, [P, I64, P, P, P, I, I, U64, I64, P, P, P, P, P, P, P]),
+        "gbp_stream_create": (I, [I, P]),
+        "gbp_stream_destroy": (I, [P]),
+        "gbp_tree_create": (I, [I, I64, P]),
+        "gbp_tree_destroy": (I, [P]),
+        "gbp_tree_init": (I, [P, P, P]),
+        "gbp_tree_reserve": (I, [P, I64, P]),
+        "gbp_tree_capacity": (I, [P, P]),
+        "gbp_tree_size": (I, [P, P, P]),
+        "gbp_tree_read": (I, [P, I64, I64, P, P, P, P, P]),
+        "gbp_tree_append_host": (I, [P, I64, P, P, P, P]),
+        "gbp_tree_device_ptrs": (I, [P, P, P]),
+        "gbp_plan_ws_create": (I, [P, I64, P]),
+        "gbp_plan_ws_destroy": (I, [P]),
+        "gbp_plan_reset": (I, [P, I64, P]),
+        "gbp_plan_half_dev": (I, [P, P, P, P, ctypes.c_int32, I, I64, U64, U64, I64, I, I, P]),
+        "gbp_plan_status_read": (I, [P, P, P]),
+        "gbp_plan_resolve_host": (I, [P, P, P, P, I, I64, I, P, P, P]),
+        "gbp_extend_tree_dev": (I, [P, P, P, I64, P, P, I, I, U64, I64, P, P, P]),
+        "gbp_extend_tree_finish_dev": (I, [P, P, P, I64, I, P, P, P]),
+        "gbp_extend_tree_host": (I, [P, P, P, I64, P, I, I, U64, I64, P, P, P]),
         "gbp_nearest_batch_dev": (I, [I64, P, I64, P, P, P, P]),
         "gbp_nearest_batch_host": (I, [I64, P, I64, P, P, P]),
         "gbp_neighbors_batch_dev": (I, [I64, P, I64, P, ctypes.c_double, I, P, P, P]),

@@ -1,0 +1,1301 @@
+// gbp_plan.hip — device-resident trees and the batch-synchronous RRT-Connect
+// half-iteration as one stream-ordered kernel sequence (SURVEY §8(f) row 1,
+// §8(b) items 4-5).
+//
+// One half-iteration of RRTConnectClass::runRRTConnect at batch B
+// (rrt_connect.cpp:246-312, the batched form of csrc/host/gbp_planner.cpp
+// RRTConnectClass::extendBatch + connectBatch), tree T extended toward B
+// random targets, every new vertex connected to the other tree O:
+//
+//   stage 0  k_targets          B draws of PlannerClass::randomState
+//                               (planner_class.cpp:38-76) + isValidState(STANCE)
+//   stage 1  k_compact_targets  the valid targets, in draw order
+//   stage 2  k_nn_partial/k_nn_reduce   getNearestNeighbor in T (planner_class.cpp:185-200)
+//            k_extend_prep      newConfig's 6 candidate actions (rrt.cpp:25-50)
+//            k_validate_persistent (gbp_engine.hip)  the candidates' pair checks
+//            k_select           newConfig's first valid candidate + acceptance (rrt.cpp:52-68)
+//   stage 3  k_append          non-TRAPPED successors appended to T in target order
+//                               (rrt.cpp:86-92; graph_class.cpp:28-42)
+//   stage 4  k_nn_partial/k_nn_reduce   the new vertices' nearest vertex in O
+//            k_connect          RRTConnectClass::attemptConnect (rrt_connect.cpp:20-91),
+//                               one wave per connection, the wave's 64 lanes
+//                               evaluating the pair check's samples together
+//   stage 5  k_append          non-TRAPPED connections appended to O in order;
+//                               the first REACHED one ends the search
+//
+// Every count (targets, candidates, appended vertices) stays on the device:
+// the host enqueues many half-iterations and reads one small status record
+// per group.  The appends are ordered compactions: a wave ballot + popcount
+// ranks a workgroup's kept items, the workgroups chain their counts with a
+// decoupled look-back (Merrill & Garland, "Single-pass parallel prefix scan
+// with decoupled look-back", 2016), so vertices land in exactly the order of
+// the host planner's insertion loop.
+//
+// FRAGILE decisions (gbp.h) stop the sequence at the next gate: the kernel
+// that meets one sets status.halt; every later kernel of the group returns at
+// once; the host re-decides the flagged items with glibc
+// (gbp_plan_resolve_host), patches the stage's outputs, and resumes.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "gbp.h"
+#include "gbp_device.h"
+#include "gbp_internal.h"
+#include "gbp_lane.h"
+
+using namespace gbp;
+
+// ============================================================================
+// handles
+// ============================================================================
+struct gbp_tree {
+  int device = 0;
+  int64_t cap = 0;
+  double *v = nullptr;        // [cap][8] vertex states (GraphClass vertices)
+  double *a = nullptr;        // [cap][10] the action that reached each vertex
+  double *g = nullptr;        // [cap] cost to come: g[parent] + poseDistance
+  int32_t *parent = nullptr;  // [cap], -1 at the root
+  int32_t *count = nullptr;   // [1] number of vertices (device resident)
+};
+
+struct gbp_plan_ws {
+  int device = 0;
+  int64_t bmax = 0;            // largest batch of draws per half-iteration
+  gbp_plan_status *st = nullptr;
+  unsigned long long *tiles = nullptr;  // look-back tile states
+  uint32_t epoch = 0;          // per-compaction tag of the tile states
+  int64_t ntiles = 0;
+  // stage 0-1
+  double *cand = nullptr;      // [bmax][8] drawn states
+  uint32_t *cflag = nullptr;   // [bmax] their isValidState flags
+  double *targets = nullptr;   // [bmax][8] the valid ones, in draw order
+  // stage 2-3
+  int32_t *nn = nullptr;       // [bmax] nearest vertex of T per target
+  double *cs = nullptr;        // [6 bmax][8] candidate s_near
+  double *ca = nullptr;        // [6 bmax][10] candidate actions
+  double *csn = nullptr;       // [6 bmax][8] candidate s_new
+  uint32_t *cf = nullptr;      // [6 bmax] candidate flags
+  uint32_t *cc = nullptr;      // [6 bmax] candidate counts
+  int32_t *eres = nullptr;     // [bmax] extend result
+  int32_t *echo = nullptr;     // [bmax] chosen candidate
+  double *esn = nullptr;       // [bmax][8]
+  double *ean = nullptr;       // [bmax][10]
+  uint32_t *ef = nullptr;      // [bmax] extend flags
+  int32_t *evtx = nullptr;     // [bmax] new vertex index (or -1)
+  // stage 4-5
+  int32_t *nno = nullptr;      // [bmax] nearest vertex of O per new vertex
+  int32_t *kres = nullptr;     // [bmax] connect result
+  double *ksn = nullptr;       // [bmax][8]
+  double *kan = nullptr;       // [bmax][10]
+  uint32_t *kf = nullptr;      // [bmax] connect flags
+  // nearest-neighbour partials: [NN_MAX_CHUNKS][bmax]
+  double *nn_d = nullptr;
+  int32_t *nn_i = nullptr;
+  void *block = nullptr;       // the one allocation all of the above live in
+};
+
+namespace {
+
+constexpr int WAVE = 64;
+constexpr int TB = 256;            // threads of the grid-stride kernels
+constexpr int CB = 1024;           // threads (items) per look-back tile
+constexpr int NN_QT = 256;         // queries per nearest-neighbour tile
+constexpr int NN_MAX_CHUNKS = 32;  // vertex chunks per query tile
+constexpr uint32_t LOOKBACK_SPIN_LIMIT = 1u << 24;
+
+// the gate every planner kernel checks first: a FRAGILE halt or a found
+// connection makes the rest of the enqueued sequence a no-op
+__device__ __forceinline__ bool gated(const gbp_plan_status *st) {
+  return (st->halt | st->done) != 0u;
+}
+
+__device__ __forceinline__ double pose_distance(const double *q1, const double *q2) {
+  double sum = 0;  // planning_utils.cpp:106-115
+#pragma unroll
+  for (int i = 0; i < 3; i++) sum = sum + (q2[i] - q1[i]) * (q2[i] - q1[i]);
+  return sqrt(sum);
+}
+
+__device__ __forceinline__ void copy8(double *d, const double *s) {
+#pragma unroll
+  for (int k = 0; k < 8; k++) d[k] = s[k];
+}
+__device__ __forceinline__ void copy10(double *d, const double *s) {
+#pragma unroll
+  for (int k = 0; k < 10; k++) d[k] = s[k];
+}
+
+// ---- ordered compaction across the grid ---------------------------------------
+// Block b of a CB-thread grid keeps the items whose `keep` is set; returns the
+// item's rank among all kept items of the grid (blocks in order, threads in
+// order within a block).  Tile states are 64-bit words (epoch | flag | count),
+// published and polled with agent-scope atomic RMW operations (executed at
+// memory, coherent across the XCDs' L2s).  Every block of the grid must call
+// this exactly once.  The grid must be resident at once (callers launch at
+// most a few hundred 1024-thread blocks).  *total gets the grid's total
+// (written by the last block).
+__device__ __forceinline__ unsigned long long tile_word(uint32_t epoch, uint32_t flag, uint32_t v) {
+  return ((unsigned long long)epoch << 32) | ((unsigned long long)flag << 30) | (v & 0x3FFFFFFFu);
+}
+
+__device__ uint32_t ordered_rank(bool keep, unsigned long long *tiles, uint32_t epoch,
+                                 int32_t *total, gbp_plan_status *st) {
+  __shared__ uint32_t wsum[CB / WAVE];
+  __shared__ uint32_t s_excl;
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  const unsigned long long m = __ballot(keep);
+  const uint32_t wr = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+  __syncthreads();
+  uint32_t woff = 0, bsum = 0;
+  for (int i = 0; i < (int)(blockDim.x / WAVE); i++) {
+    if (i < w) woff += wsum[i];
+    bsum += wsum[i];
+  }
+  if (threadIdx.x == 0) {
+    const uint32_t b = blockIdx.x;
+    uint32_t excl = 0;
+    if (b > 0) {
+      __hip_atomic_exchange(&tiles[b], tile_word(epoch, 1, bsum), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+      int j = (int)b - 1;
+      uint32_t spins = 0;
+      for (;;) {
+        const unsigned long long x =
+            __hip_atomic_fetch_add(&tiles[j], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t flag = (uint32_t)(x >> 30) & 3u;
+        if ((uint32_t)(x >> 32) != epoch || flag == 0) {
+          if (++spins > LOOKBACK_SPIN_LIMIT) {  // bounded: report, never hang
+            atomicOr(&st->error, 1u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+          continue;
+        }
+        excl += (uint32_t)(x & 0x3FFFFFFFu);
+        if (flag == 2 || j == 0) break;
+        --j;
+      }
+    }
+    __hip_atomic_exchange(&tiles[b], tile_word(epoch, 2, excl + bsum), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+    s_excl = excl;
+    if (b == gridDim.x - 1) *total = (int32_t)(excl + bsum);
+  }
+  __syncthreads();
+  return s_excl + woff + wr;
+}
+
+// ============================================================================
+// stage 0-1: targets
+// ============================================================================
+template <class ZT>
+__global__ __launch_bounds__(TB) void k_targets(TerrainView<ZT> T, gbp_plan_status *st, int64_t n,
+                                                uint64_t seed, uint64_t stream_id, int64_t base,
+                                                double *__restrict__ cand,
+                                                uint32_t *__restrict__ cflag, int32_t half) {
+  if (gated(st)) return;
+  bool frag = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double q[8];
+    sample_state_try(T, seed, stream_id, base + i, 0, q);  // randomState, one try
+    Acc acc{0, 0, 0};
+    const bool v = is_valid_state(T, q, GBP_STANCE, acc);   // rrt_connect.cpp:254
+    copy8(cand + 8 * i, q);
+    cflag[i] = acc.flags | (v ? GBP_F_VALID : 0u);
+    frag = frag || (acc.flags & GBP_F_FRAGILE);
+  }
+  if (__ballot(frag) && (threadIdx.x & (WAVE - 1)) == 0) {
+    atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_TARGETS);
+    st->halt_half = half;
+  }
+}
+
+__global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int64_t n,
+                                                        const double *__restrict__ cand,
+                                                        const uint32_t *__restrict__ cflag,
+                                                        double *__restrict__ targets,
+                                                        unsigned long long *tiles, uint32_t epoch) {
+  if (gated(st)) return;
+  const int64_t i = blockIdx.x * (int64_t)CB + threadIdx.x;
+  const bool keep = i < n && (cflag[i] & GBP_F_VALID);
+  const uint32_t r = ordered_rank(keep, tiles, epoch, &st->n_targets, st);
+  if (keep) copy8(targets + 8 * (size_t)r, cand + 8 * i);
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    // the extend stream of this half: RRTClass::extend_counter_ advances by
+    // the number of extends (csrc/host/gbp_planner.cpp extendBatch)
+    st->ext_base = st->ext_counter;
+    st->ext_counter += st->n_targets;
+    st->stat_targets += st->n_targets;
+  }
+}
+
+// ============================================================================
+// nearest neighbour in a device tree (planner_class.cpp:185-200)
+// ============================================================================
+// Work item (query tile qt, vertex chunk c): 256 queries (one per thread)
+// against the chunk's vertices streamed through LDS; best (distance, index)
+// per query and chunk into the partial arrays.  The chunk size is set from the
+// tree size on the device so a tile never needs more than NN_MAX_CHUNKS.
+// stateDistance's sqrt is taken only when the squared sum improves: sqrt is
+// monotone, so sum >= best_sum can never give a strictly smaller distance,
+// and equal square roots keep the earlier vertex (the strict <).
+__device__ __forceinline__ int64_t nn_chunk(int64_t nv) {
+  int64_t c = (nv + NN_MAX_CHUNKS - 1) / NN_MAX_CHUNKS;
+  c = (c + 255) & ~(int64_t)255;
+  return c < 256 ? 256 : c;
+}
+
+__global__ __launch_bounds__(TB) void k_nn_partial(const gbp_plan_status *st, const int32_t *nq_dev,
+                                                   const double *__restrict__ q,
+                                                   const int32_t *q_off_dev,
+                                                   const double *__restrict__ v,
+                                                   const int32_t *nv_dev, int64_t bmax,
+                                                   double *__restrict__ pd,
+                                                   int32_t *__restrict__ pi) {
+  if (gated(st)) return;
+  __shared__ double tile[NN_QT * 8];
+  const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
+  const int64_t ch = nn_chunk(nv);
+  const int64_t nch = (nv + ch - 1) / ch, nqt = (nq + NN_QT - 1) / NN_QT;
+  for (int64_t item = blockIdx.x; item < nqt * nch; item += gridDim.x) {
+    const int64_t qt = item / nch, c = item - qt * nch;
+    const int64_t qi = qt * NN_QT + threadIdx.x;
+    const bool live = qi < nq;
+    double qq[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) qq[k] = live ? q[8 * (q_off + qi) + k] : 0.0;
+    double best = INFINITY, best_sum = INFINITY;
+    int bi = -1;
+    const int64_t v0 = c * ch, v1 = min(nv, v0 + ch);
+    for (int64_t j0 = v0; j0 < v1; j0 += NN_QT) {
+      const int cnt = (int)min<int64_t>(NN_QT, v1 - j0);
+      __syncthreads();
+      for (int e = threadIdx.x; e < cnt * 8; e += blockDim.x) tile[e] = v[8 * j0 + e];
+      __syncthreads();
+      for (int j = 0; j < cnt; j++) {
+        double sum = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const double d = tile[8 * j + k] - qq[k];
+          sum = sum + 1.0 * d * d;  // stateDistance(q, vertex), planning_utils.cpp:116-127
+        }
+        if (sum < best_sum) {
+          const double dist = sqrt(sum);
+          if (dist < best) {
+            best = dist;
+            best_sum = sum;
+            bi = (int)(j0 + j);
+          }
+        }
+      }
+    }
+    if (live) {
+      pd[c * bmax + qi] = best;
+      pi[c * bmax + qi] = bi;
+    }
+  }
+}
+
+// chunks in index order, strict <: the lowest index among equal distances;
+// nothing < inf (a NaN query): index 0, as the reference keeps it
+__global__ __launch_bounds__(TB) void k_nn_reduce(const gbp_plan_status *st, const int32_t *nq_dev,
+                                                  const int32_t *nv_dev, int64_t bmax,
+                                                  const double *__restrict__ pd,
+                                                  const int32_t *__restrict__ pi,
+                                                  int32_t *__restrict__ out) {
+  if (gated(st)) return;
+  const int64_t nq = *nq_dev, nv = *nv_dev;
+  const int64_t ch = nn_chunk(nv), nch = (nv + ch - 1) / ch;
+  for (int64_t qi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; qi < nq;
+       qi += (int64_t)gridDim.x * blockDim.x) {
+    double best = INFINITY;
+    int bi = 0;
+    for (int64_t c = 0; c < nch; c++) {
+      const double d = pd[c * bmax + qi];
+      if (d < best) {
+        best = d;
+        bi = pi[c * bmax + qi];
+      }
+    }
+    out[qi] = bi;
+  }
+}
+
+// ============================================================================
+// stage 2: newConfig (rrt.cpp:20-70)
+// ============================================================================
+template <class ZT>
+__global__ __launch_bounds__(TB) void k_extend_prep(TerrainView<ZT> T, gbp_plan_status *st,
+                                                    const double *__restrict__ targets,
+                                                    const int32_t *__restrict__ nn,
+                                                    const double *__restrict__ tv, uint64_t seed,
+                                                    double *__restrict__ cs,
+                                                    double *__restrict__ ca) {
+  if (gated(st)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->n_validate = 0;  // the validate launch idles
+    return;
+  }
+  const int64_t n = st->n_targets, m = n * GBP_NUM_GEN_STATES, base = st->ext_base;
+  if (blockIdx.x == 0 && threadIdx.x == 0) st->n_validate = (int32_t)m;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < m;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = c / GBP_NUM_GEN_STATES;
+    const int j = (int)(c - i * GBP_NUM_GEN_STATES);
+    double nv[3];
+    surface_normal(T, targets[8 * i], targets[8 * i + 1], nv);  // rrt.cpp:25
+    double a[10];
+    sample_action(nv, seed, GBP_EXTEND_STREAM, (base + i) * 8 + j, a);  // rrt.cpp:34, :49
+    copy10(ca + 10 * c, a);
+    copy8(cs + 8 * c, tv + 8 * (int64_t)nn[i]);
+  }
+}
+
+// the first valid candidate (rrt.cpp:36-50) and the closer-than-s_near
+// acceptance (rrt.cpp:52-68, :84-101)
+__global__ __launch_bounds__(TB) void k_select(gbp_plan_status *st, const double *__restrict__ targets,
+                                               const int32_t *__restrict__ nn,
+                                               const double *__restrict__ tv,
+                                               const double *__restrict__ ca,
+                                               const double *__restrict__ csn,
+                                               const uint32_t *__restrict__ cf,
+                                               int32_t *__restrict__ eres,
+                                               int32_t *__restrict__ echo,
+                                               double *__restrict__ esn, double *__restrict__ ean,
+                                               uint32_t *__restrict__ ef, int32_t half) {
+  if (gated(st)) return;
+  const int64_t n = st->n_targets;
+  bool frag = false;
+  unsigned long long executed = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double sn[8], tg[8], sv[8];
+    copy8(sn, tv + 8 * (int64_t)nn[i]);
+    copy8(tg, targets + 8 * i);
+    int found = -1;
+    uint32_t fl = 0;
+    for (int j = 0; j < GBP_NUM_GEN_STATES; j++) {
+      const uint32_t f = cf[i * GBP_NUM_GEN_STATES + j];
+      fl |= f & (GBP_F_VALID | GBP_F_OOD | GBP_F_NAN | GBP_F_FRAGILE | GBP_F_LIMIT);
+      if (f & GBP_F_VALID) {
+        found = j;
+        break;
+      }
+    }
+    executed += found >= 0 ? found + 1 : GBP_NUM_GEN_STATES;
+    const double d0 = state_distance(sn, tg);
+    double best = d0;
+    int r = GBP_TRAPPED;
+    if (found >= 0) {
+      const int64_t c = i * GBP_NUM_GEN_STATES + found;
+      copy8(sv, csn + 8 * c);
+      const double cur = state_distance(sv, tg);
+      if (cur < best) {
+        best = cur;
+        copy8(esn + 8 * i, sv);
+        copy10(ean + 10 * i, ca + 10 * c);
+        r = (cur <= GOAL_BOUNDS) ? GBP_REACHED : GBP_ADVANCED;  // isWithinBounds(s_new, s)
+      }
+    }
+    eres[i] = r;
+    echo[i] = found;
+    ef[i] = fl;
+    frag = frag || (fl & GBP_F_FRAGILE);
+  }
+  // one atomic per wave for the statistics and the gate
+  const int lane = threadIdx.x & (WAVE - 1);
+  for (int off = WAVE / 2; off > 0; off >>= 1) executed += __shfl_down(executed, off);
+  if (lane == 0 && executed) atomicAdd((unsigned long long *)&st->stat_attempts, executed);
+  if (__ballot(frag) && lane == 0) {
+    atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_EXTEND);
+    st->halt_half = half;
+  }
+}
+
+// ============================================================================
+// stages 3 and 5: ordered appends (rrt.cpp:86-92, rrt_connect.cpp:107-116)
+// ============================================================================
+// mode 0: extend successors of the current targets into T (parent = nn[i]);
+// mode 1: connections of the new vertices into O (parent = nno[k]), the first
+// REACHED one in order recorded as the meeting point.
+__global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
+                                               const int32_t *__restrict__ res,
+                                               const int32_t *__restrict__ par,
+                                               const double *__restrict__ sn,
+                                               const double *__restrict__ an, double *__restrict__ tv,
+                                               double *__restrict__ ta, double *__restrict__ tg,
+                                               int32_t *__restrict__ tp, int32_t *__restrict__ tcount,
+                                               int32_t *__restrict__ vtx, unsigned long long *tiles,
+                                               uint32_t epoch, int32_t half) {
+  if (gated(st)) return;
+  __shared__ int32_t s_base;
+  if (threadIdx.x == 0) s_base = *tcount;  // read before this block publishes its count
+  __syncthreads();
+  const int32_t base = s_base;
+  const int64_t n = mode == 0 ? st->n_targets : st->n_added;
+  const int64_t i = blockIdx.x * (int64_t)CB + threadIdx.x;
+  const bool live = i < n;
+  const int32_t r = live ? res[i] : GBP_TRAPPED;
+  const bool keep = live && r != GBP_TRAPPED;
+  int32_t *total = mode == 0 ? &st->n_added : &st->n_conn_added;
+  const uint32_t rank = ordered_rank(keep, tiles, epoch, total, st);
+  if (keep) {
+    const int32_t idx = base + (int32_t)rank, p = par[i];
+    double s[8], pv[8];
+    copy8(s, sn + 8 * i);
+    copy8(pv, tv + 8 * (int64_t)p);
+    copy8(tv + 8 * (int64_t)idx, s);
+    copy10(ta + 10 * (int64_t)idx, an + 10 * i);
+    tp[idx] = p;
+    tg[idx] = tg[p] + pose_distance(pv, s);  // graph_class.cpp:36-42 addEdge
+    if (vtx) vtx[i] = idx;
+    if (mode == 1 && r == GBP_REACHED) {
+      atomicMin((unsigned long long *)&st->meet,
+                ((unsigned long long)i << 32) | (unsigned long long)(uint32_t)idx);
+      st->meet_half = half;
+      atomicOr(&st->done, 1u);
+    }
+  } else if (live && vtx) {
+    vtx[i] = -1;
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    const int32_t added = *total;
+    *tcount = base + added;
+    if (mode == 0) {
+      st->added_base = base;
+      st->stat_added += added;
+    } else {
+      st->stat_conn_added += added;
+    }
+  }
+}
+
+// ============================================================================
+// stage 4: RRTConnectClass::attemptConnect (rrt_connect.cpp:20-91)
+// ============================================================================
+// rrt_connect.cpp:53-63
+__device__ __forceinline__ void connect_action(const double *s_start, const double *s_goal,
+                                               double t_s, double *a) {
+  const double x_td = s_start[0], y_td = s_start[1], z_td = s_start[2];
+  const double dx_td = s_start[3], dy_td = s_start[4], dz_td = s_start[5];
+  const double x_to = s_goal[0], y_to = s_goal[1], z_to = s_goal[2];
+  const double dx_to = s_goal[3], dy_to = s_goal[4], dz_to = s_goal[5];
+  const double p_td = s_start[6], dp_td = s_start[7], p_to = s_goal[6], dp_to = s_goal[7];
+  a[0] = -(2.0 * (3.0 * x_td - 3.0 * x_to + 2.0 * dx_td * t_s + dx_to * t_s)) / (t_s * t_s);
+  a[1] = -(2.0 * (3.0 * y_td - 3.0 * y_to + 2.0 * dy_td * t_s + dy_to * t_s)) / (t_s * t_s);
+  a[2] = -(2.0 * (3.0 * z_td - 3.0 * z_to + 2.0 * dz_td * t_s + dz_to * t_s)) / (t_s * t_s);
+  a[3] = (2.0 * (3.0 * x_td - 3.0 * x_to + dx_td * t_s + 2.0 * dx_to * t_s)) / (t_s * t_s);
+  a[4] = (2.0 * (3.0 * y_td - 3.0 * y_to + dy_td * t_s + 2.0 * dy_to * t_s)) / (t_s * t_s);
+  a[5] = (2.0 * (3.0 * z_td - 3.0 * z_to + dz_td * t_s + 2.0 * dz_to * t_s)) / (t_s * t_s);
+  a[6] = t_s;
+  a[7] = 0;
+  a[8] = -(2.0 * (3.0 * p_td - 3.0 * p_to + 2.0 * dp_td * t_s + dp_to * t_s)) / (t_s * t_s);
+  a[9] = (2.0 * (3.0 * p_td - 3.0 * p_to + dp_td * t_s + 2.0 * dp_to * t_s)) / (t_s * t_s);
+}
+
+// One pair check (planning_utils.cpp:645-881) by a whole wave: every lane
+// holds the same Lane state (wave-uniform); per step, lane j evaluates the
+// sample j positions ahead on the all-pass path (advance_on_success), then
+// every lane replays the reference's transitions on the ballot of results in
+// order, stopping at the first failure, stage change or decision — exactly
+// the reference's samples are counted.  Connect actions run t_s / 0.05 + 1
+// stance samples (dozens to hundreds): a wave covers 64 of them per step.
+template <class ZT, bool ADAPTIVE, int CM>
+__device__ bool wave_pair_check(const TerrainView<ZT> &T, const double *s_in, const double *a_in,
+                                int dir, double *s_new, double &t_new, uint32_t &flags) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  double sv[8], av[10];
+  copy8(sv, s_in);
+  copy10(av, a_in);
+  Lane L;
+  L.s = sv;
+  L.a = av;
+  L.f = 0;
+  L.acc = Acc{0, 0, 0};
+  L.snew_kind = SN_NONE;
+  L.tnew_set = 0;
+  enter_stage(L, dir == GBP_FORWARD ? ST_FWD_STANCE : ST_REV_FLIGHT);
+  bool decided = false;
+  while (!decided) {
+    int stg = L.stage;
+    double t = L.t, ts = L.ts;
+    bool has = true;
+    for (int k = 0; k < lane && has; k++) has = advance_on_success<ADAPTIVE>(stg, av, t, ts);
+    const double t_eval = lane == 0 ? stage_time(L) : t;
+    Acc acc{0, L.acc.V + (uint32_t)lane, 0};
+    bool ok = false;
+    if (has) {
+      double sc[8];
+      sample_state(sv, av, stg, t_eval, sc);
+      ok = is_valid_state<ZT, CM>(T, sc, stage_phase(stg), acc);
+    }
+    const unsigned long long okm = __ballot(ok), hasm = __ballot(has);
+    for (int j = 0; j < WAVE; j++) {
+      if (!((hasm >> j) & 1ull)) break;
+      const uint32_t fj = __shfl(acc.flags, j), gj = __shfl(acc.G, j);
+      const bool okj = (okm >> j) & 1ull;
+      L.acc.G += gj;
+      L.acc.flags |= fj;
+      if (fj & GBP_F_LIMIT) {
+        decided = true;
+        break;
+      }
+      L.acc.V += 1;
+      decided = transition<ADAPTIVE>(L, okj);
+      if (decided || !okj || L.stage != stg) break;
+    }
+  }
+  uint32_t f = L.f | L.acc.flags;
+  if (L.snew_kind != SN_NONE) {
+    f |= GBP_F_SNEW_SET;
+    sample_state(sv, av,
+                 L.snew_kind == SN_STANCE_S ? ST_FWD_STANCE
+                                            : (L.snew_kind == SN_FLIGHT_B ? ST_FWD_LAND : ST_REV_STANCE),
+                 L.snew_p, s_new);
+  }
+  if (L.tnew_set) {
+    f |= GBP_F_TNEW_SET;
+    t_new = L.tnew;
+  }
+  flags = f;
+  return (f & GBP_F_VALID) != 0;
+}
+
+// one wave per new vertex k of T: connect it to its nearest vertex of O with
+// the recursion as a loop over levels (engine conventions of gbp.h: an
+// unassigned t_new / s_new is TRAPPED; GBP_CONNECT_MAX_DEPTH levels)
+template <class ZT, bool ADAPTIVE, int CM>
+__global__ __launch_bounds__(TB) void k_connect(TerrainView<ZT> T, gbp_plan_status *st, int cdir,
+                                                const double *__restrict__ tv,
+                                                const double *__restrict__ ov,
+                                                const int32_t *__restrict__ nno,
+                                                int32_t *__restrict__ kres,
+                                                double *__restrict__ ksn,
+                                                double *__restrict__ kan,
+                                                uint32_t *__restrict__ kf, int32_t half) {
+  if (gated(st)) return;
+  const int64_t n = st->n_added, base = st->added_base;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / WAVE);
+  bool frag = false;
+  unsigned long long capped = 0;
+  for (int64_t k = blockIdx.x * (int64_t)(blockDim.x / WAVE) + threadIdx.x / WAVE; k < n;
+       k += waves) {
+    double se[8], s[8], sn[8], an[10];
+    copy8(se, ov + 8 * (int64_t)nno[k]);  // s_near in O (rrt_connect.cpp:101-102)
+    copy8(s, tv + 8 * (base + k));
+    double t_s = pose_distance(s, se) / V_NOM;  // rrt_connect.cpp:89
+    int res = GBP_TRAPPED;
+    uint32_t cf = 0;
+    for (int depth = 0;; depth++) {
+      if (depth > GBP_CONNECT_MAX_DEPTH) {
+        cf |= GBP_F_DEPTH_CAPPED;
+        break;
+      }
+      if (t_s <= KINEMATICS_RES) break;  // :23-24
+      const double *s_start = cdir == GBP_FORWARD ? se : s;
+      const double *s_goal = cdir == GBP_FORWARD ? s : se;
+      connect_action(s_start, s_goal, t_s, an);
+      if (!is_valid_action(an)) break;  // :66
+      double psn[8], ptn = 0;
+      uint32_t pf = 0;
+      const bool ok = wave_pair_check<ZT, ADAPTIVE, CM>(T, cdir == GBP_FORWARD ? s_start : s_goal,
+                                                        an, cdir, psn, ptn, pf);
+      cf |= pf & (GBP_F_OOD | GBP_F_NAN | GBP_F_FRAGILE | GBP_F_LIMIT);
+      if (pf & GBP_F_SNEW_SET) copy8(sn, psn);
+      if (ok) {
+        res = depth == 0 ? GBP_REACHED : GBP_ADVANCED;  // :74-80
+        break;
+      }
+      if (!(pf & GBP_F_TNEW_SET) || !(pf & GBP_F_SNEW_SET)) break;
+      copy8(s, psn);  // :77 recurse toward the returned state with t_s = t_new
+      t_s = ptn;
+    }
+    if (lane == 0) {
+      kres[k] = res;
+      if (res != GBP_TRAPPED) copy8(ksn + 8 * k, sn);
+      copy10(kan + 10 * k, an);
+      kf[k] = cf;
+    }
+    frag = frag || (cf & GBP_F_FRAGILE);
+    capped += (cf & GBP_F_DEPTH_CAPPED) ? 1 : 0;
+  }
+  if (lane == 0) {
+    if (capped) atomicAdd((unsigned long long *)&st->stat_depth_capped, capped);
+    if (frag) {
+      atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_CONNECT);
+      st->halt_half = half;
+    }
+  }
+}
+
+__global__ void k_tree_init(gbp_tree t, double r0, double r1, double r2, double r3, double r4,
+                            double r5, double r6, double r7) {
+  const double r[8] = {r0, r1, r2, r3, r4, r5, r6, r7};
+  copy8(t.v, r);
+  for (int k = 0; k < 10; k++) t.a[k] = 0.0;
+  t.g[0] = 0.0;
+  t.parent[0] = -1;
+  *t.count = 1;
+}
+
+__global__ void k_tree_append(gbp_tree t, int64_t n, const double *__restrict__ s,
+                              const double *__restrict__ a, const int32_t *__restrict__ p) {
+  // sequential in index order: a parent may be appended in the same call
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  int32_t c = *t.count;
+  for (int64_t i = 0; i < n; i++, c++) {
+    copy8(t.v + 8 * (int64_t)c, s + 8 * i);
+    copy10(t.a + 10 * (int64_t)c, a + 10 * i);
+    t.parent[c] = p[i];
+    t.g[c] = p[i] >= 0 ? t.g[p[i]] + pose_distance(t.v + 8 * (int64_t)p[i], s + 8 * i) : 0.0;
+  }
+  *t.count = c;
+}
+
+__global__ void k_plan_reset(gbp_plan_status *st, int64_t ext_counter) {
+  gbp_plan_status z;
+  memset(&z, 0, sizeof z);
+  z.meet = ~0ull;
+  z.halt_half = -1;
+  z.meet_half = -1;
+  z.ext_counter = ext_counter;
+  *st = z;
+}
+
+// standalone gbp_extend_tree_dev: the batch becomes stage 2's targets
+__global__ void k_extend_setup(gbp_plan_status *st, int64_t n, const int32_t *n_dev,
+                               int64_t extend_base, const double *__restrict__ src,
+                               double *__restrict__ targets) {
+  const int64_t m = n_dev ? *n_dev : n;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->halt = 0;
+    st->done = 0;
+    st->n_targets = (int32_t)m;
+    st->ext_base = extend_base;
+  }
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < 8 * m;
+       i += (int64_t)gridDim.x * blockDim.x)
+    targets[i] = src[i];
+}
+
+__global__ void k_extend_out(const gbp_plan_status *st, int64_t n, const int32_t *__restrict__ eres,
+                             const int32_t *__restrict__ evtx, int32_t *__restrict__ result,
+                             int32_t *__restrict__ new_vertex) {
+  if (st->halt) return;  // FRAGILE: gbp_extend_tree_finish_dev after the resolution
+  const int64_t m = st->n_targets;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (result) result[i] = eres[i];
+    if (new_vertex) new_vertex[i] = eres[i] != GBP_TRAPPED ? evtx[i] : -1;
+  }
+}
+
+#define HIPCHK_P(expr)                        \
+  do {                                        \
+    hipError_t e_ = (expr);                   \
+    if (e_ != hipSuccess) return GBP_E_HIP;   \
+  } while (0)
+
+bool tree_ok(const gbp_tree *t) { return t && t->v && t->count; }
+
+uint32_t next_epoch(gbp_plan_ws *w) {
+  if (++w->epoch == 0) w->epoch = 1;
+  return w->epoch;
+}
+
+unsigned tiles_for(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + CB - 1) / CB); }
+
+int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
+              const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s) {
+  hipLaunchKernelGGL(k_nn_partial, dim3(num_cus * 2), dim3(TB), 0, s, w->st, nq_dev, q, q_off_dev,
+                     tr->v, tr->count, w->bmax, w->nn_d, w->nn_i);
+  hipLaunchKernelGGL(k_nn_reduce, dim3(grid_for(w->bmax, TB, num_cus * 4)), dim3(TB), 0, s, w->st,
+                     nq_dev, tr->count, w->bmax, w->nn_d, w->nn_i, out);
+  return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
+}
+
+template <class ZT>
+int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int32_t half,
+                   int direction, int64_t batch, uint64_t seed, uint64_t target_stream,
+                   int64_t target_base, int adaptive, int first_stage, int last_stage,
+                   hipStream_t s) {
+  const TerrainView<ZT> V = view<ZT>(t);
+  const int cus = t->num_cus;
+  gbp_plan_status *st = w->st;
+  if (first_stage <= 0 && last_stage >= 0)
+    hipLaunchKernelGGL(k_targets<ZT>, dim3(grid_for(batch, TB, cus * 8)), dim3(TB), 0, s, V, st,
+                       batch, seed, target_stream, target_base, w->cand, w->cflag, half);
+  if (first_stage <= 1 && last_stage >= 1)
+    hipLaunchKernelGGL(k_compact_targets, dim3(tiles_for(batch)), dim3(CB), 0, s, st, batch,
+                       w->cand, w->cflag, w->targets, w->tiles, next_epoch(w));
+  if (first_stage <= 2 && last_stage >= 2) {
+    int rc = nn_launch(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s);
+    if (rc) return rc;
+    const int64_t mmax = batch * GBP_NUM_GEN_STATES;
+    hipLaunchKernelGGL(k_extend_prep<ZT>, dim3(grid_for(mmax, TB, cus * 8)), dim3(TB), 0, s, V, st,
+                       w->targets, w->nn, T->v, seed, w->cs, w->ca);
+    rc = gbp_internal_validate_dev_n(t, mmax, &st->n_validate, w->cs, w->ca, nullptr, direction,
+                                     adaptive, nullptr, w->csn, nullptr, w->cf, w->cc, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_select, dim3(grid_for(batch, TB, cus * 4)), dim3(TB), 0, s, st, w->targets,
+                       w->nn, T->v, w->ca, w->csn, w->cf, w->eres, w->echo, w->esn, w->ean, w->ef,
+                       half);
+  }
+  if (first_stage <= 3 && last_stage >= 3)
+    hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 0, w->eres, w->nn,
+                       w->esn, w->ean, T->v, T->a, T->g, T->parent, T->count, w->evtx, w->tiles,
+                       next_epoch(w), half);
+  if (!O) return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
+  const int cdir = direction == GBP_FORWARD ? GBP_REVERSE : GBP_FORWARD;
+  if (first_stage <= 4 && last_stage >= 4) {
+    // queries: T's new vertices, rows [added_base, added_base + n_added)
+    int rc = nn_launch(w, &st->n_added, T->v, &st->added_base, O, w->nno, cus, s);
+    if (rc) return rc;
+    const int cm = (t->opt_affine && t->affine) ? 2 : 0;
+    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * 4, (batch + 3) / 4));
+#define GBP_KC(AD, CM)                                                                         \
+  hipLaunchKernelGGL((k_connect<ZT, AD, CM>), dim3(g), dim3(TB), 0, s, V, st, cdir, T->v, O->v, \
+                     w->nno, w->kres, w->ksn, w->kan, w->kf, half)
+    if (adaptive) {
+      if (cm == 2) GBP_KC(true, 2); else GBP_KC(true, 0);
+    } else {
+      if (cm == 2) GBP_KC(false, 2); else GBP_KC(false, 0);
+    }
+#undef GBP_KC
+  }
+  if (first_stage <= 5 && last_stage >= 5)
+    hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 1, w->kres, w->nno,
+                       w->ksn, w->kan, O->v, O->a, O->g, O->parent, O->count, nullptr, w->tiles,
+                       next_epoch(w), half);
+  return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI (include/gbp.h "device trees and the device planner loop")
+// ============================================================================
+namespace {
+
+struct Guard {
+  int prev = -1;
+  explicit Guard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~Guard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+template <class T>
+T *carve(char *&p, size_t count) {
+  p = (char *)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+  T *r = (T *)p;
+  p += count * sizeof(T);
+  return r;
+}
+
+int tree_alloc(gbp_tree *t, int64_t cap) {
+  double *v = nullptr, *a = nullptr, *g = nullptr;
+  int32_t *p = nullptr;
+  if (hipMalloc(&v, 64 * cap) != hipSuccess) return GBP_E_ALLOC;
+  if (hipMalloc(&a, 80 * cap) != hipSuccess || hipMalloc(&g, 8 * cap) != hipSuccess ||
+      hipMalloc(&p, 4 * cap) != hipSuccess) {
+    (void)hipFree(v);
+    if (a) (void)hipFree(a);
+    if (g) (void)hipFree(g);
+    return GBP_E_ALLOC;
+  }
+  t->v = v;
+  t->a = a;
+  t->g = g;
+  t->parent = p;
+  t->cap = cap;
+  return GBP_OK;
+}
+
+template <class T>
+int d2h(T *dst, const T *src, size_t count, hipStream_t s) {
+  HIPCHK_P(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyDeviceToHost, s));
+  return GBP_OK;
+}
+template <class T>
+int h2d(T *dst, const T *src, size_t count, hipStream_t s) {
+  HIPCHK_P(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyHostToDevice, s));
+  return GBP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gbp_stream_create(int device, gbp_stream *out) {
+  if (!out) return GBP_E_INVALID_ARG;
+  Guard g(device);
+  hipStream_t s = nullptr;
+  HIPCHK_P(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *out = (gbp_stream)s;
+  return GBP_OK;
+}
+
+int gbp_stream_destroy(gbp_stream stream) {
+  if (stream) HIPCHK_P(hipStreamDestroy((hipStream_t)stream));
+  return GBP_OK;
+}
+
+int gbp_tree_create(int device, int64_t capacity, gbp_tree **out) {
+  if (!out || capacity < 1 || capacity > 0x7FFFFFFF) return GBP_E_INVALID_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GBP_E_NO_DEVICE;
+  if (device < 0 || device >= ndev) return GBP_E_INVALID_ARG;
+  Guard g(device);
+  gbp_tree *t = new (std::nothrow) gbp_tree();
+  if (!t) return GBP_E_ALLOC;
+  t->device = device;
+  if (hipMalloc(&t->count, 4) != hipSuccess || tree_alloc(t, capacity) != GBP_OK) {
+    gbp_tree_destroy(t);
+    return GBP_E_ALLOC;
+  }
+  if (hipMemset(t->count, 0, 4) != hipSuccess) {
+    gbp_tree_destroy(t);
+    return GBP_E_HIP;
+  }
+  *out = t;
+  return GBP_OK;
+}
+
+int gbp_tree_destroy(gbp_tree *t) {
+  if (!t) return GBP_E_BAD_HANDLE;
+  Guard g(t->device);
+  (void)hipDeviceSynchronize();
+  void *ptrs[] = {t->v, t->a, t->g, t->parent, t->count};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  delete t;
+  return GBP_OK;
+}
+
+int gbp_tree_reserve(gbp_tree *t, int64_t capacity, gbp_stream stream) {
+  if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
+  if (capacity <= t->cap) return GBP_OK;
+  if (capacity > 0x7FFFFFFF) return GBP_E_SHAPE;
+  Guard g(t->device);
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK_P(hipStreamSynchronize(s));
+  gbp_tree old = *t;
+  int rc = tree_alloc(t, capacity);
+  if (rc) {
+    *t = old;
+    return rc;
+  }
+  HIPCHK_P(hipMemcpyAsync(t->v, old.v, 64 * old.cap, hipMemcpyDeviceToDevice, s));
+  HIPCHK_P(hipMemcpyAsync(t->a, old.a, 80 * old.cap, hipMemcpyDeviceToDevice, s));
+  HIPCHK_P(hipMemcpyAsync(t->g, old.g, 8 * old.cap, hipMemcpyDeviceToDevice, s));
+  HIPCHK_P(hipMemcpyAsync(t->parent, old.parent, 4 * old.cap, hipMemcpyDeviceToDevice, s));
+  HIPCHK_P(hipStreamSynchronize(s));
+  (void)hipFree(old.v);
+  (void)hipFree(old.a);
+  (void)hipFree(old.g);
+  (void)hipFree(old.parent);
+  return GBP_OK;
+}
+
+int gbp_tree_init(gbp_tree *t, const double *root, gbp_stream stream) {
+  if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
+  if (!root) return GBP_E_INVALID_ARG;
+  Guard g(t->device);
+  hipLaunchKernelGGL(k_tree_init, dim3(1), dim3(1), 0, (hipStream_t)stream, *t, root[0], root[1],
+                     root[2], root[3], root[4], root[5], root[6], root[7]);
+  HIPCHK_P(hipGetLastError());
+  return GBP_OK;
+}
+
+int gbp_tree_size(gbp_tree *t, int64_t *count, gbp_stream stream) {
+  if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
+  if (!count) return GBP_E_INVALID_ARG;
+  Guard g(t->device);
+  int32_t c = 0;
+  HIPCHK_P(hipMemcpyAsync(&c, t->count, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK_P(hipStreamSynchronize((hipStream_t)stream));
+  *count = c;
+  return GBP_OK;
+}
+
+int gbp_tree_capacity(gbp_tree *t, int64_t *capacity) {
+  if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
+  if (!capacity) return GBP_E_INVALID_ARG;
+  *capacity = t->cap;
+  return GBP_OK;
+}
+
+int gbp_tree_read(gbp_tree *t, int64_t first, int64_t n, double *states, double *actions,
+                  int32_t *parents, double *g, gbp_stream stream) {
+  if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
+  if (first < 0 || n < 0 || first + n > t->cap) return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  Guard gd(t->device);
+  hipStream_t s = (hipStream_t)stream;
+  int rc = GBP_OK;
+  if (!rc && states) rc = d2h(states, t->v + 8 * first, 8 * n, s);
+  if (!rc && actions) rc = d2h(actions, t->a + 10 * first, 10 * n, s);
+  if (!rc && parents) rc = d2h(parents, t->parent + first, n, s);
+  if (!rc && g) rc = d2h(g, t->g + first, n, s);
+  if (rc) return rc;
+  HIPCHK_P(hipStreamSynchronize(s));
+  return GBP_OK;
+}
+
+int gbp_tree_append_host(gbp_tree *t, int64_t n, const double *states, const double *actions,
+                         const int32_t *parents, gbp_stream stream) {
+  if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || (n > 0 && (!states || !actions || !parents))) return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  int64_t c = 0;
+  int rc = gbp_tree_size(t, &c, stream);
+  if (rc) return rc;
+  for (int64_t i = 0; i < n; i++)
+    if (parents[i] < -1 || parents[i] >= c + i) return GBP_E_INVALID_ARG;
+  if (c + n > t->cap) rc = gbp_tree_reserve(t, std::max<int64_t>(2 * t->cap, c + n), stream);
+  if (rc) return rc;
+  Guard g(t->device);
+  hipStream_t s = (hipStream_t)stream;
+  void *buf = nullptr;
+  HIPCHK_P(hipMalloc(&buf, (size_t)n * (64 + 80 + 4) + 512));
+  char *p = (char *)buf;
+  double *ds = carve<double>(p, 8 * n), *da = carve<double>(p, 10 * n);
+  int32_t *dp = carve<int32_t>(p, n);
+  rc = h2d(ds, states, 8 * n, s);
+  if (!rc) rc = h2d(da, actions, 10 * n, s);
+  if (!rc) rc = h2d(dp, parents, n, s);
+  if (!rc) {
+    hipLaunchKernelGGL(k_tree_append, dim3(1), dim3(1), 0, s, *t, n, ds, da, dp);
+    if (hipGetLastError() != hipSuccess) rc = GBP_E_HIP;
+  }
+  if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = GBP_E_HIP;
+  (void)hipFree(buf);
+  return rc;
+}
+
+int gbp_tree_device_ptrs(gbp_tree *t, double **states, int32_t **count) {
+  if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
+  if (states) *states = t->v;
+  if (count) *count = t->count;
+  return GBP_OK;
+}
+
+int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
+  if (!t || !out) return GBP_E_INVALID_ARG;
+  if (max_batch < 1 || max_batch > (1 << 24)) return GBP_E_INVALID_ARG;
+  *out = nullptr;
+  Guard g(t->device);
+  gbp_plan_ws *w = new (std::nothrow) gbp_plan_ws();
+  if (!w) return GBP_E_ALLOC;
+  w->device = t->device;
+  w->bmax = max_batch;
+  w->ntiles = (max_batch + CB - 1) / CB + 1;
+  const int64_t b = max_batch, m = GBP_NUM_GEN_STATES * max_batch;
+  const size_t bytes = sizeof(gbp_plan_status) + 8 * w->ntiles + 64 * b + 4 * b + 64 * b + 4 * b +
+                       m * (64 + 80 + 64 + 4 + 4) + b * (4 + 4 + 64 + 80 + 4 + 4) +
+                       b * (4 + 4 + 64 + 80 + 4) + NN_MAX_CHUNKS * b * (8 + 4) + 64 * 256;
+  if (hipMalloc(&w->block, bytes) != hipSuccess) {
+    delete w;
+    return GBP_E_ALLOC;
+  }
+  char *p = (char *)w->block;
+  w->st = carve<gbp_plan_status>(p, 1);
+  w->tiles = carve<unsigned long long>(p, w->ntiles);
+  w->cand = carve<double>(p, 8 * b);
+  w->cflag = carve<uint32_t>(p, b);
+  w->targets = carve<double>(p, 8 * b);
+  w->nn = carve<int32_t>(p, b);
+  w->cs = carve<double>(p, 8 * m);
+  w->ca = carve<double>(p, 10 * m);
+  w->csn = carve<double>(p, 8 * m);
+  w->cf = carve<uint32_t>(p, m);
+  w->cc = carve<uint32_t>(p, m);
+  w->eres = carve<int32_t>(p, b);
+  w->echo = carve<int32_t>(p, b);
+  w->esn = carve<double>(p, 8 * b);
+  w->ean = carve<double>(p, 10 * b);
+  w->ef = carve<uint32_t>(p, b);
+  w->evtx = carve<int32_t>(p, b);
+  w->nno = carve<int32_t>(p, b);
+  w->kres = carve<int32_t>(p, b);
+  w->ksn = carve<double>(p, 8 * b);
+  w->kan = carve<double>(p, 10 * b);
+  w->kf = carve<uint32_t>(p, b);
+  w->nn_d = carve<double>(p, NN_MAX_CHUNKS * b);
+  w->nn_i = carve<int32_t>(p, NN_MAX_CHUNKS * b);
+  if ((size_t)(p - (char *)w->block) > bytes || hipMemset(w->tiles, 0, 8 * w->ntiles) != hipSuccess) {
+    (void)hipFree(w->block);
+    delete w;
+    return GBP_E_HIP;
+  }
+  hipLaunchKernelGGL(k_plan_reset, dim3(1), dim3(1), 0, nullptr, w->st, (int64_t)0);
+  if (hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(w->block);
+    delete w;
+    return GBP_E_HIP;
+  }
+  *out = w;
+  return GBP_OK;
+}
+
+int gbp_plan_ws_destroy(gbp_plan_ws *w) {
+  if (!w) return GBP_E_BAD_HANDLE;
+  Guard g(w->device);
+  (void)hipDeviceSynchronize();
+  if (w->block) (void)hipFree(w->block);
+  delete w;
+  return GBP_OK;
+}
+
+int gbp_plan_reset(gbp_plan_ws *w, int64_t extend_counter, gbp_stream stream) {
+  if (!w) return GBP_E_BAD_HANDLE;
+  Guard g(w->device);
+  hipLaunchKernelGGL(k_plan_reset, dim3(1), dim3(1), 0, (hipStream_t)stream, w->st, extend_counter);
+  HIPCHK_P(hipGetLastError());
+  return GBP_OK;
+}
+
+int gbp_plan_status_read(gbp_plan_ws *w, gbp_plan_status *out, gbp_stream stream) {
+  if (!w) return GBP_E_BAD_HANDLE;
+  if (!out) return GBP_E_INVALID_ARG;
+  Guard g(w->device);
+  HIPCHK_P(hipMemcpyAsync(out, w->st, sizeof *out, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIPCHK_P(hipStreamSynchronize((hipStream_t)stream));
+  return GBP_OK;
+}
+
+int gbp_plan_half_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int32_t half,
+                      int direction, int64_t batch, uint64_t seed, uint64_t target_stream,
+                      int64_t target_index_base, int adaptive, int first_stage,
+                      gbp_stream stream) {
+  if (!t || !w || !tree_ok(T) || !tree_ok(O)) return GBP_E_BAD_HANDLE;
+  if (batch < 1 || batch > w->bmax || first_stage < 0 || first_stage > 5 ||
+      (direction != GBP_FORWARD && direction != GBP_REVERSE) || T == O)
+    return GBP_E_INVALID_ARG;
+  Guard g(t->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (t->storage == GBP_STORAGE_F32)
+    return enqueue_stages<float>(t, w, T, O, half, direction, batch, seed, target_stream,
+                                 target_index_base, adaptive, first_stage, 5, s);
+  return enqueue_stages<double>(t, w, T, O, half, direction, batch, seed, target_stream,
+                                target_index_base, adaptive, first_stage, 5, s);
+}
+
+int gbp_extend_tree_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, int64_t n,
+                        const double *targets, const int32_t *n_dev, int direction, int adaptive,
+                        uint64_t seed, int64_t extend_base, int32_t *result, int32_t *new_vertex,
+                        gbp_stream stream) {
+  if (!t || !w || !tree_ok(T)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || n > w->bmax || (n > 0 && !targets) ||
+      (direction != GBP_FORWARD && direction != GBP_REVERSE))
+    return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  Guard g(t->device);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_extend_setup, dim3(grid_for(8 * n, TB, t->num_cus * 4)), dim3(TB), 0, s,
+                     w->st, n, n_dev, extend_base, targets, w->targets);
+  int rc = t->storage == GBP_STORAGE_F32
+               ? enqueue_stages<float>(t, w, T, nullptr, 0, direction, n, seed, 0, 0, adaptive, 2,
+                                       3, s)
+               : enqueue_stages<double>(t, w, T, nullptr, 0, direction, n, seed, 0, 0, adaptive, 2,
+                                        3, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_extend_out, dim3(grid_for(n, TB, t->num_cus * 4)), dim3(TB), 0, s, w->st, n,
+                     w->eres, w->evtx, result, new_vertex);
+  HIPCHK_P(hipGetLastError());
+  return GBP_OK;
+}
+
+int gbp_extend_tree_finish_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, int64_t n,
+                               int direction, int32_t *result, int32_t *new_vertex,
+                               gbp_stream stream) {
+  if (!t || !w || !tree_ok(T)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || n > w->bmax) return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  Guard g(t->device);
+  hipStream_t s = (hipStream_t)stream;
+  int rc = t->storage == GBP_STORAGE_F32
+               ? enqueue_stages<float>(t, w, T, nullptr, 0, direction, n, 0, 0, 0, 0, 3, 3, s)
+               : enqueue_stages<double>(t, w, T, nullptr, 0, direction, n, 0, 0, 0, 0, 3, 3, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_extend_out, dim3(grid_for(n, TB, t->num_cus * 4)), dim3(TB), 0, s, w->st, n,
+                     w->eres, w->evtx, result, new_vertex);
+  HIPCHK_P(hipGetLastError());
+  return GBP_OK;
+}
+
+int gbp_extend_tree_host(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, int64_t n,
+                         const double *targets, int direction, int adaptive, uint64_t seed,
+                         int64_t extend_base, int32_t *result, int32_t *new_vertex,
+                         int64_t *n_resolved) {
+  if (!t || !w || !tree_ok(T)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || n > w->bmax || (n > 0 && (!targets || !result))) return GBP_E_INVALID_ARG;
+  if (n_resolved) *n_resolved = 0;
+  if (n == 0) return GBP_OK;
+  Guard g(t->device);
+  hipStream_t s = t->host_stream;
+  int64_t cnt = 0;
+  int rc = gbp_tree_size(T, &cnt, s);
+  if (!rc && cnt + n > T->cap) rc = gbp_tree_reserve(T, std::max<int64_t>(2 * T->cap, cnt + n), s);
+  if (rc) return rc;
+  void *buf = nullptr;
+  HIPCHK_P(hipMalloc(&buf, (size_t)n * (64 + 8) + 512));
+  char *p = (char *)buf;
+  double *dt = carve<double>(p, 8 * n);
+  int32_t *dr = carve<int32_t>(p, n), *dv = carve<int32_t>(p, n);
+  rc = h2d(dt, targets, 8 * n, s);
+  if (!rc) rc = gbp_plan_reset(w, 0, s);
+  if (!rc)
+    rc = gbp_extend_tree_dev(t, w, T, n, dt, nullptr, direction, adaptive, seed, extend_base, dr,
+                             dv, s);
+  gbp_plan_status st;
+  if (!rc) rc = gbp_plan_status_read(w, &st, s);
+  if (!rc && st.halt) {
+    int resume = -1;
+    rc = gbp_plan_resolve_host(t, w, T, nullptr, direction, n, adaptive, &resume, n_resolved, s);
+    if (!rc) rc = gbp_extend_tree_finish_dev(t, w, T, n, direction, dr, dv, s);
+  }
+  if (!rc) rc = d2h(result, dr, n, s);
+  if (!rc && new_vertex) rc = d2h(new_vertex, dv, n, s);
+  if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = GBP_E_HIP;
+  (void)hipFree(buf);
+  return rc;
+}
+
+int gbp_plan_resolve_host(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int direction,
+                          int64_t batch, int adaptive, int *resume_stage, int64_t *n_resolved,
+                          gbp_stream stream) {
+  if (!t || !w || !tree_ok(T)) return GBP_E_BAD_HANDLE;
+  if (!resume_stage) return GBP_E_INVALID_ARG;
+  Guard g(t->device);
+  hipStream_t s = (hipStream_t)stream;
+  gbp_plan_status st;
+  int rc = gbp_plan_status_read(w, &st, stream);
+  if (rc) return rc;
+  *resume_stage = -1;
+  int64_t k = 0;
+  if (st.halt & GBP_PLAN_HALT_TARGETS) {
+    // isValidState(s_rand, STANCE) of the half's draws (rrt_connect.cpp:254)
+    if (batch < 1 || batch > w->bmax) return GBP_E_INVALID_ARG;
+    std::vector<uint32_t> fl(batch);
+    if ((rc = d2h(fl.data(), w->cflag, batch, s))) return rc;
+    HIPCHK_P(hipStreamSynchronize(s));
+    for (int64_t i = 0; i < batch; i++) {
+      if (!(fl[i] & GBP_F_FRAGILE)) continue;
+      double q[8];
+      if ((rc = d2h(q, w->cand + 8 * i, 8, s))) return rc;
+      HIPCHK_P(hipStreamSynchronize(s));
+      gbp_host::Acc acc;
+      const bool v = gbp_host::is_valid_state(t->host, q, GBP_STANCE, acc);
+      fl[i] = acc.flags | (v ? GBP_F_VALID : 0u) | GBP_F_RESOLVED;
+      if ((rc = h2d(w->cflag + i, &fl[i], 1, s))) return rc;
+      k++;
+    }
+    *resume_stage = 1;
+  } else if (st.halt & GBP_PLAN_HALT_EXTEND) {
+    // newConfig + acceptance (rrt.cpp:20-101) of every extend with a FRAGILE
+    // executed candidate, on the device's own candidate actions
+    const int64_t n = st.n_targets;
+    std::vector<uint32_t> ef(n);
+    if ((rc = d2h(ef.data(), w->ef, n, s))) return rc;
+    HIPCHK_P(hipStreamSynchronize(s));
+    for (int64_t i = 0; i < n; i++) {
+      if (!(ef[i] & GBP_F_FRAGILE)) continue;
+      int32_t nn = 0;
+      double tg[8], sn0[8], act[10 * GBP_NUM_GEN_STATES];
+      if ((rc = d2h(&nn, w->nn + i, 1, s)) || (rc = d2h(tg, w->targets + 8 * i, 8, s)) ||
+          (rc = d2h(act, w->ca + 10 * GBP_NUM_GEN_STATES * i, 10 * GBP_NUM_GEN_STATES, s)))
+        return rc;
+      HIPCHK_P(hipStreamSynchronize(s));
+      if ((rc = d2h(sn0, T->v + 8 * (int64_t)nn, 8, s))) return rc;
+      HIPCHK_P(hipStreamSynchronize(s));
+      const double best0 = gbp_host::state_distance(sn0, tg);
+      double best = best0, s_test[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_test = 0, s_new[8];
+      uint32_t fl = 0;
+      int found = -1;
+      for (int j = 0; j < GBP_NUM_GEN_STATES; j++) {
+        uint32_t f = 0;
+        const bool v = gbp_host::pair_check(t->host, sn0, act + 10 * j, direction, adaptive, s_test,
+                                            &t_test, &f, nullptr);
+        fl |= f & (GBP_F_VALID | GBP_F_OOD | GBP_F_NAN | GBP_F_LIMIT);
+        if (v) {
+          found = j;
+          break;
+        }
+      }
+      int32_t r = GBP_TRAPPED;
+      if (found >= 0) {
+        const double cur = gbp_host::state_distance(s_test, tg);
+        if (cur < best) {
+          best = cur;
+          memcpy(s_new, s_test, sizeof s_new);
+          r = cur <= GOAL_BOUNDS ? GBP_REACHED : GBP_ADVANCED;
+          if ((rc = h2d(w->esn + 8 * i, s_new, 8, s)) ||
+              (rc = h2d(w->ean + 10 * i, act + 10 * found, 10, s)))
+            return rc;
+        }
+      }
+      const uint32_t fr = fl | GBP_F_RESOLVED;
+      if ((rc = h2d(w->eres + i, &r, 1, s)) || (rc = h2d(w->echo + i, &found, 1, s)) ||
+          (rc = h2d(w->ef + i, &fr, 1, s)))
+        return rc;
+      HIPCHK_P(hipStreamSynchronize(s));
+      k++;
+    }
+    *resume_stage = 3;
+  } else if (st.halt & GBP_PLAN_HALT_CONNECT) {
+    // RRTConnectClass::attemptConnect (rrt_connect.cpp:20-91) of every
+    // connection with a FRAGILE level, recursion replayed on the host
+    if (!tree_ok(O)) return GBP_E_BAD_HANDLE;
+    const int64_t n = st.n_added, base = st.added_base;
+    const int cdir = direction == GBP_FORWARD ? GBP_REVERSE : GBP_FORWARD;
+    std::vector<uint32_t> kf(n);
+    if ((rc = d2h(kf.data(), w->kf, n, s))) return rc;
+    HIPCHK_P(hipStreamSynchronize(s));
+    for (int64_t i = 0; i < n; i++) {
+      if (!(kf[i] & GBP_F_FRAGILE)) continue;
+      int32_t j = 0;
+      double se[8], sq[8], sn[8] = {0, 0, 0, 0, 0, 0, 0, 0}, an[10];
+      if ((rc = d2h(&j, w->nno + i, 1, s)) || (rc = d2h(sq, T->v + 8 * (base + i), 8, s))) return rc;
+      HIPCHK_P(hipStreamSynchronize(s));
+      if ((rc = d2h(se, O->v + 8 * (int64_t)j, 8, s))) return rc;
+      HIPCHK_P(hipStreamSynchronize(s));
+      const double t_s = gbp_host::pose_distance(sq, se) / V_NOM;
+      uint32_t f = 0;
+      const int32_t r = gbp_host::attempt_connect(t->host, se, sq, t_s, sn, an, cdir, adaptive,
+                                                  GBP_CONNECT_MAX_DEPTH, &f);
+      const uint32_t fr = f | GBP_F_RESOLVED;
+      if ((rc = h2d(w->kres + i, &r, 1, s)) || (rc = h2d(w->kan + 10 * i, an, 10, s)) ||
+          (rc = h2d(w->kf + i, &fr, 1, s)))
+        return rc;
+      if (r != GBP_TRAPPED && (rc = h2d(w->ksn + 8 * i, sn, 8, s))) return rc;
+      HIPCHK_P(hipStreamSynchronize(s));
+      k++;
+    }
+    *resume_stage = 5;
+  }
+  if (*resume_stage >= 0) {
+    st.halt = 0;
+    st.stat_fragile_resolved += k;
+    if ((rc = h2d(w->st, &st, 1, s))) return rc;
+    HIPCHK_P(hipStreamSynchronize(s));
+  }
+  if (n_resolved) *n_resolved = k;
+  return GBP_OK;
+}
+
+}  // extern "C"

@@ -321,4 +321,79 @@ double state_distance(const double *q1, const double *q2) {  // planning_utils.c
   return std::sqrt(sum);
 }
 
+double pose_distance(const double *q1, const double *q2) {  // planning_utils.cpp:106-115
+  double sum = 0;
+  for (int i = 0; i < 3; i++) sum = sum + (q2[i] - q1[i]) * (q2[i] - q1[i]);
+  return std::sqrt(sum);
+}
+
+bool is_valid_action(const double a[10]) {  // planning_utils.cpp:519-556
+  if ((a[6] <= 0) || (a[7] < 0)) return false;
+  const double m = 13, g = 9.81, mu = 1.0, f_max = 637;  // M_CONST, G_CONST, MU, F_MAX
+  const double f_x_td = m * a[0], f_y_td = m * a[1], f_z_td = m * (a[2] + g);
+  const double f_x_to = m * a[3], f_y_to = m * a[4], f_z_to = m * (a[5] + g);
+  if ((std::sqrt(f_x_td * f_x_td + f_y_td * f_y_td + f_z_td * f_z_td) >= f_max) ||
+      (std::sqrt(f_x_to * f_x_to + f_y_to * f_y_to + f_z_to * f_z_to) >= f_max) || (f_z_td < 0) ||
+      (f_z_to < 0) || (a[8] >= f_max) || (a[9] >= f_max))
+    return false;
+  if ((std::sqrt(f_x_td * f_x_td + f_y_td * f_y_td) >= mu * f_z_td) ||
+      (std::sqrt(f_x_to * f_x_to + f_y_to * f_y_to) >= mu * f_z_to))
+    return false;
+  return true;
+}
+
+void connect_action(const double *s_start, const double *s_goal, double t_s, double a[10]) {
+  const double x_td = s_start[0], y_td = s_start[1], z_td = s_start[2];  // rrt_connect.cpp:33-51
+  const double dx_td = s_start[3], dy_td = s_start[4], dz_td = s_start[5];
+  const double x_to = s_goal[0], y_to = s_goal[1], z_to = s_goal[2];
+  const double dx_to = s_goal[3], dy_to = s_goal[4], dz_to = s_goal[5];
+  const double p_td = s_start[6], dp_td = s_start[7], p_to = s_goal[6], dp_to = s_goal[7];
+  a[0] = -(2.0 * (3.0 * x_td - 3.0 * x_to + 2.0 * dx_td * t_s + dx_to * t_s)) / (t_s * t_s);
+  a[1] = -(2.0 * (3.0 * y_td - 3.0 * y_to + 2.0 * dy_td * t_s + dy_to * t_s)) / (t_s * t_s);
+  a[2] = -(2.0 * (3.0 * z_td - 3.0 * z_to + 2.0 * dz_td * t_s + dz_to * t_s)) / (t_s * t_s);
+  a[3] = (2.0 * (3.0 * x_td - 3.0 * x_to + dx_td * t_s + 2.0 * dx_to * t_s)) / (t_s * t_s);
+  a[4] = (2.0 * (3.0 * y_td - 3.0 * y_to + dy_td * t_s + 2.0 * dy_to * t_s)) / (t_s * t_s);
+  a[5] = (2.0 * (3.0 * z_td - 3.0 * z_to + dz_td * t_s + 2.0 * dz_to * t_s)) / (t_s * t_s);
+  a[6] = t_s;
+  a[7] = 0;
+  a[8] = -(2.0 * (3.0 * p_td - 3.0 * p_to + 2.0 * dp_td * t_s + dp_to * t_s)) / (t_s * t_s);
+  a[9] = (2.0 * (3.0 * p_td - 3.0 * p_to + dp_td * t_s + 2.0 * dp_to * t_s)) / (t_s * t_s);
+}
+
+int attempt_connect(const Terrain &T, const double *s_existing, const double *s0, double t_s,
+                    double s_new[8], double a_new[10], int direction, int adaptive, int max_depth,
+                    uint32_t *flags) {
+  double s[8];
+  std::memcpy(s, s0, sizeof s);
+  uint32_t fl = 0;
+  int result = GBP_TRAPPED;
+  for (int depth = 0;; depth++) {
+    if (depth > max_depth) {  // engine convention: the reference recursion is unbounded
+      fl |= GBP_F_DEPTH_CAPPED;
+      break;
+    }
+    if (t_s <= KINEMATICS_RES) break;  // :23-24
+    const double *s_start = direction == GBP_FORWARD ? s_existing : s;
+    const double *s_goal = direction == GBP_FORWARD ? s : s_existing;
+    connect_action(s_start, s_goal, t_s, a_new);
+    if (!is_valid_action(a_new)) break;  // :66, :83
+    double sn[8], tn = 0;
+    uint32_t f = 0;
+    const bool ok = pair_check(T, direction == GBP_FORWARD ? s_start : s_goal, a_new, direction,
+                               adaptive, sn, &tn, &f, nullptr);
+    fl |= f & (GBP_F_OOD | GBP_F_NAN | GBP_F_LIMIT);
+    if (f & GBP_F_SNEW_SET) std::memcpy(s_new, sn, sizeof sn);
+    if (ok) {
+      result = depth == 0 ? GBP_REACHED : GBP_ADVANCED;  // :74-75, :79-80
+      break;
+    }
+    // :77 recurse toward the returned state; unassigned t_new / s_new: TRAPPED
+    if (!(f & GBP_F_TNEW_SET) || !(f & GBP_F_SNEW_SET)) break;
+    std::memcpy(s, sn, sizeof s);
+    t_s = tn;
+  }
+  if (flags) *flags = fl;
+  return result;
+}
+
 }  // namespace gbp_host

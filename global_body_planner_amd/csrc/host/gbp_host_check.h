@@ -37,5 +37,19 @@ bool pair_check(const Terrain &T, const double s[8], const double a[10], int dir
 
 // rrt.cpp:24 / :55-68 stateDistance (planning_utils.cpp:116-127)
 double state_distance(const double *q1, const double *q2);
+// planning_utils.cpp:106-115
+double pose_distance(const double *q1, const double *q2);
+// planning_utils.cpp:519-556
+bool is_valid_action(const double a[10]);
+// rrt_connect.cpp:53-66: the cubic-Hermite stance action from s_start to s_goal
+void connect_action(const double *s_start, const double *s_goal, double t_s, double a[10]);
+// RRTConnectClass::attemptConnect (rrt_connect.cpp:20-84), its recursion as a
+// loop, with the engine's conventions (gbp.h): a failed check that left t_new
+// / s_new unassigned is TRAPPED, a connection still open after level max_depth
+// is TRAPPED (flags |= GBP_F_DEPTH_CAPPED).  s_new / a_new are written where the
+// reference writes them; flags collects the levels' OOD / NAN / LIMIT bits.
+int attempt_connect(const Terrain &T, const double *s_existing, const double *s, double t_s,
+                    double s_new[8], double a_new[10], int direction, int adaptive, int max_depth,
+                    uint32_t *flags);
 
 }  // namespace gbp_host

@@ -1208,6 +1208,196 @@ bool RRTConnectClass::buildRRTConnectBatched(FastTerrainMap &terrain, State s_st
   return true;
 }
 
+
+// ---- the search resident on the device (include/gbp.h device planner loop) ----
+namespace {
+
+struct DeviceTrees {
+  gbp_stream stream = nullptr;
+  gbp_plan_ws *ws = nullptr;
+  gbp_tree *tree[2] = {nullptr, nullptr};
+  ~DeviceTrees() {
+    if (stream) gbp_stream_synchronize(stream);
+    for (gbp_tree *t : tree)
+      if (t) gbp_tree_destroy(t);
+    if (ws) gbp_plan_ws_destroy(ws);
+    if (stream) gbp_stream_destroy(stream);
+  }
+};
+
+struct HostTree {  // a device tree read back once the search ends
+  std::vector<State> v;
+  std::vector<Action> a;
+  std::vector<int32_t> parent;
+  std::vector<double> g;
+};
+
+void read_tree(gbp_tree *t, gbp_stream s, HostTree &h) {
+  int64_t n = 0;
+  chk(gbp_tree_size(t, &n, s), "tree size");
+  h.v.resize(n);
+  h.a.resize(n);
+  h.parent.resize(n);
+  h.g.resize(n);
+  chk(gbp_tree_read(t, 0, n, h.v[0].data(), h.a[0].data(), h.parent.data(), h.g.data(), s),
+      "tree read");
+}
+
+std::vector<int> host_path(const HostTree &t, int idx) {  // rrt.cpp:107-118
+  std::vector<int> path{idx};
+  while (idx != 0) {
+    idx = t.parent[idx];
+    path.push_back(idx);
+  }
+  std::reverse(path.begin(), path.end());
+  return path;
+}
+
+double path_yaw(const HostTree &t, const std::vector<int> &path) {
+  // y of the last vertex: updateGYValue's sums along the parent chain (rrt.cpp:91-92)
+  double y = 0;
+  for (size_t i = 1; i < path.size(); i++)
+    y = y + stateYawDistance(t.v[path[i - 1]], t.v[path[i]]);
+  return y;
+}
+
+void extent(const HostTree &t, double e[4]) {
+  e[0] = e[2] = INFINITY;
+  e[1] = e[3] = -INFINITY;
+  for (const State &v : t.v) {
+    e[0] = std::min(e[0], v[0]);
+    e[1] = std::max(e[1], v[0]);
+    e[2] = std::min(e[2], v[1]);
+    e[3] = std::max(e[3], v[1]);
+  }
+}
+
+}  // namespace
+
+bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_start, State s_goal,
+                                            int batch, double max_time,
+                                            std::vector<State> &state_sequence,
+                                            std::vector<Action> &action_sequence,
+                                            BatchStats *stats) {
+  const auto t_start = std::chrono::high_resolution_clock::now();
+  auto since = [&]() {
+    return std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t_start).count();
+  };
+  goal_found = false;
+  wall_to_first_ = -1;
+  BatchStats local;
+  BatchStats &st = stats ? *stats : local;
+  gbp_terrain *h = terrain.handle();
+  const int dev = terrain.device();
+  const int adaptive = state_action_pair_check_adaptive_step_size_flag_ ? 1 : 0;
+  // the streams of buildRRTConnectBatched: Ta draws stream 101, Tb 102, B per half
+  const uint64_t tstream[2] = {101, 102};
+  DeviceTrees D;
+  chk(gbp_stream_create(dev, &D.stream), "stream");
+  chk(gbp_plan_ws_create(h, batch, &D.ws), "plan workspace");
+  int64_t cap = std::max<int64_t>(1 << 16, 4 * (int64_t)batch);
+  for (int k = 0; k < 2; k++) chk(gbp_tree_create(dev, cap, &D.tree[k]), "tree");
+  chk(gbp_tree_init(D.tree[0], s_start.data(), D.stream), "tree init");
+  chk(gbp_tree_init(D.tree[1], s_goal.data(), D.stream), "tree init");
+  chk(gbp_plan_reset(D.ws, extend_counter_, D.stream), "plan reset");
+  int64_t known[2] = {1, 1};
+  // half h extends tree h % 2 toward its draws [(h / 2) B, (h / 2 + 1) B)
+  auto enqueue = [&](int32_t hh, int first_stage) {
+    const int k = hh & 1;
+    chk(gbp_plan_half_dev(h, D.ws, D.tree[k], D.tree[k ^ 1], hh, k == 0 ? FORWARD : REVERSE, batch,
+                          seed_, tstream[k], (int64_t)(hh >> 1) * batch, adaptive, first_stage,
+                          D.stream),
+        "plan half");
+  };
+  // groups grow geometrically: a short search is not charged a long group's
+  // tail of gated half-iterations, a long one amortises the status read
+  const int g_max = (int)std::max<int64_t>(2, std::min<int64_t>(64, (1 << 21) / batch)) & ~1;
+  int group = 2;
+  int32_t half = 0;
+  gbp_plan_status ps{};
+  while (since() < max_time) {
+    for (int k = 0; k < 2; k++) {  // room for `group` halves of appends
+      int64_t c = 0;
+      chk(gbp_tree_capacity(D.tree[k], &c), "tree capacity");
+      if (known[k] + (int64_t)group * batch > c)
+        chk(gbp_tree_reserve(D.tree[k], std::max<int64_t>(2 * c, known[k] + (int64_t)group * batch),
+                             D.stream),
+            "tree reserve");
+    }
+    for (int g = 0; g < group; g++) enqueue(half + g, 0);
+    chk(gbp_plan_status_read(D.ws, &ps, D.stream), "plan status");
+    st.status_reads++;
+    while (ps.halt) {  // FRAGILE: re-decide on the host, resume where the sequence stopped
+      const int32_t h0 = ps.halt_half;
+      const int k = h0 & 1;
+      int resume = -1;
+      int64_t nres = 0;
+      chk(gbp_plan_resolve_host(h, D.ws, D.tree[k], D.tree[k ^ 1], k == 0 ? FORWARD : REVERSE,
+                                batch, adaptive, &resume, &nres, D.stream),
+          "plan resolve");
+      if (resume < 0) throw EngineError(GBP_E_INVALID_ARG, "plan resolve: nothing halted");
+      enqueue(h0, resume);
+      for (int32_t hh = h0 + 1; hh < half + group; hh++) enqueue(hh, 0);
+      chk(gbp_plan_status_read(D.ws, &ps, D.stream), "plan status");
+      st.status_reads++;
+    }
+    if (ps.error) throw EngineError(GBP_E_HIP, "device planner loop: look-back spin exhausted");
+    for (int k = 0; k < 2; k++) chk(gbp_tree_size(D.tree[k], &known[k], D.stream), "tree size");
+    half += group;
+    if (ps.done) {
+      goal_found = true;
+      break;
+    }
+    group = std::min(group * 2, g_max);
+  }
+  elapsed_to_first = std::chrono::high_resolution_clock::now() - t_start;
+  extend_counter_ = ps.ext_counter;
+  const int32_t halves_run = goal_found ? ps.meet_half + 1 : half;
+  st.iterations += (halves_run + 1) / 2;
+  st.targets += ps.stat_targets;
+  st.extends += ps.stat_targets;
+  st.attempts_checked += ps.stat_attempts;
+  st.connects += ps.stat_added;
+  st.fragile_resolved += ps.stat_fragile_resolved;
+  st.depth_capped += ps.stat_depth_capped;
+  HostTree A, B;
+  read_tree(D.tree[0], D.stream, A);
+  read_tree(D.tree[1], D.stream, B);
+  extent(A, st.extent_a);
+  extent(B, st.extent_b);
+  st.vertices_a = (int64_t)A.v.size();
+  st.vertices_b = (int64_t)B.v.size();
+  num_vertices = (int)(A.v.size() + B.v.size());
+  if (!goal_found) return false;
+  wall_to_first_ = elapsed_to_first.count();
+  // the meeting point: connection k of half meet_half joined T's vertex
+  // added_base + k to O's vertex o (halves after it never ran)
+  const int32_t kconn = (int32_t)(ps.meet >> 32), o = (int32_t)(ps.meet & 0xFFFFFFFFu);
+  const int32_t tvtx = ps.added_base + kconn;
+  const bool t_is_a = (ps.meet_half & 1) == 0;
+  const int ia = t_is_a ? tvtx : o, ib = t_is_a ? o : tvtx;
+  // rrt_connect.cpp:386-401 with the meeting vertices (as buildRRTConnectBatched)
+  std::vector<int> path_a = host_path(A, ia);
+  std::vector<int> path_b = host_path(B, ib);
+  std::reverse(path_b.begin(), path_b.end());
+  std::vector<Action> action_sequence_b;
+  for (size_t i = 0; i + 1 < path_b.size(); ++i) action_sequence_b.push_back(B.a[path_b[i]]);
+  const double yaw_b = path_yaw(B, host_path(B, ib));
+  path_b.erase(path_b.begin());
+  state_sequence.clear();
+  for (int i : path_a) state_sequence.push_back(A.v[i]);
+  for (int i : path_b) state_sequence.push_back(B.v[i]);
+  action_sequence.clear();
+  for (size_t i = 1; i < path_a.size(); ++i) action_sequence.push_back(A.a[path_a[i]]);
+  action_sequence.insert(action_sequence.end(), action_sequence_b.begin(), action_sequence_b.end());
+  path_length_ = A.g[ia] + B.g[ib];
+  path_yaw_ = path_yaw(A, path_a) + yaw_b;
+  path_cost_ = weightedCost(path_length_, path_yaw_);
+  path_duration_ = 0;
+  for (const Action &a : action_sequence) path_duration_ += a[6] + a[7];
+  return true;
+}
+
 bool RRTConnectClass::buildRRTConnectBatchedAnytime(FastTerrainMap &terrain, State s_start,
                                                     State s_goal, int batch, double max_time,
                                                     double max_time_opt,
@@ -1595,7 +1785,7 @@ bool RRTStarConnectClass::buildRRTStarConnectBatched(FastTerrainMap &terrain, St
 extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r,
                                     double *path_states, double *path_actions, int capacity) {
   using namespace gbp_amd;
-  if (!p || !r || p->batch < 1 || p->algorithm < 0 || p->algorithm > 2) return GBP_E_INVALID_ARG;
+  if (!p || !r || p->batch < 1 || p->algorithm < 0 || p->algorithm > 3) return GBP_E_INVALID_ARG;
   try {
     FastTerrainMap terrain(p->device);
     terrain.loadDataFlat(p->nx, p->ny, p->x, p->y, p->z, p->dx, p->dy, p->dz);
@@ -1615,6 +1805,9 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
         : p->algorithm == 2
             ? planner.buildRRTConnectBatchedAnytime(terrain, s0, s1, p->batch, p->max_time,
                                                     p->max_time_opt, states, actions, &st)
+        : p->algorithm == 3
+            ? planner.buildRRTConnectDevice(terrain, s0, s1, p->batch, p->max_time, states,
+                                            actions, &st)
             : planner.buildRRTConnectBatched(terrain, s0, s1, p->batch, p->max_time, states,
                                              actions, &st);
     double ttf = planner.wallTimeToFirst();
@@ -1639,6 +1832,9 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
       r->extent_a[k] = st.extent_a[k];
       r->extent_b[k] = st.extent_b[k];
     }
+    r->fragile_resolved = st.fragile_resolved;
+    r->depth_capped = st.depth_capped;
+    r->status_reads = st.status_reads;
     if (found) {
       double len = 0;
       for (size_t i = 1; i < states.size(); i++) len += planning_utils::poseDistance(states[i - 1], states[i]);

@@ -324,6 +324,76 @@ class Terrain:
         return h, nan, ood
 
 
+class DeviceTree:
+    """A GraphClass / PlannerClass tree resident in HBM (gbp_tree_*): states,
+    actions, parents and g on the device, its vertex count too."""
+
+    def __init__(self, root, device=0, capacity=1 << 16):
+        self._lib = L.load()
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        check(self._lib.gbp_tree_create(self.device, int(capacity), ctypes.byref(h)), "tree_create")
+        self._h = h
+        r = np.ascontiguousarray(root, np.float64).reshape(8)
+        check(self._lib.gbp_tree_init(self._h, _np_ptr(r), None), "tree_init")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._lib.gbp_tree_destroy(self._h)
+            self._h = None
+
+    def __len__(self):
+        c = ctypes.c_int64(0)
+        check(self._lib.gbp_tree_size(self._h, ctypes.byref(c), None), "tree_size")
+        return c.value
+
+    def append(self, states, actions, parents):
+        s = np.ascontiguousarray(states, np.float64).reshape(-1, 8)
+        a = np.ascontiguousarray(actions, np.float64).reshape(-1, 10)
+        p = np.ascontiguousarray(parents, np.int32).reshape(-1)
+        check(self._lib.gbp_tree_append_host(self._h, s.shape[0], _np_ptr(s), _np_ptr(a), _np_ptr(p),
+                                             None), "tree_append")
+
+    def read(self):
+        """(states [n][8], actions [n][10], parents [n], g [n]) numpy."""
+        n = len(self)
+        s, a = np.empty((n, 8)), np.empty((n, 10))
+        p, g = np.empty(n, np.int32), np.empty(n)
+        check(self._lib.gbp_tree_read(self._h, 0, n, _np_ptr(s), _np_ptr(a), _np_ptr(p), _np_ptr(g),
+                                      None), "tree_read")
+        return s, a, p, g
+
+
+class PlanWorkspace:
+    """Scratch and status of the device planner loop (gbp_plan_ws_*)."""
+
+    def __init__(self, terrain, max_batch):
+        self._lib = L.load()
+        h = ctypes.c_void_p()
+        check(self._lib.gbp_plan_ws_create(terrain._h, int(max_batch), ctypes.byref(h)), "plan_ws")
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._lib.gbp_plan_ws_destroy(self._h)
+            self._h = None
+
+    def extend_tree_host(self, terrain, tree, targets, direction, seed, extend_base=0,
+                         adaptive=False):
+        """gbp_extend_tree_host: RRTClass::extend (rrt.cpp:77-102) of `tree`
+        toward every target, nearest neighbour on the device, successors
+        appended in target order: (result, new_vertex, n_resolved)."""
+        tg = np.ascontiguousarray(targets, np.float64).reshape(-1, 8)
+        n = tg.shape[0]
+        res, vtx = np.empty(n, np.int32), np.empty(n, np.int32)
+        k = ctypes.c_int64(0)
+        check(self._lib.gbp_extend_tree_host(terrain._h, self._h, tree._h, n, _np_ptr(tg),
+                                             int(direction), int(bool(adaptive)), seed, extend_base,
+                                             _np_ptr(res), _np_ptr(vtx), ctypes.byref(k)),
+              "extend_tree_host")
+        return res, vtx, k.value
+
+
 def nearest(queries, vertices):
     """Batched PlannerClass::getNearestNeighbor (planner_class.cpp:185-200)."""
     lib = L.load()

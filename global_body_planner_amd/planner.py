@@ -37,7 +37,9 @@ class PlanResult(ctypes.Structure):
                 ("vertices_b", ctypes.c_int64), ("n_states", ctypes.c_int),
                 ("path_length", _D), ("path_cost", _D), ("path_duration", _D),
                 ("rewires", ctypes.c_int64), ("solutions", ctypes.c_int64),
-                ("extent_a", _D * 4), ("extent_b", _D * 4)]
+                ("extent_a", _D * 4), ("extent_b", _D * 4),
+                ("fragile_resolved", ctypes.c_int64), ("depth_capped", ctypes.c_int64),
+                ("status_reads", ctypes.c_int64)]
 
 
 _planner = None
@@ -73,6 +75,9 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
 
     algorithm 0: batch-synchronous RRT-Connect, stops at the first solution;
     algorithm 1: batch-synchronous RRT*-Connect, anytime until max_time;
+    algorithm 3: as 0, with the search resident on the device (trees in HBM,
+      one stream-ordered kernel sequence per half-iteration; same trees and
+      path as algorithm 0 for the same seed and batch);
     algorithm 2: RRTConnectClass::buildRRTConnect's anytime restarts
       (rrt_connect.cpp:323-467) on batch-synchronous trees: restart on the
       growing horizon, post-process every solution, keep the cheapest, stop
@@ -107,6 +112,11 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     out["states"] = states[:n].copy()
     out["actions"] = actions[:max(n - 1, 0)].copy()
     return out
+
+
+def plan_rrt_connect_device(data, start, goal, **kw):
+    """buildRRTConnectBatched with the search resident on the device (algorithm 3)."""
+    return plan_rrt_connect(data, start, goal, algorithm=3, **kw)
 
 
 def plan_rrt_star_connect(data, start, goal, **kw):

@@ -80,6 +80,7 @@ extern "C" {
 #define GBP_F_RESOLVED   (1u << 7)  /* a FRAGILE attempt whose outputs were re-decided on the
                                        host with glibc trig (gbp_resolve_fragile_host)        */
 #define GBP_MAX_SAMPLES  7000u
+#define GBP_F_DEPTH_CAPPED (1u << 12) /* a connect stopped at GBP_CONNECT_MAX_DEPTH (TRAPPED) */
 #define GBP_F_STAGE_SHIFT 8u        /* bits 8..11: stage in which the check ended          */
 #define GBP_F_STAGE_MASK  (0xFu << GBP_F_STAGE_SHIFT)
 #define GBP_STAGE_FWD_STANCE 1u     /* planning_utils.cpp:718-730 */
@@ -293,6 +294,113 @@ int gbp_neighbors_batch_dev(int64_t n_query, const double *queries, int64_t n_ve
 int gbp_neighbors_batch_host(int64_t n_query, const double *queries, int64_t n_vert,
                              const double *vertices, double radius, int max_out, int32_t *out,
                              int32_t *count);
+
+/* ---- streams ------------------------------------------------------------ */
+int gbp_stream_create(int device, gbp_stream *out);  /* a non-blocking HIP stream */
+int gbp_stream_destroy(gbp_stream stream);
+
+/* ---- device-resident trees (GraphClass / PlannerClass storage,
+ *      graph_class.cpp:28-77, planner_class.cpp) ------------------------------
+ * A tree lives in HBM as SoA arrays: states [cap][8], the action that reached
+ * each vertex [cap][10], parent [cap] (-1 at the root), g [cap] (cost to come,
+ * g[parent] + poseDistance, graph_class.cpp:36-42), and its vertex count, kept
+ * on the device so that kernels append to it without a host round trip.  The
+ * yaw cost y (stateYawDistance, an atan2) is left to the host, which computes
+ * it along the returned path with glibc, as the reference does. */
+typedef struct gbp_tree gbp_tree;
+int gbp_tree_create(int device, int64_t capacity, gbp_tree **out);
+int gbp_tree_destroy(gbp_tree *tree);
+/* GraphClass::init (graph_class.cpp:141-152): count = 1, vertex 0 = root */
+int gbp_tree_init(gbp_tree *tree, const double *root, gbp_stream stream);
+/* grows the arrays (contents kept); synchronises the stream */
+int gbp_tree_reserve(gbp_tree *tree, int64_t capacity, gbp_stream stream);
+int gbp_tree_capacity(gbp_tree *tree, int64_t *capacity);
+int gbp_tree_size(gbp_tree *tree, int64_t *count, gbp_stream stream);  /* synchronous */
+/* host copies of vertices [first, first + n); any output may be NULL (synchronous) */
+int gbp_tree_read(gbp_tree *tree, int64_t first, int64_t n, double *states, double *actions,
+                  int32_t *parents, double *g, gbp_stream stream);
+/* appends n vertices (addVertex + addEdge + addAction) in order; g computed on
+ * the device; parents may name vertices appended earlier in the same call */
+int gbp_tree_append_host(gbp_tree *tree, int64_t n, const double *states, const double *actions,
+                         const int32_t *parents, gbp_stream stream);
+/* the tree's device arrays (for gbp_nearest_batch_dev and the like) */
+int gbp_tree_device_ptrs(gbp_tree *tree, double **states, int32_t **count);
+
+/* ---- the device planner loop (RRTConnectClass::runRRTConnect,
+ *      rrt_connect.cpp:230-314, batch-synchronous) ---------------------------
+ * One half-iteration, enqueued on `stream` without any host synchronisation:
+ *   stage 0  `batch` draws of T's randomState stream (planner_class.cpp:38-76),
+ *            index target_index_base + i, and isValidState(STANCE) (:254)
+ *   stage 1  the valid draws, compacted in order (wave ballot + prefix, look-back)
+ *   stage 2  nearest vertex of T per target, newConfig's 6 candidates per target
+ *            from the extend stream (gbp_extend_batch_dev's), their pair checks,
+ *            the first valid one and the acceptance test (rrt.cpp:20-101)
+ *   stage 3  non-TRAPPED successors appended to T in target order
+ *   stage 4  each new vertex connected to its nearest vertex of O
+ *            (attemptConnect, rrt_connect.cpp:20-120), direction opposite
+ *   stage 5  non-TRAPPED connections appended to O in order; the first REACHED
+ *            one is recorded (meet) and every later enqueued stage is a no-op
+ * A FRAGILE decision halts the sequence after its stage (status.halt, every
+ * later kernel a no-op): gbp_plan_resolve_host re-decides the flagged items
+ * with glibc and returns the stage to resume the halted half-iteration at
+ * (first_stage).  The trees must have room for `batch` more vertices each. */
+#define GBP_PLAN_HALT_TARGETS 1u
+#define GBP_PLAN_HALT_EXTEND  2u
+#define GBP_PLAN_HALT_CONNECT 4u
+typedef struct {
+  uint32_t halt;          /* GBP_PLAN_HALT_* of the stage that stopped the sequence */
+  uint32_t done;          /* a connection REACHED */
+  uint32_t error;         /* a bounded device spin ran out (must be 0) */
+  int32_t halt_half;      /* the half-iteration that halted */
+  int32_t n_targets;      /* valid targets of the last executed half */
+  int32_t n_validate;     /* candidates launched (6 n_targets, 0 when gated) */
+  int32_t n_added;        /* successors appended to T */
+  int32_t added_base;     /* T's count before them */
+  int32_t n_conn_added;   /* connections appended to O */
+  int32_t meet_half;      /* the half-iteration whose connection REACHED */
+  uint64_t meet;          /* (connection index << 32) | O vertex of the first REACHED */
+  int64_t ext_base;       /* extend stream base of the last half */
+  int64_t ext_counter;    /* RRTClass extend counter after it */
+  int64_t stat_targets, stat_attempts, stat_added, stat_conn_added;
+  int64_t stat_fragile_resolved, stat_depth_capped;
+} gbp_plan_status;
+typedef struct gbp_plan_ws gbp_plan_ws;
+int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out);
+int gbp_plan_ws_destroy(gbp_plan_ws *ws);
+/* zeroes the status (meet = ~0) and sets the extend counter */
+int gbp_plan_reset(gbp_plan_ws *ws, int64_t extend_counter, gbp_stream stream);
+int gbp_plan_half_dev(gbp_terrain *t, gbp_plan_ws *ws, gbp_tree *T, gbp_tree *O, int32_t half,
+                      int direction, int64_t batch, uint64_t seed, uint64_t target_stream,
+                      int64_t target_index_base, int adaptive, int first_stage,
+                      gbp_stream stream);
+int gbp_plan_status_read(gbp_plan_ws *ws, gbp_plan_status *out, gbp_stream stream);
+/* re-decides the halted stage's FRAGILE items on the host (T, O, direction,
+ * batch of the halted half) and clears the halt; *resume_stage = the stage to
+ * resume that half at (-1: nothing was halted) */
+int gbp_plan_resolve_host(gbp_terrain *t, gbp_plan_ws *ws, gbp_tree *T, gbp_tree *O,
+                          int direction, int64_t batch, int adaptive, int *resume_stage,
+                          int64_t *n_resolved, gbp_stream stream);
+/* RRTClass::extend (rrt.cpp:77-102) for n targets against a device tree
+ * (nearest neighbour inside): targets[n][8] on the device
+ * (n_dev, if not NULL, holds the count on the device, n its maximum);
+ * result[i] = TRAPPED / ADVANCED / REACHED, new_vertex[i] = the appended vertex
+ * or -1; candidate j of extend i is drawn from the extend stream at index
+ * (extend_base + i) * 8 + j, as gbp_extend_batch_dev.  Uses ws's scratch (n <=
+ * its max_batch).  If a decision is FRAGILE the append halts (status.halt =
+ * GBP_PLAN_HALT_EXTEND): gbp_plan_resolve_host(.., O = NULL, ..) then
+ * gbp_extend_tree_finish_dev complete it.  gbp_extend_tree_host does all of
+ * that synchronously from host targets. */
+int gbp_extend_tree_dev(gbp_terrain *t, gbp_plan_ws *ws, gbp_tree *T, int64_t n,
+                        const double *targets, const int32_t *n_dev, int direction, int adaptive,
+                        uint64_t seed, int64_t extend_base, int32_t *result, int32_t *new_vertex,
+                        gbp_stream stream);
+int gbp_extend_tree_finish_dev(gbp_terrain *t, gbp_plan_ws *ws, gbp_tree *T, int64_t n,
+                               int direction, int32_t *result, int32_t *new_vertex,
+                               gbp_stream stream);
+int gbp_extend_tree_host(gbp_terrain *t, gbp_plan_ws *ws, gbp_tree *T, int64_t n,
+                         const double *targets, int direction, int adaptive, uint64_t seed,
+                         int64_t extend_base, int32_t *result, int32_t *new_vertex,
+                         int64_t *n_resolved);
 
 #ifdef __cplusplus
 }

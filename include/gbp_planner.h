@@ -328,6 +328,7 @@ struct BatchStats {
   int64_t vertices_a = 0, vertices_b = 0;
   int64_t rewires = 0, solutions = 0;
   int64_t depth_capped = 0;   // connects stopped at GBP_CONNECT_MAX_DEPTH (TRAPPED)
+  int64_t status_reads = 0;   // device loop: host synchronisations
   int64_t fragile_resolved = 0;  // attempts re-decided on the host (GBP_F_RESOLVED)
   double extent_a[4] = {0, 0, 0, 0}, extent_b[4] = {0, 0, 0, 0};  // x_min x_max y_min y_max
 };
@@ -358,6 +359,18 @@ class RRTConnectClass : public RRTClass {
   bool buildRRTConnectBatched(FastTerrainMap &terrain, State s_start, State s_goal, int batch,
                               double max_time, std::vector<State> &state_sequence,
                               std::vector<Action> &action_sequence, BatchStats *stats = nullptr);
+
+  // buildRRTConnectBatched with the whole search resident on the device
+  // (include/gbp.h "device planner loop"): both trees live in HBM, every
+  // half-iteration (targets, nearest neighbours, extends, appends, connects)
+  // is one stream-ordered kernel sequence with no host round trip, and the
+  // host reads one status record per group of half-iterations.  Same RNG
+  // streams, same insertion order, same FRAGILE re-decisions as
+  // buildRRTConnectBatched: for a given (seed, batch) both build the same trees
+  // and return the same path.
+  bool buildRRTConnectDevice(FastTerrainMap &terrain, State s_start, State s_goal, int batch,
+                             double max_time, std::vector<State> &state_sequence,
+                             std::vector<Action> &action_sequence, BatchStats *stats = nullptr);
 
   // buildRRTConnect's anytime restarts (rrt_connect.cpp:323-467) on the
   // batch-synchronous half-iterations: fresh trees every restart, a restart
@@ -509,7 +522,9 @@ typedef struct {
   int post_process;     // run postProcessPath on the found path
   int algorithm;        // 0 rrt-connect (first solution), 1 rrt-star-connect (anytime
                         // until max_time), 2 rrt-connect with the reference's anytime
-                        // restarts (best post-processed path after max_time_opt)
+                        // restarts (best post-processed path after max_time_opt),
+                        // 3 rrt-connect with the search resident on the device
+                        // (same trees and path as 0)
   double max_time_opt;  // algorithm 2: keep restarting until a solution exists and this
                         // many seconds have passed (buildRRTConnect's max_time_opt)
 } gbp_plan_params;
@@ -523,6 +538,9 @@ typedef struct {
   double path_length, path_cost, path_duration;
   int64_t rewires, solutions;  // RRT*: edges rewired, tree connections found
   double extent_a[4], extent_b[4];  // x_min, x_max, y_min, y_max of each tree's vertices
+  int64_t fragile_resolved;    // decisions re-decided on the host with glibc (GBP_F_RESOLVED)
+  int64_t depth_capped;        // connects stopped at GBP_CONNECT_MAX_DEPTH
+  int64_t status_reads;        // algorithm 3: host synchronisations of the device loop
 } gbp_plan_result;
 
 /* plans from start to goal; path_states[capacity][8] / path_actions[capacity][10]

@@ -1,0 +1,117 @@
+"""The search resident on the device (include/gbp.h "device trees and the
+device planner loop"; csrc/gbp_plan.hip) against the host-driven batched
+planner it replaces (csrc/host/gbp_planner.cpp buildRRTConnectBatched), and
+the device tree / extend-into-tree primitives (SURVEY §8(b) items 4-5,
+§8(f) row 1) against the engine's batched primitives and the oracle.
+
+Bar: for the same (seed, batch) the device loop builds the same trees and
+returns the same path, bit for bit (same RNG streams, same insertion order,
+same FRAGILE re-decisions); every path edge passes the oracle's pair check.
+Reference: rrt_connect.cpp:230-314 (runRRTConnect), rrt.cpp:77-102 (extend),
+graph_class.cpp:28-42 (addVertex / addEdge), planner_class.cpp:185-200
+(getNearestNeighbor).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from global_body_planner_amd import _lib as L
+from global_body_planner_amd import planner
+from global_body_planner_amd import terrain_data as td
+from tests.helpers import attempts_oracle, same_f64
+from tests.test_gpu_planner import _start_goal, check_path
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.mark.parametrize("name,xy,batch,seed", [
+    ("synth-rough-256", (1.0, 2.55, 4.02, 2.55), 64, 11),
+    ("synth-rough-256", (1.0, 2.55, 4.02, 2.55), 4096, 3),
+    ("slope-gridmap", (1.0, 0.0, 8.0, 0.0), 512, 3),
+])
+def test_device_loop_equals_host_batched(gpu, name, xy, batch, seed):
+    data = td.by_name(name)
+    O = oracle.OracleTerrain.from_data(data)
+    start, goal = _start_goal(O, *xy)
+    host = planner.plan_rrt_connect(data, start, goal, batch=batch, max_time=120.0, seed=seed)
+    dev = planner.plan_rrt_connect_device(data, start, goal, batch=batch, max_time=120.0, seed=seed)
+    assert host["found"] == 1 and dev["found"] == 1
+    check_path(O, dev, start, goal)
+    assert np.array_equal(dev["states"], host["states"])
+    assert np.array_equal(dev["actions"], host["actions"])
+    for k in ("vertices_a", "vertices_b", "targets", "extends", "attempts_checked", "connects",
+              "fragile_resolved", "depth_capped"):
+        assert dev[k] == host[k], (k, dev[k], host[k])
+    assert dev["path_length"] == host["path_length"] and dev["path_cost"] == host["path_cost"]
+    assert dev["status_reads"] >= 1
+    print(f"{name} batch {batch}: {dev['vertices_a']}+{dev['vertices_b']} vertices, "
+          f"{dev['extends']} extends, host {host['time_to_first']:.4f} s, device "
+          f"{dev['time_to_first']:.4f} s in {dev['status_reads']} status reads")
+
+
+def test_device_loop_stance_invalid_start(gpu):
+    """SURVEY H12 on the device loop: the STANCE-invalid slope start never grows."""
+    data = td.csv_gridmap("slope")
+    O = oracle.OracleTerrain.from_data(data)
+    start, goal = _start_goal(O, 0.0, 0.0, 8.0, 0.0)
+    out = planner.plan_rrt_connect_device(data, start, goal, batch=256, max_time=2.0, seed=1)
+    assert out["found"] == 0 and out["vertices_a"] == 1 and out["vertices_b"] > 1
+
+
+@pytest.mark.parametrize("direction", [0, 1])
+def test_extend_into_device_tree(gpu, direction):
+    """gbp_extend_tree_host (nearest neighbour, newConfig, acceptance and the
+    ordered append on the device) equals the engine's primitives composed on
+    the host: gbp_nearest_batch + gbp_extend_batch_host + appends in order; the
+    appended vertices' g is g[parent] + poseDistance (graph_class.cpp:36-42)."""
+    import global_body_planner_amd as gbp
+    data = td.synth_rough(256)
+    T = gbp.Terrain.from_data(data, device=0)
+    O = oracle.OracleTerrain.from_data(data)
+    n_tree, n = 700, 9000
+    verts, _, _, targets, _ = attempts_oracle(O, max(n_tree, n), seed=71)
+    verts, targets = verts[:n_tree], targets[:n]
+    tree = gbp.DeviceTree(verts[0], device=0)
+    tree.append(verts[1:], np.zeros((n_tree - 1, 10)), np.arange(n_tree - 1, dtype=np.int32))
+    ws = gbp.PlanWorkspace(T, n)
+    res, vtx, nres = ws.extend_tree_host(T, tree, targets, direction, seed=5, extend_base=300)
+    # the same through the batched primitives
+    idx, _ = gbp.nearest(torch.from_numpy(targets).cuda(), torch.from_numpy(verts).cuda())
+    idx = idx.cpu().numpy()
+    r2, ch2, sn2, an2, c2, f2 = T.extend_host(verts[idx], targets, direction, seed=5,
+                                              extend_base=300)
+    assert np.array_equal(res, r2)
+    keep = np.flatnonzero(r2 != L.TRAPPED)
+    assert keep.size > 0
+    assert np.array_equal(vtx[keep], n_tree + np.arange(keep.size))
+    assert np.all(vtx[r2 == L.TRAPPED] == -1)
+    s, a, p, g = tree.read()
+    assert s.shape[0] == n_tree + keep.size
+    assert np.all(same_f64(s[n_tree:], sn2[keep])) and np.all(same_f64(a[n_tree:], an2[keep]))
+    assert np.array_equal(p[n_tree:], idx[keep])
+    for j, i in enumerate(keep):
+        gp = g[idx[i]] + oracle.pose_distance(verts[idx[i]], sn2[i])
+        assert g[n_tree + j] == gp
+    print(f"direction {direction}: {keep.size} of {n} extends appended, {nres} re-decided")
+
+
+def test_device_tree_api(gpu):
+    import global_body_planner_amd as gbp
+    rng = np.random.default_rng(0)
+    root = rng.normal(size=8)
+    t = gbp.DeviceTree(root, device=0, capacity=4)
+    assert len(t) == 1
+    s = rng.normal(size=(20, 8))
+    a = rng.normal(size=(20, 10))
+    p = np.array([0] + list(range(19)), np.int32)   # a chain: parents appended in the same call
+    t.append(s, a, p)                                # grows past the initial capacity
+    S, A, P, G = t.read()
+    assert len(t) == 21 and np.array_equal(S[0], root) and np.array_equal(S[1:], s)
+    assert np.array_equal(A[1:], a) and P[0] == -1 and np.array_equal(P[1:], p)
+    acc = 0.0
+    for i in range(1, 21):
+        acc = acc + oracle.pose_distance(S[P[i]], S[i])
+        assert G[i] == G[P[i]] + oracle.pose_distance(S[P[i]], S[i])
+    with pytest.raises(L.GbpError):
+        t.append(s[:1], a[:1], np.array([99], np.int32))  # parent out of range
