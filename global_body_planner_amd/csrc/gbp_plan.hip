@@ -586,7 +586,7 @@ __global__ __launch_bounds__(TB) void k_connect(TerrainView<ZT> T, gbp_plan_stat
   const int lane = threadIdx.x & (WAVE - 1);
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x / WAVE);
   bool frag = false;
-  unsigned long long capped = 0;
+  unsigned long long capped = 0, checks = 0;
   for (int64_t k = blockIdx.x * (int64_t)(blockDim.x / WAVE) + threadIdx.x / WAVE; k < n;
        k += waves) {
     double se[8], s[8], sn[8], an[10];
@@ -607,6 +607,7 @@ __global__ __launch_bounds__(TB) void k_connect(TerrainView<ZT> T, gbp_plan_stat
       if (!is_valid_action(an)) break;  // :66
       double psn[8], ptn = 0;
       uint32_t pf = 0;
+      checks++;  // one pair check per level (BatchStats::attempts_checked)
       const bool ok = wave_pair_check<ZT, ADAPTIVE, CM>(T, cdir == GBP_FORWARD ? s_start : s_goal,
                                                         an, cdir, psn, ptn, pf);
       cf |= pf & (GBP_F_OOD | GBP_F_NAN | GBP_F_FRAGILE | GBP_F_LIMIT);
@@ -629,6 +630,7 @@ __global__ __launch_bounds__(TB) void k_connect(TerrainView<ZT> T, gbp_plan_stat
     capped += (cf & GBP_F_DEPTH_CAPPED) ? 1 : 0;
   }
   if (lane == 0) {
+    if (checks) atomicAdd((unsigned long long *)&st->stat_attempts, checks);
     if (capped) atomicAdd((unsigned long long *)&st->stat_depth_capped, capped);
     if (frag) {
       atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_CONNECT);
