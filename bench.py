@@ -74,7 +74,14 @@ def parse():
     p.add_argument("--plan-batch", type=int, default=0,
                    help="targets per half-iteration (0: SURVEY §8(d), the config's attempt batch / 6 "
                         "candidates: 43,690 at 1024^2 (256k), 10,923 at 256^2 (64k))")
-    p.add_argument("--plan-max-time", type=float, default=30.0, help="seconds per planner run")
+    p.add_argument("--plan-max-time", type=float, default=20.0, help="seconds per planner run")
+    p.add_argument("--plan-algorithm", type=int, default=3,
+                   help="3: the search resident on the device (buildRRTConnectDevice), "
+                        "0: the host-driven batched loop (buildRRTConnectBatched)")
+    p.add_argument("--config2", type=int, default=1,
+                   help="also measure config 2 (synth-rough-256, 65,536 attempts) (rank 0)")
+    p.add_argument("--fresh-batches", type=int, default=8,
+                   help="distinct resident batches cycled by the fresh-inputs serial rate")
     return p.parse_args()
 
 
@@ -171,16 +178,23 @@ def time_to_first_solution(data, name, runs, max_time, args, rank, world, dev):
     out_runs = []
     best = None
     batch = args.plan_batch or pair["batch"]
+    ext_total, time_total = 0, 0.0
     for k in range(runs):
         out = planner.plan_rrt_connect(data, start, goal, batch=batch,
-                                       max_time=max_time,
+                                       max_time=max_time, algorithm=args.plan_algorithm,
                                        seed=args.seed + 7919 * k + rank, device=dev.index)
         ttf = out["time_to_first"] if out["found"] else float("inf")
+        ext_total += out["extends"]
+        time_total += out["time_to_first"] if out["found"] else out["total_time"]
         t = torch.tensor([ttf], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
         out_runs.append({"ttfs_s": float(t.item()), "rank0_iterations": out["iterations"],
                          "rank0_extends": out["extends"],
+                         "rank0_extends_per_s": round(out["extends"] / max(
+                             out["time_to_first"] if out["found"] else out["total_time"], 1e-9), 1),
+                         "rank0_fragile_resolved": out["fragile_resolved"],
+                         "rank0_status_reads": out["status_reads"],
                          "rank0_attempts": out["attempts_checked"],
                          "rank0_vertices": out["vertices_a"] + out["vertices_b"],
                          "rank0_tree_x_extent": [round(out["extent_a"][0], 2),
@@ -198,9 +212,12 @@ def time_to_first_solution(data, name, runs, max_time, args, rank, world, dev):
     res = {"terrain": name, "value": float(np.median(solved)) if solved else None, "unit": "s",
            "solved": f"{len(solved)}/{len(out_runs)}", "runs": out_runs, "best_path": best,
            "batch": batch, "max_time_s": max_time,
+           "planner": "buildRRTConnectDevice (search resident on the device)"
+                      if args.plan_algorithm == 3 else "buildRRTConnectBatched (host loop)",
+           "planner_extends_per_s": round(ext_total / max(time_total, 1e-9), 1),
            "start": [float(v) for v in start[:3]], "goal": [float(v) for v in goal[:3]],
            "reference_s": pair["reference_s"],
-           "definition": "wall seconds from buildRRTConnectBatched start to the first REACHED "
+           "definition": "wall seconds from the build call's start to the first REACHED "
                          "connect (min over ranks), median over solved runs"}
     if pair.get("reference_note"):
         res["reference_note"] = pair["reference_note"]
@@ -251,6 +268,96 @@ def extend_micro(T, s, tgt, d, seed, launches=10):
                           "closer-than-s_near acceptance, per extend"}
 
 
+
+def measure(T, s, a, d, B, res, args, dev, world, streams=None, batches=None):
+    """The timed region of the contract: K launches back to back between a
+    barrier + synchronize on both sides, issued round-robin on S HIP streams
+    (each with its own outputs), then the same K serially on one stream, then K
+    launches bracketed by HIP events on the launch stream (the kernel's own
+    duration for the roofline).  `batches` (a list of (s, a, d) resident
+    batches) makes the serial pass cycle through distinct inputs instead.
+    Returns (elapsed_streams, elapsed_serial, kernel_ms)."""
+    import ctypes
+    VP = ctypes.c_void_p
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    ins = [(VP(x.data_ptr()), VP(y.data_ptr()), VP(z.data_ptr())) for x, y, z in (batches or [(s, a, d)])]
+    optr0 = [VP(t.data_ptr()) for t in (res.valid, res.s_new, res.t_new, res.flags, res.counts)]
+
+    def launch(inp, p, st):
+        rc = T.validate_pairs_raw(B, inp[0], inp[1], inp[2], 0, int(args.adaptive), p[0], p[1], p[2],
+                                  p[3], p[4], VP(st))
+        if rc != 0:
+            raise gbp.GbpError(rc, "validate_pairs")
+
+    S = max(1, args.streams if streams is None else streams)
+    strs = [torch.cuda.Stream(device=dev) for _ in range(S)]
+    outs = [res] + [T.validate_pairs(s, a, d, adaptive=args.adaptive) for _ in range(S - 1)]
+    optr = [[VP(t.data_ptr()) for t in (o.valid, o.s_new, o.t_new, o.flags, o.counts)] for o in outs]
+
+    def timed(fn):
+        for k in range(args.warmup):
+            fn(k)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):  # the timed region: K launches back to back
+            fn(k)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    elapsed_serial = timed(lambda k: launch(ins[k % len(ins)], optr0, sp))
+    elapsed = timed(lambda k: launch(ins[0], optr[k % S], strs[k % S].cuda_stream)) \
+        if S > 1 else elapsed_serial
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    for e0, e1 in ev:
+        e0.record(stream)
+        launch(ins[0], optr0, sp)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+    return elapsed, elapsed_serial, kern_ms
+
+
+def config2_line(args, dev):
+    """Config 2 (north_star 'extend-attempts/sec on synthetic
+    256x256'): synth-rough-256, 65,536 attempts per launch, seed 20251017, the
+    same protocol as the headline (streams, serial, HIP-event kernel time,
+    roofline, bounded single-thread CPU baseline)."""
+    data2 = td.by_name("synth-rough-256")
+    T2 = gbp.Terrain.from_data(data2, device=dev.index)
+    T2.set_option(L.OPT_WAVES, args.waves)
+    B2 = 65536
+    s2, a2, d2, _, _ = W.make_attempts(T2, B2, W.CONFIG_SEEDS[2])
+    r2 = T2.validate_pairs(s2, a2, d2, adaptive=args.adaptive)
+    torch.cuda.synchronize()
+    c = r2.counts.to(torch.int64) & 0xFFFFFFFF
+    gv = int(((c & 0xFFFF) + (c >> 16)).sum().item())
+    el, el_serial, kms = measure(T2, s2, a2, d2, B2, r2, args, dev, 1)
+    byts = B2 * (BYTES_IN + BYTES_OUT) + BYTES_PER_LOOKUP * gv
+    ach = byts / (kms * 1e-3) / 1e9
+    out = {"workload": "config 2: synth-rough-256, 65,536-attempt batch, isValidStateActionPair"
+                       "[Reverse] 50/50, seed 20251017",
+           "value": round(B2 * args.steps / el, 1), "unit": "extend-attempts/s",
+           "value_serial": round(B2 * args.steps / el_serial, 1),
+           "kernel_ms_per_launch": round(kms, 4),
+           "valid_fraction": float(r2.valid.to(torch.int64).sum().item()) / B2,
+           "lookups_per_attempt": gv / B2,
+           "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
+                        "algorithmic_bytes_per_launch": byts}}
+    if args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(data2, s2.cpu().numpy(), a2.cpu().numpy(),
+                                           d2.cpu().numpy(), min(args.cpu_seconds, 5.0))
+    return out
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -290,64 +397,22 @@ def main():
     n_frag = int(((flags & L.F_FRAGILE) != 0).sum().item())
     bytes_per_launch = B * (BYTES_IN + BYTES_OUT) + BYTES_PER_LOOKUP * gv
 
-    stream = torch.cuda.current_stream(dev)
-    sp = torch.cuda.current_stream(dev).cuda_stream
-    import ctypes
-    VP = ctypes.c_void_p
-    ptrs = [VP(t.data_ptr()) for t in (s, a, d, res.valid, res.s_new, res.t_new, res.flags, res.counts)]
-
-    def step():
-        rc = T.validate_pairs_raw(B, ptrs[0], ptrs[1], ptrs[2], 0, int(args.adaptive), ptrs[3],
-                                  ptrs[4], ptrs[5], ptrs[6], ptrs[7], VP(sp))
-        if rc != 0:
-            raise gbp.GbpError(rc, "validate_pairs")
-
-    # Steps are independent passes over the resident batch, so consecutive
-    # steps go round-robin on S non-default HIP streams (each with its own
-    # output buffers): a launch's ragged end (waves that finished their slice
-    # leave SIMD slots idle, ~27 % of a 262k launch) is filled by the next
-    # launch's start.  S = 1 is the serial loop, reported beside it.
-    S = max(1, args.streams)
-    streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
-    outs = [res] + [T.validate_pairs(s, a, d, adaptive=args.adaptive) for _ in range(S - 1)]
-    optr = [[VP(t.data_ptr()) for t in (o.valid, o.s_new, o.t_new, o.flags, o.counts)] for o in outs]
-
-    def step_on(k):
-        p = optr[k % S]
-        rc = T.validate_pairs_raw(B, ptrs[0], ptrs[1], ptrs[2], 0, int(args.adaptive), p[0], p[1],
-                                  p[2], p[3], p[4], VP(streams[k % S].cuda_stream))
-        if rc != 0:
-            raise gbp.GbpError(rc, "validate_pairs")
-
-    def timed(fn):
-        for k in range(args.warmup):
-            fn(k)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for k in range(args.steps):  # the timed region: K launches back to back
-            fn(k)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        return time.perf_counter() - t0
-
-    elapsed_serial = timed(lambda k: step())
-    elapsed = timed(step_on) if S > 1 else elapsed_serial
-    # the validate kernel's own duration for the roofline: HIP events around
-    # each launch on the launch stream, in a separate pass of K launches
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    for e0, e1 in ev:
-        e0.record(stream)
-        step()
-        e1.record(stream)
-    torch.cuda.synchronize()
-    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+    elapsed, elapsed_serial, kern_ms = measure(T, s, a, d, B, res, args, dev, world)
     elapsed_serial = sharding.reduce_run(elapsed_serial, [0], dev)[0]
+    # the rate a planner iteration sees: every launch on NEW inputs (distinct
+    # resident batches cycled serially, no replay of warm rows)
+    fresh = None
+    if args.fresh_batches > 1:
+        batches = [(s, a, d)] + [W.make_attempts(T, B, args.seed, index_base=base + k * world * B)[:3]
+                                 for k in range(1, args.fresh_batches)]
+        _, el_fresh, _ = measure(T, s, a, d, B, res, args, dev, world, streams=1, batches=batches)
+        el_fresh = sharding.reduce_run(el_fresh, [0], dev)[0]
+        fresh = {"value_serial_fresh": round(B * world * args.steps / el_fresh, 1),
+                 "ms_per_step": round(el_fresh / args.steps * 1e3, 4),
+                 "batches": args.fresh_batches,
+                 "definition": "serial launches, each on a different resident batch of the same "
+                               "distribution (no input reuse between consecutive launches)"}
+        del batches
 
     elapsed, sums = sharding.reduce_run(elapsed, [B, n_valid, n_ood, n_frag, gv], dev)
     sums = torch.tensor(sums, dtype=torch.float64)
@@ -383,7 +448,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "streams": S,
+            "streams": max(1, args.streams),
             "value_serial": round(tot_attempts / elapsed_serial, 1),
             "ms_per_step_serial": round(elapsed_serial / args.steps * 1e3, 4),
             "higher_is_better": True,
@@ -413,6 +478,7 @@ def main():
                 "kernel": "k_validate_persistent" if args.kernel == "persistent" else "k_validate_direct",
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },
+            "fresh_inputs": fresh,
             "time_to_first_solution": ttfs,
             "time_to_first_solution_config2": ttfs2,
             "time_to_first_solution_config1": ttfs1,
@@ -420,6 +486,11 @@ def main():
         if args.lookup_micro:
             out["terrain_lookup"] = terrain_lookup_micro(T, data, dev)
             out["extend_batch"] = extend_micro(T, s, tgt, d, args.seed)
+            if ttfs and ttfs.get("planner_extends_per_s"):
+                out["planner_vs_extend_batch"] = round(
+                    ttfs["planner_extends_per_s"] / out["extend_batch"]["extends_per_s"], 4)
+        if args.config2 and world == 1:
+            out["config2"] = config2_line(args, dev)
         if world == 1 and args.cpu_seconds > 0:
             s_h, a_h, d_h = s.cpu().numpy(), a.cpu().numpy(), d.cpu().numpy()
             out["cpu_baseline"] = cpu_baseline(data, s_h, a_h, d_h, args.cpu_seconds)
