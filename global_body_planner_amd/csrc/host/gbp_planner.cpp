@@ -802,6 +802,7 @@ void RRTConnectClass::attemptConnectBatch(const std::vector<State> &s_existing,
   std::vector<State> s = s0;
   std::vector<int> open(n);
   std::iota(open.begin(), open.end(), 0);
+  std::vector<uint8_t> resolved(stats ? n : 0, 0);  // a level was re-decided on the host
   for (int depth = 0; !open.empty() && depth <= max_depth; depth++) {
     std::vector<int> chk_idx;
     std::vector<State> cs;
@@ -832,6 +833,7 @@ void RRTConnectClass::attemptConnectBatch(const std::vector<State> &s_existing,
     if (stats) stats->attempts_checked += m;
     for (size_t j = 0; j < chk_idx.size(); j++) {
       const int k = chk_idx[j];
+      if (stats && (fl[j] & GBP_F_RESOLVED)) resolved[k] = 1;
       if (fl[j] & GBP_F_SNEW_SET) s_new[k] = sn[j];
       if (fl[j] & GBP_F_VALID) {
         result[k] = depth == 0 ? GBP_PLANNER_REACHED : GBP_PLANNER_ADVANCED;
@@ -845,6 +847,8 @@ void RRTConnectClass::attemptConnectBatch(const std::vector<State> &s_existing,
   // still open after level max_depth: TRAPPED by the engine's cap (gbp.h
   // GBP_CONNECT_MAX_DEPTH; with max_depth 0 only REACHED is asked for)
   if (stats && max_depth > 0) stats->depth_capped += (int64_t)open.size();
+  if (stats)
+    for (uint8_t r : resolved) stats->fragile_resolved += r;
 }
 
 int RRTConnectClass::connect(PlannerClass &T, State s, FastTerrainMap &terrain, int direction) {
@@ -1059,9 +1063,12 @@ void RRTConnectClass::extendBatch(PlannerClass &T, FastTerrainMap &terrain, int 
   // targets: randomState + isValidState(STANCE) (rrt_connect.cpp:249-254)
   std::vector<State> cand = T.randomStateBatch(terrain, batch);
   std::vector<uint8_t> ok(batch);
+  std::vector<uint32_t> tflags(batch);
   chk(gbp_valid_states_host(terrain.handle(), batch, cand[0].data(), nullptr, STANCE, ok.data(),
-                            nullptr, nullptr),
+                            tflags.data(), nullptr),
       "target validity");
+  if (stats)
+    for (uint32_t f : tflags) stats->fragile_resolved += (f & GBP_F_RESOLVED) ? 1 : 0;
   std::vector<State> targets;
   for (int i = 0; i < batch; i++)
     if (ok[i]) targets.push_back(cand[i]);
