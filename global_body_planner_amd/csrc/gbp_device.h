@@ -406,6 +406,11 @@ __device__ __forceinline__ void rotation_trig_nolibm(double dx, double dy, doubl
       sy = ys / r;
     }
   }
+  if (p == 0) {  // sin(+-0) = +-0, cos(+-0) = 1 exactly, as glibc
+    sp = p;
+    cp = 1.0;
+    return;
+  }
   const double z = p * p;
   double ps = KC(-1.0 / 121645100408832000.0);              // -1/19!
   ps = __builtin_fma(ps, z, KC(1.0 / 355687428096000.0));   //  1/17!
@@ -489,6 +494,13 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
   // (4) rotation :578-594
   double cy, sy, cp, sp;
   rotation_trig_nolibm(s[3], s[4], speed, s[6], cy, sy, cp, sp);
+  // A state heading along +x with zero pitch (dy = +-0, dx > 0, p = +-0: every
+  // start / goal state of the reference node, global_body_planner.cpp:219-264)
+  // has exactly glibc's trig values: atan2(+-0, dx) = +-0 -> (1, +-0), and
+  // dx / |v| = 1 since sqrt(dx*dx) == |dx| in binary64.  Its lookup points
+  // and heights are then glibc's bit for bit, so no decision can differ and
+  // nothing is FRAGILE.
+  const double feps = (s[4] == 0 && s[3] > 0 && s[6] == 0) ? 0.0 : eps;
   const double R_11 = cy * cp, R_12 = -sy, R_13 = cy * sp;
   const double R_21 = sy * cp, R_22 = cy, R_23 = sy * sp;
   const double R_31 = -sp, R_32 = 0, R_33 = cp;
@@ -523,8 +535,8 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
     alive = alive && rl == 0;
     G += alive ? 2u : 0u;  // both heights computed before the test :618-619
     bool okl, okc, nl, nc;
-    const double gl = probe_height_bf<ZT, CM>(T, pl[k], x_leg, y_leg, eps, okl, nl);
-    const double gc = probe_height_bf<ZT, CM>(T, pk[k], x_corner, y_corner, eps, okc, nc);
+    const double gl = probe_height_bf<ZT, CM>(T, pl[k], x_leg, y_leg, feps, okl, nl);
+    const double gc = probe_height_bf<ZT, CM>(T, pk[k], x_corner, y_corner, feps, okc, nc);
     if (alive && nl) fl |= GBP_F_FRAGILE;
     if (alive && !okl) fl |= GBP_F_OOD;
     alive = alive && okl;
@@ -533,20 +545,20 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
     alive = alive && okc;
     const double leg_height = z_leg - gl;
     const double corner_height = z_corner - gc;
-    if (alive && (fabs(corner_height - hmin) < eps ||
-                  (phase == GBP_STANCE && fabs(leg_height - hmax) < eps)))
+    if (alive && (fabs(corner_height - hmin) < feps ||
+                  (phase == GBP_STANCE && fabs(leg_height - hmax) < feps)))
       fl |= GBP_F_FRAGILE;
     alive = alive && !((corner_height < hmin) || ((phase == GBP_STANCE) && (leg_height > hmax)));
   }
   // (6) underside centre :630-632
   G += alive ? 1u : 0u;
   bool oku, nu;
-  const double gu = probe_height_bf<ZT, CM>(T, pu, ux, uy, eps, oku, nu);
+  const double gu = probe_height_bf<ZT, CM>(T, pu, ux, uy, feps, oku, nu);
   if (alive && nu) fl |= GBP_F_FRAGILE;
   if (alive && !oku) fl |= GBP_F_OOD;
   alive = alive && oku;
   const double height = (s[2] + R_33 * z_body) - gu;
-  if (alive && fabs(height - hmin) < eps) fl |= GBP_F_FRAGILE;
+  if (alive && fabs(height - hmin) < feps) fl |= GBP_F_FRAGILE;
   alive = alive && !(height < hmin);
   acc.G += G;
   acc.flags |= fl;

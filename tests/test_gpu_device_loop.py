@@ -70,8 +70,13 @@ def test_extend_into_device_tree(gpu, direction):
     T = gbp.Terrain.from_data(data, device=0)
     O = oracle.OracleTerrain.from_data(data)
     n_tree, n = 700, 9000
-    verts, _, _, targets, _ = attempts_oracle(O, max(n_tree, n), seed=71)
-    verts, targets = verts[:n_tree], targets[:n]
+    verts = attempts_oracle(O, n_tree, seed=71)[0]
+    # targets near the tree (a perturbed vertex each), so that some extends get
+    # closer than their nearest vertex and are appended (rrt.cpp:52-68)
+    rng = np.random.default_rng(direction)
+    targets = verts[rng.integers(0, n_tree, n)].copy()
+    targets[:, :2] += rng.normal(scale=0.4, size=(n, 2))
+    targets[:, 3:6] += rng.normal(scale=0.5, size=(n, 3))
     tree = gbp.DeviceTree(verts[0], device=0)
     tree.append(verts[1:], np.zeros((n_tree - 1, 10)), np.arange(n_tree - 1, dtype=np.int32))
     ws = gbp.PlanWorkspace(T, n)
