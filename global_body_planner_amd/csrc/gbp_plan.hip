@@ -106,7 +106,7 @@ namespace {
 constexpr int WAVE = 64;
 constexpr int TB = 256;            // threads of the grid-stride kernels
 constexpr int CB = 1024;           // threads (items) per look-back tile
-constexpr int NN_QT = 256;         // queries per nearest-neighbour tile
+constexpr int NN_QT = 512;         // queries per nearest-neighbour tile (2 per lane)
 constexpr int NN_MAX_CHUNKS = 32;  // vertex chunks per query tile
 constexpr uint32_t LOOKBACK_SPIN_LIMIT = 1u << 24;
 
@@ -241,67 +241,82 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
 // ============================================================================
 // nearest neighbour in a device tree (planner_class.cpp:185-200)
 // ============================================================================
-// Work item (query tile qt, vertex chunk c): 256 queries (one per thread)
-// against the chunk's vertices streamed through LDS; best (distance, index)
-// per query and chunk into the partial arrays.  The chunk size is set from the
-// tree size on the device so a tile never needs more than NN_MAX_CHUNKS.
-// stateDistance's sqrt is taken only when the squared sum improves: sqrt is
-// monotone, so sum >= best_sum can never give a strictly smaller distance,
-// and equal square roots keep the earlier vertex (the strict <).
+// Work item (query tile qt, vertex chunk c): NN_QT queries, NN_QPL per lane,
+// against the chunk's vertices.  The vertex index is wave-uniform, so each
+// vertex's eight doubles arrive by one scalar load (s_load_dwordx16) and feed
+// the VALU as SGPR operands: no LDS traffic, no per-lane address arithmetic;
+// every vertex load serves 64 x NN_QPL distance evaluations.  Best (distance,
+// index) per query and chunk go to the partial arrays; the chunk size is set
+// from the tree size on the device so a tile never needs more than
+// NN_MAX_CHUNKS of them.  stateDistance's sqrt is taken only when the squared
+// sum improves: sqrt is monotone, so sum >= best_sum can never give a
+// strictly smaller distance, and equal square roots keep the earlier vertex
+// (the reference's strict <).
+constexpr int NN_QPL = 2;
+
 __device__ __forceinline__ int64_t nn_chunk(int64_t nv) {
   int64_t c = (nv + NN_MAX_CHUNKS - 1) / NN_MAX_CHUNKS;
   c = (c + 255) & ~(int64_t)255;
   return c < 256 ? 256 : c;
 }
 
-__global__ __launch_bounds__(TB) void k_nn_partial(const gbp_plan_status *st, const int32_t *nq_dev,
+__global__ __launch_bounds__(TB) void k_nn_partial(const gbp_plan_status *__restrict__ st,
+                                                   const int32_t *__restrict__ nq_dev,
                                                    const double *__restrict__ q,
-                                                   const int32_t *q_off_dev,
+                                                   const int32_t *__restrict__ q_off_dev,
                                                    const double *__restrict__ v,
-                                                   const int32_t *nv_dev, int64_t bmax,
+                                                   const int32_t *__restrict__ nv_dev, int64_t bmax,
                                                    double *__restrict__ pd,
                                                    int32_t *__restrict__ pi) {
   if (gated(st)) return;
-  __shared__ double tile[NN_QT * 8];
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   const int64_t ch = nn_chunk(nv);
   const int64_t nch = (nv + ch - 1) / ch, nqt = (nq + NN_QT - 1) / NN_QT;
   for (int64_t item = blockIdx.x; item < nqt * nch; item += gridDim.x) {
     const int64_t qt = item / nch, c = item - qt * nch;
-    const int64_t qi = qt * NN_QT + threadIdx.x;
-    const bool live = qi < nq;
-    double qq[8];
+    double qq[NN_QPL][8], best[NN_QPL], best_sum[NN_QPL];
+    int bi[NN_QPL];
+    int64_t qi[NN_QPL];
 #pragma unroll
-    for (int k = 0; k < 8; k++) qq[k] = live ? q[8 * (q_off + qi) + k] : 0.0;
-    double best = INFINITY, best_sum = INFINITY;
-    int bi = -1;
-    const int64_t v0 = c * ch, v1 = min(nv, v0 + ch);
-    for (int64_t j0 = v0; j0 < v1; j0 += NN_QT) {
-      const int cnt = (int)min<int64_t>(NN_QT, v1 - j0);
-      __syncthreads();
-      for (int e = threadIdx.x; e < cnt * 8; e += blockDim.x) tile[e] = v[8 * j0 + e];
-      __syncthreads();
-      for (int j = 0; j < cnt; j++) {
+    for (int u = 0; u < NN_QPL; u++) {
+      qi[u] = qt * NN_QT + u * TB + threadIdx.x;
+      const bool live = qi[u] < nq;
+#pragma unroll
+      for (int k = 0; k < 8; k++) qq[u][k] = live ? q[8 * (q_off + qi[u]) + k] : 0.0;
+      best[u] = INFINITY;
+      best_sum[u] = INFINITY;
+      bi[u] = -1;
+    }
+    const int j0 = (int)(c * ch), j1 = (int)min(nv, (c + 1) * ch);
+    for (int j = j0; j < j1; j++) {
+      const double *vj = v + 8 * (int64_t)__builtin_amdgcn_readfirstlane(j);
+      double vv[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) vv[k] = vj[k];
+#pragma unroll
+      for (int u = 0; u < NN_QPL; u++) {
         double sum = 0;
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-          const double d = tile[8 * j + k] - qq[k];
+          const double d = vv[k] - qq[u][k];
           sum = sum + 1.0 * d * d;  // stateDistance(q, vertex), planning_utils.cpp:116-127
         }
-        if (sum < best_sum) {
+        if (sum < best_sum[u]) {
           const double dist = sqrt(sum);
-          if (dist < best) {
-            best = dist;
-            best_sum = sum;
-            bi = (int)(j0 + j);
+          if (dist < best[u]) {
+            best[u] = dist;
+            best_sum[u] = sum;
+            bi[u] = j;
           }
         }
       }
     }
-    if (live) {
-      pd[c * bmax + qi] = best;
-      pi[c * bmax + qi] = bi;
-    }
+#pragma unroll
+    for (int u = 0; u < NN_QPL; u++)
+      if (qi[u] < nq) {
+        pd[c * bmax + qi[u]] = best[u];
+        pi[c * bmax + qi[u]] = bi[u];
+      }
   }
 }
 
