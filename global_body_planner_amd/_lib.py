@@ -46,7 +46,7 @@ EXPORTS = [
     "gbp_tree_size", "gbp_tree_read", "gbp_tree_append_host", "gbp_tree_device_ptrs",
     "gbp_plan_ws_create", "gbp_plan_ws_destroy", "gbp_plan_reset", "gbp_plan_half_dev",
     "gbp_plan_status_read", "gbp_plan_resolve_host", "gbp_extend_tree_dev",
-    "gbp_extend_tree_finish_dev", "gbp_extend_tree_host",
+    "gbp_extend_tree_finish_dev", "gbp_extend_tree_host", "gbp_tree_nearest_dev",
 ]
 
 
@@ -126,6 +126,7 @@ def load(path=None):
         "gbp_extend_tree_dev": (I, [P, P, P, I64, P, P, I, I, U64, I64, P, P, P]),
         "gbp_extend_tree_finish_dev": (I, [P, P, P, I64, I, P, P, P]),
         "gbp_extend_tree_host": (I, [P, P, P, I64, P, I, I, U64, I64, P, P, P]),
+        "gbp_tree_nearest_dev": (I, [P, P, I64, P, P, P]),
         "gbp_nearest_batch_dev": (I, [I64, P, I64, P, P, P, P]),
         "gbp_nearest_batch_host": (I, [I64, P, I64, P, P, P]),
         "gbp_neighbors_batch_dev": (I, [I64, P, I64, P, ctypes.c_double, I, P, P, P]),

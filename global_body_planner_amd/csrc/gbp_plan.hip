@@ -41,6 +41,7 @@
 #include <stdint.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -67,6 +68,7 @@ struct gbp_tree {
 
 struct gbp_plan_ws {
   int device = 0;
+  int num_cus = 256;
   int64_t bmax = 0;            // largest batch of draws per half-iteration
   gbp_plan_status *st = nullptr;
   unsigned long long *tiles = nullptr;  // look-back tile states
@@ -106,7 +108,6 @@ namespace {
 constexpr int WAVE = 64;
 constexpr int TB = 256;            // threads of the grid-stride kernels
 constexpr int CB = 1024;           // threads (items) per look-back tile
-constexpr int NN_QT = 512;         // queries per nearest-neighbour tile (2 per lane)
 constexpr int NN_MAX_CHUNKS = 32;  // vertex chunks per query tile
 constexpr uint32_t LOOKBACK_SPIN_LIMIT = 1u << 24;
 
@@ -252,7 +253,6 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
 // sum improves: sqrt is monotone, so sum >= best_sum can never give a
 // strictly smaller distance, and equal square roots keep the earlier vertex
 // (the reference's strict <).
-constexpr int NN_QPL = 2;
 
 __device__ __forceinline__ int64_t nn_chunk(int64_t nv) {
   int64_t c = (nv + NN_MAX_CHUNKS - 1) / NN_MAX_CHUNKS;
@@ -260,6 +260,7 @@ __device__ __forceinline__ int64_t nn_chunk(int64_t nv) {
   return c < 256 ? 256 : c;
 }
 
+template <int NN_QPL, int UNR>
 __global__ __launch_bounds__(TB) void k_nn_partial(const gbp_plan_status *__restrict__ st,
                                                    const int32_t *__restrict__ nq_dev,
                                                    const double *__restrict__ q,
@@ -271,7 +272,8 @@ __global__ __launch_bounds__(TB) void k_nn_partial(const gbp_plan_status *__rest
   if (gated(st)) return;
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   const int64_t ch = nn_chunk(nv);
-  const int64_t nch = (nv + ch - 1) / ch, nqt = (nq + NN_QT - 1) / NN_QT;
+  const int64_t qtile = (int64_t)NN_QPL * TB;
+  const int64_t nch = (nv + ch - 1) / ch, nqt = (nq + qtile - 1) / qtile;
   for (int64_t item = blockIdx.x; item < nqt * nch; item += gridDim.x) {
     const int64_t qt = item / nch, c = item - qt * nch;
     double qq[NN_QPL][8], best[NN_QPL], best_sum[NN_QPL];
@@ -279,7 +281,7 @@ __global__ __launch_bounds__(TB) void k_nn_partial(const gbp_plan_status *__rest
     int64_t qi[NN_QPL];
 #pragma unroll
     for (int u = 0; u < NN_QPL; u++) {
-      qi[u] = qt * NN_QT + u * TB + threadIdx.x;
+      qi[u] = qt * qtile + u * TB + threadIdx.x;
       const bool live = qi[u] < nq;
 #pragma unroll
       for (int k = 0; k < 8; k++) qq[u][k] = live ? q[8 * (q_off + qi[u]) + k] : 0.0;
@@ -288,25 +290,34 @@ __global__ __launch_bounds__(TB) void k_nn_partial(const gbp_plan_status *__rest
       bi[u] = -1;
     }
     const int j0 = (int)(c * ch), j1 = (int)min(nv, (c + 1) * ch);
-    for (int j = j0; j < j1; j++) {
-      const double *vj = v + 8 * (int64_t)__builtin_amdgcn_readfirstlane(j);
-      double vv[8];
+    for (int jb = j0; jb < j1; jb += UNR) {
+      // UNR vertices' scalar loads issued together, then their distances
+      double vv[UNR][8];
 #pragma unroll
-      for (int k = 0; k < 8; k++) vv[k] = vj[k];
+      for (int r = 0; r < UNR; r++) {
+        const int j = min(jb + r, j1 - 1);  // a clamped duplicate is skipped below
+        const double *vj = v + 8 * (int64_t)__builtin_amdgcn_readfirstlane(j);
 #pragma unroll
-      for (int u = 0; u < NN_QPL; u++) {
-        double sum = 0;
+        for (int k = 0; k < 8; k++) vv[r][k] = vj[k];
+      }
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-          const double d = vv[k] - qq[u][k];
-          sum = sum + 1.0 * d * d;  // stateDistance(q, vertex), planning_utils.cpp:116-127
-        }
-        if (sum < best_sum[u]) {
-          const double dist = sqrt(sum);
-          if (dist < best[u]) {
-            best[u] = dist;
-            best_sum[u] = sum;
-            bi[u] = j;
+      for (int r = 0; r < UNR; r++) {
+        if (jb + r >= j1) break;
+#pragma unroll
+        for (int u = 0; u < NN_QPL; u++) {
+          double sum = 0;
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const double d = vv[r][k] - qq[u][k];
+            sum = sum + 1.0 * d * d;  // stateDistance(q, vertex), planning_utils.cpp:116-127
+          }
+          if (sum < best_sum[u]) {
+            const double dist = sqrt(sum);
+            if (dist < best[u]) {
+              best[u] = dist;
+              best_sum[u] = sum;
+              bi[u] = jb + r;
+            }
           }
         }
       }
@@ -704,6 +715,12 @@ __global__ void k_extend_setup(gbp_plan_status *st, int64_t n, const int32_t *n_
     targets[i] = src[i];
 }
 
+__global__ void k_set_queries(gbp_plan_status *st, int32_t n) {
+  st->halt = 0;
+  st->done = 0;
+  st->n_targets = n;
+}
+
 __global__ void k_extend_out(const gbp_plan_status *st, int64_t n, const int32_t *__restrict__ eres,
                              const int32_t *__restrict__ evtx, int32_t *__restrict__ result,
                              int32_t *__restrict__ new_vertex) {
@@ -731,10 +748,39 @@ uint32_t next_epoch(gbp_plan_ws *w) {
 
 unsigned tiles_for(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + CB - 1) / CB); }
 
+int nn_variant() {  // GBP_NN_VARIANT=qpl*10+unroll (tuning only)
+  static int v = [] {
+    const char *e = getenv("GBP_NN_VARIANT");
+    return e ? atoi(e) : 22;
+  }();
+  return v;
+}
+int nn_grid_mult() {
+  static int v = [] {
+    const char *e = getenv("GBP_NN_GRID");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
 int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
               const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s) {
-  hipLaunchKernelGGL(k_nn_partial, dim3(num_cus * 2), dim3(TB), 0, s, w->st, nq_dev, q, q_off_dev,
-                     tr->v, tr->count, w->bmax, w->nn_d, w->nn_i);
+  const dim3 g(num_cus * nn_grid_mult()), b(TB);
+#define GBP_NN(Q, U)                                                                            \
+  hipLaunchKernelGGL((k_nn_partial<Q, U>), g, b, 0, s, w->st, nq_dev, q, q_off_dev, tr->v,      \
+                     tr->count, w->bmax, w->nn_d, w->nn_i)
+  switch (nn_variant()) {
+    case 11: GBP_NN(1, 1); break;
+    case 12: GBP_NN(1, 2); break;
+    case 14: GBP_NN(1, 4); break;
+    case 21: GBP_NN(2, 1); break;
+    case 24: GBP_NN(2, 4); break;
+    case 41: GBP_NN(4, 1); break;
+    case 42: GBP_NN(4, 2); break;
+    case 44: GBP_NN(4, 4); break;
+    default: GBP_NN(2, 2); break;
+  }
+#undef GBP_NN
   hipLaunchKernelGGL(k_nn_reduce, dim3(grid_for(w->bmax, TB, num_cus * 4)), dim3(TB), 0, s, w->st,
                      nq_dev, tr->count, w->bmax, w->nn_d, w->nn_i, out);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
@@ -1019,6 +1065,7 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   gbp_plan_ws *w = new (std::nothrow) gbp_plan_ws();
   if (!w) return GBP_E_ALLOC;
   w->device = t->device;
+  w->num_cus = t->num_cus;
   w->bmax = max_batch;
   w->ntiles = (max_batch + CB - 1) / CB + 1;
   const int64_t b = max_batch, m = GBP_NUM_GEN_STATES * max_batch;
@@ -1191,6 +1238,17 @@ int gbp_extend_tree_host(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, int64_t n,
   if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = GBP_E_HIP;
   (void)hipFree(buf);
   return rc;
+}
+
+int gbp_tree_nearest_dev(gbp_plan_ws *w, gbp_tree *T, int64_t n, const double *queries,
+                         int32_t *index, gbp_stream stream) {
+  if (!w || !tree_ok(T)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || n > w->bmax || (n > 0 && (!queries || !index))) return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  Guard g(w->device);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_set_queries, dim3(1), dim3(1), 0, s, w->st, (int32_t)n);
+  return nn_launch(w, &w->st->n_targets, queries, nullptr, T, index, w->num_cus, s);
 }
 
 int gbp_plan_resolve_host(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int direction,

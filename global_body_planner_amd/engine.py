@@ -378,6 +378,14 @@ class PlanWorkspace:
             self._lib.gbp_plan_ws_destroy(self._h)
             self._h = None
 
+    def nearest(self, tree, queries):
+        """gbp_tree_nearest_dev: nearest vertex of `tree` per query (device tensors)."""
+        q = queries.contiguous()
+        idx = torch.empty(q.shape[0], dtype=torch.int32, device=q.device)
+        check(self._lib.gbp_tree_nearest_dev(self._h, tree._h, q.shape[0], _ptr(q), _ptr(idx),
+                                             _stream(q.device.index or 0)), "tree_nearest")
+        return idx
+
     def extend_tree_host(self, terrain, tree, targets, direction, seed, extend_base=0,
                          adaptive=False):
         """gbp_extend_tree_host: RRTClass::extend (rrt.cpp:77-102) of `tree`

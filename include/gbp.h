@@ -308,6 +308,7 @@ int gbp_stream_destroy(gbp_stream stream);
  * yaw cost y (stateYawDistance, an atan2) is left to the host, which computes
  * it along the returned path with glibc, as the reference does. */
 typedef struct gbp_tree gbp_tree;
+typedef struct gbp_plan_ws gbp_plan_ws;
 int gbp_tree_create(int device, int64_t capacity, gbp_tree **out);
 int gbp_tree_destroy(gbp_tree *tree);
 /* GraphClass::init (graph_class.cpp:141-152): count = 1, vertex 0 = root */
@@ -323,6 +324,12 @@ int gbp_tree_read(gbp_tree *tree, int64_t first, int64_t n, double *states, doub
  * the device; parents may name vertices appended earlier in the same call */
 int gbp_tree_append_host(gbp_tree *tree, int64_t n, const double *states, const double *actions,
                          const int32_t *parents, gbp_stream stream);
+/* PlannerClass::getNearestNeighbor (planner_class.cpp:185-200) for n device
+ * queries[n][8] against the tree (count read on the device): index[n], ties to
+ * the lowest index like gbp_nearest_batch_dev.  Uses ws's status and scratch
+ * (n <= its max_batch). */
+int gbp_tree_nearest_dev(gbp_plan_ws *ws, gbp_tree *tree, int64_t n, const double *queries,
+                         int32_t *index, gbp_stream stream);
 /* the tree's device arrays (for gbp_nearest_batch_dev and the like) */
 int gbp_tree_device_ptrs(gbp_tree *tree, double **states, int32_t **count);
 
@@ -364,7 +371,6 @@ typedef struct {
   int64_t stat_targets, stat_attempts, stat_added, stat_conn_added;
   int64_t stat_fragile_resolved, stat_depth_capped;
 } gbp_plan_status;
-typedef struct gbp_plan_ws gbp_plan_ws;
 int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out);
 int gbp_plan_ws_destroy(gbp_plan_ws *ws);
 /* zeroes the status (meet = ~0) and sets the extend counter */
