@@ -242,7 +242,7 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
 // ============================================================================
 // nearest neighbour in a device tree (planner_class.cpp:185-200)
 // ============================================================================
-// Work item (query tile qt, vertex chunk c): NN_QT queries, NN_QPL per lane,
+// Work item (query tile qt, vertex chunk c): NN_QPL x 256 queries,
 // against the chunk's vertices.  The vertex index is wave-uniform, so each
 // vertex's eight doubles arrive by one scalar load (s_load_dwordx16) and feed
 // the VALU as SGPR operands: no LDS traffic, no per-lane address arithmetic;
@@ -748,39 +748,15 @@ uint32_t next_epoch(gbp_plan_ws *w) {
 
 unsigned tiles_for(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + CB - 1) / CB); }
 
-int nn_variant() {  // GBP_NN_VARIANT=qpl*10+unroll (tuning only)
-  static int v = [] {
-    const char *e = getenv("GBP_NN_VARIANT");
-    return e ? atoi(e) : 22;
-  }();
-  return v;
-}
-int nn_grid_mult() {
-  static int v = [] {
-    const char *e = getenv("GBP_NN_GRID");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
-}
-
 int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
               const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s) {
-  const dim3 g(num_cus * nn_grid_mult()), b(TB);
-#define GBP_NN(Q, U)                                                                            \
-  hipLaunchKernelGGL((k_nn_partial<Q, U>), g, b, 0, s, w->st, nq_dev, q, q_off_dev, tr->v,      \
-                     tr->count, w->bmax, w->nn_d, w->nn_i)
-  switch (nn_variant()) {
-    case 11: GBP_NN(1, 1); break;
-    case 12: GBP_NN(1, 2); break;
-    case 14: GBP_NN(1, 4); break;
-    case 21: GBP_NN(2, 1); break;
-    case 24: GBP_NN(2, 4); break;
-    case 41: GBP_NN(4, 1); break;
-    case 42: GBP_NN(4, 2); break;
-    case 44: GBP_NN(4, 4); break;
-    default: GBP_NN(2, 2); break;
-  }
-#undef GBP_NN
+  // one query per lane, four vertices' scalar loads in flight, 4 workgroups
+  // per CU: the fastest of {1, 2, 4} queries per lane x {1, 2, 4} vertices x
+  // {2, 4} workgroups per CU (tools/nn_micro.py, profiles/r02_nn_variants.jsonl):
+  // 0.82 T pairs/s at 20k queries x 20k vertices, 7.6x the one-workgroup-per-
+  // query / LDS-tile gbp_nearest_batch_dev
+  hipLaunchKernelGGL((k_nn_partial<1, 4>), dim3(num_cus * 4), dim3(TB), 0, s, w->st, nq_dev, q,
+                     q_off_dev, tr->v, tr->count, w->bmax, w->nn_d, w->nn_i);
   hipLaunchKernelGGL(k_nn_reduce, dim3(grid_for(w->bmax, TB, num_cus * 4)), dim3(TB), 0, s, w->st,
                      nq_dev, tr->count, w->bmax, w->nn_d, w->nn_i, out);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
