@@ -595,6 +595,18 @@ int coord_mode(const gbp_terrain *t, bool lds_ok) {
   return (t->opt_affine && t->affine) ? 2 : 0;
 }
 
+// the validate kernels' coordinate mode: LDS only if the vectors fit next to
+// the attempt rows with room for the W workgroups of 256 lanes that share a CU
+// (160 KB per CU; the direct kernel has no rows)
+int validate_coord_mode(const gbp_terrain *t, bool direct) {
+  const size_t rows = sizeof(double) * SA_ROW * (size_t)t->opt_block;
+  const size_t per_cu = std::max<int64_t>(1, t->opt_waves * 256 / t->opt_block) *
+                        (stage_bytes(t->nx, t->ny) + rows);
+  const bool lds_ok = t->opt_lds_coords && stage_bytes(t->nx, t->ny) + rows <= t->lds_max &&
+                      (direct || per_cu <= 160 * 1024);
+  return coord_mode(t, lds_ok);
+}
+
 template <class ZT, bool AD, int W, int CM>
 int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *a,
                       const uint8_t *dir, int dir_all, uint8_t *valid, double *s_new,
@@ -649,12 +661,7 @@ int launch_validate(gbp_terrain *t, int64_t n, const double *s, const double *a,
   // coordinates computed when the affine form is exact; else in LDS only if
   // they fit next to the attempt rows, with room for the W workgroups of 256
   // lanes that share a CU (160 KB per CU); else read from global memory
-  const size_t rows = sizeof(double) * SA_ROW * (size_t)t->opt_block;
-  const size_t per_cu = std::max<int64_t>(1, (int64_t)w * 256 / t->opt_block) *
-                        (stage_bytes(t->nx, t->ny) + rows);
-  const bool lds_ok = t->opt_lds_coords && stage_bytes(t->nx, t->ny) + rows <= t->lds_max &&
-                      ((t->opt_kernel == GBP_KERNEL_DIRECT && !n_dev) || per_cu <= 160 * 1024);
-  const int cm = coord_mode(t, lds_ok);
+  const int cm = validate_coord_mode(t, t->opt_kernel == GBP_KERNEL_DIRECT && !n_dev);
   // W = 1 and 2 give the same allocation (the kernel needs < 256 VGPRs)
   if (adaptive) return w >= 4 ? GBP_LV(true, 4) : (w == 3 ? GBP_LV(true, 3) : GBP_LV(true, 2));
   return w >= 4 ? GBP_LV(false, 4) : (w == 3 ? GBP_LV(false, 3) : GBP_LV(false, 2));
@@ -1011,7 +1018,9 @@ int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value) {
     case GBP_OPT_AFFINE_COORDS: *value = t->opt_affine; return GBP_OK;
     case GBP_OPT_XCD_MAP: *value = t->opt_xcd_map; return GBP_OK;
     case GBP_OPT_FAST_RCP: *value = t->opt_fast_rcp ? (t->rcp_seed != 0.0 ? 1 : 0) : 0; return GBP_OK;
-    case GBP_OPT_COORD_MODE: *value = coord_mode(t, t->opt_lds_coords != 0); return GBP_OK;
+    case GBP_OPT_COORD_MODE:  // what the validate kernel of the current options uses
+      *value = validate_coord_mode(t, t->opt_kernel == GBP_KERNEL_DIRECT);
+      return GBP_OK;
     default: return GBP_E_INVALID_ARG;
   }
 }

@@ -333,7 +333,9 @@ def test_validate_pairs_variants(gpu, coords, helpers, waves):
     T.set_option(L.OPT_AFFINE_COORDS, 1 if coords == 2 else 0)
     T.set_option(L.OPT_HELPERS, helpers)
     T.set_option(L.OPT_WAVES, waves)
-    assert T.get_option(L.OPT_COORD_MODE) == coords
+    # four 256-lane workgroups of attempt rows + coordinates exceed a CU's
+    # 160 KB of LDS: the kernel then reads the vectors from global memory
+    assert T.get_option(L.OPT_COORD_MODE) == (0 if coords == 1 and waves == 4 else coords)
     try:
         for n in (1, 63, 5000):
             s, a, d, _, _ = attempts_oracle(O, n, seed=1000 + n)
