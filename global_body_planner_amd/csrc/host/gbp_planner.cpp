@@ -11,7 +11,9 @@
 #include <cstdio>
 #include <cstring>
 #include <climits>
+#include <fstream>
 #include <numeric>
+#include <sstream>
 
 namespace gbp_amd {
 
@@ -26,9 +28,106 @@ static inline double std_min(double a, double b) { return (b < a) ? b : a; }
 static inline double std_max(double a, double b) { return (a < b) ? b : a; }
 
 // ============================================================================
+// terrain ingest (terrain_map_publisher.cpp:290-370, fast_terrain_map.cpp:31-91)
+// ============================================================================
+std::vector<std::vector<double>> loadCSV(const std::string &filename) {
+  std::vector<std::vector<double>> data;
+  std::ifstream input(filename);
+  if (!input) throw std::runtime_error("File not found: " + filename);
+  int l = 0;
+  std::string line;
+  while (std::getline(input, line)) {
+    l++;
+    if (!line.empty() && line[0] == '#') continue;  // :301 comment lines
+    std::istringstream ss(line);
+    std::vector<double> record;
+    std::string num;
+    while (std::getline(ss, num, ',')) {
+      try {
+        record.push_back(std::stod(num));
+      } catch (const std::invalid_argument &) {  // :311-314
+        std::printf("NaN found in file %s line %d\n", filename.c_str(), l);
+      }
+    }
+    data.push_back(record);
+  }
+  return data;
+}
+
+TerrainArrays terrainArraysFromCSV(const std::string &dir) {
+  const auto x_data = loadCSV(dir + "/xdata.csv");  // :333-338
+  const auto y_data = loadCSV(dir + "/ydata.csv");
+  const auto z_data = loadCSV(dir + "/zdata.csv");
+  const auto dx_data = loadCSV(dir + "/dxdata.csv");
+  const auto dy_data = loadCSV(dir + "/dydata.csv");
+  const auto dz_data = loadCSV(dir + "/dzdata.csv");
+  if (x_data.empty() || x_data[0].size() < 2 || y_data.size() < 2 || z_data.empty() ||
+      y_data[0].empty() || y_data[1].empty())
+    throw std::runtime_error("terrain CSVs too small in " + dir);
+  const int x_size = (int)z_data[0].size();  // :341-342
+  const int y_size = (int)z_data.size();
+  const float x_res = x_data[0][1] - x_data[0][0];  // :343-344 (float)
+  const float y_res = y_data[1][0] - y_data[0][0];
+  const double x_length = x_data[0].back() - x_data[0].front() + x_res;  // :345-346
+  const double y_length = y_data.back()[0] - y_data.front()[0] + y_res;
+  if (x_res != y_res)  // :347-348
+    throw std::runtime_error(
+        "Map did not have square elements, make sure x and y resolution are equal.");
+  // grid_map::GridMap::setGeometry(Length(x_length, y_length), x_res, Position(..)) (:352-356)
+  const double res = x_res;
+  const double pos[2] = {x_data[0].front() - 0.5 * x_res + 0.5 * x_length,
+                         y_data.front()[0] - 0.5 * y_res + 0.5 * y_length};
+  const int size[2] = {(int)std::round(x_length / res), (int)std::round(y_length / res)};
+  const double length[2] = {size[0] * res, size[1] * res};
+  if (size[0] != x_size || size[1] != y_size)
+    throw std::runtime_error("grid_map size differs from the CSV size");
+  for (const auto *layer : {&z_data, &dx_data, &dy_data, &dz_data}) {
+    if ((int)layer->size() < y_size) throw std::runtime_error("short terrain layer in " + dir);
+    for (int j = 0; j < y_size; j++)
+      if ((int)(*layer)[j].size() < x_size) throw std::runtime_error("short terrain row in " + dir);
+  }
+  // GridMapMath getPositionFromIndex: map position + vector to the first cell
+  // + resolution * (-index) (buffer start index 0)
+  auto position = [&](int axis, int index) {
+    const double to_first_cell = 0.5 * length[axis] - 0.5 * res;
+    return (pos[axis] + to_first_cell) + res * (double)(-index);
+  };
+  TerrainArrays t;
+  t.x_size = x_size;
+  t.y_size = y_size;
+  t.x.resize(x_size);
+  t.y.resize(y_size);
+  for (int i = 0; i < x_size; i++) t.x[i] = position(0, (x_size - 1) - i);  // fast_terrain_map.cpp:43-48
+  for (int i = 0; i < y_size; i++) t.y[i] = position(1, (y_size - 1) - i);  // :49-54
+  const size_t cells = (size_t)x_size * y_size;
+  t.z.resize(cells);
+  t.dx.resize(cells);
+  t.dy.resize(cells);
+  t.dz.resize(cells);
+  // grid_map index (ix, iy) holds data[(y_size-1) - iy][(x_size-1) - ix] as a
+  // float (:363-368); loadDataFromGridMap reads index ((x_size-1)-i, (y_size-1)-j)
+  // into z_data[i][j] (:57-68): data[j][i]
+  for (int i = 0; i < x_size; i++)
+    for (int j = 0; j < y_size; j++) {
+      const size_t k = (size_t)i * y_size + j;
+      t.z[k] = (double)(float)z_data[j][i];
+      t.dx[k] = (double)(float)dx_data[j][i];
+      t.dy[k] = (double)(float)dy_data[j][i];
+      t.dz[k] = (double)(float)dz_data[j][i];
+    }
+  return t;
+}
+
+// ============================================================================
 // FastTerrainMap
 // ============================================================================
 FastTerrainMap::FastTerrainMap(int device) : device_(device) {}
+
+void FastTerrainMap::loadMapFromCSV(const std::string &dir) {
+  const TerrainArrays t = terrainArraysFromCSV(dir);
+  loadDataFlat(t.x_size, t.y_size, t.x.data(), t.y.data(), t.z.data(), t.dx.data(), t.dy.data(),
+               t.dz.data());
+}
 
 FastTerrainMap FastTerrainMap::borrow(gbp_terrain *handle) {
   FastTerrainMap m;
@@ -967,6 +1066,22 @@ void RRTConnectClass::buildRRTConnect(FastTerrainMap &terrain, State s_start, St
                                       std::vector<State> &state_sequence,
                                       std::vector<Action> &action_sequence,
                                       double max_time_opt) {  // rrt_connect.cpp:323-467
+  if (engine_batch_ > 0) {
+    // the same restart loop (anytime horizons, post-processed solutions, the
+    // cheapest kept, stop once one exists and max_time_opt has passed), each
+    // restart's runRRTConnect run as the device-resident batched search
+    const auto t0 = std::chrono::high_resolution_clock::now();
+    success_ = 0;
+    BatchStats st;
+    const bool found = buildRRTConnectBatchedAnytime(terrain, s_start, s_goal, engine_batch_,
+                                                     max_time_solve, max_time_opt, state_sequence,
+                                                     action_sequence, &st, true);
+    elapsed_total = std::chrono::high_resolution_clock::now() - t0;
+    elapsed_to_first = std::chrono::duration<double>(wall_to_first_ >= 0 ? wall_to_first_ : 0.0);
+    num_vertices = (int)(st.vertices_a + st.vertices_b);
+    if (found && elapsed_total.count() <= 5.0) success_ = 1;  // :462-464
+    return;
+  }
   const auto t_start = std::chrono::high_resolution_clock::now();
   success_ = 0;
   length_vector_.clear();
@@ -1285,7 +1400,8 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
                                             int batch, double max_time,
                                             std::vector<State> &state_sequence,
                                             std::vector<Action> &action_sequence,
-                                            BatchStats *stats) {
+                                            BatchStats *stats, uint64_t stream_a,
+                                            uint64_t stream_b) {
   const auto t_start = std::chrono::high_resolution_clock::now();
   auto since = [&]() {
     return std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t_start).count();
@@ -1297,8 +1413,8 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
   gbp_terrain *h = terrain.handle();
   const int dev = terrain.device();
   const int adaptive = state_action_pair_check_adaptive_step_size_flag_ ? 1 : 0;
-  // the streams of buildRRTConnectBatched: Ta draws stream 101, Tb 102, B per half
-  const uint64_t tstream[2] = {101, 102};
+  // the target streams (buildRRTConnectBatched's: Ta 101, Tb 102), B draws per half
+  const uint64_t tstream[2] = {stream_a, stream_b};
   DeviceTrees D;
   chk(gbp_stream_create(dev, &D.stream), "stream");
   chk(gbp_plan_ws_create(h, batch, &D.ws), "plan workspace");
@@ -1376,6 +1492,7 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
   st.vertices_b = (int64_t)B.v.size();
   num_vertices = (int)(A.v.size() + B.v.size());
   if (!goal_found) return false;
+  st.solutions++;
   wall_to_first_ = elapsed_to_first.count();
   // the meeting point: connection k of half meet_half joined T's vertex
   // added_base + k to O's vertex o (halves after it never ran)
@@ -1410,7 +1527,7 @@ bool RRTConnectClass::buildRRTConnectBatchedAnytime(FastTerrainMap &terrain, Sta
                                                     double max_time_opt,
                                                     std::vector<State> &state_sequence,
                                                     std::vector<Action> &action_sequence,
-                                                    BatchStats *stats) {
+                                                    BatchStats *stats, bool device_loop) {
   const auto t_start = std::chrono::high_resolution_clock::now();
   auto since = [](std::chrono::high_resolution_clock::time_point t0) {
     return std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t0).count();
@@ -1430,6 +1547,37 @@ bool RRTConnectClass::buildRRTConnectBatchedAnytime(FastTerrainMap &terrain, Sta
   std::vector<Action> best_actions;
   double best_length = 0, best_yaw = 0;
   for (int restart = 0;; restart++) {  // :350-420, one pair of fresh trees per restart
+    if (device_loop) {  // the restart's runRRTConnect as the device-resident search
+      const double budget = std::min(anytime_horizon, std::max(0.0, max_time - since(t_start)));
+      std::vector<State> states;
+      std::vector<Action> actions;
+      const double w0 = wall_to_first_;
+      const bool found = buildRRTConnectDevice(terrain, s_start, s_goal, batch, budget, states,
+                                               actions, &st, 2000 + 2 * restart, 2001 + 2 * restart);
+      wall_to_first_ = w0;
+      if (!found) anytime_horizon *= horizon_expansion_factor;  // :238-242
+      double el = since(t_start);
+      if (found) {  // (buildRRTConnectDevice counted the solution)
+        if (wall_to_first_ < 0) wall_to_first_ = el;
+        postProcessPath(states, actions, terrain);  // :398
+        if (path_cost_ < cost_so_far) {             // :401-414
+          cost_so_far = path_cost_;
+          best_length = path_length_;
+          best_yaw = path_yaw_;
+          best_states = states;
+          best_actions = actions;
+          el = since(t_start);
+          length_vector_.push_back(best_length);
+          yaw_vector_.push_back(best_yaw);
+          cost_vector_.push_back(cost_so_far);
+          cost_vector_times_.push_back(el);
+        }
+        goal_found = true;
+      }
+      if (goal_found && el >= max_time_opt) break;
+      if (el >= max_time) break;
+      continue;
+    }
     PlannerClass Ta(terrain.device()), Tb(terrain.device());
     Ta.setStream(seed_, 2000 + 2 * restart);
     Tb.setStream(seed_, 2001 + 2 * restart);
@@ -1792,7 +1940,7 @@ bool RRTStarConnectClass::buildRRTStarConnectBatched(FastTerrainMap &terrain, St
 extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r,
                                     double *path_states, double *path_actions, int capacity) {
   using namespace gbp_amd;
-  if (!p || !r || p->batch < 1 || p->algorithm < 0 || p->algorithm > 3) return GBP_E_INVALID_ARG;
+  if (!p || !r || p->batch < 1 || p->algorithm < 0 || p->algorithm > 4) return GBP_E_INVALID_ARG;
   try {
     FastTerrainMap terrain(p->device);
     terrain.loadDataFlat(p->nx, p->ny, p->x, p->y, p->z, p->dx, p->dy, p->dz);
@@ -1815,11 +1963,15 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
         : p->algorithm == 3
             ? planner.buildRRTConnectDevice(terrain, s0, s1, p->batch, p->max_time, states,
                                             actions, &st)
+        : p->algorithm == 4
+            ? planner.buildRRTConnectBatchedAnytime(terrain, s0, s1, p->batch, p->max_time,
+                                                    p->max_time_opt, states, actions, &st, true)
             : planner.buildRRTConnectBatched(terrain, s0, s1, p->batch, p->max_time, states,
                                              actions, &st);
     double ttf = planner.wallTimeToFirst();
-    // algorithm 2's paths are post-processed inside the restarts (as buildRRTConnect)
-    if (found && p->post_process && p->algorithm != 2) planner.postProcessPath(states, actions, terrain);
+    // algorithm 2 / 4's paths are post-processed inside the restarts (as buildRRTConnect)
+    if (found && p->post_process && p->algorithm != 2 && p->algorithm != 4)
+      planner.postProcessPath(states, actions, terrain);
     const std::chrono::duration<double> tot = std::chrono::high_resolution_clock::now() - t0;
     memset(r, 0, sizeof(*r));
     r->found = found ? 1 : 0;
@@ -1859,6 +2011,29 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     return GBP_OK;
   } catch (const EngineError &e) {
     return e.status;
+  } catch (...) {
+    return GBP_E_INVALID_ARG;
+  }
+}
+
+extern "C" int gbp_terrain_arrays_from_csv(const char *dir, int *nx, int *ny, double *x,
+                                           double *y, double *z, double *dx, double *dy,
+                                           double *dz, int64_t capacity) {
+  if (!dir || !nx || !ny) return GBP_E_INVALID_ARG;
+  try {
+    const gbp_amd::TerrainArrays t = gbp_amd::terrainArraysFromCSV(dir);
+    *nx = t.x_size;
+    *ny = t.y_size;
+    if (!z) return GBP_OK;
+    const size_t cells = (size_t)t.x_size * t.y_size;
+    if (capacity < (int64_t)cells) return GBP_E_SHAPE;
+    if (x) std::copy(t.x.begin(), t.x.end(), x);
+    if (y) std::copy(t.y.begin(), t.y.end(), y);
+    std::copy(t.z.begin(), t.z.end(), z);
+    if (dx) std::copy(t.dx.begin(), t.dx.end(), dx);
+    if (dy) std::copy(t.dy.begin(), t.dy.end(), dy);
+    if (dz) std::copy(t.dz.begin(), t.dz.end(), dz);
+    return GBP_OK;
   } catch (...) {
     return GBP_E_INVALID_ARG;
   }

@@ -56,11 +56,36 @@ def load():
         L.gbp_plan_rrt_connect.restype = ctypes.c_int
         L.gbp_plan_rrt_connect.argtypes = [ctypes.POINTER(PlanParams), ctypes.POINTER(PlanResult),
                                            _P, _P, ctypes.c_int]
+        L.gbp_terrain_arrays_from_csv.restype = ctypes.c_int
+        L.gbp_terrain_arrays_from_csv.argtypes = [ctypes.c_char_p, _P, _P, _P, _P, _P, _P, _P, _P,
+                                                  ctypes.c_int64]
         L.gbp_attempt_connect_batch.restype = ctypes.c_int
         L.gbp_attempt_connect_batch.argtypes = [_P, ctypes.c_int64, _P, _P, _P, ctypes.c_int,
                                                 ctypes.c_int, _P, _P, _P]
         _planner = L
     return _planner
+
+
+def terrain_from_csv(directory):
+    """The C++ ingest (gbp_terrain_arrays_from_csv: TerrainMapPublisher::loadCSV
+    + loadMapFromCSV's grid_map geometry + FastTerrainMap::loadDataFromGridMap)
+    of the reference CSVs in `directory` -> terrain_data.TerrainData."""
+    from .terrain_data import TerrainData
+    L = load()
+    d = os.fsencode(str(directory))
+    nx, ny = ctypes.c_int(0), ctypes.c_int(0)
+    rc = L.gbp_terrain_arrays_from_csv(d, ctypes.byref(nx), ctypes.byref(ny), None, None, None,
+                                       None, None, None, 0)
+    if rc != 0:
+        raise _lib.GbpError(rc, f"gbp_terrain_arrays_from_csv({directory})")
+    x, y = np.empty(nx.value), np.empty(ny.value)
+    z, dx, dy, dz = (np.empty((nx.value, ny.value)) for _ in range(4))
+    rc = L.gbp_terrain_arrays_from_csv(d, ctypes.byref(nx), ctypes.byref(ny), x.ctypes.data,
+                                       y.ctypes.data, z.ctypes.data, dx.ctypes.data, dy.ctypes.data,
+                                       dz.ctypes.data, z.size)
+    if rc != 0:
+        raise _lib.GbpError(rc, f"gbp_terrain_arrays_from_csv({directory})")
+    return TerrainData(x, y, z, dx, dy, dz, name=os.path.basename(str(directory)) + "-cpp-csv")
 
 
 def start_goal_state(height, x, y):
@@ -78,6 +103,8 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     algorithm 3: as 0, with the search resident on the device (trees in HBM,
       one stream-ordered kernel sequence per half-iteration; same trees and
       path as algorithm 0 for the same seed and batch);
+    algorithm 4: as 2, each restart's search resident on the device (what
+      buildRRTConnect does by default, RRTConnectClass::set_engine_batch);
     algorithm 2: RRTConnectClass::buildRRTConnect's anytime restarts
       (rrt_connect.cpp:323-467) on batch-synchronous trees: restart on the
       growing horizon, post-process every solution, keep the cheapest, stop
@@ -124,11 +151,13 @@ def plan_rrt_star_connect(data, start, goal, **kw):
     return plan_rrt_connect(data, start, goal, algorithm=1, **kw)
 
 
-def plan_rrt_connect_anytime(data, start, goal, max_time_opt=1.0, **kw):
+def plan_rrt_connect_anytime(data, start, goal, max_time_opt=1.0, device_loop=False, **kw):
     """RRTConnectClass::buildRRTConnect's anytime restarts, batch-synchronous
-    (algorithm 2); `cost_history` is not returned, `solutions` counts the
+    (algorithm 2; algorithm 4 with device_loop: every restart's search resident
+    on the device); `cost_history` is not returned, `solutions` counts the
     restarts that reached the goal."""
-    return plan_rrt_connect(data, start, goal, algorithm=2, max_time_opt=max_time_opt, **kw)
+    return plan_rrt_connect(data, start, goal, algorithm=4 if device_loop else 2,
+                            max_time_opt=max_time_opt, **kw)
 
 
 def attempt_connect(terrain, s_existing, s, direction, t_s=None, adaptive=False, s_new=None,

@@ -80,6 +80,31 @@ struct EngineError : std::runtime_error {
   EngineError(int s, const std::string &what);
 };
 
+// ---- terrain ingest without ROS ---------------------------------------------
+// TerrainMapPublisher::loadCSV (terrain_map_publisher.cpp:290-327): comma
+// separated doubles per line, '#' lines skipped, unparsable fields reported
+// on stdout and skipped (stod("nan") parses)
+std::vector<std::vector<double>> loadCSV(const std::string &filename);
+
+// The arrays FastTerrainMap holds after the reference's CSV -> grid_map ->
+// FastTerrainMap path: TerrainMapPublisher::loadMapFromCSV (:330-370) sets a
+// grid_map geometry with a FLOAT resolution (:343-346) and float layers
+// (x-major transpose at :363-368); FastTerrainMap::loadDataFromGridMap
+// (fast_terrain_map.cpp:31-91) reads the cell-centre positions back in
+// reversed index order and casts the layers float -> double.  grid_map_core's
+// setGeometry / getPosition arithmetic (GridMap.cpp, GridMapMath.cpp; not in
+// this image) is restated: size = round(length / res), length = size * res,
+// position(index) = (map_position + (0.5 length - 0.5 res)) + res * (-index).
+struct TerrainArrays {
+  int x_size = 0, y_size = 0;
+  std::vector<double> x, y;           // ascending (x_data_, y_data_)
+  std::vector<double> z, dx, dy, dz;  // x-major [x_size][y_size]
+};
+// dir holds xdata.csv, ydata.csv, zdata.csv, dxdata.csv, dydata.csv, dzdata.csv
+// (data/<terrain_type>/ in the reference); throws std::runtime_error on a
+// missing file or non-square cells (:347-348)
+TerrainArrays terrainArraysFromCSV(const std::string &dir);
+
 // ---- FastTerrainMap (fast_terrain_map.h:14-120) ------------------------------
 class FastTerrainMap {
  public:
@@ -102,6 +127,8 @@ class FastTerrainMap {
   // used there (getSize, getPosition, at, exists); see INTEGRATION.md
   template <class GridMap>
   void loadDataFromGridMap(const GridMap &map);
+  // the node's map_data_source "csv" path without ROS (terrainArraysFromCSV)
+  void loadMapFromCSV(const std::string &dir);
 
   double getGroundHeight(const double x, const double y);               // :94-132
   bool heightIsNan(const double x, const double y);                     // :135-157
@@ -370,7 +397,8 @@ class RRTConnectClass : public RRTClass {
   // and return the same path.
   bool buildRRTConnectDevice(FastTerrainMap &terrain, State s_start, State s_goal, int batch,
                              double max_time, std::vector<State> &state_sequence,
-                             std::vector<Action> &action_sequence, BatchStats *stats = nullptr);
+                             std::vector<Action> &action_sequence, BatchStats *stats = nullptr,
+                             uint64_t stream_a = 101, uint64_t stream_b = 102);
 
   // buildRRTConnect's anytime restarts (rrt_connect.cpp:323-467) on the
   // batch-synchronous half-iterations: fresh trees every restart, a restart
@@ -379,11 +407,20 @@ class RRTConnectClass : public RRTClass {
   // first REACHED connect; every solution is post-processed and the cheapest
   // (path_cost_) kept.  Stops once a solution exists and max_time_opt has
   // passed, or at max_time without one.  Returns the best path.
+  // device_loop: each restart's search runs device-resident (buildRRTConnectDevice).
   bool buildRRTConnectBatchedAnytime(FastTerrainMap &terrain, State s_start, State s_goal,
                                      int batch, double max_time, double max_time_opt,
                                      std::vector<State> &state_sequence,
                                      std::vector<Action> &action_sequence,
-                                     BatchStats *stats = nullptr);
+                                     BatchStats *stats = nullptr, bool device_loop = false);
+
+  // How buildRRTConnect (the call GlobalBodyPlanner::callPlanner makes,
+  // global_body_planner.cpp:115) searches: batch > 0 (default 1024) runs its
+  // restart loop on the device-resident batched search with that many random
+  // targets per half-iteration; 0 runs the reference's sequential
+  // runRRTConnect, one engine call per extend / connect.
+  void set_engine_batch(int batch) { engine_batch_ = batch; }
+  int engine_batch() const { return engine_batch_; }
 
   // attemptConnect for many independent pairs (lock-step rounds, one engine
   // launch per recursion depth); s_new / a_new are in/out per pair
@@ -400,6 +437,7 @@ class RRTConnectClass : public RRTClass {
   const double planning_rate_estimate = 16.0;
   double horizon_expansion_factor = 1.2;
   const int max_time_solve = 4000;
+  int engine_batch_ = 1024;
 
   // lock-step attemptConnect for many (s_existing, s, t_s) triples; with
   // max_depth = 0 only REACHED is decided (callers that test == REACHED)
@@ -524,7 +562,7 @@ typedef struct {
                         // until max_time), 2 rrt-connect with the reference's anytime
                         // restarts (best post-processed path after max_time_opt),
                         // 3 rrt-connect with the search resident on the device
-                        // (same trees and path as 0)
+                        // (same trees and path as 0), 4 = 2 on the device-resident search
   double max_time_opt;  // algorithm 2: keep restarting until a solution exists and this
                         // many seconds have passed (buildRRTConnect's max_time_opt)
 } gbp_plan_params;
@@ -547,6 +585,15 @@ typedef struct {
  * (may be NULL).  Returns GBP_OK or a negative status. */
 int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r, double *path_states,
                          double *path_actions, int capacity);
+
+/* terrainArraysFromCSV (host only, no device): the FastTerrainMap arrays of
+ * the reference's CSV -> grid_map -> FastTerrainMap path for the CSVs in dir.
+ * Call with z == NULL to get nx / ny; then x[nx], y[ny], z/dx/dy/dz[nx][ny]
+ * (x-major; any of dx/dy/dz may be NULL) are filled when capacity >= nx * ny.
+ * Returns GBP_OK, GBP_E_SHAPE (capacity too small) or GBP_E_INVALID_ARG
+ * (unreadable / non-square map). */
+int gbp_terrain_arrays_from_csv(const char *dir, int *nx, int *ny, double *x, double *y,
+                                double *z, double *dx, double *dy, double *dz, int64_t capacity);
 
 /* RRTConnectClass::attemptConnect (rrt_connect.cpp:20-91) for n independent
  * (s_existing, s) pairs on an engine terrain handle, lock-step batched.

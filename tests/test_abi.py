@@ -100,7 +100,8 @@ def test_planner_library_exports_and_fails_without_device():
     out = subprocess.run(["nm", "-D", "--defined-only", planner.PLANNER_PATH], capture_output=True,
                          text=True, check=True).stdout
     c_syms = set(re.findall(r"\bT (gbp_\w+)", out))
-    assert c_syms == {"gbp_plan_rrt_connect", "gbp_attempt_connect_batch"}
+    assert c_syms == {"gbp_plan_rrt_connect", "gbp_attempt_connect_batch",
+                      "gbp_terrain_arrays_from_csv"}
     txt = open(os.path.join(ROOT, "include", "gbp_planner.h")).read()
     for name in c_syms:
         assert f"int {name}(" in txt
@@ -116,13 +117,18 @@ def test_planner_library_exports_and_fails_without_device():
         assert e.value.status == -6
 
 
-def build_node_callsite(out):
+def build_node_callsite(out, src="node_callsite.cpp"):
     """g++ the ROS-node call-site check against the reference's global names."""
     lib = os.path.join(ROOT, "global_body_planner_amd", "lib")
     subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "tests", "integration", "node_callsite.cpp"), "-L", lib,
+                    os.path.join(ROOT, "tests", "integration", src), "-L", lib,
                     "-lgbp_planner", "-lgbp", f"-Wl,-rpath,{lib}", "-o", str(out)], check=True)
     return str(out)
+
+
+def test_node_config1_compiles(tmp_path):
+    """The config-1 node twin (CSV ingest + buildRRTConnect) builds against the drop-in."""
+    assert os.path.exists(build_node_callsite(tmp_path / "node_config1", src="node_config1.cpp"))
 
 
 def test_node_callsite_compiles_links_and_refuses_cpu(tmp_path):

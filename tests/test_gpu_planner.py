@@ -196,3 +196,26 @@ def test_plan_anytime_restarts_synth256(gpu):
                                            max_time=30.0, seed=9)
     assert one["found"] == 1 and one["solutions"] == 1
     assert out["path_cost"] <= one["path_cost"] + 1e-12  # same first restart, then only improvements
+
+
+def test_node_entry_point_config1(gpu, tmp_path):
+    """Config 1 through the node's own call (tests/integration/node_config1.cpp:
+    CSV ingest in C++, setStartAndGoalStates, RRTConnectClass::buildRRTConnect
+    with replan_time_limit 0, getStatistics, getInterpPath) on the slope CSV,
+    (1, 0) -> (8, 0): the default device-resident batched search and the
+    sequential per-call loop (set_engine_batch(0)) both return a valid path.
+    Reference wall times: 12.0 / 27.0 / 28.8 s (seeds 3/1/2)."""
+    import json
+    import subprocess
+    from tests.test_abi import build_node_callsite
+    from tests.test_csv_ingest import write_csvs
+    exe = build_node_callsite(tmp_path / "node_config1", src="node_config1.cpp")
+    d = write_csvs("slope", tmp_path / "slope")
+    for batch, seeds, limit in ((1024, ["1", "2", "3"], 120), (0, ["1"], 300)):
+        r = subprocess.run(["timeout", "-k", "10", str(limit), exe, str(d), str(batch)] + seeds,
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
+        runs = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+        assert len(runs) == len(seeds) and all(x["ok"] == 1 for x in runs)
+        for x in runs:
+            print("node_config1", json.dumps(x))
