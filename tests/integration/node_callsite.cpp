@@ -46,6 +46,8 @@ struct GridMap {
 
 int main(int argc, char **argv) {
   const bool star = argc > 1 && std::string(argv[1]) == "star";  // algorithm: rrt-star-connect
+  // "seq": buildRRTConnect's sequential per-call search (set_engine_batch(0))
+  const bool seq = argc > 1 && std::string(argv[1]) == "seq";
   fake_grid_map::GridMap map{120, 60, 0.05, {}};
   map.z.assign((size_t)map.nx * map.ny, 0.0f);  // flat ground
   FastTerrainMap terrain_;
@@ -64,6 +66,7 @@ int main(int argc, char **argv) {
     o->set_action_direction_sampling(false, 0.15);
     o->set_state_direction_sampling(false, 0.05, false);
   }
+  if (seq) rrt_connect_obj.set_engine_batch(0);
 
   std::vector<State> state_sequence_;
   std::vector<Action> action_sequence_;
