@@ -226,9 +226,10 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
     // Normally a lane evaluates its own attempt's next sample.  In a wave's
     // tail (no work left to refill idle lanes) the idle lanes become helpers:
     // helper j of owner r evaluates the owner's sample `slot` steps ahead,
-    // assuming the samples in between pass (advance_on_success); the owner
-    // then consumes the results in order and stops at the first failure or
-    // stage change, so exactly the reference's samples are counted.
+    // assuming the samples in between pass (advance_on_success, across stage
+    // boundaries: stance -> flight -> landing on the all-pass path); the
+    // owner then consumes the results in order and stops at the first
+    // failure or decision, so exactly the reference's samples are counted.
     const int n_act = __popcll(act);
     const bool tail = helpers && n_act < WAVE;  // every idle lane is exhausted here
     int st = L.stage, slot = 0;
@@ -248,7 +249,7 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
       if (!owner) {
         has = true;
         for (int k = 0; k < slot && has; k++) has = advance_on_success<ADAPTIVE>(st, ps + 8, t, ts);
-        t_eval = t;
+        t_eval = sample_time(st, ps + 8, t);
       }
     }
     Acc acc_s{0, vbase + (uint32_t)slot, 0};
@@ -272,7 +273,7 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
                           ((acc_s.V - (vbase + (uint32_t)slot)) << 18);
       const uint32_t w1 = acc_s.G;
       const int my_rank = __popcll(act & lt_mask);
-      bool chain = owner && !decided && ok && L.stage == st;
+      bool chain = owner && !decided && ok;
       const int kmax = (n_idle + n_act - 1) / n_act;
       for (int k = 1; k <= kmax; k++) {
         const int j = (k - 1) * n_act + my_rank;
@@ -285,7 +286,7 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
           L.acc.flags |= r0 & 0xFFFFu;
           const bool okk = (r0 >> 16) & 1u;
           decided = (r0 & GBP_F_LIMIT) ? true : transition<ADAPTIVE>(L, okk);
-          chain = !decided && okk && L.stage == st;
+          chain = !decided && okk;
         } else {
           chain = false;
         }

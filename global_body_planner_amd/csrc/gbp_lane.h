@@ -176,26 +176,51 @@ __device__ __forceinline__ double stage_time(const Lane &L) {
   return L.stage == ST_FWD_LAND ? L.a[7] : (L.stage == ST_REV_START ? 0.0 : L.t);
 }
 
-// Advance (t, ts) the way a SUCCESSFUL sample of loop stage `st` does in
-// transition() below, and test the loop condition: the time of the next
-// sample if the current one passes.  false: the loop ends (or a one-sample
-// stage).  Used by tail helpers to evaluate an owner's future samples.
+// Advance (st, t, ts) the way a SUCCESSFUL sample does in transition() below,
+// across stage boundaries (enter_stage's resets and skips included): the
+// stage and time of the attempt's next sample if the current one passes.
+// false: a passing sample decides the attempt (FWD_LAND, REV_START).  On the
+// success path the sample sequence is deterministic, so tail helpers use this
+// to evaluate an owner's future samples, in the same stage or a later one.
 template <bool ADAPTIVE>
-__device__ __forceinline__ bool advance_on_success(int st, const double *a, double &t, double &ts) {
+__device__ __forceinline__ bool advance_on_success(int &st, const double *a, double &t, double &ts) {
   switch (st) {
-    case ST_FWD_STANCE:
+    case ST_FWD_STANCE:  // transition :218-230
       if (ADAPTIVE) { ts += KINEMATICS_RES; t += ts; } else { t += KINEMATICS_RES; }
-      return t <= a[6];
+      if (t <= a[6]) return true;
+      st = ST_FWD_FLIGHT;  // enter_stage(FWD_FLIGHT)
+      t = 0;
+      ts = KINEMATICS_RES;
+      if (t < a[7]) return true;
+      st = ST_FWD_LAND;
+      return true;
     case ST_FWD_FLIGHT:
+      if (ADAPTIVE) { ts += KINEMATICS_RES; t += ts; } else { t += KINEMATICS_RES; }
+      if (t < a[7]) return true;
+      st = ST_FWD_LAND;
+      return true;
     case ST_REV_FLIGHT:
       if (ADAPTIVE) { ts += KINEMATICS_RES; t += ts; } else { t += KINEMATICS_RES; }
-      return t < a[7];
+      if (t < a[7]) return true;
+      st = ST_REV_STANCE;  // enter_stage(REV_STANCE)
+      t = a[6];
+      ts = KINEMATICS_RES;
+      if (t >= 0) return true;
+      st = ST_REV_START;
+      return true;
     case ST_REV_STANCE:
       if (ADAPTIVE) { ts += KINEMATICS_RES; t -= ts; } else { t -= KINEMATICS_RES; }
-      return t >= 0;
+      if (t >= 0) return true;
+      st = ST_REV_START;
+      return true;
     default:
       return false;
   }
+}
+
+// the sample time of stage st at loop time t (stage_time for a helper's copy)
+__device__ __forceinline__ double sample_time(int st, const double *a, double t) {
+  return st == ST_FWD_LAND ? a[7] : (st == ST_REV_START ? 0.0 : t);
 }
 
 // the reference's control flow after one isValidState result `ok` of the

@@ -531,8 +531,9 @@ __device__ __forceinline__ void connect_action(const double *s_start, const doub
 // holds the same Lane state (wave-uniform); per step, lane j evaluates the
 // sample j positions ahead on the all-pass path (advance_on_success), then
 // every lane replays the reference's transitions on the ballot of results in
-// order, stopping at the first failure, stage change or decision — exactly
-// the reference's samples are counted.  Connect actions run t_s / 0.05 + 1
+// order, stopping at the first failure or decision (the all-pass path crosses
+// stage boundaries deterministically) — exactly the reference's samples are
+// counted.  Connect actions run t_s / 0.05 + 1
 // stance samples (dozens to hundreds): a wave covers 64 of them per step.
 template <class ZT, bool ADAPTIVE, int CM>
 __device__ bool wave_pair_check(const TerrainView<ZT> &T, const double *s_in, const double *a_in,
@@ -555,7 +556,7 @@ __device__ bool wave_pair_check(const TerrainView<ZT> &T, const double *s_in, co
     double t = L.t, ts = L.ts;
     bool has = true;
     for (int k = 0; k < lane && has; k++) has = advance_on_success<ADAPTIVE>(stg, av, t, ts);
-    const double t_eval = lane == 0 ? stage_time(L) : t;
+    const double t_eval = lane == 0 ? stage_time(L) : sample_time(stg, av, t);
     Acc acc{0, L.acc.V + (uint32_t)lane, 0};
     bool ok = false;
     if (has) {
@@ -576,7 +577,7 @@ __device__ bool wave_pair_check(const TerrainView<ZT> &T, const double *s_in, co
       }
       L.acc.V += 1;
       decided = transition<ADAPTIVE>(L, okj);
-      if (decided || !okj || L.stage != stg) break;
+      if (decided || !okj) break;
     }
   }
   uint32_t f = L.f | L.acc.flags;
