@@ -130,9 +130,38 @@ __device__ __forceinline__ void fetch_cell(const TerrainView<ZT> &T, int ix, int
   q[3] = c[3];
 }
 
-// bracket() of axis AX of the view, coordinates per CM
-template <int CM, int AX, class ZT>
+// bracket() of axis AX of the view, coordinates per CM.  ONE: the caller has
+// checked (wave-uniformly) that the view's one-step guess is exact on both
+// axes; the bracket is then straight-line code — the guess from a point
+// clamped into the domain (so the coordinate reads stay in range and a NaN
+// never reaches the int conversion), one correction step, and the
+// out-of-domain codes as selects — so the ten probes of a state check form
+// one block the compiler schedules together (their coordinate reads and
+// terrain gathers in flight at once) instead of ten branchy regions each
+// waiting on its own reads.
+// `cell` receives a valid cell index (the bracket, or 0 without one) that the
+// caller fetches from unconditionally: the straight-line form's index is then
+// used on every path, so the compiler cannot sink its computation (and the
+// coordinate reads) back under a branch.
+template <int CM, int AX, bool ONE = false, class ZT>
+__device__ __forceinline__ int bracket_ax(const TerrainView<ZT> &T, double v, int &cell) {
+  const double d0 = AX == 0 ? T.x0 : T.y0, dN = AX == 0 ? T.xN : T.yN;
+  const int n = AX == 0 ? T.nx : T.ny;
+  if constexpr (ONE) {
+    const bool in = (v >= d0) & (v < dN);
+    const double vc = in ? v : d0;  // no bracket: cell 0 (its guess is 0, its correction 0)
+    int i = bracket_guess(n, d0, AX == 0 ? T.inv_hx : T.inv_hy, vc);
+    i += (vc >= coord<CM, AX>(T, i + 1) ? 1 : 0) - (vc < coord<CM, AX>(T, i) ? 1 : 0);
+    cell = i;
+    return in ? i : (v >= dN ? BR_HIGH : BR_LOW);
+  }
+  const int r = bracket_ax<CM, AX, false>(T, v);
+  cell = r < 0 ? 0 : r;
+  return r;
+}
+template <int CM, int AX, bool ONE = false, class ZT>
 __device__ __forceinline__ int bracket_ax(const TerrainView<ZT> &T, double v) {
+  static_assert(!ONE, "the straight-line bracket returns its cell");
   const double d0 = AX == 0 ? T.x0 : T.y0, dN = AX == 0 ? T.xN : T.yN;
   const int n = AX == 0 ? T.nx : T.ny;
   if (!(v >= d0 && v < dN)) return (v >= dN) ? BR_HIGH : BR_LOW;
@@ -225,15 +254,15 @@ __device__ __forceinline__ bool height_at(const TerrainView<ZT> &T, double x, do
 template <class ZT>
 struct Probe {
   int ix, iy;   // bracket codes: >= 0, BR_LOW or BR_HIGH
-  ZT q[4];      // z[cx][cy], z[cx][cy+1], z[cx+1][cy], z[cx+1][cy+1] of the clamped cell
+  int cx, cy;   // the fetched cell: the bracket, or 0 on an axis without one
+  ZT q[4];      // z[cx][cy], z[cx][cy+1], z[cx+1][cy], z[cx+1][cy+1]
 };
 
-template <class ZT, int CM = 0>
+template <class ZT, int CM = 0, bool ONE = false>
 __device__ __forceinline__ void probe(const TerrainView<ZT> &T, double x, double y, Probe<ZT> &p) {
-  p.ix = bracket_ax<CM, 0>(T, x);
-  p.iy = bracket_ax<CM, 1>(T, y);
-  const int cx = p.ix < 0 ? 0 : p.ix, cy = p.iy < 0 ? 0 : p.iy;
-  fetch_cell(T, cx, cy, p.q);
+  p.ix = bracket_ax<CM, 0, ONE>(T, x, p.cx);
+  p.iy = bracket_ax<CM, 1, ONE>(T, y, p.cy);
+  fetch_cell(T, p.cx, p.cy, p.q);
 }
 
 // heightIsNan on a probe: -1 = UB (BR_HIGH), else the reference's bool
@@ -451,10 +480,9 @@ __device__ __forceinline__ double probe_height_bf(const TerrainView<ZT> &T, cons
                                                   double x, double y, double eps, bool &ok,
                                                   bool &near) {
   const bool nanxy = isnan(x) || isnan(y);
-  const bool br = p.ix >= 0 && p.iy >= 0;
-  const int cx = br ? p.ix : 0, cy = br ? p.iy : 0;
-  const double x1 = coord<CM, 0>(T, cx), x2 = coord<CM, 0>(T, cx + 1);
-  const double y1 = coord<CM, 1>(T, cy), y2 = coord<CM, 1>(T, cy + 1);
+  const bool br = p.ix >= 0 && p.iy >= 0;  // else the value below is not used
+  const double x1 = coord<CM, 0>(T, p.cx), x2 = coord<CM, 0>(T, p.cx + 1);
+  const double y1 = coord<CM, 1>(T, p.cy), y2 = coord<CM, 1>(T, p.cy + 1);
   ok = br || nanxy;
   near = br && !nanxy &&
          (fabs(x - x1) < eps || fabs(x2 - x) < eps || fabs(y - y1) < eps || fabs(y2 - y) < eps);
@@ -471,7 +499,7 @@ __device__ __forceinline__ double probe_height_bf(const TerrainView<ZT> &T, cons
 // anyway and pays the exec-mask bookkeeping on top; here the wave issues one
 // path.  Same values, same decisions, same G/V and flags as the reference's
 // executed calls.
-template <class ZT, int CM = 0>
+template <class ZT, int CM = 0, bool ONE = false>
 __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int phase, Acc &acc) {
   if (acc.V >= GBP_MAX_SAMPLES) {  // engine guard: the reference loop would not terminate
     acc.flags |= GBP_F_LIMIT;
@@ -480,7 +508,7 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
   acc.V++;
   const double eps = FRAGILE_EPS, hmin = H_MIN, hmax = H_MAX, hl = 0.5 * ROBOT_L, hw = 0.5 * ROBOT_W;
   Probe<ZT> pc;
-  probe<ZT, CM>(T, s[0], s[1], pc);
+  probe<ZT, CM, ONE>(T, s[0], s[1], pc);
   const bool outside = (s[0] < T.x0) || (s[0] > T.xN) || (s[1] < T.y0) || (s[1] > T.yN);
   const double speed = sqrt(s[3] * s[3] + s[4] * s[4]);
   uint32_t fl = 0;
@@ -512,11 +540,11 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
     const double y_body = (k & 1) ? hw : -hw;
     const double x_leg = s[0] + R_11 * x_body + R_12 * y_body;
     const double y_leg = s[1] + R_21 * x_body + R_22 * y_body;
-    probe<ZT, CM>(T, x_leg, y_leg, pl[k]);
-    probe<ZT, CM>(T, x_leg + R_13 * z_body, y_leg + R_23 * z_body, pk[k]);
+    probe<ZT, CM, ONE>(T, x_leg, y_leg, pl[k]);
+    probe<ZT, CM, ONE>(T, x_leg + R_13 * z_body, y_leg + R_23 * z_body, pk[k]);
   }
   const double ux = s[0] + R_13 * z_body, uy = s[1] + R_23 * z_body;
-  probe<ZT, CM>(T, ux, uy, pu);
+  probe<ZT, CM, ONE>(T, ux, uy, pu);
   uint32_t G = 0;
   // (5) four corners :601-627, x_body outer, y_body inner, in reference order
 #pragma unroll

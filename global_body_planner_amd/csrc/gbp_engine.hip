@@ -174,6 +174,7 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
   double *const SA = gbp_smem + (CM == 1 ? (T0.nx + T0.ny + 1) & ~1 : 0);  // attempt rows
   double *const wave_rows = SA + (size_t)(threadIdx.x & ~(WAVE - 1)) * SA_ROW;
+  const bool one = T0.one_x && T0.one_y;  // wave-uniform: straight-line brackets
   Lane L;
   L.s = SA + (size_t)threadIdx.x * SA_ROW;
   L.a = L.s + 8;
@@ -257,7 +258,8 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
     if (has) {
       double sc[8];
       sample_state(ps, ps + 8, st, t_eval, sc);
-      ok = is_valid_state<ZT, CM>(T, sc, stage_phase(st), acc_s);
+      ok = one ? is_valid_state<ZT, CM, true>(T, sc, stage_phase(st), acc_s)
+               : is_valid_state<ZT, CM, false>(T, sc, stage_phase(st), acc_s);
     }
     bool decided = false;
     if (owner) {  // the lane's own sample
