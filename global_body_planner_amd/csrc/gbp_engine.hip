@@ -635,8 +635,9 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
       hipLaunchKernelGGL((k_validate_direct<ZT, AD, 1, CM == 2 ? 0 : CM>), dim3(g), dim3(db), coords, st, T, m,
                          s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn, flags + off, c);
     } else {
-      // persistent: one workgroup per resident slot (W waves per SIMD)
-      const int64_t resident = (int64_t)t->num_cus * std::max<int64_t>(1, W * 256 / block);
+      // persistent: one workgroup per resident slot (opt_waves waves per SIMD;
+      // W, the register budget, allows at least that many)
+      const int64_t resident = (int64_t)t->num_cus * std::max<int64_t>(1, t->opt_waves * 256 / block);
       const int64_t g = std::max<int64_t>(1, std::min<int64_t>(resident, (m + block - 1) / block));
       hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, CM>), dim3((unsigned)g), dim3(block),
                          coords + rows, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,

@@ -10,13 +10,13 @@
 //   stage 0  k_targets          B draws of PlannerClass::randomState
 //                               (planner_class.cpp:38-76) + isValidState(STANCE)
 //   stage 1  k_compact_targets  the valid targets, in draw order
-//   stage 2  k_nn_partial/k_nn_reduce   getNearestNeighbor in T (planner_class.cpp:185-200)
+//   stage 2  k_nn_filter/k_nn_reduce   getNearestNeighbor in T (planner_class.cpp:185-200)
 //            k_extend_prep      newConfig's 6 candidate actions (rrt.cpp:25-50)
 //            k_validate_persistent (gbp_engine.hip)  the candidates' pair checks
 //            k_select           newConfig's first valid candidate + acceptance (rrt.cpp:52-68)
 //   stage 3  k_append          non-TRAPPED successors appended to T in target order
 //                               (rrt.cpp:86-92; graph_class.cpp:28-42)
-//   stage 4  k_nn_partial/k_nn_reduce   the new vertices' nearest vertex in O
+//   stage 4  k_nn_filter/k_nn_reduce   the new vertices' nearest vertex in O
 //            k_connect          RRTConnectClass::attemptConnect (rrt_connect.cpp:20-91),
 //                               one wave per connection, the wave's 64 lanes
 //                               evaluating the pair check's samples together
@@ -44,6 +44,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "gbp.h"
@@ -60,6 +61,8 @@ struct gbp_tree {
   int device = 0;
   int64_t cap = 0;
   double *v = nullptr;        // [cap][8] vertex states (GraphClass vertices)
+  float *vf = nullptr;        // [cap][8] the same rounded to fp32 (nearest-neighbour filter)
+  float *vmax = nullptr;      // [8] max |vf[j][k]| over the vertices (NaN skipped)
   double *a = nullptr;        // [cap][10] the action that reached each vertex
   double *g = nullptr;        // [cap] cost to come: g[parent] + poseDistance
   int32_t *parent = nullptr;  // [cap], -1 at the root
@@ -242,17 +245,45 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
 // ============================================================================
 // nearest neighbour in a device tree (planner_class.cpp:185-200)
 // ============================================================================
-// Work item (query tile qt, vertex chunk c): NN_QPL x 256 queries,
-// against the chunk's vertices.  The vertex index is wave-uniform, so each
-// vertex's eight doubles arrive by one scalar load (s_load_dwordx16) and feed
-// the VALU as SGPR operands: no LDS traffic, no per-lane address arithmetic;
-// every vertex load serves 64 x NN_QPL distance evaluations.  Best (distance,
-// index) per query and chunk go to the partial arrays; the chunk size is set
-// from the tree size on the device so a tile never needs more than
-// NN_MAX_CHUNKS of them.  stateDistance's sqrt is taken only when the squared
-// sum improves: sqrt is monotone, so sum >= best_sum can never give a
-// strictly smaller distance, and equal square roots keep the earlier vertex
-// (the reference's strict <).
+// Work item (query tile qt, vertex chunk c): 256 queries (one per lane)
+// against the chunk's vertices; best (distance, index) per query and chunk go
+// to the partial arrays (the chunk size is set from the tree size on the
+// device so a tile never needs more than NN_MAX_CHUNKS of them).
+//
+// The exact answer (stateDistance in fp64, planning_utils.cpp:116-127, the
+// lowest index among equal distances) is found through an fp32 filter:
+//   pass 1  B = min_j S_j over the chunk, S_j = |fl32(v_j) - fl32(q)|^2 in
+//           fp32 (packed FMAs; the tree's vf mirror, rows by scalar loads:
+//           wave-uniform row, SGPR operands);
+//   pass 2  the same S_j again; j is recorded as a candidate iff S_j <= T(B)
+//           (tested once per block of rows on the wave's ballot: with the
+//           final minimum the threshold is tight, so almost no block holds
+//           a candidate in any lane);
+//   exact   stateDistance in fp64 for the candidates; the smallest
+//           (distance, index) pair wins, which is the reference's ascending
+//           scan with strict < (the first index reaching the minimum).
+// T(B) = ((1 + 2^-19) sqrt(B) + 2.5 E)^2 (1 + 2^-20) with E^2 =
+// sum_k (2^-22 (M_k + |q_k|))^2 and M_k >= max |v_jk| over the tree (kept by
+// the appends, gbp_tree.vmax).  Why no minimiser is lost: each fp32
+// difference is within 2.01 u (|v_k| + |q_k|) of v_k - q_k (u = 2^-24: two
+// input roundings and the subtraction), so the fp32 vector's length is within
+// E/2 of the true distance D_j; the FMA sum of the 8 squares is within a
+// relative gamma_8 < 4.8e-7; a minimiser j* of the fp64 distance has
+// D_j* <= D_i (1 + 3e-15) for every i.  Hence
+// sqrt(S_j*) <= sqrt((1+g)/(1-g)) (1 + 3e-15) sqrt(B) + 1.01 E sqrt(1+g)
+// < T(B)^(1/2): j* is recorded, and so is every index tying with it.  The
+// bound assumes |v|, |q| < 1e15 (no fp32 overflow of the squares); a wave
+// with a query or tree outside that, or with more than NN_CAND candidates in
+// a lane, scans the chunk in fp64 instead (ascending, strict <).
+// Measured alternatives (profiles/r02h_nn_filter.txt): one pass with a running
+// threshold (a branch per row: slower, and insertion-order trends make the
+// running minimum fall slowly), bit-reversed visiting orders (scattered
+// scalar loads), double-buffered scalar loads, two queries per lane, rows
+// staged in LDS (every broadcast row read still moves 64 x 32 B through the
+// LDS port) or fed through v_readlane: all between 1.0x and 1.9x slower.
+constexpr int NN_CAND = 16;
+
+typedef float nnf2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int64_t nn_chunk(int64_t nv) {
   int64_t c = (nv + NN_MAX_CHUNKS - 1) / NN_MAX_CHUNKS;
@@ -260,74 +291,178 @@ __device__ __forceinline__ int64_t nn_chunk(int64_t nv) {
   return c < 256 ? 256 : c;
 }
 
-template <int NN_QPL, int UNR>
-__global__ __launch_bounds__(TB) void k_nn_partial(const gbp_plan_status *__restrict__ st,
-                                                   const int32_t *__restrict__ nq_dev,
-                                                   const double *__restrict__ q,
-                                                   const int32_t *__restrict__ q_off_dev,
-                                                   const double *__restrict__ v,
-                                                   const int32_t *__restrict__ nv_dev, int64_t bmax,
-                                                   double *__restrict__ pd,
-                                                   int32_t *__restrict__ pi) {
+// stateDistance(q, vertex j) exactly as the reference evaluates it
+__device__ __forceinline__ double nn_dist64(const double qq[8], const double *vj) {
+  double sum = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const double d = vj[k] - qq[k];
+    sum = sum + 1.0 * d * d;  // planning_utils.cpp:116-127
+  }
+  return sqrt(sum);
+}
+
+// the fp64 scan of vertices [j0, j1), ascending, strict < (getNearestNeighbor);
+// rows by scalar loads, UNR in flight (full blocks carry no bounds test, so
+// the compiler cannot sink a row's load under one)
+template <int UNR>
+__device__ __forceinline__ void nn_scan64(const double qq[8], const double *__restrict__ v, int j0,
+                                          int j1, double &best, int &bi) {
+  auto body = [&](int jb, int m) {
+    double vv[UNR][8];
+#pragma unroll
+    for (int r = 0; r < UNR; r++) {
+      if (r >= m) break;
+      const double *vj = v + 8 * (int64_t)__builtin_amdgcn_readfirstlane(jb + r);
+#pragma unroll
+      for (int k = 0; k < 8; k++) vv[r][k] = vj[k];
+    }
+#pragma unroll
+    for (int r = 0; r < UNR; r++) {
+      if (r >= m) break;
+      const double d = nn_dist64(qq, vv[r]);
+      if (d < best) {
+        best = d;
+        bi = jb + r;
+      }
+    }
+  };
+  int jb = j0;
+  for (; jb + UNR <= j1; jb += UNR) body(jb, UNR);
+  for (; jb < j1; jb++) body(jb, 1);
+}
+
+__device__ __forceinline__ float nn_threshold(float B, double b) {
+  const double tb = (1.0 + 0x1p-19) * sqrt((double)B) + b;
+  return (float)(tb * tb * (1.0 + 0x1p-20));
+}
+
+// UNR consecutive rows [jb, jb + UNR) by one contiguous scalar load
+template <int UNR>
+__device__ __forceinline__ void nn_load_rows(const float *__restrict__ vf, int jb,
+                                             float (&rv)[UNR][8]) {
+  const float *vj = vf + 8 * (int64_t)__builtin_amdgcn_readfirstlane(jb);
+#pragma unroll
+  for (int r = 0; r < UNR; r++)
+#pragma unroll
+    for (int c = 0; c < 8; c++) rv[r][c] = vj[8 * r + c];
+}
+
+__device__ __forceinline__ float nn_s32(const nnf2 (&qf)[4], const float (&rv)[8]) {
+  nnf2 acc = {0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const nnf2 vk = {rv[2 * c], rv[2 * c + 1]};
+    const nnf2 d = vk - qf[c];
+    acc = __builtin_elementwise_fma(d, d, acc);
+  }
+  return acc.x + acc.y;
+}
+
+// Rows [j0, j1) in blocks of UNR (the tail row by row).  MODE 0: B = min S
+// (selects, no branch); MODE 1: record the rows with S <= T, tested once per
+// block on the wave's ballot (the threshold is tight, so a block almost
+// never holds a candidate in any lane).
+template <int UNR, int MODE>
+__device__ __forceinline__ void nn_sweep(const nnf2 (&qf)[4], const float *__restrict__ vf, int j0,
+                                         int j1, float &B, float T, int &cnt,
+                                         int32_t (*cand)[TB]) {
+  auto block = [&](int jb, auto m_tag) {
+    constexpr int M = decltype(m_tag)::value;
+    float rv[M][8];
+    nn_load_rows<M>(vf, jb, rv);
+    float S[M];
+#pragma unroll
+    for (int r = 0; r < M; r++) S[r] = nn_s32(qf, rv[r]);
+    if (MODE == 0) {
+#pragma unroll
+      for (int r = 0; r < M; r++) B = S[r] < B ? S[r] : B;
+    } else {
+      bool hit = false;
+#pragma unroll
+      for (int r = 0; r < M; r++) hit = hit || S[r] <= T;
+      if (__ballot(hit)) {
+#pragma unroll
+        for (int r = 0; r < M; r++)
+          if (S[r] <= T) {
+            if (cnt < NN_CAND) cand[cnt][threadIdx.x] = jb + r;
+            cnt++;
+          }
+      }
+    }
+  };
+  int jb = j0;
+  for (; jb + UNR <= j1; jb += UNR) block(jb, std::integral_constant<int, UNR>{});
+  for (; jb < j1; jb++) block(jb, std::integral_constant<int, 1>{});
+}
+
+template <int UNR>
+__global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restrict__ st,
+                                                  const int32_t *__restrict__ nq_dev,
+                                                  const double *__restrict__ q,
+                                                  const int32_t *__restrict__ q_off_dev,
+                                                  const double *__restrict__ v,
+                                                  const float *__restrict__ vf,
+                                                  const float *__restrict__ vmax,
+                                                  const int32_t *__restrict__ nv_dev, int64_t bmax,
+                                                  double *__restrict__ pd,
+                                                  int32_t *__restrict__ pi) {
   if (gated(st)) return;
+  __shared__ int32_t cand[NN_CAND][TB];
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   const int64_t ch = nn_chunk(nv);
-  const int64_t qtile = (int64_t)NN_QPL * TB;
-  const int64_t nch = (nv + ch - 1) / ch, nqt = (nq + qtile - 1) / qtile;
+  const int64_t nch = (nv + ch - 1) / ch, nqt = (nq + TB - 1) / TB;
+  double mk[8];
+  bool tree_bad = false;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    mk[k] = (double)vmax[k] * (1.0 + 0x1p-20);
+    tree_bad = tree_bad || !(mk[k] < 1e15);
+  }
   for (int64_t item = blockIdx.x; item < nqt * nch; item += gridDim.x) {
     const int64_t qt = item / nch, c = item - qt * nch;
-    double qq[NN_QPL][8], best[NN_QPL], best_sum[NN_QPL];
-    int bi[NN_QPL];
-    int64_t qi[NN_QPL];
-#pragma unroll
-    for (int u = 0; u < NN_QPL; u++) {
-      qi[u] = qt * qtile + u * TB + threadIdx.x;
-      const bool live = qi[u] < nq;
-#pragma unroll
-      for (int k = 0; k < 8; k++) qq[u][k] = live ? q[8 * (q_off + qi[u]) + k] : 0.0;
-      best[u] = INFINITY;
-      best_sum[u] = INFINITY;
-      bi[u] = -1;
-    }
     const int j0 = (int)(c * ch), j1 = (int)min(nv, (c + 1) * ch);
-    for (int jb = j0; jb < j1; jb += UNR) {
-      // UNR vertices' scalar loads issued together, then their distances
-      double vv[UNR][8];
+    const int64_t qi = qt * TB + threadIdx.x;
+    const bool live = qi < nq;
+    double qq[8], e2 = 0.0;
+    bool bad = tree_bad;
 #pragma unroll
-      for (int r = 0; r < UNR; r++) {
-        const int j = min(jb + r, j1 - 1);  // a clamped duplicate is skipped below
-        const double *vj = v + 8 * (int64_t)__builtin_amdgcn_readfirstlane(j);
+    for (int k = 0; k < 8; k++) {
+      qq[k] = live ? q[8 * (q_off + qi) + k] : 0.0;
+      const double ak = fabs(qq[k]);
+      const double dk = 0x1p-22 * (mk[k] + ak);
+      e2 = e2 + dk * dk;
+      bad = bad || (live && !(ak < 1e15));
+    }
+    double best = INFINITY;
+    int bi = -1;
+    bool scan64 = __ballot(bad) != 0ull;
+    if (!scan64) {
+      nnf2 qf[4];
 #pragma unroll
-        for (int k = 0; k < 8; k++) vv[r][k] = vj[k];
-      }
-#pragma unroll
-      for (int r = 0; r < UNR; r++) {
-        if (jb + r >= j1) break;
-#pragma unroll
-        for (int u = 0; u < NN_QPL; u++) {
-          double sum = 0;
-#pragma unroll
-          for (int k = 0; k < 8; k++) {
-            const double d = vv[r][k] - qq[u][k];
-            sum = sum + 1.0 * d * d;  // stateDistance(q, vertex), planning_utils.cpp:116-127
-          }
-          if (sum < best_sum[u]) {
-            const double dist = sqrt(sum);
-            if (dist < best[u]) {
-              best[u] = dist;
-              best_sum[u] = sum;
-              bi[u] = jb + r;
-            }
+      for (int k = 0; k < 4; k++) qf[k] = nnf2{(float)qq[2 * k], (float)qq[2 * k + 1]};
+      float B = INFINITY;
+      int cnt = 0;
+      nn_sweep<UNR, 0>(qf, vf, j0, j1, B, 0.f, cnt, cand);
+      const float T = live ? nn_threshold(B, 2.5 * sqrt(e2) + 1e-30) : -1.0f;
+      nn_sweep<UNR, 1>(qf, vf, j0, j1, B, T, cnt, cand);
+      scan64 = __ballot(cnt > NN_CAND) != 0ull;
+      if (!scan64) {
+        for (int m = 0; m < cnt; m++) {
+          const int j = cand[m][threadIdx.x];
+          const double d = nn_dist64(qq, v + 8 * (int64_t)j);
+          if (d < best || (d == best && j < bi)) {
+            best = d;
+            bi = j;
           }
         }
       }
     }
-#pragma unroll
-    for (int u = 0; u < NN_QPL; u++)
-      if (qi[u] < nq) {
-        pd[c * bmax + qi[u]] = best[u];
-        pi[c * bmax + qi[u]] = bi[u];
-      }
+    if (scan64) nn_scan64<4>(qq, v, j0, j1, best, bi);
+    if (live) {
+      pd[c * bmax + qi] = best;
+      pi[c * bmax + qi] = bi;
+    }
   }
 }
 
@@ -452,11 +587,18 @@ __global__ __launch_bounds__(TB) void k_select(gbp_plan_status *st, const double
 // mode 0: extend successors of the current targets into T (parent = nn[i]);
 // mode 1: connections of the new vertices into O (parent = nno[k]), the first
 // REACHED one in order recorded as the meeting point.
+// running max |x| over a tree's fp32 rows (non-negative floats order as their
+// bit patterns; NaN is skipped: it never passes a distance comparison)
+__device__ __forceinline__ void vmax_update(float *m, float x) {
+  if (!isnan(x)) atomicMax((unsigned int *)m, __float_as_uint(fabsf(x)));
+}
+
 __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
                                                const int32_t *__restrict__ res,
                                                const int32_t *__restrict__ par,
                                                const double *__restrict__ sn,
                                                const double *__restrict__ an, double *__restrict__ tv,
+                                               float *__restrict__ tvf, float *__restrict__ tvmax,
                                                double *__restrict__ ta, double *__restrict__ tg,
                                                int32_t *__restrict__ tp, int32_t *__restrict__ tcount,
                                                int32_t *__restrict__ vtx, unsigned long long *tiles,
@@ -479,6 +621,12 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
     copy8(s, sn + 8 * i);
     copy8(pv, tv + 8 * (int64_t)p);
     copy8(tv + 8 * (int64_t)idx, s);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const float f = (float)s[k];
+      tvf[8 * (int64_t)idx + k] = f;
+      vmax_update(tvmax + k, f);
+    }
     copy10(ta + 10 * (int64_t)idx, an + 10 * i);
     tp[idx] = p;
     tg[idx] = tg[p] + pose_distance(pv, s);  // graph_class.cpp:36-42 addEdge
@@ -670,6 +818,10 @@ __global__ void k_tree_init(gbp_tree t, double r0, double r1, double r2, double 
                             double r5, double r6, double r7) {
   const double r[8] = {r0, r1, r2, r3, r4, r5, r6, r7};
   copy8(t.v, r);
+  for (int k = 0; k < 8; k++) {
+    t.vf[k] = (float)r[k];
+    t.vmax[k] = isnan(t.vf[k]) ? 0.f : fabsf(t.vf[k]);
+  }
   for (int k = 0; k < 10; k++) t.a[k] = 0.0;
   t.g[0] = 0.0;
   t.parent[0] = -1;
@@ -683,6 +835,10 @@ __global__ void k_tree_append(gbp_tree t, int64_t n, const double *__restrict__ 
   int32_t c = *t.count;
   for (int64_t i = 0; i < n; i++, c++) {
     copy8(t.v + 8 * (int64_t)c, s + 8 * i);
+    for (int k = 0; k < 8; k++) {
+      t.vf[8 * (int64_t)c + k] = (float)s[8 * i + k];
+      vmax_update(t.vmax + k, t.vf[8 * (int64_t)c + k]);
+    }
     copy10(t.a + 10 * (int64_t)c, a + 10 * i);
     t.parent[c] = p[i];
     t.g[c] = p[i] >= 0 ? t.g[p[i]] + pose_distance(t.v + 8 * (int64_t)p[i], s + 8 * i) : 0.0;
@@ -751,13 +907,11 @@ unsigned tiles_for(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + CB - 
 
 int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
               const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s) {
-  // one query per lane, four vertices' scalar loads in flight, 4 workgroups
-  // per CU: the fastest of {1, 2, 4} queries per lane x {1, 2, 4} vertices x
-  // {2, 4} workgroups per CU (tools/nn_micro.py, profiles/r02_nn_variants.jsonl):
-  // 0.82 T pairs/s at 20k queries x 20k vertices, 7.6x the one-workgroup-per-
-  // query / LDS-tile gbp_nearest_batch_dev
-  hipLaunchKernelGGL((k_nn_partial<1, 4>), dim3(num_cus * 4), dim3(TB), 0, s, w->st, nq_dev, q,
-                     q_off_dev, tr->v, tr->count, w->bmax, w->nn_d, w->nn_i);
+  // one query per lane, four rows per scalar load, 8 workgroups per CU: the
+  // fastest of {2, 4, 8} rows x {4, 8} workgroups per CU, and 1.4x the fp64
+  // scan it replaces (tools/nn_sweep.sh, profiles/r02h_nn_filter.txt)
+  hipLaunchKernelGGL((k_nn_filter<4>), dim3(num_cus * 8), dim3(TB), 0, s, w->st, nq_dev, q,
+                     q_off_dev, tr->v, tr->vf, tr->vmax, tr->count, w->bmax, w->nn_d, w->nn_i);
   hipLaunchKernelGGL(k_nn_reduce, dim3(grid_for(w->bmax, TB, num_cus * 4)), dim3(TB), 0, s, w->st,
                      nq_dev, tr->count, w->bmax, w->nn_d, w->nn_i, out);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
@@ -792,7 +946,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   }
   if (first_stage <= 3 && last_stage >= 3)
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 0, w->eres, w->nn,
-                       w->esn, w->ean, T->v, T->a, T->g, T->parent, T->count, w->evtx, w->tiles,
+                       w->esn, w->ean, T->v, T->vf, T->vmax, T->a, T->g, T->parent, T->count, w->evtx, w->tiles,
                        next_epoch(w), half);
   if (!O) return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   const int cdir = direction == GBP_FORWARD ? GBP_REVERSE : GBP_FORWARD;
@@ -814,7 +968,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   }
   if (first_stage <= 5 && last_stage >= 5)
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 1, w->kres, w->nno,
-                       w->ksn, w->kan, O->v, O->a, O->g, O->parent, O->count, nullptr, w->tiles,
+                       w->ksn, w->kan, O->v, O->vf, O->vmax, O->a, O->g, O->parent, O->count, nullptr, w->tiles,
                        next_epoch(w), half);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
@@ -847,16 +1001,19 @@ T *carve(char *&p, size_t count) {
 
 int tree_alloc(gbp_tree *t, int64_t cap) {
   double *v = nullptr, *a = nullptr, *g = nullptr;
+  float *vf = nullptr;
   int32_t *p = nullptr;
   if (hipMalloc(&v, 64 * cap) != hipSuccess) return GBP_E_ALLOC;
   if (hipMalloc(&a, 80 * cap) != hipSuccess || hipMalloc(&g, 8 * cap) != hipSuccess ||
-      hipMalloc(&p, 4 * cap) != hipSuccess) {
+      hipMalloc(&p, 4 * cap) != hipSuccess || hipMalloc(&vf, 32 * cap) != hipSuccess) {
     (void)hipFree(v);
     if (a) (void)hipFree(a);
     if (g) (void)hipFree(g);
+    if (p) (void)hipFree(p);
     return GBP_E_ALLOC;
   }
   t->v = v;
+  t->vf = vf;
   t->a = a;
   t->g = g;
   t->parent = p;
@@ -903,11 +1060,12 @@ int gbp_tree_create(int device, int64_t capacity, gbp_tree **out) {
   gbp_tree *t = new (std::nothrow) gbp_tree();
   if (!t) return GBP_E_ALLOC;
   t->device = device;
-  if (hipMalloc(&t->count, 4) != hipSuccess || tree_alloc(t, capacity) != GBP_OK) {
+  if (hipMalloc(&t->count, 4) != hipSuccess || hipMalloc(&t->vmax, 32) != hipSuccess ||
+      tree_alloc(t, capacity) != GBP_OK) {
     gbp_tree_destroy(t);
     return GBP_E_ALLOC;
   }
-  if (hipMemset(t->count, 0, 4) != hipSuccess) {
+  if (hipMemset(t->count, 0, 4) != hipSuccess || hipMemset(t->vmax, 0, 32) != hipSuccess) {
     gbp_tree_destroy(t);
     return GBP_E_HIP;
   }
@@ -919,7 +1077,7 @@ int gbp_tree_destroy(gbp_tree *t) {
   if (!t) return GBP_E_BAD_HANDLE;
   Guard g(t->device);
   (void)hipDeviceSynchronize();
-  void *ptrs[] = {t->v, t->a, t->g, t->parent, t->count};
+  void *ptrs[] = {t->v, t->vf, t->a, t->g, t->parent, t->count, t->vmax};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   delete t;
@@ -940,11 +1098,13 @@ int gbp_tree_reserve(gbp_tree *t, int64_t capacity, gbp_stream stream) {
     return rc;
   }
   HIPCHK_P(hipMemcpyAsync(t->v, old.v, 64 * old.cap, hipMemcpyDeviceToDevice, s));
+  HIPCHK_P(hipMemcpyAsync(t->vf, old.vf, 32 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->a, old.a, 80 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->g, old.g, 8 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->parent, old.parent, 4 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipStreamSynchronize(s));
   (void)hipFree(old.v);
+  (void)hipFree(old.vf);
   (void)hipFree(old.a);
   (void)hipFree(old.g);
   (void)hipFree(old.parent);

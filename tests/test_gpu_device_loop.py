@@ -120,3 +120,52 @@ def test_device_tree_api(gpu):
         assert G[i] == G[P[i]] + oracle.pose_distance(S[P[i]], S[i])
     with pytest.raises(L.GbpError):
         t.append(s[:1], a[:1], np.array([99], np.int32))  # parent out of range
+
+
+def test_tree_nearest_fp32_filter_exact(gpu):
+    """gbp_tree_nearest_dev (k_nn_filter: fp32 filter, fp64 re-check of the
+    candidates) returns exactly the fp64 scan's index (gbp_nearest_batch_dev,
+    planner_class.cpp:185-200: lowest index among equal distances) on random
+    states and on the cases that stress the filter: exact duplicates (ties),
+    vertices that are equal in fp32 but distinct in fp64 (more than NN_CAND of
+    them in one chunk: the overflow scan), magnitudes past the filter's bound
+    (the fp64 scan) and NaN queries (index 0)."""
+    import global_body_planner_amd as gbp
+    data = td.synth_rough(256)
+    T = gbp.Terrain.from_data(data, device=0)
+    rng = np.random.default_rng(5)
+    nq = 4096
+    ws = gbp.PlanWorkspace(T, nq)
+
+    def check(verts, q, label):
+        tree = gbp.DeviceTree(verts[0], device=0, capacity=verts.shape[0] + 1)
+        tree.append(verts[1:], np.zeros((verts.shape[0] - 1, 10)),
+                    np.zeros(verts.shape[0] - 1, np.int32))
+        qt = torch.from_numpy(np.ascontiguousarray(q)).cuda()
+        got = ws.nearest(tree, qt).cpu().numpy()
+        ref, _ = gbp.nearest(qt, torch.from_numpy(verts).cuda())
+        ref = ref.cpu().numpy()
+        bad = np.flatnonzero(got != ref)
+        assert bad.size == 0, (label, bad[:5], got[bad[:5]], ref[bad[:5]])
+
+    # random states, a tree spanning many chunks
+    verts = T.sample_states(20000, seed=41, stream_id=1)[0].cpu().numpy()
+    q = T.sample_states(nq, seed=42, stream_id=2)[0].cpu().numpy()
+    check(verts, q, "random")
+    # clusters: 64 centres, 300 vertices each within 1e-9 (fp32-identical),
+    # exact duplicates among them; queries at and near the centres
+    base = verts[:64]
+    cl = np.repeat(base, 300, axis=0) + rng.normal(scale=1e-9, size=(64 * 300, 8))
+    cl[::7] = np.repeat(base, 300, axis=0)[::7]          # exact copies of a centre
+    perm = rng.permutation(cl.shape[0])
+    cl = np.ascontiguousarray(cl[perm])
+    qc = np.repeat(base, nq // 64, axis=0) + rng.normal(scale=1e-10, size=(nq, 8))
+    qc[::3] = np.repeat(base, nq // 64, axis=0)[::3]
+    check(cl, qc, "clusters")
+    # magnitudes beyond the fp32 bound, and NaN queries
+    big = verts.copy()
+    big[::1000, 2] = 3e16
+    qn = q.copy()
+    qn[::97, 4] = np.nan
+    qn[5::101, 0] = 2e16
+    check(big, qn, "big/nan")
