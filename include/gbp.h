@@ -330,7 +330,9 @@ int gbp_tree_append_host(gbp_tree *tree, int64_t n, const double *states, const 
  * (n <= its max_batch). */
 int gbp_tree_nearest_dev(gbp_plan_ws *ws, gbp_tree *tree, int64_t n, const double *queries,
                          int32_t *index, gbp_stream stream);
-/* the tree's device arrays (for gbp_nearest_batch_dev and the like) */
+/* the tree's device arrays (for gbp_nearest_batch_dev and the like): READ ONLY —
+ * vertices are written through init / append only, which also keep the fp32
+ * mirror and magnitude bound the nearest-neighbour filter relies on */
 int gbp_tree_device_ptrs(gbp_tree *tree, double **states, int32_t **count);
 
 /* ---- the device planner loop (RRTConnectClass::runRRTConnect,
