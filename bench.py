@@ -391,6 +391,9 @@ def main():
     # per-launch algorithmic bytes from the kernel's own G/V counters
     c = res.counts.to(torch.int64) & 0xFFFFFFFF
     gv = int(((c & 0xFFFF) + (c >> 16)).sum().item())
+    # the kernel fetches all ten probes of every evaluated sample (straight-line
+    # isValidState): 10 V probes issued by the charged samples, beside G + V
+    probes = 10 * int((c >> 16).sum().item())
     n_valid = int(res.valid.to(torch.int64).sum().item())
     flags = res.flags.to(torch.int64) & 0xFFFFFFFF
     n_ood = int(((flags & L.F_OOD) != 0).sum().item())
@@ -414,7 +417,7 @@ def main():
                                "distribution (no input reuse between consecutive launches)"}
         del batches
 
-    elapsed, sums = sharding.reduce_run(elapsed, [B, n_valid, n_ood, n_frag, gv], dev)
+    elapsed, sums = sharding.reduce_run(elapsed, [B, n_valid, n_ood, n_frag, gv, probes], dev)
     sums = torch.tensor(sums, dtype=torch.float64)
     tot_attempts = float(sums[0].item()) * args.steps
     value = tot_attempts / elapsed
@@ -469,6 +472,7 @@ def main():
             "ood_fraction": float(sums[2].item()) / float(sums[0].item()),
             "fragile": int(sums[3].item()),
             "lookups_per_attempt": float(sums[4].item()) / float(sums[0].item()),
+            "probes_issued_per_attempt": float(sums[5].item()) / float(sums[0].item()),
             "kernel_ms_per_launch": round(kern_ms, 4),
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
