@@ -221,3 +221,39 @@ def test_node_entry_point_config1(gpu, tmp_path):
         assert len(runs) == len(seeds) and all(x["ok"] == 1 for x in runs)
         for x in runs:
             print("node_config1", json.dumps(x))
+
+
+def test_long_straight_connect_and_sample_cap(gpu):
+    """A connect longer than round 1's 4096-sample guard (about 153 m at V_NOM)
+    on a flat 300 m map: t_s = 229 / V_NOM = 305 s, ~6,100 stance samples, below
+    GBP_MAX_SAMPLES = 7000, so the engine finishes the loop as the reference
+    would (rrt_connect.cpp:20-91) and agrees with the oracle; a pair with
+    t_s = inf (the reference never terminates) stops at the cap with
+    GBP_F_LIMIT and is reported invalid."""
+    import torch
+    import global_body_planner_amd as gbp
+    from global_body_planner_amd import _lib as L
+    from tests.helpers import same_f64
+    x = np.arange(3001) * 0.1
+    y = np.arange(41) * 0.1
+    data = td.TerrainData(x=x, y=y, z=np.zeros((x.size, y.size)), name="flat-300m")
+    T = gbp.Terrain.from_data(data, device=0)
+    O = oracle.OracleTerrain.from_data(data)
+    start = planner.start_goal_state(0.0, 1.0, 2.0)
+    goal = planner.start_goal_state(0.0, 230.0, 2.0)
+    for direction in (0, 1):
+        a, b = (start, goal) if direction == 0 else (goal, start)
+        r, sn, an = planner.attempt_connect(T, a[None, :], b[None, :], direction)
+        ro, sno, ano = O.attempt_connect(a, b, direction)
+        assert r[0] == ro == 2, (direction, r[0], ro)          # REACHED
+        assert np.all(same_f64(sn[0], sno)) and np.all(same_f64(an[0], ano))
+        assert an[0][6] > 4096 * 0.05                          # past the old guard
+    st = start.copy()
+    st[3] = 0.0                       # at rest: the state stays valid at every sample
+    s = torch.tensor(st[None, :]).cuda()
+    act = torch.zeros((1, 10), dtype=torch.float64)
+    act[0, 6] = float("inf")          # zero accelerations, endless stance
+    res = T.validate_pairs(s, act.cuda(), torch.zeros(1, dtype=torch.uint8).cuda())
+    f = int(res.flags.cpu().numpy()[0]) & 0xFFFFFFFF
+    assert f & L.F_LIMIT and not (f & L.F_VALID)
+    assert (int(res.counts.cpu().numpy()[0]) & 0xFFFFFFFF) >> 16 == L.MAX_SAMPLES
