@@ -100,7 +100,7 @@ struct gbp_plan_ws {
   double *ksn = nullptr;       // [bmax][8]
   double *kan = nullptr;       // [bmax][10]
   uint32_t *kf = nullptr;      // [bmax] connect flags
-  // nearest-neighbour partials: [NN_MAX_CHUNKS][bmax]
+  // nearest-neighbour partials: NN_MAX_CHUNKS * bmax slots, pd[c * nq + qi]
   double *nn_d = nullptr;
   int32_t *nn_i = nullptr;
   void *block = nullptr;       // the one allocation all of the above live in
@@ -111,7 +111,7 @@ namespace {
 constexpr int WAVE = 64;
 constexpr int TB = 256;            // threads of the grid-stride kernels
 constexpr int CB = 1024;           // threads (items) per look-back tile
-constexpr int NN_MAX_CHUNKS = 32;  // vertex chunks per query tile
+constexpr int NN_MAX_CHUNKS = 32;  // partial slots per query at the largest batch
 constexpr uint32_t LOOKBACK_SPIN_LIMIT = 1u << 24;
 
 // the gate every planner kernel checks first: a FRAGILE halt or a found
@@ -247,8 +247,8 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
 // ============================================================================
 // Work item (query tile qt, vertex chunk c): 256 queries (one per lane)
 // against the chunk's vertices; best (distance, index) per query and chunk go
-// to the partial arrays (the chunk size is set from the tree size on the
-// device so a tile never needs more than NN_MAX_CHUNKS of them).
+// to the partial arrays (chunk size and count set on the device from the
+// query and tree sizes, nn_geometry).
 //
 // The exact answer (stateDistance in fp64, planning_utils.cpp:116-127, the
 // lowest index among equal distances) is found through an fp32 filter:
@@ -285,10 +285,21 @@ constexpr int NN_CAND = 16;
 
 typedef float nnf2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ int64_t nn_chunk(int64_t nv) {
-  int64_t c = (nv + NN_MAX_CHUNKS - 1) / NN_MAX_CHUNKS;
-  c = (c + 255) & ~(int64_t)255;
-  return c < 256 ? 256 : c;
+// Vertex chunk size and count for nq queries against nv vertices: enough
+// (query tile, chunk) items to occupy the GPU (~2048), chunks of at least 64
+// rows, and at most NN_MAX_CHUNKS * bmax partial slots (pd[c * nq + qi]).  A
+// handful of queries (the connect stage's new vertices) thus still spreads
+// over hundreds of chunks instead of scanning the tree serially.
+__device__ __forceinline__ void nn_geometry(int64_t nq, int64_t nv, int64_t bmax, int64_t &ch,
+                                            int64_t &nch) {
+  const int64_t nqt = nq > 0 ? (nq + TB - 1) / TB : 1;
+  const int64_t want = (2048 + nqt - 1) / nqt;
+  ch = (((nv + want - 1) / want) + 63) & ~(int64_t)63;
+  if (ch < 64) ch = 64;
+  const int64_t slots = (NN_MAX_CHUNKS * bmax) / (nq > 0 ? nq : 1);  // chunks per query
+  const int64_t ch_min = (nv + slots - 1) / slots;
+  if (ch < ch_min) ch = (ch_min + 63) & ~(int64_t)63;
+  nch = nv > 0 ? (nv + ch - 1) / ch : 1;
 }
 
 // stateDistance(q, vertex j) exactly as the reference evaluates it
@@ -410,8 +421,9 @@ __global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restr
   if (gated(st)) return;
   __shared__ int32_t cand[NN_CAND][TB];
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
-  const int64_t ch = nn_chunk(nv);
-  const int64_t nch = (nv + ch - 1) / ch, nqt = (nq + TB - 1) / TB;
+  int64_t ch, nch;
+  nn_geometry(nq, nv, bmax, ch, nch);
+  const int64_t nqt = (nq + TB - 1) / TB;
   double mk[8];
   bool tree_bad = false;
 #pragma unroll
@@ -424,6 +436,7 @@ __global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restr
     const int j0 = (int)(c * ch), j1 = (int)min(nv, (c + 1) * ch);
     const int64_t qi = qt * TB + threadIdx.x;
     const bool live = qi < nq;
+    if (!__ballot(live)) continue;  // a wave past the last query (no barriers here)
     double qq[8], e2 = 0.0;
     bool bad = tree_bad;
 #pragma unroll
@@ -460,8 +473,8 @@ __global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restr
     }
     if (scan64) nn_scan64<4>(qq, v, j0, j1, best, bi);
     if (live) {
-      pd[c * bmax + qi] = best;
-      pi[c * bmax + qi] = bi;
+      pd[c * nq + qi] = best;
+      pi[c * nq + qi] = bi;
     }
   }
 }
@@ -475,16 +488,17 @@ __global__ __launch_bounds__(TB) void k_nn_reduce(const gbp_plan_status *st, con
                                                   int32_t *__restrict__ out) {
   if (gated(st)) return;
   const int64_t nq = *nq_dev, nv = *nv_dev;
-  const int64_t ch = nn_chunk(nv), nch = (nv + ch - 1) / ch;
+  int64_t ch, nch;
+  nn_geometry(nq, nv, bmax, ch, nch);
   for (int64_t qi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; qi < nq;
        qi += (int64_t)gridDim.x * blockDim.x) {
     double best = INFINITY;
     int bi = 0;
     for (int64_t c = 0; c < nch; c++) {
-      const double d = pd[c * bmax + qi];
+      const double d = pd[c * nq + qi];
       if (d < best) {
         best = d;
-        bi = pi[c * bmax + qi];
+        bi = pi[c * nq + qi];
       }
     }
     out[qi] = bi;
