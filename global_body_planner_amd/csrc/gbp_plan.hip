@@ -480,7 +480,10 @@ __global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restr
 }
 
 // chunks in index order, strict <: the lowest index among equal distances;
-// nothing < inf (a NaN query): index 0, as the reference keeps it
+// nothing < inf (a NaN query): index 0, as the reference keeps it.  A thread
+// per query; past 64 chunks (the few-query searches have hundreds) a wave per
+// query: lanes take strided chunks, then a butterfly on (distance, chunk)
+// picks the lowest chunk among equal distances.
 __global__ __launch_bounds__(TB) void k_nn_reduce(const gbp_plan_status *st, const int32_t *nq_dev,
                                                   const int32_t *nv_dev, int64_t bmax,
                                                   const double *__restrict__ pd,
@@ -490,18 +493,44 @@ __global__ __launch_bounds__(TB) void k_nn_reduce(const gbp_plan_status *st, con
   const int64_t nq = *nq_dev, nv = *nv_dev;
   int64_t ch, nch;
   nn_geometry(nq, nv, bmax, ch, nch);
-  for (int64_t qi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; qi < nq;
-       qi += (int64_t)gridDim.x * blockDim.x) {
+  if (nch <= WAVE) {
+    for (int64_t qi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; qi < nq;
+         qi += (int64_t)gridDim.x * blockDim.x) {
+      double best = INFINITY;
+      int bi = 0;
+      for (int64_t c = 0; c < nch; c++) {
+        const double d = pd[c * nq + qi];
+        if (d < best) {
+          best = d;
+          bi = pi[c * nq + qi];
+        }
+      }
+      out[qi] = bi;
+    }
+    return;
+  }
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / WAVE);
+  for (int64_t qi = blockIdx.x * (int64_t)(blockDim.x / WAVE) + threadIdx.x / WAVE; qi < nq;
+       qi += waves) {
     double best = INFINITY;
-    int bi = 0;
-    for (int64_t c = 0; c < nch; c++) {
+    int64_t bc = nch;  // chunk of the best (none)
+    for (int64_t c = lane; c < nch; c += WAVE) {
       const double d = pd[c * nq + qi];
       if (d < best) {
         best = d;
-        bi = pi[c * nq + qi];
+        bc = c;
       }
     }
-    out[qi] = bi;
+    for (int off = WAVE / 2; off > 0; off >>= 1) {
+      const double od = __shfl_xor(best, off);
+      const int64_t oc = __shfl_xor(bc, off);
+      if (od < best || (od == best && oc < bc)) {
+        best = od;
+        bc = oc;
+      }
+    }
+    if (lane == 0) out[qi] = bc < nch ? pi[bc * nq + qi] : 0;
   }
 }
 
