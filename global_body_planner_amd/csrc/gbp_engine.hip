@@ -638,7 +638,11 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
       // persistent: one workgroup per resident slot (opt_waves waves per SIMD;
       // W, the register budget, allows at least that many)
       const int64_t resident = (int64_t)t->num_cus * std::max<int64_t>(1, t->opt_waves * 256 / block);
-      const int64_t g = std::max<int64_t>(1, std::min<int64_t>(resident, (m + block - 1) / block));
+      // every resident slot as long as each wave gets an attempt: a batch
+      // smaller than the resident lanes still spreads over every CU, its
+      // waves starting with idle lanes that help from the first step
+      // (65,536 attempts: 0.084 -> 0.072 ms; 262,144: unchanged)
+      const int64_t g = std::max<int64_t>(1, std::min<int64_t>(resident, (m + WAVE - 1) / WAVE));
       hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, CM>), dim3((unsigned)g), dim3(block),
                          coords + rows, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
                          flags + off, c, n_dev, (int)t->opt_helpers,
