@@ -12,11 +12,15 @@ no data-path collective ("scaling": "weak"); only the timing max and the
 counter sums cross ranks.
 
 The timed region is K back-to-back launches (no events inside), issued
-round-robin on `--streams` HIP streams (default 4; the steps are independent
+round-robin on `--streams` HIP streams (default 2; the steps are independent
 passes, each with its own output buffers, so one launch's ragged end overlaps
 the next one's start); the serial single-stream loop is timed too and
-reported as `value_serial`.  A further pass of K launches bracketed by HIP
-events on one stream gives the kernel's own duration for the roofline.
+reported as `value_serial`.  Step k runs on resident batch k mod
+`--fresh-batches` (8 distinct batches of the same distribution, all resident
+before timing), so no launch replays the previous one's Infinity-Cache-warm
+rows; the one-batch replay rates are reported under `replay`.  A further pass
+of K launches bracketed by HIP events on one stream gives the kernel's own
+duration for the roofline.
 
 Extra fields: `roofline` for the validate kernel (algorithmic bytes per
 SURVEY §8(d): 144 B in + 76 B out + 32 B x (G + V) per attempt, G/V = the
@@ -60,7 +64,7 @@ def parse():
     p.add_argument("--seed", type=int, default=W.CONFIG_SEEDS[3])
     p.add_argument("--kernel", choices=["persistent", "direct"], default="persistent")
     p.add_argument("--waves", type=int, default=2)
-    p.add_argument("--streams", type=int, default=4,
+    p.add_argument("--streams", type=int, default=2,
                    help="HIP streams the K independent steps are issued on round-robin (1: serial)")
     p.add_argument("--adaptive", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0,
@@ -81,7 +85,7 @@ def parse():
     p.add_argument("--config2", type=int, default=1,
                    help="also measure config 2 (synth-rough-256, 65,536 attempts) (rank 0)")
     p.add_argument("--fresh-batches", type=int, default=8,
-                   help="distinct resident batches cycled by the fresh-inputs serial rate")
+                   help="distinct resident batches the timed steps cycle through (1: replay one)")
     return p.parse_args()
 
 
@@ -400,25 +404,24 @@ def main():
     n_frag = int(((flags & L.F_FRAGILE) != 0).sum().item())
     bytes_per_launch = B * (BYTES_IN + BYTES_OUT) + BYTES_PER_LOOKUP * gv
 
-    elapsed, elapsed_serial, kern_ms = measure(T, s, a, d, B, res, args, dev, world)
-    elapsed_serial = sharding.reduce_run(elapsed_serial, [0], dev)[0]
-    # the rate a planner iteration sees: every launch on NEW inputs (distinct
-    # resident batches cycled serially, no replay of warm rows)
-    fresh = None
+    # every timed step runs on a NEW resident batch (8 distinct batches of the
+    # same distribution cycled): no replay of Infinity-Cache-warm rows, as in a
+    # planner whose iterations never repeat their inputs
+    batches = None
     if args.fresh_batches > 1:
         batches = [(s, a, d)] + [W.make_attempts(T, B, args.seed, index_base=base + k * world * B)[:3]
                                  for k in range(1, args.fresh_batches)]
-        el_fs, el_fresh, _ = measure(T, s, a, d, B, res, args, dev, world, batches=batches)
-        el_fresh = sharding.reduce_run(el_fresh, [0], dev)[0]
-        el_fs = sharding.reduce_run(el_fs, [0], dev)[0]
-        fresh = {"value_fresh": round(B * world * args.steps / el_fs, 1),
-                 "value_serial_fresh": round(B * world * args.steps / el_fresh, 1),
-                 "ms_per_step": round(el_fresh / args.steps * 1e3, 4),
-                 "batches": args.fresh_batches,
-                 "definition": "each launch on a different resident batch of the same distribution "
-                               "(no input reuse between consecutive launches), on the headline's "
-                               "streams (value_fresh) and serially on one (value_serial_fresh)"}
-        del batches
+    replay = None
+    if batches is not None:  # (measured first: it also brings the GPU to its clocks)
+        el_rp, el_rps, _ = measure(T, s, a, d, B, res, args, dev, world)
+        el_rp = sharding.reduce_run(el_rp, [0], dev)[0]
+        el_rps = sharding.reduce_run(el_rps, [0], dev)[0]
+        replay = {"value": round(B * world * args.steps / el_rp, 1),
+                  "value_serial": round(B * world * args.steps / el_rps, 1),
+                  "definition": "every step on the same resident batch (round 1's protocol)"}
+    elapsed, elapsed_serial, kern_ms = measure(T, s, a, d, B, res, args, dev, world, batches=batches)
+    elapsed_serial = sharding.reduce_run(elapsed_serial, [0], dev)[0]
+    del batches
 
     elapsed, sums = sharding.reduce_run(elapsed, [B, n_valid, n_ood, n_frag, gv, probes], dev)
     sums = torch.tensor(sums, dtype=torch.float64)
@@ -485,7 +488,9 @@ def main():
                 "kernel": "k_validate_persistent" if args.kernel == "persistent" else "k_validate_direct",
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },
-            "fresh_inputs": fresh,
+            "inputs": (f"fresh: step k runs on resident batch k mod {args.fresh_batches} "
+                       "(distinct batches of the same distribution)" if replay else "one resident batch"),
+            "replay": replay,
             "time_to_first_solution": ttfs,
             "time_to_first_solution_config2": ttfs2,
             "time_to_first_solution_config1": ttfs1,
