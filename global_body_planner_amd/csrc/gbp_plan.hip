@@ -61,8 +61,8 @@ struct gbp_tree {
   int device = 0;
   int64_t cap = 0;
   double *v = nullptr;        // [cap][8] vertex states (GraphClass vertices)
-  float *vf = nullptr;        // [cap][8] the same rounded to fp32 (nearest-neighbour filter)
-  float *vmax = nullptr;      // [8] max |vf[j][k]| over the vertices (NaN skipped)
+  float *vf = nullptr;        // [(cap+1)/2][18] fp32 row pairs (nearest-neighbour filter, nn_put_row)
+  float *vmax = nullptr;      // [8] max |fl32(v[j][k])| over the vertices (NaN skipped)
   double *a = nullptr;        // [cap][10] the action that reached each vertex
   double *g = nullptr;        // [cap] cost to come: g[parent] + poseDistance
   int32_t *parent = nullptr;  // [cap], -1 at the root
@@ -251,10 +251,15 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
 // query and tree sizes, nn_geometry).
 //
 // The exact answer (stateDistance in fp64, planning_utils.cpp:116-127, the
-// lowest index among equal distances) is found through an fp32 filter:
-//   pass 1  B = min_j S_j over the chunk, S_j = |fl32(v_j) - fl32(q)|^2 in
-//           fp32 (packed FMAs; the tree's vf mirror, rows by scalar loads:
-//           wave-uniform row, SGPR operands);
+// lowest index among equal distances) is found through an fp32 filter in the
+// dot-product form:
+//   pass 1  B = min_j S_j over the chunk, S_j = n_j - 2 g.f_j: f_j = fl32(v_j)
+//           and n_j = fl32(|f_j|^2) from the tree's row pairs (nn_put_row),
+//           g = fl32(q); |g|^2 + S_j is the fp32-space squared distance.  Two
+//           rows are interleaved by component, so one packed FMA with the row
+//           pair as its SGPR operand advances both: 4 packed FMAs + 1 min per
+//           row (the difference form took 4 subtractions + 4 FMAs + 1 add +
+//           1 min);
 //   pass 2  the same S_j again; j is recorded as a candidate iff S_j <= T(B)
 //           (tested once per block of rows on the wave's ballot: with the
 //           final minimum the threshold is tight, so almost no block holds
@@ -262,19 +267,21 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
 //   exact   stateDistance in fp64 for the candidates; the smallest
 //           (distance, index) pair wins, which is the reference's ascending
 //           scan with strict < (the first index reaching the minimum).
-// T(B) = ((1 + 2^-19) sqrt(B) + 2.5 E)^2 (1 + 2^-20) with E^2 =
-// sum_k (2^-22 (M_k + |q_k|))^2 and M_k >= max |v_jk| over the tree (kept by
-// the appends, gbp_tree.vmax).  Why no minimiser is lost: each fp32
-// difference is within 2.01 u (|v_k| + |q_k|) of v_k - q_k (u = 2^-24: two
-// input roundings and the subtraction), so the fp32 vector's length is within
-// E/2 of the true distance D_j; the FMA sum of the 8 squares is within a
-// relative gamma_8 < 4.8e-7; a minimiser j* of the fp64 distance has
-// D_j* <= D_i (1 + 3e-15) for every i.  Hence
-// sqrt(S_j*) <= sqrt((1+g)/(1-g)) (1 + 3e-15) sqrt(B) + 1.01 E sqrt(1+g)
-// < T(B)^(1/2): j* is recorded, and so is every index tying with it.  The
-// bound assumes |v|, |q| < 1e15 (no fp32 overflow of the squares); a wave
-// with a query or tree outside that, or with more than NN_CAND candidates in
-// a lane, scans the chunk in fp64 instead (ascending, strict <).
+// Why no minimiser is lost (u = 2^-24, M_k = tree.vmax[k] >= max_j |f_jk|,
+// R^2 = sum_k (M_k + |g_k|)^2, P_j = |f_j - g|^2 exactly, D_j = |v_j - q|):
+//   * the 8-FMA chain from n_j and the fp64-summed, fp32-rounded n_j put
+//     S_j + |g|^2 within eps = 10 u R^2 of P_j (gamma_8 (n_j + 2 sum|g_k f_jk|)
+//     + 1.01 u |f_j|^2 <= 9.1 u R^2);
+//   * |sqrt(P_j) - D_j| <= |f_j - v_j| + |g - q| <= del = 2 u R;
+//   * the fp64 minimiser j* has D_j* <= D_i (1 + 3e-15) for every i.
+// With i0 the pass-1 argmin, r0 = sqrt(max(0, B + |g|^2 + eps)) bounds
+// sqrt(P_i0), so sqrt(P_j*) <= r1 = (r0 + del)(1 + 4e-15) + del and
+// S_j* <= r1^2 - |g|^2 + eps = T(B) (evaluated in fp64, rounded up to fp32):
+// j* is recorded, and so is every index tying with it.  The bound assumes
+// |v|, |q| < 1e15 (no fp32 overflow of the squares); a wave with a query or
+// tree outside that, or with more than NN_CAND candidates in a lane, scans
+// the chunk in fp64 instead (ascending, strict <).  eps is ~1e-3 m^2 on the
+// planner's maps against nearest distances of metres: one or two candidates.
 // Measured alternatives (profiles/r02h_nn_filter.txt): one pass with a running
 // threshold (a branch per row: slower, and insertion-order trends make the
 // running minimum fall slowly), bit-reversed visiting orders (scattered
@@ -282,6 +289,9 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
 // staged in LDS (every broadcast row read still moves 64 x 32 B through the
 // LDS port) or fed through v_readlane: all between 1.0x and 1.9x slower.
 constexpr int NN_CAND = 16;
+// floats per row pair: [2k + (j & 1)] component k of rows 2p, 2p+1 (k < 8),
+// [16 + (j & 1)] their fp32 squared norms
+constexpr int NN_PAIR = 18;
 
 typedef float nnf2 __attribute__((ext_vector_type(2)));
 
@@ -289,7 +299,8 @@ typedef float nnf2 __attribute__((ext_vector_type(2)));
 // (query tile, chunk) items to occupy the GPU (~2048), chunks of at least 64
 // rows, and at most NN_MAX_CHUNKS * bmax partial slots (pd[c * nq + qi]).  A
 // handful of queries (the connect stage's new vertices) thus still spreads
-// over hundreds of chunks instead of scanning the tree serially.
+// over hundreds of chunks instead of scanning the tree serially.  Chunks
+// start at even rows (whole row pairs).
 __device__ __forceinline__ void nn_geometry(int64_t nq, int64_t nv, int64_t bmax, int64_t &ch,
                                             int64_t &nch) {
   const int64_t nqt = nq > 0 ? (nq + TB - 1) / TB : 1;
@@ -300,6 +311,20 @@ __device__ __forceinline__ void nn_geometry(int64_t nq, int64_t nv, int64_t bmax
   const int64_t ch_min = (nv + slots - 1) / slots;
   if (ch < ch_min) ch = (ch_min + 63) & ~(int64_t)63;
   nch = nv > 0 ? (nv + ch - 1) / ch : 1;
+}
+
+// the filter's row j: fl32 of the state and the fp32 rounding of its fp64
+// squared norm (each fl32 square is exact in fp64)
+__device__ __forceinline__ void nn_put_row(float *__restrict__ vp, int64_t j, const double *s) {
+  float *b = vp + NN_PAIR * (j >> 1) + (j & 1);
+  double n = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const float f = (float)s[k];
+    b[2 * k] = f;
+    n = n + (double)f * (double)f;
+  }
+  b[16] = (float)n;
 }
 
 // stateDistance(q, vertex j) exactly as the reference evaluates it
@@ -343,68 +368,81 @@ __device__ __forceinline__ void nn_scan64(const double qq[8], const double *__re
   for (; jb < j1; jb++) body(jb, 1);
 }
 
-__device__ __forceinline__ float nn_threshold(float B, double b) {
-  const double tb = (1.0 + 0x1p-19) * sqrt((double)B) + b;
-  return (float)(tb * tb * (1.0 + 0x1p-20));
+// T(B) above; g2 = |g|^2, r2 = R^2
+__device__ __forceinline__ float nn_threshold(float B, double g2, double r2) {
+  const double eps = 10.0 * 0x1p-24 * r2, del = 2.0 * 0x1p-24 * sqrt(r2);
+  const double r0 = sqrt(fmax(0.0, (double)B + g2 + eps));
+  const double r1 = (r0 + del) * (1.0 + 4e-15) + del;
+  return nextafterf((float)(r1 * r1 * (1.0 + 1e-12) - g2 + eps), INFINITY);
 }
 
-// UNR consecutive rows [jb, jb + UNR) by one contiguous scalar load
+// UNR consecutive row pairs from pair pb, one contiguous scalar load
 template <int UNR>
-__device__ __forceinline__ void nn_load_rows(const float *__restrict__ vf, int jb,
-                                             float (&rv)[UNR][8]) {
-  const float *vj = vf + 8 * (int64_t)__builtin_amdgcn_readfirstlane(jb);
+__device__ __forceinline__ void nn_load_pairs(const float *__restrict__ vp, int pb,
+                                              float (&rv)[UNR][NN_PAIR]) {
+  const float *b = vp + NN_PAIR * (int64_t)__builtin_amdgcn_readfirstlane(pb);
 #pragma unroll
   for (int r = 0; r < UNR; r++)
 #pragma unroll
-    for (int c = 0; c < 8; c++) rv[r][c] = vj[8 * r + c];
+    for (int c = 0; c < NN_PAIR; c++) rv[r][c] = b[NN_PAIR * r + c];
 }
 
-__device__ __forceinline__ float nn_s32(const nnf2 (&qf)[4], const float (&rv)[8]) {
-  nnf2 acc = {0.f, 0.f};
+// S of both rows of a pair: a = -2 g
+__device__ __forceinline__ nnf2 nn_s2(const float (&a)[8], const float (&rv)[NN_PAIR]) {
+  nnf2 acc = {rv[16], rv[17]};
 #pragma unroll
-  for (int c = 0; c < 4; c++) {
-    const nnf2 vk = {rv[2 * c], rv[2 * c + 1]};
-    const nnf2 d = vk - qf[c];
-    acc = __builtin_elementwise_fma(d, d, acc);
-  }
-  return acc.x + acc.y;
+  for (int k = 0; k < 8; k++)
+    acc = __builtin_elementwise_fma(nnf2{rv[2 * k], rv[2 * k + 1]}, nnf2{a[k], a[k]}, acc);
+  return acc;
 }
 
-// Rows [j0, j1) in blocks of UNR (the tail row by row).  MODE 0: B = min S
-// (selects, no branch); MODE 1: record the rows with S <= T, tested once per
-// block on the wave's ballot (the threshold is tight, so a block almost
-// never holds a candidate in any lane).
+// Rows [j0, j1), j0 even, as row pairs in blocks of UNR (then pair by pair; an
+// odd j1 leaves its last row alone in a pair, whose partner is masked).
+// MODE 0: B = min S (selects, no branch); MODE 1: record the rows with
+// S <= T, tested once per block on the wave's ballot (the threshold is tight,
+// so a block almost never holds a candidate in any lane).
 template <int UNR, int MODE>
-__device__ __forceinline__ void nn_sweep(const nnf2 (&qf)[4], const float *__restrict__ vf, int j0,
+__device__ __forceinline__ void nn_sweep(const float (&a)[8], const float *__restrict__ vp, int j0,
                                          int j1, float &B, float T, int &cnt,
                                          int32_t (*cand)[TB]) {
-  auto block = [&](int jb, auto m_tag) {
+  auto block = [&](int pb, auto m_tag, bool lone) {
     constexpr int M = decltype(m_tag)::value;
-    float rv[M][8];
-    nn_load_rows<M>(vf, jb, rv);
-    float S[M];
+    float rv[M][NN_PAIR];
+    nn_load_pairs<M>(vp, pb, rv);
+    nnf2 S[M];
 #pragma unroll
-    for (int r = 0; r < M; r++) S[r] = nn_s32(qf, rv[r]);
+    for (int r = 0; r < M; r++) S[r] = nn_s2(a, rv[r]);
+    if (lone) S[M - 1].y = __builtin_nanf("");  // past j1: never < B, never <= T
     if (MODE == 0) {
 #pragma unroll
-      for (int r = 0; r < M; r++) B = S[r] < B ? S[r] : B;
+      for (int r = 0; r < M; r++) {
+        B = S[r].x < B ? S[r].x : B;
+        B = S[r].y < B ? S[r].y : B;
+      }
     } else {
       bool hit = false;
 #pragma unroll
-      for (int r = 0; r < M; r++) hit = hit || S[r] <= T;
+      for (int r = 0; r < M; r++) hit = hit || S[r].x <= T || S[r].y <= T;
       if (__ballot(hit)) {
 #pragma unroll
-        for (int r = 0; r < M; r++)
-          if (S[r] <= T) {
-            if (cnt < NN_CAND) cand[cnt][threadIdx.x] = jb + r;
+        for (int r = 0; r < M; r++) {
+          if (S[r].x <= T) {
+            if (cnt < NN_CAND) cand[cnt][threadIdx.x] = 2 * (pb + r);
             cnt++;
           }
+          if (S[r].y <= T) {
+            if (cnt < NN_CAND) cand[cnt][threadIdx.x] = 2 * (pb + r) + 1;
+            cnt++;
+          }
+        }
       }
     }
   };
-  int jb = j0;
-  for (; jb + UNR <= j1; jb += UNR) block(jb, std::integral_constant<int, UNR>{});
-  for (; jb < j1; jb++) block(jb, std::integral_constant<int, 1>{});
+  const int pf = j1 >> 1;  // full pairs [j0/2, pf)
+  int pb = j0 >> 1;
+  for (; pb + UNR <= pf; pb += UNR) block(pb, std::integral_constant<int, UNR>{}, false);
+  for (; pb < pf; pb++) block(pb, std::integral_constant<int, 1>{}, false);
+  if (j1 & 1) block(pf, std::integral_constant<int, 1>{}, true);
 }
 
 template <int UNR>
@@ -413,7 +451,7 @@ __global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restr
                                                   const double *__restrict__ q,
                                                   const int32_t *__restrict__ q_off_dev,
                                                   const double *__restrict__ v,
-                                                  const float *__restrict__ vf,
+                                                  const float *__restrict__ vp,
                                                   const float *__restrict__ vmax,
                                                   const int32_t *__restrict__ nv_dev, int64_t bmax,
                                                   double *__restrict__ pd,
@@ -428,7 +466,7 @@ __global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restr
   bool tree_bad = false;
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    mk[k] = (double)vmax[k] * (1.0 + 0x1p-20);
+    mk[k] = (double)vmax[k];
     tree_bad = tree_bad || !(mk[k] < 1e15);
   }
   for (int64_t item = blockIdx.x; item < nqt * nch; item += gridDim.x) {
@@ -437,28 +475,28 @@ __global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restr
     const int64_t qi = qt * TB + threadIdx.x;
     const bool live = qi < nq;
     if (!__ballot(live)) continue;  // a wave past the last query (no barriers here)
-    double qq[8], e2 = 0.0;
+    double qq[8], g2 = 0.0, r2 = 0.0;
+    float a[8];
     bool bad = tree_bad;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       qq[k] = live ? q[8 * (q_off + qi) + k] : 0.0;
-      const double ak = fabs(qq[k]);
-      const double dk = 0x1p-22 * (mk[k] + ak);
-      e2 = e2 + dk * dk;
-      bad = bad || (live && !(ak < 1e15));
+      const float gk = (float)qq[k];
+      a[k] = -2.0f * gk;
+      const double ak = fabs((double)gk);
+      g2 = g2 + ak * ak;
+      r2 = r2 + (mk[k] + ak) * (mk[k] + ak);
+      bad = bad || (live && !(fabs(qq[k]) < 1e15));
     }
     double best = INFINITY;
     int bi = -1;
     bool scan64 = __ballot(bad) != 0ull;
     if (!scan64) {
-      nnf2 qf[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) qf[k] = nnf2{(float)qq[2 * k], (float)qq[2 * k + 1]};
       float B = INFINITY;
       int cnt = 0;
-      nn_sweep<UNR, 0>(qf, vf, j0, j1, B, 0.f, cnt, cand);
-      const float T = live ? nn_threshold(B, 2.5 * sqrt(e2) + 1e-30) : -1.0f;
-      nn_sweep<UNR, 1>(qf, vf, j0, j1, B, T, cnt, cand);
+      nn_sweep<UNR, 0>(a, vp, j0, j1, B, 0.f, cnt, cand);
+      const float T = live ? nn_threshold(B, g2, r2) : -1.0f;
+      nn_sweep<UNR, 1>(a, vp, j0, j1, B, T, cnt, cand);
       scan64 = __ballot(cnt > NN_CAND) != 0ull;
       if (!scan64) {
         for (int m = 0; m < cnt; m++) {
@@ -664,12 +702,9 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
     copy8(s, sn + 8 * i);
     copy8(pv, tv + 8 * (int64_t)p);
     copy8(tv + 8 * (int64_t)idx, s);
+    nn_put_row(tvf, idx, s);
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const float f = (float)s[k];
-      tvf[8 * (int64_t)idx + k] = f;
-      vmax_update(tvmax + k, f);
-    }
+    for (int k = 0; k < 8; k++) vmax_update(tvmax + k, (float)s[k]);
     copy10(ta + 10 * (int64_t)idx, an + 10 * i);
     tp[idx] = p;
     tg[idx] = tg[p] + pose_distance(pv, s);  // graph_class.cpp:36-42 addEdge
@@ -861,9 +896,10 @@ __global__ void k_tree_init(gbp_tree t, double r0, double r1, double r2, double 
                             double r5, double r6, double r7) {
   const double r[8] = {r0, r1, r2, r3, r4, r5, r6, r7};
   copy8(t.v, r);
+  nn_put_row(t.vf, 0, r);
   for (int k = 0; k < 8; k++) {
-    t.vf[k] = (float)r[k];
-    t.vmax[k] = isnan(t.vf[k]) ? 0.f : fabsf(t.vf[k]);
+    const float f = (float)r[k];
+    t.vmax[k] = isnan(f) ? 0.f : fabsf(f);
   }
   for (int k = 0; k < 10; k++) t.a[k] = 0.0;
   t.g[0] = 0.0;
@@ -878,10 +914,8 @@ __global__ void k_tree_append(gbp_tree t, int64_t n, const double *__restrict__ 
   int32_t c = *t.count;
   for (int64_t i = 0; i < n; i++, c++) {
     copy8(t.v + 8 * (int64_t)c, s + 8 * i);
-    for (int k = 0; k < 8; k++) {
-      t.vf[8 * (int64_t)c + k] = (float)s[8 * i + k];
-      vmax_update(t.vmax + k, t.vf[8 * (int64_t)c + k]);
-    }
+    nn_put_row(t.vf, c, s + 8 * i);
+    for (int k = 0; k < 8; k++) vmax_update(t.vmax + k, (float)s[8 * i + k]);
     copy10(t.a + 10 * (int64_t)c, a + 10 * i);
     t.parent[c] = p[i];
     t.g[c] = p[i] >= 0 ? t.g[p[i]] + pose_distance(t.v + 8 * (int64_t)p[i], s + 8 * i) : 0.0;
@@ -950,9 +984,9 @@ unsigned tiles_for(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + CB - 
 
 int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
               const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s) {
-  // one query per lane, four rows per scalar load, 8 workgroups per CU: the
-  // fastest of {2, 4, 8} rows x {4, 8} workgroups per CU, and 1.4x the fp64
-  // scan it replaces (tools/nn_sweep.sh, profiles/r02h_nn_filter.txt)
+  // one query per lane, four row pairs per scalar load, 8 workgroups per CU:
+  // the fastest of {1, 2, 4} pairs x {4, 8} workgroups per CU
+  // (profiles/r02j_nn_dot.txt)
   hipLaunchKernelGGL((k_nn_filter<4>), dim3(num_cus * 8), dim3(TB), 0, s, w->st, nq_dev, q,
                      q_off_dev, tr->v, tr->vf, tr->vmax, tr->count, w->bmax, w->nn_d, w->nn_i);
   hipLaunchKernelGGL(k_nn_reduce, dim3(grid_for(w->bmax, TB, num_cus * 4)), dim3(TB), 0, s, w->st,
@@ -1048,7 +1082,7 @@ int tree_alloc(gbp_tree *t, int64_t cap) {
   int32_t *p = nullptr;
   if (hipMalloc(&v, 64 * cap) != hipSuccess) return GBP_E_ALLOC;
   if (hipMalloc(&a, 80 * cap) != hipSuccess || hipMalloc(&g, 8 * cap) != hipSuccess ||
-      hipMalloc(&p, 4 * cap) != hipSuccess || hipMalloc(&vf, 32 * cap) != hipSuccess) {
+      hipMalloc(&p, 4 * cap) != hipSuccess || hipMalloc(&vf, 4 * NN_PAIR * ((cap + 1) / 2)) != hipSuccess) {
     (void)hipFree(v);
     if (a) (void)hipFree(a);
     if (g) (void)hipFree(g);
@@ -1141,7 +1175,7 @@ int gbp_tree_reserve(gbp_tree *t, int64_t capacity, gbp_stream stream) {
     return rc;
   }
   HIPCHK_P(hipMemcpyAsync(t->v, old.v, 64 * old.cap, hipMemcpyDeviceToDevice, s));
-  HIPCHK_P(hipMemcpyAsync(t->vf, old.vf, 32 * old.cap, hipMemcpyDeviceToDevice, s));
+  HIPCHK_P(hipMemcpyAsync(t->vf, old.vf, 4 * NN_PAIR * ((old.cap + 1) / 2), hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->a, old.a, 80 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->g, old.g, 8 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->parent, old.parent, 4 * old.cap, hipMemcpyDeviceToDevice, s));

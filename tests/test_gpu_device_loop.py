@@ -152,6 +152,15 @@ def test_tree_nearest_fp32_filter_exact(gpu):
     verts = T.sample_states(20000, seed=41, stream_id=1)[0].cpu().numpy()
     q = T.sample_states(nq, seed=42, stream_id=2)[0].cpu().numpy()
     check(verts, q, "random")
+    # odd vertex counts (a chunk ending inside a row pair) and a single vertex
+    for nv in (4097, 20000 - 63, 1):
+        check(np.ascontiguousarray(verts[:nv]), q, f"odd {nv}")
+    # far from the origin: the dot-product form's cancellation widens the
+    # threshold (eps ~ 10 u R^2), so more candidates and the overflow scan
+    for off in (40.0, 300.0, 5000.0):
+        sh = np.zeros(8)
+        sh[:2] = off
+        check(verts + sh, q + sh, f"offset {off}")
     # clusters: 64 centres, 300 vertices each within 1e-9 (fp32-identical),
     # exact duplicates among them; queries at and near the centres
     base = verts[:64]
