@@ -288,7 +288,7 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
 // scalar loads), double-buffered scalar loads, two queries per lane, rows
 // staged in LDS (every broadcast row read still moves 64 x 32 B through the
 // LDS port) or fed through v_readlane: all between 1.0x and 1.9x slower.
-constexpr int NN_CAND = 16;
+constexpr int NN_CAND = 8;
 // floats per row pair: [2k + (j & 1)] component k of rows 2p, 2p+1 (k < 8),
 // [16 + (j & 1)] their fp32 squared norms
 constexpr int NN_PAIR = 18;
@@ -301,9 +301,9 @@ typedef float nnf2 __attribute__((ext_vector_type(2)));
 // handful of queries (the connect stage's new vertices) thus still spreads
 // over hundreds of chunks instead of scanning the tree serially.  Chunks
 // start at even rows (whole row pairs).
-__device__ __forceinline__ void nn_geometry(int64_t nq, int64_t nv, int64_t bmax, int64_t &ch,
-                                            int64_t &nch) {
-  const int64_t nqt = nq > 0 ? (nq + TB - 1) / TB : 1;
+__device__ __forceinline__ void nn_geometry(int64_t nq, int64_t nv, int64_t bmax, int64_t qts,
+                                            int64_t &ch, int64_t &nch) {
+  const int64_t nqt = nq > 0 ? (nq + qts - 1) / qts : 1;
   const int64_t want = (2048 + nqt - 1) / nqt;
   ch = (((nv + want - 1) / want) + 63) & ~(int64_t)63;
   if (ch < 64) ch = 64;
@@ -401,40 +401,53 @@ __device__ __forceinline__ nnf2 nn_s2(const float (&a)[8], const float (&rv)[NN_
 // MODE 0: B = min S (selects, no branch); MODE 1: record the rows with
 // S <= T, tested once per block on the wave's ballot (the threshold is tight,
 // so a block almost never holds a candidate in any lane).
-template <int UNR, int MODE>
-__device__ __forceinline__ void nn_sweep(const float (&a)[8], const float *__restrict__ vp, int j0,
-                                         int j1, float &B, float T, int &cnt,
-                                         int32_t (*cand)[TB]) {
+template <int UNR, int MODE, int QPL>
+__device__ __forceinline__ void nn_sweep(const float (&a)[QPL][8], const float *__restrict__ vp,
+                                         int j0, int j1, float (&B)[QPL], const float (&T)[QPL],
+                                         int (&cnt)[QPL], int32_t (*cand)[NN_CAND][TB]) {
   auto block = [&](int pb, auto m_tag, bool lone) {
     constexpr int M = decltype(m_tag)::value;
     float rv[M][NN_PAIR];
     nn_load_pairs<M>(vp, pb, rv);
-    nnf2 S[M];
+    nnf2 S[QPL][M];
 #pragma unroll
-    for (int r = 0; r < M; r++) S[r] = nn_s2(a, rv[r]);
-    if (lone) S[M - 1].y = __builtin_nanf("");  // past j1: never < B, never <= T
+    for (int u = 0; u < QPL; u++)
+#pragma unroll
+      for (int r = 0; r < M; r++) S[u][r] = nn_s2(a[u], rv[r]);
+    if (lone)  // past j1: never < B, never <= T
+#pragma unroll
+      for (int u = 0; u < QPL; u++) S[u][M - 1].y = __builtin_nanf("");
+    // minNum (v_min3_f32 over a pair): a NaN row is skipped, as the
+    // reference's strict < skips it; the sign of a zero minimum is immaterial
+    // to T(B)
     if (MODE == 0) {
 #pragma unroll
-      for (int r = 0; r < M; r++) {
-        B = S[r].x < B ? S[r].x : B;
-        B = S[r].y < B ? S[r].y : B;
-      }
+      for (int u = 0; u < QPL; u++)
+#pragma unroll
+        for (int r = 0; r < M; r++) B[u] = fminf(fminf(B[u], S[u][r].x), S[u][r].y);
     } else {
       bool hit = false;
 #pragma unroll
-      for (int r = 0; r < M; r++) hit = hit || S[r].x <= T || S[r].y <= T;
+      for (int u = 0; u < QPL; u++) {
+        float m = S[u][0].x;
+#pragma unroll
+        for (int r = 0; r < M; r++) m = fminf(fminf(m, S[u][r].x), S[u][r].y);
+        hit = hit || m <= T[u];
+      }
       if (__ballot(hit)) {
 #pragma unroll
-        for (int r = 0; r < M; r++) {
-          if (S[r].x <= T) {
-            if (cnt < NN_CAND) cand[cnt][threadIdx.x] = 2 * (pb + r);
-            cnt++;
+        for (int u = 0; u < QPL; u++)
+#pragma unroll
+          for (int r = 0; r < M; r++) {
+            if (S[u][r].x <= T[u]) {
+              if (cnt[u] < NN_CAND) cand[u][cnt[u]][threadIdx.x] = 2 * (pb + r);
+              cnt[u]++;
+            }
+            if (S[u][r].y <= T[u]) {
+              if (cnt[u] < NN_CAND) cand[u][cnt[u]][threadIdx.x] = 2 * (pb + r) + 1;
+              cnt[u]++;
+            }
           }
-          if (S[r].y <= T) {
-            if (cnt < NN_CAND) cand[cnt][threadIdx.x] = 2 * (pb + r) + 1;
-            cnt++;
-          }
-        }
       }
     }
   };
@@ -445,7 +458,9 @@ __device__ __forceinline__ void nn_sweep(const float (&a)[8], const float *__res
   if (j1 & 1) block(pf, std::integral_constant<int, 1>{}, true);
 }
 
-template <int UNR>
+// QPL queries per lane (tile of TB * QPL queries): each row pair loaded once
+// feeds QPL queries' FMAs, halving the scalar-load bytes per VALU instruction
+template <int UNR, int QPL>
 __global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restrict__ st,
                                                   const int32_t *__restrict__ nq_dev,
                                                   const double *__restrict__ q,
@@ -457,50 +472,72 @@ __global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restr
                                                   double *__restrict__ pd,
                                                   int32_t *__restrict__ pi) {
   if (gated(st)) return;
-  __shared__ int32_t cand[NN_CAND][TB];
+  __shared__ int32_t cand[QPL][NN_CAND][TB];
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   int64_t ch, nch;
-  nn_geometry(nq, nv, bmax, ch, nch);
-  const int64_t nqt = (nq + TB - 1) / TB;
-  double mk[8];
+  nn_geometry(nq, nv, bmax, TB * QPL, ch, nch);
+  const int64_t nqt = (nq + TB * QPL - 1) / (TB * QPL);
   bool tree_bad = false;
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
-    mk[k] = (double)vmax[k];
-    tree_bad = tree_bad || !(mk[k] < 1e15);
-  }
+  for (int k = 0; k < 8; k++) tree_bad = tree_bad || !(vmax[k] < 1e15f);
   for (int64_t item = blockIdx.x; item < nqt * nch; item += gridDim.x) {
     const int64_t qt = item / nch, c = item - qt * nch;
     const int j0 = (int)(c * ch), j1 = (int)min(nv, (c + 1) * ch);
-    const int64_t qi = qt * TB + threadIdx.x;
-    const bool live = qi < nq;
-    if (!__ballot(live)) continue;  // a wave past the last query (no barriers here)
-    double qq[8], g2 = 0.0, r2 = 0.0;
-    float a[8];
-    bool bad = tree_bad;
+    int64_t qi[QPL];
+    bool live[QPL], any = false, bad = tree_bad;
+    float a[QPL][8], T[QPL];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      qq[k] = live ? q[8 * (q_off + qi) + k] : 0.0;
-      const float gk = (float)qq[k];
-      a[k] = -2.0f * gk;
-      const double ak = fabs((double)gk);
-      g2 = g2 + ak * ak;
-      r2 = r2 + (mk[k] + ak) * (mk[k] + ak);
-      bad = bad || (live && !(fabs(qq[k]) < 1e15));
+    for (int u = 0; u < QPL; u++) {
+      qi[u] = qt * (TB * QPL) + u * TB + threadIdx.x;
+      live[u] = qi[u] < nq;
+      any = any || live[u];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const double x = live[u] ? q[8 * (q_off + qi[u]) + k] : 0.0;
+        a[u][k] = -2.0f * (float)x;
+        bad = bad || (live[u] && !(fabs(x) < 1e15));
+      }
     }
-    double best = INFINITY;
-    int bi = -1;
+    if (!__ballot(any)) continue;  // a wave past the last query (no barriers here)
     bool scan64 = __ballot(bad) != 0ull;
+    int cnt[QPL];
     if (!scan64) {
-      float B = INFINITY;
-      int cnt = 0;
-      nn_sweep<UNR, 0>(a, vp, j0, j1, B, 0.f, cnt, cand);
-      const float T = live ? nn_threshold(B, g2, r2) : -1.0f;
-      nn_sweep<UNR, 1>(a, vp, j0, j1, B, T, cnt, cand);
-      scan64 = __ballot(cnt > NN_CAND) != 0ull;
-      if (!scan64) {
-        for (int m = 0; m < cnt; m++) {
-          const int j = cand[m][threadIdx.x];
+      float B[QPL];
+#pragma unroll
+      for (int u = 0; u < QPL; u++) {
+        B[u] = INFINITY;
+        T[u] = 0.f;
+        cnt[u] = 0;
+      }
+      nn_sweep<UNR, 0, QPL>(a, vp, j0, j1, B, T, cnt, cand);
+#pragma unroll
+      for (int u = 0; u < QPL; u++) {
+        double g2 = 0.0, r2 = 0.0;  // |g|^2 and R^2 (g = -a / 2 exactly)
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const double ak = fabs(-0.5 * (double)a[u][k]), mk = (double)vmax[k];
+          g2 = g2 + ak * ak;
+          r2 = r2 + (mk + ak) * (mk + ak);
+        }
+        T[u] = live[u] ? nn_threshold(B[u], g2, r2) : -1.0f;
+      }
+      nn_sweep<UNR, 1, QPL>(a, vp, j0, j1, B, T, cnt, cand);
+      bool over = false;
+#pragma unroll
+      for (int u = 0; u < QPL; u++) over = over || cnt[u] > NN_CAND;
+      scan64 = __ballot(over) != 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < QPL; u++) {
+      double qq[8], best = INFINITY;
+      int bi = -1;
+#pragma unroll
+      for (int k = 0; k < 8; k++) qq[k] = live[u] ? q[8 * (q_off + qi[u]) + k] : 0.0;
+      if (scan64) {
+        nn_scan64<1>(qq, v, j0, j1, best, bi);
+      } else {
+        for (int m = 0; m < cnt[u]; m++) {
+          const int j = cand[u][m][threadIdx.x];
           const double d = nn_dist64(qq, v + 8 * (int64_t)j);
           if (d < best || (d == best && j < bi)) {
             best = d;
@@ -508,11 +545,10 @@ __global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restr
           }
         }
       }
-    }
-    if (scan64) nn_scan64<4>(qq, v, j0, j1, best, bi);
-    if (live) {
-      pd[c * nq + qi] = best;
-      pi[c * nq + qi] = bi;
+      if (live[u]) {
+        pd[c * nq + qi[u]] = best;
+        pi[c * nq + qi[u]] = bi;
+      }
     }
   }
 }
@@ -523,20 +559,36 @@ __global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restr
 // query: lanes take strided chunks, then a butterfly on (distance, chunk)
 // picks the lowest chunk among equal distances.
 __global__ __launch_bounds__(TB) void k_nn_reduce(const gbp_plan_status *st, const int32_t *nq_dev,
-                                                  const int32_t *nv_dev, int64_t bmax,
+                                                  const int32_t *nv_dev, int64_t bmax, int qts,
                                                   const double *__restrict__ pd,
                                                   const int32_t *__restrict__ pi,
                                                   int32_t *__restrict__ out) {
   if (gated(st)) return;
   const int64_t nq = *nq_dev, nv = *nv_dev;
   int64_t ch, nch;
-  nn_geometry(nq, nv, bmax, ch, nch);
+  nn_geometry(nq, nv, bmax, qts, ch, nch);
   if (nch <= WAVE) {
     for (int64_t qi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; qi < nq;
          qi += (int64_t)gridDim.x * blockDim.x) {
       double best = INFINITY;
       int bi = 0;
-      for (int64_t c = 0; c < nch; c++) {
+      int64_t c = 0;
+      for (; c + 4 <= nch; c += 4) {  // four chunks' loads in flight
+        double d[4];
+        int32_t id[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          d[r] = pd[(c + r) * nq + qi];
+          id[r] = pi[(c + r) * nq + qi];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+          if (d[r] < best) {
+            best = d[r];
+            bi = id[r];
+          }
+      }
+      for (; c < nch; c++) {
         const double d = pd[c * nq + qi];
         if (d < best) {
           best = d;
@@ -984,13 +1036,14 @@ unsigned tiles_for(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + CB - 
 
 int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
               const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s) {
-  // one query per lane, four row pairs per scalar load, 8 workgroups per CU:
-  // the fastest of {1, 2, 4} pairs x {4, 8} workgroups per CU
-  // (profiles/r02j_nn_dot.txt)
-  hipLaunchKernelGGL((k_nn_filter<4>), dim3(num_cus * 8), dim3(TB), 0, s, w->st, nq_dev, q,
+  // two queries per lane, four row pairs per scalar load, 8 workgroups per
+  // CU: the fastest of {1, 2, 4} pairs x {1, 2} queries x {4, 8} workgroups
+  // per CU on trees past ~20k vertices (profiles/r02j_nn_dot.txt)
+  constexpr int QPL = 2;
+  hipLaunchKernelGGL((k_nn_filter<4, QPL>), dim3(num_cus * 8), dim3(TB), 0, s, w->st, nq_dev, q,
                      q_off_dev, tr->v, tr->vf, tr->vmax, tr->count, w->bmax, w->nn_d, w->nn_i);
   hipLaunchKernelGGL(k_nn_reduce, dim3(grid_for(w->bmax, TB, num_cus * 4)), dim3(TB), 0, s, w->st,
-                     nq_dev, tr->count, w->bmax, w->nn_d, w->nn_i, out);
+                     nq_dev, tr->count, w->bmax, TB * QPL, w->nn_d, w->nn_i, out);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
 
