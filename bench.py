@@ -32,6 +32,7 @@ restatement with the reference's O(N) scans, one host thread, rank 0, N=1),
 """
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -63,7 +64,9 @@ def parse():
     p.add_argument("--terrain", default="synth-rough-1024")
     p.add_argument("--seed", type=int, default=W.CONFIG_SEEDS[3])
     p.add_argument("--kernel", choices=["persistent", "direct"], default="persistent")
-    p.add_argument("--waves", type=int, default=2)
+    p.add_argument("--waves", type=int, default=3,
+                   help="waves per SIMD of the headline's validate launches (3: best with the "
+                        "launches overlapping on --streams; the planner's serial launches keep 2)")
     p.add_argument("--streams", type=int, default=2,
                    help="HIP streams the K independent steps are issued on round-robin (1: serial)")
     p.add_argument("--adaptive", action="store_true")
@@ -84,6 +87,9 @@ def parse():
                         "0: the host-driven batched loop (buildRRTConnectBatched)")
     p.add_argument("--config2", type=int, default=1,
                    help="also measure config 2 (synth-rough-256, 65,536 attempts) (rank 0)")
+    p.add_argument("--config2-waves", type=int, default=2,
+                   help="waves per SIMD for config 2's 65,536-attempt launches (2: their fill and "
+                        "drain dominate; 3 measured slower)")
     p.add_argument("--fresh-batches", type=int, default=8,
                    help="distinct resident batches the timed steps cycle through (1: replay one)")
     return p.parse_args()
@@ -336,7 +342,7 @@ def config2_line(args, dev):
     roofline, bounded single-thread CPU baseline)."""
     data2 = td.by_name("synth-rough-256")
     T2 = gbp.Terrain.from_data(data2, device=dev.index)
-    T2.set_option(L.OPT_WAVES, args.waves)
+    T2.set_option(L.OPT_WAVES, args.config2_waves)
     B2 = 65536
     s2, a2, d2, _, _ = W.make_attempts(T2, B2, W.CONFIG_SEEDS[2])
     r2 = T2.validate_pairs(s2, a2, d2, adaptive=args.adaptive)
@@ -350,7 +356,7 @@ def config2_line(args, dev):
                        "[Reverse] 50/50, seed 20251017",
            "value": round(B2 * args.steps / el, 1), "unit": "extend-attempts/s",
            "value_serial": round(B2 * args.steps / el_serial, 1),
-           "kernel_ms_per_launch": round(kms, 4),
+           "kernel_ms_per_launch": round(kms, 4), "waves": args.config2_waves,
            "valid_fraction": float(r2.valid.to(torch.int64).sum().item()) / B2,
            "lookups_per_attempt": gv / B2,
            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
@@ -445,7 +451,10 @@ def main():
             try:
                 with open(args.traffic_json) as f:
                     tj = json.load(f)
-                if tj.get("terrain") == args.terrain and tj.get("batch") == B:
+                km = re.search(r"<[^,]+, (true|false), (\d+),", tj.get("kernel", ""))
+                if (tj.get("terrain") == args.terrain and tj.get("batch") == B and km
+                        and int(km.group(2)) == args.waves
+                        and (km.group(1) == "true") == bool(args.adaptive)):
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
