@@ -296,15 +296,15 @@ constexpr int NN_PAIR = 18;
 typedef float nnf2 __attribute__((ext_vector_type(2)));
 
 // Vertex chunk size and count for nq queries against nv vertices: enough
-// (query tile, chunk) items to occupy the GPU (~2048), chunks of at least 64
+// (query tile, chunk) items to occupy the GPU (`items`, 2048), chunks of at least 64
 // rows, and at most NN_MAX_CHUNKS * bmax partial slots (pd[c * nq + qi]).  A
 // handful of queries (the connect stage's new vertices) thus still spreads
 // over hundreds of chunks instead of scanning the tree serially.  Chunks
 // start at even rows (whole row pairs).
 __device__ __forceinline__ void nn_geometry(int64_t nq, int64_t nv, int64_t bmax, int64_t qts,
-                                            int64_t &ch, int64_t &nch) {
+                                            int64_t items, int64_t &ch, int64_t &nch) {
   const int64_t nqt = nq > 0 ? (nq + qts - 1) / qts : 1;
-  const int64_t want = (2048 + nqt - 1) / nqt;
+  const int64_t want = (items + nqt - 1) / nqt;
   ch = (((nv + want - 1) / want) + 63) & ~(int64_t)63;
   if (ch < 64) ch = 64;
   const int64_t slots = (NN_MAX_CHUNKS * bmax) / (nq > 0 ? nq : 1);  // chunks per query
@@ -405,10 +405,8 @@ template <int UNR, int MODE, int QPL>
 __device__ __forceinline__ void nn_sweep(const float (&a)[QPL][8], const float *__restrict__ vp,
                                          int j0, int j1, float (&B)[QPL], const float (&T)[QPL],
                                          int (&cnt)[QPL], int32_t (*cand)[NN_CAND][TB]) {
-  auto block = [&](int pb, auto m_tag, bool lone) {
-    constexpr int M = decltype(m_tag)::value;
-    float rv[M][NN_PAIR];
-    nn_load_pairs<M>(vp, pb, rv);
+  auto proc = [&](int pb, auto &rv, bool lone) {
+    constexpr int M = sizeof(rv) / sizeof(rv[0]);
     nnf2 S[QPL][M];
 #pragma unroll
     for (int u = 0; u < QPL; u++)
@@ -451,6 +449,12 @@ __device__ __forceinline__ void nn_sweep(const float (&a)[QPL][8], const float *
       }
     }
   };
+  auto block = [&](int pb, auto m_tag, bool lone) {
+    constexpr int M = decltype(m_tag)::value;
+    float rv[M][NN_PAIR];
+    nn_load_pairs<M>(vp, pb, rv);
+    proc(pb, rv, lone);
+  };
   const int pf = j1 >> 1;  // full pairs [j0/2, pf)
   int pb = j0 >> 1;
   for (; pb + UNR <= pf; pb += UNR) block(pb, std::integral_constant<int, UNR>{}, false);
@@ -469,13 +473,13 @@ __global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restr
                                                   const float *__restrict__ vp,
                                                   const float *__restrict__ vmax,
                                                   const int32_t *__restrict__ nv_dev, int64_t bmax,
-                                                  double *__restrict__ pd,
+                                                  int items, double *__restrict__ pd,
                                                   int32_t *__restrict__ pi) {
   if (gated(st)) return;
   __shared__ int32_t cand[QPL][NN_CAND][TB];
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   int64_t ch, nch;
-  nn_geometry(nq, nv, bmax, TB * QPL, ch, nch);
+  nn_geometry(nq, nv, bmax, TB * QPL, items, ch, nch);
   const int64_t nqt = (nq + TB * QPL - 1) / (TB * QPL);
   bool tree_bad = false;
 #pragma unroll
@@ -559,14 +563,14 @@ __global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restr
 // query: lanes take strided chunks, then a butterfly on (distance, chunk)
 // picks the lowest chunk among equal distances.
 __global__ __launch_bounds__(TB) void k_nn_reduce(const gbp_plan_status *st, const int32_t *nq_dev,
-                                                  const int32_t *nv_dev, int64_t bmax, int qts,
+                                                  const int32_t *nv_dev, int64_t bmax, int qts, int items,
                                                   const double *__restrict__ pd,
                                                   const int32_t *__restrict__ pi,
                                                   int32_t *__restrict__ out) {
   if (gated(st)) return;
   const int64_t nq = *nq_dev, nv = *nv_dev;
   int64_t ch, nch;
-  nn_geometry(nq, nv, bmax, qts, ch, nch);
+  nn_geometry(nq, nv, bmax, qts, items, ch, nch);
   if (nch <= WAVE) {
     for (int64_t qi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; qi < nq;
          qi += (int64_t)gridDim.x * blockDim.x) {
@@ -1039,11 +1043,11 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
   // two queries per lane, four row pairs per scalar load, 8 workgroups per
   // CU: the fastest of {1, 2, 4} pairs x {1, 2} queries x {4, 8} workgroups
   // per CU on trees past ~20k vertices (profiles/r02j_nn_dot.txt)
-  constexpr int QPL = 2;
+  constexpr int QPL = 2, items = 2048;  // (query tile, chunk) items per call, nn_geometry
   hipLaunchKernelGGL((k_nn_filter<4, QPL>), dim3(num_cus * 8), dim3(TB), 0, s, w->st, nq_dev, q,
-                     q_off_dev, tr->v, tr->vf, tr->vmax, tr->count, w->bmax, w->nn_d, w->nn_i);
+                     q_off_dev, tr->v, tr->vf, tr->vmax, tr->count, w->bmax, items, w->nn_d, w->nn_i);
   hipLaunchKernelGGL(k_nn_reduce, dim3(grid_for(w->bmax, TB, num_cus * 4)), dim3(TB), 0, s, w->st,
-                     nq_dev, tr->count, w->bmax, TB * QPL, w->nn_d, w->nn_i, out);
+                     nq_dev, tr->count, w->bmax, TB * QPL, items, w->nn_d, w->nn_i, out);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
 
