@@ -161,6 +161,17 @@ def test_tree_nearest_fp32_filter_exact(gpu):
         sh = np.zeros(8)
         sh[:2] = off
         check(verts + sh, q + sh, f"offset {off}")
+    # near-equal distances: 5 vertices on a unit shell around each query, radii
+    # 1 + O(1e-8), so the fp32 scores order them almost at random and only the
+    # threshold keeps the fp64 minimiser (tests/test_nn_filter_bound.py)
+    for off in (0.0, 300.0):
+        sh = np.zeros(8)
+        sh[:2] = off
+        dirs = rng.normal(size=(nq, 5, 8))
+        dirs /= np.linalg.norm(dirs, axis=2, keepdims=True)
+        rad = 1.0 + rng.normal(scale=1e-8, size=(nq, 5, 1))
+        shell = np.ascontiguousarray(((q + sh)[:, None, :] + dirs * rad).reshape(-1, 8))
+        check(shell, q + sh, f"shell {off}")
     # clusters: 64 centres, 300 vertices each within 1e-9 (fp32-identical),
     # exact duplicates among them; queries at and near the centres
     base = verts[:64]
