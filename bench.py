@@ -90,6 +90,8 @@ def parse():
     p.add_argument("--config2-waves", type=int, default=2,
                    help="waves per SIMD for config 2's 65,536-attempt launches (2: their fill and "
                         "drain dominate; 3 measured slower)")
+    p.add_argument("--config2-streams", type=int, default=4,
+                   help="HIP streams for config 2's launches (small launches: more overlap pays)")
     p.add_argument("--fresh-batches", type=int, default=8,
                    help="distinct resident batches the timed steps cycle through (1: replay one)")
     return p.parse_args()
@@ -349,7 +351,12 @@ def config2_line(args, dev):
     torch.cuda.synchronize()
     c = r2.counts.to(torch.int64) & 0xFFFFFFFF
     gv = int(((c & 0xFFFF) + (c >> 16)).sum().item())
-    el, el_serial, kms = measure(T2, s2, a2, d2, B2, r2, args, dev, 1)
+    batches2 = None  # fresh inputs per step, as the headline
+    if args.fresh_batches > 1:
+        batches2 = [(s2, a2, d2)] + [W.make_attempts(T2, B2, W.CONFIG_SEEDS[2], index_base=k * B2)[:3]
+                                     for k in range(1, args.fresh_batches)]
+    el, el_serial, kms = measure(T2, s2, a2, d2, B2, r2, args, dev, 1, streams=args.config2_streams,
+                                 batches=batches2)
     byts = B2 * (BYTES_IN + BYTES_OUT) + BYTES_PER_LOOKUP * gv
     ach = byts / (kms * 1e-3) / 1e9
     out = {"workload": "config 2: synth-rough-256, 65,536-attempt batch, isValidStateActionPair"
@@ -357,6 +364,8 @@ def config2_line(args, dev):
            "value": round(B2 * args.steps / el, 1), "unit": "extend-attempts/s",
            "value_serial": round(B2 * args.steps / el_serial, 1),
            "kernel_ms_per_launch": round(kms, 4), "waves": args.config2_waves,
+           "streams": args.config2_streams,
+           "inputs": f"fresh: step k runs on resident batch k mod {max(1, args.fresh_batches)}",
            "valid_fraction": float(r2.valid.to(torch.int64).sum().item()) / B2,
            "lookups_per_attempt": gv / B2,
            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
