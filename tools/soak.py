@@ -29,6 +29,8 @@ def main():
     p.add_argument("--seeds", type=int, default=4)
     p.add_argument("--batch", type=int, default=262144)
     p.add_argument("--threads", type=int, default=16)
+    p.add_argument("--waves", type=int, default=2,
+                   help="GBP_OPT_WAVES of the launches (3: bench.py's headline launch)")
     a = p.parse_args()
     oracle.set_scan_mode(1)  # bisection brackets: equal to the linear scan, faster
     total = frag_total = valid_total = 0
@@ -38,6 +40,8 @@ def main():
         T = gbp.Terrain.from_data(data, device=0)
         O = oracle.OracleTerrain.from_data(data)
         T.set_option(L.OPT_KERNEL, L.KERNEL_PERSISTENT)
+        T.set_option(L.OPT_WAVES, a.waves)
+        print(f"{name}: waves {a.waves}, coordinate mode {T.get_option(L.OPT_COORD_MODE)}", flush=True)
         for k in range(a.seeds):
             seed = 7919 * (k + 1) + len(name)
             s, act, d, _, tries = W.make_attempts(T, a.batch, seed)
