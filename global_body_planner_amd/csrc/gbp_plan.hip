@@ -245,7 +245,7 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
 // ============================================================================
 // nearest neighbour in a device tree (planner_class.cpp:185-200)
 // ============================================================================
-// Work item (query tile qt, vertex chunk c): 256 queries (one per lane)
+// Work item (query tile qt, vertex chunk c): 512 queries (two per lane)
 // against the chunk's vertices; best (distance, index) per query and chunk go
 // to the partial arrays (chunk size and count set on the device from the
 // query and tree sizes, nn_geometry).
@@ -257,9 +257,9 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
 //           and n_j = fl32(|f_j|^2) from the tree's row pairs (nn_put_row),
 //           g = fl32(q); |g|^2 + S_j is the fp32-space squared distance.  Two
 //           rows are interleaved by component, so one packed FMA with the row
-//           pair as its SGPR operand advances both: 4 packed FMAs + 1 min per
-//           row (the difference form took 4 subtractions + 4 FMAs + 1 add +
-//           1 min);
+//           pair as its SGPR operand advances both: 4 packed FMAs + half a
+//           v_min3_f32 per row (the difference form took 4 subtractions + 4
+//           FMAs + 1 add + a compare and select);
 //   pass 2  the same S_j again; j is recorded as a candidate iff S_j <= T(B)
 //           (tested once per block of rows on the wave's ballot: with the
 //           final minimum the threshold is tight, so almost no block holds
@@ -282,7 +282,9 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
 // tree outside that, or with more than NN_CAND candidates in a lane, scans
 // the chunk in fp64 instead (ascending, strict <).  eps is ~1e-3 m^2 on the
 // planner's maps against nearest distances of metres: one or two candidates.
-// Measured alternatives (profiles/r02h_nn_filter.txt): one pass with a running
+// Measured alternatives (profiles/r02h_nn_filter.txt, r02j_nn_dot.txt:
+// double-buffered row loads, other item counts, a best-block pass 2 were
+// neutral or slower in the dot form): one pass with a running
 // threshold (a branch per row: slower, and insertion-order trends make the
 // running minimum fall slowly), bit-reversed visiting orders (scattered
 // scalar loads), double-buffered scalar loads, two queries per lane, rows
