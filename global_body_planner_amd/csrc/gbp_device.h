@@ -139,24 +139,27 @@ __device__ __forceinline__ void fetch_cell(const TerrainView<ZT> &T, int ix, int
 // one block the compiler schedules together (their coordinate reads and
 // terrain gathers in flight at once) instead of ten branchy regions each
 // waiting on its own reads.
-// `cell` receives a valid cell index (the bracket, or 0 without one) that the
-// caller fetches from unconditionally: the straight-line form's index is then
-// used on every path, so the compiler cannot sink its computation (and the
-// coordinate reads) back under a branch.
+// `cell` receives a valid cell index that the caller fetches from
+// unconditionally: the bracket; without one, the cell at the domain edge the
+// point lies beyond (0 below d[0] or for NaN — the cell the reference's
+// heightIsNan tests — and n-2 at or above d[n-1]), so the cell's bounding
+// coordinates are the lines a FRAGILE margin must be measured to.  The
+// straight-line form's index is then used on every path, so the compiler
+// cannot sink its computation (and the coordinate reads) back under a branch.
 template <int CM, int AX, bool ONE = false, class ZT>
 __device__ __forceinline__ int bracket_ax(const TerrainView<ZT> &T, double v, int &cell) {
   const double d0 = AX == 0 ? T.x0 : T.y0, dN = AX == 0 ? T.xN : T.yN;
   const int n = AX == 0 ? T.nx : T.ny;
   if constexpr (ONE) {
-    const bool in = (v >= d0) & (v < dN);
-    const double vc = in ? v : d0;  // no bracket: cell 0 (its guess is 0, its correction 0)
+    const bool in = (v >= d0) & (v < dN), hi = v >= dN;
+    const double vc = in ? v : d0;  // no bracket: guess from d0 (guess 0, correction 0)
     int i = bracket_guess(n, d0, AX == 0 ? T.inv_hx : T.inv_hy, vc);
     i += (vc >= coord<CM, AX>(T, i + 1) ? 1 : 0) - (vc < coord<CM, AX>(T, i) ? 1 : 0);
-    cell = i;
-    return in ? i : (v >= dN ? BR_HIGH : BR_LOW);
+    cell = in ? i : (hi ? n - 2 : 0);
+    return in ? i : (hi ? BR_HIGH : BR_LOW);
   }
   const int r = bracket_ax<CM, AX, false>(T, v);
-  cell = r < 0 ? 0 : r;
+  cell = r >= 0 ? r : (r == BR_HIGH ? n - 2 : 0);
   return r;
 }
 template <int CM, int AX, bool ONE = false, class ZT>
@@ -474,7 +477,11 @@ struct Acc {
 
 // getGroundHeight on a probe, evaluated unconditionally (branch-free form):
 // the bilinear value of the clamped cell, `ok` = the reference's call would not
-// be UB, `near` = in-domain point within FRAGILE_EPS of a grid line
+// be UB, `near` = the point is within FRAGILE_EPS of a line bounding its cell
+// (bracket_ax): an interior grid line, or the map edge an out-of-domain point
+// lies beyond or an in-domain point lies next to — where a last-ulp difference
+// of the point moves it into another cell (another height, another NaN test)
+// or across the domain edge (defined <-> OOD)
 template <class ZT, int CM>
 __device__ __forceinline__ double probe_height_bf(const TerrainView<ZT> &T, const Probe<ZT> &p,
                                                   double x, double y, double eps, bool &ok,
@@ -484,7 +491,7 @@ __device__ __forceinline__ double probe_height_bf(const TerrainView<ZT> &T, cons
   const double x1 = coord<CM, 0>(T, p.cx), x2 = coord<CM, 0>(T, p.cx + 1);
   const double y1 = coord<CM, 1>(T, p.cy), y2 = coord<CM, 1>(T, p.cy + 1);
   ok = br || nanxy;
-  near = br && !nanxy &&
+  near = !nanxy &&
          (fabs(x - x1) < eps || fabs(x2 - x) < eps || fabs(y - y1) < eps || fabs(y2 - y) < eps);
   const double h = bilinear((double)p.q[0], (double)p.q[1], (double)p.q[2], (double)p.q[3], x1, x2,
                             y1, y2, x, y, T.rcp_seed);
@@ -558,14 +565,17 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
     const double y_corner = y_leg + R_23 * z_body;
     const double z_corner = z_leg + R_33 * z_body;
     const int rl = probe_nan(pl[k]);  // heightIsNan(leg) :614
+    bool okl, okc, nl, nc;
+    const double gl = probe_height_bf<ZT, CM>(T, pl[k], x_leg, y_leg, feps, okl, nl);
+    const double gc = probe_height_bf<ZT, CM>(T, pk[k], x_corner, y_corner, feps, okc, nc);
+    // a leg near a line bounding its cell is FRAGILE from its heightIsNan on:
+    // glibc's leg may sit in the neighbouring cell (NaN <-> finite) or across
+    // the map edge (OOD <-> in domain) as well as give another height
+    if (alive && nl) fl |= GBP_F_FRAGILE;
     if (alive && rl < 0) fl |= GBP_F_OOD;
     if (alive && rl > 0) fl |= GBP_F_NAN;
     alive = alive && rl == 0;
     G += alive ? 2u : 0u;  // both heights computed before the test :618-619
-    bool okl, okc, nl, nc;
-    const double gl = probe_height_bf<ZT, CM>(T, pl[k], x_leg, y_leg, feps, okl, nl);
-    const double gc = probe_height_bf<ZT, CM>(T, pk[k], x_corner, y_corner, feps, okc, nc);
-    if (alive && nl) fl |= GBP_F_FRAGILE;
     if (alive && !okl) fl |= GBP_F_OOD;
     alive = alive && okl;
     if (alive && nc) fl |= GBP_F_FRAGILE;

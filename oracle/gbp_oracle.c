@@ -206,11 +206,21 @@ int orc_is_valid_action(const double *a) {
   return 1;
 }
 
-/* does a lookup point sit within FRAGILE_EPS of a grid line (bracket could
- * move under a last-ulp trig difference)? */
-static int near_grid_line(const double *d, int n, int i, double v) {
-  if (i < 0) return 0;
-  return fabs(v - d[i]) < FRAGILE_EPS || (i + 1 < n && fabs(d[i + 1] - v) < FRAGILE_EPS);
+/* Does a trig-dependent lookup coordinate sit within FRAGILE_EPS of a line
+ * bounding its cell, so that a last-ulp trig difference could move it into
+ * another cell (another height, another heightIsNan cell: NaN <-> finite) or
+ * across the map edge (defined <-> OOD)?  The cell of a point with no bracket
+ * is the one at the edge it lies beyond: 0 below d[0] (the cell the
+ * reference's heightIsNan tests), n-2 at or above d[n-1]. */
+static int near_cell_line(const double *d, int n, int i, double v) {
+  int c = i >= 0 ? i : (i == BR_HIGH ? n - 2 : 0);
+  return fabs(v - d[c]) < FRAGILE_EPS || fabs(d[c + 1] - v) < FRAGILE_EPS;
+}
+
+static int near_point(const orc_terrain *T, double x, double y) {
+  if (isnan(x) || isnan(y)) return 0; /* NaN heights whatever the trig */
+  return near_cell_line(T->x, T->nx, bracket(T->x, T->nx, x), x) ||
+         near_cell_line(T->y, T->ny, bracket(T->y, T->ny, y), y);
 }
 
 static double cell_height(const orc_terrain *T, int ix, int iy, double x, double y) {
@@ -221,10 +231,9 @@ static double cell_height(const orc_terrain *T, int ix, int iy, double x, double
  * 1 = value in *h (NaN for NaN coordinates) */
 static int height_at(const orc_terrain *T, double x, double y, double *h, orc_stats *st) {
   if (isnan(x) || isnan(y)) { *h = NAN; return 1; }
+  if (near_point(T, x, y)) st->flags |= GBP_F_FRAGILE;
   int ix = bracket(T->x, T->nx, x), iy = bracket(T->y, T->ny, y);
   if (ix < 0 || iy < 0) return 0;
-  if (near_grid_line(T->x, T->nx, ix, x) || near_grid_line(T->y, T->ny, iy, y))
-    st->flags |= GBP_F_FRAGILE;
   *h = cell_height(T, ix, iy, x, y);
   return 1;
 }
@@ -280,7 +289,9 @@ int orc_is_valid_state(const orc_terrain *T, const double *s, int phase, orc_sta
       double x_corner = x_leg + R_13 * z_body;
       double y_corner = y_leg + R_23 * z_body;
       double z_corner = z_leg + R_33 * z_body;
-      /* heightIsNan(leg) :614 */
+      /* heightIsNan(leg) :614; FRAGILE from here on when the leg is near a
+       * line bounding its cell (NaN-cell boundaries and the map edge too) */
+      if (near_point(T, x_leg, y_leg)) st->flags |= GBP_F_FRAGILE;
       int rl = nan_at(T, x_leg, y_leg);
       if (rl < 0) { st->flags |= GBP_F_OOD; return 0; }
       if (rl) { st->flags |= GBP_F_NAN; return 0; }

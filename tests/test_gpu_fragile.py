@@ -95,6 +95,173 @@ def near_threshold_states(O, data, n_base, seed):
     return np.array(out), np.array(kind)
 
 
+def _lookup_points(s):
+    legs, corners, under = geometry(s)
+    return np.concatenate([legs[:, :2], corners[:, :2], under[None, :2]])   # 9 x (x, y)
+
+
+# offsets from a line: +-1e-13 (inside FRAGILE_EPS) and a few ulps (the size of
+# a trig difference), both sides, and exactly on it
+LINE_OFFSETS = (-1e-13, -3e-15, -1e-15, 0.0, 1e-15, 3e-15, 1e-13)
+
+
+def edge_states(O, data, n_base, seed):
+    """Valid STANCE states translated so that one of isValidState's
+    trig-dependent lookup points (a leg, a corner or the underside) lies
+    within +-1e-13 / a few ulps of a map edge (x0, xN, y0, yN): glibc's point
+    may then be in the domain where the kernel's is out of it (a defined
+    reference decision vs the OOD convention), or the other way round
+    (fast_terrain_map.cpp:101-117, the scan's domain [d[0], d[n-1]))."""
+    base, _ = O.sample_states(n_base, seed, 1, 0, L.STANCE, 256)
+    base = base[np.isfinite(base).all(1)]
+    x0, xN, y0, yN = data.bounds
+    rng = np.random.default_rng(seed)
+    out = []
+    for s in base:
+        pts = _lookup_points(s)
+        for axis, lo, hi in ((0, x0, xN), (1, y0, yN)):
+            # the outermost point towards each edge (reached unless an earlier
+            # leg fails), and one other point
+            for edge, k in ((lo, int(np.argmin(pts[:, axis]))), (hi, int(np.argmax(pts[:, axis]))),
+                            (lo, int(rng.integers(9))), (hi, int(rng.integers(9)))):
+                for off in LINE_OFFSETS:
+                    c = s.copy()
+                    c[axis] = s[axis] + (edge + off - pts[k, axis])
+                    out.append(c)
+    return np.array(out)
+
+
+def nan_map(n=256):
+    """synth-rough-n with blocks of NaN heights (grid_map maps carry NaN
+    cells): a NaN node makes the four cells around it NaN for heightIsNan."""
+    data = td.synth_rough(n)
+    z = data.z.copy()
+    blocks = [(40, 70, 60, 100), (120, 135, 20, 40), (180, 220, 150, 200), (60, 62, 190, 230)]
+    for i0, i1, j0, j1 in blocks:
+        z[i0:i1, j0:j1] = np.nan
+    return td.TerrainData(data.x, data.y, z, data.dx, data.dy, data.dz, name=f"synth-rough-{n}-nan"), blocks
+
+
+def nan_boundary_states(O, data, blocks, n_base, seed):
+    """Valid STANCE states (of the NaN map) translated so that one lookup
+    point sits within +-1e-13 / a few ulps of a grid line bounding a NaN
+    block: the cells on its two sides are NaN and finite, so glibc's leg may
+    pass heightIsNan where the kernel's fails it (or the other way round), and
+    a corner / underside height may be NaN on one side only
+    (fast_terrain_map.cpp:135-157, planning_utils.cpp:601-632)."""
+    base, _ = O.sample_states(n_base, seed, 1, 0, L.STANCE, 256)
+    base = base[np.isfinite(base).all(1)]
+    x, y = data.x, data.y
+    rng = np.random.default_rng(seed)
+    out = []
+    for s in base:
+        pts = _lookup_points(s)
+        i0, i1, j0, j1 = blocks[int(rng.integers(len(blocks)))]
+        # lines between a finite and a NaN cell: x[i0-1], x[i1]; y[j0-1], y[j1]
+        lines = [(0, x[i0 - 1]), (0, x[i1]), (1, y[j0 - 1]), (1, y[j1])]
+        for axis, line in lines:
+            k = 0 if rng.random() < 0.5 else int(rng.integers(9))   # leg 0 is tested first
+            other = 1 - axis
+            lo, hi = (y[j0], y[j1 - 1]) if axis == 0 else (x[i0], x[i1 - 1])
+            along = rng.uniform(lo, hi)                            # beside the NaN block
+            for off in LINE_OFFSETS:
+                c = s.copy()
+                c[axis] = s[axis] + (line + off - pts[k, axis])
+                c[other] = s[other] + (along - pts[k, other])
+                out.append(c)
+    return np.array(out)
+
+
+def _check_states_product_equals_oracle(T, O, st, label):
+    """The product's decisions (host entry: kernel + glibc re-decision of
+    FRAGILE states) equal the oracle's on every state, both phases; every
+    state the oracle flags FRAGILE is flagged by the kernel too.  Returns a
+    report line per phase."""
+    lines = []
+    for phase in (L.STANCE, L.FLIGHT):
+        v, f, c = T.valid_states(torch.from_numpy(st), phase)
+        rv, rf, rc = O.valid_states(st, phase, nthreads=8)
+        gf = u32(f)
+        gfrag, rfrag = (gf & L.F_FRAGILE) != 0, (rf & L.F_FRAGILE) != 0
+        missed = np.flatnonzero(rfrag & ~gfrag)
+        assert missed.size == 0, f"{label}: oracle-FRAGILE states not flagged by the kernel {missed[:10]}"
+        raw_diff = int((v.cpu().numpy() != rv).sum())
+        # every raw difference is a flagged (hence re-decided) state
+        assert np.all(gfrag[v.cpu().numpy() != rv]), label
+        hv, hf, hc = T.valid_states_host(st, phase)
+        assert np.array_equal(hv, rv), (label, np.flatnonzero(hv != rv)[:10])
+        assert np.array_equal(hf & MASK, rf & MASK), label
+        assert np.array_equal(hc, rc), label
+        lines.append(f"{label} phase {phase}: {st.shape[0]} states, {int(gfrag.sum())} FRAGILE "
+                     f"(oracle {int(rfrag.sum())}), {int(((rf & L.F_OOD) != 0).sum())} OOD, "
+                     f"{int(((rf & L.F_NAN) != 0).sum())} NaN, {raw_diff} raw kernel decisions "
+                     f"differed from glibc, 0 after resolution")
+    return lines
+
+
+@pytest.mark.parametrize("name", ["synth-rough-256", "slope-gridmap"])
+def test_map_edge_states(gpu, name):
+    """Lookup points within 1e-13 of each map edge: flagged, and the product's
+    decision equals the oracle's (glibc) with no exclusion."""
+    data, T, O = pair_of(name)
+    st = edge_states(O, data, 80, 17)
+    assert st.shape[0] > 2000
+    for line in _check_states_product_equals_oracle(T, O, st, name):
+        print(line)
+    rv, rf, _ = O.valid_states(st, L.STANCE, nthreads=8)
+    # both outcomes occur: the edge decides OOD vs in-domain
+    assert ((rf & L.F_OOD) != 0).sum() > 0 and ((rf & L.F_OOD) == 0).sum() > 0
+    assert ((rf & L.F_FRAGILE) != 0).sum() > st.shape[0] // 4
+
+
+def test_nan_boundary_states(gpu):
+    """Lookup points within 1e-13 of a grid line between a NaN and a finite
+    cell: flagged, and the product's decision equals the oracle's."""
+    import global_body_planner_amd as gbp
+    data, blocks = nan_map()
+    T = gbp.Terrain(data.x, data.y, data.z, data.dx, data.dy, data.dz, device=0)
+    O = oracle.OracleTerrain(data.x, data.y, data.z, data.dx, data.dy, data.dz)
+    st = nan_boundary_states(O, data, blocks, 150, 23)
+    assert st.shape[0] > 2000
+    for line in _check_states_product_equals_oracle(T, O, st, "synth-rough-256-nan"):
+        print(line)
+    rv, rf, _ = O.valid_states(st, L.STANCE, nthreads=8)
+    assert ((rf & L.F_NAN) != 0).sum() > 0 and ((rf & L.F_NAN) == 0).sum() > 0
+    assert ((rf & L.F_FRAGILE) != 0).sum() > st.shape[0] // 4
+
+
+@pytest.mark.parametrize("family", ["edge", "nan"])
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_edge_and_nan_boundary_pairs(gpu, family, adaptive):
+    """Pair checks whose first sample is such a state (forward stance at t = 0,
+    reverse flight at t = -0: the state itself, H12): the product (host entry;
+    _dev + resolve) equals the oracle on every attempt."""
+    import global_body_planner_amd as gbp
+    if family == "edge":
+        data, T, O = pair_of("synth-rough-256")
+        st = edge_states(O, data, 30, 29)
+    else:
+        data, blocks = nan_map()
+        T = gbp.Terrain(data.x, data.y, data.z, data.dx, data.dy, data.dz, device=0)
+        O = oracle.OracleTerrain(data.x, data.y, data.z, data.dx, data.dy, data.dz)
+        st = nan_boundary_states(O, data, blocks, 60, 31)
+    n = st.shape[0]
+    _, a, d, _, _ = attempts_oracle(O, n, seed=92)
+    ref = O.validate_pairs(st, a, d, adaptive=adaptive, nthreads=8)
+    host = T.validate_pairs_host(st, a, d, adaptive=adaptive)
+    nres = assert_pairs_equal(host, ref, f"{family} host", resolve=lambda g: g)
+    res = T.validate_pairs(torch.from_numpy(st), torch.from_numpy(a), torch.from_numpy(d),
+                           adaptive=adaptive)
+    gpu_t = (res.valid.cpu().numpy(), res.s_new.cpu().numpy(), res.t_new.cpu().numpy(),
+             u32(res.flags), u32(res.counts))
+    raw_diff = int((gpu_t[0] != ref[0]).sum())
+    nres2 = assert_pairs_equal(gpu_t, ref, f"{family} dev+resolve",
+                               resolve=resolver(T, st, a, d, adaptive))
+    assert nres2 > n // 8, (nres2, n)
+    print(f"{family} adaptive {adaptive}: {n} pairs, {nres2} FRAGILE re-decided, {raw_diff} raw "
+          f"kernel decisions differed from glibc, 0 after resolution")
+
+
 @pytest.mark.parametrize("name", ["synth-rough-256", "slope-gridmap"])
 def test_near_threshold_states(gpu, name):
     data, T, O = pair_of(name)
