@@ -23,7 +23,8 @@ F_STAGE_SHIFT = 8
 F_STAGE_MASK = 0xF << F_STAGE_SHIFT
 STORAGE_AUTO, STORAGE_F32, STORAGE_F64 = 0, 1, 2
 OPT_KERNEL, OPT_BLOCK, OPT_WAVES, OPT_LDS_COORDS, OPT_HELPERS = 1, 2, 4, 5, 8
-OPT_AFFINE_COORDS, OPT_COORD_MODE, OPT_XCD_MAP, OPT_FAST_RCP = 9, 10, 13, 14
+OPT_AFFINE_COORDS, OPT_COORD_MODE, OPT_XCD_MAP, OPT_FAST_RCP, OPT_FRAGILE_EPS = 9, 10, 13, 14, 15
+PLAN_HALT_TARGETS, PLAN_HALT_EXTEND, PLAN_HALT_CONNECT = 1, 2, 4
 KERNEL_DIRECT, KERNEL_PERSISTENT = 0, 1
 
 EXPORTS = [
@@ -36,7 +37,9 @@ EXPORTS = [
     "gbp_valid_states_dev", "gbp_valid_states_host",
     "gbp_validate_pairs_dev", "gbp_validate_pairs_host",
     "gbp_sample_states_dev", "gbp_sample_states_host", "gbp_sample_actions_dev",
-    "gbp_sample_actions_host",
+    "gbp_sample_actions_host", "gbp_terrain_set_sampling", "gbp_terrain_get_sampling",
+    "gbp_sample_states_dir_dev", "gbp_sample_states_dir_host", "gbp_sample_actions_dir_dev",
+    "gbp_sample_actions_dir_host",
     "gbp_extend_batch_dev", "gbp_extend_batch_host",
     "gbp_nearest_batch_dev", "gbp_nearest_batch_host",
     "gbp_neighbors_batch_dev", "gbp_neighbors_batch_host",
@@ -48,6 +51,20 @@ EXPORTS = [
     "gbp_plan_status_read", "gbp_plan_resolve_host", "gbp_extend_tree_dev",
     "gbp_extend_tree_finish_dev", "gbp_extend_tree_host", "gbp_tree_nearest_dev",
 ]
+
+
+class Sampling(ctypes.Structure):
+    """gbp_sampling (include/gbp.h): direction-biased sampling, params.yaml:21-27."""
+    _fields_ = [("state_flag", ctypes.c_int32), ("state_speed_direction", ctypes.c_int32),
+                ("state_p", ctypes.c_double), ("action_flag", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("action_p", ctypes.c_double)]
+
+
+def sampling(state_flag=False, state_p=0.05, speed_direction=False, action_flag=False,
+             action_p=0.15):
+    """A Sampling record (defaults: the reference's rrt.h:194-200 thresholds, flags off)."""
+    return Sampling(int(bool(state_flag)), int(bool(speed_direction)), float(state_p),
+                    int(bool(action_flag)), 0, float(action_p))
 
 
 class GbpError(RuntimeError):
@@ -101,6 +118,12 @@ def load(path=None):
         "gbp_sample_actions_dev": (I, [I64, P, U64, U64, I64, P, P]),
         "gbp_sample_states_host": (I, [P, I64, U64, U64, I64, I, I, P, P]),
         "gbp_sample_actions_host": (I, [P, I64, P, U64, U64, I64, P]),
+        "gbp_terrain_set_sampling": (I, [P, P]),
+        "gbp_terrain_get_sampling": (I, [P, P]),
+        "gbp_sample_states_dir_dev": (I, [P, I64, U64, U64, I64, P, P, P, P, P]),
+        "gbp_sample_states_dir_host": (I, [P, I64, U64, U64, I64, P, P, P, P]),
+        "gbp_sample_actions_dir_dev": (I, [P, I64, P, P, P, P, I, P, U64, U64, I64, P, P]),
+        "gbp_sample_actions_dir_host": (I, [P, I64, P, P, P, P, I, P, U64, U64, I64, P]),
         "gbp_extend_batch_dev": (I, [P, I64, P, P, P, I, I, U64, I64, P, P, P, P, P, P, P]),
         "gbp_extend_batch_host": (I, [P, I64, P, P, P, I, I, U64, I64, P, P, P, P, P, P]),
         "gbp_resolve_fragile_host": (I, [P, I64, P, P, P, I, I, P, P, P, P, P, P]),

@@ -77,6 +77,9 @@ struct TerrainView {
   // Newton steps from this seed give exactly 1.0 / ((x2-x1)*(y2-y1)) for every
   // pair of grid spacings of the terrain (recip_area)
   double rcp_seed;
+  // the FRAGILE margin (GBP_OPT_FRAGILE_EPS): FRAGILE_EPS unless a caller asked
+  // for a wider one (more host re-decisions, never a different result)
+  double feps;
 };
 
 // Coordinate modes of the hot kernels (template CM): 0 = coordinate vectors
@@ -513,7 +516,7 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
     return false;
   }
   acc.V++;
-  const double eps = FRAGILE_EPS, hmin = H_MIN, hmax = H_MAX, hl = 0.5 * ROBOT_L, hw = 0.5 * ROBOT_W;
+  const double eps = T.feps, hmin = H_MIN, hmax = H_MAX, hl = 0.5 * ROBOT_L, hw = 0.5 * ROBOT_W;
   Probe<ZT> pc;
   probe<ZT, CM, ONE>(T, s[0], s[1], pc);
   const bool outside = (s[0] < T.x0) || (s[0] > T.xN) || (s[1] < T.y0) || (s[1] > T.yN);
@@ -832,6 +835,124 @@ __device__ __forceinline__ void sample_state_try(const TerrainView<ZT> &T, uint6
   q[5] = v * cos(theta);
   q[6] = 2 * P_MAX * u31 - P_MAX;
   q[7] = 0.0;
+}
+
+// ---- direction-biased sampling (gbp.h gbp_sampling) -----------------------------
+// The coin of a draw: the reference's `(double) rand() / RAND_MAX <= threshold`
+// (planner_class.cpp:27-29, planning_utils.cpp:381-383) as a uniform of its own
+// purpose, so either branch consumes the same counter-addressed draws.
+constexpr uint32_t PURPOSE_COIN = 3u;
+__device__ __forceinline__ bool coin(uint64_t seed, uint64_t stream_id, int64_t index,
+                                     uint32_t draw, double p) {
+  double c0, c1;
+  uniform2(seed, stream_id, PURPOSE_COIN, index, draw, c0, c1);
+  return c0 <= p;
+}
+
+// getRandomActionDirection (planning_utils.cpp:443-515): sample_action's draws
+// (f_z td/to, f_x td/to, f_y td/to, t_f, the normal pair), each tangential
+// force on the side of the velocity change s_from -> s_to: [0, mu f_z] where
+// the component grows, else [-mu f_z, 0]
+__device__ __forceinline__ void sample_action_direction(const double *nrm, const double *s_from,
+                                                        const double *s_to, uint64_t seed,
+                                                        uint64_t stream_id, int64_t index,
+                                                        double *a) {
+  double u[10];
+#pragma unroll
+  for (uint32_t d = 0; d < 5; d++) uniform2(seed, stream_id, PURPOSE_ACTION, index, d, u[2 * d], u[2 * d + 1]);
+  const bool dx_inc = s_to[3] > s_from[3], dy_inc = s_to[4] > s_from[4];
+  const double f_z_td = F_MAX * u[0];
+  const double f_z_to = F_MAX * u[1];
+  const double ff_td = MU * f_z_td, ff_to = MU * f_z_to;
+  const double f_x_td = dx_inc ? ff_td * u[2] : ff_td * u[2] - ff_td;
+  const double f_x_to = dx_inc ? ff_to * u[3] : ff_to * u[3] - ff_to;
+  const double f_y_td = dy_inc ? ff_td * u[4] : ff_td * u[4] - ff_td;
+  const double f_y_to = dy_inc ? ff_to * u[5] : ff_to * u[5] - ff_to;
+  const double f_td[3] = {f_x_td, f_y_td, f_z_td}, f_to[3] = {f_x_to, f_y_to, f_z_to};
+  double r_td[3], r_to[3];
+  rotate_grf(nrm, f_td, r_td);
+  rotate_grf(nrm, f_to, r_to);
+  a[0] = r_td[0] / M_CONST;
+  a[1] = r_td[1] / M_CONST;
+  a[2] = r_td[2] / M_CONST - G_CONST;
+  a[3] = r_to[0] / M_CONST;
+  a[4] = r_to[1] / M_CONST;
+  a[5] = r_to[2] / M_CONST - G_CONST;
+  a[6] = 0.3;
+  a[7] = (T_F_MAX - T_F_MIN) * u[6] + T_F_MIN;
+  double z0, z1;
+  box_muller(u[8], u[9], z0, z1);
+  a[8] = std_max(std_min(z0 * (ANG_ACC_MAX / 4.0) + 0.0, ANG_ACC_MAX), -ANG_ACC_MAX);
+  a[9] = std_max(std_min(z1 * (ANG_ACC_MAX / 4.0) + 0.0, ANG_ACC_MAX), -ANG_ACC_MAX);
+}
+
+// getRandomAction(surf_norm, direction, flag, p, s, s_near) (planning_utils.cpp:379-391)
+__device__ __forceinline__ void sample_action_cfg(const double *nrm, const gbp_sampling &cfg,
+                                                  int direction, const double *s,
+                                                  const double *s_near, uint64_t seed,
+                                                  uint64_t stream_id, int64_t index, double *a) {
+  if (cfg.action_flag && coin(seed, stream_id, index, 0, cfg.action_p)) {
+    if (direction == GBP_FORWARD)
+      sample_action_direction(nrm, s_near, s, seed, stream_id, index, a);
+    else
+      sample_action_direction(nrm, s, s_near, seed, stream_id, index, a);
+    return;
+  }
+  sample_action(nrm, seed, stream_id, index, a);
+}
+
+// PlannerClass::randomStateDirection (planner_class.cpp:82-148), try k of
+// index i: sample_state_try's draws, x and y over the rectangle spanned by
+// s_from and s_to, the heading atan2(to - from) when speed_direction
+template <class ZT>
+__device__ __forceinline__ void sample_state_direction_try(const TerrainView<ZT> &T,
+                                                           const double *s_from, const double *s_to,
+                                                           int speed_direction, uint64_t seed,
+                                                           uint64_t stream_id, int64_t index, int k,
+                                                           double *q) {
+  const double x_min = std_min(s_from[0], s_to[0]), x_max = std_max(s_from[0], s_to[0]);
+  const double y_min = std_min(s_from[1], s_to[1]), y_max = std_max(s_from[1], s_to[1]);
+  const double z_min_rel = H_MIN + ROBOT_H, z_max_rel = H_MAX + ROBOT_H;
+  const double mean = 0.5 * (z_max_rel + z_min_rel);
+  const double sd = (z_max_rel - z_min_rel) * (1.0 / (2 * 3.0));
+  double u00, u01, u10, u11, u20, u21, u30, u31;
+  uniform2(seed, stream_id, PURPOSE_STATE, index, 4u * k + 0, u00, u01);
+  uniform2(seed, stream_id, PURPOSE_STATE, index, 4u * k + 1, u10, u11);
+  uniform2(seed, stream_id, PURPOSE_STATE, index, 4u * k + 2, u20, u21);
+  uniform2(seed, stream_id, PURPOSE_STATE, index, 4u * k + 3, u30, u31);
+  double z0, z1;
+  box_muller(u10, u11, z0, z1);
+  const double hz = z0 * sd + mean;
+  q[0] = (x_max - x_min) * u00 + x_min;
+  q[1] = (y_max - y_min) * u01 + y_min;
+  double g;
+  bool near = false;
+  if (!height_at(T, q[0], q[1], g, near)) g = __builtin_nan("");
+  q[2] = std_max(std_min(hz, z_max_rel), z_min_rel) + g;
+  const double phi = speed_direction ? atan2(s_to[1] - s_from[1], s_to[0] - s_from[0])
+                                     : (2.0 * MY_PI) * u20;
+  const double cos_theta = 2.0 * u21 - 1.0;
+  const double theta = acos(cos_theta);
+  const double v = u30 * V_MAX;
+  q[3] = v * sin(theta) * cos(phi);
+  q[4] = v * sin(theta) * sin(phi);
+  q[5] = v * cos(theta);
+  q[6] = 2 * P_MAX * u31 - P_MAX;
+  q[7] = 0.0;
+}
+
+// PlannerClass::randomState(terrain, flag, p, speed_direction_flag, s_from, s_to)
+// (planner_class.cpp:22-35), try k: the coin is draw k of its purpose
+template <class ZT>
+__device__ __forceinline__ void sample_state_cfg_try(const TerrainView<ZT> &T, const gbp_sampling &cfg,
+                                                     const double *s_from, const double *s_to,
+                                                     uint64_t seed, uint64_t stream_id,
+                                                     int64_t index, int k, double *q) {
+  if (cfg.state_flag && coin(seed, stream_id, index, (uint32_t)k, cfg.state_p))
+    sample_state_direction_try(T, s_from, s_to, cfg.state_speed_direction, seed, stream_id, index,
+                               k, q);
+  else
+    sample_state_try(T, seed, stream_id, index, k, q);
 }
 
 }  // namespace gbp

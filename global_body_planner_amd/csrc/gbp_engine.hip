@@ -331,17 +331,23 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
 // ============================================================================
 // K3: samplers and the batched extend
 // ============================================================================
+// s_from / s_to of the direction-biased draws (rrt_connect.cpp:248-252)
+struct DirPair {
+  double from[8], to[8];
+};
+
 template <class ZT>
 __global__ void k_sample_states(TerrainView<ZT> T, int64_t n, uint64_t seed, uint64_t stream_id,
                                 int64_t index_base, int require_phase, int max_tries,
-                                double *__restrict__ states, int32_t *__restrict__ tries) {
+                                double *__restrict__ states, int32_t *__restrict__ tries,
+                                gbp_sampling cfg, DirPair dp) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     double q[8];
     int got = -1;
     const int mt = max_tries > 0 ? max_tries : 1;
     for (int k = 0; k < mt; k++) {
-      sample_state_try(T, seed, stream_id, index_base + i, k, q);
+      sample_state_cfg_try(T, cfg, dp.from, dp.to, seed, stream_id, index_base + i, k, q);
       if (require_phase < 0) { got = k + 1; break; }
       Acc acc{0, 0, 0};
       if (is_valid_state(T, q, require_phase, acc)) { got = k + 1; break; }
@@ -365,14 +371,33 @@ __global__ void k_sample_actions(int64_t n, const double *__restrict__ normals, 
   }
 }
 
+// getRandomAction(surf_norm, direction, flag, p, s, s_near) for n draws
+// (gbp_sample_actions_dir_dev)
+__global__ void k_sample_actions_dir(int64_t n, const double *__restrict__ normals,
+                                     const double *__restrict__ s, const double *__restrict__ s_near,
+                                     const uint8_t *__restrict__ dir, int dir_all, gbp_sampling cfg,
+                                     uint64_t seed, uint64_t stream_id, int64_t index_base,
+                                     double *__restrict__ actions) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const double nv[3] = {normals[3 * i], normals[3 * i + 1], normals[3 * i + 2]};
+    double a[10];
+    sample_action_cfg(nv, cfg, dir ? dir[i] : dir_all, s + 8 * i, s_near + 8 * i, seed, stream_id,
+                      index_base + i, a);
+#pragma unroll
+    for (int k = 0; k < 10; k++) actions[10 * i + k] = a[k];
+  }
+}
+
 // one thread per (extend i, candidate j): candidate action j of extend i is
-// getRandomAction(getSurfaceNormal(target_i)) from stream (seed, EXTD, (base+i)*8+j)
+// getRandomAction(getSurfaceNormal(target_i), direction, flag, p, target_i,
+// s_near_i) (rrt.cpp:34, :49) from stream (seed, EXTD, (base+i)*8+j)
 template <class ZT>
 __global__ void k_extend_prep(TerrainView<ZT> T, int64_t n, const double *__restrict__ s_near,
                               const double *__restrict__ target, const uint8_t *__restrict__ dir,
                               int dir_all, uint64_t seed, int64_t extend_base,
                               double *__restrict__ cand_s, double *__restrict__ cand_a,
-                              uint8_t *__restrict__ cand_dir) {
+                              uint8_t *__restrict__ cand_dir, gbp_sampling cfg) {
   const int64_t m = n * GBP_NUM_GEN_STATES;
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < m;
        c += (int64_t)gridDim.x * blockDim.x) {
@@ -381,12 +406,14 @@ __global__ void k_extend_prep(TerrainView<ZT> T, int64_t n, const double *__rest
     double nv[3];
     surface_normal(T, target[8 * i], target[8 * i + 1], nv);  // rrt.cpp:25
     double a[10];
-    sample_action(nv, seed, EXTEND_STREAM, (extend_base + i) * 8 + j, a);
+    const int d = dir ? dir[i] : dir_all;
+    sample_action_cfg(nv, cfg, d, target + 8 * i, s_near + 8 * i, seed, EXTEND_STREAM,
+                      (extend_base + i) * 8 + j, a);
 #pragma unroll
     for (int k = 0; k < 10; k++) cand_a[10 * c + k] = a[k];
 #pragma unroll
     for (int k = 0; k < 8; k++) cand_s[8 * c + k] = s_near[8 * i + k];
-    cand_dir[c] = dir ? dir[i] : (uint8_t)dir_all;
+    cand_dir[c] = (uint8_t)d;
   }
 }
 
@@ -1009,6 +1036,10 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
     case GBP_OPT_FAST_RCP:
       t->opt_fast_rcp = value ? 1 : 0;
       return GBP_OK;
+    case GBP_OPT_FRAGILE_EPS:  // in 1e-15 units; never below the default margin
+      if (value < 1000 || value > 1000000000000000LL) return GBP_E_INVALID_ARG;
+      t->fragile_eps = (double)value * 1e-15;
+      return GBP_OK;
     default:
       return GBP_E_INVALID_ARG;
   }
@@ -1026,6 +1057,7 @@ int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value) {
     case GBP_OPT_AFFINE_COORDS: *value = t->opt_affine; return GBP_OK;
     case GBP_OPT_XCD_MAP: *value = t->opt_xcd_map; return GBP_OK;
     case GBP_OPT_FAST_RCP: *value = t->opt_fast_rcp ? (t->rcp_seed != 0.0 ? 1 : 0) : 0; return GBP_OK;
+    case GBP_OPT_FRAGILE_EPS: *value = (int64_t)std::llround(t->fragile_eps * 1e15); return GBP_OK;
     case GBP_OPT_COORD_MODE:  // what the validate kernel of the current options uses
       *value = validate_coord_mode(t, t->opt_kernel == GBP_KERNEL_DIRECT);
       return GBP_OK;
@@ -1119,22 +1151,82 @@ int gbp_validate_pairs_dev(gbp_terrain *t, int64_t n, const double *s, const dou
 }
 
 // ---- K3 ---------------------------------------------------------------------
+namespace {
+int launch_sample_states(gbp_terrain *t, int64_t n, uint64_t seed, uint64_t stream_id,
+                         int64_t index_base, int require_phase, int max_tries, double *states,
+                         int32_t *tries, const gbp_sampling &cfg, const DirPair &dp,
+                         gbp_stream stream) {
+  DeviceGuard g(t->device);
+  const unsigned grid = grid_for(n, 256, t->num_cus * 16);
+  if (t->storage == GBP_STORAGE_F32)
+    hipLaunchKernelGGL(k_sample_states<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       view<float>(t), n, seed, stream_id, index_base, require_phase, max_tries,
+                       states, tries, cfg, dp);
+  else
+    hipLaunchKernelGGL(k_sample_states<double>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       view<double>(t), n, seed, stream_id, index_base, require_phase, max_tries,
+                       states, tries, cfg, dp);
+  HIPCHK(hipGetLastError());
+  return GBP_OK;
+}
+
+bool sampling_ok(const gbp_sampling &c) {
+  return !(c.state_flag && std::isnan(c.state_p)) && !(c.action_flag && std::isnan(c.action_p));
+}
+}  // namespace
+
 int gbp_sample_states_dev(gbp_terrain *t, int64_t n, uint64_t seed, uint64_t stream_id,
                           int64_t index_base, int require_phase, int max_tries, double *states,
                           int32_t *tries, gbp_stream stream) {
   if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
   if (n < 0 || (n > 0 && !states)) return GBP_E_INVALID_ARG;
   if (n == 0) return GBP_OK;
+  return launch_sample_states(t, n, seed, stream_id, index_base, require_phase, max_tries, states,
+                              tries, gbp_sampling{}, DirPair{}, stream);
+}
+
+int gbp_terrain_set_sampling(gbp_terrain *t, const gbp_sampling *cfg) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (cfg && !sampling_ok(*cfg)) return GBP_E_INVALID_ARG;
+  t->sampling = cfg ? *cfg : gbp_sampling{};
+  return GBP_OK;
+}
+
+int gbp_terrain_get_sampling(const gbp_terrain *t, gbp_sampling *cfg) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (!cfg) return GBP_E_INVALID_ARG;
+  *cfg = t->sampling;
+  return GBP_OK;
+}
+
+int gbp_sample_states_dir_dev(gbp_terrain *t, int64_t n, uint64_t seed, uint64_t stream_id,
+                              int64_t index_base, const gbp_sampling *cfg, const double *s_from,
+                              const double *s_to, double *states, gbp_stream stream) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || (n > 0 && (!states || !s_from || !s_to))) return GBP_E_INVALID_ARG;
+  if (cfg && !sampling_ok(*cfg)) return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  DirPair dp;
+  memcpy(dp.from, s_from, sizeof dp.from);
+  memcpy(dp.to, s_to, sizeof dp.to);
+  return launch_sample_states(t, n, seed, stream_id, index_base, -1, 1, states, nullptr,
+                              cfg ? *cfg : t->sampling, dp, stream);
+}
+
+int gbp_sample_actions_dir_dev(gbp_terrain *t, int64_t n, const double *normals, const double *s,
+                               const double *s_near, const uint8_t *direction, int direction_all,
+                               const gbp_sampling *cfg, uint64_t seed, uint64_t stream_id,
+                               int64_t index_base, double *actions, gbp_stream stream) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n < 0 || (n > 0 && (!normals || !s || !s_near || !actions))) return GBP_E_INVALID_ARG;
+  if (!direction && direction_all != GBP_FORWARD && direction_all != GBP_REVERSE)
+    return GBP_E_INVALID_ARG;
+  if (cfg && !sampling_ok(*cfg)) return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
   DeviceGuard g(t->device);
-  const unsigned grid = grid_for(n, 256, t->num_cus * 16);
-  if (t->storage == GBP_STORAGE_F32)
-    hipLaunchKernelGGL(k_sample_states<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                       view<float>(t), n, seed, stream_id, index_base, require_phase, max_tries,
-                       states, tries);
-  else
-    hipLaunchKernelGGL(k_sample_states<double>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                       view<double>(t), n, seed, stream_id, index_base, require_phase, max_tries,
-                       states, tries);
+  hipLaunchKernelGGL(k_sample_actions_dir, dim3(grid_for(n, 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, n, normals, s, s_near, direction, direction_all,
+                     cfg ? *cfg : t->sampling, seed, stream_id, index_base, actions);
   HIPCHK(hipGetLastError());
   return GBP_OK;
 }
@@ -1184,10 +1276,12 @@ int gbp_extend_batch_dev(gbp_terrain *t, int64_t n, const double *s_near, const 
   const unsigned grid = grid_for(m, 256, t->num_cus * 16);
   if (t->storage == GBP_STORAGE_F32)
     hipLaunchKernelGGL(k_extend_prep<float>, dim3(grid), dim3(256), 0, st, view<float>(t), n,
-                       s_near, target, direction, direction_all, seed, extend_base, cs, ca, cd);
+                       s_near, target, direction, direction_all, seed, extend_base, cs, ca, cd,
+                       t->sampling);
   else
     hipLaunchKernelGGL(k_extend_prep<double>, dim3(grid), dim3(256), 0, st, view<double>(t), n,
-                       s_near, target, direction, direction_all, seed, extend_base, cs, ca, cd);
+                       s_near, target, direction, direction_all, seed, extend_base, cs, ca, cd,
+                       t->sampling);
   HIPCHK(hipGetLastError());
   rc = gbp_validate_pairs_dev(t, m, cs, ca, cd, 0, adaptive, nullptr, csn, nullptr, cf, cc,
                               stream);
@@ -1424,6 +1518,52 @@ int gbp_sample_states_host(gbp_terrain *t, int64_t n, uint64_t seed, uint64_t st
   return GBP_OK;
 }
 
+int gbp_sample_states_dir_host(gbp_terrain *t, int64_t n, uint64_t seed, uint64_t stream_id,
+                               int64_t index_base, const gbp_sampling *cfg, const double *s_from,
+                               const double *s_to, double *states) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n <= 0) return n == 0 ? GBP_OK : GBP_E_INVALID_ARG;
+  if (!states || !s_from || !s_to) return GBP_E_INVALID_ARG;
+  DeviceGuard g(t->device);
+  hipStream_t st = t->host_stream;
+  int rc = ensure_ws(&t->ws, &t->ws_bytes, rnd(64 * n) + 1024);
+  if (rc) return rc;
+  Stage S{t, (char *)t->ws};
+  double *ds = S.take<double>(8 * n);
+  rc = gbp_sample_states_dir_dev(t, n, seed, stream_id, index_base, cfg, s_from, s_to, ds, st);
+  if (rc) return rc;
+  D2H(states, ds, 64 * n);
+  HIPCHK(hipStreamSynchronize(st));
+  return GBP_OK;
+}
+
+int gbp_sample_actions_dir_host(gbp_terrain *t, int64_t n, const double *normals, const double *s,
+                                const double *s_near, const uint8_t *direction, int direction_all,
+                                const gbp_sampling *cfg, uint64_t seed, uint64_t stream_id,
+                                int64_t index_base, double *actions) {
+  if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
+  if (n <= 0) return n == 0 ? GBP_OK : GBP_E_INVALID_ARG;
+  if (!normals || !s || !s_near || !actions) return GBP_E_INVALID_ARG;
+  DeviceGuard g(t->device);
+  hipStream_t st = t->host_stream;
+  int rc = ensure_ws(&t->ws, &t->ws_bytes, rnd(24 * n) + 2 * rnd(64 * n) + rnd(n) + rnd(80 * n) + 2048);
+  if (rc) return rc;
+  Stage S{t, (char *)t->ws};
+  double *dn = S.take<double>(3 * n), *ds = S.take<double>(8 * n), *dsn = S.take<double>(8 * n);
+  uint8_t *dd = S.take<uint8_t>(n);
+  double *da = S.take<double>(10 * n);
+  H2D(dn, normals, 24 * n);
+  H2D(ds, s, 64 * n);
+  H2D(dsn, s_near, 64 * n);
+  if (direction) H2D(dd, direction, n);
+  rc = gbp_sample_actions_dir_dev(t, n, dn, ds, dsn, direction ? dd : nullptr, direction_all, cfg,
+                                  seed, stream_id, index_base, da, st);
+  if (rc) return rc;
+  D2H(actions, da, 80 * n);
+  HIPCHK(hipStreamSynchronize(st));
+  return GBP_OK;
+}
+
 int gbp_sample_actions_host(gbp_terrain *t, int64_t n, const double *normals, uint64_t seed,
                             uint64_t stream_id, int64_t index_base, double *actions) {
   if (!valid_handle(t)) return GBP_E_BAD_HANDLE;
@@ -1566,13 +1706,19 @@ int gbp_extend_resolve_host(gbp_terrain *t, int64_t n, const double *s_near, con
     if (!(flags[i] & GBP_F_FRAGILE)) continue;
     const double *tg = target + 8 * i, *sn0 = s_near + 8 * i;
     double nrm[3 * GBP_NUM_GEN_STATES], act[10 * GBP_NUM_GEN_STATES];
+    double tgs[8 * GBP_NUM_GEN_STATES], sns[8 * GBP_NUM_GEN_STATES];
     int rc = gbp_normal_batch_host(t, 1, tg, nrm, nullptr);  // rrt.cpp:25 (k_extend_prep)
     if (rc) return rc;
-    for (int j = 1; j < GBP_NUM_GEN_STATES; j++) memcpy(nrm + 3 * j, nrm, 3 * sizeof(double));
-    rc = gbp_sample_actions_host(t, GBP_NUM_GEN_STATES, nrm, seed, EXTEND_STREAM,
-                                 (extend_base + i) * 8, act);
-    if (rc) return rc;
+    for (int j = 0; j < GBP_NUM_GEN_STATES; j++) {
+      if (j) memcpy(nrm + 3 * j, nrm, 3 * sizeof(double));
+      memcpy(tgs + 8 * j, tg, 8 * sizeof(double));
+      memcpy(sns + 8 * j, sn0, 8 * sizeof(double));
+    }
     const int d = direction ? direction[i] : direction_all;
+    // the candidates k_extend_prep drew (the handle's sampling configuration)
+    rc = gbp_sample_actions_dir_host(t, GBP_NUM_GEN_STATES, nrm, tgs, sns, nullptr, d, nullptr,
+                                     seed, EXTEND_STREAM, (extend_base + i) * 8, act);
+    if (rc) return rc;
     const double best0 = gbp_host::state_distance(sn0, tg);
     double best = best0, s_test[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_test = 0;
     uint32_t G = 0, V = 0, ef = 0;

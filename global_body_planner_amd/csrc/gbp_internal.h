@@ -37,7 +37,9 @@ struct gbp_terrain {
   int64_t opt_affine = 1;           // compute coordinates when the affine form is exact
   int64_t opt_fast_rcp = 1;         // cell-area reciprocal by verified Newton steps
   double rcp_seed = 0;              // verified_rcp_seed (0: every spacing pair not exact)
+  double fragile_eps = gbp::FRAGILE_EPS;  // GBP_OPT_FRAGILE_EPS (>= the default)
   int64_t opt_xcd_map = 0;          // persistent kernel: slices numbered XCD-major
+  gbp_sampling sampling{};          // direction-biased sampling (gbp_terrain_set_sampling), off
   int affine = 0;                   // host-verified affine coordinates (both axes)
   int bx = 0, by = 0;
   double ax = 0, hx = 0, ay = 0, hy = 0;
@@ -99,6 +101,7 @@ inline gbp::TerrainView<ZT> view(const gbp_terrain *t) {
   v.ay = t->ay;
   v.hy = t->hy;
   v.rcp_seed = t->opt_fast_rcp ? t->rcp_seed : 0.0;
+  v.feps = t->fragile_eps;
   return v;
 }
 

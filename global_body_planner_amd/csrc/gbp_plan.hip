@@ -76,6 +76,7 @@ struct gbp_plan_ws {
   gbp_plan_status *st = nullptr;
   unsigned long long *tiles = nullptr;  // look-back tile states
   uint32_t epoch = 0;          // per-compaction tag of the tile states
+  uint64_t seq = 0;            // launch sequence number of the planner kernels (gated())
   int64_t ntiles = 0;
   // stage 0-1
   double *cand = nullptr;      // [bmax][8] drawn states
@@ -115,9 +116,17 @@ constexpr int NN_MAX_CHUNKS = 32;  // partial slots per query at the largest bat
 constexpr uint32_t LOOKBACK_SPIN_LIMIT = 1u << 24;
 
 // the gate every planner kernel checks first: a FRAGILE halt or a found
-// connection makes the rest of the enqueued sequence a no-op
-__device__ __forceinline__ bool gated(const gbp_plan_status *st) {
-  return (st->halt | st->done) != 0u;
+// connection raised by an EARLIER launch makes the rest of the enqueued
+// sequence a no-op.  Each launch carries its sequence number `seq`
+// (gbp_plan_ws::seq); the launch that raises the gate records its own
+// (gate_seq, atomicMin), so a workgroup dispatched after another workgroup of
+// the same launch raised it still computes its items — the host's
+// resolution and resume rely on every item of the halted stage being final.
+__device__ __forceinline__ bool gated(const gbp_plan_status *st, uint64_t seq) {
+  return __hip_atomic_load(&st->gate_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < seq;
+}
+__device__ __forceinline__ void raise_gate(gbp_plan_status *st, uint64_t seq) {
+  atomicMin((unsigned long long *)&st->gate_seq, (unsigned long long)seq);
 }
 
 __device__ __forceinline__ double pose_distance(const double *q1, const double *q2) {
@@ -204,13 +213,24 @@ template <class ZT>
 __global__ __launch_bounds__(TB) void k_targets(TerrainView<ZT> T, gbp_plan_status *st, int64_t n,
                                                 uint64_t seed, uint64_t stream_id, int64_t base,
                                                 double *__restrict__ cand,
-                                                uint32_t *__restrict__ cflag, int32_t half) {
-  if (gated(st)) return;
+                                                uint32_t *__restrict__ cflag, int32_t half,
+                                                uint64_t seq, gbp_sampling cfg,
+                                                const double *__restrict__ tv,
+                                                const int32_t *__restrict__ tcount,
+                                                const double *__restrict__ ov, int direction) {
+  if (gated(st, seq)) return;
+  // direction-biased draws (rrt_connect.cpp:248-252, :283-287): s_from / s_to
+  // are T's last vertex and O's root (FORWARD half, T = Ta), or O's root and
+  // T's last vertex (REVERSE half, T = Tb), as the trees stand when the half
+  // starts (the batch-synchronous snapshot; batch 1 is the reference's loop)
+  const double *t_last = tv + 8 * (int64_t)(*tcount - 1);
+  const double *s_from = direction == GBP_FORWARD ? t_last : ov;
+  const double *s_to = direction == GBP_FORWARD ? ov : t_last;
   bool frag = false;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     double q[8];
-    sample_state_try(T, seed, stream_id, base + i, 0, q);  // randomState, one try
+    sample_state_cfg_try(T, cfg, s_from, s_to, seed, stream_id, base + i, 0, q);  // randomState
     Acc acc{0, 0, 0};
     const bool v = is_valid_state(T, q, GBP_STANCE, acc);   // rrt_connect.cpp:254
     copy8(cand + 8 * i, q);
@@ -220,6 +240,7 @@ __global__ __launch_bounds__(TB) void k_targets(TerrainView<ZT> T, gbp_plan_stat
   if (__ballot(frag) && (threadIdx.x & (WAVE - 1)) == 0) {
     atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_TARGETS);
     st->halt_half = half;
+    raise_gate(st, seq);
   }
 }
 
@@ -227,8 +248,9 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
                                                         const double *__restrict__ cand,
                                                         const uint32_t *__restrict__ cflag,
                                                         double *__restrict__ targets,
-                                                        unsigned long long *tiles, uint32_t epoch) {
-  if (gated(st)) return;
+                                                        unsigned long long *tiles, uint32_t epoch,
+                                                        uint64_t seq) {
+  if (gated(st, seq)) return;
   const int64_t i = blockIdx.x * (int64_t)CB + threadIdx.x;
   const bool keep = i < n && (cflag[i] & GBP_F_VALID);
   const uint32_t r = ordered_rank(keep, tiles, epoch, &st->n_targets, st);
@@ -476,8 +498,8 @@ __global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restr
                                                   const float *__restrict__ vmax,
                                                   const int32_t *__restrict__ nv_dev, int64_t bmax,
                                                   int items, double *__restrict__ pd,
-                                                  int32_t *__restrict__ pi) {
-  if (gated(st)) return;
+                                                  int32_t *__restrict__ pi, uint64_t seq) {
+  if (gated(st, seq)) return;
   __shared__ int32_t cand[QPL][NN_CAND][TB];
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   int64_t ch, nch;
@@ -568,8 +590,8 @@ __global__ __launch_bounds__(TB) void k_nn_reduce(const gbp_plan_status *st, con
                                                   const int32_t *nv_dev, int64_t bmax, int qts, int items,
                                                   const double *__restrict__ pd,
                                                   const int32_t *__restrict__ pi,
-                                                  int32_t *__restrict__ out) {
-  if (gated(st)) return;
+                                                  int32_t *__restrict__ out, uint64_t seq) {
+  if (gated(st, seq)) return;
   const int64_t nq = *nq_dev, nv = *nv_dev;
   int64_t ch, nch;
   nn_geometry(nq, nv, bmax, qts, items, ch, nch);
@@ -639,8 +661,9 @@ __global__ __launch_bounds__(TB) void k_extend_prep(TerrainView<ZT> T, gbp_plan_
                                                     const int32_t *__restrict__ nn,
                                                     const double *__restrict__ tv, uint64_t seed,
                                                     double *__restrict__ cs,
-                                                    double *__restrict__ ca) {
-  if (gated(st)) {
+                                                    double *__restrict__ ca, uint64_t seq,
+                                                    gbp_sampling cfg, int direction) {
+  if (gated(st, seq)) {
     if (blockIdx.x == 0 && threadIdx.x == 0) st->n_validate = 0;  // the validate launch idles
     return;
   }
@@ -653,7 +676,8 @@ __global__ __launch_bounds__(TB) void k_extend_prep(TerrainView<ZT> T, gbp_plan_
     double nv[3];
     surface_normal(T, targets[8 * i], targets[8 * i + 1], nv);  // rrt.cpp:25
     double a[10];
-    sample_action(nv, seed, GBP_EXTEND_STREAM, (base + i) * 8 + j, a);  // rrt.cpp:34, :49
+    sample_action_cfg(nv, cfg, direction, targets + 8 * i, tv + 8 * (int64_t)nn[i], seed,
+                      GBP_EXTEND_STREAM, (base + i) * 8 + j, a);  // rrt.cpp:34, :49
     copy10(ca + 10 * c, a);
     copy8(cs + 8 * c, tv + 8 * (int64_t)nn[i]);
   }
@@ -670,8 +694,9 @@ __global__ __launch_bounds__(TB) void k_select(gbp_plan_status *st, const double
                                                int32_t *__restrict__ eres,
                                                int32_t *__restrict__ echo,
                                                double *__restrict__ esn, double *__restrict__ ean,
-                                               uint32_t *__restrict__ ef, int32_t half) {
-  if (gated(st)) return;
+                                               uint32_t *__restrict__ ef, int32_t half,
+                                               uint64_t seq) {
+  if (gated(st, seq)) return;
   const int64_t n = st->n_targets;
   bool frag = false;
   unsigned long long executed = 0;
@@ -717,6 +742,7 @@ __global__ __launch_bounds__(TB) void k_select(gbp_plan_status *st, const double
   if (__ballot(frag) && lane == 0) {
     atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_EXTEND);
     st->halt_half = half;
+    raise_gate(st, seq);
   }
 }
 
@@ -741,8 +767,9 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
                                                double *__restrict__ ta, double *__restrict__ tg,
                                                int32_t *__restrict__ tp, int32_t *__restrict__ tcount,
                                                int32_t *__restrict__ vtx, unsigned long long *tiles,
-                                               uint32_t epoch, int32_t half) {
-  if (gated(st)) return;
+                                               uint32_t epoch, int32_t half, int64_t cap,
+                                               uint64_t seq) {
+  if (gated(st, seq)) return;
   __shared__ int32_t s_base;
   if (threadIdx.x == 0) s_base = *tcount;  // read before this block publishes its count
   __syncthreads();
@@ -754,7 +781,10 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
   const bool keep = live && r != GBP_TRAPPED;
   int32_t *total = mode == 0 ? &st->n_added : &st->n_conn_added;
   const uint32_t rank = ordered_rank(keep, tiles, epoch, total, st);
-  if (keep) {
+  if (keep && (int64_t)base + rank >= cap) {  // the caller reserved too little: drop, report
+    atomicOr(&st->error, 2u);
+    if (vtx) vtx[i] = -1;
+  } else if (keep) {
     const int32_t idx = base + (int32_t)rank, p = par[i];
     double s[8], pv[8];
     copy8(s, sn + 8 * i);
@@ -772,13 +802,14 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
                 ((unsigned long long)i << 32) | (unsigned long long)(uint32_t)idx);
       st->meet_half = half;
       atomicOr(&st->done, 1u);
+      raise_gate(st, seq);
     }
   } else if (live && vtx) {
     vtx[i] = -1;
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
     const int32_t added = *total;
-    *tcount = base + added;
+    *tcount = (int32_t)min<int64_t>((int64_t)base + added, cap);
     if (mode == 0) {
       st->added_base = base;
       st->stat_added += added;
@@ -891,8 +922,9 @@ __global__ __launch_bounds__(TB) void k_connect(TerrainView<ZT> T, gbp_plan_stat
                                                 int32_t *__restrict__ kres,
                                                 double *__restrict__ ksn,
                                                 double *__restrict__ kan,
-                                                uint32_t *__restrict__ kf, int32_t half) {
-  if (gated(st)) return;
+                                                uint32_t *__restrict__ kf, int32_t half,
+                                                uint64_t seq) {
+  if (gated(st, seq)) return;
   const int64_t n = st->n_added, base = st->added_base;
   const int lane = threadIdx.x & (WAVE - 1);
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x / WAVE);
@@ -946,6 +978,7 @@ __global__ __launch_bounds__(TB) void k_connect(TerrainView<ZT> T, gbp_plan_stat
     if (frag) {
       atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_CONNECT);
       st->halt_half = half;
+      raise_gate(st, seq);
     }
   }
 }
@@ -985,6 +1018,7 @@ __global__ void k_plan_reset(gbp_plan_status *st, int64_t ext_counter) {
   gbp_plan_status z;
   memset(&z, 0, sizeof z);
   z.meet = ~0ull;
+  z.gate_seq = ~0ull;
   z.halt_half = -1;
   z.meet_half = -1;
   z.ext_counter = ext_counter;
@@ -999,6 +1033,7 @@ __global__ void k_extend_setup(gbp_plan_status *st, int64_t n, const int32_t *n_
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st->halt = 0;
     st->done = 0;
+    st->gate_seq = ~0ull;
     st->n_targets = (int32_t)m;
     st->ext_base = extend_base;
   }
@@ -1010,6 +1045,7 @@ __global__ void k_extend_setup(gbp_plan_status *st, int64_t n, const int32_t *n_
 __global__ void k_set_queries(gbp_plan_status *st, int32_t n) {
   st->halt = 0;
   st->done = 0;
+  st->gate_seq = ~0ull;
   st->n_targets = n;
 }
 
@@ -1047,9 +1083,10 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
   // per CU on trees past ~20k vertices (profiles/r02j_nn_dot.txt)
   constexpr int QPL = 2, items = 2048;  // (query tile, chunk) items per call, nn_geometry
   hipLaunchKernelGGL((k_nn_filter<4, QPL>), dim3(num_cus * 8), dim3(TB), 0, s, w->st, nq_dev, q,
-                     q_off_dev, tr->v, tr->vf, tr->vmax, tr->count, w->bmax, items, w->nn_d, w->nn_i);
+                     q_off_dev, tr->v, tr->vf, tr->vmax, tr->count, w->bmax, items, w->nn_d, w->nn_i,
+                     ++w->seq);
   hipLaunchKernelGGL(k_nn_reduce, dim3(grid_for(w->bmax, TB, num_cus * 4)), dim3(TB), 0, s, w->st,
-                     nq_dev, tr->count, w->bmax, TB * QPL, items, w->nn_d, w->nn_i, out);
+                     nq_dev, tr->count, w->bmax, TB * QPL, items, w->nn_d, w->nn_i, out, ++w->seq);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
 
@@ -1063,27 +1100,29 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   gbp_plan_status *st = w->st;
   if (first_stage <= 0 && last_stage >= 0)
     hipLaunchKernelGGL(k_targets<ZT>, dim3(grid_for(batch, TB, cus * 8)), dim3(TB), 0, s, V, st,
-                       batch, seed, target_stream, target_base, w->cand, w->cflag, half);
+                       batch, seed, target_stream, target_base, w->cand, w->cflag, half, ++w->seq,
+                       t->sampling, T->v, T->count, O ? O->v : T->v, direction);
   if (first_stage <= 1 && last_stage >= 1)
     hipLaunchKernelGGL(k_compact_targets, dim3(tiles_for(batch)), dim3(CB), 0, s, st, batch,
-                       w->cand, w->cflag, w->targets, w->tiles, next_epoch(w));
+                       w->cand, w->cflag, w->targets, w->tiles, next_epoch(w), ++w->seq);
   if (first_stage <= 2 && last_stage >= 2) {
     int rc = nn_launch(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s);
     if (rc) return rc;
     const int64_t mmax = batch * GBP_NUM_GEN_STATES;
     hipLaunchKernelGGL(k_extend_prep<ZT>, dim3(grid_for(mmax, TB, cus * 8)), dim3(TB), 0, s, V, st,
-                       w->targets, w->nn, T->v, seed, w->cs, w->ca);
+                       w->targets, w->nn, T->v, seed, w->cs, w->ca, ++w->seq, t->sampling,
+                       direction);
     rc = gbp_internal_validate_dev_n(t, mmax, &st->n_validate, w->cs, w->ca, nullptr, direction,
                                      adaptive, nullptr, w->csn, nullptr, w->cf, w->cc, s);
     if (rc) return rc;
     hipLaunchKernelGGL(k_select, dim3(grid_for(batch, TB, cus * 4)), dim3(TB), 0, s, st, w->targets,
                        w->nn, T->v, w->ca, w->csn, w->cf, w->eres, w->echo, w->esn, w->ean, w->ef,
-                       half);
+                       half, ++w->seq);
   }
   if (first_stage <= 3 && last_stage >= 3)
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 0, w->eres, w->nn,
                        w->esn, w->ean, T->v, T->vf, T->vmax, T->a, T->g, T->parent, T->count, w->evtx, w->tiles,
-                       next_epoch(w), half);
+                       next_epoch(w), half, T->cap, ++w->seq);
   if (!O) return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   const int cdir = direction == GBP_FORWARD ? GBP_REVERSE : GBP_FORWARD;
   if (first_stage <= 4 && last_stage >= 4) {
@@ -1092,9 +1131,10 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     if (rc) return rc;
     const int cm = (t->opt_affine && t->affine) ? 2 : 0;
     const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * 4, (batch + 3) / 4));
+    const uint64_t kseq = ++w->seq;
 #define GBP_KC(AD, CM)                                                                         \
   hipLaunchKernelGGL((k_connect<ZT, AD, CM>), dim3(g), dim3(TB), 0, s, V, st, cdir, T->v, O->v, \
-                     w->nno, w->kres, w->ksn, w->kan, w->kf, half)
+                     w->nno, w->kres, w->ksn, w->kan, w->kf, half, kseq)
     if (adaptive) {
       if (cm == 2) GBP_KC(true, 2); else GBP_KC(true, 0);
     } else {
@@ -1105,7 +1145,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   if (first_stage <= 5 && last_stage >= 5)
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 1, w->kres, w->nno,
                        w->ksn, w->kan, O->v, O->vf, O->vmax, O->a, O->g, O->parent, O->count, nullptr, w->tiles,
-                       next_epoch(w), half);
+                       next_epoch(w), half, O->cap, ++w->seq);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
 
@@ -1638,6 +1678,7 @@ int gbp_plan_resolve_host(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree 
   }
   if (*resume_stage >= 0) {
     st.halt = 0;
+    if (!st.done) st.gate_seq = ~0ull;
     st.stat_fragile_resolved += k;
     if ((rc = h2d(w->st, &st, 1, s))) return rc;
     HIPCHK_P(hipStreamSynchronize(s));

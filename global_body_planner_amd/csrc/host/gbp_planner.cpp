@@ -441,10 +441,49 @@ void isValidStateActionPairBatch(const std::vector<State> &s, const std::vector<
   if (flags) flags->swap(f);
 }
 
-Action getRandomAction(std::array<double, 3> surf_norm) {
-  throw std::logic_error("getRandomAction(surf_norm) needs a terrain handle: use "
-                         "RRTClass::newConfig (engine-sampled candidates)");
-  (void)surf_norm;
+// The free samplers draw from their own counter stream on a minimal engine
+// handle of device 0 (the sampler reads no terrain; the handle carries the
+// stream's workspace).  It lives as long as the thread's process: it is not
+// destroyed at exit, where the HIP runtime may already be gone.
+static constexpr uint64_t FREE_ACTION_STREAM = 0x46524545ull;  // "FREE"
+
+static Action free_action(const std::array<double, 3> &n, int direction, const gbp_sampling &cfg,
+                          const State &s, const State &s_near) {
+  static thread_local gbp_terrain *h = nullptr;
+  if (!h) {
+    const double xy[2] = {0.0, 1.0}, z[4] = {0.0, 0.0, 0.0, 0.0};
+    chk(gbp_terrain_create(0, 2, 2, xy, xy, z, nullptr, nullptr, nullptr, GBP_STORAGE_AUTO, &h),
+        "getRandomAction handle");
+  }
+  Action a;
+  chk(gbp_sample_actions_dir_host(h, 1, n.data(), s.data(), s_near.data(), nullptr, direction, &cfg,
+                                  g_seed, FREE_ACTION_STREAM, g_action_draws++, a.data()),
+      "getRandomAction");
+  return a;
+}
+
+Action getRandomAction(std::array<double, 3> surf_norm, int direction,
+                       bool action_direction_sampling_flag,
+                       double action_direction_sampling_probability_threshold, State s,
+                       State s_near) {  // planning_utils.cpp:379-391
+  gbp_sampling cfg{};
+  cfg.action_flag = action_direction_sampling_flag ? 1 : 0;
+  cfg.action_p = action_direction_sampling_probability_threshold;
+  return free_action(surf_norm, direction, cfg, s, s_near);
+}
+
+Action getRandomAction(std::array<double, 3> surf_norm) {  // :392-442
+  const State z{};
+  return free_action(surf_norm, FORWARD, gbp_sampling{}, z, z);
+}
+
+Action getRandomActionDirection(std::array<double, 3> surf_norm, State s_from,
+                                State s_to) {  // :443-515
+  gbp_sampling cfg{};
+  cfg.action_flag = 1;
+  cfg.action_p = 2.0;  // the coin always lands: the direction variant itself
+  // FORWARD draws getRandomActionDirection(surf_norm, s_near, s)
+  return free_action(surf_norm, FORWARD, cfg, s_to, s_from);
 }
 
 void interpStateActionPair(State s, Action a, double t0, double dt, std::vector<State> &path,
@@ -614,6 +653,33 @@ State PlannerClass::randomState(FastTerrainMap &terrain) {  // planner_class.cpp
   return q;
 }
 
+State PlannerClass::randomState(FastTerrainMap &terrain, bool flag, double p,
+                                bool speed_direction_flag, State s_from,
+                                State s_to) {  // planner_class.cpp:22-35
+  gbp_sampling cfg{};
+  cfg.state_flag = flag ? 1 : 0;
+  cfg.state_p = p;
+  cfg.state_speed_direction = speed_direction_flag ? 1 : 0;
+  return randomStateBatch(terrain, 1, cfg, s_from, s_to)[0];
+}
+
+State PlannerClass::randomStateDirection(FastTerrainMap &terrain, State s_from, State s_to,
+                                         bool speed_direction_flag) {  // :82-148
+  return randomState(terrain, true, 2.0, speed_direction_flag, s_from, s_to);  // the coin always lands
+}
+
+std::vector<State> PlannerClass::randomStateBatch(FastTerrainMap &terrain, int n,
+                                                  const gbp_sampling &cfg, const State &s_from,
+                                                  const State &s_to) {
+  std::vector<State> q(n);
+  if (n <= 0) return q;
+  chk(gbp_sample_states_dir_host(terrain.handle(), n, seed_, stream_id_, draws_, &cfg,
+                                 s_from.data(), s_to.data(), q[0].data()),
+      "randomState(direction)");
+  draws_ += n;
+  return q;
+}
+
 std::vector<State> PlannerClass::randomStateBatch(FastTerrainMap &terrain, int n) {
   std::vector<State> q(n);
   if (n <= 0) return q;
@@ -719,10 +785,24 @@ std::vector<int> PlannerClass::neighborhoodN(State q, int N) {  // :151-171
 // ============================================================================
 // RRTClass
 // ============================================================================
+gbp_sampling RRTClass::samplingConfig() const {
+  gbp_sampling c{};
+  c.state_flag = state_direction_sampling_flag_ ? 1 : 0;
+  c.state_speed_direction = state_direction_sampling_speed_direction_flag_ ? 1 : 0;
+  c.state_p = state_direction_sampling_probability_threshold_;
+  c.action_flag = action_direction_sampling_flag_ ? 1 : 0;
+  c.action_p = action_direction_sampling_probability_threshold_;
+  return c;
+}
+
+void RRTClass::applySampling(FastTerrainMap &terrain) const {
+  const gbp_sampling c = samplingConfig();
+  chk(gbp_terrain_set_sampling(terrain.handle(), &c), "direction sampling");
+}
+
 bool RRTClass::newConfig(State s, State s_near, State &s_new, Action &a_new, FastTerrainMap &terrain,
                          int direction) {  // rrt.cpp:20-70 on the engine (6 candidates, one launch)
-  if (action_direction_sampling_flag_ || state_direction_sampling_flag_)
-    throw std::logic_error("direction sampling (planning_utils.cpp:445-515) is not implemented");
+  applySampling(terrain);  // getRandomAction(surf_norm, direction, flag, p, s, s_near): rrt.cpp:34, :49
   int32_t result, chosen;
   uint32_t counts;
   State sn = s_new;
@@ -1034,7 +1114,11 @@ void RRTConnectClass::runRRTConnect(PlannerClass &Ta, PlannerClass &Tb,
       anytime_horizon = anytime_horizon * horizon_expansion_factor;
       return;
     }
-    State s_rand = Ta.randomState(terrain);
+    // direction-biased draws between the trees (rrt_connect.cpp:248-252)
+    State s_from = Ta.getVertex(Ta.getNumVertices() - 1), s_to = Tb.getVertex(0);
+    State s_rand = Ta.randomState(terrain, state_direction_sampling_flag_,
+                                  state_direction_sampling_probability_threshold_,
+                                  state_direction_sampling_speed_direction_flag_, s_from, s_to);
     if (isValidState(s_rand, terrain, STANCE)) {
       if (extend(Ta, s_rand, terrain, FORWARD) != GBP_PLANNER_TRAPPED) {
         const State s_new = Ta.getVertex(Ta.getNumVertices() - 1);
@@ -1045,7 +1129,11 @@ void RRTConnectClass::runRRTConnect(PlannerClass &Ta, PlannerClass &Tb,
         }
       }
     }
-    s_rand = Tb.randomState(terrain);
+    s_from = Ta.getVertex(0);  // :283-287
+    s_to = Tb.getVertex(Tb.getNumVertices() - 1);
+    s_rand = Tb.randomState(terrain, state_direction_sampling_flag_,
+                            state_direction_sampling_probability_threshold_,
+                            state_direction_sampling_speed_direction_flag_, s_from, s_to);
     if (isValidState(s_rand, terrain, STANCE)) {
       if (extend(Tb, s_rand, terrain, REVERSE) != GBP_PLANNER_TRAPPED) {
         const State s_new = Tb.getVertex(Tb.getNumVertices() - 1);
@@ -1171,12 +1259,23 @@ void RRTConnectClass::buildRRTConnect(FastTerrainMap &terrain, State s_start, St
 // connect every new vertex to O (direction of the connect = opposite of dir)
 void RRTConnectClass::extendBatch(PlannerClass &T, FastTerrainMap &terrain, int dir, int batch,
                                   std::vector<int> &added, std::vector<int> &nearest,
-                                  std::vector<Action> &a_out, bool insert, BatchStats *stats) {
+                                  std::vector<Action> &a_out, bool insert, BatchStats *stats,
+                                  const PlannerClass *O) {
   added.clear();
   nearest.clear();
   a_out.clear();
-  // targets: randomState + isValidState(STANCE) (rrt_connect.cpp:249-254)
-  std::vector<State> cand = T.randomStateBatch(terrain, batch);
+  applySampling(terrain);  // newConfig's candidates (rrt.cpp:34, :49)
+  // targets: randomState + isValidState(STANCE) (rrt_connect.cpp:249-254); with
+  // O, the direction-biased draw between T's last vertex and O's root
+  // (FORWARD: T = Ta, :248) or O's root and T's last vertex (REVERSE, :283)
+  std::vector<State> cand;
+  if (O) {
+    const State last = T.getVertex(T.getNumVertices() - 1), root = O->getVertex(0);
+    cand = T.randomStateBatch(terrain, batch, samplingConfig(), dir == FORWARD ? last : root,
+                              dir == FORWARD ? root : last);
+  } else {
+    cand = T.randomStateBatch(terrain, batch);
+  }
   std::vector<uint8_t> ok(batch);
   std::vector<uint32_t> tflags(batch);
   chk(gbp_valid_states_host(terrain.handle(), batch, cand[0].data(), nullptr, STANCE, ok.data(),
@@ -1266,7 +1365,7 @@ int RRTConnectClass::halfIterationBatched(PlannerClass &T, PlannerClass &O, Fast
                                           BatchStats *stats) {
   std::vector<int> added, nearest;
   std::vector<Action> a_new;
-  extendBatch(T, terrain, dir, batch, added, nearest, a_new, true, stats);
+  extendBatch(T, terrain, dir, batch, added, nearest, a_new, true, stats, &O);
   const std::vector<std::pair<int, int>> reached = connectBatch(T, O, terrain, dir, added, stats);
   if (reached.empty()) return 0;
   meet_t = reached.front().first;
@@ -1415,6 +1514,7 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
   const int adaptive = state_action_pair_check_adaptive_step_size_flag_ ? 1 : 0;
   // the target streams (buildRRTConnectBatched's: Ta 101, Tb 102), B draws per half
   const uint64_t tstream[2] = {stream_a, stream_b};
+  applySampling(terrain);  // the device loop's targets and candidates read it from the handle
   DeviceTrees D;
   chk(gbp_stream_create(dev, &D.stream), "stream");
   chk(gbp_plan_ws_create(h, batch, &D.ws), "plan workspace");
@@ -1451,6 +1551,7 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
     chk(gbp_plan_status_read(D.ws, &ps, D.stream), "plan status");
     st.status_reads++;
     while (ps.halt) {  // FRAGILE: re-decide on the host, resume where the sequence stopped
+      for (int b = 0; b < 3; b++) st.halts[b] += (ps.halt >> b) & 1u;
       const int32_t h0 = ps.halt_half;
       const int k = h0 & 1;
       int resume = -1;
@@ -1464,7 +1565,8 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
       chk(gbp_plan_status_read(D.ws, &ps, D.stream), "plan status");
       st.status_reads++;
     }
-    if (ps.error) throw EngineError(GBP_E_HIP, "device planner loop: look-back spin exhausted");
+    if (ps.error & 1u) throw EngineError(GBP_E_HIP, "device planner loop: look-back spin exhausted");
+    if (ps.error) throw EngineError(GBP_E_SHAPE, "device planner loop: a tree ran out of capacity");
     for (int k = 0; k < 2; k++) chk(gbp_tree_size(D.tree[k], &known[k], D.stream), "tree size");
     half += group;
     if (ps.done) {
@@ -1944,8 +2046,15 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
   try {
     FastTerrainMap terrain(p->device);
     terrain.loadDataFlat(p->nx, p->ny, p->x, p->y, p->z, p->dx, p->dy, p->dz);
+    if (p->fragile_eps_fm)
+      chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_FRAGILE_EPS, p->fragile_eps_fm),
+          "fragile eps");
     RRTStarConnectClass planner;  // is-a RRTConnectClass: algorithm 0 uses the plain build
     planner.setSeed(p->seed);
+    planner.set_state_direction_sampling(p->sampling.state_flag != 0, p->sampling.state_p,
+                                         p->sampling.state_speed_direction != 0);
+    planner.set_action_direction_sampling(p->sampling.action_flag != 0, p->sampling.action_p);
+    planner.set_state_action_pair_check_adaptive_step_size_flag_(p->adaptive != 0);
     State s0, s1;
     std::copy(p->start, p->start + 8, s0.begin());
     std::copy(p->goal, p->goal + 8, s1.begin());
@@ -1994,6 +2103,7 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     r->fragile_resolved = st.fragile_resolved;
     r->depth_capped = st.depth_capped;
     r->status_reads = st.status_reads;
+    for (int k = 0; k < 3; k++) r->halts[k] = st.halts[k];
     if (found) {
       double len = 0;
       for (size_t i = 1; i < states.size(); i++) len += planning_utils::poseDistance(states[i - 1], states[i]);

@@ -207,6 +207,48 @@ class Terrain:
                                                _stream(self.device)), "sample_actions")
         return a
 
+    # ---- direction-biased sampling (gbp_sampling, params.yaml:21-27) --------------
+    def set_sampling(self, cfg=None):
+        """Install a _lib.Sampling on the handle (None: off); newConfig's candidates
+        (extend, extend_host) and the device planner loop's targets use it."""
+        check(self._lib.gbp_terrain_set_sampling(self._h, None if cfg is None else ctypes.byref(cfg)),
+              "set_sampling")
+
+    def get_sampling(self):
+        cfg = _lib.Sampling()
+        check(self._lib.gbp_terrain_get_sampling(self._h, ctypes.byref(cfg)), "get_sampling")
+        return cfg
+
+    def sample_states_dir(self, n, seed, stream_id, s_from, s_to, index_base=0, cfg=None):
+        """PlannerClass::randomState(terrain, flag, p, speed, s_from, s_to)
+        (planner_class.cpp:22-35, :82-148); cfg None: the handle's."""
+        st = self._empty((n, 8), torch.float64)
+        f = np.ascontiguousarray(s_from, np.float64).reshape(8)
+        t = np.ascontiguousarray(s_to, np.float64).reshape(8)
+        check(self._lib.gbp_sample_states_dir_dev(
+            self._h, n, seed, stream_id, index_base, None if cfg is None else ctypes.byref(cfg),
+            _np_ptr(f), _np_ptr(t), _ptr(st), _stream(self.device)), "sample_states_dir")
+        return st
+
+    def sample_actions_dir(self, normals, s, s_near, direction, seed, stream_id, index_base=0,
+                           cfg=None):
+        """getRandomAction(surf_norm, direction, flag, p, s, s_near)
+        (planning_utils.cpp:379-391, :443-515); cfg None: the handle's."""
+        nr = self._dev(normals, torch.float64, (3,))
+        sv = self._dev(s, torch.float64, (8,))
+        sn = self._dev(s_near, torch.float64, (8,))
+        n = nr.shape[0]
+        if isinstance(direction, torch.Tensor) or np.ndim(direction) > 0:
+            d, dall = self._dev(direction, torch.uint8), 0
+        else:
+            d, dall = None, int(direction)
+        a = self._empty((n, 10), torch.float64)
+        check(self._lib.gbp_sample_actions_dir_dev(
+            self._h, n, _ptr(nr), _ptr(sv), _ptr(sn), _ptr(d), dall,
+            None if cfg is None else ctypes.byref(cfg), seed, stream_id, index_base, _ptr(a),
+            _stream(self.device)), "sample_actions_dir")
+        return a
+
     def extend(self, s_near, target, direction, seed, extend_base=0, adaptive=False):
         """Batched RRTClass::newConfig + extend acceptance (rrt.cpp:20-102)."""
         sn = self._dev(s_near, torch.float64, (8,))

@@ -26,7 +26,9 @@ class PlanParams(ctypes.Structure):
                 ("x", _P), ("y", _P), ("z", _P), ("dx", _P), ("dy", _P), ("dz", _P),
                 ("start", _D * 8), ("goal", _D * 8), ("batch", ctypes.c_int),
                 ("max_time", _D), ("seed", ctypes.c_uint64), ("post_process", ctypes.c_int),
-                ("algorithm", ctypes.c_int), ("max_time_opt", _D)]
+                ("algorithm", ctypes.c_int), ("max_time_opt", _D),
+                ("sampling", _lib.Sampling), ("fragile_eps_fm", ctypes.c_int64),
+                ("adaptive", ctypes.c_int)]
 
 
 class PlanResult(ctypes.Structure):
@@ -39,7 +41,7 @@ class PlanResult(ctypes.Structure):
                 ("rewires", ctypes.c_int64), ("solutions", ctypes.c_int64),
                 ("extent_a", _D * 4), ("extent_b", _D * 4),
                 ("fragile_resolved", ctypes.c_int64), ("depth_capped", ctypes.c_int64),
-                ("status_reads", ctypes.c_int64)]
+                ("status_reads", ctypes.c_int64), ("halts", ctypes.c_int64 * 3)]
 
 
 _planner = None
@@ -95,7 +97,8 @@ def start_goal_state(height, x, y):
 
 
 def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018,
-                     post_process=False, device=0, capacity=4096, algorithm=0, max_time_opt=0.0):
+                     post_process=False, device=0, capacity=4096, algorithm=0, max_time_opt=0.0,
+                     sampling=None, fragile_eps=None, adaptive=False):
     """Plan start -> goal on terrain `data` (terrain_data.TerrainData).
 
     algorithm 0: batch-synchronous RRT-Connect, stops at the first solution;
@@ -110,7 +113,10 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
       growing horizon, post-process every solution, keep the cheapest, stop
       once a solution exists and `max_time_opt` seconds have passed.
     Returns a dict with the C result fields plus `states` [n][8] and
-    `actions` [n-1][10] (the found path; empty if none)."""
+    `actions` [n-1][10] (the found path; empty if none).
+    sampling: a _lib.Sampling (direction-biased draws, params.yaml:21-27);
+    fragile_eps: a wider FRAGILE margin (forces host re-decisions: tests);
+    adaptive: the adaptive-step pair checks (params.yaml:16)."""
     L = load()
     x = np.ascontiguousarray(data.x, dtype=np.float64)
     y = np.ascontiguousarray(data.y, dtype=np.float64)
@@ -126,6 +132,10 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     p.batch, p.max_time, p.seed, p.post_process = int(batch), float(max_time), int(seed), int(post_process)
     p.algorithm = int(algorithm)
     p.max_time_opt = float(max_time_opt)
+    if sampling is not None:
+        p.sampling = sampling
+    p.fragile_eps_fm = 0 if fragile_eps is None else int(round(fragile_eps * 1e15))
+    p.adaptive = int(bool(adaptive))
     r = PlanResult()
     states = np.zeros((capacity, 8))
     actions = np.zeros((capacity, 10))
@@ -135,6 +145,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
         raise _lib.GbpError(rc, "gbp_plan_rrt_connect")
     out = {k: getattr(r, k) for k, _ in PlanResult._fields_}
     out["extent_a"], out["extent_b"] = list(r.extent_a), list(r.extent_b)
+    out["halts"] = list(r.halts)
     n = r.n_states
     out["states"] = states[:n].copy()
     out["actions"] = actions[:max(n - 1, 0)].copy()

@@ -145,6 +145,10 @@ int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage,
 #define GBP_OPT_FAST_RCP     14  /* 1 (default): the bilinear 1/((x2-x1)(y2-y1)) by two
                                     Newton steps when gbp_terrain_create verified them
                                     bit-exact for every spacing pair; get: 1 = in use   */
+#define GBP_OPT_FRAGILE_EPS  15  /* the FRAGILE margin in units of 1e-15 (default 1000 =
+                                    1e-12, the smallest accepted): a wider margin flags
+                                    and re-decides more attempts on the host, with the
+                                    same results (tests use it to force host resolutions) */
 #define GBP_KERNEL_DIRECT     0  /* one lane per attempt                              */
 #define GBP_KERNEL_PERSISTENT 1  /* persistent waves, lanes re-packed per sample      */
 int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value);
@@ -218,12 +222,62 @@ int gbp_sample_actions_dev(int64_t n, const double *normals, uint64_t seed,
 int gbp_sample_actions_host(gbp_terrain *t, int64_t n, const double *normals, uint64_t seed,
                             uint64_t stream_id, int64_t index_base, double *actions);
 
+/* ---- direction-biased sampling (ROS params state_direction_sampling/... and
+ *      action_direction_sampling/..., config/params.yaml:21-27, forwarded by
+ *      global_body_planner.cpp:193-205 to RRTClass::set_state_direction_sampling /
+ *      set_action_direction_sampling, rrt.cpp:268-278).  Off by default, as in
+ *      the reference.  The reference's coin is `rand()/RAND_MAX <= p`; the engine's
+ *      is a Philox uniform of its own purpose (index, try) so both branches keep
+ *      their counter-addressed draws. */
+typedef struct {
+  int32_t state_flag;            /* randomState -> randomStateDirection with probability state_p */
+  int32_t state_speed_direction; /* speed_direction_flag: velocity heading = atan2(to - from) */
+  double state_p;                /* probability_threshold */
+  int32_t action_flag;           /* getRandomAction -> getRandomActionDirection with prob. action_p */
+  int32_t reserved;
+  double action_p;
+} gbp_sampling;
+/* The handle's sampling configuration (NULL = off): applied by every entry
+ * point that draws newConfig's candidate actions (gbp_extend_batch_*,
+ * gbp_extend_resolve_host, gbp_extend_tree_*) and by the device planner loop's
+ * targets (gbp_plan_half_dev: s_from / s_to as rrt_connect.cpp:248-252, :283-287,
+ * the trees' last vertices and roots when the half starts). */
+int gbp_terrain_set_sampling(gbp_terrain *t, const gbp_sampling *cfg);
+int gbp_terrain_get_sampling(const gbp_terrain *t, gbp_sampling *cfg);
+/* PlannerClass::randomState(terrain, flag, p, speed_direction_flag, s_from, s_to)
+ * (planner_class.cpp:22-35): index i of stream draws the coin, then either
+ * randomStateDirection (:82-148: x, y uniform over the s_from / s_to rectangle,
+ * heading atan2(to - from) when speed_direction) or randomState (:38-76) from
+ * the same draws as gbp_sample_states_dev.  s_from[8], s_to[8] are HOST arrays;
+ * cfg NULL = the handle's configuration. */
+int gbp_sample_states_dir_dev(gbp_terrain *t, int64_t n, uint64_t seed, uint64_t stream_id,
+                              int64_t index_base, const gbp_sampling *cfg, const double *s_from,
+                              const double *s_to, double *states, gbp_stream stream);
+int gbp_sample_states_dir_host(gbp_terrain *t, int64_t n, uint64_t seed, uint64_t stream_id,
+                               int64_t index_base, const gbp_sampling *cfg, const double *s_from,
+                               const double *s_to, double *states);
+/* getRandomAction(surf_norm, direction, flag, p, s, s_near) (planning_utils.cpp:379-391):
+ * the coin, then getRandomActionDirection(surf_norm, s_from, s_to) (:443-515,
+ * FORWARD: s_near -> s, REVERSE: s -> s_near) or getRandomAction(surf_norm).
+ * normals[n][3], s[n][8] (the state extended toward), s_near[n][8], direction[n]
+ * (or NULL => direction_all); cfg NULL = the handle's configuration. */
+int gbp_sample_actions_dir_dev(gbp_terrain *t, int64_t n, const double *normals, const double *s,
+                               const double *s_near, const uint8_t *direction, int direction_all,
+                               const gbp_sampling *cfg, uint64_t seed, uint64_t stream_id,
+                               int64_t index_base, double *actions, gbp_stream stream);
+int gbp_sample_actions_dir_host(gbp_terrain *t, int64_t n, const double *normals, const double *s,
+                                const double *s_near, const uint8_t *direction, int direction_all,
+                                const gbp_sampling *cfg, uint64_t seed, uint64_t stream_id,
+                                int64_t index_base, double *actions);
+
 /* ---- batched extend (RRTClass::newConfig + the acceptance half of
  *      RRTClass::extend, rrt.cpp:20-102) --------------------------------------
  * For extend i: s_near[i] (the nearest vertex, found by gbp_nearest_batch),
  * target[i] (the state the tree is extended towards).  Candidate action j
  * (j = 0..5) is getRandomAction(getSurfaceNormal(target)) drawn from stream
- * (seed, extend_base + i, j); candidates are checked (forward or reverse by
+ * (seed, extend_base + i, j) — with the handle's gbp_sampling, the reference's
+ * getRandomAction(surf_norm, direction, flag, p, target, s_near) (rrt.cpp:34, :49)
+ * as gbp_sample_actions_dir_dev; candidates are checked (forward or reverse by
  * direction) and the LOWEST valid j is taken — the sequential newConfig.
  * result[i] = TRAPPED / ADVANCED / REACHED (isWithinBounds(s_new, target));
  * chosen[i] = j or -1; s_new[i], a_new[i] written when result != TRAPPED.   */
@@ -352,14 +406,16 @@ int gbp_tree_device_ptrs(gbp_tree *tree, double **states, int32_t **count);
  * A FRAGILE decision halts the sequence after its stage (status.halt, every
  * later kernel a no-op): gbp_plan_resolve_host re-decides the flagged items
  * with glibc and returns the stage to resume the halted half-iteration at
- * (first_stage).  The trees must have room for `batch` more vertices each. */
+ * (first_stage).  The trees must have room for `batch` more vertices each (an
+ * append past a tree's capacity is not written and sets status.error bit 1). */
 #define GBP_PLAN_HALT_TARGETS 1u
 #define GBP_PLAN_HALT_EXTEND  2u
 #define GBP_PLAN_HALT_CONNECT 4u
 typedef struct {
   uint32_t halt;          /* GBP_PLAN_HALT_* of the stage that stopped the sequence */
   uint32_t done;          /* a connection REACHED */
-  uint32_t error;         /* a bounded device spin ran out (must be 0) */
+  uint32_t error;         /* must be 0: bit 0 a bounded device spin ran out,
+                             bit 1 an append found its tree full */
   int32_t halt_half;      /* the half-iteration that halted */
   int32_t n_targets;      /* valid targets of the last executed half */
   int32_t n_validate;     /* candidates launched (6 n_targets, 0 when gated) */
@@ -372,6 +428,11 @@ typedef struct {
   int64_t ext_counter;    /* RRTClass extend counter after it */
   int64_t stat_targets, stat_attempts, stat_added, stat_conn_added;
   int64_t stat_fragile_resolved, stat_depth_capped;
+  /* the gate: sequence number of the first planner kernel launch that raised
+   * halt or done (~0: none).  Every launch carries its own number and is a
+   * no-op only if the gate was raised by an EARLIER launch, so all workgroups
+   * of the launch that raised it still finish their items. */
+  uint64_t gate_seq;
 } gbp_plan_status;
 int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out);
 int gbp_plan_ws_destroy(gbp_plan_ws *ws);
@@ -394,7 +455,9 @@ int gbp_plan_resolve_host(gbp_terrain *t, gbp_plan_ws *ws, gbp_tree *T, gbp_tree
  * result[i] = TRAPPED / ADVANCED / REACHED, new_vertex[i] = the appended vertex
  * or -1; candidate j of extend i is drawn from the extend stream at index
  * (extend_base + i) * 8 + j, as gbp_extend_batch_dev.  Uses ws's scratch (n <=
- * its max_batch).  If a decision is FRAGILE the append halts (status.halt =
+ * its max_batch).  T must have room for n more vertices (gbp_tree_reserve;
+ * gbp_extend_tree_host reserves itself): appends past the capacity are
+ * dropped and set status.error bit 1.  If a decision is FRAGILE the append halts (status.halt =
  * GBP_PLAN_HALT_EXTEND): gbp_plan_resolve_host(.., O = NULL, ..) then
  * gbp_extend_tree_finish_dev complete it.  gbp_extend_tree_host does all of
  * that synchronously from host targets. */

@@ -193,9 +193,17 @@ void isValidStateActionPairBatch(const std::vector<State> &s, const std::vector<
                                  bool adaptive, std::vector<uint8_t> &valid,
                                  std::vector<State> &s_new, std::vector<double> &t_new,
                                  std::vector<uint32_t> *flags = nullptr);
-// planning_utils.cpp:392-442 on the engine's counter-based stream
-// (the reference's rand() / clock-seeded engines are not reproducible)
-Action getRandomAction(std::array<double, 3> surf_norm);
+// planning_utils.cpp:379-515 on the engine's counter-based stream (the
+// reference's rand() / clock-seeded engines are not reproducible): draw k of
+// the process's free-function stream (seed setRandomSeed, index k counting up
+// per thread), sampled by the engine on device 0 (gbp_sample_actions_dir_host)
+Action getRandomAction(std::array<double, 3> surf_norm, int direction,
+                       bool action_direction_sampling_flag,
+                       double action_direction_sampling_probability_threshold, State s,
+                       State s_near);                                       // :379-391
+Action getRandomAction(std::array<double, 3> surf_norm);                    // :392-442
+Action getRandomActionDirection(std::array<double, 3> surf_norm, State s_from,
+                                State s_to);                                // :443-515
 void setRandomSeed(uint64_t seed);
 // planning_utils.cpp:142-193
 void interpStateActionPair(State s, Action a, double t0, double dt,
@@ -233,8 +241,19 @@ class PlannerClass {
 
   // planner_class.cpp:38-76 on the engine sampler (stream = this tree's id)
   State randomState(FastTerrainMap &terrain);
+  // planner_class.cpp:22-35: randomStateDirection with probability p, else
+  // randomState (one draw of this tree's stream either way)
+  State randomState(FastTerrainMap &terrain, bool state_direction_sampling_flag,
+                    double state_direction_sampling_probability_threshold,
+                    bool speed_direction_flag, State s_from, State s_to);
+  // planner_class.cpp:82-148
+  State randomStateDirection(FastTerrainMap &terrain, State s_from, State s_to,
+                             bool speed_direction_flag);
   // n consecutive randomState draws of this tree's stream in one launch
   std::vector<State> randomStateBatch(FastTerrainMap &terrain, int n);
+  // ... with the direction-biased variant of cfg (s_from / s_to for all n)
+  std::vector<State> randomStateBatch(FastTerrainMap &terrain, int n, const gbp_sampling &cfg,
+                                      const State &s_from, const State &s_to);
   // planner_class.cpp:185-200 on the engine (ties -> lowest index)
   int getNearestNeighbor(State q);
   std::vector<int> getNearestNeighborBatch(const std::vector<State> &q);
@@ -292,9 +311,10 @@ class RRTClass {
                      std::vector<std::vector<double>> &allStatePosition);
   void printPath(PlannerClass &T, std::vector<int> path);                  // rrt.cpp:143-152
   void saveStateSequence(PlannerClass &T);                                 // rrt.cpp:253-265
-  // rrt.cpp:268-280: stored like the reference; direction sampling (default
-  // off, params.yaml:25-27) is not implemented by the engine samplers, so
-  // newConfig throws std::logic_error when a flag is on
+  // rrt.cpp:268-280 (params.yaml:21-27, off by default): newConfig's
+  // candidates and every search's targets (sequential, batched and
+  // device-resident) draw the direction-biased variants when a flag is on
+  // (gbp_sampling, applied to the terrain handle the search runs on)
   void set_action_direction_sampling(bool flag, double threshold) {
     action_direction_sampling_flag_ = flag;
     action_direction_sampling_probability_threshold_ = threshold;
@@ -326,8 +346,13 @@ class RRTClass {
                               : length;
   }
   const std::vector<double> &costHistory() const { return cost_vector_; }
+  // this planner's direction-sampling parameters as the engine's gbp_sampling
+  gbp_sampling samplingConfig() const;
 
  protected:
+  // installs samplingConfig() on the terrain handle (the candidate sampler and
+  // the device loop's targets read it there)
+  void applySampling(FastTerrainMap &terrain) const;
   bool goal_found = false;
   std::chrono::duration<double> elapsed_total{0};
   std::chrono::duration<double> elapsed_to_first{0};
@@ -357,6 +382,8 @@ struct BatchStats {
   int64_t depth_capped = 0;   // connects stopped at GBP_CONNECT_MAX_DEPTH (TRAPPED)
   int64_t status_reads = 0;   // device loop: host synchronisations
   int64_t fragile_resolved = 0;  // attempts re-decided on the host (GBP_F_RESOLVED)
+  int64_t halts[3] = {0, 0, 0};  // device loop: FRAGILE halts in the targets / extend /
+                                 // connect stage (GBP_PLAN_HALT_*)
   double extent_a[4] = {0, 0, 0, 0}, extent_b[4] = {0, 0, 0, 0};  // x_min x_max y_min y_max
 };
 
@@ -454,10 +481,13 @@ class RRTConnectClass : public RRTClass {
                                                 const std::vector<int> &added, BatchStats *stats);
   // draw `batch` targets, keep the STANCE-valid ones, extend T toward all of
   // them against T's snapshot; returns the inserted vertices (in target order),
-  // their nearest vertices and actions
+  // their nearest vertices and actions.  With O, the targets are
+  // randomState(terrain, state_direction_sampling_*, s_from, s_to) with the
+  // reference's s_from / s_to (rrt_connect.cpp:248-252, :283-287) as the
+  // trees stand when the half starts; without, plain randomState (RRT*).
   void extendBatch(PlannerClass &T, FastTerrainMap &terrain, int dir, int batch,
                    std::vector<int> &added, std::vector<int> &nearest, std::vector<Action> &a_new,
-                   bool insert, BatchStats *stats);
+                   bool insert, BatchStats *stats, const PlannerClass *O = nullptr);
   int halfIterationBatched(PlannerClass &T, PlannerClass &O, FastTerrainMap &terrain, int dir,
                            int batch, int &meet_t, int &meet_o, BatchStats *stats);
 };
@@ -565,6 +595,10 @@ typedef struct {
                         // (same trees and path as 0), 4 = 2 on the device-resident search
   double max_time_opt;  // algorithm 2: keep restarting until a solution exists and this
                         // many seconds have passed (buildRRTConnect's max_time_opt)
+  gbp_sampling sampling;  // direction-biased sampling (RRTClass::set_*_direction_sampling,
+                          // params.yaml:21-27); all zero = off, the reference default
+  int64_t fragile_eps_fm; // FRAGILE margin in 1e-15 units (GBP_OPT_FRAGILE_EPS); 0 = default
+  int adaptive;           // state_action_pair_check_adaptive_step_size_flag (params.yaml:16)
 } gbp_plan_params;
 
 typedef struct {
@@ -579,6 +613,8 @@ typedef struct {
   int64_t fragile_resolved;    // decisions re-decided on the host with glibc (GBP_F_RESOLVED)
   int64_t depth_capped;        // connects stopped at GBP_CONNECT_MAX_DEPTH
   int64_t status_reads;        // algorithm 3: host synchronisations of the device loop
+  int64_t halts[3];            // algorithm 3/4: FRAGILE halts in the targets / extend /
+                               // connect stage of the device loop
 } gbp_plan_result;
 
 /* plans from start to goal; path_states[capacity][8] / path_actions[capacity][10]

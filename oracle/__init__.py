@@ -78,6 +78,8 @@ def lib():
             "orc_neighbors_batch": (None, [I64, P, I, P, D, I, P, P, I]),
             "orc_sample_states": (None, [P, I64, U64, U64, I64, I, I, P, P, I]),
             "orc_sample_actions": (None, [I64, P, U64, U64, I64, P, I]),
+            "orc_sample_states_dir": (None, [P, I64, U64, U64, I64, I, D, I, P, P, P, I]),
+            "orc_sample_actions_dir": (None, [I64, P, P, P, P, I, I, D, U64, U64, I64, P, I]),
             "orc_philox4x32_10": (None, [P, P, P]),
             "orc_uniform2": (None, [U64, U64, ctypes.c_uint32, I64, ctypes.c_uint32, P]),
         }
@@ -217,6 +219,17 @@ class OracleTerrain:
                                 max_tries, _p(st), _p(tries), nthreads)
         return st, tries
 
+    def sample_states_dir(self, n, seed, stream_id, s_from, s_to, index_base=0, state_flag=True,
+                          state_p=0.05, speed_direction=False, nthreads=1):
+        """PlannerClass::randomState(terrain, flag, p, speed, s_from, s_to)
+        (planner_class.cpp:22-35, :82-148), one try per index."""
+        st = np.empty((n, 8))
+        f, t = _c(s_from, np.float64), _c(s_to, np.float64)
+        lib().orc_sample_states_dir(self.ref, n, seed, stream_id, index_base, int(bool(state_flag)),
+                                    float(state_p), int(bool(speed_direction)), _p(f), _p(t),
+                                    _p(st), nthreads)
+        return st
+
     def attempt_connect(self, s_existing, s, direction, t_s=0.0, adaptive=False):
         s_existing = _c(s_existing, np.float64)
         s = _c(s, np.float64)
@@ -232,6 +245,25 @@ def sample_actions(normals, seed, stream_id, index_base=0, nthreads=1):
     n = normals.shape[0]
     out = np.empty((n, 10))
     lib().orc_sample_actions(n, _p(normals), seed, stream_id, index_base, _p(out), nthreads)
+    return out
+
+
+def sample_actions_dir(normals, s, s_near, direction, seed, stream_id, index_base=0,
+                       action_flag=True, action_p=0.15, nthreads=1):
+    """getRandomAction(surf_norm, direction, flag, p, s, s_near)
+    (planning_utils.cpp:379-391, :443-515)."""
+    normals = _c(normals, np.float64).reshape(-1, 3)
+    n = normals.shape[0]
+    s = _c(s, np.float64).reshape(n, 8)
+    s_near = _c(s_near, np.float64).reshape(n, 8)
+    if np.ndim(direction) > 0:
+        d, dall = _c(direction, np.uint8), 0
+    else:
+        d, dall = None, int(direction)
+    out = np.empty((n, 10))
+    lib().orc_sample_actions_dir(n, _p(normals), _p(s), _p(s_near), _p(d), dall,
+                                 int(bool(action_flag)), float(action_p), seed, stream_id,
+                                 index_base, _p(out), nthreads)
     return out
 
 

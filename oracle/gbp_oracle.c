@@ -878,6 +878,143 @@ void orc_sample_action(const double *nrm, uint64_t seed, uint64_t stream_id, int
   a[9] = std_max(std_min(n1, ANG_ACC_MAX), -ANG_ACC_MAX);
 }
 
+/* ---- direction-biased sampling ----------------------------------------------
+ * The reference's coin `(double) rand() / RAND_MAX <= threshold`
+ * (planner_class.cpp:27-29, planning_utils.cpp:381-383) is the engine's
+ * uniform of purpose PURPOSE_COIN (index, draw = try / 0). */
+#define PURPOSE_COIN 3u
+static int coin(uint64_t seed, uint64_t stream_id, int64_t index, uint32_t draw, double p) {
+  double c[2];
+  orc_uniform2(seed, stream_id, PURPOSE_COIN, index, draw, c);
+  return c[0] <= p;
+}
+
+/* planning_utils.cpp:443-515 (the draws of orc_sample_action, the tangential
+ * forces on the side of the velocity change s_from -> s_to) */
+static void sample_action_direction(const double *nrm, const double *s_from, const double *s_to,
+                                    uint64_t seed, uint64_t stream_id, int64_t index, double *a) {
+  double u[5][2];
+  for (uint32_t d = 0; d < 5; d++) orc_uniform2(seed, stream_id, PURPOSE_ACTION, index, d, u[d]);
+  int dx_increase_flag = s_to[3] > s_from[3];
+  int dy_increase_flag = s_to[4] > s_from[4];
+  double f_z_td = F_MAX * u[0][0];
+  double f_z_to = F_MAX * u[0][1];
+  double f_friction_td = MU * f_z_td;
+  double f_friction_to = MU * f_z_to;
+  double f_x_td, f_x_to, f_y_td, f_y_to;
+  if (dx_increase_flag) {
+    f_x_td = f_friction_td * u[1][0];
+    f_x_to = f_friction_to * u[1][1];
+  } else {
+    f_x_td = f_friction_td * u[1][0] - f_friction_td;
+    f_x_to = f_friction_to * u[1][1] - f_friction_to;
+  }
+  if (dy_increase_flag) {
+    f_y_td = f_friction_td * u[2][0];
+    f_y_to = f_friction_to * u[2][1];
+  } else {
+    f_y_td = f_friction_td * u[2][0] - f_friction_td;
+    f_y_to = f_friction_to * u[2][1] - f_friction_to;
+  }
+  double f_td[3] = {f_x_td, f_y_td, f_z_td}, f_to[3] = {f_x_to, f_y_to, f_z_to};
+  double r_td[3], r_to[3];
+  orc_rotate_grf(nrm, f_td, r_td);
+  orc_rotate_grf(nrm, f_to, r_to);
+  a[0] = r_td[0] / M_CONST;
+  a[1] = r_td[1] / M_CONST;
+  a[2] = r_td[2] / M_CONST - G_CONST;
+  a[3] = r_to[0] / M_CONST;
+  a[4] = r_to[1] / M_CONST;
+  a[5] = r_to[2] / M_CONST - G_CONST;
+  a[6] = 0.3;
+  a[7] = (T_F_MAX - T_F_MIN) * u[3][0] + T_F_MIN;
+  double z0, z1;
+  box_muller(u[4][0], u[4][1], &z0, &z1);
+  double n0 = z0 * (ANG_ACC_MAX / 4.0) + 0.0, n1 = z1 * (ANG_ACC_MAX / 4.0) + 0.0;
+  a[8] = std_max(std_min(n0, ANG_ACC_MAX), -ANG_ACC_MAX);
+  a[9] = std_max(std_min(n1, ANG_ACC_MAX), -ANG_ACC_MAX);
+}
+
+/* planning_utils.cpp:379-391 */
+static void sample_action_any(const double *nrm, int direction, int flag, double p,
+                              const double *s, const double *s_near, uint64_t seed,
+                              uint64_t stream_id, int64_t index, double *a) {
+  if (flag && coin(seed, stream_id, index, 0, p)) {
+    if (direction == GBP_FORWARD)
+      sample_action_direction(nrm, s_near, s, seed, stream_id, index, a);
+    else
+      sample_action_direction(nrm, s, s_near, seed, stream_id, index, a);
+  } else {
+    orc_sample_action(nrm, seed, stream_id, index, a);
+  }
+}
+
+/* planner_class.cpp:82-148, one try (draws 0..3 of the index) */
+static void sample_state_direction(const orc_terrain *T, const double *s_from, const double *s_to,
+                                   int speed_direction_flag, uint64_t seed, uint64_t stream_id,
+                                   int64_t index, double *q) {
+  double x_min = std_min(s_from[0], s_to[0]);
+  double x_max = std_max(s_from[0], s_to[0]);
+  double y_min = std_min(s_from[1], s_to[1]);
+  double y_max = std_max(s_from[1], s_to[1]);
+  double z_min_rel = H_MIN + ROBOT_H, z_max_rel = H_MAX + ROBOT_H;
+  double mean = 0.5 * (z_max_rel + z_min_rel);
+  double sd = (z_max_rel - z_min_rel) * (1.0 / (2 * 3.0));
+  double u0[2], u1[2], u2[2], u3[2];
+  orc_uniform2(seed, stream_id, PURPOSE_STATE, index, 0, u0);
+  orc_uniform2(seed, stream_id, PURPOSE_STATE, index, 1, u1);
+  orc_uniform2(seed, stream_id, PURPOSE_STATE, index, 2, u2);
+  orc_uniform2(seed, stream_id, PURPOSE_STATE, index, 3, u3);
+  double z0, z1;
+  box_muller(u1[0], u1[1], &z0, &z1);
+  double hz = z0 * sd + mean;
+  q[0] = (x_max - x_min) * u0[0] + x_min;
+  q[1] = (y_max - y_min) * u0[1] + y_min;
+  q[2] = std_max(std_min(hz, z_max_rel), z_min_rel) + orc_ground_height(T, q[0], q[1], 0);
+  double phi;
+  if (speed_direction_flag) {
+    double delta_x = s_to[0] - s_from[0];
+    double delta_y = s_to[1] - s_from[1];
+    phi = atan2(delta_y, delta_x);
+  } else {
+    phi = (2.0 * MY_PI) * u2[0];
+  }
+  double cos_theta = 2.0 * u2[1] - 1.0;
+  double theta = acos(cos_theta);
+  double v = u3[0] * V_MAX;
+  q[3] = v * sin(theta) * cos(phi);
+  q[4] = v * sin(theta) * sin(phi);
+  q[5] = v * cos(theta);
+  q[6] = 2 * P_MAX * u3[1] - P_MAX;
+  q[7] = 0.0;
+}
+
+void orc_sample_states_dir(const orc_terrain *T, int64_t n, uint64_t seed, uint64_t stream_id,
+                           int64_t index_base, int state_flag, double state_p, int speed_direction,
+                           const double *s_from, const double *s_to, double *states, int nthreads) {
+  if (nthreads <= 0) nthreads = 1;
+  OMP_FOR
+  for (int64_t i = 0; i < n; i++) {
+    const int64_t idx = index_base + i;
+    if (state_flag && coin(seed, stream_id, idx, 0, state_p)) /* planner_class.cpp:22-35 */
+      sample_state_direction(T, s_from, s_to, speed_direction, seed, stream_id, idx, states + 8 * i);
+    else
+      orc_sample_state(T, seed, stream_id, idx, -1, 1, states + 8 * i);
+  }
+}
+
+void orc_sample_actions_dir(int64_t n, const double *normals, const double *s,
+                            const double *s_near, const uint8_t *direction, int direction_all,
+                            int action_flag, double action_p, uint64_t seed, uint64_t stream_id,
+                            int64_t index_base, double *actions, int nthreads) {
+  if (nthreads <= 0) nthreads = 1;
+  OMP_FOR
+  for (int64_t i = 0; i < n; i++)
+    sample_action_any(normals + 3 * i, direction ? direction[i] : direction_all, action_flag,
+                      action_p, s + 8 * i, s_near + 8 * i, seed, stream_id, index_base + i,
+                      actions + 10 * i);
+}
+
 void orc_sample_states(const orc_terrain *T, int64_t n, uint64_t seed, uint64_t stream_id,
                        int64_t index_base, int require_phase, int max_tries, double *states,
                        int32_t *tries, int nthreads) {

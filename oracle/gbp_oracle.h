@@ -135,6 +135,16 @@ void orc_sample_states(const orc_terrain *T, int64_t n, uint64_t seed, uint64_t 
                        int32_t *tries, int nthreads);
 void orc_sample_actions(int64_t n, const double *normals, uint64_t seed, uint64_t stream_id,
                         int64_t index_base, double *actions, int nthreads);
+/* direction-biased sampling (the engine's gbp_sampling; coin = uniform of purpose 3).
+ * planner_class.cpp:22-35 + :82-148, one try of each index (s_from / s_to shared) */
+void orc_sample_states_dir(const orc_terrain *T, int64_t n, uint64_t seed, uint64_t stream_id,
+                           int64_t index_base, int state_flag, double state_p, int speed_direction,
+                           const double *s_from, const double *s_to, double *states, int nthreads);
+/* planning_utils.cpp:379-391 + :443-515: s[n][8] the state extended toward, s_near[n][8] */
+void orc_sample_actions_dir(int64_t n, const double *normals, const double *s,
+                            const double *s_near, const uint8_t *direction, int direction_all,
+                            int action_flag, double action_p, uint64_t seed, uint64_t stream_id,
+                            int64_t index_base, double *actions, int nthreads);
 
 #ifdef __cplusplus
 }

@@ -47,7 +47,10 @@ struct GridMap {
 int main(int argc, char **argv) {
   const bool star = argc > 1 && std::string(argv[1]) == "star";  // algorithm: rrt-star-connect
   // "seq": buildRRTConnect's sequential per-call search (set_engine_batch(0))
-  const bool seq = argc > 1 && std::string(argv[1]) == "seq";
+  const bool seq = argc > 1 && (std::string(argv[1]) == "seq" || std::string(argv[1]) == "dirseq");
+  // "dir" / "dirseq": the direction-sampling parameters switched on
+  // (config/params.yaml:21-27 with flag: true, forwarded as :193-205)
+  const bool dir = argc > 1 && (std::string(argv[1]) == "dir" || std::string(argv[1]) == "dirseq");
   fake_grid_map::GridMap map{120, 60, 0.05, {}};
   map.z.assign((size_t)map.nx * map.ny, 0.0f);  // flat ground
   FastTerrainMap terrain_;
@@ -63,8 +66,24 @@ int main(int argc, char **argv) {
   for (RRTClass *o : {(RRTClass *)&rrt_connect_obj, (RRTClass *)&rrt_star_connect_obj}) {
     o->set_state_action_pair_check_adaptive_step_size_flag_(false);   // :182 setPlannerParameter
     o->set_cost_add_yaw(false, 1.0, 1.0);                             // :190
-    o->set_action_direction_sampling(false, 0.15);
-    o->set_state_direction_sampling(false, 0.05, false);
+    o->set_action_direction_sampling(dir, 0.1);
+    o->set_state_direction_sampling(dir, 0.05, false);
+  }
+  if (dir) {
+    // the free samplers (planning_utils.cpp:379-515): t_s fixed, t_f in range,
+    // and on flat ground the direction variant's tangential forces follow the
+    // velocity change (FORWARD: s_near -> s)
+    const std::array<double, 3> up = {0.0, 0.0, 1.0};
+    const State slow = {0, 0, 0.4, 0.1, 0.5, 0, 0, 0}, fast = {1, 0, 0.4, 1.0, -0.5, 0, 0, 0};
+    for (int k = 0; k < 64; k++) {
+      const Action a = getRandomAction(up);
+      const Action d = getRandomActionDirection(up, slow, fast);
+      const Action c = getRandomAction(up, FORWARD, true, 1.0, fast, slow);
+      for (const Action *x : {&a, &d, &c})
+        if ((*x)[6] != 0.3 || !((*x)[7] >= 0 && (*x)[7] < 0.5)) return 2;
+      if (!(d[0] >= 0 && d[3] >= 0 && d[1] <= 0 && d[4] <= 0)) return 3;  // dx grows, dy shrinks
+      if (!(c[0] >= 0 && c[3] >= 0 && c[1] <= 0 && c[4] <= 0)) return 4;
+    }
   }
   if (seq) rrt_connect_obj.set_engine_batch(0);
 

@@ -50,6 +50,34 @@ def test_device_loop_equals_host_batched(gpu, name, xy, batch, seed):
           f"{dev['time_to_first']:.4f} s in {dev['status_reads']} status reads")
 
 
+@pytest.mark.parametrize("batch,seed", [(4096, 3), (1024, 8)])
+def test_device_loop_forced_halts_equal_host_batched(gpu, batch, seed):
+    """Halt -> gbp_plan_resolve_host -> resume in every stage.  A FRAGILE
+    margin of 1e-5 (GBP_OPT_FRAGILE_EPS; any margin >= 1e-12 leaves results
+    unchanged, only more of them are re-decided with glibc) flags about 2 % of
+    the state checks, so the targets, extend and connect stages all halt many
+    times; k_connect's 1024-workgroup grid (batch 4096) exceeds what is
+    resident at once, so workgroups start after the halt was raised in their
+    own launch and must still compute their items (gate_seq).  The device
+    loop must still equal the host batched planner bit for bit."""
+    data = td.synth_rough(256)
+    O = oracle.OracleTerrain.from_data(data)
+    start, goal = _start_goal(O, 1.0, 2.55, 4.02, 2.55)
+    kw = dict(batch=batch, max_time=120.0, seed=seed, fragile_eps=1e-5)
+    host = planner.plan_rrt_connect(data, start, goal, **kw)
+    dev = planner.plan_rrt_connect_device(data, start, goal, **kw)
+    assert host["found"] == 1 and dev["found"] == 1
+    check_path(O, dev, start, goal)
+    assert np.array_equal(dev["states"], host["states"])
+    assert np.array_equal(dev["actions"], host["actions"])
+    for k in ("vertices_a", "vertices_b", "targets", "extends", "attempts_checked", "connects",
+              "fragile_resolved", "depth_capped"):
+        assert dev[k] == host[k], (k, dev[k], host[k])
+    assert all(h > 0 for h in dev["halts"]), dev["halts"]   # targets, extend, connect
+    print(f"batch {batch}: halts {dev['halts']}, {dev['fragile_resolved']} re-decided, "
+          f"{dev['status_reads']} status reads")
+
+
 def test_device_loop_stance_invalid_start(gpu):
     """SURVEY H12 on the device loop: the STANCE-invalid slope start never grows."""
     data = td.csv_gridmap("slope")

@@ -1,0 +1,217 @@
+"""Direction-biased sampling (the ROS params state_direction_sampling/* and
+action_direction_sampling/*, config/params.yaml:21-27, forwarded by
+global_body_planner.cpp:193-205) on the engine, against the oracle.
+
+  * PlannerClass::randomState(terrain, flag, p, speed_direction_flag, s_from,
+    s_to) -> randomStateDirection (planner_class.cpp:22-35, :82-148);
+  * getRandomAction(surf_norm, direction, flag, p, s, s_near) ->
+    getRandomActionDirection (planning_utils.cpp:379-391, :443-515);
+  * newConfig's candidates with the action flag on (rrt.cpp:34, :49): the
+    engine's extend equals the oracle's extend on the same candidates;
+  * the device planner loop with both flags on builds the same trees as the
+    host batched planner, and the node's buildRRTConnect plans with them.
+
+Samplers use device atan2 / acos / sin / cos / log: compared at rtol 1e-12
+(the tolerance of the plain samplers, tests/test_gpu_parity.py); the coin
+(Philox) and every branch it selects are exact.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from global_body_planner_amd import _lib as L
+from global_body_planner_amd import planner
+from global_body_planner_amd import terrain_data as td
+from tests.helpers import attempts_oracle, bits, same_f64, u32
+from tests.test_gpu_planner import _start_goal, check_path
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+_cache = {}
+
+
+def pair_of(name):
+    import global_body_planner_amd as gbp
+    if name not in _cache:
+        data = td.by_name(name)
+        _cache[name] = (data, gbp.Terrain.from_data(data, device=0),
+                        oracle.OracleTerrain.from_data(data))
+    return _cache[name]
+
+
+def np_(t):
+    return t.cpu().numpy()
+
+
+S_FROM = np.array([1.0, 2.55, 0.6, 1.0, 0.0, 0.0, 0.0, 0.0])
+S_TO = np.array([4.02, 1.10, 0.5, 0.2, 0.4, 0.0, 0.0, 0.0])
+
+
+@pytest.mark.parametrize("speed", [False, True])
+def test_state_direction_sampler_matches_oracle(gpu, speed):
+    data, T, O = pair_of("synth-rough-256")
+    n = 20000
+    cfg = L.sampling(state_flag=True, state_p=0.5, speed_direction=speed)
+    g = np_(T.sample_states_dir(n, 31, 7, S_FROM, S_TO, index_base=5, cfg=cfg))
+    r = O.sample_states_dir(n, 31, 7, S_FROM, S_TO, index_base=5, state_p=0.5,
+                            speed_direction=speed, nthreads=8)
+    np.testing.assert_allclose(g, r, rtol=1e-12, atol=1e-12)
+    # x and y come from multiplications of exact uniforms: bit-exact on both branches
+    assert np.array_equal(bits(g[:, :2]), bits(r[:, :2]))
+    # the coin picks the rectangle about half the time (plain draws cover the map)
+    inside = ((g[:, 0] >= 1.0) & (g[:, 0] <= 4.02) & (g[:, 1] >= 1.10) & (g[:, 1] <= 2.55))
+    plain, _ = T.sample_states(n, 31, 7, 5)
+    plain = np_(plain)
+    moved = np.any(bits(g) != bits(plain), axis=1)
+    assert 0.45 < moved.mean() < 0.55, moved.mean()
+    assert inside[moved].all()
+    if speed:  # the heading of a direction draw is atan2(to - from)
+        yaw = np.arctan2(g[moved, 4], g[moved, 3])
+        ref = np.arctan2(S_TO[1] - S_FROM[1], S_TO[0] - S_FROM[0])
+        fast = np.hypot(g[moved, 3], g[moved, 4]) > 1e-6
+        np.testing.assert_allclose(yaw[fast], ref, atol=1e-9)
+    # flag off: exactly the plain sampler (planner_class.cpp:31-32)
+    g0 = np_(T.sample_states_dir(n, 31, 7, S_FROM, S_TO, index_base=5, cfg=L.sampling()))
+    assert np.array_equal(bits(g0), bits(plain))
+
+
+def test_action_direction_sampler_matches_oracle(gpu):
+    data, T, O = pair_of("synth-rough-256")
+    n = 20000
+    s_near, _, d, target, _ = attempts_oracle(O, n, seed=77)
+    nrm = O.normal_batch(target[:, :2])[0]
+    cfg = L.sampling(action_flag=True, action_p=0.5)
+    ga = np_(T.sample_actions_dir(torch.from_numpy(nrm), torch.from_numpy(target),
+                                  torch.from_numpy(s_near), torch.from_numpy(d), 31, 3, cfg=cfg))
+    ra = oracle.sample_actions_dir(nrm, target, s_near, d, 31, 3, action_p=0.5, nthreads=8)
+    np.testing.assert_allclose(ga, ra, rtol=1e-12, atol=1e-12)
+    assert np.array_equal(ga[:, 6], ra[:, 6]) and np.array_equal(ga[:, 7], ra[:, 7])
+    plain = np_(T.sample_actions(torch.from_numpy(nrm), 31, 3))
+    moved = np.any(bits(ga) != bits(plain), axis=1)
+    assert 0.45 < moved.mean() < 0.55, moved.mean()
+    # flat ground: the direction draws' tangential forces follow the velocity
+    # change s_from -> s_to (FORWARD: s_near -> target, REVERSE: target -> s_near)
+    up = np.tile([0.0, 0.0, 1.0], (n, 1))
+    fa = np_(T.sample_actions_dir(torch.from_numpy(up), torch.from_numpy(target),
+                                  torch.from_numpy(s_near), torch.from_numpy(d), 31, 3, cfg=cfg))
+    fr = oracle.sample_actions_dir(up, target, s_near, d, 31, 3, action_p=0.5, nthreads=8)
+    np.testing.assert_allclose(fa, fr, rtol=1e-12, atol=1e-12)
+    fwd = d == L.FORWARD
+    dv = np.where(fwd[:, None], target[:, 3:5] - s_near[:, 3:5], s_near[:, 3:5] - target[:, 3:5])
+    sgn = np.where(dv > 0, 1.0, -1.0)
+    assert np.all(fa[moved][:, [0, 3]] * sgn[moved][:, [0]] >= 0)
+    assert np.all(fa[moved][:, [1, 4]] * sgn[moved][:, [1]] >= 0)
+    # flag off: exactly getRandomAction(surf_norm)
+    g0 = np_(T.sample_actions_dir(torch.from_numpy(nrm), torch.from_numpy(target),
+                                  torch.from_numpy(s_near), torch.from_numpy(d), 31, 3,
+                                  cfg=L.sampling()))
+    assert np.array_equal(bits(g0), bits(plain))
+
+
+@pytest.mark.parametrize("name", ["synth-rough-256", "rough_terrain-gridmap"])
+def test_extend_with_action_direction_matches_oracle(gpu, name):
+    """newConfig with action_direction_sampling on (rrt.cpp:34, :49): the
+    engine's extend (dev and host entries) equals the oracle's extend on the
+    candidates the engine drew, re-drawn through the public sampler."""
+    data, T, O = pair_of(name)
+    n = 6000
+    s_near, _, d, target, _ = attempts_oracle(O, n, seed=43)
+    base = 2000
+    cfg = L.sampling(action_flag=True, action_p=0.4)
+    T.set_sampling(cfg)
+    try:
+        got = T.get_sampling()
+        assert got.action_flag == 1 and got.action_p == 0.4
+        r = T.extend(torch.from_numpy(s_near), torch.from_numpy(target), torch.from_numpy(d),
+                     seed=43, extend_base=base)
+        rr_h, ch_h, sn_h, an_h, c_h, f_h = T.extend_host(s_near, target, d, seed=43,
+                                                         extend_base=base)
+    finally:
+        T.set_sampling(None)
+    nrm = O.normal_batch(target[:, :2])[0]
+    rep = lambda x: np.repeat(x, 8, axis=0)
+    dense = np_(T.sample_actions_dir(torch.from_numpy(rep(nrm)), torch.from_numpy(rep(target)),
+                                     torch.from_numpy(rep(s_near)), torch.from_numpy(rep(d)), 43,
+                                     0x45585444, base * 8, cfg=cfg)).reshape(n, 8, 10)
+    cand = np.ascontiguousarray(dense[:, :6])
+    rr, rch, rsn, ran, rc = O.extend_batch(s_near, target, cand, d, nthreads=8)
+    acc = rr != L.TRAPPED
+    # _dev: FRAGILE extends (flags) are the caller's to resolve; _host: final
+    fr = (u32(r.flags) & L.F_FRAGILE) != 0
+    assert np.array_equal(np_(r.result)[~fr], rr[~fr])
+    assert np.array_equal(np_(r.chosen)[~fr], rch[~fr])
+    assert np.array_equal(rr_h, rr) and np.array_equal(ch_h, rch) and np.array_equal(c_h, rc)
+    assert np.all(same_f64(sn_h[acc], rsn[acc])) and np.all(same_f64(an_h[acc], ran[acc]))
+    assert (rch >= 0).sum() > 0
+    # some chosen candidates are direction draws
+    plain = np_(T.sample_actions(torch.from_numpy(rep(nrm)), 43, 0x45585444, base * 8)).reshape(n, 8, 10)
+    moved = np.any(bits(dense[:, :6]) != bits(plain[:, :6]), axis=2)
+    ch = rch[rch >= 0]
+    assert moved[np.flatnonzero(rch >= 0), ch].any()
+
+
+DIR_ON = dict(state_flag=True, state_p=0.3, speed_direction=True, action_flag=True, action_p=0.3)
+
+
+@pytest.mark.parametrize("name,xy,batch,seed", [
+    ("synth-rough-256", (1.0, 2.55, 4.02, 2.55), 512, 5),
+    ("slope-gridmap", (1.0, 0.0, 8.0, 0.0), 256, 7),
+])
+def test_device_loop_with_direction_sampling_equals_host_batched(gpu, name, xy, batch, seed):
+    """Both flags on: the device-resident search (targets' s_from / s_to from
+    the device trees, rrt_connect.cpp:248-252, :283-287) builds the same trees
+    and path as the host batched planner (s_from / s_to from the host trees)."""
+    data = td.by_name(name)
+    O = oracle.OracleTerrain.from_data(data)
+    start, goal = _start_goal(O, *xy)
+    cfg = L.sampling(**DIR_ON)
+    host = planner.plan_rrt_connect(data, start, goal, batch=batch, max_time=120.0, seed=seed,
+                                    sampling=cfg)
+    dev = planner.plan_rrt_connect_device(data, start, goal, batch=batch, max_time=120.0, seed=seed,
+                                          sampling=cfg)
+    assert host["found"] == 1 and dev["found"] == 1
+    check_path(O, dev, start, goal)
+    assert np.array_equal(dev["states"], host["states"])
+    assert np.array_equal(dev["actions"], host["actions"])
+    for k in ("vertices_a", "vertices_b", "targets", "extends", "attempts_checked", "connects",
+              "fragile_resolved"):
+        assert dev[k] == host[k], (k, dev[k], host[k])
+    # the flags change the search (same seed, plain sampling)
+    plain = planner.plan_rrt_connect_device(data, start, goal, batch=batch, max_time=120.0,
+                                            seed=seed)
+    assert plain["found"] == 1
+    assert (plain["vertices_a"], plain["vertices_b"], plain["targets"]) != \
+        (dev["vertices_a"], dev["vertices_b"], dev["targets"])
+    print(f"{name}: direction sampling {dev['vertices_a']}+{dev['vertices_b']} vertices, "
+          f"{dev['time_to_first'] * 1e3:.2f} ms; plain {plain['vertices_a']}+{plain['vertices_b']}, "
+          f"{plain['time_to_first'] * 1e3:.2f} ms")
+
+
+def test_sequential_and_anytime_with_direction_sampling(gpu):
+    """The reference's own loop (batch 1 = runRRTConnect, rrt_connect.cpp:230-314)
+    and buildRRTConnect's anytime restarts on the device loop (what the node
+    calls) both plan with params.yaml's thresholds and the flags on."""
+    data = td.synth_rough(256)
+    O = oracle.OracleTerrain.from_data(data)
+    start, goal = _start_goal(O, 1.0, 2.55, 4.02, 2.55)
+    cfg = L.sampling(state_flag=True, state_p=0.05, speed_direction=False, action_flag=True,
+                     action_p=0.1)
+    seq = planner.plan_rrt_connect(data, start, goal, batch=1, max_time=60.0, seed=3, sampling=cfg)
+    check_path(O, seq, start, goal)
+    any_ = planner.plan_rrt_connect_anytime(data, start, goal, max_time_opt=0.2, device_loop=True,
+                                            batch=1024, max_time=60.0, seed=3, sampling=cfg)
+    check_path(O, any_, start, goal)
+
+
+def test_node_callsite_with_direction_flags(gpu, tmp_path):
+    """global_body_planner.cpp's call sequence with params.yaml:21-27's flags
+    true: buildRRTConnect (device-resident, and the sequential engine path)
+    plans; the free getRandomAction / getRandomActionDirection run on the
+    engine (tests/integration/node_callsite.cpp "dir" / "dirseq")."""
+    import subprocess
+    from tests.test_abi import build_node_callsite
+    exe = build_node_callsite(tmp_path / "node_callsite")
+    for mode in ("dir", "dirseq"):
+        r = subprocess.run(["timeout", "-k", "10", "120", exe, mode], capture_output=True, text=True)
+        assert r.returncode == 0, (mode, r.returncode, r.stdout + r.stderr)
+        assert r.stdout.startswith("states ")
