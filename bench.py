@@ -165,6 +165,12 @@ TTFS_PAIRS = {
     "synth-rough-1024": {"start": (1.0, 10.23), "goal": (19.42, 10.23), "reference_s": None,
                          "reference_note": "no solution within 1700 s (BASELINE §2.1)",
                          "batch": 262144 // 6},
+    # the same start, the goal on the start side of the 0.55-m step up at x = 7.0
+    # (the first STANCE-valid point scanning x down from 6.8 along y = 10.23, as
+    # §8(d) scans for the SURVEY goal; tools/wall_check.py)
+    "synth-rough-1024-near": {"terrain": "synth-rough-1024", "start": (1.0, 10.23),
+                              "goal": (6.8, 10.23), "reference_s": None,
+                              "reference_note": "not measured by the survey", "batch": 262144 // 6},
     "synth-rough-256": {"start": (1.0, 2.55), "goal": (4.02, 2.55),
                         "reference_s": [0.05, 1.19, 2.64], "batch": 65536 // 6},
     # config 1: the slope CSV through the grid_map geometry; the
@@ -174,14 +180,14 @@ TTFS_PAIRS = {
 }
 
 
-def time_to_first_solution(data, name, runs, max_time, args, rank, world, dev):
+def time_to_first_solution(data, name, runs, max_time, args, rank, world, dev, pair_key=None):
     """Batch-synchronous RRT-Connect (include/gbp_planner.h) from the pair's
     start to its goal, z = 0.375 + ground, v = (1, 0, 0).  With N ranks each run
     is config 4: one independent tree pair per GPU (seed + rank), first solution
     = min over ranks, best path shared by one all_gather of the fixed-size record."""
     from global_body_planner_amd import planner
     T = gbp.Terrain.from_data(data, device=dev.index)
-    pair = TTFS_PAIRS[name]
+    pair = TTFS_PAIRS[pair_key or name]
     xy = torch.tensor([pair["start"], pair["goal"]], dtype=torch.float64, device=dev)
     h = T.height(xy)[0].cpu().numpy()
     xy = xy.cpu().numpy()
@@ -214,14 +220,17 @@ def time_to_first_solution(data, name, runs, max_time, args, rank, world, dev):
                                                  round(out["extent_b"][0], 2),
                                                  round(out["extent_b"][1], 2)]})
         if k == runs - 1:
-            cost = out["path_length"] if out["found"] else float("nan")
-            rec = sharding.pack_path(cost, out["path_length"], 0.0,
-                                     out["states"] if out["found"] else None,
-                                     out["actions"] if out["found"] else None, device=dev)
-            who, rec = sharding.allgather_best_path(rec)
-            best = {"rank": who, "cost": sharding.unpack_path(rec)["cost"]}
+            # ranked by the reference's path_cost_ (rrt_connect.cpp:304-313, :401)
+            cost = out["path_cost"] if out["found"] else float("nan")
+            who, rec = sharding.gather_best_path(cost, out["path_length"], 0.0,
+                                                 out["states"] if out["found"] else None,
+                                                 out["actions"] if out["found"] else None,
+                                                 device=dev)
+            u = sharding.unpack_path(rec)
+            best = {"rank": who, "cost": u["cost"], "n_states": int(u["states"].shape[0])}
     solved = [r["ttfs_s"] for r in out_runs if np.isfinite(r["ttfs_s"])]
-    res = {"terrain": name, "value": float(np.median(solved)) if solved else None, "unit": "s",
+    res = {"terrain": name, "pair": pair_key or name,
+           "value": float(np.median(solved)) if solved else None, "unit": "s",
            "solved": f"{len(solved)}/{len(out_runs)}", "runs": out_runs, "best_path": best,
            "batch": batch, "max_time_s": max_time,
            "planner": "buildRRTConnectDevice (search resident on the device)"
@@ -443,10 +452,14 @@ def main():
     tot_attempts = float(sums[0].item()) * args.steps
     value = tot_attempts / elapsed
 
-    ttfs = ttfs2 = ttfs1 = None
+    ttfs = ttfs2 = ttfs1 = ttfs_near = None
     if args.ttfs_runs > 0:
         ttfs = time_to_first_solution(data, args.terrain, args.ttfs_runs, args.plan_max_time, args,
                                       rank, world, dev) if args.terrain in TTFS_PAIRS else None
+        if args.terrain == "synth-rough-1024":
+            ttfs_near = time_to_first_solution(data, args.terrain, args.ttfs_runs,
+                                               args.plan_max_time, args, rank, world, dev,
+                                               pair_key="synth-rough-1024-near")
         # config 2 (synth-rough-256), where the reference has wall times to compare with
         ttfs2 = time_to_first_solution(td.by_name("synth-rough-256"), "synth-rough-256", 3, 20.0,
                                        args, rank, world, dev)
@@ -510,6 +523,7 @@ def main():
                        "(distinct batches of the same distribution)" if replay else "one resident batch"),
             "replay": replay,
             "time_to_first_solution": ttfs,
+            "time_to_first_solution_before_wall": ttfs_near,
             "time_to_first_solution_config2": ttfs2,
             "time_to_first_solution_config1": ttfs1,
         }

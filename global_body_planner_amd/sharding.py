@@ -37,26 +37,34 @@ def reduce_run(elapsed_s, counters, device):
     return float(t.item()), [float(v) for v in c.tolist()]
 
 
-def pack_path(cost, length, yaw, states, actions, device="cpu"):
-    """Fixed-size best-path record (states [k, 8], actions [k-1, 10], k <= PATH_MAX)."""
-    rec = torch.full((REC_SIZE,), float("nan"), dtype=torch.float64, device=device)
+def pack_path(cost, length, yaw, states, actions, device="cpu", cap=PATH_MAX):
+    """Fixed-size best-path record of `cap` states (states [k, 8], actions
+    [k-1, 10]).  Never raises: every rank must reach the collective that
+    follows.  A path longer than `cap` gives a record with n_states = -k and
+    cost NaN (it cannot win); gather_best_path sizes the records so that this
+    does not happen."""
+    size = REC_HEADER + cap * 8 + cap * 10
+    rec = torch.full((size,), float("nan"), dtype=torch.float64, device=device)
     k = 0 if states is None else int(len(states))
-    if k > PATH_MAX:
-        raise ValueError(f"path of {k} states exceeds PATH_MAX={PATH_MAX}")
+    if k > cap:
+        rec[1], rec[2], rec[3] = float(length), float(yaw), float(-k)
+        return rec
     rec[0], rec[1], rec[2], rec[3] = float(cost), float(length), float(yaw), float(k)
     if k:
         rec[REC_HEADER:REC_HEADER + 8 * k] = torch.as_tensor(states, dtype=torch.float64).reshape(-1)
         if actions is not None and len(actions):
             a = torch.as_tensor(actions, dtype=torch.float64).reshape(-1)
-            off = REC_HEADER + PATH_MAX * 8
+            off = REC_HEADER + cap * 8
             rec[off:off + a.numel()] = a
     return rec
 
 
 def unpack_path(rec):
+    cap = (rec.numel() - REC_HEADER) // 18
     k = int(rec[3].item()) if rec[3] == rec[3] else 0
+    k = max(k, 0)  # a truncated record (-k) carries no states
     states = rec[REC_HEADER:REC_HEADER + 8 * k].reshape(k, 8)
-    off = REC_HEADER + PATH_MAX * 8
+    off = REC_HEADER + cap * 8
     actions = rec[off:off + 10 * max(k - 1, 0)].reshape(max(k - 1, 0), 10)
     return {"cost": float(rec[0]), "length": float(rec[1]), "yaw": float(rec[2]),
             "states": states, "actions": actions}
@@ -64,7 +72,8 @@ def unpack_path(rec):
 
 def allgather_best_path(rec):
     """all_gather every rank's record; every rank picks argmin(cost), ties to the
-    lowest rank.  NaN cost = no solution."""
+    lowest rank.  NaN cost = no solution.  Records must
+    have the same size on every rank."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return 0, rec
     world = dist.get_world_size()
@@ -76,3 +85,22 @@ def allgather_best_path(rec):
         if c == c and c < best_cost:
             best, best_cost = r, c
     return best, out[best]
+
+
+def gather_best_path(cost, length, yaw, states, actions, device="cpu"):
+    """Config 4's exchange (rrt_connect.cpp:401-414 across ranks): one
+    all_reduce(MAX) of the path lengths sizes the records (at least PATH_MAX
+    states), then one all_gather of every rank's record; argmin of the
+    reference's path_cost_ (length, or the cost_add_yaw weighted sum), ties to
+    the lowest rank.  No rank can fail between the two collectives.  Returns
+    (winning rank, its record)."""
+    k = 0 if states is None else int(len(states))
+    cap = PATH_MAX
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        t = torch.tensor([float(k)], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        cap = max(cap, int(t.item()))
+    else:
+        cap = max(cap, k)
+    rec = pack_path(cost, length, yaw, states, actions, device=device, cap=cap)
+    return allgather_best_path(rec)

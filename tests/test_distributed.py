@@ -34,12 +34,15 @@ def _worker(rank, world, port, q):
         v, sn, tn, f, c = O.validate_pairs(s, a, d, nthreads=2)
         gv = int(((c & 0xFFFF) + (c >> 16)).sum())
         el, sums = sharding.reduce_run(0.1 * (rank + 1), [n, int(v.sum()), gv], "cpu")
-        # config 4: every rank proposes a path, rank 1 has the lower cost
-        states = np.full((3, 8), float(rank))
-        acts = np.full((2, 10), float(rank))
-        rec = sharding.pack_path(10.0 - rank, 5.0, 0.1, states, acts)
-        best, brec = sharding.allgather_best_path(rec)
-        q.put((rank, el, sums, best, sharding.unpack_path(brec)["states"].numpy().tolist()))
+        # config 4: every rank proposes a path, rank 1 has the lower cost and a
+        # path longer than PATH_MAX (the records are sized first: no rank raises
+        # before the all_gather, the long path travels whole)
+        k = 3 if rank == 0 else sharding.PATH_MAX + 44
+        states = np.full((k, 8), float(rank))
+        acts = np.full((k - 1, 10), float(rank))
+        best, brec = sharding.gather_best_path(10.0 - rank, 5.0, 0.1, states, acts)
+        u = sharding.unpack_path(brec)
+        q.put((rank, el, sums, best, u["states"].numpy().tolist(), u["actions"].shape[0]))
     finally:
         dist.destroy_process_group()
 
@@ -68,9 +71,11 @@ def test_gloo_world2_sharding_and_best_path():
     s, a, d, _, _ = attempts_oracle(O, 1400, seed=99, nthreads=2)
     v, sn, tn, f, c = O.validate_pairs(s, a, d, nthreads=2)
     assert res[0][2] == [1400.0, float(v.sum()), float(((c & 0xFFFF) + (c >> 16)).sum())]
-    # best path: rank 1's record (cost 9 < 10) on both ranks
+    # best path: rank 1's record (cost 9 < 10, 300 states) on both ranks
+    k = 256 + 44
     assert res[0][3] == 1 and res[1][3] == 1
-    assert res[0][4] == res[1][4] == [[1.0] * 8] * 3
+    assert res[0][4] == res[1][4] == [[1.0] * 8] * k
+    assert res[0][5] == res[1][5] == k - 1
 
 
 def test_pack_unpack_roundtrip():
@@ -83,3 +88,11 @@ def test_pack_unpack_roundtrip():
     assert u["cost"] == 3.5 and np.array_equal(u["states"].numpy(), st)
     assert np.array_equal(u["actions"].numpy(), ac)
     assert sharding.strong_shard(1, 3, 10) == (3, 3)
+    # a path past the record's capacity gives an unusable record instead of raising
+    t = sharding.pack_path(1.0, 2.0, 0.0, np.zeros((sharding.PATH_MAX + 1, 8)),
+                           np.zeros((sharding.PATH_MAX, 10)))
+    ut = sharding.unpack_path(t)
+    assert np.isnan(ut["cost"]) and ut["states"].shape == (0, 8)
+    # a sized record holds it (single process: no collective)
+    who, rec = sharding.gather_best_path(1.0, 2.0, 0.0, np.ones((300, 8)), np.ones((299, 10)))
+    assert who == 0 and sharding.unpack_path(rec)["states"].shape == (300, 8)

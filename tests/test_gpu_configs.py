@@ -4,12 +4,14 @@ Config 4 — "1024x1024 rough_terrain, 8 independent restart trees sharded
 1-per-GPU, RCCL best-path allgather" (rrt_connect.cpp:350-425):
 world-size-2 processes (gloo here; bench.py runs the same code over RCCL), both
 on cuda:0, each running one independent tree pair of the device-resident
-planner (seed + rank), then one all_gather of the fixed-size best-path record
-(sharding.allgather_best_path).  Every rank must hold the same argmin record
+planner (seed + rank), then the sized best-path exchange
+(sharding.gather_best_path: all_reduce(MAX) of the path lengths, one
+all_gather, argmin of path_cost).  Every rank must hold the same argmin record
 (ties to the lowest rank), and the record's path must pass the oracle's edge
-checks.  The config-2 start/goal pair is used: synth-rough-1024's goal sits
-beyond the nearest-neighbour-upsampled walls no planner has crossed
-(DESIGN.md §8), so a solvable pair is needed to compare paths.
+checks.  Two pairs: config 2's (synth-rough-256) and config 4's own terrain
+with the goal on the start side of the 0.55-m step at x = 7.0 (the SURVEY
+pair's goal lies past it and past a 0.65-m drop at x = 11.2:
+tools/wall_check.py).
 
 Config 5 — "4096x4096 synthetic fractal terrain, RRT*-Connect rewire with
 k-nearest wavefront scan" (rrt_star_connect.cpp:12-75): pair-check and
@@ -41,25 +43,24 @@ def _free_port():
     return p
 
 
-def _config4_worker(rank, world, port, q):
+def _config4_worker(rank, world, port, q, name, xy, batch):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import global_body_planner_amd as gbp
         from global_body_planner_amd import planner, sharding
-        data = td.synth_rough(256)
+        data = td.by_name(name)
         T = gbp.Terrain.from_data(data, device=0)
-        h = T.height_host([[1.0, 2.55], [4.02, 2.55]])[0]
-        start = planner.start_goal_state(h[0], 1.0, 2.55)
-        goal = planner.start_goal_state(h[1], 4.02, 2.55)
-        out = planner.plan_rrt_connect_device(data, start, goal, batch=1024, max_time=60.0,
+        h = T.height_host([[xy[0], xy[1]], [xy[2], xy[3]]])[0]
+        start = planner.start_goal_state(h[0], xy[0], xy[1])
+        goal = planner.start_goal_state(h[1], xy[2], xy[3])
+        out = planner.plan_rrt_connect_device(data, start, goal, batch=batch, max_time=60.0,
                                               seed=20251019 + rank, post_process=True)
         cost = out["path_cost"] if out["found"] else float("nan")
-        rec = sharding.pack_path(cost, out["path_length"], 0.0,
-                                 out["states"] if out["found"] else None,
-                                 out["actions"] if out["found"] else None)
-        best, brec = sharding.allgather_best_path(rec)
+        best, brec = sharding.gather_best_path(cost, out["path_length"], 0.0,
+                                               out["states"] if out["found"] else None,
+                                               out["actions"] if out["found"] else None)
         u = sharding.unpack_path(brec)
         q.put((rank, bool(out["found"]), cost, best, u["cost"], u["states"].numpy(),
                u["actions"].numpy(), start, goal))
@@ -67,13 +68,20 @@ def _config4_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_config4_restart_trees_best_path_allgather(gpu):
+@pytest.mark.parametrize("name,xy,batch", [
+    ("synth-rough-256", (1.0, 2.55, 4.02, 2.55), 1024),
+    # config 4's own terrain, the goal on the start side of the 0.55-m step at
+    # x = 7.0 (bench.py TTFS_PAIRS "synth-rough-1024-near", tools/wall_check.py)
+    ("synth-rough-1024", (1.0, 10.23, 6.8, 10.23), 8192),
+])
+def test_config4_restart_trees_best_path_allgather(gpu, name, xy, batch):
     import torch.multiprocessing as mp
     from tests.test_gpu_planner import check_path
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_config4_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_config4_worker, args=(r, 2, port, q, name, xy, batch))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=240) for _ in procs)
@@ -86,13 +94,76 @@ def test_config4_restart_trees_best_path_allgather(gpu):
     for r in res:
         assert r[3] == want and r[4] == costs[want]
         assert np.array_equal(r[5], res[0][5]) and np.array_equal(r[6], res[0][6])
-    data = td.synth_rough(256)
+    data = td.by_name(name)
     O = oracle.OracleTerrain.from_data(data)
     S, A = res[0][5], res[0][6]
     out = {"found": 1, "states": S, "actions": A,
            "path_duration": float(np.sum(A[:, 6] + A[:, 7]))}
     check_path(O, out, res[0][7], res[0][8])
-    print(f"config 4 (2 ranks): costs {costs}, best rank {want}, {len(S)} states")
+    print(f"config 4 (2 ranks, {name}): costs {costs}, best rank {want}, {len(S)} states")
+
+
+def _throughput_worker(rank, world, port, q, per_rank, seed):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import global_body_planner_amd as gbp
+        from global_body_planner_amd import sharding
+        from global_body_planner_amd import workload as W
+        T = gbp.Terrain.from_data(td.synth_rough(256), device=0)
+        base, n = sharding.weak_shard(rank, per_rank)
+        s, a, d, _, _ = W.make_attempts(T, n, seed, index_base=base)
+        r = T.validate_pairs(s, a, d)
+        torch.cuda.synchronize()
+        c = u32(r.counts).astype(np.int64)
+        gv = int(((c & 0xFFFF) + (c >> 16)).sum())
+        el, sums = sharding.reduce_run(0.5 + rank, [n, int(r.valid.sum().item()), gv], "cpu")
+        q.put((rank, el, sums, r.valid.cpu().numpy(), r.s_new.cpu().numpy(), r.t_new.cpu().numpy(),
+               u32(r.flags), u32(r.counts)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_engine_weak_sharding_world2(gpu):
+    """The throughput configs' multi-GPU path on the engine: two
+    ranks (gloo, both on cuda:0) each generate their weak shard
+    [r B, (r + 1) B) of the Philox stream on the device and validate it; the
+    only cross-rank traffic is reduce_run (MAX time, SUM counters).  The summed
+    counters equal the single-process 2B batch, and each rank's outputs are
+    bit-identical to the matching half of that batch."""
+    import global_body_planner_amd as gbp
+    import torch.multiprocessing as mp
+    from global_body_planner_amd import workload as W
+    per, seed = 16384, W.CONFIG_SEEDS[2]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_throughput_worker, args=(r, 2, port, q, per, seed)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    T = gbp.Terrain.from_data(td.synth_rough(256), device=0)
+    s, a, d, _, _ = W.make_attempts(T, 2 * per, seed)
+    ref = T.validate_pairs(s, a, d)
+    torch.cuda.synchronize()
+    rv, rsn, rtn = ref.valid.cpu().numpy(), ref.s_new.cpu().numpy(), ref.t_new.cpu().numpy()
+    rf, rc = u32(ref.flags), u32(ref.counts)
+    c = rc.astype(np.int64)
+    want = [2.0 * per, float(rv.sum()), float(((c & 0xFFFF) + (c >> 16)).sum())]
+    for r in res:
+        assert r[1] == 1.5 and r[2] == want   # MAX of the elapsed times, SUM of the counters
+        sl = slice(r[0] * per, (r[0] + 1) * per)
+        assert np.array_equal(r[3], rv[sl]) and np.array_equal(r[6], rf[sl])
+        assert np.array_equal(r[7], rc[sl])
+        sn_set = (rf[sl] & L.F_SNEW_SET) != 0
+        tn_set = (rf[sl] & L.F_TNEW_SET) != 0
+        assert np.array_equal(r[4][sn_set].view(np.uint64), rsn[sl][sn_set].view(np.uint64))
+        assert np.array_equal(r[5][tn_set].view(np.uint64), rtn[sl][tn_set].view(np.uint64))
+    print(f"weak shards: 2 x {per} attempts, {int(want[1])} valid, {int(want[2])} lookups")
 
 
 _fractal = {}

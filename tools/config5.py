@@ -64,9 +64,9 @@ def main():
                                         seed=a.seed + rank, device=local)
     found = bool(out["found"])
     cost = out["path_cost"] if found else float("nan")
-    rec = sharding.pack_path(cost, out["path_length"], 0.0, out["states"] if found else None,
-                             out["actions"] if found else None, device=dev)
-    who, best = sharding.allgather_best_path(rec)
+    who, best = sharding.gather_best_path(cost, out["path_length"], 0.0,
+                                          out["states"] if found else None,
+                                          out["actions"] if found else None, device=dev)
     ttf = torch.tensor([out["time_to_first"] if found else float("inf")], dtype=torch.float64,
                        device=dev)
     work = torch.tensor([float(out["attempts_checked"]), float(out["rewires"]),
