@@ -215,7 +215,7 @@ class Terrain:
               "set_sampling")
 
     def get_sampling(self):
-        cfg = _lib.Sampling()
+        cfg = L.Sampling()
         check(self._lib.gbp_terrain_get_sampling(self._h, ctypes.byref(cfg)), "get_sampling")
         return cfg
 
