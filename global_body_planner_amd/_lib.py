@@ -156,7 +156,11 @@ def load(path=None):
         "gbp_neighbors_batch_host": (I, [I64, P, I64, P, ctypes.c_double, I, P, P]),
     }
     for name, (res, args) in sig.items():
-        f = getattr(L, name)
+        f = getattr(L, name, None)
+        if f is None:
+            if path is None:  # the product library must export the whole ABI
+                raise AttributeError(f"{p}: missing symbol {name}")
+            continue  # a diagnostic build of an older ABI (tools/lib_ab.py)
         f.restype = res
         f.argtypes = args
     if path is None:

@@ -62,6 +62,7 @@ struct TerrainView {
   const double *dx, *dy, *dz;    // slope layers, x-major fp64, may be null
   int nx, ny;
   double x0, xN, y0, yN;         // x[0], x[nx-1], y[0], y[ny-1]
+  double xNm, yNm;               // x[nx-2], y[ny-2]: the last cell's lower lines
   double inv_hx, inv_hy;         // 1 / mean spacing (bracket guess only)
   int one_x, one_y;              // host-verified: the guess is within one cell of the
                                  // bracket for every v (gbp_terrain_create), so a single
@@ -154,12 +155,15 @@ __device__ __forceinline__ int bracket_ax(const TerrainView<ZT> &T, double v, in
   const double d0 = AX == 0 ? T.x0 : T.y0, dN = AX == 0 ? T.xN : T.yN;
   const int n = AX == 0 ? T.nx : T.ny;
   if constexpr (ONE) {
-    const bool in = (v >= d0) & (v < dN), hi = v >= dN;
-    const double vc = in ? v : d0;  // no bracket: guess from d0 (guess 0, correction 0)
+    const bool in = (v >= d0) & (v < dN);
+    // the point clamped into [d[0], d[n-2]]: itself in the domain, d[0] below
+    // it or for NaN (fmax returns the non-NaN operand), d[n-2] at or above
+    // d[n-1] — whose brackets are the cells above (guess 0 / n-2, exact)
+    const double vc = fmin(fmax(v, d0), AX == 0 ? T.xNm : T.yNm);
     int i = bracket_guess(n, d0, AX == 0 ? T.inv_hx : T.inv_hy, vc);
     i += (vc >= coord<CM, AX>(T, i + 1) ? 1 : 0) - (vc < coord<CM, AX>(T, i) ? 1 : 0);
-    cell = in ? i : (hi ? n - 2 : 0);
-    return in ? i : (hi ? BR_HIGH : BR_LOW);
+    cell = i;
+    return in ? i : (v >= dN ? BR_HIGH : BR_LOW);
   }
   const int r = bracket_ax<CM, AX, false>(T, v);
   cell = r >= 0 ? r : (r == BR_HIGH ? n - 2 : 0);

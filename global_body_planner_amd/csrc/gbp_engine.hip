@@ -912,6 +912,8 @@ int gbp_terrain_create(int device, int nx, int ny, const double *x, const double
   t->bounds[1] = x[nx - 1];
   t->bounds[2] = y[0];
   t->bounds[3] = y[ny - 1];
+  t->xNm = x[nx - 2];
+  t->yNm = y[ny - 2];
   t->inv_hx = (x[nx - 1] > x[0]) ? (double)(nx - 1) / (x[nx - 1] - x[0]) : 0.0;
   t->inv_hy = (y[ny - 1] > y[0]) ? (double)(ny - 1) / (y[ny - 1] - y[0]) : 0.0;
   t->one_x = one_step_exact(x, nx, t->inv_hx);

@@ -23,6 +23,7 @@ struct gbp_terrain {
   int nx = 0, ny = 0;
   int storage = GBP_STORAGE_F64;
   double bounds[4] = {0, 0, 0, 0};
+  double xNm = 0, yNm = 0;          // x[nx-2], y[ny-2]
   double inv_hx = 0, inv_hy = 0;
   int one_x = 0, one_y = 0;         // one-step bracket correction is exact (verified)
   double *d_x = nullptr, *d_y = nullptr;
@@ -89,6 +90,8 @@ inline gbp::TerrainView<ZT> view(const gbp_terrain *t) {
   v.xN = t->bounds[1];
   v.y0 = t->bounds[2];
   v.yN = t->bounds[3];
+  v.xNm = t->xNm;
+  v.yNm = t->yNm;
   v.inv_hx = t->inv_hx;
   v.inv_hy = t->inv_hy;
   v.one_x = t->one_x;
