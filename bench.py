@@ -64,9 +64,10 @@ def parse():
     p.add_argument("--terrain", default="synth-rough-1024")
     p.add_argument("--seed", type=int, default=W.CONFIG_SEEDS[3])
     p.add_argument("--kernel", choices=["persistent", "direct"], default="persistent")
-    p.add_argument("--waves", type=int, default=3,
-                   help="waves per SIMD of the headline's validate launches (3: best with the "
-                        "launches overlapping on --streams; the planner's serial launches keep 2)")
+    p.add_argument("--waves", type=int, default=2,
+                   help="waves per SIMD of the headline's validate launches (2: best alone and "
+                        "overlapped on --streams since the kernel holds one bracket form, "
+                        "profiles/r03f_wave_sweep.jsonl)")
     p.add_argument("--streams", type=int, default=2,
                    help="HIP streams the K independent steps are issued on round-robin (1: serial)")
     p.add_argument("--adaptive", action="store_true")

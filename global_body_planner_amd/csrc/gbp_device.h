@@ -276,11 +276,15 @@ __device__ __forceinline__ void probe(const TerrainView<ZT> &T, double x, double
 }
 
 // heightIsNan on a probe: -1 = UB (BR_HIGH), else the reference's bool
+// Branch-free (bitwise ors, a select): the cell's heights are then used on
+// every path, so the compiler keeps the probe's fetch with the others instead
+// of sinking it under the BR_HIGH test and waiting on it at once (the centre
+// probe's gather was issued and waited for alone, before the rotation).
 template <class ZT>
 __device__ __forceinline__ int probe_nan(const Probe<ZT> &p) {
-  if (p.ix == BR_HIGH || p.iy == BR_HIGH) return -1;
-  return (isnan((double)p.q[0]) || isnan((double)p.q[1]) || isnan((double)p.q[2]) ||
-          isnan((double)p.q[3])) ? 1 : 0;
+  const bool high = (p.ix == BR_HIGH) | (p.iy == BR_HIGH);
+  const bool nan4 = isnan(p.q[0]) | isnan(p.q[1]) | isnan(p.q[2]) | isnan(p.q[3]);
+  return high ? -1 : (nan4 ? 1 : 0);
 }
 
 // getGroundHeight on a probe (same contract as height_at)
@@ -521,21 +525,14 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
   }
   acc.V++;
   const double eps = T.feps, hmin = H_MIN, hmax = H_MAX, hl = 0.5 * ROBOT_L, hw = 0.5 * ROBOT_W;
-  Probe<ZT> pc;
-  probe<ZT, CM, ONE>(T, s[0], s[1], pc);
   const bool outside = (s[0] < T.x0) || (s[0] > T.xN) || (s[1] < T.y0) || (s[1] > T.yN);
   const double speed = sqrt(s[3] * s[3] + s[4] * s[4]);
-  uint32_t fl = 0;
-  // (1) heightIsNan(centre) :564 (x or y >= the last coordinate: UB, rejected
-  //     by (2) unless exactly equal)
-  const int r = probe_nan(pc);
-  if (r < 0 && !outside) fl |= GBP_F_OOD;
-  if (r > 0) fl |= GBP_F_NAN;
-  // (2) bounds + |pitch| :568-571, (3) horizontal speed :574
-  bool alive = r == 0 && !(outside || (fabs(s[6]) >= P_MAX)) && !(speed > V_MAX);
-  // (4) rotation :578-594
+  // (4) rotation :578-594, formed first so that the centre's gather is issued
+  // with the nine others (one round trip per state check, not two)
   double cy, sy, cp, sp;
   rotation_trig_nolibm(s[3], s[4], speed, s[6], cy, sy, cp, sp);
+  Probe<ZT> pc;
+  probe<ZT, CM, ONE>(T, s[0], s[1], pc);
   // A state heading along +x with zero pitch (dy = +-0, dx > 0, p = +-0: every
   // start / goal state of the reference node, global_body_planner.cpp:219-264)
   // has exactly glibc's trig values: atan2(+-0, dx) = +-0 -> (1, +-0), and
@@ -559,6 +556,14 @@ __device__ bool is_valid_state(const TerrainView<ZT> &T, const double *s, int ph
   }
   const double ux = s[0] + R_13 * z_body, uy = s[1] + R_23 * z_body;
   probe<ZT, CM, ONE>(T, ux, uy, pu);
+  uint32_t fl = 0;
+  // (1) heightIsNan(centre) :564 (x or y >= the last coordinate: UB, rejected
+  //     by (2) unless exactly equal)
+  const int r = probe_nan(pc);
+  if (r < 0 && !outside) fl |= GBP_F_OOD;
+  if (r > 0) fl |= GBP_F_NAN;
+  // (2) bounds + |pitch| :568-571, (3) horizontal speed :574
+  bool alive = r == 0 && !(outside || (fabs(s[6]) >= P_MAX)) && !(speed > V_MAX);
   uint32_t G = 0;
   // (5) four corners :601-627, x_body outer, y_body inner, in reference order
 #pragma unroll

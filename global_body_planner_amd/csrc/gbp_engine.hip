@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256, W) void k_validate_direct(
 // (lane state machine: gbp_lane.h)
 
 
-template <class ZT, bool ADAPTIVE, int W, int CM>
+template <class ZT, bool ADAPTIVE, int W, int CM, bool ONE>
 __global__ __launch_bounds__(512, W) void k_validate_persistent(
     TerrainView<ZT> T0, int n, const double *__restrict__ S, const double *__restrict__ A,
     const uint8_t *__restrict__ dir, int dir_all, uint8_t *__restrict__ valid,
@@ -174,7 +174,6 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
   double *const SA = gbp_smem + (CM == 1 ? (T0.nx + T0.ny + 1) & ~1 : 0);  // attempt rows
   double *const wave_rows = SA + (size_t)(threadIdx.x & ~(WAVE - 1)) * SA_ROW;
-  const bool one = T0.one_x && T0.one_y;  // wave-uniform: straight-line brackets
   Lane L;
   L.s = SA + (size_t)threadIdx.x * SA_ROW;
   L.a = L.s + 8;
@@ -258,8 +257,9 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
     if (has) {
       double sc[8];
       sample_state(ps, ps + 8, st, t_eval, sc);
-      ok = one ? is_valid_state<ZT, CM, true>(T, sc, stage_phase(st), acc_s)
-               : is_valid_state<ZT, CM, false>(T, sc, stage_phase(st), acc_s);
+      // ONE (a template parameter, so the kernel holds one bracket form and
+      // its registers): the terrain's one-step guess is exact on both axes
+      ok = is_valid_state<ZT, CM, ONE>(T, sc, stage_phase(st), acc_s);
     }
     bool decided = false;
     if (owner) {  // the lane's own sample
@@ -634,10 +634,14 @@ int validate_coord_mode(const gbp_terrain *t, bool direct) {
                         (stage_bytes(t->nx, t->ny) + rows);
   const bool lds_ok = t->opt_lds_coords && stage_bytes(t->nx, t->ny) + rows <= t->lds_max &&
                       (direct || per_cu <= 160 * 1024);
+  // the persistent kernel's LDS / computed modes are instantiated with the
+  // straight-line bracket only: a terrain whose one-step guess is not exact
+  // on both axes reads its vectors from global memory (general search)
+  if (!direct && !(t->one_x && t->one_y)) return 0;
   return coord_mode(t, lds_ok);
 }
 
-template <class ZT, bool AD, int W, int CM>
+template <class ZT, bool AD, int W, int CM, bool ONE>
 int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *a,
                       const uint8_t *dir, int dir_all, uint8_t *valid, double *s_new,
                       double *t_new, uint32_t *flags, uint32_t *counts, hipStream_t st,
@@ -670,7 +674,7 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
       // waves starting with idle lanes that help from the first step
       // (65,536 attempts: 0.084 -> 0.072 ms; 262,144: unchanged)
       const int64_t g = std::max<int64_t>(1, std::min<int64_t>(resident, (m + WAVE - 1) / WAVE));
-      hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, CM>), dim3((unsigned)g), dim3(block),
+      hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, CM, ONE>), dim3((unsigned)g), dim3(block),
                          coords + rows, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
                          flags + off, c, n_dev, (int)t->opt_helpers,
                          (int)t->opt_xcd_map);
@@ -685,22 +689,24 @@ int launch_validate(gbp_terrain *t, int64_t n, const double *s, const double *a,
                     const uint8_t *dir, int dir_all, int adaptive, uint8_t *valid,
                     double *s_new, double *t_new, uint32_t *flags, uint32_t *counts,
                     hipStream_t st, const int *n_dev = nullptr) {
-#define GBP_LV(AD, W)                                                                       \
-  (cm == 2 ? launch_validate_w<ZT, AD, W, 2>(t, n, s, a, dir, dir_all, valid, s_new, t_new,  \
-                                             flags, counts, st, n_dev)                       \
-   : cm == 1 ? launch_validate_w<ZT, AD, W, 1>(t, n, s, a, dir, dir_all, valid, s_new, t_new, \
-                                               flags, counts, st, n_dev)                     \
-             : launch_validate_w<ZT, AD, W, 0>(t, n, s, a, dir, dir_all, valid, s_new, t_new, \
-                                               flags, counts, st, n_dev))
+#define GBP_LVW(AD, W, CM, ONE)                                                              \
+  launch_validate_w<ZT, AD, W, CM, ONE>(t, n, s, a, dir, dir_all, valid, s_new, t_new, flags,  \
+                                        counts, st, n_dev)
+#define GBP_LV(AD, W)                                                                        \
+  (cm == 2 ? GBP_LVW(AD, W, 2, true)                                                         \
+   : cm == 1 ? GBP_LVW(AD, W, 1, true)                                                       \
+             : (one ? GBP_LVW(AD, W, 0, true) : GBP_LVW(AD, W, 0, false)))
   const int64_t w = t->opt_waves;
   // coordinates computed when the affine form is exact; else in LDS only if
   // they fit next to the attempt rows, with room for the W workgroups of 256
   // lanes that share a CU (160 KB per CU); else read from global memory
   const int cm = validate_coord_mode(t, t->opt_kernel == GBP_KERNEL_DIRECT && !n_dev);
+  const bool one = t->one_x && t->one_y;  // straight-line brackets (modes 1, 2 imply it)
   // W = 1 and 2 give the same allocation (the kernel needs < 256 VGPRs)
   if (adaptive) return w >= 4 ? GBP_LV(true, 4) : (w == 3 ? GBP_LV(true, 3) : GBP_LV(true, 2));
   return w >= 4 ? GBP_LV(false, 4) : (w == 3 ? GBP_LV(false, 3) : GBP_LV(false, 2));
 #undef GBP_LV
+#undef GBP_LVW
 }
 
 bool valid_handle(const gbp_terrain *t) { return t != nullptr && t->d_z != nullptr; }

@@ -141,8 +141,12 @@ __device__ __forceinline__ void sample_state(const double *s_in, const double *a
     o[3] = b[3] - a[0] * d1 - q2[0];
     o[4] = b[4] - a[1] * d1 - q2[1];
     o[5] = b[5] - a[2] * d1 - q2[2];
-    o[7] = b[7] - a[8] * d1 - q2[3];
+    // (the reference assigns [7] before [6]; the values are independent.  The
+    // stores follow the forward branch's order so that the compiler's sinking
+    // of the two branches' last stores meets one address, not a phi of two,
+    // which would index the caller's state array dynamically: scratch)
     o[6] = b[6] - cp * d1 - 0.5 * a[8] * d2 - q6[3];
+    o[7] = b[7] - a[8] * d1 - q2[3];
     return;
   }
   // planning_utils.cpp:262-271
