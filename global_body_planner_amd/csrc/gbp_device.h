@@ -283,7 +283,7 @@ __device__ __forceinline__ void probe(const TerrainView<ZT> &T, double x, double
 template <class ZT>
 __device__ __forceinline__ int probe_nan(const Probe<ZT> &p) {
   const bool high = (p.ix == BR_HIGH) | (p.iy == BR_HIGH);
-  const bool nan4 = isnan(p.q[0]) | isnan(p.q[1]) | isnan(p.q[2]) | isnan(p.q[3]);
+  const bool nan4 = (int)isnan(p.q[0]) | (int)isnan(p.q[1]) | (int)isnan(p.q[2]) | (int)isnan(p.q[3]);
   return high ? -1 : (nan4 ? 1 : 0);
 }
 

@@ -67,6 +67,21 @@ struct gbp_tree {
   double *g = nullptr;        // [cap] cost to come: g[parent] + poseDistance
   int32_t *parent = nullptr;  // [cap], -1 at the root
   int32_t *count = nullptr;   // [1] number of vertices (device resident)
+  // nearest-neighbour index (gbp_tree_index_build, k_nn_pruned): the first
+  // idx_n vertices sorted by the Morton key of (x, y), chunks of NN_CH rows
+  // with 8-D boxes of their fp32 rows and a representative (middle) row each
+  int32_t idx_n = 0;          // vertices indexed (even; 0: no index)
+  int64_t idx_cap = 0;        // rows the index arrays hold
+  float *isp = nullptr;       // [idx_cap/2][NN_PAIR] indexed rows in key order (row pairs)
+  int32_t *isid = nullptr;    // [idx_cap] vertex index of sorted row p
+  double *isv = nullptr;      // [idx_cap][8] the fp64 vertices in key order (exact stage)
+  float *ibox = nullptr;      // [idx_cap/NN_CH + 1][16] chunk boxes: lo[8], hi[8]
+  float *imed = nullptr;      // [idx_cap/NN_CH/2 + 1][NN_PAIR] each chunk's middle row
+  uint32_t *ikey = nullptr;   // [2 idx_cap] sort keys in / out
+  int32_t *ival = nullptr;    // [idx_cap] sort values in (out: isid)
+  void *isort = nullptr;      // radix-sort scratch
+  size_t isort_bytes = 0;
+  double ibounds[4] = {0, 1, 0, 1};  // the keys' (x, y) quantisation box (also the queries')
 };
 
 struct gbp_plan_ws {
@@ -104,6 +119,10 @@ struct gbp_plan_ws {
   // nearest-neighbour partials: NN_MAX_CHUNKS * bmax slots, pd[c * nq + qi]
   double *nn_d = nullptr;
   int32_t *nn_i = nullptr;
+  // indexed search (k_nnq_*, k_nn_pruned): queries bucketed by Morton cell
+  int32_t *bcnt = nullptr;     // [NN_QCELLS] queries per Morton cell (zeroed after each search)
+  int32_t *bq = nullptr;       // [NN_QCELLS][bmax] each cell's query indices
+  float *qpt = nullptr;        // [bmax] per query: the chunk-pruning threshold
   void *block = nullptr;       // the one allocation all of the above live in
 };
 
@@ -241,26 +260,6 @@ __global__ __launch_bounds__(TB) void k_targets(TerrainView<ZT> T, gbp_plan_stat
     atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_TARGETS);
     st->halt_half = half;
     raise_gate(st, seq);
-  }
-}
-
-__global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int64_t n,
-                                                        const double *__restrict__ cand,
-                                                        const uint32_t *__restrict__ cflag,
-                                                        double *__restrict__ targets,
-                                                        unsigned long long *tiles, uint32_t epoch,
-                                                        uint64_t seq) {
-  if (gated(st, seq)) return;
-  const int64_t i = blockIdx.x * (int64_t)CB + threadIdx.x;
-  const bool keep = i < n && (cflag[i] & GBP_F_VALID);
-  const uint32_t r = ordered_rank(keep, tiles, epoch, &st->n_targets, st);
-  if (keep) copy8(targets + 8 * (size_t)r, cand + 8 * i);
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
-    // the extend stream of this half: RRTClass::extend_counter_ advances by
-    // the number of extends (csrc/host/gbp_planner.cpp extendBatch)
-    st->ext_base = st->ext_counter;
-    st->ext_counter += st->n_targets;
-    st->stat_targets += st->n_targets;
   }
 }
 
@@ -650,6 +649,485 @@ __global__ __launch_bounds__(TB) void k_nn_reduce(const gbp_plan_status *st, con
     }
     if (lane == 0) out[qi] = bc < nch ? pi[bc * nq + qi] : 0;
   }
+}
+
+// ============================================================================
+// nearest neighbour through the tree's index (gbp_tree_index_build)
+// ============================================================================
+// The index holds the tree's first idx_n vertices sorted by the Morton key of
+// (x, y), cut into chunks of NN_CH rows; per chunk the fp32 rows' 8-D box
+// [lo, hi] and its middle row.  A search with many queries (the targets'
+// nearest vertices, stage 2):
+//   k_nnq_hist / k_nnq_scatter_ub  bucket the queries by Morton cell (a wave
+//        then holds 64 queries from one small area) and give each query an
+//        upper bound on its nearest distance: the fp32 filter's minimum over
+//        the chunks' middle rows, turned into a rigorous pruning threshold
+//        PT (below);
+//   k_nn_pruned  item = (wave of 64 cell-sorted queries, segment of chunks):
+//        pass 1 scans (fp32 dot form, as k_nn_filter) only the chunks whose
+//        box lower bound LB2 <= PT for some lane, tightening PT with each
+//        scanned chunk's minimum; pass 2 revisits the chunks that still pass
+//        and records the candidates S_j <= T(B); the exact fp64 distances of
+//        the candidates decide.  The vertices appended since the index was
+//        built (the tail) form one more segment, scanned in full;
+//   k_nn_reduce_idx  lexicographic (distance, vertex index) minimum over the
+//        segments: the reference's ascending scan with strict <.
+// Why a pruned chunk cannot hold the answer (notation of the k_nn_filter
+// proof above; P_j = |f_j - g|^2 in fp32 space, exact):
+//   * a box holds its chunk's fp32 rows, so LB2 = sum_k max(lo_k - g_k,
+//     g_k - hi_k, 0)^2 <= P_j for each of them; evaluated in fp32 (two
+//     subtractions rounded up by at most (1+u), eight FMAs) the computed
+//     LB2c <= P_j (1 + 10.1u);
+//   * for any row i with fp32 value S_i (B = S_i, or the minimum over rows),
+//     the fp64 minimiser j* satisfies sqrt(P_j*) <= r1(B) (the threshold
+//     proof: D_j* <= D_i (1 + 3e-15)), and so does every index tying with it;
+//   * PT = r1(B)^2 (1 + 1e-12)(1 + 16u), rounded up to fp32.  A chunk with
+//     LB2c > PT has P_j > r1^2 for all its rows: neither j* nor a tie is in it.
+// Rows scanned in pass 1 but not needed by a lane only lower its B (still a
+// real row: the bound holds).  A query or tree magnitude >= 1e15, or more
+// than NN_CAND candidates, sends the wave to the fp64 scan of its segment.
+constexpr int NN_CH = 64;          // rows per index chunk
+constexpr int NN_QBITS = 4;        // query cells: 2^4 x 2^4 Morton cells
+constexpr int NN_QCELLS = 1 << (2 * NN_QBITS);
+// Items of a search: per wave of 64 cell-sorted queries, NN_SORTED_SEGS
+// segments of R <= 256 chunks each (R >= 16: the mask phase's R iterations
+// stay short; at most 4 blocks of 64 chunk boxes) and the unindexed tail in
+// segments of >= 256 rows; all of them partial slots (NN_MAX_CHUNKS).
+constexpr int NN_SORTED_SEGS = 24;
+constexpr int NN_SEG_BLOCKS = 4;
+constexpr int NN_TAIL_ROWS = 256;
+constexpr int64_t NN_INDEX_MAX_ROWS = (int64_t)NN_SORTED_SEGS * NN_SEG_BLOCKS * WAVE * NN_CH;
+
+struct NnIdxGeom {
+  int R;      // chunks per sorted segment
+  int nseg;   // sorted segments
+  int ts;     // rows per tail segment (even)
+  int ntail;  // tail segments
+};
+__device__ __forceinline__ NnIdxGeom nn_idx_geometry(int64_t nc, int64_t tail) {
+  NnIdxGeom g;
+  int64_t R = 16;
+  if ((nc + R - 1) / R > NN_SORTED_SEGS) R = (nc + NN_SORTED_SEGS - 1) / NN_SORTED_SEGS;
+  g.R = (int)R;
+  g.nseg = nc > 0 ? (int)((nc + R - 1) / R) : 0;
+  const int64_t slots = NN_MAX_CHUNKS - g.nseg;
+  int64_t ts = (tail + slots - 1) / slots;
+  if (ts < NN_TAIL_ROWS) ts = NN_TAIL_ROWS;
+  g.ts = (int)((ts + 1) & ~(int64_t)1);
+  g.ntail = tail > 0 ? (int)((tail + g.ts - 1) / g.ts) : 0;
+  return g;
+}
+
+__device__ __forceinline__ uint32_t spread16(uint32_t v) {  // bit i -> bit 2i
+  v &= 0xFFFFu;
+  v = (v | (v << 8)) & 0x00FF00FFu;
+  v = (v | (v << 4)) & 0x0F0F0F0Fu;
+  v = (v | (v << 2)) & 0x33333333u;
+  v = (v | (v << 1)) & 0x55555555u;
+  return v;
+}
+// (x, y) quantised to `bits` per axis over bounds {x0, xN, y0, yN}, clamped;
+// NaN goes to the last cell
+__device__ __forceinline__ uint32_t morton_key(double x, double y, const double *bd, int bits) {
+  const double sc = (double)(1u << bits);
+  const double ux = (x - bd[0]) / (bd[1] - bd[0]) * sc, uy = (y - bd[2]) / (bd[3] - bd[2]) * sc;
+  const uint32_t hi = (1u << bits) - 1u;
+  const uint32_t qx = isnan(ux) ? hi : (ux <= 0.0 ? 0u : (ux >= (double)hi ? hi : (uint32_t)ux));
+  const uint32_t qy = isnan(uy) ? hi : (uy <= 0.0 ? 0u : (uy >= (double)hi ? hi : (uint32_t)uy));
+  return (spread16(qx) << 1) | spread16(qy);
+}
+
+// PT above from a filter minimum B (fp32 S space); g2 = |g|^2, r2 = R^2.
+// B = +inf (nothing finite scanned) gives +inf: no chunk can be pruned
+__device__ __forceinline__ float nn_prune_threshold(float B, double g2, double r2) {
+  const double eps = 10.0 * 0x1p-24 * r2, del = 2.0 * 0x1p-24 * sqrt(r2);
+  const double r0 = sqrt(fmax(0.0, (double)B + g2 + eps));
+  const double r1 = (r0 + del) * (1.0 + 4e-15) + del;
+  const double pt = r1 * r1 * (1.0 + 1e-12) * (1.0 + 16.0 * 0x1p-24);
+  return isinf(pt) || isnan(pt) ? INFINITY : nextafterf((float)pt, INFINITY);
+}
+
+// lane u's value for the whole wave (v_readlane: an SGPR operand)
+__device__ __forceinline__ float lane_bcast(float x, int u) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), u));
+}
+
+// LB2c of the query g (fp32) against a chunk box
+__device__ __forceinline__ float nn_box_lb2(const float (&g)[8], const float *__restrict__ box) {
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const float d = fmaxf(fmaxf(box[k] - g[k], g[k] - box[8 + k]), 0.f);
+    acc = fmaf(d, d, acc);
+  }
+  return acc;
+}
+
+// |g|^2 and R^2 of a query (g = -a / 2 exactly), R with the tree's vmax
+__device__ __forceinline__ void nn_g2r2(const float (&a)[8], const float *__restrict__ vmax,
+                                        double &g2, double &r2) {
+  g2 = 0.0;
+  r2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const double ak = fabs(-0.5 * (double)a[k]), mk = (double)vmax[k];
+    g2 = g2 + ak * ak;
+    r2 = r2 + (mk + ak) * (mk + ak);
+  }
+}
+
+__global__ void k_idx_keys(const double *__restrict__ v, int64_t n, double bx0, double bxN,
+                           double by0, double byN, uint32_t *__restrict__ keys,
+                           int32_t *__restrict__ ids) {
+  const double bd[4] = {bx0, bxN, by0, byN};
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    keys[j] = morton_key(v[8 * j], v[8 * j + 1], bd, 16);
+    ids[j] = (int32_t)j;
+  }
+}
+
+// the sorted rows in the filter's pair format and in fp64 (from the vertices)
+__global__ void k_idx_rows(const double *__restrict__ v, const int32_t *__restrict__ sid, int64_t n,
+                           float *__restrict__ sp, double *__restrict__ sv) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    const double *r = v + 8 * (int64_t)sid[p];
+    nn_put_row(sp, p, r);
+    copy8(sv + 8 * p, r);
+  }
+}
+
+// per chunk: the box of its fp32 rows (NaN components skipped: a NaN row is
+// never a nearest vertex) and its middle row
+__global__ void k_idx_boxes(const float *__restrict__ sp, int64_t n, float *__restrict__ box,
+                            float *__restrict__ med) {
+  const int64_t nc = (n + NN_CH - 1) / NN_CH;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nc;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j0 = c * NN_CH, j1 = min(n, j0 + NN_CH);
+    float lo[8], hi[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      lo[k] = INFINITY;
+      hi[k] = -INFINITY;
+    }
+    for (int64_t j = j0; j < j1; j++) {
+      const float *r = sp + NN_PAIR * (j >> 1) + (j & 1);
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        lo[k] = fminf(lo[k], r[2 * k]);
+        hi[k] = fmaxf(hi[k], r[2 * k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      box[16 * c + k] = lo[k];
+      box[16 * c + 8 + k] = hi[k];
+    }
+    const int64_t m = j0 + (j1 - j0 - 1) / 2;
+    const float *r = sp + NN_PAIR * (m >> 1) + (m & 1);
+    float *o = med + NN_PAIR * (c >> 1) + (c & 1);
+#pragma unroll
+    for (int k = 0; k < 8; k++) o[2 * k] = r[2 * k];
+    o[16] = r[16];
+    if ((c & 1) == 0 && c + 1 == nc) {  // the last pair's empty slot: never a minimum
+#pragma unroll
+      for (int k = 0; k < 8; k++) o[2 * k + 1] = __builtin_nanf("");
+      o[17] = __builtin_nanf("");
+    }
+  }
+}
+
+// The indexed search's query side (NnBucket): query r goes to the bucket of
+// its Morton cell (bq[cell][slot], any order within a cell) and gets its
+// chunk-pruning threshold from the fp32 filter's minimum over the index's
+// middle rows.  k_nn_pruned walks the buckets in Morton order (a prefix over
+// bcnt), so its waves hold 64 queries from one small area.  Called for the
+// compacted targets inside k_compact_targets, else by k_nnq_bucket.
+struct NnBucket {
+  int32_t *bcnt, *bq;
+  float *qpt;
+  const float *imed, *vmax;
+  int nc;
+  int64_t cap;
+  double bd[4];
+};
+
+// every lane of the wave must call this (the middle-row scan is wave-uniform)
+template <int UNR>
+__device__ __forceinline__ void nn_bucket_query(const NnBucket &nb, const double *__restrict__ x,
+                                                int64_t r, bool live) {
+  float a[1][8];
+  bool qnan = false;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const double v = live ? x[k] : 0.0;
+    a[0][k] = -2.0f * (float)v;
+    qnan = qnan || isnan(v);
+  }
+  if (live) {
+    const uint32_t cell = morton_key(x[0], x[1], nb.bd, NN_QBITS);
+    nb.bq[(int64_t)cell * nb.cap + atomicAdd(&nb.bcnt[cell], 1)] = (int32_t)r;
+  }
+  float B[1] = {INFINITY}, T[1] = {0.f};
+  int cnt[1] = {0};
+  nn_sweep<UNR, 0, 1>(a, nb.imed, 0, nb.nc, B, T, cnt, nullptr);
+  double g2, r2;
+  nn_g2r2(a[0], nb.vmax, g2, r2);
+  // a NaN query has no nearest vertex (index 0, the reduce's default):
+  // threshold -1 excludes every chunk
+  if (live) nb.qpt[r] = qnan ? -1.0f : nn_prune_threshold(B[0], g2, r2);
+}
+
+__global__ __launch_bounds__(TB) void k_nnq_bucket(const gbp_plan_status *__restrict__ st,
+                                                   const int32_t *__restrict__ nq_dev,
+                                                   const double *__restrict__ q,
+                                                   const int32_t *__restrict__ q_off_dev, NnBucket nb,
+                                                   uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t nq = *nq_dev, q_off = q_off_dev ? *q_off_dev : 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t iters = (nq + stride - 1) / stride;  // whole waves run the middle-row scan
+  for (int64_t it = 0; it < iters; it++) {
+    const int64_t i = it * stride + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    nn_bucket_query<4>(nb, q + 8 * (q_off + (i < nq ? i : 0)), i, i < nq);
+  }
+}
+
+// the compacted targets (stage 1).  (Bucketing them for the indexed search
+// here as well was measured slower: the 43 tiles' middle-row scans and the
+// cell-count atomics made the compaction 10 -> 62 us.)
+__global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int64_t n,
+                                                        const double *__restrict__ cand,
+                                                        const uint32_t *__restrict__ cflag,
+                                                        double *__restrict__ targets,
+                                                        unsigned long long *tiles, uint32_t epoch,
+                                                        uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t i = blockIdx.x * (int64_t)CB + threadIdx.x;
+  const bool keep = i < n && (cflag[i] & GBP_F_VALID);
+  const uint32_t r = ordered_rank(keep, tiles, epoch, &st->n_targets, st);
+  if (keep) copy8(targets + 8 * (size_t)r, cand + 8 * i);
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    // the extend stream of this half: RRTClass::extend_counter_ advances by
+    // the number of extends (csrc/host/gbp_planner.cpp extendBatch)
+    st->ext_base = st->ext_counter;
+    st->ext_counter += st->n_targets;
+    st->stat_targets += st->n_targets;
+  }
+}
+
+// the fp64 scan of rows [j0, j1) of a row set whose vertex indices are ids[]
+// (nullptr: the rows are vertices j0..j1-1): lexicographic (distance, index)
+__device__ __forceinline__ void nn_scan64_ids(const double qq[8], const double *__restrict__ v,
+                                              const int32_t *__restrict__ ids, int j0, int j1,
+                                              double &best, int &bi) {
+  for (int j = j0; j < j1; j++) {
+    const int vj = ids ? ids[__builtin_amdgcn_readfirstlane(j)] : j;
+    const double d = nn_dist64(qq, v + 8 * (int64_t)__builtin_amdgcn_readfirstlane(vj));
+    if (d < best || (d == best && vj < bi)) {
+      best = d;
+      bi = vj;
+    }
+  }
+}
+
+// Item (query wave, segment).  Mask phase: the segment's chunk boxes, 64 at a
+// time, in the VGPRs of lanes 0..63 (one coalesced load); each chunk's box
+// broadcast by v_readlane, every lane tests its own query, and the chunks
+// some lane cannot exclude form one 64-bit ballot per block.  Then pass 1 and
+// pass 2 of the filter run over the masked chunks only (row pairs by scalar
+// load, as k_nn_filter), and the candidates are decided in fp64.  Tail
+// segments scan their rows in full.
+template <int UNR>
+__global__ __launch_bounds__(TB) void k_nn_pruned(
+    const gbp_plan_status *__restrict__ st, const int32_t *__restrict__ nq_dev,
+    const double *__restrict__ q, const int32_t *__restrict__ q_off_dev,
+    const int32_t *__restrict__ bcnt, const int32_t *__restrict__ bq, int64_t bcap,
+    const float *__restrict__ qpt, const double *__restrict__ v, const float *__restrict__ vf,
+    const float *__restrict__ vmax, const int32_t *__restrict__ nv_dev,
+    const float *__restrict__ isp, const int32_t *__restrict__ isid, const double *__restrict__ isv,
+    const float *__restrict__ ibox, int idx_n, double *__restrict__ pd, int32_t *__restrict__ pi,
+    uint64_t seq) {
+  if (gated(st, seq)) return;
+  __shared__ int32_t cand[1][NN_CAND][TB];
+  __shared__ int32_t bpre[NN_QCELLS + 1];  // bucket prefix: queries before each cell
+  const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
+  if (threadIdx.x == 0) {  // NN_QCELLS is small: one thread
+    int32_t acc = 0;
+    for (int c = 0; c < NN_QCELLS; c++) {
+      bpre[c] = acc;
+      acc += bcnt[c];
+    }
+    bpre[NN_QCELLS] = acc;
+  }
+  __syncthreads();
+  const int nc = (idx_n + NN_CH - 1) / NN_CH;
+  const NnIdxGeom G = nn_idx_geometry(nc, nv - idx_n);
+  const int nslot = G.nseg + G.ntail;
+  const int64_t nqw = (nq + WAVE - 1) / WAVE, nitems = nqw * nslot;
+  bool tree_bad = false;
+#pragma unroll
+  for (int k = 0; k < 8; k++) tree_bad = tree_bad || !(vmax[k] < 1e15f);
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t wstride = (int64_t)gridDim.x * (TB / WAVE);
+  // the item and everything derived from it are wave-uniform; readfirstlane
+  // tells the compiler so, and the row pairs then arrive by scalar load
+  const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+  for (int64_t item = blockIdx.x * (int64_t)(TB / WAVE) + wid; item < nitems; item += wstride) {
+    // slot-major order: a wave's consecutive items are different query waves
+    // of the same segment (their chunk boxes and rows shared in the caches)
+    const int sg = (int)(item / nqw);
+    const int64_t wq = item - (int64_t)sg * nqw;
+    const int64_t p = wq * WAVE + lane;
+    const bool live = p < nq;
+    // the p-th query in cell order: its cell by binary search of the prefix
+    int lo = 0, hi = NN_QCELLS;  // bpre[lo] <= p < bpre[hi]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (bpre[mid] <= p) lo = mid; else hi = mid;
+    }
+    const int64_t qi = live ? bq[(int64_t)lo * bcap + (p - bpre[lo])] : 0;
+    const double *qrow = q + 8 * (q_off + qi);
+    float a[1][8], g[8];
+    bool bad = tree_bad;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const double x = live ? qrow[k] : 0.0;
+      a[0][k] = -2.0f * (float)x;
+      g[k] = (float)x;
+      bad = bad || (live && !(fabs(x) < 1e15));
+    }
+    const bool sorted = sg < G.nseg;
+    // the item's rows: sorted chunks [c0, c1) or tail rows [r0, r1)
+    const int c0 = sorted ? sg * G.R : 0, c1 = sorted ? min(nc, (sg + 1) * G.R) : 0;
+    const float *rows = sorted ? isp : vf;
+    const int32_t *ids = sorted ? isid : nullptr;
+    const int t0 = idx_n + (sg - G.nseg) * G.ts;
+    const int r0 = sorted ? c0 * NN_CH : t0;
+    const int r1 = sorted ? min(idx_n, c1 * NN_CH) : (int)min(nv, (int64_t)t0 + G.ts);
+    double best = INFINITY;
+    int bi = -1;
+    bool scan64 = __ballot(bad) != 0ull;
+    int cnt[1] = {0};
+    if (!scan64 && r0 < r1) {
+      uint64_t cm[NN_SEG_BLOCKS];
+      if (sorted) {
+        const float pt = live ? qpt[qi] : -1.0f;
+#pragma unroll
+        for (int b = 0; b < NN_SEG_BLOCKS; b++) {
+          cm[b] = 0;
+          const int cb = c0 + b * WAVE;
+          if (cb >= c1) continue;
+          const int nb = min(WAVE, c1 - cb);
+          float bx[16];
+          const float4 *src = (const float4 *)(ibox + 16 * (int64_t)(cb + min(lane, nb - 1)));
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const float4 t4 = src[r];
+            bx[4 * r] = t4.x;
+            bx[4 * r + 1] = t4.y;
+            bx[4 * r + 2] = t4.z;
+            bx[4 * r + 3] = t4.w;
+          }
+          uint64_t m = 0;
+          for (int u = 0; u < nb; u++) {
+            float box[16];  // chunk cb + u, broadcast
+#pragma unroll
+            for (int k = 0; k < 16; k++) box[k] = lane_bcast(bx[k], u);
+            if (__ballot(nn_box_lb2(g, box) <= pt)) m |= 1ull << u;
+          }
+          cm[b] = m;
+        }
+      }
+      float B[1] = {INFINITY}, T[1] = {0.f};
+      double g2, r2;
+      nn_g2r2(a[0], vmax, g2, r2);
+      // pass 1: B over the masked chunks (the tail: all its rows)
+      if (sorted) {
+#pragma unroll
+        for (int b = 0; b < NN_SEG_BLOCKS; b++)
+          for (uint64_t m = cm[b]; m; m &= m - 1) {
+            const int c = c0 + b * WAVE + __builtin_ctzll(m);
+            nn_sweep<UNR, 0, 1>(a, rows, c * NN_CH, min(idx_n, (c + 1) * NN_CH), B, T, cnt, cand);
+          }
+      } else {
+        nn_sweep<UNR, 0, 1>(a, rows, r0, r1, B, T, cnt, cand);
+      }
+      T[0] = live ? nn_threshold(B[0], g2, r2) : -1.0f;
+      // pass 2: the candidates S_j <= T(B) of the same rows
+      if (sorted) {
+#pragma unroll
+        for (int b = 0; b < NN_SEG_BLOCKS; b++)
+          for (uint64_t m = cm[b]; m; m &= m - 1) {
+            const int c = c0 + b * WAVE + __builtin_ctzll(m);
+            nn_sweep<UNR, 1, 1>(a, rows, c * NN_CH, min(idx_n, (c + 1) * NN_CH), B, T, cnt, cand);
+          }
+      } else {
+        nn_sweep<UNR, 1, 1>(a, rows, r0, r1, B, T, cnt, cand);
+      }
+      scan64 = __ballot(cnt[0] > NN_CAND) != 0ull;
+    }
+    double qq[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) qq[k] = live ? qrow[k] : 0.0;
+    if (scan64) {
+      nn_scan64_ids(qq, v, ids, r0, r1, best, bi);
+    } else {
+      // candidates: rows of the sorted copy (isv) or of the tree (tail);
+      // distances first, vertex indices only for the ones that could win
+      const double *rv = sorted ? isv : v;
+      for (int m = 0; m < cnt[0]; m++) {
+        const int r = cand[0][m][threadIdx.x];
+        const double d = nn_dist64(qq, rv + 8 * (int64_t)r);
+        if (d <= best) {
+          const int j = sorted ? ids[r] : r;
+          if (d < best || j < bi) {
+            best = d;
+            bi = j;
+          }
+        }
+      }
+    }
+    if (live) {
+      pd[sg * nq + qi] = best;
+      pi[sg * nq + qi] = bi;
+    }
+  }
+}
+
+// lexicographic (distance, index) minimum over a query's segments; nothing
+// finite (a NaN query, or no row): index 0, as the reference keeps it.  Also
+// clears the query buckets' counts for the next search.
+__global__ __launch_bounds__(TB) void k_nn_reduce_idx(const gbp_plan_status *st,
+                                                      const int32_t *nq_dev,
+                                                      const int32_t *nv_dev, int idx_n,
+                                                      const double *__restrict__ pd,
+                                                      const int32_t *__restrict__ pi,
+                                                      int32_t *__restrict__ out,
+                                                      int32_t *__restrict__ bcnt, uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t nq = *nq_dev;
+  const NnIdxGeom G = nn_idx_geometry((idx_n + NN_CH - 1) / NN_CH, *nv_dev - idx_n);
+  const int nslot = G.nseg + G.ntail;
+  for (int64_t qi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; qi < nq;
+       qi += (int64_t)gridDim.x * blockDim.x) {
+    double best = INFINITY;
+    int bi = 0;
+    for (int sg = 0; sg < nslot; sg++) {
+      const double d = pd[sg * nq + qi];
+      const int j = pi[sg * nq + qi];
+      if (j >= 0 && (d < best || (d == best && j < bi))) {
+        best = d;
+        bi = j;
+      }
+    }
+    out[qi] = bi;
+  }
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < NN_QCELLS;
+       c += (int64_t)gridDim.x * blockDim.x)
+    bcnt[c] = 0;
 }
 
 // ============================================================================
@@ -1076,8 +1554,35 @@ uint32_t next_epoch(gbp_plan_ws *w) {
 
 unsigned tiles_for(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + CB - 1) / CB); }
 
+NnBucket nn_bucket_args(gbp_plan_ws *w, const gbp_tree *tr) {
+  NnBucket nb;
+  nb.bcnt = w->bcnt;
+  nb.bq = w->bq;
+  nb.qpt = w->qpt;
+  nb.imed = tr->imed;
+  nb.vmax = tr->vmax;
+  nb.nc = (tr->idx_n + NN_CH - 1) / NN_CH;
+  nb.cap = w->bmax;
+  for (int k = 0; k < 4; k++) nb.bd[k] = tr->ibounds[k];
+  return nb;
+}
+
+// use_index: the search goes through tr's index
 int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
-              const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s) {
+              const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s, bool use_index = false) {
+  if (use_index && tr->idx_n > 0) {
+    // the indexed search: queries bucketed by Morton cell, pruned chunk scans
+    const unsigned gq = grid_for(w->bmax, TB, num_cus * 4);
+    hipLaunchKernelGGL(k_nnq_bucket, dim3(gq), dim3(TB), 0, s, w->st, nq_dev, q, q_off_dev,
+                       nn_bucket_args(w, tr), ++w->seq);
+    hipLaunchKernelGGL((k_nn_pruned<4>), dim3(num_cus * 8), dim3(TB), 0, s, w->st, nq_dev, q,
+                       q_off_dev, w->bcnt, w->bq, w->bmax, w->qpt, tr->v, tr->vf, tr->vmax,
+                       tr->count, tr->isp, tr->isid, tr->isv, tr->ibox, tr->idx_n, w->nn_d, w->nn_i,
+                       ++w->seq);
+    hipLaunchKernelGGL(k_nn_reduce_idx, dim3(gq), dim3(TB), 0, s, w->st, nq_dev, tr->count,
+                       tr->idx_n, w->nn_d, w->nn_i, out, w->bcnt, ++w->seq);
+    return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
+  }
   // two queries per lane, four row pairs per scalar load, 8 workgroups per
   // CU: the fastest of {1, 2, 4} pairs x {1, 2} queries x {4, 8} workgroups
   // per CU on trees past ~20k vertices (profiles/r02j_nn_dot.txt)
@@ -1106,7 +1611,10 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     hipLaunchKernelGGL(k_compact_targets, dim3(tiles_for(batch)), dim3(CB), 0, s, st, batch,
                        w->cand, w->cflag, w->targets, w->tiles, next_epoch(w), ++w->seq);
   if (first_stage <= 2 && last_stage >= 2) {
-    int rc = nn_launch(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s);
+    // the targets' nearest vertices through T's index when GBP_OPT_NN_INDEX
+    // asks for it and the index holds at least that many vertices
+    const bool idx = t->opt_nn_index > 0 && T->idx_n >= t->opt_nn_index;
+    int rc = nn_launch(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, idx);
     if (rc) return rc;
     const int64_t mmax = batch * GBP_NUM_GEN_STATES;
     hipLaunchKernelGGL(k_extend_prep<ZT>, dim3(grid_for(mmax, TB, cus * 8)), dim3(TB), 0, s, V, st,
@@ -1253,7 +1761,8 @@ int gbp_tree_destroy(gbp_tree *t) {
   if (!t) return GBP_E_BAD_HANDLE;
   Guard g(t->device);
   (void)hipDeviceSynchronize();
-  void *ptrs[] = {t->v, t->vf, t->a, t->g, t->parent, t->count, t->vmax};
+  void *ptrs[] = {t->v,    t->vf,   t->a,    t->g,    t->parent, t->count, t->vmax, t->isp,
+                  t->isid, t->isv,  t->ibox, t->imed, t->ikey,   t->ival,  t->isort};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   delete t;
@@ -1370,6 +1879,88 @@ int gbp_tree_device_ptrs(gbp_tree *t, double **states, int32_t **count) {
   return GBP_OK;
 }
 
+int gbp_tree_index_build(gbp_tree *t, const double *bounds, gbp_stream stream) {
+  if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
+  int64_t n = 0;
+  int rc = gbp_tree_size(t, &n, stream);
+  if (rc) return rc;
+  Guard g(t->device);
+  hipStream_t s = (hipStream_t)stream;
+  n &= ~(int64_t)1;  // whole row pairs: the tail then starts on a pair
+  n = std::min<int64_t>(n, NN_INDEX_MAX_ROWS);
+  if (n < 2) {
+    t->idx_n = 0;
+    return GBP_OK;
+  }
+  double bd[4];
+  if (bounds) {
+    for (int k = 0; k < 4; k++) bd[k] = bounds[k];
+  } else {  // the tree's own |x|, |y| bound
+    float vm[2];
+    if ((rc = d2h(vm, t->vmax, 2, s))) return rc;
+    HIPCHK_P(hipStreamSynchronize(s));
+    bd[0] = -(double)vm[0];
+    bd[1] = (double)vm[0];
+    bd[2] = -(double)vm[1];
+    bd[3] = (double)vm[1];
+  }
+  if (!(bd[1] > bd[0]) || !(bd[3] > bd[2]) || !std::isfinite(bd[1] - bd[0]) ||
+      !std::isfinite(bd[3] - bd[2])) {
+    bd[0] = bd[2] = 0.0;  // degenerate (one point, NaN): one key for all, still exact
+    bd[1] = bd[3] = 1.0;
+  }
+  if (n > t->idx_cap) {  // grow (contents rebuilt below)
+    const int64_t cap = std::max<int64_t>(n, 2 * t->idx_cap);
+    const int64_t nc = cap / NN_CH + 2;
+    void *old[] = {t->isp, t->isid, t->isv, t->ibox, t->imed, t->ikey, t->ival, t->isort};
+    HIPCHK_P(hipStreamSynchronize(s));
+    for (void *p : old)
+      if (p) (void)hipFree(p);
+    t->isp = nullptr;
+    t->isid = t->ival = nullptr;
+    t->isv = nullptr;
+    t->ibox = t->imed = nullptr;
+    t->ikey = nullptr;
+    t->isort = nullptr;
+    t->idx_cap = 0;
+    t->idx_n = 0;
+    size_t sort_bytes = 0;
+    if ((rc = gbp_internal_sort_pairs_u32(nullptr, &sort_bytes, nullptr, nullptr, nullptr, nullptr,
+                                          cap, s)))
+      return rc;
+    if (hipMalloc(&t->isp, 4 * NN_PAIR * ((cap + 1) / 2)) != hipSuccess ||
+        hipMalloc(&t->isid, 4 * cap) != hipSuccess || hipMalloc(&t->isv, 64 * cap) != hipSuccess ||
+        hipMalloc(&t->ibox, 64 * nc) != hipSuccess ||
+        hipMalloc(&t->imed, 4 * NN_PAIR * (nc / 2 + 1)) != hipSuccess ||
+        hipMalloc(&t->ikey, 8 * cap) != hipSuccess || hipMalloc(&t->ival, 4 * cap) != hipSuccess ||
+        hipMalloc(&t->isort, std::max<size_t>(sort_bytes, 256)) != hipSuccess)
+      return GBP_E_ALLOC;
+    t->isort_bytes = std::max<size_t>(sort_bytes, 256);
+    t->idx_cap = cap;
+  }
+  const unsigned gr = grid_for(n, TB, 4096);
+  hipLaunchKernelGGL(k_idx_keys, dim3(gr), dim3(TB), 0, s, t->v, n, bd[0], bd[1], bd[2], bd[3],
+                     t->ikey, t->ival);
+  size_t sb = t->isort_bytes;
+  if ((rc = gbp_internal_sort_pairs_u32(t->isort, &sb, t->ikey, t->ikey + t->idx_cap, t->ival,
+                                        t->isid, n, s)))
+    return rc;
+  hipLaunchKernelGGL(k_idx_rows, dim3(gr), dim3(TB), 0, s, t->v, t->isid, n, t->isp, t->isv);
+  hipLaunchKernelGGL(k_idx_boxes, dim3(grid_for((n + NN_CH - 1) / NN_CH, 64, 4096)), dim3(64), 0, s,
+                     t->isp, n, t->ibox, t->imed);
+  HIPCHK_P(hipGetLastError());
+  t->idx_n = (int32_t)n;
+  for (int k = 0; k < 4; k++) t->ibounds[k] = bd[k];
+  return GBP_OK;
+}
+
+int gbp_tree_index_size(gbp_tree *t, int64_t *indexed) {
+  if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
+  if (!indexed) return GBP_E_INVALID_ARG;
+  *indexed = t->idx_n;
+  return GBP_OK;
+}
+
 int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   if (!t || !out) return GBP_E_INVALID_ARG;
   if (max_batch < 1 || max_batch > (1 << 24)) return GBP_E_INVALID_ARG;
@@ -1384,7 +1975,8 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   const int64_t b = max_batch, m = GBP_NUM_GEN_STATES * max_batch;
   const size_t bytes = sizeof(gbp_plan_status) + 8 * w->ntiles + 64 * b + 4 * b + 64 * b + 4 * b +
                        m * (64 + 80 + 64 + 4 + 4) + b * (4 + 4 + 64 + 80 + 4 + 4) +
-                       b * (4 + 4 + 64 + 80 + 4) + NN_MAX_CHUNKS * b * (8 + 4) + 64 * 256;
+                       b * (4 + 4 + 64 + 80 + 4) + NN_MAX_CHUNKS * b * (8 + 4) +
+                       4 * NN_QCELLS + 4 * NN_QCELLS * b + 4 * b + 64 * 256;
   if (hipMalloc(&w->block, bytes) != hipSuccess) {
     delete w;
     return GBP_E_ALLOC;
@@ -1414,7 +2006,11 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->kf = carve<uint32_t>(p, b);
   w->nn_d = carve<double>(p, NN_MAX_CHUNKS * b);
   w->nn_i = carve<int32_t>(p, NN_MAX_CHUNKS * b);
-  if ((size_t)(p - (char *)w->block) > bytes || hipMemset(w->tiles, 0, 8 * w->ntiles) != hipSuccess) {
+  w->bcnt = carve<int32_t>(p, NN_QCELLS);
+  w->bq = carve<int32_t>(p, (size_t)NN_QCELLS * b);
+  w->qpt = carve<float>(p, b);
+  if ((size_t)(p - (char *)w->block) > bytes || hipMemset(w->tiles, 0, 8 * w->ntiles) != hipSuccess ||
+      hipMemset(w->bcnt, 0, 4 * NN_QCELLS) != hipSuccess) {
     (void)hipFree(w->block);
     delete w;
     return GBP_E_HIP;
@@ -1561,7 +2157,8 @@ int gbp_tree_nearest_dev(gbp_plan_ws *w, gbp_tree *T, int64_t n, const double *q
   Guard g(w->device);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_set_queries, dim3(1), dim3(1), 0, s, w->st, (int32_t)n);
-  return nn_launch(w, &w->st->n_targets, queries, nullptr, T, index, w->num_cus, s);
+  return nn_launch(w, &w->st->n_targets, queries, nullptr, T, index, w->num_cus, s,
+                   T->idx_n > 0);
 }
 
 int gbp_plan_resolve_host(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int direction,

@@ -396,6 +396,20 @@ class DeviceTree:
         check(self._lib.gbp_tree_append_host(self._h, s.shape[0], _np_ptr(s), _np_ptr(a), _np_ptr(p),
                                              None), "tree_append")
 
+    def build_index(self, bounds=None):
+        """gbp_tree_index_build: index the tree's vertices for pruned nearest-
+        neighbour searches (bounds = (x0, xN, y0, yN) of the Morton key, None:
+        the tree's own |x|, |y| bound).  Returns the number of vertices indexed."""
+        b = None if bounds is None else np.ascontiguousarray(bounds, np.float64).reshape(4)
+        check(self._lib.gbp_tree_index_build(self._h, None if b is None else _np_ptr(b), None),
+              "tree_index_build")
+        return self.index_size()
+
+    def index_size(self):
+        c = ctypes.c_int64(0)
+        check(self._lib.gbp_tree_index_size(self._h, ctypes.byref(c)), "tree_index_size")
+        return c.value
+
     def read(self):
         """(states [n][8], actions [n][10], parents [n], g [n]) numpy."""
         n = len(self)

@@ -149,6 +149,12 @@ int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage,
                                     1e-12, the smallest accepted): a wider margin flags
                                     and re-decides more attempts on the host, with the
                                     same results (tests use it to force host resolutions) */
+#define GBP_OPT_NN_INDEX     16  /* v > 0: the device planner loop finds the targets'
+                                    nearest vertices through a tree's index
+                                    (gbp_tree_index_build) once it holds >= v vertices;
+                                    0 (default): the full filtered scan, measured faster
+                                    at the planner's tree sizes.  Same
+                                    results either way.                              */
 #define GBP_KERNEL_DIRECT     0  /* one lane per attempt                              */
 #define GBP_KERNEL_PERSISTENT 1  /* persistent waves, lanes re-packed per sample      */
 int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value);
@@ -384,6 +390,19 @@ int gbp_tree_append_host(gbp_tree *tree, int64_t n, const double *states, const 
  * (n <= its max_batch). */
 int gbp_tree_nearest_dev(gbp_plan_ws *ws, gbp_tree *tree, int64_t n, const double *queries,
                          int32_t *index, gbp_stream stream);
+/* The tree's nearest-neighbour index: PlannerClass::getNearestNeighbor
+ * (planner_class.cpp:185-200) made sub-linear for searches with many queries.
+ * Vertices [0, n) — n = the tree's size now, rounded down to even; the call
+ * synchronises the stream — are sorted by the Morton key of (x, y) over
+ * bounds = {x0, xN, y0, yN} (NULL: the tree's own |x|, |y| bound) and cut into
+ * chunks of 64 with the 8-D box of their fp32 rows.  gbp_tree_nearest_dev and
+ * the planner loop's target searches then skip every chunk whose box is
+ * provably farther than a known vertex and scan the vertices appended since
+ * the build in full: the same indices as without the index, ties included.
+ * Rebuild as the tree grows (buildRRTConnectDevice does once the unindexed
+ * tail exceeds an eighth of the index). */
+int gbp_tree_index_build(gbp_tree *tree, const double *bounds, gbp_stream stream);
+int gbp_tree_index_size(gbp_tree *tree, int64_t *indexed);
 /* the tree's device arrays (for gbp_nearest_batch_dev and the like): READ ONLY —
  * vertices are written through init / append only, which also keep the fp32
  * mirror and magnitude bound the nearest-neighbour filter relies on */

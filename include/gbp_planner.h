@@ -599,6 +599,8 @@ typedef struct {
                           // params.yaml:21-27); all zero = off, the reference default
   int64_t fragile_eps_fm; // FRAGILE margin in 1e-15 units (GBP_OPT_FRAGILE_EPS); 0 = default
   int adaptive;           // state_action_pair_check_adaptive_step_size_flag (params.yaml:16)
+  int64_t nn_index;       // GBP_OPT_NN_INDEX: trees of at least this many vertices search
+                          // through their index (0 = the handle's default, off; < 0 = off)
 } gbp_plan_params;
 
 typedef struct {

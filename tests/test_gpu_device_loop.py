@@ -50,6 +50,34 @@ def test_device_loop_equals_host_batched(gpu, name, xy, batch, seed):
           f"{dev['time_to_first']:.4f} s in {dev['status_reads']} status reads")
 
 
+@pytest.mark.parametrize("name,xy,batch,seed,nn_index", [
+    ("synth-rough-256", (1.0, 2.55, 4.02, 2.55), 4096, 3, 8),
+    ("slope-gridmap", (1.0, 0.0, 8.0, 0.0), 512, 3, 32),
+    ("synth-rough-1024", (1.0, 10.23, 6.8, 10.23), 8192, 5, 64),
+])
+def test_device_loop_nn_index_equals_host_batched(gpu, name, xy, batch, seed, nn_index):
+    """The targets' nearest vertices through the trees' indices (GBP_OPT_NN_INDEX
+    = a small tree size, so the index is built early and rebuilt often as the
+    trees grow; k_nnq_* + k_nn_pruned with an unindexed tail) give the same
+    trees and path as the host batched planner's fp64 scans, bit for bit."""
+    data = td.by_name(name)
+    O = oracle.OracleTerrain.from_data(data)
+    start, goal = _start_goal(O, *xy)
+    kw = dict(batch=batch, max_time=120.0, seed=seed)
+    host = planner.plan_rrt_connect(data, start, goal, **kw)
+    dev = planner.plan_rrt_connect_device(data, start, goal, nn_index=nn_index, **kw)
+    assert host["found"] == 1 and dev["found"] == 1
+    check_path(O, dev, start, goal)
+    assert np.array_equal(dev["states"], host["states"])
+    assert np.array_equal(dev["actions"], host["actions"])
+    for k in ("vertices_a", "vertices_b", "targets", "extends", "attempts_checked", "connects",
+              "fragile_resolved", "depth_capped"):
+        assert dev[k] == host[k], (k, dev[k], host[k])
+    assert max(dev["vertices_a"], dev["vertices_b"]) >= 2 * nn_index  # the index was used
+    print(f"{name} batch {batch} index >= {nn_index}: {dev['vertices_a']}+{dev['vertices_b']} "
+          f"vertices, {dev['extends']} extends")
+
+
 @pytest.mark.parametrize("batch,seed", [(4096, 3), (1024, 8)])
 def test_device_loop_forced_halts_equal_host_batched(gpu, batch, seed):
     """Halt -> gbp_plan_resolve_host -> resume in every stage.  A FRAGILE
@@ -150,14 +178,18 @@ def test_device_tree_api(gpu):
         t.append(s[:1], a[:1], np.array([99], np.int32))  # parent out of range
 
 
-def test_tree_nearest_fp32_filter_exact(gpu):
+@pytest.mark.parametrize("indexed", [0.0, 1.0, 0.7])
+def test_tree_nearest_fp32_filter_exact(gpu, indexed):
     """gbp_tree_nearest_dev (k_nn_filter: fp32 filter, fp64 re-check of the
     candidates) returns exactly the fp64 scan's index (gbp_nearest_batch_dev,
     planner_class.cpp:185-200: lowest index among equal distances) on random
     states and on the cases that stress the filter: exact duplicates (ties),
     vertices that are equal in fp32 but distinct in fp64 (more than NN_CAND of
     them in one chunk: the overflow scan), magnitudes past the filter's bound
-    (the fp64 scan) and NaN queries (index 0)."""
+    (the fp64 scan) and NaN queries (index 0).  `indexed`: the fraction of the
+    tree's vertices put in its nearest-neighbour index (gbp_tree_index_build,
+    k_nn_pruned) before the rest are appended (0: no index; 0.7: an unindexed
+    tail scanned in full beside the pruned chunks)."""
     import global_body_planner_amd as gbp
     data = td.synth_rough(256)
     T = gbp.Terrain.from_data(data, device=0)
@@ -167,8 +199,14 @@ def test_tree_nearest_fp32_filter_exact(gpu):
 
     def check(verts, q, label):
         tree = gbp.DeviceTree(verts[0], device=0, capacity=verts.shape[0] + 1)
-        tree.append(verts[1:], np.zeros((verts.shape[0] - 1, 10)),
-                    np.zeros(verts.shape[0] - 1, np.int32))
+        n = verts.shape[0]
+        k = max(1, int(round(indexed * n))) if indexed else n
+        tree.append(verts[1:k], np.zeros((k - 1, 10)), np.zeros(k - 1, np.int32))
+        if indexed:
+            got_n = tree.build_index(data.bounds if label == "random" else None)
+            assert got_n == (k & ~1)
+            if k < n:
+                tree.append(verts[k:], np.zeros((n - k, 10)), np.zeros(n - k, np.int32))
         qt = torch.from_numpy(np.ascontiguousarray(q)).cuda()
         got = ws.nearest(tree, qt).cpu().numpy()
         ref, _ = gbp.nearest(qt, torch.from_numpy(verts).cuda())

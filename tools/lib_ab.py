@@ -5,6 +5,10 @@ on the launch stream, validate kernel only), rounds interleaved; decisions,
 counts and s_new must agree across builds.
 
     python tools/lib_ab.py ab_libs/libgbp_old.so ab_libs/libgbp_new.so --waves 3
+    python tools/lib_ab.py global_body_planner_amd/lib/libgbp.so --opts "lds:LDS_COORDS=1;cm2:LDS_COORDS=0"
+
+--opts: named option sets (GBP_OPT_* names without the prefix) applied to
+every library's handle in turn, as further variants of the same interleaving.
 """
 import argparse
 import json
@@ -31,6 +35,7 @@ def main():
     p.add_argument("--rounds", type=int, default=7)
     p.add_argument("--launches", type=int, default=10)
     p.add_argument("--out", default=None)
+    p.add_argument("--opts", default="", help="'name:OPT=v,OPT=v;name2:...' option variants")
     a = p.parse_args()
     data = td.by_name(a.terrain)
     base = gbp.Terrain.from_data(data, device=0)
@@ -38,12 +43,21 @@ def main():
     Ts = [(os.path.basename(path), gbp.Terrain.from_data(data, device=0, lib=L.load(path)))
           for path in a.libs]
     waves = [int(w) for w in a.waves.split(",")]
-    keys = [(name, w) for name, _ in Ts for w in waves]
+    variants = [("", {})]
+    if a.opts:
+        variants = []
+        for part in a.opts.split(";"):
+            nm, _, kv = part.partition(":")
+            variants.append((nm, {k: int(v) for k, v in (x.split("=") for x in kv.split(",") if x)}))
+    Ts = [(f"{name}{'/' + vn if vn else ''}", T, vo) for name, T in Ts for vn, vo in variants]
+    keys = [(name, w) for name, _, _ in Ts for w in waves]
     times = {k: [] for k in keys}
     ref = None
     st = torch.cuda.current_stream()
     for r in range(a.rounds):
-        for (name, T) in Ts:
+        for (name, T, vo) in Ts:
+            for k, v in vo.items():
+                T.set_option(getattr(L, "OPT_" + k), v)
             for w in waves:
                 T.set_option(L.OPT_WAVES, w)
                 out = T.validate_pairs(s, act, d)
