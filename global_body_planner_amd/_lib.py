@@ -24,7 +24,7 @@ F_STAGE_MASK = 0xF << F_STAGE_SHIFT
 STORAGE_AUTO, STORAGE_F32, STORAGE_F64 = 0, 1, 2
 OPT_KERNEL, OPT_BLOCK, OPT_WAVES, OPT_LDS_COORDS, OPT_HELPERS = 1, 2, 4, 5, 8
 OPT_AFFINE_COORDS, OPT_COORD_MODE, OPT_XCD_MAP, OPT_FAST_RCP, OPT_FRAGILE_EPS = 9, 10, 13, 14, 15
-OPT_NN_INDEX = 16
+OPT_NN_INDEX, OPT_NN_FILTER, OPT_NN_STATS = 16, 17, 18
 PLAN_HALT_TARGETS, PLAN_HALT_EXTEND, PLAN_HALT_CONNECT = 1, 2, 4
 KERNEL_DIRECT, KERNEL_PERSISTENT = 0, 1
 

@@ -63,6 +63,8 @@ struct gbp_tree {
   double *v = nullptr;        // [cap][8] vertex states (GraphClass vertices)
   float *vf = nullptr;        // [(cap+1)/2][18] fp32 row pairs (nearest-neighbour filter, nn_put_row)
   float *vmax = nullptr;      // [8] max |fl32(v[j][k])| over the vertices (NaN skipped)
+  _Float16 *vh = nullptr;     // [cap][NH_ROW] fp16 split rows (matrix-core search, nn_put_hrow)
+  float *hm = nullptr;        // [16]: [0, 8) max |64 v[j][k]|, [8] (bits) 1 = a row outside fp16
   double *a = nullptr;        // [cap][10] the action that reached each vertex
   double *g = nullptr;        // [cap] cost to come: g[parent] + poseDistance
   int32_t *parent = nullptr;  // [cap], -1 at the root
@@ -92,6 +94,8 @@ struct gbp_plan_ws {
   unsigned long long *tiles = nullptr;  // look-back tile states
   uint32_t epoch = 0;          // per-compaction tag of the tile states
   uint64_t seq = 0;            // launch sequence number of the planner kernels (gated())
+  int nn_mode = 0;             // GBP_OPT_NN_FILTER of the last terrain that enqueued (0: k_nn_mfma)
+  int nn_stats = 0;            // GBP_OPT_NN_STATS: k_nn_hreduce counts its re-checks in the status
   int64_t ntiles = 0;
   // stage 0-1
   double *cand = nullptr;      // [bmax][8] drawn states
@@ -648,6 +652,435 @@ __global__ __launch_bounds__(TB) void k_nn_reduce(const gbp_plan_status *st, con
       }
     }
     if (lane == 0) out[qi] = bc < nch ? pi[bc * nq + qi] : 0;
+  }
+}
+
+// ============================================================================
+// nearest neighbour on the matrix cores (GBP_OPT_NN_FILTER 0, the default)
+// ============================================================================
+// The filter's scores S_j = |F_j|^2 - 2 G.F_j (F_j = 64 v_j, G = 64 q: scaled
+// by a power of two, so exactly; |G - F_j|^2 = |G|^2 + S_j) for a tile of 32
+// vertex rows x 32 queries are two v_mfma_f32_32x32x16_f16 with fp32
+// accumulation, from each coordinate split into two fp16 parts (hi + lo):
+//   MFMA 1  K = [F_hi(8) | F_lo(8)] . [-2 G_hi | -2 G_hi]
+//   MFMA 2  K = [F_hi(8) | N_1 N_2 N_3 0..] . [-2 G_lo | 2^14 2^14 2^14 0..]
+// with N_1 + N_2 + N_3 the row's fp64 squared norm times 2^-14 in three fp16
+// parts (nn_put_hrow).  The dropped G_lo.F_lo term and the parts' rounding are
+// ~2^-20 of the products, so the matrix cores score 1024 (query, vertex) pairs
+// per 64 MFMA cycles where the packed fp32 filter (k_nn_filter) spends ~4.5
+// VALU instructions per pair per pass.  The VALU only reduces: per lane (its
+// query, its 16 rows of the 32-row chunk: a "half-chunk"), the chunk minimum
+// by v_min3, then the running minimum m1, its half-chunk, and the second
+// smallest half-chunk minimum m2 (v_med3).  Work item = (4 query tiles = 128
+// queries, segment of chunks), one wave each; its (m1, m2, half-chunk) per
+// query go to the partial slots; k_nn_hreduce then takes B = min m1 over the
+// segments and re-checks in fp64 every half-chunk whose minimum is <= T(B),
+// and every row of a segment whose m2 is <= T(B) (a second half-chunk within
+// the threshold: rare).
+// Why no minimiser is lost (everything in the scaled units; M_k = the tree's
+// hmax[k] >= max_j |F_jk|; S~_j the computed score):
+//   * each fp16 split has |x - hi - lo| <= 2^-20 |x| + 2^-14 (lo may be
+//     subnormal or flushed), the dropped G_lo F_lo term is <= 2^-20 |G_k||F_k|,
+//     the norm's three parts are within 2^-29 |F|^2 + 1, and 32 fp32
+//     accumulations (rounding or truncating) add at most
+//     gamma (sum |terms|), gamma = 33 * 2^-23; so |S~_j - S_j| <= eps(G)
+//     (nh_eps: gamma (1.01 MM + 2.02 GM) + 2^-29 MM + 1 + 2 sum_k
+//     [(4 * 2^-20 |G_k| + 1.01 * 2^-14) M_k + 1.01 * 2^-14 |G_k| + 2^-27], MM = sum M_k^2,
+//     GM = sum |G_k| M_k);
+//   * the fp64 minimiser j* (the reference's sqrt of an fp64 sum) has
+//     |G - F_j*|^2 <= |G - F_i|^2 (1 + 5e-15) for every row i, so with i the
+//     row scoring B: S~_j* <= B + 2 eps + 5e-15 (B + eps + |G|^2) <= T(B)
+//     (nh_threshold: fp64, 1e-14, rounded up to fp32) — and so does every row
+//     tying with j*.  Its half-chunk has minimum <= T (checked), or another
+//     half-chunk of that segment holds the segment's m1 and then m2 <= T (the
+//     segment is scanned).
+// Rows with |F_k| >= 2^13 (|v_k| >= 128) or NaN mark the tree (hbad): its
+// searches scan in fp64.  So do queries with |G_k| >= 2^13 or NaN.
+constexpr int NH_ROW = 32;             // fp16 per row: F_hi[8] F_lo[8] F_hi[8] N_1 N_2 N_3 0[5]
+constexpr double NH_SCALE = 64.0;      // F = 64 v (exact)
+constexpr double NH_LIM = 8192.0;      // |F_k| < 2^13: |F|^2 * 2^-14 < 2^15 fits fp16
+constexpr double NH_NSCALE = 0x1p-14;  // the norm parts are |F|^2 * 2^-14 ...
+constexpr float NH_NCONST = 16384.0f;  // ... times 2^14 on the query side
+constexpr int NH_NT = 4;               // query tiles (32 queries) per wave
+constexpr int NH_ITEMS = 4096;         // waves a search aims for
+constexpr int NH_MAX_SEG = 64;         // segments per query (the reduce reads them all)
+constexpr int NH_TB = 256;             // 4 independent waves per workgroup
+constexpr int NH_RTB = 256;            // reduce: 16 lanes per query
+
+typedef _Float16 nh8 __attribute__((ext_vector_type(8)));
+typedef float nhacc __attribute__((ext_vector_type(16)));
+
+// fp16 hi + lo of a scaled coordinate (|x| < 2^13)
+__device__ __forceinline__ void nh_split(double x, _Float16 &hi, _Float16 &lo) {
+  hi = (_Float16)(float)x;
+  lo = (_Float16)(float)(x - (double)hi);
+}
+
+// row j of the fp16 rows; hm = {hmax[8], hbad}
+__device__ __forceinline__ void nn_put_hrow(_Float16 *__restrict__ vh, float *__restrict__ hm,
+                                            int64_t j, const double *s, bool init) {
+  nh8 fh, fl, nr;
+  double n = 0.0;
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const double x = s[k] * NH_SCALE;
+    const bool ok = fabs(x) < NH_LIM;
+    bad = bad || !ok;
+    _Float16 hi, lo;
+    nh_split(ok ? x : 0.0, hi, lo);
+    fh[k] = hi;
+    fl[k] = lo;
+    n = n + x * x;
+    const float ax = ok ? (float)fabs(x) : 0.f;
+    if (init)
+      hm[k] = ax;
+    else
+      atomicMax((unsigned int *)(hm + k), __float_as_uint(ax));
+  }
+  const double ns = bad ? 0.0 : n * NH_NSCALE;
+  const _Float16 n1 = (_Float16)(float)ns;
+  const double r1 = ns - (double)n1;
+  const _Float16 n2 = (_Float16)(float)r1;
+  const _Float16 n3 = (_Float16)(float)(r1 - (double)n2);
+  nr = nh8{n1, n2, n3, 0, 0, 0, 0, 0};
+  nh8 *r = (nh8 *)(vh + (int64_t)NH_ROW * j);
+  r[0] = fh;
+  r[1] = fl;
+  r[2] = fh;
+  r[3] = nr;
+  if (init)
+    ((uint32_t *)hm)[8] = bad ? 1u : 0u;
+  else if (bad)
+    atomicOr((uint32_t *)hm + 8, 1u);
+}
+
+// items: query groups (NH_NT tiles) x segments of cps chunks (32 rows); at
+// most NN_MAX_CHUNKS * bmax partial slots (pm[seg * nq + qi])
+__device__ __forceinline__ void nh_geometry(int64_t nq, int64_t nv, int64_t bmax, int64_t &nqg,
+                                            int64_t &nseg, int64_t &cps, int64_t &nch) {
+  nch = nv > 0 ? (nv + 31) / 32 : 1;
+  nqg = nq > 0 ? (nq + 32 * NH_NT - 1) / (32 * NH_NT) : 1;
+  int64_t want = (NH_ITEMS + nqg - 1) / nqg;
+  const int64_t slots = (NN_MAX_CHUNKS * bmax) / (nq > 0 ? nq : 1);
+  if (want > slots) want = slots;
+  if (want > NH_MAX_SEG) want = NH_MAX_SEG;
+  if (want > nch) want = nch;
+  if (want < 1) want = 1;
+  cps = (nch + want - 1) / want;
+  nseg = (nch + cps - 1) / cps;
+}
+
+// eps(G) above; g: the query's scaled coordinates, hm: the tree's hmax
+__device__ __forceinline__ double nh_eps(const double (&g)[8], const float *__restrict__ hm) {
+  double mm = 0.0, gm = 0.0, lin = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const double m = (double)hm[k] * (1.0 + 0x1p-22), ag = fabs(g[k]);
+    mm += m * m;
+    gm += ag * m;
+    lin += (4.0 * 0x1p-20 * ag + 1.01 * 0x1p-14) * m + 1.01 * 0x1p-14 * ag + 0x1p-27;
+  }
+  const double gamma = 33.0 * 0x1p-23;
+  return gamma * (1.01 * mm + 2.02 * gm) + 0x1p-29 * mm + 1.0 + 2.0 * lin;
+}
+
+__device__ __forceinline__ float nh_threshold(float B, double eps, double g2) {
+  const double t = (double)B + 2.0 * eps + 1e-14 * (fabs((double)B) + eps + g2);
+  return isnan(t) ? INFINITY : nextafterf((float)t, INFINITY);
+}
+
+// min over the 16 scores of a lane (its half-chunk)
+__device__ __forceinline__ float nh_min16(const nhacc &a) {
+  const float m0 = fminf(fminf(fminf(a[0], a[1]), a[2]), a[3]);
+  float m1 = fminf(fminf(a[4], a[5]), a[6]);
+  float m2 = fminf(fminf(a[7], a[8]), a[9]);
+  float m3 = fminf(fminf(a[10], a[11]), a[12]);
+  float m4 = fminf(fminf(a[13], a[14]), a[15]);
+  return fminf(fminf(fminf(m0, m1), fminf(m2, m3)), m4);
+}
+
+// a lane's two smallest half-chunk minima (m1 <= m2, chunks i1, i2) and a
+// lower bound m3 on every other half-chunk's minimum
+struct NhTop {
+  float m1 = INFINITY, m2 = INFINITY, m3 = INFINITY;
+  int i1 = -1, i2 = -1;
+  __device__ __forceinline__ void insert(float cm, int c) {
+    const bool lt1 = cm < m1, lt2 = cm < m2;
+    m3 = __builtin_amdgcn_fmed3f(m2, cm, m3);
+    m2 = __builtin_amdgcn_fmed3f(m1, cm, m2);
+    i2 = lt1 ? i1 : (lt2 ? c : i2);
+    i1 = lt1 ? c : i1;
+    m1 = fminf(m1, cm);
+  }
+};
+
+// pass of one wave over chunks [c0, c1) (wave-uniform, as is nv): NT query
+// tiles (B operands b1, b2).  Lane (r, h) reads row c*32 + r: part h (F_hi /
+// F_lo) for MFMA 1 and part 2 + h (F_hi / norm) for MFMA 2, two 16-B loads
+// with one address; the row arrays hold whole chunks (tree_alloc), rows past
+// nv are masked.
+template <int NT>
+__device__ __forceinline__ void nh_sweep(const _Float16 *__restrict__ vh, int c0, int c1, int nv,
+                                         const nh8 (&b1)[NT], const nh8 (&b2)[NT], NhTop (&t)[NT]) {
+  const int lane = threadIdx.x & (WAVE - 1), r = lane & 31, h = lane >> 5;
+  const nh8 *base = (const nh8 *)vh + (NH_ROW / 8) * r + h;
+  constexpr int64_t CS = NH_ROW * 4;  // nh8 per chunk
+  // scores of chunk c for every tile; TAIL: the last chunk, rows past nv masked
+  auto score = [&](int c, const nh8 &a1, const nh8 &a2, auto tail_tag) {
+    constexpr bool TAIL = decltype(tail_tag)::value;
+#pragma unroll
+    for (int u = 0; u < NT; u++) {
+      nhacc acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1[u], nhacc{}, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2, b2[u], acc, 0, 0, 0);
+      if (TAIL) {
+        const int rem = nv - 32 * c;
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+          if ((i & 3) + 8 * (i >> 2) + 4 * h >= rem) acc[i] = INFINITY;
+      }
+      t[u].insert(nh_min16(acc), c);
+    }
+  };
+  // the full chunks, two chunks' rows in flight ahead of the one being scored
+  const int cf = min(c1, nv >> 5);
+  if (c0 < cf) {
+    nh8 a1 = base[CS * c0], a2 = base[CS * c0 + 2], p1, p2, q1, q2;
+    if (c0 + 1 < cf) {
+      p1 = base[CS * (c0 + 1)];
+      p2 = base[CS * (c0 + 1) + 2];
+    }
+    for (int c = c0; c < cf; c++) {
+      if (c + 2 < cf) {
+        q1 = base[CS * (c + 2)];
+        q2 = base[CS * (c + 2) + 2];
+      }
+      score(c, a1, a2, std::false_type{});
+      a1 = p1;
+      a2 = p2;
+      p1 = q1;
+      p2 = q2;
+    }
+  }
+  if (cf < c1)  // the tree's last, partial chunk (the row arrays hold whole chunks)
+    score(cf, base[CS * cf], base[CS * cf + 2], std::true_type{});
+}
+
+template <int NT>
+__global__ __launch_bounds__(NH_TB) void k_nn_mfma(const gbp_plan_status *__restrict__ st,
+                                                   const int32_t *__restrict__ nq_dev,
+                                                   const double *__restrict__ q,
+                                                   const int32_t *__restrict__ q_off_dev,
+                                                   const _Float16 *__restrict__ vh,
+                                                   const float *__restrict__ hm,
+                                                   const int32_t *__restrict__ nv_dev, int64_t bmax,
+                                                   float4 *__restrict__ pm, int2 *__restrict__ pid,
+                                                   uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
+  int64_t nqg, nseg, cps, nch;
+  nh_geometry(nq, nv, bmax, nqg, nseg, cps, nch);
+  const bool tree_bad = ((const uint32_t *)hm)[8] != 0u || nv <= 0;
+  const int lane = threadIdx.x & (WAVE - 1), r = lane & 31, h = lane >> 5;
+  const int waves = gridDim.x * (NH_TB / WAVE);
+  const int items = (int)(nqg * nseg), ns = (int)nseg;
+  for (int item = __builtin_amdgcn_readfirstlane(blockIdx.x * (NH_TB / WAVE) + threadIdx.x / WAVE);
+       item < items; item += waves) {
+    const int qg = item / ns, sg = item - qg * ns;
+    const int c0 = sg * (int)cps, c1 = min((int)nch, c0 + (int)cps);
+    nh8 b1[NT], b2[NT];
+    NhTop t[NT];
+#pragma unroll
+    for (int u = 0; u < NT; u++) {
+      const int64_t qi = qg * (32 * NT) + 32 * u + r;
+      const bool live = qi < nq;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const double x = live ? q[8 * (q_off + qi) + k] * NH_SCALE : 0.0;
+        _Float16 hi, lo;
+        nh_split(fabs(x) < NH_LIM ? x : 0.0, hi, lo);  // a bad query is scanned in fp64
+        b1[u][k] = (_Float16)(-2.0f) * hi;
+        b2[u][k] = h ? (k < 3 ? (_Float16)NH_NCONST : (_Float16)0.0f) : (_Float16)(-2.0f) * lo;
+      }
+    }
+    if (tree_bad) {  // every segment scanned in fp64 by the reduce
+#pragma unroll
+      for (int u = 0; u < NT; u++) t[u].m1 = t[u].m2 = t[u].m3 = -INFINITY;
+    } else {
+      nh_sweep<NT>(vh, c0, c1, (int)nv, b1, b2, t);
+    }
+    // the two lanes of a query (rows 4h + ...): merge to one entry, the two
+    // smallest half-chunks (half-chunk id = 2 chunk + h) and a lower bound on
+    // the rest
+#pragma unroll
+    for (int u = 0; u < NT; u++) {
+      const float a1 = t[u].m1, a2 = t[u].m2, a3 = t[u].m3;
+      const int ia1 = t[u].i1 >= 0 ? 2 * t[u].i1 + h : -1, ia2 = t[u].i2 >= 0 ? 2 * t[u].i2 + h : -1;
+      const float b1v = __shfl_xor(a1, 32), b2v = __shfl_xor(a2, 32), b3v = __shfl_xor(a3, 32);
+      const int ib1 = __shfl_xor(ia1, 32), ib2 = __shfl_xor(ia2, 32);
+      const bool fa = a1 <= b1v;
+      // first: the smaller head; second: the smaller of the other head and the
+      // first list's second; bound: min(the larger of those two, both lists'
+      // thirds and the other list's second)
+      const float e1 = fa ? a1 : b1v, x2 = fa ? a2 : b2v, y1 = fa ? b1v : a1;
+      const int ie1 = fa ? ia1 : ib1, ix2 = fa ? ia2 : ib2, iy1 = fa ? ib1 : ia1;
+      const float y2 = fa ? b2v : a2;
+      const bool sx = x2 <= y1;
+      const float e2 = sx ? x2 : y1;
+      const int ie2 = sx ? ix2 : iy1;
+      const float e3 = fminf(fminf(fmaxf(x2, y1), y2), fminf(a3, b3v));
+      const int64_t qi = (int64_t)qg * (32 * NT) + 32 * u + r;
+      if (h == 0 && qi < nq) {
+        pm[(int64_t)sg * nq + qi] = float4{e1, e2, e3, 0.f};
+        pid[(int64_t)sg * nq + qi] = int2{ie1, ie2};
+      }
+    }
+  }
+}
+
+// 16 lanes per query: B, T(B), the fp64 re-checks, lexicographic (distance,
+// index) minimum; nothing < inf (a NaN query): index 0
+__global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
+                                                       const int32_t *__restrict__ nq_dev,
+                                                       const double *__restrict__ q,
+                                                       const int32_t *__restrict__ q_off_dev,
+                                                       const double *__restrict__ v,
+                                                       const float *__restrict__ hm,
+                                                       const int32_t *__restrict__ nv_dev,
+                                                       int64_t bmax, const float4 *__restrict__ pm,
+                                                       const int2 *__restrict__ pid,
+                                                       int32_t *__restrict__ out, uint64_t seq,
+                                                       int stats) {
+  if (gated(st, seq)) return;
+  const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
+  int64_t nqg, nseg, cps, nch;
+  nh_geometry(nq, nv, bmax, nqg, nseg, cps, nch);
+  const bool tree_bad = ((const uint32_t *)hm)[8] != 0u || nv <= 0;
+  const int sl = threadIdx.x & 15;
+  const int64_t groups = (int64_t)gridDim.x * (NH_RTB / 16);
+  const int64_t iters = (nq + groups - 1) / groups;  // whole groups iterate together
+  for (int64_t it = 0; it < iters; it++) {
+    const int64_t qi = it * groups + blockIdx.x * (int64_t)(NH_RTB / 16) + threadIdx.x / 16;
+    const bool live = qi < nq;
+    double qq[8], g[8], g2 = 0.0;
+    bool qbad = false;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      qq[k] = live ? q[8 * (q_off + qi) + k] : 0.0;
+      g[k] = qq[k] * NH_SCALE;
+      qbad = qbad || !(fabs(g[k]) < NH_LIM);
+      g2 += g[k] * g[k];
+    }
+    // the group's entries, lane sl holding segments sl, sl + 16, ... (<= 4)
+    float4 e[NH_MAX_SEG / 16];
+    float B = INFINITY;
+#pragma unroll
+    for (int k = 0; k < NH_MAX_SEG / 16; k++) {
+      const int64_t s = sl + 16 * k;
+      e[k] = live && s < nseg ? pm[s * nq + qi] : float4{INFINITY, INFINITY, INFINITY, 0.f};
+      B = fminf(B, e[k].x);
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) B = fminf(B, __shfl_xor(B, off, 16));
+    const float T = nh_threshold(B, nh_eps(g, hm), g2);
+    double best = INFINITY;
+    int bi = 0x7FFFFFFF, nrc = 0, nsc = 0;
+    if (live && (qbad || tree_bad || !(B < INFINITY))) {  // the whole tree in fp64
+      nsc = sl == 0;
+      for (int64_t j = sl; j < nv; j += 16) {
+        const double d = nn_dist64(qq, v + 8 * j);
+        if (d < best) {  // ascending per lane: the first index at its minimum
+          best = d;
+          bi = (int)j;
+        }
+      }
+    }
+    // the half-chunks to re-check and the segments to scan go round the
+    // group: a half-chunk's 16 rows one per lane, a segment's rows strided
+    // over the 16 lanes (a single lane walking them was the search's
+    // critical path)
+    const bool part = live && !(qbad || tree_bad || !(B < INFINITY));
+    const int gbit = (threadIdx.x & (WAVE - 1)) & ~15;
+#pragma unroll
+    for (int k = 0; k < NH_MAX_SEG / 16; k++) {
+      if (16 * k >= nseg) break;  // wave-uniform
+      const int64_t s0 = 16 * k, s = s0 + sl;
+      bool chk1 = false, chk2 = false, scan = false;
+      int2 hid = {-1, -1};
+      if (part && s < nseg) {
+        scan = e[k].z <= T;  // a third half-chunk within T: the segment in full
+        if (!scan && e[k].x <= T) {
+          hid = pid[s * nq + qi];
+          chk1 = hid.x >= 0;
+          chk2 = e[k].y <= T && hid.y >= 0;
+        }
+      }
+      uint32_t cmask = (uint32_t)(__ballot(chk1) >> gbit) & 0xFFFFu;
+      uint32_t cmask2 = (uint32_t)(__ballot(chk2) >> gbit) & 0xFFFFu;
+      uint32_t smask = (uint32_t)(__ballot(scan) >> gbit) & 0xFFFFu;
+      nrc += sl == 0 ? __popc(cmask) + __popc(cmask2) : 0;
+      nsc += sl == 0 ? __popc(smask) : 0;
+      while (__ballot((cmask | cmask2) != 0u)) {
+        if (cmask | cmask2) {
+          int h;
+          if (cmask) {
+            const int src = __ffs(cmask) - 1;
+            cmask &= cmask - 1u;
+            h = __shfl(hid.x, src, 16);
+          } else {
+            const int src = __ffs(cmask2) - 1;
+            cmask2 &= cmask2 - 1u;
+            h = __shfl(hid.y, src, 16);
+          }
+          const int64_t j = (int64_t)(h >> 1) * 32 + 4 * (h & 1) + (sl & 3) + 8 * (sl >> 2);
+          if (j < nv) {
+            const double d = nn_dist64(qq, v + 8 * j);
+            if (d < best || (d == best && j < bi)) {
+              best = d;
+              bi = (int)j;
+            }
+          }
+        }
+      }
+      while (__ballot(smask != 0u)) {
+        if (smask) {
+          const int64_t ss = s0 + (__ffs(smask) - 1);
+          smask &= smask - 1u;
+          const int64_t j1 = min(nv, min(nch, (ss + 1) * cps) * 32);
+          for (int64_t j = ss * cps * 32 + sl; j < j1; j += 64) {  // 4 rows in flight
+            double d[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+              d[r] = j + 16 * r < j1 ? nn_dist64(qq, v + 8 * (j + 16 * r)) : INFINITY;
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+              if (d[r] < best || (d[r] == best && j + 16 * r < bi)) {
+                best = d[r];
+                bi = (int)(j + 16 * r);
+              }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {
+      const double od = __shfl_xor(best, off, 16);
+      const int oi = __shfl_xor(bi, off, 16);
+      if (od < best || (od == best && oi < bi)) {
+        best = od;
+        bi = oi;
+      }
+    }
+    if (live && sl == 0) out[qi] = bi == 0x7FFFFFFF ? 0 : bi;
+    if (!stats) continue;  // diagnostics (GBP_OPT_NN_STATS): same-address atomics serialise
+    for (int off = 32; off > 0; off >>= 1) {
+      nrc += __shfl_xor(nrc, off);
+      nsc += __shfl_xor(nsc, off);
+    }
+    if ((threadIdx.x & (WAVE - 1)) == 0 && (nrc | nsc)) {
+      atomicAdd((unsigned long long *)&st->stat_nn_rechecks, (unsigned long long)nrc);
+      atomicAdd((unsigned long long *)&st->stat_nn_scans, (unsigned long long)nsc);
+    }
   }
 }
 
@@ -1242,6 +1675,7 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
                                                const double *__restrict__ sn,
                                                const double *__restrict__ an, double *__restrict__ tv,
                                                float *__restrict__ tvf, float *__restrict__ tvmax,
+                                               _Float16 *__restrict__ tvh, float *__restrict__ thm,
                                                double *__restrict__ ta, double *__restrict__ tg,
                                                int32_t *__restrict__ tp, int32_t *__restrict__ tcount,
                                                int32_t *__restrict__ vtx, unsigned long long *tiles,
@@ -1269,6 +1703,7 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
     copy8(pv, tv + 8 * (int64_t)p);
     copy8(tv + 8 * (int64_t)idx, s);
     nn_put_row(tvf, idx, s);
+    nn_put_hrow(tvh, thm, idx, s, false);
 #pragma unroll
     for (int k = 0; k < 8; k++) vmax_update(tvmax + k, (float)s[k]);
     copy10(ta + 10 * (int64_t)idx, an + 10 * i);
@@ -1466,6 +1901,7 @@ __global__ void k_tree_init(gbp_tree t, double r0, double r1, double r2, double 
   const double r[8] = {r0, r1, r2, r3, r4, r5, r6, r7};
   copy8(t.v, r);
   nn_put_row(t.vf, 0, r);
+  nn_put_hrow(t.vh, t.hm, 0, r, true);
   for (int k = 0; k < 8; k++) {
     const float f = (float)r[k];
     t.vmax[k] = isnan(f) ? 0.f : fabsf(f);
@@ -1484,6 +1920,7 @@ __global__ void k_tree_append(gbp_tree t, int64_t n, const double *__restrict__ 
   for (int64_t i = 0; i < n; i++, c++) {
     copy8(t.v + 8 * (int64_t)c, s + 8 * i);
     nn_put_row(t.vf, c, s + 8 * i);
+    nn_put_hrow(t.vh, t.hm, c, s + 8 * i, false);
     for (int k = 0; k < 8; k++) vmax_update(t.vmax + k, (float)s[8 * i + k]);
     copy10(t.a + 10 * (int64_t)c, a + 10 * i);
     t.parent[c] = p[i];
@@ -1583,6 +2020,15 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
                        tr->idx_n, w->nn_d, w->nn_i, out, w->bcnt, ++w->seq);
     return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   }
+  if (w->nn_mode == 0) {  // the matrix cores (k_nn_mfma), GBP_OPT_NN_FILTER 0
+    hipLaunchKernelGGL((k_nn_mfma<NH_NT>), dim3(num_cus * (NH_ITEMS / 4) / 256), dim3(NH_TB), 0, s,
+                       w->st, nq_dev, q, q_off_dev, tr->vh, tr->hm, tr->count, w->bmax,
+                       (float4 *)w->nn_d, (int2 *)w->nn_i, ++w->seq);
+    hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(16 * w->bmax, NH_RTB, num_cus * 8)), dim3(NH_RTB),
+                       0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, tr->count, w->bmax,
+                       (const float4 *)w->nn_d, (const int2 *)w->nn_i, out, ++w->seq, w->nn_stats);
+    return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
+  }
   // two queries per lane, four row pairs per scalar load, 8 workgroups per
   // CU: the fastest of {1, 2, 4} pairs x {1, 2} queries x {4, 8} workgroups
   // per CU on trees past ~20k vertices (profiles/r02j_nn_dot.txt)
@@ -1603,6 +2049,8 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   const TerrainView<ZT> V = view<ZT>(t);
   const int cus = t->num_cus;
   gbp_plan_status *st = w->st;
+  w->nn_mode = t->opt_nn_filter;
+  w->nn_stats = t->opt_nn_stats;
   if (first_stage <= 0 && last_stage >= 0)
     hipLaunchKernelGGL(k_targets<ZT>, dim3(grid_for(batch, TB, cus * 8)), dim3(TB), 0, s, V, st,
                        batch, seed, target_stream, target_base, w->cand, w->cflag, half, ++w->seq,
@@ -1629,7 +2077,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   }
   if (first_stage <= 3 && last_stage >= 3)
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 0, w->eres, w->nn,
-                       w->esn, w->ean, T->v, T->vf, T->vmax, T->a, T->g, T->parent, T->count, w->evtx, w->tiles,
+                       w->esn, w->ean, T->v, T->vf, T->vmax, T->vh, T->hm, T->a, T->g, T->parent, T->count, w->evtx, w->tiles,
                        next_epoch(w), half, T->cap, ++w->seq);
   if (!O) return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   const int cdir = direction == GBP_FORWARD ? GBP_REVERSE : GBP_FORWARD;
@@ -1652,7 +2100,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   }
   if (first_stage <= 5 && last_stage >= 5)
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 1, w->kres, w->nno,
-                       w->ksn, w->kan, O->v, O->vf, O->vmax, O->a, O->g, O->parent, O->count, nullptr, w->tiles,
+                       w->ksn, w->kan, O->v, O->vf, O->vmax, O->vh, O->hm, O->a, O->g, O->parent, O->count, nullptr, w->tiles,
                        next_epoch(w), half, O->cap, ++w->seq);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
@@ -1686,18 +2134,22 @@ T *carve(char *&p, size_t count) {
 int tree_alloc(gbp_tree *t, int64_t cap) {
   double *v = nullptr, *a = nullptr, *g = nullptr;
   float *vf = nullptr;
+  _Float16 *vh = nullptr;
   int32_t *p = nullptr;
   if (hipMalloc(&v, 64 * cap) != hipSuccess) return GBP_E_ALLOC;
   if (hipMalloc(&a, 80 * cap) != hipSuccess || hipMalloc(&g, 8 * cap) != hipSuccess ||
-      hipMalloc(&p, 4 * cap) != hipSuccess || hipMalloc(&vf, 4 * NN_PAIR * ((cap + 1) / 2)) != hipSuccess) {
+      hipMalloc(&p, 4 * cap) != hipSuccess || hipMalloc(&vf, 4 * NN_PAIR * ((cap + 1) / 2)) != hipSuccess ||
+        hipMalloc(&vh, 2 * NH_ROW * ((cap + 31) & ~(int64_t)31)) != hipSuccess) {
     (void)hipFree(v);
     if (a) (void)hipFree(a);
     if (g) (void)hipFree(g);
     if (p) (void)hipFree(p);
+    if (vf) (void)hipFree(vf);
     return GBP_E_ALLOC;
   }
   t->v = v;
   t->vf = vf;
+  t->vh = vh;
   t->a = a;
   t->g = g;
   t->parent = p;
@@ -1745,11 +2197,12 @@ int gbp_tree_create(int device, int64_t capacity, gbp_tree **out) {
   if (!t) return GBP_E_ALLOC;
   t->device = device;
   if (hipMalloc(&t->count, 4) != hipSuccess || hipMalloc(&t->vmax, 32) != hipSuccess ||
-      tree_alloc(t, capacity) != GBP_OK) {
+      hipMalloc(&t->hm, 64) != hipSuccess || tree_alloc(t, capacity) != GBP_OK) {
     gbp_tree_destroy(t);
     return GBP_E_ALLOC;
   }
-  if (hipMemset(t->count, 0, 4) != hipSuccess || hipMemset(t->vmax, 0, 32) != hipSuccess) {
+  if (hipMemset(t->count, 0, 4) != hipSuccess || hipMemset(t->vmax, 0, 32) != hipSuccess ||
+      hipMemset(t->hm, 0, 64) != hipSuccess) {
     gbp_tree_destroy(t);
     return GBP_E_HIP;
   }
@@ -1761,8 +2214,9 @@ int gbp_tree_destroy(gbp_tree *t) {
   if (!t) return GBP_E_BAD_HANDLE;
   Guard g(t->device);
   (void)hipDeviceSynchronize();
-  void *ptrs[] = {t->v,    t->vf,   t->a,    t->g,    t->parent, t->count, t->vmax, t->isp,
-                  t->isid, t->isv,  t->ibox, t->imed, t->ikey,   t->ival,  t->isort};
+  void *ptrs[] = {t->v,    t->vf,   t->vh,   t->hm,   t->a,    t->g,    t->parent, t->count,
+                  t->vmax, t->isp,  t->isid, t->isv,  t->ibox, t->imed, t->ikey,   t->ival,
+                  t->isort};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   delete t;
@@ -1784,12 +2238,14 @@ int gbp_tree_reserve(gbp_tree *t, int64_t capacity, gbp_stream stream) {
   }
   HIPCHK_P(hipMemcpyAsync(t->v, old.v, 64 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->vf, old.vf, 4 * NN_PAIR * ((old.cap + 1) / 2), hipMemcpyDeviceToDevice, s));
+  HIPCHK_P(hipMemcpyAsync(t->vh, old.vh, 2 * NH_ROW * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->a, old.a, 80 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->g, old.g, 8 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->parent, old.parent, 4 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipStreamSynchronize(s));
   (void)hipFree(old.v);
   (void)hipFree(old.vf);
+  (void)hipFree(old.vh);
   (void)hipFree(old.a);
   (void)hipFree(old.g);
   (void)hipFree(old.parent);
@@ -1970,12 +2426,14 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   if (!w) return GBP_E_ALLOC;
   w->device = t->device;
   w->num_cus = t->num_cus;
+  w->nn_mode = t->opt_nn_filter;
+  w->nn_stats = t->opt_nn_stats;
   w->bmax = max_batch;
   w->ntiles = (max_batch + CB - 1) / CB + 1;
   const int64_t b = max_batch, m = GBP_NUM_GEN_STATES * max_batch;
   const size_t bytes = sizeof(gbp_plan_status) + 8 * w->ntiles + 64 * b + 4 * b + 64 * b + 4 * b +
                        m * (64 + 80 + 64 + 4 + 4) + b * (4 + 4 + 64 + 80 + 4 + 4) +
-                       b * (4 + 4 + 64 + 80 + 4) + NN_MAX_CHUNKS * b * (8 + 4) +
+                       b * (4 + 4 + 64 + 80 + 4) + NN_MAX_CHUNKS * b * (16 + 8) +
                        4 * NN_QCELLS + 4 * NN_QCELLS * b + 4 * b + 64 * 256;
   if (hipMalloc(&w->block, bytes) != hipSuccess) {
     delete w;
@@ -2004,8 +2462,8 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->ksn = carve<double>(p, 8 * b);
   w->kan = carve<double>(p, 10 * b);
   w->kf = carve<uint32_t>(p, b);
-  w->nn_d = carve<double>(p, NN_MAX_CHUNKS * b);
-  w->nn_i = carve<int32_t>(p, NN_MAX_CHUNKS * b);
+  w->nn_d = carve<double>(p, 2 * NN_MAX_CHUNKS * b);   // k_nn_mfma: float4 per slot
+  w->nn_i = carve<int32_t>(p, 2 * NN_MAX_CHUNKS * b);  // k_nn_mfma: int2 per slot
   w->bcnt = carve<int32_t>(p, NN_QCELLS);
   w->bq = carve<int32_t>(p, (size_t)NN_QCELLS * b);
   w->qpt = carve<float>(p, b);

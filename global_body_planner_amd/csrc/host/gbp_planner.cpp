@@ -2065,6 +2065,7 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     if (p->nn_index)
       chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_NN_INDEX, p->nn_index < 0 ? 0 : p->nn_index),
           "nn index");
+    chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_NN_FILTER, p->nn_filter), "nn filter");
     RRTStarConnectClass planner;  // is-a RRTConnectClass: algorithm 0 uses the plain build
     planner.setSeed(p->seed);
     planner.set_state_direction_sampling(p->sampling.state_flag != 0, p->sampling.state_p,

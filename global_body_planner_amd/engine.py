@@ -420,6 +420,21 @@ class DeviceTree:
         return s, a, p, g
 
 
+class PlanStatus(ctypes.Structure):
+    """gbp_plan_status (include/gbp.h)."""
+    _fields_ = [("halt", ctypes.c_uint32), ("done", ctypes.c_uint32), ("error", ctypes.c_uint32),
+                ("halt_half", ctypes.c_int32), ("n_targets", ctypes.c_int32),
+                ("n_validate", ctypes.c_int32), ("n_added", ctypes.c_int32),
+                ("added_base", ctypes.c_int32), ("n_conn_added", ctypes.c_int32),
+                ("meet_half", ctypes.c_int32), ("meet", ctypes.c_uint64),
+                ("ext_base", ctypes.c_int64), ("ext_counter", ctypes.c_int64),
+                ("stat_targets", ctypes.c_int64), ("stat_attempts", ctypes.c_int64),
+                ("stat_added", ctypes.c_int64), ("stat_conn_added", ctypes.c_int64),
+                ("stat_fragile_resolved", ctypes.c_int64), ("stat_depth_capped", ctypes.c_int64),
+                ("gate_seq", ctypes.c_uint64), ("stat_nn_rechecks", ctypes.c_int64),
+                ("stat_nn_scans", ctypes.c_int64)]
+
+
 class PlanWorkspace:
     """Scratch and status of the device planner loop (gbp_plan_ws_*)."""
 
@@ -433,6 +448,15 @@ class PlanWorkspace:
         if getattr(self, "_h", None):
             self._lib.gbp_plan_ws_destroy(self._h)
             self._h = None
+
+    def status(self, device=0):
+        """gbp_plan_status_read as a dict."""
+        st = PlanStatus()
+        check(self._lib.gbp_plan_status_read(self._h, ctypes.byref(st), _stream(device)), "status")
+        return {k: getattr(st, k) for k, _ in PlanStatus._fields_}
+
+    def reset(self, device=0):
+        check(self._lib.gbp_plan_reset(self._h, 0, _stream(device)), "plan_reset")
 
     def nearest(self, tree, queries):
         """gbp_tree_nearest_dev: nearest vertex of `tree` per query (device tensors)."""

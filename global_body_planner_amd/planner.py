@@ -28,7 +28,8 @@ class PlanParams(ctypes.Structure):
                 ("max_time", _D), ("seed", ctypes.c_uint64), ("post_process", ctypes.c_int),
                 ("algorithm", ctypes.c_int), ("max_time_opt", _D),
                 ("sampling", _lib.Sampling), ("fragile_eps_fm", ctypes.c_int64),
-                ("adaptive", ctypes.c_int), ("nn_index", ctypes.c_int64)]
+                ("adaptive", ctypes.c_int), ("nn_index", ctypes.c_int64),
+                ("nn_filter", ctypes.c_int)]
 
 
 class PlanResult(ctypes.Structure):
@@ -98,7 +99,8 @@ def start_goal_state(height, x, y):
 
 def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018,
                      post_process=False, device=0, capacity=4096, algorithm=0, max_time_opt=0.0,
-                     sampling=None, fragile_eps=None, adaptive=False, nn_index=0):
+                     sampling=None, fragile_eps=None, adaptive=False, nn_index=0,
+                     nn_filter=0):
     """Plan start -> goal on terrain `data` (terrain_data.TerrainData).
 
     algorithm 0: batch-synchronous RRT-Connect, stops at the first solution;
@@ -118,7 +120,9 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     fragile_eps: a wider FRAGILE margin (forces host re-decisions: tests);
     adaptive: the adaptive-step pair checks (params.yaml:16);
     nn_index: GBP_OPT_NN_INDEX, the smallest tree the device loop searches
-      through its nearest-neighbour index (0: the default, never; < 0: never)."""
+      through its nearest-neighbour index (0: the default, never; < 0: never);
+    nn_filter: GBP_OPT_NN_FILTER, the nearest-neighbour scan (0 matrix cores,
+      1 packed fp32: same results)."""
     L = load()
     x = np.ascontiguousarray(data.x, dtype=np.float64)
     y = np.ascontiguousarray(data.y, dtype=np.float64)
@@ -139,6 +143,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     p.fragile_eps_fm = 0 if fragile_eps is None else int(round(fragile_eps * 1e15))
     p.adaptive = int(bool(adaptive))
     p.nn_index = int(nn_index)
+    p.nn_filter = int(nn_filter)
     r = PlanResult()
     states = np.zeros((capacity, 8))
     actions = np.zeros((capacity, 10))

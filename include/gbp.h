@@ -155,6 +155,13 @@ int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage,
                                     0 (default): the full filtered scan, measured faster
                                     at the planner's tree sizes.  Same
                                     results either way.                              */
+#define GBP_OPT_NN_FILTER    17  /* the nearest-neighbour scan's filter: 0 (default)
+                                    fp16-split scores on the matrix cores (k_nn_mfma,
+                                    DESIGN §5.3), 1 the packed fp32 VALU filter
+                                    (k_nn_filter).  Same results either way.         */
+#define GBP_OPT_NN_STATS     18  /* 1: the matrix-core search counts its fp64 re-checks
+                                    in gbp_plan_status.stat_nn_* (diagnostics: costs
+                                    same-address atomics; default 0)                  */
 #define GBP_KERNEL_DIRECT     0  /* one lane per attempt                              */
 #define GBP_KERNEL_PERSISTENT 1  /* persistent waves, lanes re-packed per sample      */
 int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value);
@@ -452,6 +459,9 @@ typedef struct {
    * no-op only if the gate was raised by an EARLIER launch, so all workgroups
    * of the launch that raised it still finish their items. */
   uint64_t gate_seq;
+  /* the matrix-core nearest-neighbour search's fp64 re-checks (k_nn_hreduce):
+   * half-chunks of 16 rows re-checked, and segments scanned in full */
+  int64_t stat_nn_rechecks, stat_nn_scans;
 } gbp_plan_status;
 int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out);
 int gbp_plan_ws_destroy(gbp_plan_ws *ws);

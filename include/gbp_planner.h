@@ -601,6 +601,7 @@ typedef struct {
   int adaptive;           // state_action_pair_check_adaptive_step_size_flag (params.yaml:16)
   int64_t nn_index;       // GBP_OPT_NN_INDEX: trees of at least this many vertices search
                           // through their index (0 = the handle's default, off; < 0 = off)
+  int nn_filter;          // GBP_OPT_NN_FILTER: 0 matrix cores (default), 1 packed fp32
 } gbp_plan_params;
 
 typedef struct {

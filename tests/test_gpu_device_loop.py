@@ -50,6 +50,22 @@ def test_device_loop_equals_host_batched(gpu, name, xy, batch, seed):
           f"{dev['time_to_first']:.4f} s in {dev['status_reads']} status reads")
 
 
+def test_device_loop_fp32_filter_equals_host_batched(gpu):
+    """The device loop with the packed fp32 nearest-neighbour filter
+    (GBP_OPT_NN_FILTER 1) builds the same trees and path as the host batched
+    planner (and so as the default matrix-core search)."""
+    data = td.by_name("synth-rough-256")
+    O = oracle.OracleTerrain.from_data(data)
+    start, goal = _start_goal(O, 1.0, 2.55, 4.02, 2.55)
+    kw = dict(batch=4096, max_time=120.0, seed=3)
+    host = planner.plan_rrt_connect(data, start, goal, **kw)
+    dev = planner.plan_rrt_connect_device(data, start, goal, nn_filter=1, **kw)
+    assert host["found"] == 1 and dev["found"] == 1
+    assert np.array_equal(dev["states"], host["states"])
+    for k in ("vertices_a", "vertices_b", "targets", "extends", "attempts_checked", "connects"):
+        assert dev[k] == host[k], (k, dev[k], host[k])
+
+
 @pytest.mark.parametrize("name,xy,batch,seed,nn_index", [
     ("synth-rough-256", (1.0, 2.55, 4.02, 2.55), 4096, 3, 8),
     ("slope-gridmap", (1.0, 0.0, 8.0, 0.0), 512, 3, 32),
@@ -178,8 +194,8 @@ def test_device_tree_api(gpu):
         t.append(s[:1], a[:1], np.array([99], np.int32))  # parent out of range
 
 
-@pytest.mark.parametrize("indexed", [0.0, 1.0, 0.7])
-def test_tree_nearest_fp32_filter_exact(gpu, indexed):
+@pytest.mark.parametrize("indexed,nn_filter", [(0.0, 0), (0.0, 1), (1.0, 0), (0.7, 0)])
+def test_tree_nearest_fp32_filter_exact(gpu, indexed, nn_filter):
     """gbp_tree_nearest_dev (k_nn_filter: fp32 filter, fp64 re-check of the
     candidates) returns exactly the fp64 scan's index (gbp_nearest_batch_dev,
     planner_class.cpp:185-200: lowest index among equal distances) on random
@@ -189,10 +205,15 @@ def test_tree_nearest_fp32_filter_exact(gpu, indexed):
     (the fp64 scan) and NaN queries (index 0).  `indexed`: the fraction of the
     tree's vertices put in its nearest-neighbour index (gbp_tree_index_build,
     k_nn_pruned) before the rest are appended (0: no index; 0.7: an unindexed
-    tail scanned in full beside the pruned chunks)."""
+    tail scanned in full beside the pruned chunks).  `nn_filter`
+    (GBP_OPT_NN_FILTER): 0 the fp16-split scores on the matrix cores
+    (k_nn_mfma + k_nn_hreduce), 1 the packed fp32 filter (k_nn_filter); the
+    offsets of 300 and 5000 put the tree past the fp16 rows' range (|v| >= 128:
+    the fp64 scan)."""
     import global_body_planner_amd as gbp
     data = td.synth_rough(256)
     T = gbp.Terrain.from_data(data, device=0)
+    T.set_option(L.OPT_NN_FILTER, nn_filter)
     rng = np.random.default_rng(5)
     nq = 4096
     ws = gbp.PlanWorkspace(T, nq)

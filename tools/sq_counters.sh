@@ -15,18 +15,19 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_MISC" \
            "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM" \
            "SQ_INSTS_BRANCH SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64" \
-           "SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM SQ_INST_LEVEL_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS"; do
+           "SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM SQ_INST_LEVEL_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS" \
+           "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_WAVE_CYCLES"; do
   i=$((i+1))
   echo "sq pass $i: $grp"
   timeout -k 10 150 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o sq -- \
-      python3 bench.py $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i ($grp) rc=$?"; tail -3 $OUT/p$i.log; }
+      ${SQ_CMD:-python3 bench.py $ARGS} > $OUT/p$i.log 2>&1 || { echo "pass $i ($grp) rc=$?"; tail -3 $OUT/p$i.log; }
 done
-python3 - "$OUT" <<'PY'
+python3 - "$OUT" "${SQ_KERNEL:-k_validate}" <<'PY'
 import csv, glob, collections, sys
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for p in glob.glob(sys.argv[1] + "/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(p)):
-        if "k_validate" in r["Kernel_Name"]:
+        if sys.argv[2] in r["Kernel_Name"]:
             acc[r["Kernel_Name"][:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in acc.items():
     print(k)
