@@ -53,6 +53,7 @@
 #include "gbp_lane.h"
 
 using namespace gbp;
+static_assert(sizeof(gbp_plan_status) == 136, "engine.PlanStatus mirrors this layout");
 
 // ============================================================================
 // handles
