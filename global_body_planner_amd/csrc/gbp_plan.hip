@@ -939,8 +939,24 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(const gbp_plan_status *__rest
   }
 }
 
+// newConfig's candidate inputs for the extends (stage 2), fused into the
+// reduce of the targets' search when GBP_OPT_NN_FILTER is 0: rrt.cpp:25
+// surface normal, :34 the six actions (Philox extend stream; direction-biased
+// draws see s_near = the nearest vertex just found), s_near copied per
+// candidate — what k_extend_prep does
+template <class ZT>
+struct NhPrep {
+  TerrainView<ZT> T;
+  uint64_t seed;
+  double *cs, *ca;
+  gbp_sampling cfg;
+  int direction;
+};
+
 // 16 lanes per query: B, T(B), the fp64 re-checks, lexicographic (distance,
-// index) minimum; nothing < inf (a NaN query): index 0
+// index) minimum; nothing < inf (a NaN query): index 0.  PREP: lanes 0-5 of
+// the query's group then write its six extend candidates (NhPrep)
+template <class ZT, bool PREP>
 __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
                                                        const int32_t *__restrict__ nq_dev,
                                                        const double *__restrict__ q,
@@ -951,8 +967,13 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
                                                        int64_t bmax, const float4 *__restrict__ pm,
                                                        const int2 *__restrict__ pid,
                                                        int32_t *__restrict__ out, uint64_t seq,
-                                                       int stats) {
-  if (gated(st, seq)) return;
+                                                       int stats, NhPrep<ZT> pp) {
+  if (gated(st, seq)) {
+    if (PREP && blockIdx.x == 0 && threadIdx.x == 0) st->n_validate = 0;  // the validate launch idles
+    return;
+  }
+  if (PREP && blockIdx.x == 0 && threadIdx.x == 0)
+    st->n_validate = (int32_t)(st->n_targets * GBP_NUM_GEN_STATES);
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   int64_t nqg, nseg, cps, nch;
   nh_geometry(nq, nv, bmax, nqg, nseg, cps, nch);
@@ -1073,6 +1094,16 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
       }
     }
     if (live && sl == 0) out[qi] = bi == 0x7FFFFFFF ? 0 : bi;
+    if (PREP && live && sl < GBP_NUM_GEN_STATES) {
+      const int64_t c = qi * GBP_NUM_GEN_STATES + sl;
+      const double *sn = v + 8 * (int64_t)(bi == 0x7FFFFFFF ? 0 : bi);
+      double nrm[3], a[10];
+      surface_normal(pp.T, qq[0], qq[1], nrm);  // rrt.cpp:25
+      sample_action_cfg(nrm, pp.cfg, pp.direction, qq, sn, pp.seed, GBP_EXTEND_STREAM,
+                        (st->ext_base + qi) * 8 + sl, a);  // rrt.cpp:34, :49
+      copy10(pp.ca + 10 * c, a);
+      copy8(pp.cs + 8 * c, sn);
+    }
     if (!stats) continue;  // diagnostics (GBP_OPT_NN_STATS): same-address atomics serialise
     for (int off = 32; off > 0; off >>= 1) {
       nrc += __shfl_xor(nrc, off);
@@ -1647,10 +1678,18 @@ __global__ __launch_bounds__(TB) void k_select(gbp_plan_status *st, const double
     ef[i] = fl;
     frag = frag || (fl & GBP_F_FRAGILE);
   }
-  // one atomic per wave for the statistics and the gate
+  // one atomic per workgroup for the statistics (same-address atomics
+  // serialise: one per wave cost ~2 us a launch), one per wave for the gate
   const int lane = threadIdx.x & (WAVE - 1);
   for (int off = WAVE / 2; off > 0; off >>= 1) executed += __shfl_down(executed, off);
-  if (lane == 0 && executed) atomicAdd((unsigned long long *)&st->stat_attempts, executed);
+  __shared__ unsigned long long s_exec[TB / WAVE];
+  if (lane == 0) s_exec[threadIdx.x / WAVE] = executed;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long e = 0;
+    for (int k = 0; k < TB / WAVE; k++) e += s_exec[k];
+    if (e) atomicAdd((unsigned long long *)&st->stat_attempts, e);
+  }
   if (__ballot(frag) && lane == 0) {
     atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_EXTEND);
     st->halt_half = half;
@@ -2005,9 +2044,13 @@ NnBucket nn_bucket_args(gbp_plan_ws *w, const gbp_tree *tr) {
   return nb;
 }
 
-// use_index: the search goes through tr's index
+// use_index: the search goes through tr's index; prep: the extends' candidate
+// inputs are written by the matrix-core search's reduce (returns *prepped)
+template <class ZT = float>
 int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
-              const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s, bool use_index = false) {
+              const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s, bool use_index = false,
+              const NhPrep<ZT> *prep = nullptr, bool *prepped = nullptr) {
+  if (prepped) *prepped = false;
   if (use_index && tr->idx_n > 0) {
     // the indexed search: queries bucketed by Morton cell, pruned chunk scans
     const unsigned gq = grid_for(w->bmax, TB, num_cus * 4);
@@ -2025,9 +2068,17 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
     hipLaunchKernelGGL((k_nn_mfma<NH_NT>), dim3(num_cus * (NH_ITEMS / 4) / 256), dim3(NH_TB), 0, s,
                        w->st, nq_dev, q, q_off_dev, tr->vh, tr->hm, tr->count, w->bmax,
                        (float4 *)w->nn_d, (int2 *)w->nn_i, ++w->seq);
-    hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(16 * w->bmax, NH_RTB, num_cus * 8)), dim3(NH_RTB),
-                       0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, tr->count, w->bmax,
-                       (const float4 *)w->nn_d, (const int2 *)w->nn_i, out, ++w->seq, w->nn_stats);
+    const dim3 g(grid_for(16 * w->bmax, NH_RTB, num_cus * 8));
+    if (prep) {
+      hipLaunchKernelGGL((k_nn_hreduce<ZT, true>), g, dim3(NH_RTB), 0, s, w->st, nq_dev, q, q_off_dev,
+                         tr->v, tr->hm, tr->count, w->bmax, (const float4 *)w->nn_d,
+                         (const int2 *)w->nn_i, out, ++w->seq, w->nn_stats, *prep);
+      if (prepped) *prepped = true;
+    } else {
+      hipLaunchKernelGGL((k_nn_hreduce<float, false>), g, dim3(NH_RTB), 0, s, w->st, nq_dev, q,
+                         q_off_dev, tr->v, tr->hm, tr->count, w->bmax, (const float4 *)w->nn_d,
+                         (const int2 *)w->nn_i, out, ++w->seq, w->nn_stats, NhPrep<float>{});
+    }
     return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   }
   // two queries per lane, four row pairs per scalar load, 8 workgroups per
@@ -2063,12 +2114,16 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     // the targets' nearest vertices through T's index when GBP_OPT_NN_INDEX
     // asks for it and the index holds at least that many vertices
     const bool idx = t->opt_nn_index > 0 && T->idx_n >= t->opt_nn_index;
-    int rc = nn_launch(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, idx);
+    const NhPrep<ZT> prep{V, seed, w->cs, w->ca, t->sampling, direction};
+    bool prepped = false;
+    int rc = nn_launch<ZT>(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, idx, &prep,
+                           &prepped);
     if (rc) return rc;
     const int64_t mmax = batch * GBP_NUM_GEN_STATES;
-    hipLaunchKernelGGL(k_extend_prep<ZT>, dim3(grid_for(mmax, TB, cus * 8)), dim3(TB), 0, s, V, st,
-                       w->targets, w->nn, T->v, seed, w->cs, w->ca, ++w->seq, t->sampling,
-                       direction);
+    if (!prepped)
+      hipLaunchKernelGGL(k_extend_prep<ZT>, dim3(grid_for(mmax, TB, cus * 8)), dim3(TB), 0, s, V, st,
+                         w->targets, w->nn, T->v, seed, w->cs, w->ca, ++w->seq, t->sampling,
+                         direction);
     rc = gbp_internal_validate_dev_n(t, mmax, &st->n_validate, w->cs, w->ca, nullptr, direction,
                                      adaptive, nullptr, w->csn, nullptr, w->cf, w->cc, s);
     if (rc) return rc;
