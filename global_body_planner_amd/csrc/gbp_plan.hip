@@ -769,15 +769,16 @@ __device__ __forceinline__ void nh_geometry(int64_t nq, int64_t nv, int64_t bmax
   if (want > nch) want = nch;
   if (want < 1) want = 1;
   cps = (nch + want - 1) / want;
+  cps += cps & 1;  // whole units (pairs of chunks)
   nseg = (nch + cps - 1) / cps;
 }
 
-// eps(G) above; g: the query's scaled coordinates, hm: the tree's hmax
-__device__ __forceinline__ double nh_eps(const double (&g)[8], const float *__restrict__ hm) {
+// eps(G) above; q: the query (G = 64 q), hm: the tree's hmax
+__device__ __forceinline__ double nh_eps(const double (&q)[8], const float *__restrict__ hm) {
   double mm = 0.0, gm = 0.0, lin = 0.0;
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    const double m = (double)hm[k] * (1.0 + 0x1p-22), ag = fabs(g[k]);
+    const double m = (double)hm[k] * (1.0 + 0x1p-22), ag = fabs(q[k] * NH_SCALE);
     mm += m * m;
     gm += ag * m;
     lin += (4.0 * 0x1p-20 * ag + 1.01 * 0x1p-14) * m + 1.01 * 0x1p-14 * ag + 0x1p-27;
@@ -791,80 +792,99 @@ __device__ __forceinline__ float nh_threshold(float B, double eps, double g2) {
   return isnan(t) ? INFINITY : nextafterf((float)t, INFINITY);
 }
 
-// min over the 16 scores of a lane (its half-chunk)
+// min of two (v_med3 against -inf: no canonicalising v_max as fminf brings)
+__device__ __forceinline__ float nh_min2(float a, float b) {
+  return __builtin_amdgcn_fmed3f(a, b, -INFINITY);
+}
+// min over the 16 scores of a lane: 7 v_min3 + 1 v_med3
 __device__ __forceinline__ float nh_min16(const nhacc &a) {
-  const float m0 = fminf(fminf(fminf(a[0], a[1]), a[2]), a[3]);
-  float m1 = fminf(fminf(a[4], a[5]), a[6]);
-  float m2 = fminf(fminf(a[7], a[8]), a[9]);
-  float m3 = fminf(fminf(a[10], a[11]), a[12]);
-  float m4 = fminf(fminf(a[13], a[14]), a[15]);
-  return fminf(fminf(fminf(m0, m1), fminf(m2, m3)), m4);
+  const float x0 = fminf(fminf(a[0], a[1]), a[2]), x1 = fminf(fminf(a[3], a[4]), a[5]);
+  const float x2 = fminf(fminf(a[6], a[7]), a[8]), x3 = fminf(fminf(a[9], a[10]), a[11]);
+  const float x4 = fminf(fminf(a[12], a[13]), a[14]);
+  return nh_min2(fminf(fminf(x0, x1), x2), fminf(fminf(x3, x4), a[15]));
 }
 
-// a lane's two smallest half-chunk minima (m1 <= m2, chunks i1, i2) and a
-// lower bound m3 on every other half-chunk's minimum
+// a lane's two smallest unit minima (m1 <= m2, units i1, i2) and a lower
+// bound m3 on every other unit's minimum; branch-free (2 v_cmp, 2 v_med3,
+// 4 v_cndmask)
 struct NhTop {
   float m1 = INFINITY, m2 = INFINITY, m3 = INFINITY;
   int i1 = -1, i2 = -1;
   __device__ __forceinline__ void insert(float cm, int c) {
     const bool lt1 = cm < m1, lt2 = cm < m2;
-    m3 = __builtin_amdgcn_fmed3f(m2, cm, m3);
-    m2 = __builtin_amdgcn_fmed3f(m1, cm, m2);
-    i2 = lt1 ? i1 : (lt2 ? c : i2);
-    i1 = lt1 ? c : i1;
-    m1 = fminf(m1, cm);
+    const float n3 = __builtin_amdgcn_fmed3f(m2, cm, m3), n2 = __builtin_amdgcn_fmed3f(m1, cm, m2);
+    const int j1 = lt1 ? c : i1, j2a = lt1 ? i1 : c, j2 = lt2 ? j2a : i2;
+    const float n1 = lt1 ? cm : m1;
+    m1 = n1;
+    m2 = n2;
+    m3 = n3;
+    i1 = j1;
+    i2 = j2;
   }
 };
 
-// pass of one wave over chunks [c0, c1) (wave-uniform, as is nv): NT query
-// tiles (B operands b1, b2).  Lane (r, h) reads row c*32 + r: part h (F_hi /
-// F_lo) for MFMA 1 and part 2 + h (F_hi / norm) for MFMA 2, two 16-B loads
-// with one address; the row arrays hold whole chunks (tree_alloc), rows past
-// nv are masked.
+// pass of one wave over chunks [c0, c1) (c0 even; wave-uniform, as is nv):
+// NT query tiles (B operands b1, b2).  Lane (r, h) reads row c*32 + r: part
+// h (F_hi / F_lo) for MFMA 1 and part 2 + h (F_hi / norm) for MFMA 2, two
+// 16-B loads with one address; the row arrays hold whole units (tree_alloc),
+// rows past nv are masked.  A lane's unit u is its 32 rows of chunks 2u and
+// 2u + 1 (rows 64u + 32b + 4h + (i & 3) + 8 (i >> 2), b < 2, i < 16): the
+// top-2 bookkeeping runs once per unit
 template <int NT>
 __device__ __forceinline__ void nh_sweep(const _Float16 *__restrict__ vh, int c0, int c1, int nv,
                                          const nh8 (&b1)[NT], const nh8 (&b2)[NT], NhTop (&t)[NT]) {
   const int lane = threadIdx.x & (WAVE - 1), r = lane & 31, h = lane >> 5;
   const nh8 *base = (const nh8 *)vh + (NH_ROW / 8) * r + h;
   constexpr int64_t CS = NH_ROW * 4;  // nh8 per chunk
-  // scores of chunk c for every tile; TAIL: the last chunk, rows past nv masked
-  auto score = [&](int c, const nh8 &a1, const nh8 &a2, auto tail_tag) {
+  // tile u's minimum over its lane-unit: the scores of chunks c and c + 1
+  // (TAIL: rows past nv masked, chunk c + 1 absent when c + 1 >= c1)
+  auto unit_min = [&](int u, int c, const nh8 (&a)[4], auto tail_tag) {
     constexpr bool TAIL = decltype(tail_tag)::value;
+    float m = INFINITY;
 #pragma unroll
-    for (int u = 0; u < NT; u++) {
-      nhacc acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1[u], nhacc{}, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2, b2[u], acc, 0, 0, 0);
+    for (int k = 0; k < 2; k++) {
+      if (TAIL && c + k >= c1) break;
+      nhacc acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * k], b1[u], nhacc{}, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * k + 1], b2[u], acc, 0, 0, 0);
       if (TAIL) {
-        const int rem = nv - 32 * c;
+        const int rem = nv - 32 * (c + k);
 #pragma unroll
         for (int i = 0; i < 16; i++)
           if ((i & 3) + 8 * (i >> 2) + 4 * h >= rem) acc[i] = INFINITY;
       }
-      t[u].insert(nh_min16(acc), c);
+      m = k ? nh_min2(m, nh_min16(acc)) : nh_min16(acc);
     }
+    return m;
   };
-  // the full chunks, two chunks' rows in flight ahead of the one being scored
-  const int cf = min(c1, nv >> 5);
-  if (c0 < cf) {
-    nh8 a1 = base[CS * c0], a2 = base[CS * c0 + 2], p1, p2, q1, q2;
-    if (c0 + 1 < cf) {
-      p1 = base[CS * (c0 + 1)];
-      p2 = base[CS * (c0 + 1) + 2];
-    }
-    for (int c = c0; c < cf; c++) {
-      if (c + 2 < cf) {
-        q1 = base[CS * (c + 2)];
-        q2 = base[CS * (c + 2) + 2];
+  auto load = [&](int c, nh8 (&d)[4]) {
+    d[0] = base[CS * c];
+    d[1] = base[CS * c + 2];
+    d[2] = base[CS * (c + 1)];
+    d[3] = base[CS * (c + 1) + 2];
+  };
+  // full units, the next unit's rows in flight while one is scored; a
+  // scheduling barrier per tile keeps one tile's accumulators live at a time
+  const int uf = min(c1, nv >> 5) & ~1;  // chunks [c0, uf) form full units
+  if (c0 < uf) {
+    nh8 a[4], p[4];
+    load(c0, a);
+    for (int c = c0; c < uf; c += 2) {
+      if (c + 2 < uf) load(c + 2, p);
+#pragma unroll
+      for (int u = 0; u < NT; u++) {
+        t[u].insert(unit_min(u, c, a, std::false_type{}), c >> 1);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      score(c, a1, a2, std::false_type{});
-      a1 = p1;
-      a2 = p2;
-      p1 = q1;
-      p2 = q2;
+#pragma unroll
+      for (int k = 0; k < 4; k++) a[k] = p[k];
     }
   }
-  if (cf < c1)  // the tree's last, partial chunk (the row arrays hold whole chunks)
-    score(cf, base[CS * cf], base[CS * cf + 2], std::true_type{});
+  if (uf < c1) {  // the last unit: a lone chunk and/or rows past the tree's end
+    nh8 a[4];
+    load(uf, a);  // the row arrays hold whole units
+#pragma unroll
+    for (int u = 0; u < NT; u++) t[u].insert(unit_min(u, uf, a, std::true_type{}), uf >> 1);
+  }
 }
 
 template <int NT>
@@ -911,8 +931,7 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(const gbp_plan_status *__rest
       nh_sweep<NT>(vh, c0, c1, (int)nv, b1, b2, t);
     }
     // the two lanes of a query (rows 4h + ...): merge to one entry, the two
-    // smallest half-chunks (half-chunk id = 2 chunk + h) and a lower bound on
-    // the rest
+    // smallest lane-units (id = 2 unit + h) and a lower bound on the rest
 #pragma unroll
     for (int u = 0; u < NT; u++) {
       const float a1 = t[u].m1, a2 = t[u].m2, a3 = t[u].m3;
@@ -939,24 +958,10 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(const gbp_plan_status *__rest
   }
 }
 
-// newConfig's candidate inputs for the extends (stage 2), fused into the
-// reduce of the targets' search when GBP_OPT_NN_FILTER is 0: rrt.cpp:25
-// surface normal, :34 the six actions (Philox extend stream; direction-biased
-// draws see s_near = the nearest vertex just found), s_near copied per
-// candidate — what k_extend_prep does
-template <class ZT>
-struct NhPrep {
-  TerrainView<ZT> T;
-  uint64_t seed;
-  double *cs, *ca;
-  gbp_sampling cfg;
-  int direction;
-};
-
 // 16 lanes per query: B, T(B), the fp64 re-checks, lexicographic (distance,
-// index) minimum; nothing < inf (a NaN query): index 0.  PREP: lanes 0-5 of
-// the query's group then write its six extend candidates (NhPrep)
-template <class ZT, bool PREP>
+// index) minimum; nothing < inf (a NaN query): index 0.  (Writing the six
+// extend candidates from here instead of k_extend_prep was measured slower:
+// the sampler's registers halved the reduce's occupancy, 16 + 15.9 -> 63 us.)
 __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
                                                        const int32_t *__restrict__ nq_dev,
                                                        const double *__restrict__ q,
@@ -967,13 +972,8 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
                                                        int64_t bmax, const float4 *__restrict__ pm,
                                                        const int2 *__restrict__ pid,
                                                        int32_t *__restrict__ out, uint64_t seq,
-                                                       int stats, NhPrep<ZT> pp) {
-  if (gated(st, seq)) {
-    if (PREP && blockIdx.x == 0 && threadIdx.x == 0) st->n_validate = 0;  // the validate launch idles
-    return;
-  }
-  if (PREP && blockIdx.x == 0 && threadIdx.x == 0)
-    st->n_validate = (int32_t)(st->n_targets * GBP_NUM_GEN_STATES);
+                                                       int stats) {
+  if (gated(st, seq)) return;
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   int64_t nqg, nseg, cps, nch;
   nh_geometry(nq, nv, bmax, nqg, nseg, cps, nch);
@@ -984,27 +984,25 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
   for (int64_t it = 0; it < iters; it++) {
     const int64_t qi = it * groups + blockIdx.x * (int64_t)(NH_RTB / 16) + threadIdx.x / 16;
     const bool live = qi < nq;
-    double qq[8], g[8], g2 = 0.0;
+    double qq[8], g2 = 0.0;
     bool qbad = false;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       qq[k] = live ? q[8 * (q_off + qi) + k] : 0.0;
-      g[k] = qq[k] * NH_SCALE;
-      qbad = qbad || !(fabs(g[k]) < NH_LIM);
-      g2 += g[k] * g[k];
+      const double gk = qq[k] * NH_SCALE;
+      qbad = qbad || !(fabs(gk) < NH_LIM);
+      g2 += gk * gk;
     }
-    // the group's entries, lane sl holding segments sl, sl + 16, ... (<= 4)
-    float4 e[NH_MAX_SEG / 16];
+    // the group's entries, lane sl reading segments sl, sl + 16, ... (<= 4)
     float B = INFINITY;
 #pragma unroll
     for (int k = 0; k < NH_MAX_SEG / 16; k++) {
       const int64_t s = sl + 16 * k;
-      e[k] = live && s < nseg ? pm[s * nq + qi] : float4{INFINITY, INFINITY, INFINITY, 0.f};
-      B = fminf(B, e[k].x);
+      if (live && s < nseg) B = fminf(B, pm[s * nq + qi].x);
     }
 #pragma unroll
     for (int off = 8; off > 0; off >>= 1) B = fminf(B, __shfl_xor(B, off, 16));
-    const float T = nh_threshold(B, nh_eps(g, hm), g2);
+    const float T = nh_threshold(B, nh_eps(qq, hm), g2);
     double best = INFINITY;
     int bi = 0x7FFFFFFF, nrc = 0, nsc = 0;
     if (live && (qbad || tree_bad || !(B < INFINITY))) {  // the whole tree in fp64
@@ -1023,18 +1021,17 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
     // critical path)
     const bool part = live && !(qbad || tree_bad || !(B < INFINITY));
     const int gbit = (threadIdx.x & (WAVE - 1)) & ~15;
-#pragma unroll
-    for (int k = 0; k < NH_MAX_SEG / 16; k++) {
-      if (16 * k >= nseg) break;  // wave-uniform
-      const int64_t s0 = 16 * k, s = s0 + sl;
+    for (int64_t s0 = 0; s0 < nseg; s0 += 16) {
+      const int64_t s = s0 + sl;
       bool chk1 = false, chk2 = false, scan = false;
       int2 hid = {-1, -1};
       if (part && s < nseg) {
-        scan = e[k].z <= T;  // a third half-chunk within T: the segment in full
-        if (!scan && e[k].x <= T) {
+        const float4 e = pm[s * nq + qi];  // L2-warm since the first pass
+        scan = e.z <= T;  // a third half-chunk within T: the segment in full
+        if (!scan && e.x <= T) {
           hid = pid[s * nq + qi];
           chk1 = hid.x >= 0;
-          chk2 = e[k].y <= T && hid.y >= 0;
+          chk2 = e.y <= T && hid.y >= 0;
         }
       }
       uint32_t cmask = (uint32_t)(__ballot(chk1) >> gbit) & 0xFFFFu;
@@ -1054,12 +1051,17 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
             cmask2 &= cmask2 - 1u;
             h = __shfl(hid.y, src, 16);
           }
-          const int64_t j = (int64_t)(h >> 1) * 32 + 4 * (h & 1) + (sl & 3) + 8 * (sl >> 2);
-          if (j < nv) {
-            const double d = nn_dist64(qq, v + 8 * j);
-            if (d < best || (d == best && j < bi)) {
-              best = d;
-              bi = (int)j;
+          // the lane-unit's 32 rows, two per lane
+#pragma unroll
+          for (int b = 0; b < 2; b++) {
+            const int64_t j =
+                (int64_t)(h >> 1) * 64 + 32 * b + 4 * (h & 1) + (sl & 3) + 8 * (sl >> 2);
+            if (j < nv) {
+              const double d = nn_dist64(qq, v + 8 * j);
+              if (d < best || (d == best && j < bi)) {
+                best = d;
+                bi = (int)j;
+              }
             }
           }
         }
@@ -1069,17 +1071,12 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
           const int64_t ss = s0 + (__ffs(smask) - 1);
           smask &= smask - 1u;
           const int64_t j1 = min(nv, min(nch, (ss + 1) * cps) * 32);
-          for (int64_t j = ss * cps * 32 + sl; j < j1; j += 64) {  // 4 rows in flight
-            double d[4];
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-              d[r] = j + 16 * r < j1 ? nn_dist64(qq, v + 8 * (j + 16 * r)) : INFINITY;
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-              if (d[r] < best || (d[r] == best && j + 16 * r < bi)) {
-                best = d[r];
-                bi = (int)(j + 16 * r);
-              }
+          for (int64_t j = ss * cps * 32 + sl; j < j1; j += 16) {
+            const double d = nn_dist64(qq, v + 8 * j);
+            if (d < best || (d == best && j < bi)) {
+              best = d;
+              bi = (int)j;
+            }
           }
         }
       }
@@ -1094,16 +1091,6 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
       }
     }
     if (live && sl == 0) out[qi] = bi == 0x7FFFFFFF ? 0 : bi;
-    if (PREP && live && sl < GBP_NUM_GEN_STATES) {
-      const int64_t c = qi * GBP_NUM_GEN_STATES + sl;
-      const double *sn = v + 8 * (int64_t)(bi == 0x7FFFFFFF ? 0 : bi);
-      double nrm[3], a[10];
-      surface_normal(pp.T, qq[0], qq[1], nrm);  // rrt.cpp:25
-      sample_action_cfg(nrm, pp.cfg, pp.direction, qq, sn, pp.seed, GBP_EXTEND_STREAM,
-                        (st->ext_base + qi) * 8 + sl, a);  // rrt.cpp:34, :49
-      copy10(pp.ca + 10 * c, a);
-      copy8(pp.cs + 8 * c, sn);
-    }
     if (!stats) continue;  // diagnostics (GBP_OPT_NN_STATS): same-address atomics serialise
     for (int off = 32; off > 0; off >>= 1) {
       nrc += __shfl_xor(nrc, off);
@@ -2044,13 +2031,9 @@ NnBucket nn_bucket_args(gbp_plan_ws *w, const gbp_tree *tr) {
   return nb;
 }
 
-// use_index: the search goes through tr's index; prep: the extends' candidate
-// inputs are written by the matrix-core search's reduce (returns *prepped)
-template <class ZT = float>
+// use_index: the search goes through tr's index
 int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
-              const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s, bool use_index = false,
-              const NhPrep<ZT> *prep = nullptr, bool *prepped = nullptr) {
-  if (prepped) *prepped = false;
+              const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s, bool use_index = false) {
   if (use_index && tr->idx_n > 0) {
     // the indexed search: queries bucketed by Morton cell, pruned chunk scans
     const unsigned gq = grid_for(w->bmax, TB, num_cus * 4);
@@ -2068,17 +2051,9 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
     hipLaunchKernelGGL((k_nn_mfma<NH_NT>), dim3(num_cus * (NH_ITEMS / 4) / 256), dim3(NH_TB), 0, s,
                        w->st, nq_dev, q, q_off_dev, tr->vh, tr->hm, tr->count, w->bmax,
                        (float4 *)w->nn_d, (int2 *)w->nn_i, ++w->seq);
-    const dim3 g(grid_for(16 * w->bmax, NH_RTB, num_cus * 8));
-    if (prep) {
-      hipLaunchKernelGGL((k_nn_hreduce<ZT, true>), g, dim3(NH_RTB), 0, s, w->st, nq_dev, q, q_off_dev,
-                         tr->v, tr->hm, tr->count, w->bmax, (const float4 *)w->nn_d,
-                         (const int2 *)w->nn_i, out, ++w->seq, w->nn_stats, *prep);
-      if (prepped) *prepped = true;
-    } else {
-      hipLaunchKernelGGL((k_nn_hreduce<float, false>), g, dim3(NH_RTB), 0, s, w->st, nq_dev, q,
-                         q_off_dev, tr->v, tr->hm, tr->count, w->bmax, (const float4 *)w->nn_d,
-                         (const int2 *)w->nn_i, out, ++w->seq, w->nn_stats, NhPrep<float>{});
-    }
+    hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(16 * w->bmax, NH_RTB, num_cus * 8)), dim3(NH_RTB),
+                       0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, tr->count, w->bmax,
+                       (const float4 *)w->nn_d, (const int2 *)w->nn_i, out, ++w->seq, w->nn_stats);
     return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   }
   // two queries per lane, four row pairs per scalar load, 8 workgroups per
@@ -2114,16 +2089,12 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     // the targets' nearest vertices through T's index when GBP_OPT_NN_INDEX
     // asks for it and the index holds at least that many vertices
     const bool idx = t->opt_nn_index > 0 && T->idx_n >= t->opt_nn_index;
-    const NhPrep<ZT> prep{V, seed, w->cs, w->ca, t->sampling, direction};
-    bool prepped = false;
-    int rc = nn_launch<ZT>(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, idx, &prep,
-                           &prepped);
+    int rc = nn_launch(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, idx);
     if (rc) return rc;
     const int64_t mmax = batch * GBP_NUM_GEN_STATES;
-    if (!prepped)
-      hipLaunchKernelGGL(k_extend_prep<ZT>, dim3(grid_for(mmax, TB, cus * 8)), dim3(TB), 0, s, V, st,
-                         w->targets, w->nn, T->v, seed, w->cs, w->ca, ++w->seq, t->sampling,
-                         direction);
+    hipLaunchKernelGGL(k_extend_prep<ZT>, dim3(grid_for(mmax, TB, cus * 8)), dim3(TB), 0, s, V, st,
+                       w->targets, w->nn, T->v, seed, w->cs, w->ca, ++w->seq, t->sampling,
+                       direction);
     rc = gbp_internal_validate_dev_n(t, mmax, &st->n_validate, w->cs, w->ca, nullptr, direction,
                                      adaptive, nullptr, w->csn, nullptr, w->cf, w->cc, s);
     if (rc) return rc;
@@ -2195,7 +2166,7 @@ int tree_alloc(gbp_tree *t, int64_t cap) {
   if (hipMalloc(&v, 64 * cap) != hipSuccess) return GBP_E_ALLOC;
   if (hipMalloc(&a, 80 * cap) != hipSuccess || hipMalloc(&g, 8 * cap) != hipSuccess ||
       hipMalloc(&p, 4 * cap) != hipSuccess || hipMalloc(&vf, 4 * NN_PAIR * ((cap + 1) / 2)) != hipSuccess ||
-        hipMalloc(&vh, 2 * NH_ROW * ((cap + 31) & ~(int64_t)31)) != hipSuccess) {
+        hipMalloc(&vh, 2 * NH_ROW * ((cap + 63) & ~(int64_t)63)) != hipSuccess) {
     (void)hipFree(v);
     if (a) (void)hipFree(a);
     if (g) (void)hipFree(g);

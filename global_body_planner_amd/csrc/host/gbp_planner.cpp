@@ -1598,6 +1598,8 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
   st.connects += ps.stat_added;
   st.fragile_resolved += ps.stat_fragile_resolved;
   st.depth_capped += ps.stat_depth_capped;
+  st.nn_rechecks += ps.stat_nn_rechecks;
+  st.nn_scans += ps.stat_nn_scans;
   HostTree A, B;
   read_tree(D.tree[0], D.stream, A);
   read_tree(D.tree[1], D.stream, B);
@@ -2066,6 +2068,7 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
       chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_NN_INDEX, p->nn_index < 0 ? 0 : p->nn_index),
           "nn index");
     chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_NN_FILTER, p->nn_filter), "nn filter");
+    chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_NN_STATS, p->nn_stats), "nn stats");
     RRTStarConnectClass planner;  // is-a RRTConnectClass: algorithm 0 uses the plain build
     planner.setSeed(p->seed);
     planner.set_state_direction_sampling(p->sampling.state_flag != 0, p->sampling.state_p,
@@ -2121,6 +2124,8 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     r->depth_capped = st.depth_capped;
     r->status_reads = st.status_reads;
     for (int k = 0; k < 3; k++) r->halts[k] = st.halts[k];
+    r->nn_rechecks = st.nn_rechecks;
+    r->nn_scans = st.nn_scans;
     if (found) {
       double len = 0;
       for (size_t i = 1; i < states.size(); i++) len += planning_utils::poseDistance(states[i - 1], states[i]);

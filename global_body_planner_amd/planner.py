@@ -29,7 +29,7 @@ class PlanParams(ctypes.Structure):
                 ("algorithm", ctypes.c_int), ("max_time_opt", _D),
                 ("sampling", _lib.Sampling), ("fragile_eps_fm", ctypes.c_int64),
                 ("adaptive", ctypes.c_int), ("nn_index", ctypes.c_int64),
-                ("nn_filter", ctypes.c_int)]
+                ("nn_filter", ctypes.c_int), ("nn_stats", ctypes.c_int)]
 
 
 class PlanResult(ctypes.Structure):
@@ -42,7 +42,8 @@ class PlanResult(ctypes.Structure):
                 ("rewires", ctypes.c_int64), ("solutions", ctypes.c_int64),
                 ("extent_a", _D * 4), ("extent_b", _D * 4),
                 ("fragile_resolved", ctypes.c_int64), ("depth_capped", ctypes.c_int64),
-                ("status_reads", ctypes.c_int64), ("halts", ctypes.c_int64 * 3)]
+                ("status_reads", ctypes.c_int64), ("halts", ctypes.c_int64 * 3),
+                ("nn_rechecks", ctypes.c_int64), ("nn_scans", ctypes.c_int64)]
 
 
 _planner = None
@@ -100,7 +101,7 @@ def start_goal_state(height, x, y):
 def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018,
                      post_process=False, device=0, capacity=4096, algorithm=0, max_time_opt=0.0,
                      sampling=None, fragile_eps=None, adaptive=False, nn_index=0,
-                     nn_filter=0):
+                     nn_filter=0, nn_stats=False):
     """Plan start -> goal on terrain `data` (terrain_data.TerrainData).
 
     algorithm 0: batch-synchronous RRT-Connect, stops at the first solution;
@@ -144,6 +145,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     p.adaptive = int(bool(adaptive))
     p.nn_index = int(nn_index)
     p.nn_filter = int(nn_filter)
+    p.nn_stats = int(bool(nn_stats))
     r = PlanResult()
     states = np.zeros((capacity, 8))
     actions = np.zeros((capacity, 10))

@@ -384,6 +384,8 @@ struct BatchStats {
   int64_t fragile_resolved = 0;  // attempts re-decided on the host (GBP_F_RESOLVED)
   int64_t halts[3] = {0, 0, 0};  // device loop: FRAGILE halts in the targets / extend /
                                  // connect stage (GBP_PLAN_HALT_*)
+  int64_t nn_rechecks = 0, nn_scans = 0;  // device loop with GBP_OPT_NN_STATS: the matrix-core
+                                          // search's fp64 half-chunk re-checks / segment scans
   double extent_a[4] = {0, 0, 0, 0}, extent_b[4] = {0, 0, 0, 0};  // x_min x_max y_min y_max
 };
 
@@ -602,6 +604,7 @@ typedef struct {
   int64_t nn_index;       // GBP_OPT_NN_INDEX: trees of at least this many vertices search
                           // through their index (0 = the handle's default, off; < 0 = off)
   int nn_filter;          // GBP_OPT_NN_FILTER: 0 matrix cores (default), 1 packed fp32
+  int nn_stats;           // GBP_OPT_NN_STATS: count the search's fp64 re-checks (diagnostics)
 } gbp_plan_params;
 
 typedef struct {
@@ -618,6 +621,8 @@ typedef struct {
   int64_t status_reads;        // algorithm 3: host synchronisations of the device loop
   int64_t halts[3];            // algorithm 3/4: FRAGILE halts in the targets / extend /
                                // connect stage of the device loop
+  int64_t nn_rechecks, nn_scans;  // algorithm 3 with nn_stats: the matrix-core search's
+                                  // fp64 half-chunk re-checks and segment scans
 } gbp_plan_result;
 
 /* plans from start to goal; path_states[capacity][8] / path_actions[capacity][10]
