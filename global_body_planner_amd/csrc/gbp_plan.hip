@@ -102,6 +102,7 @@ struct gbp_plan_ws {
   double *cand = nullptr;      // [bmax][8] drawn states
   uint32_t *cflag = nullptr;   // [bmax] their isValidState flags
   double *targets = nullptr;   // [bmax][8] the valid ones, in draw order
+  _Float16 *tqh = nullptr;     // [bmax][NH_ROW] their fp16 rows (k_nn_mfma's queries)
   // stage 2-3
   int32_t *nn = nullptr;       // [bmax] nearest vertex of T per target
   double *cs = nullptr;        // [6 bmax][8] candidate s_near
@@ -734,6 +735,7 @@ __device__ __forceinline__ void nn_put_hrow(_Float16 *__restrict__ vh, float *__
     fl[k] = lo;
     n = n + x * x;
     const float ax = ok ? (float)fabs(x) : 0.f;
+    if (!hm) continue;  // a query row
     if (init)
       hm[k] = ax;
     else
@@ -750,6 +752,7 @@ __device__ __forceinline__ void nn_put_hrow(_Float16 *__restrict__ vh, float *__
   r[1] = fl;
   r[2] = fh;
   r[3] = nr;
+  if (!hm) return;
   if (init)
     ((uint32_t *)hm)[8] = bad ? 1u : 0u;
   else if (bad)
@@ -892,6 +895,7 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(const gbp_plan_status *__rest
                                                    const int32_t *__restrict__ nq_dev,
                                                    const double *__restrict__ q,
                                                    const int32_t *__restrict__ q_off_dev,
+                                                   const _Float16 *__restrict__ qh,
                                                    const _Float16 *__restrict__ vh,
                                                    const float *__restrict__ hm,
                                                    const int32_t *__restrict__ nv_dev, int64_t bmax,
@@ -911,17 +915,25 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(const gbp_plan_status *__rest
     const int c0 = sg * (int)cps, c1 = min((int)nch, c0 + (int)cps);
     nh8 b1[NT], b2[NT];
     NhTop t[NT];
+    const nh8 ncst = {(_Float16)NH_NCONST, (_Float16)NH_NCONST, (_Float16)NH_NCONST, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int u = 0; u < NT; u++) {
       const int64_t qi = qg * (32 * NT) + 32 * u + r;
       const bool live = qi < nq;
+      if (qh) {  // the queries' fp16 rows (nn_put_hrow layout: F_hi, F_lo)
+        const nh8 *qr = (const nh8 *)(qh + (int64_t)NH_ROW * (q_off + (live ? qi : 0)));
+        const nh8 zh = {}, hi = live ? qr[0] : zh, lo = live ? qr[1] : zh;
+        b1[u] = hi * (_Float16)(-2.0f);
+        b2[u] = h ? ncst : lo * (_Float16)(-2.0f);
+      } else {
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const double x = live ? q[8 * (q_off + qi) + k] * NH_SCALE : 0.0;
-        _Float16 hi, lo;
-        nh_split(fabs(x) < NH_LIM ? x : 0.0, hi, lo);  // a bad query is scanned in fp64
-        b1[u][k] = (_Float16)(-2.0f) * hi;
-        b2[u][k] = h ? (k < 3 ? (_Float16)NH_NCONST : (_Float16)0.0f) : (_Float16)(-2.0f) * lo;
+        for (int k = 0; k < 8; k++) {
+          const double x = live ? q[8 * (q_off + qi) + k] * NH_SCALE : 0.0;
+          _Float16 hi, lo;
+          nh_split(fabs(x) < NH_LIM ? x : 0.0, hi, lo);  // a bad query is scanned in fp64
+          b1[u][k] = (_Float16)(-2.0f) * hi;
+          b2[u][k] = h ? ncst[k] : (_Float16)(-2.0f) * lo;
+        }
       }
     }
     if (tree_bad) {  // every segment scanned in fp64 by the reduce
@@ -1066,18 +1078,42 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
           }
         }
       }
-      while (__ballot(smask != 0u)) {
-        if (smask) {
-          const int64_t ss = s0 + (__ffs(smask) - 1);
-          smask &= smask - 1u;
-          const int64_t j1 = min(nv, min(nch, (ss + 1) * cps) * 32);
-          for (int64_t j = ss * cps * 32 + sl; j < j1; j += 16) {
-            const double d = nn_dist64(qq, v + 8 * j);
-            if (d < best || (d == best && j < bi)) {
-              best = d;
-              bi = (int)j;
-            }
+      // segment scans, the whole wave on one (group, segment) at a time: the
+      // planner's clustered trees ask for a few per launch, and one group
+      // walking ~1k rows alone was the launch's tail
+      for (;;) {
+        const unsigned long long pend = __ballot(smask != 0u);
+        if (!pend) break;
+        const int src = __ffsll((long long)pend) - 1;  // first lane of the owning group
+        const uint32_t sm = (uint32_t)__shfl((int)smask, src);
+        const bool owner = gbit == (src & ~15);
+        if (owner) smask &= smask - 1u;
+        double oq[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) oq[k] = __shfl(qq[k], src);
+        const int64_t ss = s0 + (__ffs(sm) - 1);
+        const int64_t j1 = min(nv, min(nch, (ss + 1) * cps) * 32);
+        double wb = INFINITY;
+        int wi = 0x7FFFFFFF;
+        for (int64_t j = ss * cps * 32 + (threadIdx.x & (WAVE - 1)); j < j1; j += WAVE) {
+          const double d = nn_dist64(oq, v + 8 * j);
+          if (d < wb) {  // ascending per lane
+            wb = d;
+            wi = (int)j;
           }
+        }
+#pragma unroll
+        for (int off = WAVE / 2; off > 0; off >>= 1) {
+          const double od = __shfl_xor(wb, off);
+          const int oi = __shfl_xor(wi, off);
+          if (od < wb || (od == wb && oi < wi)) {
+            wb = od;
+            wi = oi;
+          }
+        }
+        if (owner && (wb < best || (wb == best && wi < bi))) {
+          best = wb;
+          bi = wi;
         }
       }
     }
@@ -1354,13 +1390,17 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
                                                         const double *__restrict__ cand,
                                                         const uint32_t *__restrict__ cflag,
                                                         double *__restrict__ targets,
+                                                        _Float16 *__restrict__ tqh,
                                                         unsigned long long *tiles, uint32_t epoch,
                                                         uint64_t seq) {
   if (gated(st, seq)) return;
   const int64_t i = blockIdx.x * (int64_t)CB + threadIdx.x;
   const bool keep = i < n && (cflag[i] & GBP_F_VALID);
   const uint32_t r = ordered_rank(keep, tiles, epoch, &st->n_targets, st);
-  if (keep) copy8(targets + 8 * (size_t)r, cand + 8 * i);
+  if (keep) {
+    copy8(targets + 8 * (size_t)r, cand + 8 * i);
+    nn_put_hrow(tqh, nullptr, r, cand + 8 * i, false);  // the search's query rows
+  }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
     // the extend stream of this half: RRTClass::extend_counter_ advances by
     // the number of extends (csrc/host/gbp_planner.cpp extendBatch)
@@ -2031,9 +2071,11 @@ NnBucket nn_bucket_args(gbp_plan_ws *w, const gbp_tree *tr) {
   return nb;
 }
 
-// use_index: the search goes through tr's index
+// use_index: the search goes through tr's index; qh: the queries' fp16 rows
+// (nn_put_hrow layout, same offsets as q) for the matrix-core search
 int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
-              const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s, bool use_index = false) {
+              const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s, bool use_index = false,
+              const _Float16 *qh = nullptr) {
   if (use_index && tr->idx_n > 0) {
     // the indexed search: queries bucketed by Morton cell, pruned chunk scans
     const unsigned gq = grid_for(w->bmax, TB, num_cus * 4);
@@ -2049,7 +2091,7 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
   }
   if (w->nn_mode == 0) {  // the matrix cores (k_nn_mfma), GBP_OPT_NN_FILTER 0
     hipLaunchKernelGGL((k_nn_mfma<NH_NT>), dim3(num_cus * (NH_ITEMS / 4) / 256), dim3(NH_TB), 0, s,
-                       w->st, nq_dev, q, q_off_dev, tr->vh, tr->hm, tr->count, w->bmax,
+                       w->st, nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
                        (float4 *)w->nn_d, (int2 *)w->nn_i, ++w->seq);
     hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(16 * w->bmax, NH_RTB, num_cus * 8)), dim3(NH_RTB),
                        0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, tr->count, w->bmax,
@@ -2084,12 +2126,12 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
                        t->sampling, T->v, T->count, O ? O->v : T->v, direction);
   if (first_stage <= 1 && last_stage >= 1)
     hipLaunchKernelGGL(k_compact_targets, dim3(tiles_for(batch)), dim3(CB), 0, s, st, batch,
-                       w->cand, w->cflag, w->targets, w->tiles, next_epoch(w), ++w->seq);
+                       w->cand, w->cflag, w->targets, w->tqh, w->tiles, next_epoch(w), ++w->seq);
   if (first_stage <= 2 && last_stage >= 2) {
     // the targets' nearest vertices through T's index when GBP_OPT_NN_INDEX
     // asks for it and the index holds at least that many vertices
     const bool idx = t->opt_nn_index > 0 && T->idx_n >= t->opt_nn_index;
-    int rc = nn_launch(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, idx);
+    int rc = nn_launch(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, idx, w->tqh);
     if (rc) return rc;
     const int64_t mmax = batch * GBP_NUM_GEN_STATES;
     hipLaunchKernelGGL(k_extend_prep<ZT>, dim3(grid_for(mmax, TB, cus * 8)), dim3(TB), 0, s, V, st,
@@ -2110,7 +2152,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   const int cdir = direction == GBP_FORWARD ? GBP_REVERSE : GBP_FORWARD;
   if (first_stage <= 4 && last_stage >= 4) {
     // queries: T's new vertices, rows [added_base, added_base + n_added)
-    int rc = nn_launch(w, &st->n_added, T->v, &st->added_base, O, w->nno, cus, s);
+    int rc = nn_launch(w, &st->n_added, T->v, &st->added_base, O, w->nno, cus, s, false, T->vh);
     if (rc) return rc;
     const int cm = (t->opt_affine && t->affine) ? 2 : 0;
     const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * 4, (batch + 3) / 4));
@@ -2460,7 +2502,7 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   const int64_t b = max_batch, m = GBP_NUM_GEN_STATES * max_batch;
   const size_t bytes = sizeof(gbp_plan_status) + 8 * w->ntiles + 64 * b + 4 * b + 64 * b + 4 * b +
                        m * (64 + 80 + 64 + 4 + 4) + b * (4 + 4 + 64 + 80 + 4 + 4) +
-                       b * (4 + 4 + 64 + 80 + 4) + NN_MAX_CHUNKS * b * (16 + 8) +
+                       b * (4 + 4 + 64 + 80 + 4) + NN_MAX_CHUNKS * b * (16 + 8) + 64 * b + 256 +
                        4 * NN_QCELLS + 4 * NN_QCELLS * b + 4 * b + 64 * 256;
   if (hipMalloc(&w->block, bytes) != hipSuccess) {
     delete w;
@@ -2472,6 +2514,7 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->cand = carve<double>(p, 8 * b);
   w->cflag = carve<uint32_t>(p, b);
   w->targets = carve<double>(p, 8 * b);
+  w->tqh = carve<_Float16>(p, 32 * b);
   w->nn = carve<int32_t>(p, b);
   w->cs = carve<double>(p, 8 * m);
   w->ca = carve<double>(p, 10 * m);
