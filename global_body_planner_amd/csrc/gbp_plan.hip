@@ -2010,7 +2010,7 @@ __global__ void k_plan_reset(gbp_plan_status *st, int64_t ext_counter) {
 // standalone gbp_extend_tree_dev: the batch becomes stage 2's targets
 __global__ void k_extend_setup(gbp_plan_status *st, int64_t n, const int32_t *n_dev,
                                int64_t extend_base, const double *__restrict__ src,
-                               double *__restrict__ targets) {
+                               double *__restrict__ targets, _Float16 *__restrict__ tqh) {
   const int64_t m = n_dev ? *n_dev : n;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st->halt = 0;
@@ -2022,6 +2022,9 @@ __global__ void k_extend_setup(gbp_plan_status *st, int64_t n, const int32_t *n_
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < 8 * m;
        i += (int64_t)gridDim.x * blockDim.x)
     targets[i] = src[i];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x)
+    nn_put_hrow(tqh, nullptr, i, src + 8 * i, false);  // the search's query rows
 }
 
 __global__ void k_set_queries(gbp_plan_status *st, int32_t n) {
@@ -2608,7 +2611,7 @@ int gbp_extend_tree_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, int64_t n,
   Guard g(t->device);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_extend_setup, dim3(grid_for(8 * n, TB, t->num_cus * 4)), dim3(TB), 0, s,
-                     w->st, n, n_dev, extend_base, targets, w->targets);
+                     w->st, n, n_dev, extend_base, targets, w->targets, w->tqh);
   int rc = t->storage == GBP_STORAGE_F32
                ? enqueue_stages<float>(t, w, T, nullptr, 0, direction, n, seed, 0, 0, adaptive, 2,
                                        3, s)
