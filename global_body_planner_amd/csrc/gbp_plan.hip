@@ -890,8 +890,25 @@ __device__ __forceinline__ void nh_sweep(const _Float16 *__restrict__ vh, int c0
   }
 }
 
-template <int NT>
-__global__ __launch_bounds__(NH_TB) void k_nn_mfma(const gbp_plan_status *__restrict__ st,
+// newConfig's candidate actions for the extends (rrt.cpp:25 surface normal,
+// :34 the six draws of the extend stream) do not depend on the nearest vertex
+// unless the draws are direction-biased, so stage 2 computes them in extra
+// workgroups of the search's launch (PREP): they run beside the MFMA waves
+// (VALU and transcendental work next to matrix-core work) instead of as a
+// launch of their own after the search (k_extend_prep); the reduce then
+// copies s_near into the candidates (k_nn_hreduce cs).
+template <class ZT>
+struct NhPrep {
+  TerrainView<ZT> T;
+  uint64_t seed;
+  double *ca;
+  gbp_sampling cfg;
+  int direction;
+  int first_block;  // blocks [first_block, gridDim.x) draw the actions
+};
+
+template <int NT, class ZT, bool PREP>
+__global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__ st,
                                                    const int32_t *__restrict__ nq_dev,
                                                    const double *__restrict__ q,
                                                    const int32_t *__restrict__ q_off_dev,
@@ -900,14 +917,32 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(const gbp_plan_status *__rest
                                                    const float *__restrict__ hm,
                                                    const int32_t *__restrict__ nv_dev, int64_t bmax,
                                                    float4 *__restrict__ pm, int2 *__restrict__ pid,
-                                                   uint64_t seq) {
-  if (gated(st, seq)) return;
+                                                   uint64_t seq, NhPrep<ZT> pp) {
+  if (gated(st, seq)) {
+    if (PREP && blockIdx.x == pp.first_block && threadIdx.x == 0) st->n_validate = 0;
+    return;
+  }
+  if (PREP && (int)blockIdx.x >= pp.first_block) {  // the extends' candidate actions
+    const int64_t n = st->n_targets, m = n * GBP_NUM_GEN_STATES, base = st->ext_base;
+    if (blockIdx.x == pp.first_block && threadIdx.x == 0) st->n_validate = (int32_t)m;
+    for (int64_t c = (blockIdx.x - pp.first_block) * (int64_t)NH_TB + threadIdx.x; c < m;
+         c += (int64_t)(gridDim.x - pp.first_block) * NH_TB) {
+      const int64_t i = c / GBP_NUM_GEN_STATES;
+      const int j = (int)(c - i * GBP_NUM_GEN_STATES);
+      double nrm[3], a[10];
+      surface_normal(pp.T, q[8 * i], q[8 * i + 1], nrm);  // rrt.cpp:25
+      sample_action_cfg(nrm, pp.cfg, pp.direction, q + 8 * i, q + 8 * i /* unused: not biased */,
+                        pp.seed, GBP_EXTEND_STREAM, (base + i) * 8 + j, a);  // rrt.cpp:34, :49
+      copy10(pp.ca + 10 * c, a);
+    }
+    return;
+  }
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   int64_t nqg, nseg, cps, nch;
   nh_geometry(nq, nv, bmax, nqg, nseg, cps, nch);
   const bool tree_bad = ((const uint32_t *)hm)[8] != 0u || nv <= 0;
   const int lane = threadIdx.x & (WAVE - 1), r = lane & 31, h = lane >> 5;
-  const int waves = gridDim.x * (NH_TB / WAVE);
+  const int waves = (PREP ? pp.first_block : (int)gridDim.x) * (NH_TB / WAVE);
   const int items = (int)(nqg * nseg), ns = (int)nseg;
   for (int item = __builtin_amdgcn_readfirstlane(blockIdx.x * (NH_TB / WAVE) + threadIdx.x / WAVE);
        item < items; item += waves) {
@@ -984,7 +1019,7 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
                                                        int64_t bmax, const float4 *__restrict__ pm,
                                                        const int2 *__restrict__ pid,
                                                        int32_t *__restrict__ out, uint64_t seq,
-                                                       int stats) {
+                                                       int stats, double *__restrict__ cs) {
   if (gated(st, seq)) return;
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   int64_t nqg, nseg, cps, nch;
@@ -1127,6 +1162,8 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
       }
     }
     if (live && sl == 0) out[qi] = bi == 0x7FFFFFFF ? 0 : bi;
+    if (cs && live && sl < GBP_NUM_GEN_STATES)  // s_near of the six candidates (k_extend_prep)
+      copy8(cs + 8 * (qi * GBP_NUM_GEN_STATES + sl), v + 8 * (int64_t)(bi == 0x7FFFFFFF ? 0 : bi));
     if (!stats) continue;  // diagnostics (GBP_OPT_NN_STATS): same-address atomics serialise
     for (int off = 32; off > 0; off >>= 1) {
       nrc += __shfl_xor(nrc, off);
@@ -2075,10 +2112,15 @@ NnBucket nn_bucket_args(gbp_plan_ws *w, const gbp_tree *tr) {
 }
 
 // use_index: the search goes through tr's index; qh: the queries' fp16 rows
-// (nn_put_hrow layout, same offsets as q) for the matrix-core search
+// (nn_put_hrow layout, same offsets as q) for the matrix-core search; prep:
+// the extends' candidates are drawn inside the matrix-core search (returns
+// *prepped)
+template <class ZT = float>
 int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
               const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s, bool use_index = false,
-              const _Float16 *qh = nullptr) {
+              const _Float16 *qh = nullptr, const NhPrep<ZT> *prep = nullptr,
+              double *cs = nullptr, bool *prepped = nullptr) {
+  if (prepped) *prepped = false;
   if (use_index && tr->idx_n > 0) {
     // the indexed search: queries bucketed by Morton cell, pruned chunk scans
     const unsigned gq = grid_for(w->bmax, TB, num_cus * 4);
@@ -2093,12 +2135,24 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
     return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   }
   if (w->nn_mode == 0) {  // the matrix cores (k_nn_mfma), GBP_OPT_NN_FILTER 0
-    hipLaunchKernelGGL((k_nn_mfma<NH_NT>), dim3(num_cus * (NH_ITEMS / 4) / 256), dim3(NH_TB), 0, s,
-                       w->st, nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
-                       (float4 *)w->nn_d, (int2 *)w->nn_i, ++w->seq);
+    const int gm = num_cus * (NH_ITEMS / 4) / 256;  // the search's workgroups
+    if (prep) {
+      NhPrep<ZT> pp = *prep;
+      pp.first_block = gm;
+      const int gp = (int)grid_for(GBP_NUM_GEN_STATES * w->bmax, NH_TB, num_cus * 4);
+      hipLaunchKernelGGL((k_nn_mfma<NH_NT, ZT, true>), dim3(gm + gp), dim3(NH_TB), 0, s, w->st,
+                         nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
+                         (float4 *)w->nn_d, (int2 *)w->nn_i, ++w->seq, pp);
+      if (prepped) *prepped = true;
+    } else {
+      hipLaunchKernelGGL((k_nn_mfma<NH_NT, float, false>), dim3(gm), dim3(NH_TB), 0, s, w->st,
+                         nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
+                         (float4 *)w->nn_d, (int2 *)w->nn_i, ++w->seq, NhPrep<float>{});
+    }
     hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(16 * w->bmax, NH_RTB, num_cus * 8)), dim3(NH_RTB),
                        0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, tr->count, w->bmax,
-                       (const float4 *)w->nn_d, (const int2 *)w->nn_i, out, ++w->seq, w->nn_stats);
+                       (const float4 *)w->nn_d, (const int2 *)w->nn_i, out, ++w->seq, w->nn_stats,
+                       prep ? cs : nullptr);
     return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   }
   // two queries per lane, four row pairs per scalar load, 8 workgroups per
@@ -2134,12 +2188,19 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     // the targets' nearest vertices through T's index when GBP_OPT_NN_INDEX
     // asks for it and the index holds at least that many vertices
     const bool idx = t->opt_nn_index > 0 && T->idx_n >= t->opt_nn_index;
-    int rc = nn_launch(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, idx, w->tqh);
+    // the candidates' actions inside the search unless they are direction-biased
+    // (then they depend on s_near: k_extend_prep after the search)
+    const NhPrep<ZT> prep{V, seed, w->ca, t->sampling, direction, 0};
+    const bool early = !t->sampling.action_flag;
+    bool prepped = false;
+    int rc = nn_launch<ZT>(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, idx, w->tqh,
+                           early ? &prep : nullptr, w->cs, &prepped);
     if (rc) return rc;
     const int64_t mmax = batch * GBP_NUM_GEN_STATES;
-    hipLaunchKernelGGL(k_extend_prep<ZT>, dim3(grid_for(mmax, TB, cus * 8)), dim3(TB), 0, s, V, st,
-                       w->targets, w->nn, T->v, seed, w->cs, w->ca, ++w->seq, t->sampling,
-                       direction);
+    if (!prepped)
+      hipLaunchKernelGGL(k_extend_prep<ZT>, dim3(grid_for(mmax, TB, cus * 8)), dim3(TB), 0, s, V, st,
+                         w->targets, w->nn, T->v, seed, w->cs, w->ca, ++w->seq, t->sampling,
+                         direction);
     rc = gbp_internal_validate_dev_n(t, mmax, &st->n_validate, w->cs, w->ca, nullptr, direction,
                                      adaptive, nullptr, w->csn, nullptr, w->cf, w->cc, s);
     if (rc) return rc;

@@ -1,0 +1,44 @@
+"""Mean duration per position in the device planner's half-iteration, from a
+rocprofv3 --kernel-trace CSV of tools/plan_run.py (halves start at k_targets);
+the last --halves halves."""
+import argparse
+import csv
+import collections
+import re
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("trace")
+    p.add_argument("--halves", type=int, default=4000)
+    a = p.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    halves, cur = [], None
+    for r in rows:
+        n = r["Kernel_Name"]
+        if "k_targets" in n:
+            cur = []
+            halves.append(cur)
+        if cur is not None:
+            short = re.sub(r"^.*?(k_[a-z0-9_]+).*$", r"\1", n.replace("_ZN12_GLOBAL__N_1", ""))
+            short = re.sub(r"^\d+", "", short)
+            cur.append((short, int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    halves = [h for h in halves if len(h) >= 10][-a.halves:]
+    pos = collections.defaultdict(list)
+    span = []
+    for h in halves:
+        for i, (n, s, e) in enumerate(h):
+            pos[(i, n)].append((e - s) / 1e3)
+        span.append((h[-1][2] - h[0][1]) / 1e3)
+    tot = 0.0
+    for (i, n), v in sorted(pos.items()):
+        m = sum(v) / len(v)
+        tot += m
+        print(f"{i:3d} {n:28s} {len(v):6d} {m:8.1f} us")
+    print(f"sum of kernel means per half {tot:.1f} us; first-start to last-end per half "
+          f"{sum(span) / len(span):.1f} us over {len(halves)} halves")
+
+
+if __name__ == "__main__":
+    main()
