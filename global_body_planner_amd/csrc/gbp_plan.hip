@@ -1040,12 +1040,19 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
       qbad = qbad || !(fabs(gk) < NH_LIM);
       g2 += gk * gk;
     }
-    // the group's entries, lane sl reading segments sl, sl + 16, ... (<= 4)
+    // the group's entries, lane sl holding segments sl, sl + 16, ... (<= 4),
+    // values and unit ids read together
+    constexpr int KE = NH_MAX_SEG / 16;
+    float4 e[KE];
+    int2 hid[KE];
     float B = INFINITY;
 #pragma unroll
-    for (int k = 0; k < NH_MAX_SEG / 16; k++) {
+    for (int k = 0; k < KE; k++) {
       const int64_t s = sl + 16 * k;
-      if (live && s < nseg) B = fminf(B, pm[s * nq + qi].x);
+      const bool in = live && s < nseg;
+      e[k] = in ? pm[s * nq + qi] : float4{INFINITY, INFINITY, INFINITY, 0.f};
+      hid[k] = in ? pid[s * nq + qi] : int2{-1, -1};
+      B = fminf(B, e[k].x);
     }
 #pragma unroll
     for (int off = 8; off > 0; off >>= 1) B = fminf(B, __shfl_xor(B, off, 16));
@@ -1062,70 +1069,78 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
         }
       }
     }
-    // the half-chunks to re-check and the segments to scan go round the
-    // group: a half-chunk's 16 rows one per lane, a segment's rows strided
-    // over the 16 lanes (a single lane walking them was the search's
-    // critical path)
+    // the lane-units to re-check (slot 2k + i: entry k's i-th unit) and the
+    // segments to scan, as group masks; the units go round the group two at a
+    // time, each lane loading two rows of each (four rows in flight)
     const bool part = live && !(qbad || tree_bad || !(B < INFINITY));
     const int gbit = (threadIdx.x & (WAVE - 1)) & ~15;
-    for (int64_t s0 = 0; s0 < nseg; s0 += 16) {
-      const int64_t s = s0 + sl;
-      bool chk1 = false, chk2 = false, scan = false;
-      int2 hid = {-1, -1};
-      if (part && s < nseg) {
-        const float4 e = pm[s * nq + qi];  // L2-warm since the first pass
-        scan = e.z <= T;  // a third half-chunk within T: the segment in full
-        if (!scan && e.x <= T) {
-          hid = pid[s * nq + qi];
-          chk1 = hid.x >= 0;
-          chk2 = e.y <= T && hid.y >= 0;
-        }
-      }
-      uint32_t cmask = (uint32_t)(__ballot(chk1) >> gbit) & 0xFFFFu;
-      uint32_t cmask2 = (uint32_t)(__ballot(chk2) >> gbit) & 0xFFFFu;
-      uint32_t smask = (uint32_t)(__ballot(scan) >> gbit) & 0xFFFFu;
-      nrc += sl == 0 ? __popc(cmask) + __popc(cmask2) : 0;
-      nsc += sl == 0 ? __popc(smask) : 0;
-      while (__ballot((cmask | cmask2) != 0u)) {
-        if (cmask | cmask2) {
-          int h;
-          if (cmask) {
-            const int src = __ffs(cmask) - 1;
-            cmask &= cmask - 1u;
-            h = __shfl(hid.x, src, 16);
-          } else {
-            const int src = __ffs(cmask2) - 1;
-            cmask2 &= cmask2 - 1u;
-            h = __shfl(hid.y, src, 16);
-          }
-          // the lane-unit's 32 rows, two per lane
+    uint32_t cm[2 * KE], smask[KE];
 #pragma unroll
-          for (int b = 0; b < 2; b++) {
-            const int64_t j =
-                (int64_t)(h >> 1) * 64 + 32 * b + 4 * (h & 1) + (sl & 3) + 8 * (sl >> 2);
-            if (j < nv) {
-              const double d = nn_dist64(qq, v + 8 * j);
-              if (d < best || (d == best && j < bi)) {
-                best = d;
-                bi = (int)j;
-              }
-            }
-          }
+    for (int k = 0; k < KE; k++) {
+      const bool scan = part && e[k].z <= T;  // a third unit within T: the segment in full
+      const bool c1 = part && !scan && e[k].x <= T && hid[k].x >= 0;
+      const bool c2 = c1 && e[k].y <= T && hid[k].y >= 0;
+      cm[2 * k] = (uint32_t)(__ballot(c1) >> gbit) & 0xFFFFu;
+      cm[2 * k + 1] = (uint32_t)(__ballot(c2) >> gbit) & 0xFFFFu;
+      smask[k] = (uint32_t)(__ballot(scan) >> gbit) & 0xFFFFu;
+      nrc += sl == 0 ? __popc(cm[2 * k]) + __popc(cm[2 * k + 1]) : 0;
+      nsc += sl == 0 ? __popc(smask[k]) : 0;
+    }
+    // next pending unit of the group (-1: none), popped from the masks
+    auto pop = [&]() {
+      int h = -1;
+#pragma unroll
+      for (int x = 0; x < 2 * KE; x++) {
+        if (h < 0 && cm[x]) {
+          const int src = __ffs(cm[x]) - 1;
+          cm[x] &= cm[x] - 1u;
+          const int val = (x & 1) ? hid[x >> 1].y : hid[x >> 1].x;
+          h = __shfl(val, src, 16);
         }
       }
+      return h;
+    };
+    auto pending = [&]() {
+      uint32_t any = 0;
+#pragma unroll
+      for (int x = 0; x < 2 * KE; x++) any |= cm[x];
+      return any != 0u;
+    };
+    while (__ballot(pending())) {
+      const int ha = pop(), hb = pop();
+      int64_t j[4];
+      double d[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int h = r < 2 ? ha : hb;
+        j[r] = h < 0 ? nv
+                     : (int64_t)(h >> 1) * 64 + 32 * (r & 1) + 4 * (h & 1) + (sl & 3) + 8 * (sl >> 2);
+        d[r] = j[r] < nv ? nn_dist64(qq, v + 8 * j[r]) : INFINITY;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        if (d[r] < best || (d[r] == best && j[r] < bi)) {
+          best = d[r];
+          bi = (int)j[r];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < KE; k++) {
+      if (16 * k >= nseg) break;  // wave-uniform
+      const int64_t s0 = 16 * k;
       // segment scans, the whole wave on one (group, segment) at a time: the
       // planner's clustered trees ask for a few per launch, and one group
       // walking ~1k rows alone was the launch's tail
       for (;;) {
-        const unsigned long long pend = __ballot(smask != 0u);
+        const unsigned long long pend = __ballot(smask[k] != 0u);
         if (!pend) break;
         const int src = __ffsll((long long)pend) - 1;  // first lane of the owning group
-        const uint32_t sm = (uint32_t)__shfl((int)smask, src);
+        const uint32_t sm = (uint32_t)__shfl((int)smask[k], src);
         const bool owner = gbit == (src & ~15);
-        if (owner) smask &= smask - 1u;
+        if (owner) smask[k] &= smask[k] - 1u;
         double oq[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) oq[k] = __shfl(qq[k], src);
+        for (int c = 0; c < 8; c++) oq[c] = __shfl(qq[c], src);
         const int64_t ss = s0 + (__ffs(sm) - 1);
         const int64_t j1 = min(nv, min(nch, (ss + 1) * cps) * 32);
         double wb = INFINITY;
