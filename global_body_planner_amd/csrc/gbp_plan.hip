@@ -807,22 +807,26 @@ __device__ __forceinline__ float nh_min16(const nhacc &a) {
   return nh_min2(fminf(fminf(x0, x1), x2), fminf(fminf(x3, x4), a[15]));
 }
 
-// a lane's two smallest unit minima (m1 <= m2, units i1, i2) and a lower
-// bound m3 on every other unit's minimum; branch-free (2 v_cmp, 2 v_med3,
-// 4 v_cndmask)
+// a lane's three smallest unit minima (m1 <= m2 <= m3, units i1, i2, i3) and
+// a lower bound m4 on every other unit's minimum; branch-free (3 v_cmp,
+// 3 v_med3, 6 v_cndmask).  Planner trees are clustered: with two units a
+// third within the threshold (a segment scan) came ~25 times per half-iteration.
 struct NhTop {
-  float m1 = INFINITY, m2 = INFINITY, m3 = INFINITY;
-  int i1 = -1, i2 = -1;
+  float m1 = INFINITY, m2 = INFINITY, m3 = INFINITY, m4 = INFINITY;
+  int i1 = -1, i2 = -1, i3 = -1;
   __device__ __forceinline__ void insert(float cm, int c) {
-    const bool lt1 = cm < m1, lt2 = cm < m2;
-    const float n3 = __builtin_amdgcn_fmed3f(m2, cm, m3), n2 = __builtin_amdgcn_fmed3f(m1, cm, m2);
+    const bool lt1 = cm < m1, lt2 = cm < m2, lt3 = cm < m3;
+    const float n4 = __builtin_amdgcn_fmed3f(m3, cm, m4), n3 = __builtin_amdgcn_fmed3f(m2, cm, m3);
+    const float n2 = __builtin_amdgcn_fmed3f(m1, cm, m2), n1 = lt1 ? cm : m1;
     const int j1 = lt1 ? c : i1, j2a = lt1 ? i1 : c, j2 = lt2 ? j2a : i2;
-    const float n1 = lt1 ? cm : m1;
+    const int j3a = lt2 ? i2 : c, j3 = lt3 ? j3a : i3;
     m1 = n1;
     m2 = n2;
     m3 = n3;
+    m4 = n4;
     i1 = j1;
     i2 = j2;
+    i3 = j3;
   }
 };
 
@@ -916,7 +920,7 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
                                                    const _Float16 *__restrict__ vh,
                                                    const float *__restrict__ hm,
                                                    const int32_t *__restrict__ nv_dev, int64_t bmax,
-                                                   float4 *__restrict__ pm, int2 *__restrict__ pid,
+                                                   float4 *__restrict__ pm, int4 *__restrict__ pid,
                                                    uint64_t seq, NhPrep<ZT> pp) {
   if (gated(st, seq)) {
     if (PREP && blockIdx.x == pp.first_block && threadIdx.x == 0) st->n_validate = 0;
@@ -971,35 +975,38 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
         }
       }
     }
-    if (tree_bad) {  // every segment scanned in fp64 by the reduce
+    if (!tree_bad) nh_sweep<NT>(vh, c0, c1, (int)nv, b1, b2, t);
+    // the two lanes of a query (rows 4h + ...): merge to one entry, the three
+    // smallest lane-units (id = 2 unit + h) and a lower bound on the rest:
+    // the other lane's three inserted into this lane's list
+    if (tree_bad) {
 #pragma unroll
-      for (int u = 0; u < NT; u++) t[u].m1 = t[u].m2 = t[u].m3 = -INFINITY;
-    } else {
-      nh_sweep<NT>(vh, c0, c1, (int)nv, b1, b2, t);
+      for (int u = 0; u < NT; u++) {
+        const int64_t qi = (int64_t)qg * (32 * NT) + 32 * u + r;
+        if (h == 0 && qi < nq) {
+          pm[(int64_t)sg * nq + qi] = float4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+          pid[(int64_t)sg * nq + qi] = int4{-1, -1, -1, -1};
+        }
+      }
+      continue;
     }
-    // the two lanes of a query (rows 4h + ...): merge to one entry, the two
-    // smallest lane-units (id = 2 unit + h) and a lower bound on the rest
 #pragma unroll
     for (int u = 0; u < NT; u++) {
-      const float a1 = t[u].m1, a2 = t[u].m2, a3 = t[u].m3;
-      const int ia1 = t[u].i1 >= 0 ? 2 * t[u].i1 + h : -1, ia2 = t[u].i2 >= 0 ? 2 * t[u].i2 + h : -1;
-      const float b1v = __shfl_xor(a1, 32), b2v = __shfl_xor(a2, 32), b3v = __shfl_xor(a3, 32);
-      const int ib1 = __shfl_xor(ia1, 32), ib2 = __shfl_xor(ia2, 32);
-      const bool fa = a1 <= b1v;
-      // first: the smaller head; second: the smaller of the other head and the
-      // first list's second; bound: min(the larger of those two, both lists'
-      // thirds and the other list's second)
-      const float e1 = fa ? a1 : b1v, x2 = fa ? a2 : b2v, y1 = fa ? b1v : a1;
-      const int ie1 = fa ? ia1 : ib1, ix2 = fa ? ia2 : ib2, iy1 = fa ? ib1 : ia1;
-      const float y2 = fa ? b2v : a2;
-      const bool sx = x2 <= y1;
-      const float e2 = sx ? x2 : y1;
-      const int ie2 = sx ? ix2 : iy1;
-      const float e3 = fminf(fminf(fmaxf(x2, y1), y2), fminf(a3, b3v));
+      NhTop e = t[u];
+      e.i1 = e.i1 >= 0 ? 2 * e.i1 + h : -1;
+      e.i2 = e.i2 >= 0 ? 2 * e.i2 + h : -1;
+      e.i3 = e.i3 >= 0 ? 2 * e.i3 + h : -1;
+      const float o1 = __shfl_xor(e.m1, 32), o2 = __shfl_xor(e.m2, 32), o3 = __shfl_xor(e.m3, 32);
+      const float o4 = __shfl_xor(e.m4, 32);
+      const int p1 = __shfl_xor(e.i1, 32), p2 = __shfl_xor(e.i2, 32), p3 = __shfl_xor(e.i3, 32);
+      e.insert(o1, p1);
+      e.insert(o2, p2);
+      e.insert(o3, p3);
+      e.m4 = fminf(e.m4, o4);
       const int64_t qi = (int64_t)qg * (32 * NT) + 32 * u + r;
       if (h == 0 && qi < nq) {
-        pm[(int64_t)sg * nq + qi] = float4{e1, e2, e3, 0.f};
-        pid[(int64_t)sg * nq + qi] = int2{ie1, ie2};
+        pm[(int64_t)sg * nq + qi] = float4{e.m1, e.m2, e.m3, e.m4};
+        pid[(int64_t)sg * nq + qi] = int4{e.i1, e.i2, e.i3, 0};
       }
     }
   }
@@ -1017,7 +1024,7 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
                                                        const float *__restrict__ hm,
                                                        const int32_t *__restrict__ nv_dev,
                                                        int64_t bmax, const float4 *__restrict__ pm,
-                                                       const int2 *__restrict__ pid,
+                                                       const int4 *__restrict__ pid,
                                                        int32_t *__restrict__ out, uint64_t seq,
                                                        int stats, double *__restrict__ cs) {
   if (gated(st, seq)) return;
@@ -1040,19 +1047,12 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
       qbad = qbad || !(fabs(gk) < NH_LIM);
       g2 += gk * gk;
     }
-    // the group's entries, lane sl holding segments sl, sl + 16, ... (<= 4),
-    // values and unit ids read together
-    constexpr int KE = NH_MAX_SEG / 16;
-    float4 e[KE];
-    int2 hid[KE];
+    // the group's entries, lane sl reading segments sl, sl + 16, ... (<= 4)
     float B = INFINITY;
 #pragma unroll
-    for (int k = 0; k < KE; k++) {
+    for (int k = 0; k < NH_MAX_SEG / 16; k++) {
       const int64_t s = sl + 16 * k;
-      const bool in = live && s < nseg;
-      e[k] = in ? pm[s * nq + qi] : float4{INFINITY, INFINITY, INFINITY, 0.f};
-      hid[k] = in ? pid[s * nq + qi] : int2{-1, -1};
-      B = fminf(B, e[k].x);
+      if (live && s < nseg) B = fminf(B, pm[s * nq + qi].x);
     }
 #pragma unroll
     for (int off = 8; off > 0; off >>= 1) B = fminf(B, __shfl_xor(B, off, 16));
@@ -1069,78 +1069,76 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
         }
       }
     }
-    // the lane-units to re-check (slot 2k + i: entry k's i-th unit) and the
-    // segments to scan, as group masks; the units go round the group two at a
-    // time, each lane loading two rows of each (four rows in flight)
+    // the half-chunks to re-check and the segments to scan go round the
+    // group: a half-chunk's 16 rows one per lane, a segment's rows strided
+    // over the 16 lanes (a single lane walking them was the search's
+    // critical path)
     const bool part = live && !(qbad || tree_bad || !(B < INFINITY));
     const int gbit = (threadIdx.x & (WAVE - 1)) & ~15;
-    uint32_t cm[2 * KE], smask[KE];
-#pragma unroll
-    for (int k = 0; k < KE; k++) {
-      const bool scan = part && e[k].z <= T;  // a third unit within T: the segment in full
-      const bool c1 = part && !scan && e[k].x <= T && hid[k].x >= 0;
-      const bool c2 = c1 && e[k].y <= T && hid[k].y >= 0;
-      cm[2 * k] = (uint32_t)(__ballot(c1) >> gbit) & 0xFFFFu;
-      cm[2 * k + 1] = (uint32_t)(__ballot(c2) >> gbit) & 0xFFFFu;
-      smask[k] = (uint32_t)(__ballot(scan) >> gbit) & 0xFFFFu;
-      nrc += sl == 0 ? __popc(cm[2 * k]) + __popc(cm[2 * k + 1]) : 0;
-      nsc += sl == 0 ? __popc(smask[k]) : 0;
-    }
-    // next pending unit of the group (-1: none), popped from the masks
-    auto pop = [&]() {
-      int h = -1;
-#pragma unroll
-      for (int x = 0; x < 2 * KE; x++) {
-        if (h < 0 && cm[x]) {
-          const int src = __ffs(cm[x]) - 1;
-          cm[x] &= cm[x] - 1u;
-          const int val = (x & 1) ? hid[x >> 1].y : hid[x >> 1].x;
-          h = __shfl(val, src, 16);
+    for (int64_t s0 = 0; s0 < nseg; s0 += 16) {
+      const int64_t s = s0 + sl;
+      bool chk1 = false, chk2 = false, chk3 = false, scan = false;
+      int4 hid = {-1, -1, -1, 0};
+      if (part && s < nseg) {
+        const float4 e = pm[s * nq + qi];  // L2-warm since the first pass
+        scan = e.w <= T;  // a fourth unit within T: the segment in full
+        if (!scan && e.x <= T) {
+          hid = pid[s * nq + qi];
+          chk1 = hid.x >= 0;
+          chk2 = e.y <= T && hid.y >= 0;
+          chk3 = e.z <= T && hid.z >= 0;
         }
       }
-      return h;
-    };
-    auto pending = [&]() {
-      uint32_t any = 0;
+      uint32_t cmask = (uint32_t)(__ballot(chk1) >> gbit) & 0xFFFFu;
+      uint32_t cmask2 = (uint32_t)(__ballot(chk2) >> gbit) & 0xFFFFu;
+      uint32_t cmask3 = (uint32_t)(__ballot(chk3) >> gbit) & 0xFFFFu;
+      uint32_t smask = (uint32_t)(__ballot(scan) >> gbit) & 0xFFFFu;
+      nrc += sl == 0 ? __popc(cmask) + __popc(cmask2) + __popc(cmask3) : 0;
+      nsc += sl == 0 ? __popc(smask) : 0;
+      while (__ballot((cmask | cmask2 | cmask3) != 0u)) {
+        if (cmask | cmask2 | cmask3) {
+          int h;
+          if (cmask) {
+            const int src = __ffs(cmask) - 1;
+            cmask &= cmask - 1u;
+            h = __shfl(hid.x, src, 16);
+          } else if (cmask2) {
+            const int src = __ffs(cmask2) - 1;
+            cmask2 &= cmask2 - 1u;
+            h = __shfl(hid.y, src, 16);
+          } else {
+            const int src = __ffs(cmask3) - 1;
+            cmask3 &= cmask3 - 1u;
+            h = __shfl(hid.z, src, 16);
+          }
+          // the lane-unit's 32 rows, two per lane
 #pragma unroll
-      for (int x = 0; x < 2 * KE; x++) any |= cm[x];
-      return any != 0u;
-    };
-    while (__ballot(pending())) {
-      const int ha = pop(), hb = pop();
-      int64_t j[4];
-      double d[4];
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int h = r < 2 ? ha : hb;
-        j[r] = h < 0 ? nv
-                     : (int64_t)(h >> 1) * 64 + 32 * (r & 1) + 4 * (h & 1) + (sl & 3) + 8 * (sl >> 2);
-        d[r] = j[r] < nv ? nn_dist64(qq, v + 8 * j[r]) : INFINITY;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; r++)
-        if (d[r] < best || (d[r] == best && j[r] < bi)) {
-          best = d[r];
-          bi = (int)j[r];
+          for (int b = 0; b < 2; b++) {
+            const int64_t j =
+                (int64_t)(h >> 1) * 64 + 32 * b + 4 * (h & 1) + (sl & 3) + 8 * (sl >> 2);
+            if (j < nv) {
+              const double d = nn_dist64(qq, v + 8 * j);
+              if (d < best || (d == best && j < bi)) {
+                best = d;
+                bi = (int)j;
+              }
+            }
+          }
         }
-    }
-#pragma unroll
-    for (int k = 0; k < KE; k++) {
-      if (16 * k >= nseg) break;  // wave-uniform
-      const int64_t s0 = 16 * k;
+      }
       // segment scans, the whole wave on one (group, segment) at a time: the
       // planner's clustered trees ask for a few per launch, and one group
       // walking ~1k rows alone was the launch's tail
       for (;;) {
-        const unsigned long long pend = __ballot(smask[k] != 0u);
+        const unsigned long long pend = __ballot(smask != 0u);
         if (!pend) break;
         const int src = __ffsll((long long)pend) - 1;  // first lane of the owning group
-        const uint32_t sm = (uint32_t)__shfl((int)smask[k], src);
+        const uint32_t sm = (uint32_t)__shfl((int)smask, src);
         const bool owner = gbit == (src & ~15);
-        if (owner) smask[k] &= smask[k] - 1u;
+        if (owner) smask &= smask - 1u;
         double oq[8];
 #pragma unroll
-        for (int c = 0; c < 8; c++) oq[c] = __shfl(qq[c], src);
+        for (int k = 0; k < 8; k++) oq[k] = __shfl(qq[k], src);
         const int64_t ss = s0 + (__ffs(sm) - 1);
         const int64_t j1 = min(nv, min(nch, (ss + 1) * cps) * 32);
         double wb = INFINITY;
@@ -2157,16 +2155,16 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
       const int gp = (int)grid_for(GBP_NUM_GEN_STATES * w->bmax, NH_TB, num_cus * 4);
       hipLaunchKernelGGL((k_nn_mfma<NH_NT, ZT, true>), dim3(gm + gp), dim3(NH_TB), 0, s, w->st,
                          nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
-                         (float4 *)w->nn_d, (int2 *)w->nn_i, ++w->seq, pp);
+                         (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, pp);
       if (prepped) *prepped = true;
     } else {
       hipLaunchKernelGGL((k_nn_mfma<NH_NT, float, false>), dim3(gm), dim3(NH_TB), 0, s, w->st,
                          nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
-                         (float4 *)w->nn_d, (int2 *)w->nn_i, ++w->seq, NhPrep<float>{});
+                         (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, NhPrep<float>{});
     }
     hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(16 * w->bmax, NH_RTB, num_cus * 8)), dim3(NH_RTB),
                        0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, tr->count, w->bmax,
-                       (const float4 *)w->nn_d, (const int2 *)w->nn_i, out, ++w->seq, w->nn_stats,
+                       (const float4 *)w->nn_d, (const int4 *)w->nn_i, out, ++w->seq, w->nn_stats,
                        prep ? cs : nullptr);
     return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   }
@@ -2581,7 +2579,7 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   const int64_t b = max_batch, m = GBP_NUM_GEN_STATES * max_batch;
   const size_t bytes = sizeof(gbp_plan_status) + 8 * w->ntiles + 64 * b + 4 * b + 64 * b + 4 * b +
                        m * (64 + 80 + 64 + 4 + 4) + b * (4 + 4 + 64 + 80 + 4 + 4) +
-                       b * (4 + 4 + 64 + 80 + 4) + NN_MAX_CHUNKS * b * (16 + 8) + 64 * b + 256 +
+                       b * (4 + 4 + 64 + 80 + 4) + NN_MAX_CHUNKS * b * (16 + 16) + 64 * b + 256 +
                        4 * NN_QCELLS + 4 * NN_QCELLS * b + 4 * b + 64 * 256;
   if (hipMalloc(&w->block, bytes) != hipSuccess) {
     delete w;
@@ -2612,7 +2610,7 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->kan = carve<double>(p, 10 * b);
   w->kf = carve<uint32_t>(p, b);
   w->nn_d = carve<double>(p, 2 * NN_MAX_CHUNKS * b);   // k_nn_mfma: float4 per slot
-  w->nn_i = carve<int32_t>(p, 2 * NN_MAX_CHUNKS * b);  // k_nn_mfma: int2 per slot
+  w->nn_i = carve<int32_t>(p, 4 * NN_MAX_CHUNKS * b);  // k_nn_mfma: int4 per slot
   w->bcnt = carve<int32_t>(p, NN_QCELLS);
   w->bq = carve<int32_t>(p, (size_t)NN_QCELLS * b);
   w->qpt = carve<float>(p, b);
