@@ -1055,6 +1055,9 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
     case GBP_OPT_NN_STATS:
       t->opt_nn_stats = value ? 1 : 0;
       return GBP_OK;
+    case GBP_OPT_PLAN_OVERLAP:
+      t->opt_plan_overlap = value ? 1 : 0;
+      return GBP_OK;
     case GBP_OPT_FRAGILE_EPS:  // in 1e-15 units; never below the default margin
       if (value < 1000 || value > 1000000000000000LL) return GBP_E_INVALID_ARG;
       t->fragile_eps = (double)value * 1e-15;
@@ -1079,6 +1082,7 @@ int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value) {
     case GBP_OPT_NN_INDEX: *value = t->opt_nn_index; return GBP_OK;
     case GBP_OPT_NN_FILTER: *value = t->opt_nn_filter; return GBP_OK;
     case GBP_OPT_NN_STATS: *value = t->opt_nn_stats; return GBP_OK;
+    case GBP_OPT_PLAN_OVERLAP: *value = t->opt_plan_overlap; return GBP_OK;
     case GBP_OPT_FRAGILE_EPS: *value = (int64_t)std::llround(t->fragile_eps * 1e15); return GBP_OK;
     case GBP_OPT_COORD_MODE:  // what the validate kernel of the current options uses
       *value = validate_coord_mode(t, t->opt_kernel == GBP_KERNEL_DIRECT);

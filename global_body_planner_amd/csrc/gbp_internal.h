@@ -41,7 +41,8 @@ struct gbp_terrain {
   double fragile_eps = gbp::FRAGILE_EPS;  // GBP_OPT_FRAGILE_EPS (>= the default)
   int64_t opt_xcd_map = 0;          // persistent kernel: slices numbered XCD-major
   int opt_nn_filter = 0;
-  int opt_nn_stats = 0;             // 1: the matrix-core NN search counts its fp64 re-checks            // planner NN: 0 matrix-core fp16-split filter, 1 packed fp32 filter
+  int opt_nn_stats = 0;
+  int opt_plan_overlap = 0;         // gbp_plan_halves_dev: next half's draws on a second stream             // 1: the matrix-core NN search counts its fp64 re-checks            // planner NN: 0 matrix-core fp16-split filter, 1 packed fp32 filter
   int64_t opt_nn_index = 0;         // planner: trees this large search through their index (0: off)
   gbp_sampling sampling{};          // direction-biased sampling (gbp_terrain_set_sampling), off
   int affine = 0;                   // host-verified affine coordinates (both axes)

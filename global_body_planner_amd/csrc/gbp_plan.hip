@@ -53,7 +53,7 @@
 #include "gbp_lane.h"
 
 using namespace gbp;
-static_assert(sizeof(gbp_plan_status) == 136, "engine.PlanStatus mirrors this layout");
+static_assert(sizeof(gbp_plan_status) == 160, "engine.PlanStatus mirrors this layout");
 
 // ============================================================================
 // handles
@@ -97,6 +97,8 @@ struct gbp_plan_ws {
   uint64_t seq = 0;            // launch sequence number of the planner kernels (gated())
   int nn_mode = 0;             // GBP_OPT_NN_FILTER of the last terrain that enqueued (0: k_nn_mfma)
   int nn_stats = 0;            // GBP_OPT_NN_STATS: k_nn_hreduce counts its re-checks in the status
+  hipStream_t aux = nullptr;   // gbp_plan_halves_dev: the next half's draws
+  hipEvent_t ev_a = nullptr, ev_b = nullptr;  // stage 3 of half h done / draws of h + 1 done
   int64_t ntiles = 0;
   // stage 0-1
   double *cand = nullptr;      // [bmax][8] drawn states
@@ -251,7 +253,9 @@ __global__ __launch_bounds__(TB) void k_targets(TerrainView<ZT> T, gbp_plan_stat
   const double *t_last = tv + 8 * (int64_t)(*tcount - 1);
   const double *s_from = direction == GBP_FORWARD ? t_last : ov;
   const double *s_to = direction == GBP_FORWARD ? ov : t_last;
-  bool frag = false;
+  // FRAGILE draws are flagged here and halt the sequence in the compaction
+  // (k_compact_targets, in stream order), so this kernel may run beside the
+  // previous half's connect stages (gbp_plan_halves_dev)
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     double q[8];
@@ -260,12 +264,6 @@ __global__ __launch_bounds__(TB) void k_targets(TerrainView<ZT> T, gbp_plan_stat
     const bool v = is_valid_state(T, q, GBP_STANCE, acc);   // rrt_connect.cpp:254
     copy8(cand + 8 * i, q);
     cflag[i] = acc.flags | (v ? GBP_F_VALID : 0u);
-    frag = frag || (acc.flags & GBP_F_FRAGILE);
-  }
-  if (__ballot(frag) && (threadIdx.x & (WAVE - 1)) == 0) {
-    atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_TARGETS);
-    st->halt_half = half;
-    raise_gate(st, seq);
   }
 }
 
@@ -1442,10 +1440,16 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
                                                         double *__restrict__ targets,
                                                         _Float16 *__restrict__ tqh,
                                                         unsigned long long *tiles, uint32_t epoch,
-                                                        uint64_t seq) {
+                                                        int32_t half, uint64_t seq) {
   if (gated(st, seq)) return;
   const int64_t i = blockIdx.x * (int64_t)CB + threadIdx.x;
-  const bool keep = i < n && (cflag[i] & GBP_F_VALID);
+  const uint32_t f = i < n ? cflag[i] : 0u;
+  const bool keep = f & GBP_F_VALID;
+  if (__ballot(f & GBP_F_FRAGILE) && (threadIdx.x & (WAVE - 1)) == 0) {  // the targets stage halts
+    atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_TARGETS);
+    st->halt_half = half;
+    raise_gate(st, seq);
+  }
   const uint32_t r = ordered_rank(keep, tiles, epoch, &st->n_targets, st);
   if (keep) {
     copy8(targets + 8 * (size_t)r, cand + 8 * i);
@@ -1453,10 +1457,18 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
     // the extend stream of this half: RRTClass::extend_counter_ advances by
-    // the number of extends (csrc/host/gbp_planner.cpp extendBatch)
-    st->ext_base = st->ext_counter;
-    st->ext_counter += st->n_targets;
-    st->stat_targets += st->n_targets;
+    // the number of extends (csrc/host/gbp_planner.cpp extendBatch); a re-run
+    // for the same half (resumed after a FRAGILE halt) starts from the same
+    // counters
+    const bool again = st->ext_half == half;
+    const int64_t base = again ? st->ext_prev : st->ext_counter;
+    const int64_t tg = again ? st->stat_targets_prev : st->stat_targets;
+    st->ext_half = half;
+    st->ext_prev = base;
+    st->stat_targets_prev = tg;
+    st->ext_base = base;
+    st->ext_counter = base + st->n_targets;
+    st->stat_targets = tg + st->n_targets;
   }
 }
 
@@ -2052,6 +2064,7 @@ __global__ void k_plan_reset(gbp_plan_status *st, int64_t ext_counter) {
   z.meet = ~0ull;
   z.gate_seq = ~0ull;
   z.halt_half = -1;
+  z.ext_half = -1;
   z.meet_half = -1;
   z.ext_counter = ext_counter;
   *st = z;
@@ -2196,7 +2209,8 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
                        t->sampling, T->v, T->count, O ? O->v : T->v, direction);
   if (first_stage <= 1 && last_stage >= 1)
     hipLaunchKernelGGL(k_compact_targets, dim3(tiles_for(batch)), dim3(CB), 0, s, st, batch,
-                       w->cand, w->cflag, w->targets, w->tqh, w->tiles, next_epoch(w), ++w->seq);
+                       w->cand, w->cflag, w->targets, w->tqh, w->tiles, next_epoch(w), half,
+                       ++w->seq);
   if (first_stage <= 2 && last_stage >= 2) {
     // the targets' nearest vertices through T's index when GBP_OPT_NN_INDEX
     // asks for it and the index holds at least that many vertices
@@ -2621,7 +2635,13 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
     return GBP_E_HIP;
   }
   hipLaunchKernelGGL(k_plan_reset, dim3(1), dim3(1), 0, nullptr, w->st, (int64_t)0);
-  if (hipDeviceSynchronize() != hipSuccess) {
+  if (hipStreamCreateWithFlags(&w->aux, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&w->ev_a, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&w->ev_b, hipEventDisableTiming) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    if (w->ev_a) (void)hipEventDestroy(w->ev_a);
+    if (w->ev_b) (void)hipEventDestroy(w->ev_b);
+    if (w->aux) (void)hipStreamDestroy(w->aux);
     (void)hipFree(w->block);
     delete w;
     return GBP_E_HIP;
@@ -2635,6 +2655,9 @@ int gbp_plan_ws_destroy(gbp_plan_ws *w) {
   Guard g(w->device);
   (void)hipDeviceSynchronize();
   if (w->block) (void)hipFree(w->block);
+  if (w->ev_a) (void)hipEventDestroy(w->ev_a);
+  if (w->ev_b) (void)hipEventDestroy(w->ev_b);
+  if (w->aux) (void)hipStreamDestroy(w->aux);
   delete w;
   return GBP_OK;
 }
@@ -2671,6 +2694,61 @@ int gbp_plan_half_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, 
                                  target_index_base, adaptive, first_stage, 5, s);
   return enqueue_stages<double>(t, w, T, O, half, direction, batch, seed, target_stream,
                                 target_index_base, adaptive, first_stage, 5, s);
+}
+
+int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *Tb,
+                        int32_t first_half, int32_t n_halves, int64_t batch, uint64_t seed,
+                        uint64_t stream_a, uint64_t stream_b, int adaptive, int first_stage,
+                        gbp_stream stream) {
+  if (!t || !w || !tree_ok(Ta) || !tree_ok(Tb)) return GBP_E_BAD_HANDLE;
+  if (batch < 1 || batch > w->bmax || first_stage < 0 || first_stage > 5 || n_halves < 0 ||
+      first_half < 0 || Ta == Tb)
+    return GBP_E_INVALID_ARG;
+  Guard g(t->device);
+  hipStream_t s = (hipStream_t)stream;
+  const bool overlap = t->opt_plan_overlap && !t->sampling.state_flag && n_halves > 1;
+  bool drawn = false;  // this half's stage 0 already ran on the second stream
+  for (int32_t i = 0; i < n_halves; i++) {
+    const int32_t h = first_half + i;
+    const int k = h & 1;
+    gbp_tree *T = k ? Tb : Ta, *O = k ? Ta : Tb;
+    const int dir = k ? GBP_REVERSE : GBP_FORWARD;
+    const uint64_t ts = k ? stream_b : stream_a;
+    const int64_t tb = (int64_t)(h >> 1) * batch;
+    int fs = i == 0 ? first_stage : 0;
+    if (drawn) {
+      HIPCHK_P(hipStreamWaitEvent(s, w->ev_b, 0));
+      fs = std::max(fs, 1);
+    }
+    auto stages = [&](gbp_tree *TT, gbp_tree *OO, int32_t hh, int d, uint64_t tst, int64_t tbase,
+                      int first, int last, hipStream_t st) {
+      return t->storage == GBP_STORAGE_F32
+                 ? enqueue_stages<float>(t, w, TT, OO, hh, d, batch, seed, tst, tbase, adaptive, first,
+                                         last, st)
+                 : enqueue_stages<double>(t, w, TT, OO, hh, d, batch, seed, tst, tbase, adaptive,
+                                          first, last, st);
+    };
+    int rc = stages(T, O, h, dir, ts, tb, fs, 1, s);
+    if (rc) return rc;
+    drawn = false;
+    if (overlap && i + 1 < n_halves) {
+      // half h + 1's draws once this half's compaction has read its own
+      // (the draw buffers are shared), beside this half's search and
+      // validation (VALU draws next to matrix-core and memory-latency work)
+      const int32_t h1 = h + 1;
+      const int k1 = h1 & 1;
+      HIPCHK_P(hipEventRecord(w->ev_a, s));
+      HIPCHK_P(hipStreamWaitEvent(w->aux, w->ev_a, 0));
+      rc = stages(k1 ? Tb : Ta, k1 ? Ta : Tb, h1, k1 ? GBP_REVERSE : GBP_FORWARD,
+                  k1 ? stream_b : stream_a, (int64_t)(h1 >> 1) * batch, 0, 0, w->aux);
+      if (rc) return rc;
+      HIPCHK_P(hipEventRecord(w->ev_b, w->aux));
+      drawn = true;
+    }
+    rc = stages(T, O, h, dir, ts, tb, std::max(fs, 2), 5, s);
+    if (rc) return rc;
+  }
+  return GBP_OK;
 }
 
 int gbp_extend_tree_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, int64_t n,

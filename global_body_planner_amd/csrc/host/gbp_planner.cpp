@@ -1531,13 +1531,6 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
   double bounds[4];
   chk(gbp_terrain_info(h, nullptr, nullptr, nullptr, bounds, nullptr), "terrain info");
   // half h extends tree h % 2 toward its draws [(h / 2) B, (h / 2 + 1) B)
-  auto enqueue = [&](int32_t hh, int first_stage) {
-    const int k = hh & 1;
-    chk(gbp_plan_half_dev(h, D.ws, D.tree[k], D.tree[k ^ 1], hh, k == 0 ? FORWARD : REVERSE, batch,
-                          seed_, tstream[k], (int64_t)(hh >> 1) * batch, adaptive, first_stage,
-                          D.stream),
-        "plan half");
-  };
   // groups grow geometrically: a short search is not charged a long group's
   // tail of gated half-iterations, a long one amortises the status read
   const int g_max = (int)std::max<int64_t>(2, std::min<int64_t>(64, (1 << 21) / batch)) & ~1;
@@ -1553,7 +1546,11 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
                              D.stream),
             "tree reserve");
     }
-    for (int g = 0; g < group; g++) enqueue(half + g, 0);
+    // the group's halves, each half's draws beside the previous half's connect
+    // stages (gbp_plan_halves_dev, GBP_OPT_PLAN_OVERLAP)
+    chk(gbp_plan_halves_dev(h, D.ws, D.tree[0], D.tree[1], half, group, batch, seed_, tstream[0],
+                            tstream[1], adaptive, 0, D.stream),
+        "plan halves");
     chk(gbp_plan_status_read(D.ws, &ps, D.stream), "plan status");
     st.status_reads++;
     while (ps.halt) {  // FRAGILE: re-decide on the host, resume where the sequence stopped
@@ -1566,8 +1563,9 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
                                 batch, adaptive, &resume, &nres, D.stream),
           "plan resolve");
       if (resume < 0) throw EngineError(GBP_E_INVALID_ARG, "plan resolve: nothing halted");
-      enqueue(h0, resume);
-      for (int32_t hh = h0 + 1; hh < half + group; hh++) enqueue(hh, 0);
+      chk(gbp_plan_halves_dev(h, D.ws, D.tree[0], D.tree[1], h0, half + group - h0, batch, seed_,
+                              tstream[0], tstream[1], adaptive, resume, D.stream),
+          "plan halves");
       chk(gbp_plan_status_read(D.ws, &ps, D.stream), "plan status");
       st.status_reads++;
     }
@@ -2069,6 +2067,8 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
           "nn index");
     chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_NN_FILTER, p->nn_filter), "nn filter");
     chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_NN_STATS, p->nn_stats), "nn stats");
+    if (p->no_overlap)
+      chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_PLAN_OVERLAP, 0), "plan overlap");
     RRTStarConnectClass planner;  // is-a RRTConnectClass: algorithm 0 uses the plain build
     planner.setSeed(p->seed);
     planner.set_state_direction_sampling(p->sampling.state_flag != 0, p->sampling.state_p,

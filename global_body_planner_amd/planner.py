@@ -29,7 +29,8 @@ class PlanParams(ctypes.Structure):
                 ("algorithm", ctypes.c_int), ("max_time_opt", _D),
                 ("sampling", _lib.Sampling), ("fragile_eps_fm", ctypes.c_int64),
                 ("adaptive", ctypes.c_int), ("nn_index", ctypes.c_int64),
-                ("nn_filter", ctypes.c_int), ("nn_stats", ctypes.c_int)]
+                ("nn_filter", ctypes.c_int), ("nn_stats", ctypes.c_int),
+                ("no_overlap", ctypes.c_int)]
 
 
 class PlanResult(ctypes.Structure):
@@ -101,7 +102,7 @@ def start_goal_state(height, x, y):
 def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018,
                      post_process=False, device=0, capacity=4096, algorithm=0, max_time_opt=0.0,
                      sampling=None, fragile_eps=None, adaptive=False, nn_index=0,
-                     nn_filter=0, nn_stats=False):
+                     nn_filter=0, nn_stats=False, overlap=True):
     """Plan start -> goal on terrain `data` (terrain_data.TerrainData).
 
     algorithm 0: batch-synchronous RRT-Connect, stops at the first solution;
@@ -146,6 +147,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     p.nn_index = int(nn_index)
     p.nn_filter = int(nn_filter)
     p.nn_stats = int(bool(nn_stats))
+    p.no_overlap = 0 if overlap else 1
     r = PlanResult()
     states = np.zeros((capacity, 8))
     actions = np.zeros((capacity, 10))

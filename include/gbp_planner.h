@@ -605,6 +605,7 @@ typedef struct {
                           // through their index (0 = the handle's default, off; < 0 = off)
   int nn_filter;          // GBP_OPT_NN_FILTER: 0 matrix cores (default), 1 packed fp32
   int nn_stats;           // GBP_OPT_NN_STATS: count the search's fp64 re-checks (diagnostics)
+  int no_overlap;         // 1: GBP_OPT_PLAN_OVERLAP off (0 = the handle's default)
 } gbp_plan_params;
 
 typedef struct {
