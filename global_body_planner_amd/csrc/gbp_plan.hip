@@ -705,7 +705,8 @@ constexpr int NH_NT = 4;               // query tiles (32 queries) per wave
 constexpr int NH_ITEMS = 4096;         // waves a search aims for
 constexpr int NH_MAX_SEG = 64;         // segments per query (the reduce reads them all)
 constexpr int NH_TB = 256;             // 4 independent waves per workgroup
-constexpr int NH_RTB = 256;            // reduce: 16 lanes per query
+constexpr int NH_RTB = 256;            // reduce: workgroup size
+constexpr int NH_G = 16;               // reduce: lanes per query
 
 typedef _Float16 nh8 __attribute__((ext_vector_type(8)));
 typedef float nhacc __attribute__((ext_vector_type(16)));
@@ -1030,11 +1031,11 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
   int64_t nqg, nseg, cps, nch;
   nh_geometry(nq, nv, bmax, nqg, nseg, cps, nch);
   const bool tree_bad = ((const uint32_t *)hm)[8] != 0u || nv <= 0;
-  const int sl = threadIdx.x & 15;
-  const int64_t groups = (int64_t)gridDim.x * (NH_RTB / 16);
+  const int sl = threadIdx.x & (NH_G - 1);
+  const int64_t groups = (int64_t)gridDim.x * (NH_RTB / NH_G);
   const int64_t iters = (nq + groups - 1) / groups;  // whole groups iterate together
   for (int64_t it = 0; it < iters; it++) {
-    const int64_t qi = it * groups + blockIdx.x * (int64_t)(NH_RTB / 16) + threadIdx.x / 16;
+    const int64_t qi = it * groups + blockIdx.x * (int64_t)(NH_RTB / NH_G) + threadIdx.x / NH_G;
     const bool live = qi < nq;
     double qq[8], g2 = 0.0;
     bool qbad = false;
@@ -1045,21 +1046,21 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
       qbad = qbad || !(fabs(gk) < NH_LIM);
       g2 += gk * gk;
     }
-    // the group's entries, lane sl reading segments sl, sl + 16, ... (<= 4)
+    // the group's entries, lane sl reading segments sl, sl + NH_G, ...
     float B = INFINITY;
 #pragma unroll
-    for (int k = 0; k < NH_MAX_SEG / 16; k++) {
-      const int64_t s = sl + 16 * k;
+    for (int k = 0; k < NH_MAX_SEG / NH_G; k++) {
+      const int64_t s = sl + NH_G * k;
       if (live && s < nseg) B = fminf(B, pm[s * nq + qi].x);
     }
 #pragma unroll
-    for (int off = 8; off > 0; off >>= 1) B = fminf(B, __shfl_xor(B, off, 16));
+    for (int off = NH_G / 2; off > 0; off >>= 1) B = fminf(B, __shfl_xor(B, off, NH_G));
     const float T = nh_threshold(B, nh_eps(qq, hm), g2);
     double best = INFINITY;
     int bi = 0x7FFFFFFF, nrc = 0, nsc = 0;
     if (live && (qbad || tree_bad || !(B < INFINITY))) {  // the whole tree in fp64
       nsc = sl == 0;
-      for (int64_t j = sl; j < nv; j += 16) {
+      for (int64_t j = sl; j < nv; j += NH_G) {
         const double d = nn_dist64(qq, v + 8 * j);
         if (d < best) {  // ascending per lane: the first index at its minimum
           best = d;
@@ -1072,8 +1073,9 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
     // over the 16 lanes (a single lane walking them was the search's
     // critical path)
     const bool part = live && !(qbad || tree_bad || !(B < INFINITY));
-    const int gbit = (threadIdx.x & (WAVE - 1)) & ~15;
-    for (int64_t s0 = 0; s0 < nseg; s0 += 16) {
+    const int gbit = (threadIdx.x & (WAVE - 1)) & ~(NH_G - 1);
+    constexpr uint32_t GM = NH_G == 32 ? 0xFFFFFFFFu : (1u << NH_G) - 1u;
+    for (int64_t s0 = 0; s0 < nseg; s0 += NH_G) {
       const int64_t s = s0 + sl;
       bool chk1 = false, chk2 = false, chk3 = false, scan = false;
       int4 hid = {-1, -1, -1, 0};
@@ -1087,10 +1089,10 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
           chk3 = e.z <= T && hid.z >= 0;
         }
       }
-      uint32_t cmask = (uint32_t)(__ballot(chk1) >> gbit) & 0xFFFFu;
-      uint32_t cmask2 = (uint32_t)(__ballot(chk2) >> gbit) & 0xFFFFu;
-      uint32_t cmask3 = (uint32_t)(__ballot(chk3) >> gbit) & 0xFFFFu;
-      uint32_t smask = (uint32_t)(__ballot(scan) >> gbit) & 0xFFFFu;
+      uint32_t cmask = (uint32_t)(__ballot(chk1) >> gbit) & GM;
+      uint32_t cmask2 = (uint32_t)(__ballot(chk2) >> gbit) & GM;
+      uint32_t cmask3 = (uint32_t)(__ballot(chk3) >> gbit) & GM;
+      uint32_t smask = (uint32_t)(__ballot(scan) >> gbit) & GM;
       nrc += sl == 0 ? __popc(cmask) + __popc(cmask2) + __popc(cmask3) : 0;
       nsc += sl == 0 ? __popc(smask) : 0;
       while (__ballot((cmask | cmask2 | cmask3) != 0u)) {
@@ -1099,21 +1101,22 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
           if (cmask) {
             const int src = __ffs(cmask) - 1;
             cmask &= cmask - 1u;
-            h = __shfl(hid.x, src, 16);
+            h = __shfl(hid.x, src, NH_G);
           } else if (cmask2) {
             const int src = __ffs(cmask2) - 1;
             cmask2 &= cmask2 - 1u;
-            h = __shfl(hid.y, src, 16);
+            h = __shfl(hid.y, src, NH_G);
           } else {
             const int src = __ffs(cmask3) - 1;
             cmask3 &= cmask3 - 1u;
-            h = __shfl(hid.z, src, 16);
+            h = __shfl(hid.z, src, NH_G);
           }
-          // the lane-unit's 32 rows, two per lane
+          // the lane-unit's 32 rows, 32 / NH_G per lane
 #pragma unroll
-          for (int b = 0; b < 2; b++) {
+          for (int r = 0; r < 32 / NH_G; r++) {
+            const int x = sl + NH_G * r, b = x >> 4, i = x & 15;
             const int64_t j =
-                (int64_t)(h >> 1) * 64 + 32 * b + 4 * (h & 1) + (sl & 3) + 8 * (sl >> 2);
+                (int64_t)(h >> 1) * 64 + 32 * b + 4 * (h & 1) + (i & 3) + 8 * (i >> 2);
             if (j < nv) {
               const double d = nn_dist64(qq, v + 8 * j);
               if (d < best || (d == best && j < bi)) {
@@ -1132,7 +1135,7 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
         if (!pend) break;
         const int src = __ffsll((long long)pend) - 1;  // first lane of the owning group
         const uint32_t sm = (uint32_t)__shfl((int)smask, src);
-        const bool owner = gbit == (src & ~15);
+        const bool owner = gbit == (src & ~(NH_G - 1));
         if (owner) smask &= smask - 1u;
         double oq[8];
 #pragma unroll
@@ -1164,9 +1167,9 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
       }
     }
 #pragma unroll
-    for (int off = 8; off > 0; off >>= 1) {
-      const double od = __shfl_xor(best, off, 16);
-      const int oi = __shfl_xor(bi, off, 16);
+    for (int off = NH_G / 2; off > 0; off >>= 1) {
+      const double od = __shfl_xor(best, off, NH_G);
+      const int oi = __shfl_xor(bi, off, NH_G);
       if (od < best || (od == best && oi < bi)) {
         best = od;
         bi = oi;
@@ -2175,7 +2178,7 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
                          nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
                          (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, NhPrep<float>{});
     }
-    hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(16 * w->bmax, NH_RTB, num_cus * 8)), dim3(NH_RTB),
+    hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(NH_G * w->bmax, NH_RTB, num_cus * 8)), dim3(NH_RTB),
                        0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, tr->count, w->bmax,
                        (const float4 *)w->nn_d, (const int4 *)w->nn_i, out, ++w->seq, w->nn_stats,
                        prep ? cs : nullptr);
