@@ -9,14 +9,19 @@
 //
 //   stage 0  k_targets          B draws of PlannerClass::randomState
 //                               (planner_class.cpp:38-76) + isValidState(STANCE)
-//   stage 1  k_compact_targets  the valid targets, in draw order
-//   stage 2  k_nn_filter/k_nn_reduce   getNearestNeighbor in T (planner_class.cpp:185-200)
-//            k_extend_prep      newConfig's 6 candidate actions (rrt.cpp:25-50)
+//   stage 1  k_compact_targets  the valid targets, in draw order (and their fp16
+//                               rows); a FRAGILE draw halts the sequence here
+//   stage 2  k_nn_mfma/k_nn_hreduce    getNearestNeighbor in T on the matrix cores
+//                               (planner_class.cpp:185-200); extra workgroups of the
+//                               same launch draw newConfig's 6 candidate actions
+//                               (rrt.cpp:25-50; k_extend_prep when they are
+//                               direction-biased), the reduce copies s_near
+//                               (GBP_OPT_NN_FILTER 1: k_nn_filter/k_nn_reduce)
 //            k_validate_persistent (gbp_engine.hip)  the candidates' pair checks
 //            k_select           newConfig's first valid candidate + acceptance (rrt.cpp:52-68)
 //   stage 3  k_append          non-TRAPPED successors appended to T in target order
 //                               (rrt.cpp:86-92; graph_class.cpp:28-42)
-//   stage 4  k_nn_filter/k_nn_reduce   the new vertices' nearest vertex in O
+//   stage 4  k_nn_mfma/k_nn_hreduce    the new vertices' nearest vertex in O
 //            k_connect          RRTConnectClass::attemptConnect (rrt_connect.cpp:20-91),
 //                               one wave per connection, the wave's 64 lanes
 //                               evaluating the pair check's samples together
