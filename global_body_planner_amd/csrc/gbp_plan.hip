@@ -674,14 +674,15 @@ __global__ __launch_bounds__(TB) void k_nn_reduce(const gbp_plan_status *st, con
 // ~2^-20 of the products, so the matrix cores score 1024 (query, vertex) pairs
 // per 64 MFMA cycles where the packed fp32 filter (k_nn_filter) spends ~4.5
 // VALU instructions per pair per pass.  The VALU only reduces: per lane (its
-// query, its 16 rows of the 32-row chunk: a "half-chunk"), the chunk minimum
-// by v_min3, then the running minimum m1, its half-chunk, and the second
-// smallest half-chunk minimum m2 (v_med3).  Work item = (4 query tiles = 128
-// queries, segment of chunks), one wave each; its (m1, m2, half-chunk) per
-// query go to the partial slots; k_nn_hreduce then takes B = min m1 over the
-// segments and re-checks in fp64 every half-chunk whose minimum is <= T(B),
-// and every row of a segment whose m2 is <= T(B) (a second half-chunk within
-// the threshold: rare).
+// query and its 32 rows of two consecutive chunks: a "lane-unit") the minimum
+// by v_min3, then the three smallest unit minima with their units and a bound
+// m4 on every other unit (NhTop: v_med3 / v_cndmask, branch-free).  Work item
+// = (4 query tiles = 128 queries, a segment of whole units), one wave each;
+// the two lanes of a query merge their lists and the (m1..m4, units) entry goes
+// to the partial slots; k_nn_hreduce then takes B = min m1 over the segments
+// and re-checks in fp64 every listed unit whose minimum is <= T(B), and every
+// row of a segment whose m4 is <= T(B) (a fourth unit within the threshold:
+// ~4 per planner half-iteration).
 // Why no minimiser is lost (everything in the scaled units; M_k = the tree's
 // hmax[k] >= max_j |F_jk|; S~_j the computed score):
 //   * each fp16 split has |x - hi - lo| <= 2^-20 |x| + 2^-14 (lo may be
@@ -696,8 +697,8 @@ __global__ __launch_bounds__(TB) void k_nn_reduce(const gbp_plan_status *st, con
 //     |G - F_j*|^2 <= |G - F_i|^2 (1 + 5e-15) for every row i, so with i the
 //     row scoring B: S~_j* <= B + 2 eps + 5e-15 (B + eps + |G|^2) <= T(B)
 //     (nh_threshold: fp64, 1e-14, rounded up to fp32) — and so does every row
-//     tying with j*.  Its half-chunk has minimum <= T (checked), or another
-//     half-chunk of that segment holds the segment's m1 and then m2 <= T (the
+//     tying with j*.  Its unit has minimum <= T: it is listed (checked), or
+//     three other units of that segment are listed and then m4 <= T (the
 //     segment is scanned).
 // Rows with |F_k| >= 2^13 (|v_k| >= 128) or NaN mark the tree (hbad): its
 // searches scan in fp64.  So do queries with |G_k| >= 2^13 or NaN.
