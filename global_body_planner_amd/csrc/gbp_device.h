@@ -752,11 +752,137 @@ __device__ __forceinline__ void uniform2(uint64_t seed, uint64_t stream_id, uint
   u1 = (double)(w1 >> 11) * 0x1p-53;
 }
 
+// ---- the samplers' transcendentals -------------------------------------------
+// The reference's draws (rand(), clock-seeded engines) are not reproducible
+// (SURVEY H11), so the engine defines its own streams and with them the log /
+// sin / cos / acos / atan2 that shape the uniforms.  The device libm and glibc
+// differ in the last bits; these routines use only +, -, *, /, sqrt, floor and
+// frexp (correctly rounded or exact in binary64), no contraction, a fixed
+// Horner order — the CPU restatement under oracle/ restates them, so the
+// host and the device draw bit-identical targets and candidate actions and a
+// whole planner run can be replayed on the CPU bit for bit.  A few ulp of
+// accuracy (series past 1e-17 relative): the sampled distributions are the
+// reference's.
+constexpr double RM_SIN[9] = {-0x1.5555555555555p-3, 0x1.1111111111111p-7,
+                                       -0x1.a01a01a01a01ap-13, 0x1.71de3a556c734p-19,
+                                       -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33,
+                                       -0x1.ae7f3e733b81fp-41, 0x1.952c77030ad4ap-49,
+                                       -0x1.2f49b46814157p-57};
+constexpr double RM_COS[9] = {-0x1.0000000000000p-1, 0x1.5555555555555p-5,
+                                       -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16,
+                                       -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29,
+                                       -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45,
+                                       -0x1.6827863b97d97p-53};
+constexpr double RM_LOG[11] = {0x1.5555555555555p-1, 0x1.999999999999ap-2,
+                                        0x1.2492492492492p-2, 0x1.c71c71c71c71cp-3,
+                                        0x1.745d1745d1746p-3, 0x1.3b13b13b13b14p-3,
+                                        0x1.1111111111111p-3, 0x1.e1e1e1e1e1e1ep-4,
+                                        0x1.af286bca1af28p-4, 0x1.8618618618618p-4,
+                                        0x1.642c8590b2164p-4};
+constexpr double RM_ATAN[12] = {-0x1.5555555555555p-2, 0x1.999999999999ap-3,
+                                         -0x1.2492492492492p-3, 0x1.c71c71c71c71cp-4,
+                                         -0x1.745d1745d1746p-4, 0x1.3b13b13b13b14p-4,
+                                         -0x1.1111111111111p-4, 0x1.e1e1e1e1e1e1ep-5,
+                                         -0x1.af286bca1af28p-5, 0x1.8618618618618p-5,
+                                         -0x1.642c8590b2164p-5, 0x1.47ae147ae147bp-5};
+constexpr double RM_INVPIO2 = 0x1.45f306dc9c883p-1;
+constexpr double RM_PIO2_1 = 0x1.921fb54400000p+0, RM_PIO2_2 = 0x1.0b4611a600000p-34,
+                 RM_PIO2_2T = 0x1.3198a2e037073p-69;
+constexpr double RM_PIO2_HI = 0x1.921fb54442d18p+0, RM_PIO2_LO = 0x1.1a62633145c07p-54;
+constexpr double RM_PI_HI = 0x1.921fb54442d18p+1, RM_PI_LO = 0x1.1a62633145c07p-53;
+constexpr double RM_LN2_HI = 0x1.62e42fee00000p-1, RM_LN2_LO = 0x1.a39ef35793c76p-33;
+
+// ln x, x > 0 finite: x = m 2^e, m in [sqrt(1/2), sqrt(2)), ln m = 2 atanh(f)
+__device__ __forceinline__ double rm_log(double x) {
+  int e;
+  double m = frexp(x, &e);
+  if (m < 0x1.6a09e667f3bcdp-1) {
+    m = m * 2.0;
+    e = e - 1;
+  }
+  const double f = (m - 1.0) / (m + 1.0);
+  const double w = f * f;
+  double p = RM_LOG[10];
+#pragma unroll
+  for (int k = 9; k >= 0; k--) p = RM_LOG[k] + w * p;
+  const double l = 2.0 * f + f * w * p;
+  const double de = (double)e;
+  return de * RM_LN2_HI + (l + de * RM_LN2_LO);
+}
+
+// sin x, cos x for |x| < 2^20: x = k pi/2 + r (Cody-Waite, three parts)
+__device__ __forceinline__ void rm_sincos(double x, double &s, double &c) {
+  const double kf = floor(x * RM_INVPIO2 + 0.5);
+  const double r = ((x - kf * RM_PIO2_1) - kf * RM_PIO2_2) - kf * RM_PIO2_2T;
+  const double z = r * r;
+  double ps = RM_SIN[8], pc = RM_COS[8];
+#pragma unroll
+  for (int k = 7; k >= 0; k--) {
+    ps = RM_SIN[k] + z * ps;
+    pc = RM_COS[k] + z * pc;
+  }
+  const double sr = r + r * z * ps;
+  const double cr = 1.0 + z * pc;
+  const int q = (int)kf & 3;
+  const double a = (q & 1) ? cr : sr, b = (q & 1) ? sr : cr;  // sin / cos of r + (q&1) pi/2, unsigned
+  s = (q == 0 || q == 1) ? a : -a;
+  c = (q == 0 || q == 3) ? b : -b;
+}
+
+// atan t, t in [0, 1]: two halvings atan t = 2 atan(t / (1 + sqrt(1 + t^2))),
+// then the series on [0, tan(pi/16)]
+__device__ __forceinline__ double rm_atan01(double t) {
+  t = t / (1.0 + sqrt(1.0 + t * t));
+  t = t / (1.0 + sqrt(1.0 + t * t));
+  const double v = t * t;
+  double p = RM_ATAN[11];
+#pragma unroll
+  for (int k = 10; k >= 0; k--) p = RM_ATAN[k] + v * p;
+  return 4.0 * (t + t * v * p);
+}
+
+// atan2 with glibc's signed-zero / axis conventions
+__device__ __forceinline__ double rm_atan2(double y, double x) {
+  if (isnan(x) || isnan(y)) return x + y;
+  const double ax = fabs(x), ay = fabs(y);
+  double a;
+  if (ay == 0.0) {
+    a = signbit(x) ? RM_PI_HI : 0.0;
+  } else if (ax == 0.0) {
+    a = RM_PIO2_HI;
+  } else {
+    if (ay <= ax)
+      a = rm_atan01(ay / ax);
+    else
+      a = RM_PIO2_HI - (rm_atan01(ax / ay) - RM_PIO2_LO);
+    if (signbit(x)) a = RM_PI_HI - (a - RM_PI_LO);
+  }
+  return copysign(a, y);
+}
+
+__device__ __forceinline__ double rm_acos(double c) {
+  return rm_atan2(sqrt((1.0 - c) * (1.0 + c)), c);
+}
+
 __device__ __forceinline__ void box_muller(double u1, double u2, double &z0, double &z1) {
-  const double r = sqrt(-2.0 * log(1.0 - u1));
+  const double r = sqrt(-2.0 * rm_log(1.0 - u1));
   const double th = 6.283185307179586 * u2;
-  z0 = r * cos(th);
-  z1 = r * sin(th);
+  double s, c;
+  rm_sincos(th, s, c);
+  z0 = r * c;
+  z1 = r * s;
+}
+
+// v (sin theta cos phi, sin theta sin phi, cos theta), theta = acos(cos_theta)
+// (planner_class.cpp:61-73)
+__device__ __forceinline__ void speed_vector(double v, double cos_theta, double phi, double *q) {
+  const double theta = rm_acos(cos_theta);
+  double st, ct, sp, cp;
+  rm_sincos(theta, st, ct);
+  rm_sincos(phi, sp, cp);
+  q[3] = v * st * cp;
+  q[4] = v * st * sp;
+  q[5] = v * ct;
 }
 
 // planning_utils.cpp:198-231 (Eigen cross / norm / I + [v]x + [v]x^2 (1-c)/s^2)
@@ -837,11 +963,8 @@ __device__ __forceinline__ void sample_state_try(const TerrainView<ZT> &T, uint6
   q[2] = std_max(std_min(hz, z_max_rel), z_min_rel) + g;
   const double phi = (2.0 * MY_PI) * u20;
   const double cos_theta = 2.0 * u21 - 1.0;
-  const double theta = acos(cos_theta);
   const double v = u30 * V_MAX;
-  q[3] = v * sin(theta) * cos(phi);
-  q[4] = v * sin(theta) * sin(phi);
-  q[5] = v * cos(theta);
+  speed_vector(v, cos_theta, phi, q);
   q[6] = 2 * P_MAX * u31 - P_MAX;
   q[7] = 0.0;
 }
@@ -938,14 +1061,11 @@ __device__ __forceinline__ void sample_state_direction_try(const TerrainView<ZT>
   bool near = false;
   if (!height_at(T, q[0], q[1], g, near)) g = __builtin_nan("");
   q[2] = std_max(std_min(hz, z_max_rel), z_min_rel) + g;
-  const double phi = speed_direction ? atan2(s_to[1] - s_from[1], s_to[0] - s_from[0])
+  const double phi = speed_direction ? rm_atan2(s_to[1] - s_from[1], s_to[0] - s_from[0])
                                      : (2.0 * MY_PI) * u20;
   const double cos_theta = 2.0 * u21 - 1.0;
-  const double theta = acos(cos_theta);
   const double v = u30 * V_MAX;
-  q[3] = v * sin(theta) * cos(phi);
-  q[4] = v * sin(theta) * sin(phi);
-  q[5] = v * cos(theta);
+  speed_vector(v, cos_theta, phi, q);
   q[6] = 2 * P_MAX * u31 - P_MAX;
   q[7] = 0.0;
 }

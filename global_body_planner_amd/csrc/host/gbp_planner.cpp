@@ -1373,6 +1373,23 @@ int RRTConnectClass::halfIterationBatched(PlannerClass &T, PlannerClass &O, Fast
   return 1;
 }
 
+static void dump_trees(const PlannerClass &Ta, const PlannerClass &Tb, TreeDump *d) {
+  if (!d) return;
+  const PlannerClass *t[2] = {&Ta, &Tb};
+  for (int k = 0; k < 2; k++) {
+    const int n = t[k]->getNumVertices();
+    d->v[k] = t[k]->vertices();
+    d->a[k].resize(n);
+    d->parent[k].resize(n);
+    d->g[k].resize(n);
+    for (int i = 0; i < n; i++) {
+      d->a[k][i] = t[k]->getAction(i);
+      d->parent[k][i] = t[k]->getPredecessor(i);
+      d->g[k][i] = t[k]->getGValue(i);
+    }
+  }
+}
+
 bool RRTConnectClass::buildRRTConnectBatched(FastTerrainMap &terrain, State s_start, State s_goal,
                                              int batch, double max_time,
                                              std::vector<State> &state_sequence,
@@ -1389,14 +1406,18 @@ bool RRTConnectClass::buildRRTConnectBatched(FastTerrainMap &terrain, State s_st
   BatchStats local;
   BatchStats &st = stats ? *stats : local;
   int ia = -1, ib = -1;
-  while (true) {
+  auto more = [&]() { return st.max_halves <= 0 || st.halves < st.max_halves; };
+  while (more()) {
     std::chrono::duration<double> el = std::chrono::high_resolution_clock::now() - t_start;
     if (el.count() >= max_time) break;
     st.iterations++;
+    st.halves++;
     if (halfIterationBatched(Ta, Tb, terrain, FORWARD, batch, ia, ib, &st)) {
       goal_found = true;
       break;
     }
+    if (!more()) break;
+    st.halves++;
     if (halfIterationBatched(Tb, Ta, terrain, REVERSE, batch, ib, ia, &st)) {
       goal_found = true;
       break;
@@ -1408,6 +1429,9 @@ bool RRTConnectClass::buildRRTConnectBatched(FastTerrainMap &terrain, State s_st
   st.vertices_a = Ta.getNumVertices();
   st.vertices_b = Tb.getNumVertices();
   num_vertices = Ta.getNumVertices() + Tb.getNumVertices();
+  dump_trees(Ta, Tb, st.dump);
+  st.meet_a = ia;
+  st.meet_b = ib;
   if (!goal_found) return false;
   wall_to_first_ = elapsed_to_first.count();
   // rrt_connect.cpp:386-401 with the meeting vertices (ia in Ta, ib in Tb)
@@ -1538,6 +1562,10 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
   int32_t half = 0;
   gbp_plan_status ps{};
   while (since() < max_time) {
+    if (st.max_halves > 0) {  // a replayable run: exactly max_halves half-iterations
+      if (half >= st.max_halves) break;
+      group = (int)std::min<int64_t>(group, st.max_halves - half);
+    }
     for (int k = 0; k < 2; k++) {  // room for `group` halves of appends
       int64_t c = 0;
       chk(gbp_tree_capacity(D.tree[k], &c), "tree capacity");
@@ -1589,6 +1617,7 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
   elapsed_to_first = std::chrono::high_resolution_clock::now() - t_start;
   extend_counter_ = ps.ext_counter;
   const int32_t halves_run = goal_found ? ps.meet_half + 1 : half;
+  st.halves += halves_run;
   st.iterations += (halves_run + 1) / 2;
   st.targets += ps.stat_targets;
   st.extends += ps.stat_targets;
@@ -1606,6 +1635,15 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
   st.vertices_a = (int64_t)A.v.size();
   st.vertices_b = (int64_t)B.v.size();
   num_vertices = (int)(A.v.size() + B.v.size());
+  if (st.dump) {
+    const HostTree *t[2] = {&A, &B};
+    for (int k = 0; k < 2; k++) {
+      st.dump->v[k] = t[k]->v;
+      st.dump->a[k] = t[k]->a;
+      st.dump->parent[k] = t[k]->parent;
+      st.dump->g[k] = t[k]->g;
+    }
+  }
   if (!goal_found) return false;
   st.solutions++;
   wall_to_first_ = elapsed_to_first.count();
@@ -1615,6 +1653,8 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
   const int32_t tvtx = ps.added_base + kconn;
   const bool t_is_a = (ps.meet_half & 1) == 0;
   const int ia = t_is_a ? tvtx : o, ib = t_is_a ? o : tvtx;
+  st.meet_a = ia;
+  st.meet_b = ib;
   // rrt_connect.cpp:386-401 with the meeting vertices (as buildRRTConnectBatched)
   std::vector<int> path_a = host_path(A, ia);
   std::vector<int> path_b = host_path(B, ib);
@@ -1994,11 +2034,12 @@ bool RRTStarConnectClass::buildRRTStarConnectBatched(FastTerrainMap &terrain, St
   std::vector<int> shared_a, shared_b;
   int best_a = -1, best_b = -1;
   double cost_so_far = INFTY;
-  while (true) {
+  while (st.max_halves <= 0 || st.halves + 2 <= st.max_halves) {
     const double el =
         std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t_start).count();
     if (el >= max_time) break;
     st.iterations++;
+    st.halves += 2;
     for (int half = 0; half < 2; half++) {
       PlannerClass &T = half == 0 ? Ta : Tb;
       PlannerClass &O = half == 0 ? Tb : Ta;
@@ -2037,6 +2078,9 @@ bool RRTStarConnectClass::buildRRTStarConnectBatched(FastTerrainMap &terrain, St
   st.vertices_b = Tb.getNumVertices();
   num_vertices = Ta.getNumVertices() + Tb.getNumVertices();
   best_cost_ = cost_so_far;
+  dump_trees(Ta, Tb, st.dump);
+  st.meet_a = best_a;
+  st.meet_b = best_b;
   if (!goal_found) return false;
   getStateAndActionSequences(Ta, Tb, best_a, best_b, state_sequence, action_sequence);
   path_length_ = Ta.getGValue(best_a) + Tb.getGValue(best_b);
@@ -2081,6 +2125,9 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     std::vector<State> states;
     std::vector<Action> actions;
     BatchStats st;
+    TreeDump dump;
+    st.max_halves = p->max_halves > 0 ? p->max_halves : 0;
+    if (p->tree_capacity > 0) st.dump = &dump;
     const auto t0 = std::chrono::high_resolution_clock::now();
     const bool found =
         p->algorithm == 1
@@ -2126,6 +2173,21 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     for (int k = 0; k < 3; k++) r->halts[k] = st.halts[k];
     r->nn_rechecks = st.nn_rechecks;
     r->nn_scans = st.nn_scans;
+    r->reported_length = found ? planner.pathLength() : 0.0;
+    r->reported_yaw = found ? planner.pathYaw() : 0.0;
+    r->meet_a = st.meet_a;
+    r->meet_b = st.meet_b;
+    r->halves = st.halves;
+    if (st.dump)
+      for (int k = 0; k < 2; k++) {
+        const int64_t n = std::min<int64_t>(p->tree_capacity, (int64_t)dump.v[k].size());
+        for (int64_t i = 0; i < n; i++) {
+          if (p->tree_v[k]) std::copy(dump.v[k][i].begin(), dump.v[k][i].end(), p->tree_v[k] + 8 * i);
+          if (p->tree_a[k]) std::copy(dump.a[k][i].begin(), dump.a[k][i].end(), p->tree_a[k] + 10 * i);
+          if (p->tree_parent[k]) p->tree_parent[k][i] = dump.parent[k][i];
+          if (p->tree_g[k]) p->tree_g[k][i] = dump.g[k][i];
+        }
+      }
     if (found) {
       double len = 0;
       for (size_t i = 1; i < states.size(); i++) len += planning_utils::poseDistance(states[i - 1], states[i]);

@@ -30,7 +30,9 @@ class PlanParams(ctypes.Structure):
                 ("sampling", _lib.Sampling), ("fragile_eps_fm", ctypes.c_int64),
                 ("adaptive", ctypes.c_int), ("nn_index", ctypes.c_int64),
                 ("nn_filter", ctypes.c_int), ("nn_stats", ctypes.c_int),
-                ("no_overlap", ctypes.c_int)]
+                ("no_overlap", ctypes.c_int), ("max_halves", ctypes.c_int64),
+                ("tree_capacity", ctypes.c_int64), ("tree_v", _P * 2), ("tree_a", _P * 2),
+                ("tree_parent", _P * 2), ("tree_g", _P * 2)]
 
 
 class PlanResult(ctypes.Structure):
@@ -44,7 +46,9 @@ class PlanResult(ctypes.Structure):
                 ("extent_a", _D * 4), ("extent_b", _D * 4),
                 ("fragile_resolved", ctypes.c_int64), ("depth_capped", ctypes.c_int64),
                 ("status_reads", ctypes.c_int64), ("halts", ctypes.c_int64 * 3),
-                ("nn_rechecks", ctypes.c_int64), ("nn_scans", ctypes.c_int64)]
+                ("nn_rechecks", ctypes.c_int64), ("nn_scans", ctypes.c_int64),
+                ("reported_length", _D), ("reported_yaw", _D), ("meet_a", ctypes.c_int32),
+                ("meet_b", ctypes.c_int32), ("halves", ctypes.c_int64)]
 
 
 _planner = None
@@ -102,7 +106,8 @@ def start_goal_state(height, x, y):
 def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018,
                      post_process=False, device=0, capacity=4096, algorithm=0, max_time_opt=0.0,
                      sampling=None, fragile_eps=None, adaptive=False, nn_index=0,
-                     nn_filter=0, nn_stats=False, overlap=True):
+                     nn_filter=0, nn_stats=False, overlap=True, max_halves=0, trees=False,
+                     tree_capacity=1 << 18):
     """Plan start -> goal on terrain `data` (terrain_data.TerrainData).
 
     algorithm 0: batch-synchronous RRT-Connect, stops at the first solution;
@@ -124,7 +129,11 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     nn_index: GBP_OPT_NN_INDEX, the smallest tree the device loop searches
       through its nearest-neighbour index (0: the default, never; < 0: never);
     nn_filter: GBP_OPT_NN_FILTER, the nearest-neighbour scan (0 matrix cores,
-      1 packed fp32: same results)."""
+      1 packed fp32: same results);
+    max_halves: algorithms 0, 1, 3 stop after this many half-iterations (a
+      replayable run; 0 = no limit);
+    trees: also return the final trees (out["a"], out["b"]: v, act, parent, g;
+      algorithms 0, 1, 3), at most tree_capacity rows each."""
     L = load()
     x = np.ascontiguousarray(data.x, dtype=np.float64)
     y = np.ascontiguousarray(data.y, dtype=np.float64)
@@ -148,6 +157,16 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     p.nn_filter = int(nn_filter)
     p.nn_stats = int(bool(nn_stats))
     p.no_overlap = 0 if overlap else 1
+    p.max_halves = int(max_halves)
+    tb = []
+    if trees:
+        p.tree_capacity = int(tree_capacity)
+        for k in range(2):
+            arrs = dict(v=np.zeros((tree_capacity, 8)), act=np.zeros((tree_capacity, 10)),
+                        parent=np.zeros(tree_capacity, np.int32), g=np.zeros(tree_capacity))
+            tb.append(arrs)
+            p.tree_v[k], p.tree_a[k] = arrs["v"].ctypes.data, arrs["act"].ctypes.data
+            p.tree_parent[k], p.tree_g[k] = arrs["parent"].ctypes.data, arrs["g"].ctypes.data
     r = PlanResult()
     states = np.zeros((capacity, 8))
     actions = np.zeros((capacity, 10))
@@ -158,6 +177,9 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     out = {k: getattr(r, k) for k, _ in PlanResult._fields_}
     out["extent_a"], out["extent_b"] = list(r.extent_a), list(r.extent_b)
     out["halts"] = list(r.halts)
+    for name, arrs, nv in zip("ab", tb, (r.vertices_a, r.vertices_b)):
+        m = min(int(nv), tree_capacity)
+        out[name] = {k: v[:m].copy() for k, v in arrs.items()}
     n = r.n_states
     out["states"] = states[:n].copy()
     out["actions"] = actions[:max(n - 1, 0)].copy()

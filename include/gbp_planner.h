@@ -339,6 +339,8 @@ class RRTClass {
   double wallTimeToFirst() const { return wall_to_first_; }
   // the last build's path cost / its history (rrt_connect.h getters' data)
   double pathCost() const { return path_cost_; }
+  double pathLength() const { return path_length_; }
+  double pathYaw() const { return path_yaw_; }
   // the reference's path cost: length, or the cost_add_yaw weighted sum
   // (rrt_connect.cpp:304-313, :193-215)
   double weightedCost(double length, double yaw) const {
@@ -375,7 +377,20 @@ class RRTClass {
   int64_t extend_counter_ = 0;
 };
 
+// The final trees of a batched / device-resident search (for callers that
+// replay it, e.g. against a CPU restatement): Ta = [0], Tb = [1].
+struct TreeDump {
+  std::vector<State> v[2];
+  std::vector<Action> a[2];
+  std::vector<int32_t> parent[2];
+  std::vector<double> g[2];
+};
+
 struct BatchStats {
+  int64_t max_halves = 0;     // in: stop after this many half-iterations (0 = no limit)
+  TreeDump *dump = nullptr;   // in: receives the final trees when set
+  int64_t halves = 0;         // half-iterations run
+  int32_t meet_a = -1, meet_b = -1;  // the joined vertices (RRT*: the best pair)
   int64_t iterations = 0, targets = 0, extends = 0, attempts_checked = 0, connects = 0;
   int64_t vertices_a = 0, vertices_b = 0;
   int64_t rewires = 0, solutions = 0;
@@ -606,6 +621,13 @@ typedef struct {
   int nn_filter;          // GBP_OPT_NN_FILTER: 0 matrix cores (default), 1 packed fp32
   int nn_stats;           // GBP_OPT_NN_STATS: count the search's fp64 re-checks (diagnostics)
   int no_overlap;         // 1: GBP_OPT_PLAN_OVERLAP off (0 = the handle's default)
+  int64_t max_halves;     // algorithms 0, 1, 3: stop after this many half-iterations
+                          // (0 = no limit): a run that can be replayed exactly
+  int64_t tree_capacity;  // rows of the tree_* buffers (0 = the trees are not returned)
+  double *tree_v[2];      // algorithms 0, 1, 3: the final trees Ta / Tb — states [cap][8],
+  double *tree_a[2];      //   the action reaching each vertex [cap][10] (root: zeros),
+  int32_t *tree_parent[2];  // parents (root -1) and g values; rows past the result's
+  double *tree_g[2];      //   vertices_a / vertices_b are not written
 } gbp_plan_params;
 
 typedef struct {
@@ -624,6 +646,12 @@ typedef struct {
                                // connect stage of the device loop
   int64_t nn_rechecks, nn_scans;  // algorithm 3 with nn_stats: the matrix-core search's
                                   // fp64 half-chunk re-checks and segment scans
+  double reported_length, reported_yaw;  // the planner's path_length_ / path_yaw_ (what
+                                         // getStatistics reports; after postProcessPath
+                                         // with its quirk, rrt_connect.cpp:202-215)
+  int32_t meet_a, meet_b;      // algorithms 0 / 3: the vertices of Ta / Tb the first REACHED
+                               // connect joined; algorithm 1: the best pair
+  int64_t halves;              // half-iterations run
 } gbp_plan_result;
 
 /* plans from start to goal; path_states[capacity][8] / path_actions[capacity][10]

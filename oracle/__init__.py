@@ -82,6 +82,9 @@ def lib():
             "orc_sample_actions_dir": (None, [I64, P, P, P, P, I, I, D, U64, U64, I64, P, I]),
             "orc_philox4x32_10": (None, [P, P, P]),
             "orc_uniform2": (None, [U64, U64, ctypes.c_uint32, I64, ctypes.c_uint32, P]),
+            "orc_rmath": (None, [I, I64, P, P, P]),
+            "orc_plan": (I, [P, P, P, P, P, P]),
+            "orc_post_process_path": (I, [P, I, P, P, I, P, P, P, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -97,6 +100,35 @@ def _p(a):
 
 def _c(a, dtype):
     return np.ascontiguousarray(a, dtype=dtype)
+
+
+class _Tree(ctypes.Structure):
+    _fields_ = [("cap", ctypes.c_int), ("n", ctypes.c_int), ("v", ctypes.c_void_p),
+                ("a", ctypes.c_void_p), ("parent", ctypes.c_void_p), ("g", ctypes.c_void_p),
+                ("y", ctypes.c_void_p), ("child", ctypes.c_void_p), ("sibling", ctypes.c_void_p)]
+
+
+class _PlanCfg(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int), ("seed", ctypes.c_uint64), ("stream_a", ctypes.c_uint64),
+                ("stream_b", ctypes.c_uint64), ("adaptive", ctypes.c_int),
+                ("state_flag", ctypes.c_int), ("state_speed_direction", ctypes.c_int),
+                ("action_flag", ctypes.c_int), ("state_p", ctypes.c_double),
+                ("action_p", ctypes.c_double), ("extend_base", ctypes.c_int64),
+                ("max_halves", ctypes.c_int64), ("star", ctypes.c_int),
+                ("star_delta", ctypes.c_double)]
+
+
+class _PlanOut(ctypes.Structure):
+    _fields_ = [("found", ctypes.c_int), ("meet_a", ctypes.c_int), ("meet_b", ctypes.c_int),
+                ("meet_half", ctypes.c_int64), ("halves", ctypes.c_int64),
+                ("targets", ctypes.c_int64), ("extends", ctypes.c_int64),
+                ("attempts", ctypes.c_int64), ("connects", ctypes.c_int64),
+                ("depth_capped", ctypes.c_int64), ("rewires", ctypes.c_int64),
+                ("solutions", ctypes.c_int64), ("ext_counter", ctypes.c_int64),
+                ("draws_a", ctypes.c_int64), ("draws_b", ctypes.c_int64),
+                ("path_length", ctypes.c_double), ("path_yaw", ctypes.c_double),
+                ("best_a", ctypes.c_int), ("best_b", ctypes.c_int),
+                ("best_cost", ctypes.c_double)]
 
 
 class OracleTerrain:
@@ -230,6 +262,56 @@ class OracleTerrain:
                                     _p(st), nthreads)
         return st
 
+    def plan(self, start, goal, *, batch, seed, stream_a=101, stream_b=102, max_halves=0,
+             adaptive=False, sampling=None, star=False, star_delta=3.0, extend_base=0,
+             capacity=200000):
+        """The batch-synchronous RRT-Connect (RRT*-Connect with star=True) the
+        engine runs, restated on the CPU (orc_plan): returns a dict with the
+        counters, the meeting / best vertices, and each tree's arrays
+        ("a"/"b": v, act, parent, g, y).  sampling: dict of gbp_sampling
+        fields (state_flag, state_p, speed_direction, action_flag, action_p)."""
+        trees, keep = [], []
+        for _ in range(2):
+            arrs = dict(v=np.zeros((capacity, 8)), act=np.zeros((capacity, 10)),
+                        parent=np.zeros(capacity, np.int32), g=np.zeros(capacity),
+                        y=np.zeros(capacity), child=np.zeros(capacity, np.int32),
+                        sibling=np.zeros(capacity, np.int32))
+            keep.append(arrs)
+            trees.append(_Tree(capacity, 0, *(arrs[k].ctypes.data for k in
+                                              ("v", "act", "parent", "g", "y", "child", "sibling"))))
+        tr = (_Tree * 2)(*trees)
+        sm = sampling or {}
+        cfg = _PlanCfg(int(batch), int(seed), int(stream_a), int(stream_b), int(bool(adaptive)),
+                       int(bool(sm.get("state_flag", False))),
+                       int(bool(sm.get("speed_direction", False))),
+                       int(bool(sm.get("action_flag", False))), float(sm.get("state_p", 0.0)),
+                       float(sm.get("action_p", 0.0)), int(extend_base), int(max_halves),
+                       int(bool(star)), float(star_delta))
+        out = _PlanOut()
+        st, gl = _c(start, np.float64), _c(goal, np.float64)
+        rc = lib().orc_plan(self.ref, _p(st), _p(gl), ctypes.byref(cfg), tr, ctypes.byref(out))
+        if rc != 0:
+            raise RuntimeError(f"orc_plan returned {rc}")
+        res = {k: getattr(out, k) for k, _ in _PlanOut._fields_}
+        for name, t, arrs in zip("ab", tr, keep):
+            n = t.n
+            res[name] = {k: arrs[k][:n].copy() for k in ("v", "act", "parent", "g", "y")}
+        if res["found"] and not star:
+            res["states"], res["actions"] = _join_path(res["a"], res["b"], res["meet_a"],
+                                                       res["meet_b"])
+        return res
+
+    def post_process_path(self, states, actions, adaptive=False):
+        """rrt_connect.cpp:139-227 -> (states, actions, path_length_, path_yaw_, path_cost_)."""
+        st = _c(states, np.float64).reshape(-1, 8)
+        ac = _c(actions, np.float64).reshape(-1, 10)
+        n = st.shape[0]
+        os_, oa = np.zeros((n, 8)), np.zeros((max(n - 1, 1), 10))
+        L, Y, C = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        m = lib().orc_post_process_path(self.ref, n, _p(st), _p(ac), int(bool(adaptive)), _p(os_),
+                                        _p(oa), ctypes.byref(L), ctypes.byref(Y), ctypes.byref(C))
+        return os_[:m].copy(), oa[:m - 1].copy(), L.value, Y.value, C.value
+
     def attempt_connect(self, s_existing, s, direction, t_s=0.0, adaptive=False):
         s_existing = _c(s_existing, np.float64)
         s = _c(s, np.float64)
@@ -238,6 +320,26 @@ class OracleTerrain:
         r = lib().orc_attempt_connect(self.ref, _p(s_existing), _p(s), float(t_s), _p(s_new),
                                       _p(a_new), int(direction), int(bool(adaptive)))
         return r, s_new, a_new
+
+
+def _path_from_start(tree, idx):  # rrt.cpp:107-118
+    path = [idx]
+    while idx != 0:
+        idx = int(tree["parent"][idx])
+        path.append(idx)
+    return path[::-1]
+
+
+def _join_path(ta, tb, ia, ib):
+    """rrt_connect.cpp:386-401: Ta's root -> ia, then Tb's ib -> root (ib itself
+    dropped), with Tb's actions in reverse (getActionSequenceReverse)."""
+    pa = _path_from_start(ta, ia)
+    pb = _path_from_start(tb, ib)[::-1]
+    act_b = [tb["act"][i] for i in pb[:-1]]
+    pb = pb[1:]
+    states = np.array([ta["v"][i] for i in pa] + [tb["v"][i] for i in pb])
+    actions = np.array([ta["act"][i] for i in pa[1:]] + act_b).reshape(-1, 10)
+    return states, actions
 
 
 def sample_actions(normals, seed, stream_id, index_base=0, nthreads=1):
@@ -327,6 +429,15 @@ def philox(ctr, key):
     o = np.empty(4, np.uint32)
     lib().orc_philox4x32_10(_p(c), _p(k), _p(o))
     return o
+
+
+def rmath(fn, x, y=None):
+    """The samplers' reproducible log / sincos / atan2 / acos (orc_rmath)."""
+    x = _c(x, np.float64).ravel()
+    yy = None if y is None else _c(y, np.float64).ravel()
+    out = np.empty(2 * x.size if fn == 1 else x.size)
+    lib().orc_rmath(int(fn), x.size, _p(x), _p(yy), _p(out))
+    return out.reshape(-1, 2) if fn == 1 else out
 
 
 def set_scan_mode(mode):

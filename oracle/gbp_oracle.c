@@ -7,6 +7,7 @@
 #include "gbp_oracle.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -570,23 +571,14 @@ int orc_extend(const orc_terrain *T, const double *s_near, const double *target,
   return (orc_state_distance(s_new, target) <= GOAL_BOUNDS) ? GBP_REACHED : GBP_ADVANCED;
 }
 
-/* rrt_connect.cpp:20-84 (recursive attemptConnect) */
-static int attempt_connect_ts(const orc_terrain *T, const double *s_existing, const double *s,
-                              double t_s, double *s_new, double *a_new, int direction,
-                              int adaptive, int depth) {
-  if (t_s <= KINEMATICS_RES) return GBP_TRAPPED;
-  /* engine convention (gbp.h GBP_CONNECT_MAX_DEPTH): the reference recursion is unbounded */
-  if (depth > GBP_CONNECT_MAX_DEPTH) return GBP_TRAPPED;
-  const double *s_start = (direction == GBP_FORWARD) ? s_existing : s;
-  const double *s_goal = (direction == GBP_FORWARD) ? s : s_existing;
-  double t_new = NAN; /* reference: uninitialised (SURVEY A11) */
-  double t_f = 0;
+/* rrt_connect.cpp:53-63: the cubic-Hermite stance action from s_start to
+ * s_goal in t_s (t_f = 0) */
+static void connect_action(const double *s_start, const double *s_goal, double t_s, double *a) {
   double x_td = s_start[0], y_td = s_start[1], z_td = s_start[2];
   double dx_td = s_start[3], dy_td = s_start[4], dz_td = s_start[5];
   double x_to = s_goal[0], y_to = s_goal[1], z_to = s_goal[2];
   double dx_to = s_goal[3], dy_to = s_goal[4], dz_to = s_goal[5];
   double p_td = s_start[6], dp_td = s_start[7], p_to = s_goal[6], dp_to = s_goal[7];
-  double a[10];
   a[0] = -(2.0 * (3.0 * x_td - 3.0 * x_to + 2.0 * dx_td * t_s + dx_to * t_s)) / (t_s * t_s);
   a[1] = -(2.0 * (3.0 * y_td - 3.0 * y_to + 2.0 * dy_td * t_s + dy_to * t_s)) / (t_s * t_s);
   a[2] = -(2.0 * (3.0 * z_td - 3.0 * z_to + 2.0 * dz_td * t_s + dz_to * t_s)) / (t_s * t_s);
@@ -594,12 +586,37 @@ static int attempt_connect_ts(const orc_terrain *T, const double *s_existing, co
   a[4] = (2.0 * (3.0 * y_td - 3.0 * y_to + dy_td * t_s + 2.0 * dy_to * t_s)) / (t_s * t_s);
   a[5] = (2.0 * (3.0 * z_td - 3.0 * z_to + dz_td * t_s + 2.0 * dz_to * t_s)) / (t_s * t_s);
   a[6] = t_s;
-  a[7] = t_f;
+  a[7] = 0;
   a[8] = -(2.0 * (3.0 * p_td - 3.0 * p_to + 2.0 * dp_td * t_s + dp_to * t_s)) / (t_s * t_s);
   a[9] = (2.0 * (3.0 * p_td - 3.0 * p_to + dp_td * t_s + 2.0 * dp_to * t_s)) / (t_s * t_s);
+}
+
+/* rrt_connect.cpp:20-84 (recursive attemptConnect) */
+typedef struct {
+  int capped;     /* the recursion reached GBP_CONNECT_MAX_DEPTH */
+  int64_t checks; /* pair checks run (the engine's attempts_checked) */
+} ac_stats;
+
+static int attempt_connect_ts(const orc_terrain *T, const double *s_existing, const double *s,
+                              double t_s, double *s_new, double *a_new, int direction,
+                              int adaptive, int depth, ac_stats *acs) {
+  /* engine convention (gbp.h GBP_CONNECT_MAX_DEPTH): the reference recursion
+   * is unbounded; levels 0 .. MAX are evaluated, a connection still open then
+   * is TRAPPED (and counted) */
+  if (depth > GBP_CONNECT_MAX_DEPTH) {
+    if (acs) acs->capped = 1;
+    return GBP_TRAPPED;
+  }
+  if (t_s <= KINEMATICS_RES) return GBP_TRAPPED;
+  const double *s_start = (direction == GBP_FORWARD) ? s_existing : s;
+  const double *s_goal = (direction == GBP_FORWARD) ? s : s_existing;
+  double t_new = NAN; /* reference: uninitialised (SURVEY A11) */
+  double a[10];
+  connect_action(s_start, s_goal, t_s, a);
   memcpy(a_new, a, sizeof a);
   if (orc_is_valid_action(a_new)) {
     uint32_t f;
+    if (acs) acs->checks++;
     int ok = (direction == GBP_FORWARD)
                  ? orc_is_valid_pair(T, s_start, a_new, GBP_FORWARD, adaptive, s_new, &t_new, &f, 0)
                  : orc_is_valid_pair(T, s_goal, a_new, GBP_REVERSE, adaptive, s_new, &t_new, &f, 0);
@@ -611,7 +628,7 @@ static int attempt_connect_ts(const orc_terrain *T, const double *s_existing, co
     double s_mid[8];
     memcpy(s_mid, s_new, sizeof s_mid);
     if (attempt_connect_ts(T, s_existing, s_mid, t_new, s_new, a_new, direction, adaptive,
-                           depth + 1) == GBP_TRAPPED)
+                           depth + 1, acs) == GBP_TRAPPED)
       return GBP_TRAPPED;
     return GBP_ADVANCED;
   }
@@ -621,7 +638,7 @@ static int attempt_connect_ts(const orc_terrain *T, const double *s_existing, co
 int orc_attempt_connect(const orc_terrain *T, const double *s_existing, const double *s,
                         double t_s, double *s_new, double *a_new, int direction, int adaptive) {
   if (!(t_s > 0)) t_s = orc_pose_distance(s, s_existing) / V_NOM; /* rrt_connect.cpp:89 */
-  return attempt_connect_ts(T, s_existing, s, t_s, s_new, a_new, direction, adaptive, 0);
+  return attempt_connect_ts(T, s_existing, s, t_s, s_new, a_new, direction, adaptive, 0, 0);
 }
 
 /* ---- batch helpers ------------------------------------------------------ */
@@ -779,13 +796,151 @@ void orc_uniform2(uint64_t seed, uint64_t stream_id, uint32_t purpose, int64_t i
   u[1] = (double)(w1 >> 11) * 0x1p-53;
 }
 
+/* ---- the samplers' transcendentals (restates gbp_device.h rm_*) -------------
+ * The reference draws from rand() and clock-seeded engines: its
+ * samples are not reproducible, so the engine defines its own streams, and
+ * with them the log / sin / cos / acos / atan2 that turn uniforms into
+ * samples.  glibc and the device libm differ in the last bits, so both sides
+ * use these routines: +, -, *, /, sqrt, floor, frexp only (all correctly
+ * rounded or exact in IEEE binary64), no contraction, fixed Horner order —
+ * host and device then draw bit-identical targets and candidate actions, and
+ * a planner run is reproducible bit for bit off the device.  Accuracy: a few
+ * ulp (Taylor / atanh series past 1e-17 relative), which leaves the
+ * distributions the reference samples unchanged. */
+static const double RM_SIN[9] = {-0x1.5555555555555p-3, 0x1.1111111111111p-7,
+                                 -0x1.a01a01a01a01ap-13, 0x1.71de3a556c734p-19,
+                                 -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33,
+                                 -0x1.ae7f3e733b81fp-41, 0x1.952c77030ad4ap-49,
+                                 -0x1.2f49b46814157p-57};
+static const double RM_COS[9] = {-0x1.0000000000000p-1, 0x1.5555555555555p-5,
+                                 -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16,
+                                 -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29,
+                                 -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45,
+                                 -0x1.6827863b97d97p-53};
+static const double RM_LOG[11] = {0x1.5555555555555p-1, 0x1.999999999999ap-2, 0x1.2492492492492p-2,
+                                  0x1.c71c71c71c71cp-3, 0x1.745d1745d1746p-3, 0x1.3b13b13b13b14p-3,
+                                  0x1.1111111111111p-3, 0x1.e1e1e1e1e1e1ep-4, 0x1.af286bca1af28p-4,
+                                  0x1.8618618618618p-4, 0x1.642c8590b2164p-4};
+static const double RM_ATAN[12] = {-0x1.5555555555555p-2, 0x1.999999999999ap-3,
+                                   -0x1.2492492492492p-3, 0x1.c71c71c71c71cp-4,
+                                   -0x1.745d1745d1746p-4, 0x1.3b13b13b13b14p-4,
+                                   -0x1.1111111111111p-4, 0x1.e1e1e1e1e1e1ep-5,
+                                   -0x1.af286bca1af28p-5, 0x1.8618618618618p-5,
+                                   -0x1.642c8590b2164p-5, 0x1.47ae147ae147bp-5};
+#define RM_INVPIO2 0x1.45f306dc9c883p-1
+#define RM_PIO2_1 0x1.921fb54400000p+0
+#define RM_PIO2_2 0x1.0b4611a600000p-34
+#define RM_PIO2_2T 0x1.3198a2e037073p-69
+#define RM_PIO2_HI 0x1.921fb54442d18p+0
+#define RM_PIO2_LO 0x1.1a62633145c07p-54
+#define RM_PI_HI 0x1.921fb54442d18p+1
+#define RM_PI_LO 0x1.1a62633145c07p-53
+#define RM_LN2_HI 0x1.62e42fee00000p-1
+#define RM_LN2_LO 0x1.a39ef35793c76p-33
+
+/* ln x, x > 0 finite: x = m 2^e, m in [sqrt(1/2), sqrt(2)), ln m = 2 atanh(f) */
+static double rm_log(double x) {
+  int e;
+  double m = frexp(x, &e);
+  if (m < 0x1.6a09e667f3bcdp-1) {
+    m = m * 2.0;
+    e = e - 1;
+  }
+  double f = (m - 1.0) / (m + 1.0);
+  double w = f * f;
+  double p = RM_LOG[10];
+  for (int k = 9; k >= 0; k--) p = RM_LOG[k] + w * p;
+  double l = 2.0 * f + f * w * p;
+  double de = (double)e;
+  return de * RM_LN2_HI + (l + de * RM_LN2_LO);
+}
+
+/* sin x, cos x for |x| < 2^20: x = k pi/2 + r (Cody-Waite, three parts) */
+static void rm_sincos(double x, double *s, double *c) {
+  double kf = floor(x * RM_INVPIO2 + 0.5);
+  double r = ((x - kf * RM_PIO2_1) - kf * RM_PIO2_2) - kf * RM_PIO2_2T;
+  double z = r * r;
+  double ps = RM_SIN[8], pc = RM_COS[8];
+  for (int k = 7; k >= 0; k--) {
+    ps = RM_SIN[k] + z * ps;
+    pc = RM_COS[k] + z * pc;
+  }
+  double sr = r + r * z * ps;
+  double cr = 1.0 + z * pc;
+  switch ((int)kf & 3) {
+    case 0: *s = sr; *c = cr; break;
+    case 1: *s = cr; *c = -sr; break;
+    case 2: *s = -sr; *c = -cr; break;
+    default: *s = -cr; *c = sr; break;
+  }
+}
+
+/* atan t, t in [0, 1]: two halvings atan t = 2 atan(t / (1 + sqrt(1 + t^2))),
+ * then the series on [0, tan(pi/16)] */
+static double rm_atan01(double t) {
+  t = t / (1.0 + sqrt(1.0 + t * t));
+  t = t / (1.0 + sqrt(1.0 + t * t));
+  double v = t * t;
+  double p = RM_ATAN[11];
+  for (int k = 10; k >= 0; k--) p = RM_ATAN[k] + v * p;
+  return 4.0 * (t + t * v * p);
+}
+
+/* atan2 with glibc's signed-zero / axis conventions */
+static double rm_atan2(double y, double x) {
+  if (isnan(x) || isnan(y)) return x + y;
+  double ax = fabs(x), ay = fabs(y), a;
+  if (ay == 0.0) {
+    a = signbit(x) ? RM_PI_HI : 0.0;
+  } else if (ax == 0.0) {
+    a = RM_PIO2_HI;
+  } else {
+    if (ay <= ax)
+      a = rm_atan01(ay / ax);
+    else
+      a = RM_PIO2_HI - (rm_atan01(ax / ay) - RM_PIO2_LO);
+    if (signbit(x)) a = RM_PI_HI - (a - RM_PI_LO);
+  }
+  return copysign(a, y);
+}
+
+/* acos c, c in [-1, 1] */
+static double rm_acos(double c) { return rm_atan2(sqrt((1.0 - c) * (1.0 + c)), c); }
+
 /* Box-Muller pair (the reference's libstdc++ polar method yields a pair too:
  * a[9] is its cached second value) */
 static void box_muller(double u1, double u2, double *z0, double *z1) {
-  double r = sqrt(-2.0 * log(1.0 - u1));
+  double r = sqrt(-2.0 * rm_log(1.0 - u1));
   double th = 6.283185307179586 * u2;
-  *z0 = r * cos(th);
-  *z1 = r * sin(th);
+  double s, c;
+  rm_sincos(th, &s, &c);
+  *z0 = r * c;
+  *z1 = r * s;
+}
+
+/* v (sin theta cos phi, sin theta sin phi, cos theta), theta = acos(cos_theta)
+ * (planner_class.cpp:61-73) */
+static void speed_vector(double v, double cos_theta, double phi, double *q) {
+  double theta = rm_acos(cos_theta);
+  double st, ct, sp, cp;
+  rm_sincos(theta, &st, &ct);
+  rm_sincos(phi, &sp, &cp);
+  q[3] = v * st * cp;
+  q[4] = v * st * sp;
+  q[5] = v * ct;
+}
+
+/* exported for the CPU tests of the routines (accuracy vs glibc) */
+void orc_rmath(int fn, int64_t n, const double *x, const double *y, double *out) {
+  for (int64_t i = 0; i < n; i++) {
+    double s, c;
+    switch (fn) {
+      case 0: out[i] = rm_log(x[i]); break;
+      case 1: rm_sincos(x[i], &s, &c); out[2 * i] = s; out[2 * i + 1] = c; break;
+      case 2: out[i] = rm_atan2(y[i], x[i]); break;
+      default: out[i] = rm_acos(x[i]); break;
+    }
+  }
 }
 
 /* planner_class.cpp:38-76 */
@@ -811,11 +966,8 @@ int orc_sample_state(const orc_terrain *T, uint64_t seed, uint64_t stream_id, in
     q[2] = std_max(std_min(hz, z_max_rel), z_min_rel) + orc_ground_height(T, q[0], q[1], 0);
     double phi = (2.0 * MY_PI) * u2[0];
     double cos_theta = 2.0 * u2[1] - 1.0;
-    double theta = acos(cos_theta);
     double v = u3[0] * V_MAX;
-    q[3] = v * sin(theta) * cos(phi);
-    q[4] = v * sin(theta) * sin(phi);
-    q[5] = v * cos(theta);
+    speed_vector(v, cos_theta, phi, q);
     q[6] = 2 * P_MAX * u3[1] - P_MAX;
     q[7] = 0.0;
     if (require_phase < 0) return k + 1;
@@ -975,16 +1127,13 @@ static void sample_state_direction(const orc_terrain *T, const double *s_from, c
   if (speed_direction_flag) {
     double delta_x = s_to[0] - s_from[0];
     double delta_y = s_to[1] - s_from[1];
-    phi = atan2(delta_y, delta_x);
+    phi = rm_atan2(delta_y, delta_x);
   } else {
     phi = (2.0 * MY_PI) * u2[0];
   }
   double cos_theta = 2.0 * u2[1] - 1.0;
-  double theta = acos(cos_theta);
   double v = u3[0] * V_MAX;
-  q[3] = v * sin(theta) * cos(phi);
-  q[4] = v * sin(theta) * sin(phi);
-  q[5] = v * cos(theta);
+  speed_vector(v, cos_theta, phi, q);
   q[6] = 2 * P_MAX * u3[1] - P_MAX;
   q[7] = 0.0;
 }
@@ -1033,4 +1182,365 @@ void orc_sample_actions(int64_t n, const double *normals, uint64_t seed, uint64_
   OMP_FOR
   for (int64_t i = 0; i < n; i++)
     orc_sample_action(normals + 3 * i, seed, stream_id, index_base + i, actions + 10 * i);
+}
+
+/* ==== the planner loop ========================================================
+ * The batch-synchronous RRT-Connect the engine runs (include/gbp_planner.h
+ * buildRRTConnectBatched / buildRRTConnectDevice) restated on the CPU: each
+ * half-iteration h extends tree h % 2 (Ta FORWARD, Tb REVERSE) toward B random
+ * targets against the tree as it stands when the half starts, appends the
+ * successors in target order, then connects each new vertex to the other tree
+ * (again against that tree's snapshot) and appends the connections in order.
+ * B = 1 is the reference's runRRTConnect (rrt_connect.cpp:230-314) on the
+ * engine's counter-based streams.  Every draw, decision and tree update
+ * below is the oracle's own (the functions above), nothing is read from the
+ * engine. */
+#define EXTD_STREAM 0x45585444ull /* newConfig's candidates: (extend index) * 8 + j */
+
+static void tree_put(orc_tree *t, const double *v, const double *a, int parent, double g,
+                     double y) {
+  int i = t->n++;
+  memcpy(t->v + 8 * (int64_t)i, v, 8 * sizeof(double));
+  if (a) memcpy(t->a + 10 * (int64_t)i, a, 10 * sizeof(double));
+  else memset(t->a + 10 * (int64_t)i, 0, 10 * sizeof(double));
+  t->parent[i] = parent;
+  t->g[i] = g;
+  t->y[i] = y;
+  if (t->child) {
+    t->child[i] = -1;
+    t->sibling[i] = -1;
+  }
+}
+
+/* graph_class.cpp:36-42 (the successor list kept as first-child / next-sibling) */
+static void tree_add_edge(orc_tree *t, int p, int c) {
+  const double *vp = t->v + 8 * (int64_t)p, *vc = t->v + 8 * (int64_t)c;
+  t->parent[c] = p;
+  if (t->child) {
+    t->sibling[c] = t->child[p];
+    t->child[p] = c;
+  }
+  t->g[c] = t->g[p] + orc_pose_distance(vp, vc);
+  t->y[c] = t->y[p] + orc_state_yaw_distance(vp, vc);
+}
+
+/* graph_class.cpp:44-58 */
+static void tree_remove_edge(orc_tree *t, int p, int c) {
+  if (t->parent[c] == p) t->parent[c] = -1;
+  int *link = &t->child[p];
+  while (*link >= 0 && *link != c) link = &t->sibling[*link];
+  if (*link == c) *link = t->sibling[c];
+}
+
+/* graph_class.cpp:131-138 (recursive over the successors) */
+static void tree_update_gy(orc_tree *t, int idx, double g, double y) {
+  t->g[idx] = g;
+  t->y[idx] = y;
+  for (int c = t->child ? t->child[idx] : -1; c >= 0; c = t->sibling[c]) {
+    const double *vi = t->v + 8 * (int64_t)idx, *vc = t->v + 8 * (int64_t)c;
+    tree_update_gy(t, c, t->g[idx] + orc_pose_distance(vi, vc),
+                   t->y[idx] + orc_state_yaw_distance(vi, vc));
+  }
+}
+
+/* attemptConnect's depth-0 decision only (callers that test == REACHED,
+ * rrt_star_connect.cpp:36, :59): REACHED iff t_s > KINEMATICS_RES, the
+ * cubic-Hermite action is valid and its pair check passes (rrt_connect.cpp:20-70);
+ * a_new receives the action */
+static int connect_reached(const orc_terrain *T, const double *s_existing, const double *s,
+                           double t_s, int direction, int adaptive, double *a_new,
+                           int64_t *checks) {
+  if (t_s <= KINEMATICS_RES) return 0;
+  const double *s_start = (direction == GBP_FORWARD) ? s_existing : s;
+  const double *s_goal = (direction == GBP_FORWARD) ? s : s_existing;
+  connect_action(s_start, s_goal, t_s, a_new);
+  if (!orc_is_valid_action(a_new)) return 0;
+  (*checks)++;
+  double sn[8], tn;
+  uint32_t f;
+  return (direction == GBP_FORWARD)
+             ? orc_is_valid_pair(T, s_start, a_new, GBP_FORWARD, adaptive, sn, &tn, &f, 0)
+             : orc_is_valid_pair(T, s_goal, a_new, GBP_REVERSE, adaptive, sn, &tn, &f, 0);
+}
+
+/* rrt_star_connect.cpp:18-66 for the vertex `idx` just added to t (its
+ * nearest `nn`, newConfig's action a_new): choose-parent among the vertices
+ * before it within `delta` (planner_class.cpp:173-182, ascending index), then
+ * rewire them through it */
+static void star_insert(const orc_terrain *T, orc_tree *t, int idx, int nn, const double *a_new,
+                        double delta, int direction, int adaptive, orc_plan_out *out) {
+  const double *s_new = t->v + 8 * (int64_t)idx;
+  const double *s_nearest = t->v + 8 * (int64_t)nn;
+  int nb_n = 0;
+  int *nb = (int *)malloc(sizeof(int) * (size_t)(idx > 0 ? idx : 1));
+  for (int j = 0; j < idx; j++) {
+    const double *vj = t->v + 8 * (int64_t)j;
+    if ((orc_state_distance(s_new, vj) <= delta) && orc_state_distance(s_new, vj) > 0) nb[nb_n++] = j;
+  }
+  out->connects += 2 * (int64_t)nb_n; /* a choose-parent and a rewire connect per neighbour */
+  int s_min = nn;
+  double a_sel[10], a_c[10];
+  memcpy(a_sel, a_new, sizeof a_sel);
+  double g_s_new = t->g[nn] + orc_pose_distance(s_new, s_nearest);
+  double y_s_new = t->y[nn] + orc_state_yaw_distance(s_new, s_nearest);
+  for (int i = 0; i < nb_n; i++) {
+    const int j = nb[i];
+    const double *s_near = t->v + 8 * (int64_t)j;
+    if (connect_reached(T, s_near, s_new, orc_pose_distance(s_new, s_near) / V_NOM, direction,
+                        adaptive, a_c, &out->attempts)) {
+      double g_s_near = t->g[j] + orc_pose_distance(s_near, s_new);
+      double y_s_near = t->y[j] + orc_state_yaw_distance(s_near, s_new);
+      if (g_s_near < g_s_new) {
+        memcpy(a_sel, a_c, sizeof a_sel);
+        s_min = j;
+        g_s_new = g_s_near;
+        y_s_new = y_s_near;
+      }
+    }
+  }
+  tree_add_edge(t, s_min, idx);
+  tree_update_gy(t, idx, g_s_new, y_s_new);
+  memcpy(t->a + 10 * (int64_t)idx, a_sel, sizeof a_sel);
+  for (int i = 0; i < nb_n; i++) {
+    const int j = nb[i];
+    const double *s_near = t->v + 8 * (int64_t)j;
+    /* the engine checks every neighbour's rewire connect in one batch, the
+     * parent's included (it only counts toward attempts) */
+    int reached = connect_reached(T, s_new, s_near, orc_pose_distance(s_near, s_new) / V_NOM,
+                                  direction, adaptive, a_c, &out->attempts);
+    if (j == s_min) continue;
+    if (reached &&
+        (t->g[j] > (t->g[idx] + orc_pose_distance(s_near, s_new)))) {
+      tree_remove_edge(t, t->parent[j], j);
+      tree_add_edge(t, idx, j);
+      tree_update_gy(t, j, t->g[idx] + orc_pose_distance(s_near, s_new),
+                     t->y[idx] + orc_state_yaw_distance(s_near, s_new));
+      memcpy(t->a + 10 * (int64_t)j, a_c, sizeof a_c);
+      out->rewires++;
+    }
+  }
+  free(nb);
+}
+
+int orc_plan(const orc_terrain *T, const double *start, const double *goal,
+             const orc_plan_cfg *cfg, orc_tree *tr, orc_plan_out *out) {
+  const int B = cfg->batch;
+  const int star = cfg->star;
+  if (B < 1 || !tr || !out) return -1;
+  memset(out, 0, sizeof *out);
+  out->meet_a = out->meet_b = -1;
+  for (int k = 0; k < 2; k++) {
+    tr[k].n = 0;
+    tree_put(&tr[k], k == 0 ? start : goal, 0, -1, 0.0, 0.0);
+  }
+  const uint64_t stream[2] = {cfg->stream_a, cfg->stream_b};
+  int64_t draws[2] = {0, 0};
+  int64_t ext = cfg->extend_base;
+  double *cand = (double *)malloc(sizeof(double) * 8 * (size_t)B);
+  double *tgt = (double *)malloc(sizeof(double) * 8 * (size_t)B);
+  int *added = (int *)malloc(sizeof(int) * (size_t)B);
+  int *nearest = (int *)malloc(sizeof(int) * (size_t)B);
+  double *a_ext = (double *)malloc(sizeof(double) * 10 * (size_t)B);
+  double *shared = 0; /* RRT*: (a, b) vertex pairs whose connect REACHED */
+  int64_t n_shared = 0, cap_shared = 0;
+  double cost_so_far = INFINITY;
+  int rc = 0;
+  for (int64_t h = 0; cfg->max_halves <= 0 || h < cfg->max_halves; h++) {
+    const int k = (int)(h & 1);
+    orc_tree *Tt = &tr[k], *O = &tr[k ^ 1];
+    const int dir = k == 0 ? GBP_FORWARD : GBP_REVERSE;
+    const int cdir = k == 0 ? GBP_REVERSE : GBP_FORWARD;
+    /* targets: randomState + isValidState(STANCE) (rrt_connect.cpp:248-254,
+     * :283-289); s_from / s_to as the trees stand when the half starts */
+    if (star) {
+      for (int i = 0; i < B; i++)
+        orc_sample_state(T, cfg->seed, stream[k], draws[k] + i, -1, 1, cand + 8 * i);
+    } else {
+      const double *last = Tt->v + 8 * (int64_t)(Tt->n - 1), *root = O->v;
+      orc_sample_states_dir(T, B, cfg->seed, stream[k], draws[k], cfg->state_flag, cfg->state_p,
+                            cfg->state_speed_direction, dir == GBP_FORWARD ? last : root,
+                            dir == GBP_FORWARD ? root : last, cand, 1);
+    }
+    draws[k] += B;
+    int nt = 0;
+    for (int i = 0; i < B; i++) {
+      orc_stats st = {0, 0, 0};
+      if (orc_is_valid_state(T, cand + 8 * i, GBP_STANCE, &st)) memcpy(tgt + 8 * nt++, cand + 8 * i, 64);
+    }
+    out->targets += nt;
+    out->extends += nt;
+    /* extend every target against the snapshot (rrt.cpp:77-102, planner_class.cpp:185-200) */
+    const int n0 = Tt->n;
+    if (Tt->n + nt > Tt->cap) { rc = -2; break; }
+    int n_added = 0;
+    for (int i = 0; i < nt; i++) {
+      const double *q = tgt + 8 * i;
+      const int nn = orc_nearest(Tt->v, n0, q, 0);
+      const double *s_near = Tt->v + 8 * (int64_t)nn;
+      double nrm[3], acts[60], sn[8], an[10];
+      int ood = 0, ch;
+      uint32_t cnt;
+      orc_surface_normal(T, q[0], q[1], nrm, &ood);
+      for (int j = 0; j < NUM_GEN_STATES; j++)
+        sample_action_any(nrm, dir, cfg->action_flag, cfg->action_p, q, s_near, cfg->seed,
+                          EXTD_STREAM, (ext + i) * 8 + j, acts + 10 * j);
+      const int r = orc_extend(T, s_near, q, acts, dir, cfg->adaptive, sn, an, &ch, &cnt);
+      out->attempts += ch >= 0 ? ch + 1 : NUM_GEN_STATES;
+      if (r == GBP_TRAPPED) continue;
+      const int idx = Tt->n;
+      tree_put(Tt, sn, an, -1, 0.0, 0.0);
+      if (!star) { /* rrt.cpp:86-92 */
+        tree_add_edge(Tt, nn, idx);
+        tree_update_gy(Tt, idx, Tt->g[nn] + orc_pose_distance(s_near, sn),
+                       Tt->y[nn] + orc_state_yaw_distance(s_near, sn));
+      }
+      added[n_added] = idx;
+      nearest[n_added] = nn;
+      memcpy(a_ext + 10 * n_added, an, sizeof an);
+      n_added++;
+    }
+    ext += nt;
+    if (star) {
+      for (int i = 0; i < n_added; i++)
+        star_insert(T, Tt, added[i], nearest[i], a_ext + 10 * i, cfg->star_delta, dir, cfg->adaptive,
+                    out);
+    }
+    /* connect each new vertex to the other tree (rrt_connect.cpp:98-120) */
+    const int m0 = O->n;
+    if (O->n + n_added > O->cap) { rc = -2; break; }
+    int meet = 0;
+    for (int i = 0; i < n_added; i++) {
+      const double *q = Tt->v + 8 * (int64_t)added[i];
+      const int nn = orc_nearest(O->v, m0, q, 0);
+      const double *s_ex = O->v + 8 * (int64_t)nn;
+      double sn[8] = {0}, an[10] = {0};
+      ac_stats acs = {0, 0};
+      const int r = attempt_connect_ts(T, s_ex, q, orc_pose_distance(q, s_ex) / V_NOM, sn, an, cdir,
+                                       cfg->adaptive, 0, &acs);
+      out->connects++;
+      out->depth_capped += acs.capped;
+      out->attempts += acs.checks;
+      if (r == GBP_TRAPPED) continue;
+      const int idx = O->n;
+      tree_put(O, sn, an, -1, 0.0, 0.0);
+      tree_add_edge(O, nn, idx);
+      tree_update_gy(O, idx, O->g[nn] + orc_pose_distance(s_ex, sn),
+                     O->y[nn] + orc_state_yaw_distance(s_ex, sn));
+      if (r != GBP_REACHED) continue;
+      const int va = k == 0 ? added[i] : idx, vb = k == 0 ? idx : added[i];
+      if (!meet && out->meet_a < 0) {
+        out->meet_a = va;
+        out->meet_b = vb;
+        out->meet_half = h;
+      }
+      meet = 1;
+      if (star) {
+        if (n_shared == cap_shared) {
+          cap_shared = cap_shared ? 2 * cap_shared : 64;
+          shared = (double *)realloc(shared, sizeof(double) * 2 * (size_t)cap_shared);
+        }
+        shared[2 * n_shared] = va;
+        shared[2 * n_shared + 1] = vb;
+        n_shared++;
+        out->solutions++;
+      }
+    }
+    out->halves = h + 1;
+    if (star) {
+      /* the cheapest connection so far with the current g values, ranked after
+       * each pair of halves (include/gbp_planner.h buildRRTStarConnectBatched) */
+      if (k == 1) {
+        for (int64_t i = 0; i < n_shared; i++) {
+          const int sa = (int)shared[2 * i], sb = (int)shared[2 * i + 1];
+          const double c = tr[0].g[sa] + tr[1].g[sb];
+          if (c < cost_so_far) {
+            cost_so_far = c;
+            out->best_a = sa;
+            out->best_b = sb;
+          }
+        }
+      }
+      continue;
+    }
+    if (meet) {
+      out->found = 1;
+      break;
+    }
+  }
+  out->ext_counter = ext;
+  out->draws_a = draws[0];
+  out->draws_b = draws[1];
+  if (star) {
+    out->found = n_shared > 0;
+    out->best_cost = cost_so_far;
+  } else if (out->found) {
+    out->path_length = tr[0].g[out->meet_a] + tr[1].g[out->meet_b];
+    out->path_yaw = tr[0].y[out->meet_a] + tr[1].y[out->meet_b];
+  }
+  free(cand);
+  free(tgt);
+  free(added);
+  free(nearest);
+  free(a_ext);
+  free(shared);
+  return rc;
+}
+
+/* std::array<double, 8> == (element-wise double ==) */
+static int state_equal(const double *a, const double *b) {
+  for (int k = 0; k < 8; k++)
+    if (!(a[k] == b[k])) return 0;
+  return 1;
+}
+
+/* rrt_connect.cpp:139-227: greedy shortcutting from the start — connect s to
+ * the farthest later state that attemptConnect(FORWARD) REACHES; when none
+ * does, step to the next state with its original action and add to
+ * path_cost_ but not to path_length_ (the reference's quirk, :202-215).
+ * Returns the new number of states (<= n). */
+int orc_post_process_path(const orc_terrain *T, int n, const double *states,
+                          const double *actions, int adaptive, double *out_states,
+                          double *out_actions, double *path_length, double *path_yaw,
+                          double *path_cost) {
+  double s[8], s_goal[8], a_new[10] = {0};
+  memcpy(s, states, sizeof s);
+  memcpy(s_goal, states + 8 * (int64_t)(n - 1), sizeof s_goal);
+  int m = 1;
+  memcpy(out_states, s, sizeof s);
+  double len = 0, yaw = 0, cost = 0;
+  while (!state_equal(s, s_goal)) {
+    int last = n - 1; /* s_next = state_sequence_copy.back() */
+    int old = -1;
+    for (;;) {
+      const double *s_next = states + 8 * (int64_t)last;
+      double dummy[8] = {0};
+      const int r = orc_attempt_connect(T, s, s_next, 0.0, dummy, a_new, GBP_FORWARD, adaptive);
+      if (r == GBP_REACHED || state_equal(s, s_next)) break;
+      old = last;
+      last--;
+    }
+    const double *s_next = states + 8 * (int64_t)last;
+    if (!state_equal(s, s_next)) {
+      memcpy(out_states + 8 * (int64_t)m, s_next, 64);
+      memcpy(out_actions + 10 * (int64_t)(m - 1), a_new, 80);
+      m++;
+      const double dl = orc_pose_distance(s, s_next), dy = orc_state_yaw_distance(s, s_next);
+      len += dl;
+      yaw += dy;
+      cost += dl;
+      memcpy(s, s_next, sizeof s);
+    } else {
+      const double *s_old = states + 8 * (int64_t)old;
+      memcpy(out_states + 8 * (int64_t)m, s_old, 64);
+      memcpy(out_actions + 10 * (int64_t)(m - 1), actions + 10 * (int64_t)(old - 1), 80);
+      m++;
+      const double dl = orc_pose_distance(s, s_old);
+      cost += dl;
+      memcpy(s, s_old, sizeof s);
+    }
+  }
+  if (path_length) *path_length = len;
+  if (path_yaw) *path_yaw = yaw;
+  if (path_cost) *path_cost = cost;
+  return m;
 }

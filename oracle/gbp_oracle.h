@@ -146,6 +146,55 @@ void orc_sample_actions_dir(int64_t n, const double *normals, const double *s,
                             int action_flag, double action_p, uint64_t seed, uint64_t stream_id,
                             int64_t index_base, double *actions, int nthreads);
 
+/* ---- the planner loop (batch-synchronous RRT-Connect / RRT*-Connect) ---- */
+typedef struct {
+  int cap;          /* rows of every array below                          */
+  int n;            /* vertices (set by orc_plan)                         */
+  double *v;        /* [cap][8] states                                    */
+  double *a;        /* [cap][10] the action reaching each vertex (root 0) */
+  int32_t *parent;  /* [cap] (root -1)                                    */
+  double *g, *y;    /* [cap] cost / yaw to come (graph_class.cpp:36-42)   */
+  int32_t *child, *sibling; /* [cap] successor lists (RRT* rewiring), may be NULL for RRT-Connect */
+} orc_tree;
+
+typedef struct {
+  int batch;                 /* targets per half-iteration (1 = runRRTConnect)        */
+  uint64_t seed, stream_a, stream_b; /* the trees' target streams                     */
+  int adaptive;              /* adaptive-step pair checks (params.yaml:16)             */
+  int state_flag, state_speed_direction, action_flag; /* gbp_sampling                 */
+  double state_p, action_p;
+  int64_t extend_base;       /* the first extend's index on the candidate stream       */
+  int64_t max_halves;        /* stop after this many half-iterations (<= 0: at a solution) */
+  int star;                  /* RRT*-Connect: choose-parent + rewire, runs max_halves  */
+  double star_delta;         /* rrt_star_connect.h:59 (3.0)                            */
+} orc_plan_cfg;
+
+typedef struct {
+  int found;
+  int meet_a, meet_b;        /* RRT-Connect: the vertices the first REACHED connect joined */
+  int64_t meet_half, halves;
+  int64_t targets, extends, attempts, connects, depth_capped, rewires, solutions;
+  int64_t ext_counter, draws_a, draws_b;
+  double path_length, path_yaw;  /* g / y of the meeting vertices (rrt_connect.cpp:304-313) */
+  int best_a, best_b;        /* RRT*: the cheapest connection ranked after each iteration */
+  double best_cost;
+} orc_plan_out;
+
+/* tr[0] = Ta (start, FORWARD), tr[1] = Tb (goal, REVERSE); returns 0, -1 (bad
+ * arguments) or -2 (a tree's capacity is exhausted) */
+int orc_plan(const orc_terrain *T, const double *start, const double *goal,
+             const orc_plan_cfg *cfg, orc_tree *tr, orc_plan_out *out);
+/* rrt_connect.cpp:139-227 (FORWARD attemptConnect, cost without yaw terms);
+ * out_states[n][8], out_actions[n-1][10]; returns the new state count */
+int orc_post_process_path(const orc_terrain *T, int n, const double *states,
+                          const double *actions, int adaptive, double *out_states,
+                          double *out_actions, double *path_length, double *path_yaw,
+                          double *path_cost);
+
+/* the samplers' reproducible transcendentals (restating gbp_device.h rm_*):
+ * fn 0 log(x), 1 sincos(x) -> out[2n] (sin, cos), 2 atan2(y, x), 3 acos(x) */
+void orc_rmath(int fn, int64_t n, const double *x, const double *y, double *out);
+
 #ifdef __cplusplus
 }
 #endif

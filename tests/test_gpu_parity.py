@@ -213,12 +213,13 @@ def test_samplers_match_oracle(gpu, name):
     g, gt = T.sample_states(n, 31, 1, 0, require_phase=L.STANCE, max_tries=256)
     r, rt = O.sample_states(n, 31, 1, 0, L.STANCE, 256, nthreads=8)
     assert np.array_equal(np_(gt), rt)  # same accepted draw for every index
-    np.testing.assert_allclose(np_(g), r, rtol=1e-12, atol=1e-12)
+    # the samplers' transcendentals are the engine's reproducible rm_* routines,
+    # restated by the oracle: every draw is bit-identical
+    assert np.all(same_f64(np_(g), r))
     nrm = O.normal_batch(r[:, :2])[0]
     ga = T.sample_actions(torch.from_numpy(nrm), 31, 3)
     ra = oracle.sample_actions(nrm, 31, 3)
-    np.testing.assert_allclose(np_(ga), ra, rtol=1e-12, atol=1e-12)
-    assert np.array_equal(np_(ga)[:, 6], ra[:, 6]) and np.array_equal(np_(ga)[:, 7], ra[:, 7])
+    assert np.array_equal(bits(np_(ga)), bits(ra))
 
 
 # ---- extend -------------------------------------------------------------------------

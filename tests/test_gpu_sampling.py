@@ -11,9 +11,9 @@ global_body_planner.cpp:193-205) on the engine, against the oracle.
   * the device planner loop with both flags on builds the same trees as the
     host batched planner, and the node's buildRRTConnect plans with them.
 
-Samplers use device atan2 / acos / sin / cos / log: compared at rtol 1e-12
-(the tolerance of the plain samplers, tests/test_gpu_parity.py); the coin
-(Philox) and every branch it selects are exact.
+The samplers' log / sin / cos / acos / atan2 are the engine's reproducible
+routines (gbp_device.h rm_*, restated by the oracle): every draw is compared
+bit for bit, as are the coin (Philox) and the branch it selects.
 """
 import numpy as np
 import pytest
@@ -55,9 +55,7 @@ def test_state_direction_sampler_matches_oracle(gpu, speed):
     g = np_(T.sample_states_dir(n, 31, 7, S_FROM, S_TO, index_base=5, cfg=cfg))
     r = O.sample_states_dir(n, 31, 7, S_FROM, S_TO, index_base=5, state_p=0.5,
                             speed_direction=speed, nthreads=8)
-    np.testing.assert_allclose(g, r, rtol=1e-12, atol=1e-12)
-    # x and y come from multiplications of exact uniforms: bit-exact on both branches
-    assert np.array_equal(bits(g[:, :2]), bits(r[:, :2]))
+    assert np.all(same_f64(g, r))
     # the coin picks the rectangle about half the time (plain draws cover the map)
     inside = ((g[:, 0] >= 1.0) & (g[:, 0] <= 4.02) & (g[:, 1] >= 1.10) & (g[:, 1] <= 2.55))
     plain, _ = T.sample_states(n, 31, 7, 5)
@@ -84,8 +82,7 @@ def test_action_direction_sampler_matches_oracle(gpu):
     ga = np_(T.sample_actions_dir(torch.from_numpy(nrm), torch.from_numpy(target),
                                   torch.from_numpy(s_near), torch.from_numpy(d), 31, 3, cfg=cfg))
     ra = oracle.sample_actions_dir(nrm, target, s_near, d, 31, 3, action_p=0.5, nthreads=8)
-    np.testing.assert_allclose(ga, ra, rtol=1e-12, atol=1e-12)
-    assert np.array_equal(ga[:, 6], ra[:, 6]) and np.array_equal(ga[:, 7], ra[:, 7])
+    assert np.array_equal(bits(ga), bits(ra))
     plain = np_(T.sample_actions(torch.from_numpy(nrm), 31, 3))
     moved = np.any(bits(ga) != bits(plain), axis=1)
     assert 0.45 < moved.mean() < 0.55, moved.mean()
@@ -95,7 +92,7 @@ def test_action_direction_sampler_matches_oracle(gpu):
     fa = np_(T.sample_actions_dir(torch.from_numpy(up), torch.from_numpy(target),
                                   torch.from_numpy(s_near), torch.from_numpy(d), 31, 3, cfg=cfg))
     fr = oracle.sample_actions_dir(up, target, s_near, d, 31, 3, action_p=0.5, nthreads=8)
-    np.testing.assert_allclose(fa, fr, rtol=1e-12, atol=1e-12)
+    assert np.array_equal(bits(fa), bits(fr))
     fwd = d == L.FORWARD
     dv = np.where(fwd[:, None], target[:, 3:5] - s_near[:, 3:5], s_near[:, 3:5] - target[:, 3:5])
     sgn = np.where(dv > 0, 1.0, -1.0)

@@ -61,6 +61,22 @@ def main(out=os.path.join(ROOT, "tests", "golden", "oracle_vectors.npz")):
         arrays.update({p + "ext_s_near": s[:m], p + "ext_target": tgt[:m], p + "ext_cand": cand,
                        p + "ext_dir": d[:m], p + "ext_result": r, p + "ext_chosen": ch,
                        p + "ext_s_new": sn, p + "ext_a_new": an, p + "ext_counts": c})
+    # the planner loop (orc_plan): batch 8, synth-256's config-2 pair, 400 halves
+    from global_body_planner_amd import planner
+    data = td.by_name("synth-rough-256")
+    O = oracle.OracleTerrain.from_data(data)
+    oracle.set_scan_mode(1)
+    hs, _ = O.ground_height(1.0, 2.55)
+    hg, _ = O.ground_height(4.02, 2.55)
+    start, goal = planner.start_goal_state(hs, 1.0, 2.55), planner.start_goal_state(hg, 4.02, 2.55)
+    r = O.plan(start, goal, batch=8, seed=5, max_halves=400)
+    arrays["loop/start"], arrays["loop/goal"] = start, goal
+    arrays["loop/counters"] = np.array([r[k] for k in ("found", "meet_a", "meet_b", "halves",
+                                                        "targets", "attempts", "connects")])
+    for t in "ab":
+        for k in ("v", "act", "parent", "g", "y"):
+            arrays[f"loop/{t}_{k}"] = r[t][k]
+    oracle.set_scan_mode(0)
     rng = np.random.default_rng(9)
     verts = rng.normal(size=(3000, 8))
     verts[11] = verts[5]
