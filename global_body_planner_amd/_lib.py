@@ -24,7 +24,7 @@ F_STAGE_MASK = 0xF << F_STAGE_SHIFT
 STORAGE_AUTO, STORAGE_F32, STORAGE_F64 = 0, 1, 2
 OPT_KERNEL, OPT_BLOCK, OPT_WAVES, OPT_LDS_COORDS, OPT_HELPERS = 1, 2, 4, 5, 8
 OPT_AFFINE_COORDS, OPT_COORD_MODE, OPT_XCD_MAP, OPT_FAST_RCP, OPT_FRAGILE_EPS = 9, 10, 13, 14, 15
-OPT_NN_INDEX, OPT_NN_FILTER, OPT_NN_STATS = 16, 17, 18
+OPT_NN_STATS = 18
 PLAN_HALT_TARGETS, PLAN_HALT_EXTEND, PLAN_HALT_CONNECT = 1, 2, 4
 KERNEL_DIRECT, KERNEL_PERSISTENT = 0, 1
 
@@ -52,7 +52,6 @@ EXPORTS = [
     "gbp_plan_halves_dev",
     "gbp_plan_status_read", "gbp_plan_resolve_host", "gbp_extend_tree_dev",
     "gbp_extend_tree_finish_dev", "gbp_extend_tree_host", "gbp_tree_nearest_dev",
-    "gbp_tree_index_build", "gbp_tree_index_size",
 ]
 
 
@@ -155,8 +154,6 @@ def load(path=None):
         "gbp_extend_tree_finish_dev": (I, [P, P, P, I64, I, P, P, P]),
         "gbp_extend_tree_host": (I, [P, P, P, I64, P, I, I, U64, I64, P, P, P]),
         "gbp_tree_nearest_dev": (I, [P, P, I64, P, P, P]),
-        "gbp_tree_index_build": (I, [P, P, P]),
-        "gbp_tree_index_size": (I, [P, P]),
         "gbp_nearest_batch_dev": (I, [I64, P, I64, P, P, P, P]),
         "gbp_nearest_batch_host": (I, [I64, P, I64, P, P, P]),
         "gbp_neighbors_batch_dev": (I, [I64, P, I64, P, ctypes.c_double, I, P, P, P]),

@@ -1044,19 +1044,8 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
     case GBP_OPT_FAST_RCP:
       t->opt_fast_rcp = value ? 1 : 0;
       return GBP_OK;
-    case GBP_OPT_NN_INDEX:  // the smallest indexed tree the planner searches through
-      if (value < 0 || value > 0x7FFFFFFF) return GBP_E_INVALID_ARG;
-      t->opt_nn_index = value;
-      return GBP_OK;
-    case GBP_OPT_NN_FILTER:  // 0 matrix cores (k_nn_mfma), 1 packed fp32 (k_nn_filter)
-      if (value < 0 || value > 1) return GBP_E_INVALID_ARG;
-      t->opt_nn_filter = (int)value;
-      return GBP_OK;
     case GBP_OPT_NN_STATS:
       t->opt_nn_stats = value ? 1 : 0;
-      return GBP_OK;
-    case GBP_OPT_PLAN_OVERLAP:
-      t->opt_plan_overlap = value ? 1 : 0;
       return GBP_OK;
     case GBP_OPT_FRAGILE_EPS:  // in 1e-15 units; never below the default margin
       if (value < 1000 || value > 1000000000000000LL) return GBP_E_INVALID_ARG;
@@ -1079,10 +1068,7 @@ int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value) {
     case GBP_OPT_AFFINE_COORDS: *value = t->opt_affine; return GBP_OK;
     case GBP_OPT_XCD_MAP: *value = t->opt_xcd_map; return GBP_OK;
     case GBP_OPT_FAST_RCP: *value = t->opt_fast_rcp ? (t->rcp_seed != 0.0 ? 1 : 0) : 0; return GBP_OK;
-    case GBP_OPT_NN_INDEX: *value = t->opt_nn_index; return GBP_OK;
-    case GBP_OPT_NN_FILTER: *value = t->opt_nn_filter; return GBP_OK;
     case GBP_OPT_NN_STATS: *value = t->opt_nn_stats; return GBP_OK;
-    case GBP_OPT_PLAN_OVERLAP: *value = t->opt_plan_overlap; return GBP_OK;
     case GBP_OPT_FRAGILE_EPS: *value = (int64_t)std::llround(t->fragile_eps * 1e15); return GBP_OK;
     case GBP_OPT_COORD_MODE:  // what the validate kernel of the current options uses
       *value = validate_coord_mode(t, t->opt_kernel == GBP_KERNEL_DIRECT);

@@ -40,10 +40,7 @@ struct gbp_terrain {
   double rcp_seed = 0;              // verified_rcp_seed (0: every spacing pair not exact)
   double fragile_eps = gbp::FRAGILE_EPS;  // GBP_OPT_FRAGILE_EPS (>= the default)
   int64_t opt_xcd_map = 0;          // persistent kernel: slices numbered XCD-major
-  int opt_nn_filter = 0;
-  int opt_nn_stats = 0;
-  int opt_plan_overlap = 0;         // gbp_plan_halves_dev: next half's draws on a second stream             // 1: the matrix-core NN search counts its fp64 re-checks            // planner NN: 0 matrix-core fp16-split filter, 1 packed fp32 filter
-  int64_t opt_nn_index = 0;         // planner: trees this large search through their index (0: off)
+  int opt_nn_stats = 0;             // 1: the matrix-core NN search counts its fp64 re-checks
   gbp_sampling sampling{};          // direction-biased sampling (gbp_terrain_set_sampling), off
   int affine = 0;                   // host-verified affine coordinates (both axes)
   int bx = 0, by = 0;
@@ -140,9 +137,3 @@ int gbp_internal_validate_dev_n(gbp_terrain *t, int64_t n_max, const int *n_dev,
                                 uint8_t *valid, double *s_new, double *t_new, uint32_t *flags,
                                 uint32_t *counts, hipStream_t st);
 
-// stable device radix sort of (key, value) pairs by the full 32-bit key
-// (rocPRIM, gbp_sort.hip); temp == nullptr: *temp_bytes receives the scratch
-// size for n pairs
-int gbp_internal_sort_pairs_u32(void *temp, size_t *temp_bytes, const uint32_t *keys_in,
-                                uint32_t *keys_out, const int32_t *vals_in, int32_t *vals_out,
-                                int64_t n, hipStream_t s);

@@ -16,7 +16,6 @@
 //                               same launch draw newConfig's 6 candidate actions
 //                               (rrt.cpp:25-50; k_extend_prep when they are
 //                               direction-biased), the reduce copies s_near
-//                               (GBP_OPT_NN_FILTER 1: k_nn_filter/k_nn_reduce)
 //            k_validate_persistent (gbp_engine.hip)  the candidates' pair checks
 //            k_select           newConfig's first valid candidate + acceptance (rrt.cpp:52-68)
 //   stage 3  k_append          non-TRAPPED successors appended to T in target order
@@ -67,29 +66,12 @@ struct gbp_tree {
   int device = 0;
   int64_t cap = 0;
   double *v = nullptr;        // [cap][8] vertex states (GraphClass vertices)
-  float *vf = nullptr;        // [(cap+1)/2][18] fp32 row pairs (nearest-neighbour filter, nn_put_row)
-  float *vmax = nullptr;      // [8] max |fl32(v[j][k])| over the vertices (NaN skipped)
   _Float16 *vh = nullptr;     // [cap][NH_ROW] fp16 split rows (matrix-core search, nn_put_hrow)
   float *hm = nullptr;        // [16]: [0, 8) max |64 v[j][k]|, [8] (bits) 1 = a row outside fp16
   double *a = nullptr;        // [cap][10] the action that reached each vertex
   double *g = nullptr;        // [cap] cost to come: g[parent] + poseDistance
   int32_t *parent = nullptr;  // [cap], -1 at the root
   int32_t *count = nullptr;   // [1] number of vertices (device resident)
-  // nearest-neighbour index (gbp_tree_index_build, k_nn_pruned): the first
-  // idx_n vertices sorted by the Morton key of (x, y), chunks of NN_CH rows
-  // with 8-D boxes of their fp32 rows and a representative (middle) row each
-  int32_t idx_n = 0;          // vertices indexed (even; 0: no index)
-  int64_t idx_cap = 0;        // rows the index arrays hold
-  float *isp = nullptr;       // [idx_cap/2][NN_PAIR] indexed rows in key order (row pairs)
-  int32_t *isid = nullptr;    // [idx_cap] vertex index of sorted row p
-  double *isv = nullptr;      // [idx_cap][8] the fp64 vertices in key order (exact stage)
-  float *ibox = nullptr;      // [idx_cap/NN_CH + 1][16] chunk boxes: lo[8], hi[8]
-  float *imed = nullptr;      // [idx_cap/NN_CH/2 + 1][NN_PAIR] each chunk's middle row
-  uint32_t *ikey = nullptr;   // [2 idx_cap] sort keys in / out
-  int32_t *ival = nullptr;    // [idx_cap] sort values in (out: isid)
-  void *isort = nullptr;      // radix-sort scratch
-  size_t isort_bytes = 0;
-  double ibounds[4] = {0, 1, 0, 1};  // the keys' (x, y) quantisation box (also the queries')
 };
 
 struct gbp_plan_ws {
@@ -100,10 +82,7 @@ struct gbp_plan_ws {
   unsigned long long *tiles = nullptr;  // look-back tile states
   uint32_t epoch = 0;          // per-compaction tag of the tile states
   uint64_t seq = 0;            // launch sequence number of the planner kernels (gated())
-  int nn_mode = 0;             // GBP_OPT_NN_FILTER of the last terrain that enqueued (0: k_nn_mfma)
   int nn_stats = 0;            // GBP_OPT_NN_STATS: k_nn_hreduce counts its re-checks in the status
-  hipStream_t aux = nullptr;   // gbp_plan_halves_dev: the next half's draws
-  hipEvent_t ev_a = nullptr, ev_b = nullptr;  // stage 3 of half h done / draws of h + 1 done
   int64_t ntiles = 0;
   // stage 0-1
   double *cand = nullptr;      // [bmax][8] drawn states
@@ -132,10 +111,6 @@ struct gbp_plan_ws {
   // nearest-neighbour partials: NN_MAX_CHUNKS * bmax slots, pd[c * nq + qi]
   double *nn_d = nullptr;
   int32_t *nn_i = nullptr;
-  // indexed search (k_nnq_*, k_nn_pruned): queries bucketed by Morton cell
-  int32_t *bcnt = nullptr;     // [NN_QCELLS] queries per Morton cell (zeroed after each search)
-  int32_t *bq = nullptr;       // [NN_QCELLS][bmax] each cell's query indices
-  float *qpt = nullptr;        // [bmax] per query: the chunk-pruning threshold
   void *block = nullptr;       // the one allocation all of the above live in
 };
 
@@ -272,396 +247,20 @@ __global__ __launch_bounds__(TB) void k_targets(TerrainView<ZT> T, gbp_plan_stat
   }
 }
 
-// ============================================================================
-// nearest neighbour in a device tree (planner_class.cpp:185-200)
-// ============================================================================
-// Work item (query tile qt, vertex chunk c): 512 queries (two per lane)
-// against the chunk's vertices; best (distance, index) per query and chunk go
-// to the partial arrays (chunk size and count set on the device from the
-// query and tree sizes, nn_geometry).
-//
-// The exact answer (stateDistance in fp64, planning_utils.cpp:116-127, the
-// lowest index among equal distances) is found through an fp32 filter in the
-// dot-product form:
-//   pass 1  B = min_j S_j over the chunk, S_j = n_j - 2 g.f_j: f_j = fl32(v_j)
-//           and n_j = fl32(|f_j|^2) from the tree's row pairs (nn_put_row),
-//           g = fl32(q); |g|^2 + S_j is the fp32-space squared distance.  Two
-//           rows are interleaved by component, so one packed FMA with the row
-//           pair as its SGPR operand advances both: 4 packed FMAs + half a
-//           v_min3_f32 per row (the difference form took 4 subtractions + 4
-//           FMAs + 1 add + a compare and select);
-//   pass 2  the same S_j again; j is recorded as a candidate iff S_j <= T(B)
-//           (tested once per block of rows on the wave's ballot: with the
-//           final minimum the threshold is tight, so almost no block holds
-//           a candidate in any lane);
-//   exact   stateDistance in fp64 for the candidates; the smallest
-//           (distance, index) pair wins, which is the reference's ascending
-//           scan with strict < (the first index reaching the minimum).
-// Why no minimiser is lost (u = 2^-24, M_k = tree.vmax[k] >= max_j |f_jk|,
-// R^2 = sum_k (M_k + |g_k|)^2, P_j = |f_j - g|^2 exactly, D_j = |v_j - q|):
-//   * the 8-FMA chain from n_j and the fp64-summed, fp32-rounded n_j put
-//     S_j + |g|^2 within eps = 10 u R^2 of P_j (gamma_8 (n_j + 2 sum|g_k f_jk|)
-//     + 1.01 u |f_j|^2 <= 9.1 u R^2);
-//   * |sqrt(P_j) - D_j| <= |f_j - v_j| + |g - q| <= del = 2 u R;
-//   * the fp64 minimiser j* has D_j* <= D_i (1 + 3e-15) for every i.
-// With i0 the pass-1 argmin, r0 = sqrt(max(0, B + |g|^2 + eps)) bounds
-// sqrt(P_i0), so sqrt(P_j*) <= r1 = (r0 + del)(1 + 4e-15) + del and
-// S_j* <= r1^2 - |g|^2 + eps = T(B) (evaluated in fp64, rounded up to fp32):
-// j* is recorded, and so is every index tying with it.  The bound assumes
-// |v|, |q| < 1e15 (no fp32 overflow of the squares); a wave with a query or
-// tree outside that, or with more than NN_CAND candidates in a lane, scans
-// the chunk in fp64 instead (ascending, strict <).  eps is ~1e-3 m^2 on the
-// planner's maps against nearest distances of metres: one or two candidates.
-// Measured alternatives (profiles/r02h_nn_filter.txt, r02j_nn_dot.txt:
-// double-buffered row loads, other item counts, a best-block pass 2 were
-// neutral or slower in the dot form): one pass with a running
-// threshold (a branch per row: slower, and insertion-order trends make the
-// running minimum fall slowly), bit-reversed visiting orders (scattered
-// scalar loads), double-buffered scalar loads, two queries per lane, rows
-// staged in LDS (every broadcast row read still moves 64 x 32 B through the
-// LDS port) or fed through v_readlane: all between 1.0x and 1.9x slower.
-constexpr int NN_CAND = 8;
-// floats per row pair: [2k + (j & 1)] component k of rows 2p, 2p+1 (k < 8),
-// [16 + (j & 1)] their fp32 squared norms
-constexpr int NN_PAIR = 18;
-
-typedef float nnf2 __attribute__((ext_vector_type(2)));
-
-// Vertex chunk size and count for nq queries against nv vertices: enough
-// (query tile, chunk) items to occupy the GPU (`items`, 2048), chunks of at least 64
-// rows, and at most NN_MAX_CHUNKS * bmax partial slots (pd[c * nq + qi]).  A
-// handful of queries (the connect stage's new vertices) thus still spreads
-// over hundreds of chunks instead of scanning the tree serially.  Chunks
-// start at even rows (whole row pairs).
-__device__ __forceinline__ void nn_geometry(int64_t nq, int64_t nv, int64_t bmax, int64_t qts,
-                                            int64_t items, int64_t &ch, int64_t &nch) {
-  const int64_t nqt = nq > 0 ? (nq + qts - 1) / qts : 1;
-  const int64_t want = (items + nqt - 1) / nqt;
-  ch = (((nv + want - 1) / want) + 63) & ~(int64_t)63;
-  if (ch < 64) ch = 64;
-  const int64_t slots = (NN_MAX_CHUNKS * bmax) / (nq > 0 ? nq : 1);  // chunks per query
-  const int64_t ch_min = (nv + slots - 1) / slots;
-  if (ch < ch_min) ch = (ch_min + 63) & ~(int64_t)63;
-  nch = nv > 0 ? (nv + ch - 1) / ch : 1;
-}
-
-// the filter's row j: fl32 of the state and the fp32 rounding of its fp64
-// squared norm (each fl32 square is exact in fp64)
-__device__ __forceinline__ void nn_put_row(float *__restrict__ vp, int64_t j, const double *s) {
-  float *b = vp + NN_PAIR * (j >> 1) + (j & 1);
-  double n = 0.0;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const float f = (float)s[k];
-    b[2 * k] = f;
-    n = n + (double)f * (double)f;
-  }
-  b[16] = (float)n;
-}
-
 // stateDistance(q, vertex j) exactly as the reference evaluates it
+// (planning_utils.cpp:116-127): the exact stage of every search below
 __device__ __forceinline__ double nn_dist64(const double qq[8], const double *vj) {
   double sum = 0;
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     const double d = vj[k] - qq[k];
-    sum = sum + 1.0 * d * d;  // planning_utils.cpp:116-127
+    sum = sum + 1.0 * d * d;
   }
   return sqrt(sum);
 }
 
-// the fp64 scan of vertices [j0, j1), ascending, strict < (getNearestNeighbor);
-// rows by scalar loads, UNR in flight (full blocks carry no bounds test, so
-// the compiler cannot sink a row's load under one)
-template <int UNR>
-__device__ __forceinline__ void nn_scan64(const double qq[8], const double *__restrict__ v, int j0,
-                                          int j1, double &best, int &bi) {
-  auto body = [&](int jb, int m) {
-    double vv[UNR][8];
-#pragma unroll
-    for (int r = 0; r < UNR; r++) {
-      if (r >= m) break;
-      const double *vj = v + 8 * (int64_t)__builtin_amdgcn_readfirstlane(jb + r);
-#pragma unroll
-      for (int k = 0; k < 8; k++) vv[r][k] = vj[k];
-    }
-#pragma unroll
-    for (int r = 0; r < UNR; r++) {
-      if (r >= m) break;
-      const double d = nn_dist64(qq, vv[r]);
-      if (d < best) {
-        best = d;
-        bi = jb + r;
-      }
-    }
-  };
-  int jb = j0;
-  for (; jb + UNR <= j1; jb += UNR) body(jb, UNR);
-  for (; jb < j1; jb++) body(jb, 1);
-}
-
-// T(B) above; g2 = |g|^2, r2 = R^2
-__device__ __forceinline__ float nn_threshold(float B, double g2, double r2) {
-  const double eps = 10.0 * 0x1p-24 * r2, del = 2.0 * 0x1p-24 * sqrt(r2);
-  const double r0 = sqrt(fmax(0.0, (double)B + g2 + eps));
-  const double r1 = (r0 + del) * (1.0 + 4e-15) + del;
-  return nextafterf((float)(r1 * r1 * (1.0 + 1e-12) - g2 + eps), INFINITY);
-}
-
-// UNR consecutive row pairs from pair pb, one contiguous scalar load
-template <int UNR>
-__device__ __forceinline__ void nn_load_pairs(const float *__restrict__ vp, int pb,
-                                              float (&rv)[UNR][NN_PAIR]) {
-  const float *b = vp + NN_PAIR * (int64_t)__builtin_amdgcn_readfirstlane(pb);
-#pragma unroll
-  for (int r = 0; r < UNR; r++)
-#pragma unroll
-    for (int c = 0; c < NN_PAIR; c++) rv[r][c] = b[NN_PAIR * r + c];
-}
-
-// S of both rows of a pair: a = -2 g
-__device__ __forceinline__ nnf2 nn_s2(const float (&a)[8], const float (&rv)[NN_PAIR]) {
-  nnf2 acc = {rv[16], rv[17]};
-#pragma unroll
-  for (int k = 0; k < 8; k++)
-    acc = __builtin_elementwise_fma(nnf2{rv[2 * k], rv[2 * k + 1]}, nnf2{a[k], a[k]}, acc);
-  return acc;
-}
-
-// Rows [j0, j1), j0 even, as row pairs in blocks of UNR (then pair by pair; an
-// odd j1 leaves its last row alone in a pair, whose partner is masked).
-// MODE 0: B = min S (selects, no branch); MODE 1: record the rows with
-// S <= T, tested once per block on the wave's ballot (the threshold is tight,
-// so a block almost never holds a candidate in any lane).
-template <int UNR, int MODE, int QPL>
-__device__ __forceinline__ void nn_sweep(const float (&a)[QPL][8], const float *__restrict__ vp,
-                                         int j0, int j1, float (&B)[QPL], const float (&T)[QPL],
-                                         int (&cnt)[QPL], int32_t (*cand)[NN_CAND][TB]) {
-  auto proc = [&](int pb, auto &rv, bool lone) {
-    constexpr int M = sizeof(rv) / sizeof(rv[0]);
-    nnf2 S[QPL][M];
-#pragma unroll
-    for (int u = 0; u < QPL; u++)
-#pragma unroll
-      for (int r = 0; r < M; r++) S[u][r] = nn_s2(a[u], rv[r]);
-    if (lone)  // past j1: never < B, never <= T
-#pragma unroll
-      for (int u = 0; u < QPL; u++) S[u][M - 1].y = __builtin_nanf("");
-    // minNum (v_min3_f32 over a pair): a NaN row is skipped, as the
-    // reference's strict < skips it; the sign of a zero minimum is immaterial
-    // to T(B)
-    if (MODE == 0) {
-#pragma unroll
-      for (int u = 0; u < QPL; u++)
-#pragma unroll
-        for (int r = 0; r < M; r++) B[u] = fminf(fminf(B[u], S[u][r].x), S[u][r].y);
-    } else {
-      bool hit = false;
-#pragma unroll
-      for (int u = 0; u < QPL; u++) {
-        float m = S[u][0].x;
-#pragma unroll
-        for (int r = 0; r < M; r++) m = fminf(fminf(m, S[u][r].x), S[u][r].y);
-        hit = hit || m <= T[u];
-      }
-      if (__ballot(hit)) {
-#pragma unroll
-        for (int u = 0; u < QPL; u++)
-#pragma unroll
-          for (int r = 0; r < M; r++) {
-            if (S[u][r].x <= T[u]) {
-              if (cnt[u] < NN_CAND) cand[u][cnt[u]][threadIdx.x] = 2 * (pb + r);
-              cnt[u]++;
-            }
-            if (S[u][r].y <= T[u]) {
-              if (cnt[u] < NN_CAND) cand[u][cnt[u]][threadIdx.x] = 2 * (pb + r) + 1;
-              cnt[u]++;
-            }
-          }
-      }
-    }
-  };
-  auto block = [&](int pb, auto m_tag, bool lone) {
-    constexpr int M = decltype(m_tag)::value;
-    float rv[M][NN_PAIR];
-    nn_load_pairs<M>(vp, pb, rv);
-    proc(pb, rv, lone);
-  };
-  const int pf = j1 >> 1;  // full pairs [j0/2, pf)
-  int pb = j0 >> 1;
-  for (; pb + UNR <= pf; pb += UNR) block(pb, std::integral_constant<int, UNR>{}, false);
-  for (; pb < pf; pb++) block(pb, std::integral_constant<int, 1>{}, false);
-  if (j1 & 1) block(pf, std::integral_constant<int, 1>{}, true);
-}
-
-// QPL queries per lane (tile of TB * QPL queries): each row pair loaded once
-// feeds QPL queries' FMAs, halving the scalar-load bytes per VALU instruction
-template <int UNR, int QPL>
-__global__ __launch_bounds__(TB) void k_nn_filter(const gbp_plan_status *__restrict__ st,
-                                                  const int32_t *__restrict__ nq_dev,
-                                                  const double *__restrict__ q,
-                                                  const int32_t *__restrict__ q_off_dev,
-                                                  const double *__restrict__ v,
-                                                  const float *__restrict__ vp,
-                                                  const float *__restrict__ vmax,
-                                                  const int32_t *__restrict__ nv_dev, int64_t bmax,
-                                                  int items, double *__restrict__ pd,
-                                                  int32_t *__restrict__ pi, uint64_t seq) {
-  if (gated(st, seq)) return;
-  __shared__ int32_t cand[QPL][NN_CAND][TB];
-  const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
-  int64_t ch, nch;
-  nn_geometry(nq, nv, bmax, TB * QPL, items, ch, nch);
-  const int64_t nqt = (nq + TB * QPL - 1) / (TB * QPL);
-  bool tree_bad = false;
-#pragma unroll
-  for (int k = 0; k < 8; k++) tree_bad = tree_bad || !(vmax[k] < 1e15f);
-  for (int64_t item = blockIdx.x; item < nqt * nch; item += gridDim.x) {
-    const int64_t qt = item / nch, c = item - qt * nch;
-    const int j0 = (int)(c * ch), j1 = (int)min(nv, (c + 1) * ch);
-    int64_t qi[QPL];
-    bool live[QPL], any = false, bad = tree_bad;
-    float a[QPL][8], T[QPL];
-#pragma unroll
-    for (int u = 0; u < QPL; u++) {
-      qi[u] = qt * (TB * QPL) + u * TB + threadIdx.x;
-      live[u] = qi[u] < nq;
-      any = any || live[u];
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const double x = live[u] ? q[8 * (q_off + qi[u]) + k] : 0.0;
-        a[u][k] = -2.0f * (float)x;
-        bad = bad || (live[u] && !(fabs(x) < 1e15));
-      }
-    }
-    if (!__ballot(any)) continue;  // a wave past the last query (no barriers here)
-    bool scan64 = __ballot(bad) != 0ull;
-    int cnt[QPL];
-    if (!scan64) {
-      float B[QPL];
-#pragma unroll
-      for (int u = 0; u < QPL; u++) {
-        B[u] = INFINITY;
-        T[u] = 0.f;
-        cnt[u] = 0;
-      }
-      nn_sweep<UNR, 0, QPL>(a, vp, j0, j1, B, T, cnt, cand);
-#pragma unroll
-      for (int u = 0; u < QPL; u++) {
-        double g2 = 0.0, r2 = 0.0;  // |g|^2 and R^2 (g = -a / 2 exactly)
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-          const double ak = fabs(-0.5 * (double)a[u][k]), mk = (double)vmax[k];
-          g2 = g2 + ak * ak;
-          r2 = r2 + (mk + ak) * (mk + ak);
-        }
-        T[u] = live[u] ? nn_threshold(B[u], g2, r2) : -1.0f;
-      }
-      nn_sweep<UNR, 1, QPL>(a, vp, j0, j1, B, T, cnt, cand);
-      bool over = false;
-#pragma unroll
-      for (int u = 0; u < QPL; u++) over = over || cnt[u] > NN_CAND;
-      scan64 = __ballot(over) != 0ull;
-    }
-#pragma unroll
-    for (int u = 0; u < QPL; u++) {
-      double qq[8], best = INFINITY;
-      int bi = -1;
-#pragma unroll
-      for (int k = 0; k < 8; k++) qq[k] = live[u] ? q[8 * (q_off + qi[u]) + k] : 0.0;
-      if (scan64) {
-        nn_scan64<1>(qq, v, j0, j1, best, bi);
-      } else {
-        for (int m = 0; m < cnt[u]; m++) {
-          const int j = cand[u][m][threadIdx.x];
-          const double d = nn_dist64(qq, v + 8 * (int64_t)j);
-          if (d < best || (d == best && j < bi)) {
-            best = d;
-            bi = j;
-          }
-        }
-      }
-      if (live[u]) {
-        pd[c * nq + qi[u]] = best;
-        pi[c * nq + qi[u]] = bi;
-      }
-    }
-  }
-}
-
-// chunks in index order, strict <: the lowest index among equal distances;
-// nothing < inf (a NaN query): index 0, as the reference keeps it.  A thread
-// per query; past 64 chunks (the few-query searches have hundreds) a wave per
-// query: lanes take strided chunks, then a butterfly on (distance, chunk)
-// picks the lowest chunk among equal distances.
-__global__ __launch_bounds__(TB) void k_nn_reduce(const gbp_plan_status *st, const int32_t *nq_dev,
-                                                  const int32_t *nv_dev, int64_t bmax, int qts, int items,
-                                                  const double *__restrict__ pd,
-                                                  const int32_t *__restrict__ pi,
-                                                  int32_t *__restrict__ out, uint64_t seq) {
-  if (gated(st, seq)) return;
-  const int64_t nq = *nq_dev, nv = *nv_dev;
-  int64_t ch, nch;
-  nn_geometry(nq, nv, bmax, qts, items, ch, nch);
-  if (nch <= WAVE) {
-    for (int64_t qi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; qi < nq;
-         qi += (int64_t)gridDim.x * blockDim.x) {
-      double best = INFINITY;
-      int bi = 0;
-      int64_t c = 0;
-      for (; c + 4 <= nch; c += 4) {  // four chunks' loads in flight
-        double d[4];
-        int32_t id[4];
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          d[r] = pd[(c + r) * nq + qi];
-          id[r] = pi[(c + r) * nq + qi];
-        }
-#pragma unroll
-        for (int r = 0; r < 4; r++)
-          if (d[r] < best) {
-            best = d[r];
-            bi = id[r];
-          }
-      }
-      for (; c < nch; c++) {
-        const double d = pd[c * nq + qi];
-        if (d < best) {
-          best = d;
-          bi = pi[c * nq + qi];
-        }
-      }
-      out[qi] = bi;
-    }
-    return;
-  }
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / WAVE);
-  for (int64_t qi = blockIdx.x * (int64_t)(blockDim.x / WAVE) + threadIdx.x / WAVE; qi < nq;
-       qi += waves) {
-    double best = INFINITY;
-    int64_t bc = nch;  // chunk of the best (none)
-    for (int64_t c = lane; c < nch; c += WAVE) {
-      const double d = pd[c * nq + qi];
-      if (d < best) {
-        best = d;
-        bc = c;
-      }
-    }
-    for (int off = WAVE / 2; off > 0; off >>= 1) {
-      const double od = __shfl_xor(best, off);
-      const int64_t oc = __shfl_xor(bc, off);
-      if (od < best || (od == best && oc < bc)) {
-        best = od;
-        bc = oc;
-      }
-    }
-    if (lane == 0) out[qi] = bc < nch ? pi[bc * nq + qi] : 0;
-  }
-}
-
 // ============================================================================
-// nearest neighbour on the matrix cores (GBP_OPT_NN_FILTER 0, the default)
+// nearest neighbour in a device tree on the matrix cores (planner_class.cpp:185-200)
 // ============================================================================
 // The filter's scores S_j = |F_j|^2 - 2 G.F_j (F_j = 64 v_j, G = 64 q: scaled
 // by a power of two, so exactly; |G - F_j|^2 = |G|^2 + S_j) for a tile of 32
@@ -672,8 +271,8 @@ __global__ __launch_bounds__(TB) void k_nn_reduce(const gbp_plan_status *st, con
 // with N_1 + N_2 + N_3 the row's fp64 squared norm times 2^-14 in three fp16
 // parts (nn_put_hrow).  The dropped G_lo.F_lo term and the parts' rounding are
 // ~2^-20 of the products, so the matrix cores score 1024 (query, vertex) pairs
-// per 64 MFMA cycles where the packed fp32 filter (k_nn_filter) spends ~4.5
-// VALU instructions per pair per pass.  The VALU only reduces: per lane (its
+// per 64 MFMA cycles (the packed fp32 VALU filter of round 2 spent ~4.5
+// instructions per pair and pass).  The VALU only reduces: per lane (its
 // query and its 32 rows of two consecutive chunks: a "lane-unit") the minimum
 // by v_min3, then the three smallest unit minima with their units and a bound
 // m4 on every other unit (NhTop: v_med3 / v_cndmask, branch-free).  Work item
@@ -1197,259 +796,16 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
 }
 
 // ============================================================================
-// nearest neighbour through the tree's index (gbp_tree_index_build)
+// stage 1: the targets' ordered compaction
 // ============================================================================
-// The index holds the tree's first idx_n vertices sorted by the Morton key of
-// (x, y), cut into chunks of NN_CH rows; per chunk the fp32 rows' 8-D box
-// [lo, hi] and its middle row.  A search with many queries (the targets'
-// nearest vertices, stage 2):
-//   k_nnq_hist / k_nnq_scatter_ub  bucket the queries by Morton cell (a wave
-//        then holds 64 queries from one small area) and give each query an
-//        upper bound on its nearest distance: the fp32 filter's minimum over
-//        the chunks' middle rows, turned into a rigorous pruning threshold
-//        PT (below);
-//   k_nn_pruned  item = (wave of 64 cell-sorted queries, segment of chunks):
-//        pass 1 scans (fp32 dot form, as k_nn_filter) only the chunks whose
-//        box lower bound LB2 <= PT for some lane, tightening PT with each
-//        scanned chunk's minimum; pass 2 revisits the chunks that still pass
-//        and records the candidates S_j <= T(B); the exact fp64 distances of
-//        the candidates decide.  The vertices appended since the index was
-//        built (the tail) form one more segment, scanned in full;
-//   k_nn_reduce_idx  lexicographic (distance, vertex index) minimum over the
-//        segments: the reference's ascending scan with strict <.
-// Why a pruned chunk cannot hold the answer (notation of the k_nn_filter
-// proof above; P_j = |f_j - g|^2 in fp32 space, exact):
-//   * a box holds its chunk's fp32 rows, so LB2 = sum_k max(lo_k - g_k,
-//     g_k - hi_k, 0)^2 <= P_j for each of them; evaluated in fp32 (two
-//     subtractions rounded up by at most (1+u), eight FMAs) the computed
-//     LB2c <= P_j (1 + 10.1u);
-//   * for any row i with fp32 value S_i (B = S_i, or the minimum over rows),
-//     the fp64 minimiser j* satisfies sqrt(P_j*) <= r1(B) (the threshold
-//     proof: D_j* <= D_i (1 + 3e-15)), and so does every index tying with it;
-//   * PT = r1(B)^2 (1 + 1e-12)(1 + 16u), rounded up to fp32.  A chunk with
-//     LB2c > PT has P_j > r1^2 for all its rows: neither j* nor a tie is in it.
-// Rows scanned in pass 1 but not needed by a lane only lower its B (still a
-// real row: the bound holds).  A query or tree magnitude >= 1e15, or more
-// than NN_CAND candidates, sends the wave to the fp64 scan of its segment.
-constexpr int NN_CH = 64;          // rows per index chunk
-constexpr int NN_QBITS = 4;        // query cells: 2^4 x 2^4 Morton cells
-constexpr int NN_QCELLS = 1 << (2 * NN_QBITS);
-// Items of a search: per wave of 64 cell-sorted queries, NN_SORTED_SEGS
-// segments of R <= 256 chunks each (R >= 16: the mask phase's R iterations
-// stay short; at most 4 blocks of 64 chunk boxes) and the unindexed tail in
-// segments of >= 256 rows; all of them partial slots (NN_MAX_CHUNKS).
-constexpr int NN_SORTED_SEGS = 24;
-constexpr int NN_SEG_BLOCKS = 4;
-constexpr int NN_TAIL_ROWS = 256;
-constexpr int64_t NN_INDEX_MAX_ROWS = (int64_t)NN_SORTED_SEGS * NN_SEG_BLOCKS * WAVE * NN_CH;
-
-struct NnIdxGeom {
-  int R;      // chunks per sorted segment
-  int nseg;   // sorted segments
-  int ts;     // rows per tail segment (even)
-  int ntail;  // tail segments
-};
-__device__ __forceinline__ NnIdxGeom nn_idx_geometry(int64_t nc, int64_t tail) {
-  NnIdxGeom g;
-  int64_t R = 16;
-  if ((nc + R - 1) / R > NN_SORTED_SEGS) R = (nc + NN_SORTED_SEGS - 1) / NN_SORTED_SEGS;
-  g.R = (int)R;
-  g.nseg = nc > 0 ? (int)((nc + R - 1) / R) : 0;
-  const int64_t slots = NN_MAX_CHUNKS - g.nseg;
-  int64_t ts = (tail + slots - 1) / slots;
-  if (ts < NN_TAIL_ROWS) ts = NN_TAIL_ROWS;
-  g.ts = (int)((ts + 1) & ~(int64_t)1);
-  g.ntail = tail > 0 ? (int)((tail + g.ts - 1) / g.ts) : 0;
-  return g;
-}
-
-__device__ __forceinline__ uint32_t spread16(uint32_t v) {  // bit i -> bit 2i
-  v &= 0xFFFFu;
-  v = (v | (v << 8)) & 0x00FF00FFu;
-  v = (v | (v << 4)) & 0x0F0F0F0Fu;
-  v = (v | (v << 2)) & 0x33333333u;
-  v = (v | (v << 1)) & 0x55555555u;
-  return v;
-}
-// (x, y) quantised to `bits` per axis over bounds {x0, xN, y0, yN}, clamped;
-// NaN goes to the last cell
-__device__ __forceinline__ uint32_t morton_key(double x, double y, const double *bd, int bits) {
-  const double sc = (double)(1u << bits);
-  const double ux = (x - bd[0]) / (bd[1] - bd[0]) * sc, uy = (y - bd[2]) / (bd[3] - bd[2]) * sc;
-  const uint32_t hi = (1u << bits) - 1u;
-  const uint32_t qx = isnan(ux) ? hi : (ux <= 0.0 ? 0u : (ux >= (double)hi ? hi : (uint32_t)ux));
-  const uint32_t qy = isnan(uy) ? hi : (uy <= 0.0 ? 0u : (uy >= (double)hi ? hi : (uint32_t)uy));
-  return (spread16(qx) << 1) | spread16(qy);
-}
-
-// PT above from a filter minimum B (fp32 S space); g2 = |g|^2, r2 = R^2.
-// B = +inf (nothing finite scanned) gives +inf: no chunk can be pruned
-__device__ __forceinline__ float nn_prune_threshold(float B, double g2, double r2) {
-  const double eps = 10.0 * 0x1p-24 * r2, del = 2.0 * 0x1p-24 * sqrt(r2);
-  const double r0 = sqrt(fmax(0.0, (double)B + g2 + eps));
-  const double r1 = (r0 + del) * (1.0 + 4e-15) + del;
-  const double pt = r1 * r1 * (1.0 + 1e-12) * (1.0 + 16.0 * 0x1p-24);
-  return isinf(pt) || isnan(pt) ? INFINITY : nextafterf((float)pt, INFINITY);
-}
-
-// lane u's value for the whole wave (v_readlane: an SGPR operand)
-__device__ __forceinline__ float lane_bcast(float x, int u) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), u));
-}
-
-// LB2c of the query g (fp32) against a chunk box
-__device__ __forceinline__ float nn_box_lb2(const float (&g)[8], const float *__restrict__ box) {
-  float acc = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const float d = fmaxf(fmaxf(box[k] - g[k], g[k] - box[8 + k]), 0.f);
-    acc = fmaf(d, d, acc);
-  }
-  return acc;
-}
-
-// |g|^2 and R^2 of a query (g = -a / 2 exactly), R with the tree's vmax
-__device__ __forceinline__ void nn_g2r2(const float (&a)[8], const float *__restrict__ vmax,
-                                        double &g2, double &r2) {
-  g2 = 0.0;
-  r2 = 0.0;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const double ak = fabs(-0.5 * (double)a[k]), mk = (double)vmax[k];
-    g2 = g2 + ak * ak;
-    r2 = r2 + (mk + ak) * (mk + ak);
-  }
-}
-
-__global__ void k_idx_keys(const double *__restrict__ v, int64_t n, double bx0, double bxN,
-                           double by0, double byN, uint32_t *__restrict__ keys,
-                           int32_t *__restrict__ ids) {
-  const double bd[4] = {bx0, bxN, by0, byN};
-  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
-       j += (int64_t)gridDim.x * blockDim.x) {
-    keys[j] = morton_key(v[8 * j], v[8 * j + 1], bd, 16);
-    ids[j] = (int32_t)j;
-  }
-}
-
-// the sorted rows in the filter's pair format and in fp64 (from the vertices)
-__global__ void k_idx_rows(const double *__restrict__ v, const int32_t *__restrict__ sid, int64_t n,
-                           float *__restrict__ sp, double *__restrict__ sv) {
-  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n;
-       p += (int64_t)gridDim.x * blockDim.x) {
-    const double *r = v + 8 * (int64_t)sid[p];
-    nn_put_row(sp, p, r);
-    copy8(sv + 8 * p, r);
-  }
-}
-
-// per chunk: the box of its fp32 rows (NaN components skipped: a NaN row is
-// never a nearest vertex) and its middle row
-__global__ void k_idx_boxes(const float *__restrict__ sp, int64_t n, float *__restrict__ box,
-                            float *__restrict__ med) {
-  const int64_t nc = (n + NN_CH - 1) / NN_CH;
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < nc;
-       c += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t j0 = c * NN_CH, j1 = min(n, j0 + NN_CH);
-    float lo[8], hi[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      lo[k] = INFINITY;
-      hi[k] = -INFINITY;
-    }
-    for (int64_t j = j0; j < j1; j++) {
-      const float *r = sp + NN_PAIR * (j >> 1) + (j & 1);
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        lo[k] = fminf(lo[k], r[2 * k]);
-        hi[k] = fmaxf(hi[k], r[2 * k]);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      box[16 * c + k] = lo[k];
-      box[16 * c + 8 + k] = hi[k];
-    }
-    const int64_t m = j0 + (j1 - j0 - 1) / 2;
-    const float *r = sp + NN_PAIR * (m >> 1) + (m & 1);
-    float *o = med + NN_PAIR * (c >> 1) + (c & 1);
-#pragma unroll
-    for (int k = 0; k < 8; k++) o[2 * k] = r[2 * k];
-    o[16] = r[16];
-    if ((c & 1) == 0 && c + 1 == nc) {  // the last pair's empty slot: never a minimum
-#pragma unroll
-      for (int k = 0; k < 8; k++) o[2 * k + 1] = __builtin_nanf("");
-      o[17] = __builtin_nanf("");
-    }
-  }
-}
-
-// The indexed search's query side (NnBucket): query r goes to the bucket of
-// its Morton cell (bq[cell][slot], any order within a cell) and gets its
-// chunk-pruning threshold from the fp32 filter's minimum over the index's
-// middle rows.  k_nn_pruned walks the buckets in Morton order (a prefix over
-// bcnt), so its waves hold 64 queries from one small area.  Called for the
-// compacted targets inside k_compact_targets, else by k_nnq_bucket.
-struct NnBucket {
-  int32_t *bcnt, *bq;
-  float *qpt;
-  const float *imed, *vmax;
-  int nc;
-  int64_t cap;
-  double bd[4];
-};
-
-// every lane of the wave must call this (the middle-row scan is wave-uniform)
-template <int UNR>
-__device__ __forceinline__ void nn_bucket_query(const NnBucket &nb, const double *__restrict__ x,
-                                                int64_t r, bool live) {
-  float a[1][8];
-  bool qnan = false;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const double v = live ? x[k] : 0.0;
-    a[0][k] = -2.0f * (float)v;
-    qnan = qnan || isnan(v);
-  }
-  if (live) {
-    const uint32_t cell = morton_key(x[0], x[1], nb.bd, NN_QBITS);
-    nb.bq[(int64_t)cell * nb.cap + atomicAdd(&nb.bcnt[cell], 1)] = (int32_t)r;
-  }
-  float B[1] = {INFINITY}, T[1] = {0.f};
-  int cnt[1] = {0};
-  nn_sweep<UNR, 0, 1>(a, nb.imed, 0, nb.nc, B, T, cnt, nullptr);
-  double g2, r2;
-  nn_g2r2(a[0], nb.vmax, g2, r2);
-  // a NaN query has no nearest vertex (index 0, the reduce's default):
-  // threshold -1 excludes every chunk
-  if (live) nb.qpt[r] = qnan ? -1.0f : nn_prune_threshold(B[0], g2, r2);
-}
-
-__global__ __launch_bounds__(TB) void k_nnq_bucket(const gbp_plan_status *__restrict__ st,
-                                                   const int32_t *__restrict__ nq_dev,
-                                                   const double *__restrict__ q,
-                                                   const int32_t *__restrict__ q_off_dev, NnBucket nb,
-                                                   uint64_t seq) {
-  if (gated(st, seq)) return;
-  const int64_t nq = *nq_dev, q_off = q_off_dev ? *q_off_dev : 0;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t iters = (nq + stride - 1) / stride;  // whole waves run the middle-row scan
-  for (int64_t it = 0; it < iters; it++) {
-    const int64_t i = it * stride + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    nn_bucket_query<4>(nb, q + 8 * (q_off + (i < nq ? i : 0)), i, i < nq);
-  }
-}
-
-// the compacted targets (stage 1).  (Bucketing them for the indexed search
-// here as well was measured slower: the 43 tiles' middle-row scans and the
-// cell-count atomics made the compaction 10 -> 62 us.)
+// the compacted targets (stage 1), in draw order, and their fp16 query rows
 __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int64_t n,
                                                         const double *__restrict__ cand,
                                                         const uint32_t *__restrict__ cflag,
                                                         double *__restrict__ targets,
                                                         _Float16 *__restrict__ tqh,
                                                         unsigned long long *tiles, uint32_t epoch,
-                                                        int32_t half, uint64_t seq) {
+                                                        int32_t half, int resumed, uint64_t seq) {
   if (gated(st, seq)) return;
   const int64_t i = blockIdx.x * (int64_t)CB + threadIdx.x;
   const uint32_t f = i < n ? cflag[i] : 0u;
@@ -1466,10 +822,10 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
     // the extend stream of this half: RRTClass::extend_counter_ advances by
-    // the number of extends (csrc/host/gbp_planner.cpp extendBatch); a re-run
-    // for the same half (resumed after a FRAGILE halt) starts from the same
-    // counters
-    const bool again = st->ext_half == half;
+    // the number of extends (csrc/host/gbp_planner.cpp extendBatch); the re-run
+    // of a compaction that halted on a FRAGILE draw (the host resumes the half
+    // at stage 1, gbp_plan_resolve_host) starts from the same counters
+    const bool again = resumed != 0;
     const int64_t base = again ? st->ext_prev : st->ext_counter;
     const int64_t tg = again ? st->stat_targets_prev : st->stat_targets;
     st->ext_half = half;
@@ -1479,218 +835,6 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
     st->ext_counter = base + st->n_targets;
     st->stat_targets = tg + st->n_targets;
   }
-}
-
-// the fp64 scan of rows [j0, j1) of a row set whose vertex indices are ids[]
-// (nullptr: the rows are vertices j0..j1-1): lexicographic (distance, index)
-__device__ __forceinline__ void nn_scan64_ids(const double qq[8], const double *__restrict__ v,
-                                              const int32_t *__restrict__ ids, int j0, int j1,
-                                              double &best, int &bi) {
-  for (int j = j0; j < j1; j++) {
-    const int vj = ids ? ids[__builtin_amdgcn_readfirstlane(j)] : j;
-    const double d = nn_dist64(qq, v + 8 * (int64_t)__builtin_amdgcn_readfirstlane(vj));
-    if (d < best || (d == best && vj < bi)) {
-      best = d;
-      bi = vj;
-    }
-  }
-}
-
-// Item (query wave, segment).  Mask phase: the segment's chunk boxes, 64 at a
-// time, in the VGPRs of lanes 0..63 (one coalesced load); each chunk's box
-// broadcast by v_readlane, every lane tests its own query, and the chunks
-// some lane cannot exclude form one 64-bit ballot per block.  Then pass 1 and
-// pass 2 of the filter run over the masked chunks only (row pairs by scalar
-// load, as k_nn_filter), and the candidates are decided in fp64.  Tail
-// segments scan their rows in full.
-template <int UNR>
-__global__ __launch_bounds__(TB) void k_nn_pruned(
-    const gbp_plan_status *__restrict__ st, const int32_t *__restrict__ nq_dev,
-    const double *__restrict__ q, const int32_t *__restrict__ q_off_dev,
-    const int32_t *__restrict__ bcnt, const int32_t *__restrict__ bq, int64_t bcap,
-    const float *__restrict__ qpt, const double *__restrict__ v, const float *__restrict__ vf,
-    const float *__restrict__ vmax, const int32_t *__restrict__ nv_dev,
-    const float *__restrict__ isp, const int32_t *__restrict__ isid, const double *__restrict__ isv,
-    const float *__restrict__ ibox, int idx_n, double *__restrict__ pd, int32_t *__restrict__ pi,
-    uint64_t seq) {
-  if (gated(st, seq)) return;
-  __shared__ int32_t cand[1][NN_CAND][TB];
-  __shared__ int32_t bpre[NN_QCELLS + 1];  // bucket prefix: queries before each cell
-  const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
-  if (threadIdx.x == 0) {  // NN_QCELLS is small: one thread
-    int32_t acc = 0;
-    for (int c = 0; c < NN_QCELLS; c++) {
-      bpre[c] = acc;
-      acc += bcnt[c];
-    }
-    bpre[NN_QCELLS] = acc;
-  }
-  __syncthreads();
-  const int nc = (idx_n + NN_CH - 1) / NN_CH;
-  const NnIdxGeom G = nn_idx_geometry(nc, nv - idx_n);
-  const int nslot = G.nseg + G.ntail;
-  const int64_t nqw = (nq + WAVE - 1) / WAVE, nitems = nqw * nslot;
-  bool tree_bad = false;
-#pragma unroll
-  for (int k = 0; k < 8; k++) tree_bad = tree_bad || !(vmax[k] < 1e15f);
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int64_t wstride = (int64_t)gridDim.x * (TB / WAVE);
-  // the item and everything derived from it are wave-uniform; readfirstlane
-  // tells the compiler so, and the row pairs then arrive by scalar load
-  const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
-  for (int64_t item = blockIdx.x * (int64_t)(TB / WAVE) + wid; item < nitems; item += wstride) {
-    // slot-major order: a wave's consecutive items are different query waves
-    // of the same segment (their chunk boxes and rows shared in the caches)
-    const int sg = (int)(item / nqw);
-    const int64_t wq = item - (int64_t)sg * nqw;
-    const int64_t p = wq * WAVE + lane;
-    const bool live = p < nq;
-    // the p-th query in cell order: its cell by binary search of the prefix
-    int lo = 0, hi = NN_QCELLS;  // bpre[lo] <= p < bpre[hi]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (bpre[mid] <= p) lo = mid; else hi = mid;
-    }
-    const int64_t qi = live ? bq[(int64_t)lo * bcap + (p - bpre[lo])] : 0;
-    const double *qrow = q + 8 * (q_off + qi);
-    float a[1][8], g[8];
-    bool bad = tree_bad;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const double x = live ? qrow[k] : 0.0;
-      a[0][k] = -2.0f * (float)x;
-      g[k] = (float)x;
-      bad = bad || (live && !(fabs(x) < 1e15));
-    }
-    const bool sorted = sg < G.nseg;
-    // the item's rows: sorted chunks [c0, c1) or tail rows [r0, r1)
-    const int c0 = sorted ? sg * G.R : 0, c1 = sorted ? min(nc, (sg + 1) * G.R) : 0;
-    const float *rows = sorted ? isp : vf;
-    const int32_t *ids = sorted ? isid : nullptr;
-    const int t0 = idx_n + (sg - G.nseg) * G.ts;
-    const int r0 = sorted ? c0 * NN_CH : t0;
-    const int r1 = sorted ? min(idx_n, c1 * NN_CH) : (int)min(nv, (int64_t)t0 + G.ts);
-    double best = INFINITY;
-    int bi = -1;
-    bool scan64 = __ballot(bad) != 0ull;
-    int cnt[1] = {0};
-    if (!scan64 && r0 < r1) {
-      uint64_t cm[NN_SEG_BLOCKS];
-      if (sorted) {
-        const float pt = live ? qpt[qi] : -1.0f;
-#pragma unroll
-        for (int b = 0; b < NN_SEG_BLOCKS; b++) {
-          cm[b] = 0;
-          const int cb = c0 + b * WAVE;
-          if (cb >= c1) continue;
-          const int nb = min(WAVE, c1 - cb);
-          float bx[16];
-          const float4 *src = (const float4 *)(ibox + 16 * (int64_t)(cb + min(lane, nb - 1)));
-#pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const float4 t4 = src[r];
-            bx[4 * r] = t4.x;
-            bx[4 * r + 1] = t4.y;
-            bx[4 * r + 2] = t4.z;
-            bx[4 * r + 3] = t4.w;
-          }
-          uint64_t m = 0;
-          for (int u = 0; u < nb; u++) {
-            float box[16];  // chunk cb + u, broadcast
-#pragma unroll
-            for (int k = 0; k < 16; k++) box[k] = lane_bcast(bx[k], u);
-            if (__ballot(nn_box_lb2(g, box) <= pt)) m |= 1ull << u;
-          }
-          cm[b] = m;
-        }
-      }
-      float B[1] = {INFINITY}, T[1] = {0.f};
-      double g2, r2;
-      nn_g2r2(a[0], vmax, g2, r2);
-      // pass 1: B over the masked chunks (the tail: all its rows)
-      if (sorted) {
-#pragma unroll
-        for (int b = 0; b < NN_SEG_BLOCKS; b++)
-          for (uint64_t m = cm[b]; m; m &= m - 1) {
-            const int c = c0 + b * WAVE + __builtin_ctzll(m);
-            nn_sweep<UNR, 0, 1>(a, rows, c * NN_CH, min(idx_n, (c + 1) * NN_CH), B, T, cnt, cand);
-          }
-      } else {
-        nn_sweep<UNR, 0, 1>(a, rows, r0, r1, B, T, cnt, cand);
-      }
-      T[0] = live ? nn_threshold(B[0], g2, r2) : -1.0f;
-      // pass 2: the candidates S_j <= T(B) of the same rows
-      if (sorted) {
-#pragma unroll
-        for (int b = 0; b < NN_SEG_BLOCKS; b++)
-          for (uint64_t m = cm[b]; m; m &= m - 1) {
-            const int c = c0 + b * WAVE + __builtin_ctzll(m);
-            nn_sweep<UNR, 1, 1>(a, rows, c * NN_CH, min(idx_n, (c + 1) * NN_CH), B, T, cnt, cand);
-          }
-      } else {
-        nn_sweep<UNR, 1, 1>(a, rows, r0, r1, B, T, cnt, cand);
-      }
-      scan64 = __ballot(cnt[0] > NN_CAND) != 0ull;
-    }
-    double qq[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) qq[k] = live ? qrow[k] : 0.0;
-    if (scan64) {
-      nn_scan64_ids(qq, v, ids, r0, r1, best, bi);
-    } else {
-      // candidates: rows of the sorted copy (isv) or of the tree (tail);
-      // distances first, vertex indices only for the ones that could win
-      const double *rv = sorted ? isv : v;
-      for (int m = 0; m < cnt[0]; m++) {
-        const int r = cand[0][m][threadIdx.x];
-        const double d = nn_dist64(qq, rv + 8 * (int64_t)r);
-        if (d <= best) {
-          const int j = sorted ? ids[r] : r;
-          if (d < best || j < bi) {
-            best = d;
-            bi = j;
-          }
-        }
-      }
-    }
-    if (live) {
-      pd[sg * nq + qi] = best;
-      pi[sg * nq + qi] = bi;
-    }
-  }
-}
-
-// lexicographic (distance, index) minimum over a query's segments; nothing
-// finite (a NaN query, or no row): index 0, as the reference keeps it.  Also
-// clears the query buckets' counts for the next search.
-__global__ __launch_bounds__(TB) void k_nn_reduce_idx(const gbp_plan_status *st,
-                                                      const int32_t *nq_dev,
-                                                      const int32_t *nv_dev, int idx_n,
-                                                      const double *__restrict__ pd,
-                                                      const int32_t *__restrict__ pi,
-                                                      int32_t *__restrict__ out,
-                                                      int32_t *__restrict__ bcnt, uint64_t seq) {
-  if (gated(st, seq)) return;
-  const int64_t nq = *nq_dev;
-  const NnIdxGeom G = nn_idx_geometry((idx_n + NN_CH - 1) / NN_CH, *nv_dev - idx_n);
-  const int nslot = G.nseg + G.ntail;
-  for (int64_t qi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; qi < nq;
-       qi += (int64_t)gridDim.x * blockDim.x) {
-    double best = INFINITY;
-    int bi = 0;
-    for (int sg = 0; sg < nslot; sg++) {
-      const double d = pd[sg * nq + qi];
-      const int j = pi[sg * nq + qi];
-      if (j >= 0 && (d < best || (d == best && j < bi))) {
-        best = d;
-        bi = j;
-      }
-    }
-    out[qi] = bi;
-  }
-  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < NN_QCELLS;
-       c += (int64_t)gridDim.x * blockDim.x)
-    bcnt[c] = 0;
 }
 
 // ============================================================================
@@ -1801,18 +945,11 @@ __global__ __launch_bounds__(TB) void k_select(gbp_plan_status *st, const double
 // mode 0: extend successors of the current targets into T (parent = nn[i]);
 // mode 1: connections of the new vertices into O (parent = nno[k]), the first
 // REACHED one in order recorded as the meeting point.
-// running max |x| over a tree's fp32 rows (non-negative floats order as their
-// bit patterns; NaN is skipped: it never passes a distance comparison)
-__device__ __forceinline__ void vmax_update(float *m, float x) {
-  if (!isnan(x)) atomicMax((unsigned int *)m, __float_as_uint(fabsf(x)));
-}
-
 __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
                                                const int32_t *__restrict__ res,
                                                const int32_t *__restrict__ par,
                                                const double *__restrict__ sn,
                                                const double *__restrict__ an, double *__restrict__ tv,
-                                               float *__restrict__ tvf, float *__restrict__ tvmax,
                                                _Float16 *__restrict__ tvh, float *__restrict__ thm,
                                                double *__restrict__ ta, double *__restrict__ tg,
                                                int32_t *__restrict__ tp, int32_t *__restrict__ tcount,
@@ -1831,8 +968,11 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
   const bool keep = live && r != GBP_TRAPPED;
   int32_t *total = mode == 0 ? &st->n_added : &st->n_conn_added;
   const uint32_t rank = ordered_rank(keep, tiles, epoch, total, st);
-  if (keep && (int64_t)base + rank >= cap) {  // the caller reserved too little: drop, report
+  if (keep && (int64_t)base + rank >= cap) {
+    // the caller reserved too little: drop, report, and gate every later
+    // launch (a search over rows past cap would read out of bounds)
     atomicOr(&st->error, 2u);
+    raise_gate(st, seq);
     if (vtx) vtx[i] = -1;
   } else if (keep) {
     const int32_t idx = base + (int32_t)rank, p = par[i];
@@ -1840,10 +980,7 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
     copy8(s, sn + 8 * i);
     copy8(pv, tv + 8 * (int64_t)p);
     copy8(tv + 8 * (int64_t)idx, s);
-    nn_put_row(tvf, idx, s);
     nn_put_hrow(tvh, thm, idx, s, false);
-#pragma unroll
-    for (int k = 0; k < 8; k++) vmax_update(tvmax + k, (float)s[k]);
     copy10(ta + 10 * (int64_t)idx, an + 10 * i);
     tp[idx] = p;
     tg[idx] = tg[p] + pose_distance(pv, s);  // graph_class.cpp:36-42 addEdge
@@ -1859,8 +996,10 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
     vtx[i] = -1;
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
-    const int32_t added = *total;
-    *tcount = (int32_t)min<int64_t>((int64_t)base + added, cap);
+    // the rows actually written (the appended count is clamped at cap)
+    const int32_t added = (int32_t)min<int64_t>(*total, cap - (int64_t)base);
+    *total = added;
+    *tcount = base + added;
     if (mode == 0) {
       st->added_base = base;
       st->stat_added += added;
@@ -2038,12 +1177,7 @@ __global__ void k_tree_init(gbp_tree t, double r0, double r1, double r2, double 
                             double r5, double r6, double r7) {
   const double r[8] = {r0, r1, r2, r3, r4, r5, r6, r7};
   copy8(t.v, r);
-  nn_put_row(t.vf, 0, r);
   nn_put_hrow(t.vh, t.hm, 0, r, true);
-  for (int k = 0; k < 8; k++) {
-    const float f = (float)r[k];
-    t.vmax[k] = isnan(f) ? 0.f : fabsf(f);
-  }
   for (int k = 0; k < 10; k++) t.a[k] = 0.0;
   t.g[0] = 0.0;
   t.parent[0] = -1;
@@ -2057,9 +1191,7 @@ __global__ void k_tree_append(gbp_tree t, int64_t n, const double *__restrict__ 
   int32_t c = *t.count;
   for (int64_t i = 0; i < n; i++, c++) {
     copy8(t.v + 8 * (int64_t)c, s + 8 * i);
-    nn_put_row(t.vf, c, s + 8 * i);
     nn_put_hrow(t.vh, t.hm, c, s + 8 * i, false);
-    for (int k = 0; k < 8; k++) vmax_update(t.vmax + k, (float)s[8 * i + k]);
     copy10(t.a + 10 * (int64_t)c, a + 10 * i);
     t.parent[c] = p[i];
     t.g[c] = p[i] >= 0 ? t.g[p[i]] + pose_distance(t.v + 8 * (int64_t)p[i], s + 8 * i) : 0.0;
@@ -2133,72 +1265,33 @@ uint32_t next_epoch(gbp_plan_ws *w) {
 
 unsigned tiles_for(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + CB - 1) / CB); }
 
-NnBucket nn_bucket_args(gbp_plan_ws *w, const gbp_tree *tr) {
-  NnBucket nb;
-  nb.bcnt = w->bcnt;
-  nb.bq = w->bq;
-  nb.qpt = w->qpt;
-  nb.imed = tr->imed;
-  nb.vmax = tr->vmax;
-  nb.nc = (tr->idx_n + NN_CH - 1) / NN_CH;
-  nb.cap = w->bmax;
-  for (int k = 0; k < 4; k++) nb.bd[k] = tr->ibounds[k];
-  return nb;
-}
-
-// use_index: the search goes through tr's index; qh: the queries' fp16 rows
-// (nn_put_hrow layout, same offsets as q) for the matrix-core search; prep:
-// the extends' candidates are drawn inside the matrix-core search (returns
-// *prepped)
+// qh: the queries' fp16 rows (nn_put_hrow layout, same offsets as q), or
+// null (converted in the search); prep: the extends' candidates are drawn
+// inside the search (returns *prepped)
 template <class ZT = float>
 int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
-              const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s, bool use_index = false,
+              const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s,
               const _Float16 *qh = nullptr, const NhPrep<ZT> *prep = nullptr,
               double *cs = nullptr, bool *prepped = nullptr) {
   if (prepped) *prepped = false;
-  if (use_index && tr->idx_n > 0) {
-    // the indexed search: queries bucketed by Morton cell, pruned chunk scans
-    const unsigned gq = grid_for(w->bmax, TB, num_cus * 4);
-    hipLaunchKernelGGL(k_nnq_bucket, dim3(gq), dim3(TB), 0, s, w->st, nq_dev, q, q_off_dev,
-                       nn_bucket_args(w, tr), ++w->seq);
-    hipLaunchKernelGGL((k_nn_pruned<4>), dim3(num_cus * 8), dim3(TB), 0, s, w->st, nq_dev, q,
-                       q_off_dev, w->bcnt, w->bq, w->bmax, w->qpt, tr->v, tr->vf, tr->vmax,
-                       tr->count, tr->isp, tr->isid, tr->isv, tr->ibox, tr->idx_n, w->nn_d, w->nn_i,
-                       ++w->seq);
-    hipLaunchKernelGGL(k_nn_reduce_idx, dim3(gq), dim3(TB), 0, s, w->st, nq_dev, tr->count,
-                       tr->idx_n, w->nn_d, w->nn_i, out, w->bcnt, ++w->seq);
-    return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
+  const int gm = num_cus * (NH_ITEMS / 4) / 256;  // the search's workgroups
+  if (prep) {
+    NhPrep<ZT> pp = *prep;
+    pp.first_block = gm;
+    const int gp = (int)grid_for(GBP_NUM_GEN_STATES * w->bmax, NH_TB, num_cus * 4);
+    hipLaunchKernelGGL((k_nn_mfma<NH_NT, ZT, true>), dim3(gm + gp), dim3(NH_TB), 0, s, w->st,
+                       nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
+                       (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, pp);
+    if (prepped) *prepped = true;
+  } else {
+    hipLaunchKernelGGL((k_nn_mfma<NH_NT, float, false>), dim3(gm), dim3(NH_TB), 0, s, w->st,
+                       nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
+                       (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, NhPrep<float>{});
   }
-  if (w->nn_mode == 0) {  // the matrix cores (k_nn_mfma), GBP_OPT_NN_FILTER 0
-    const int gm = num_cus * (NH_ITEMS / 4) / 256;  // the search's workgroups
-    if (prep) {
-      NhPrep<ZT> pp = *prep;
-      pp.first_block = gm;
-      const int gp = (int)grid_for(GBP_NUM_GEN_STATES * w->bmax, NH_TB, num_cus * 4);
-      hipLaunchKernelGGL((k_nn_mfma<NH_NT, ZT, true>), dim3(gm + gp), dim3(NH_TB), 0, s, w->st,
-                         nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
-                         (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, pp);
-      if (prepped) *prepped = true;
-    } else {
-      hipLaunchKernelGGL((k_nn_mfma<NH_NT, float, false>), dim3(gm), dim3(NH_TB), 0, s, w->st,
-                         nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
-                         (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, NhPrep<float>{});
-    }
-    hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(NH_G * w->bmax, NH_RTB, num_cus * 8)), dim3(NH_RTB),
-                       0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, tr->count, w->bmax,
-                       (const float4 *)w->nn_d, (const int4 *)w->nn_i, out, ++w->seq, w->nn_stats,
-                       prep ? cs : nullptr);
-    return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
-  }
-  // two queries per lane, four row pairs per scalar load, 8 workgroups per
-  // CU: the fastest of {1, 2, 4} pairs x {1, 2} queries x {4, 8} workgroups
-  // per CU on trees past ~20k vertices (profiles/r02j_nn_dot.txt)
-  constexpr int QPL = 2, items = 2048;  // (query tile, chunk) items per call, nn_geometry
-  hipLaunchKernelGGL((k_nn_filter<4, QPL>), dim3(num_cus * 8), dim3(TB), 0, s, w->st, nq_dev, q,
-                     q_off_dev, tr->v, tr->vf, tr->vmax, tr->count, w->bmax, items, w->nn_d, w->nn_i,
-                     ++w->seq);
-  hipLaunchKernelGGL(k_nn_reduce, dim3(grid_for(w->bmax, TB, num_cus * 4)), dim3(TB), 0, s, w->st,
-                     nq_dev, tr->count, w->bmax, TB * QPL, items, w->nn_d, w->nn_i, out, ++w->seq);
+  hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(NH_G * w->bmax, NH_RTB, num_cus * 8)), dim3(NH_RTB),
+                     0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, tr->count, w->bmax,
+                     (const float4 *)w->nn_d, (const int4 *)w->nn_i, out, ++w->seq, w->nn_stats,
+                     prep ? cs : nullptr);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
 
@@ -2210,7 +1303,6 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   const TerrainView<ZT> V = view<ZT>(t);
   const int cus = t->num_cus;
   gbp_plan_status *st = w->st;
-  w->nn_mode = t->opt_nn_filter;
   w->nn_stats = t->opt_nn_stats;
   if (first_stage <= 0 && last_stage >= 0)
     hipLaunchKernelGGL(k_targets<ZT>, dim3(grid_for(batch, TB, cus * 8)), dim3(TB), 0, s, V, st,
@@ -2219,17 +1311,14 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   if (first_stage <= 1 && last_stage >= 1)
     hipLaunchKernelGGL(k_compact_targets, dim3(tiles_for(batch)), dim3(CB), 0, s, st, batch,
                        w->cand, w->cflag, w->targets, w->tqh, w->tiles, next_epoch(w), half,
-                       ++w->seq);
+                       first_stage == 1 ? 1 : 0, ++w->seq);
   if (first_stage <= 2 && last_stage >= 2) {
-    // the targets' nearest vertices through T's index when GBP_OPT_NN_INDEX
-    // asks for it and the index holds at least that many vertices
-    const bool idx = t->opt_nn_index > 0 && T->idx_n >= t->opt_nn_index;
     // the candidates' actions inside the search unless they are direction-biased
     // (then they depend on s_near: k_extend_prep after the search)
     const NhPrep<ZT> prep{V, seed, w->ca, t->sampling, direction, 0};
     const bool early = !t->sampling.action_flag;
     bool prepped = false;
-    int rc = nn_launch<ZT>(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, idx, w->tqh,
+    int rc = nn_launch<ZT>(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, w->tqh,
                            early ? &prep : nullptr, w->cs, &prepped);
     if (rc) return rc;
     const int64_t mmax = batch * GBP_NUM_GEN_STATES;
@@ -2246,13 +1335,14 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   }
   if (first_stage <= 3 && last_stage >= 3)
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 0, w->eres, w->nn,
-                       w->esn, w->ean, T->v, T->vf, T->vmax, T->vh, T->hm, T->a, T->g, T->parent, T->count, w->evtx, w->tiles,
+                       w->esn, w->ean, T->v, T->vh, T->hm, T->a, T->g, T->parent, T->count, w->evtx,
+                       w->tiles,
                        next_epoch(w), half, T->cap, ++w->seq);
   if (!O) return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   const int cdir = direction == GBP_FORWARD ? GBP_REVERSE : GBP_FORWARD;
   if (first_stage <= 4 && last_stage >= 4) {
     // queries: T's new vertices, rows [added_base, added_base + n_added)
-    int rc = nn_launch(w, &st->n_added, T->v, &st->added_base, O, w->nno, cus, s, false, T->vh);
+    int rc = nn_launch(w, &st->n_added, T->v, &st->added_base, O, w->nno, cus, s, T->vh);
     if (rc) return rc;
     const int cm = (t->opt_affine && t->affine) ? 2 : 0;
     const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * 4, (batch + 3) / 4));
@@ -2269,7 +1359,8 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   }
   if (first_stage <= 5 && last_stage >= 5)
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 1, w->kres, w->nno,
-                       w->ksn, w->kan, O->v, O->vf, O->vmax, O->vh, O->hm, O->a, O->g, O->parent, O->count, nullptr, w->tiles,
+                       w->ksn, w->kan, O->v, O->vh, O->hm, O->a, O->g, O->parent, O->count, nullptr,
+                       w->tiles,
                        next_epoch(w), half, O->cap, ++w->seq);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
@@ -2302,22 +1393,19 @@ T *carve(char *&p, size_t count) {
 
 int tree_alloc(gbp_tree *t, int64_t cap) {
   double *v = nullptr, *a = nullptr, *g = nullptr;
-  float *vf = nullptr;
   _Float16 *vh = nullptr;
   int32_t *p = nullptr;
   if (hipMalloc(&v, 64 * cap) != hipSuccess) return GBP_E_ALLOC;
   if (hipMalloc(&a, 80 * cap) != hipSuccess || hipMalloc(&g, 8 * cap) != hipSuccess ||
-      hipMalloc(&p, 4 * cap) != hipSuccess || hipMalloc(&vf, 4 * NN_PAIR * ((cap + 1) / 2)) != hipSuccess ||
-        hipMalloc(&vh, 2 * NH_ROW * ((cap + 63) & ~(int64_t)63)) != hipSuccess) {
+      hipMalloc(&p, 4 * cap) != hipSuccess ||
+      hipMalloc(&vh, 2 * NH_ROW * ((cap + 63) & ~(int64_t)63)) != hipSuccess) {
     (void)hipFree(v);
     if (a) (void)hipFree(a);
     if (g) (void)hipFree(g);
     if (p) (void)hipFree(p);
-    if (vf) (void)hipFree(vf);
     return GBP_E_ALLOC;
   }
   t->v = v;
-  t->vf = vf;
   t->vh = vh;
   t->a = a;
   t->g = g;
@@ -2365,13 +1453,12 @@ int gbp_tree_create(int device, int64_t capacity, gbp_tree **out) {
   gbp_tree *t = new (std::nothrow) gbp_tree();
   if (!t) return GBP_E_ALLOC;
   t->device = device;
-  if (hipMalloc(&t->count, 4) != hipSuccess || hipMalloc(&t->vmax, 32) != hipSuccess ||
-      hipMalloc(&t->hm, 64) != hipSuccess || tree_alloc(t, capacity) != GBP_OK) {
+  if (hipMalloc(&t->count, 4) != hipSuccess || hipMalloc(&t->hm, 64) != hipSuccess ||
+      tree_alloc(t, capacity) != GBP_OK) {
     gbp_tree_destroy(t);
     return GBP_E_ALLOC;
   }
-  if (hipMemset(t->count, 0, 4) != hipSuccess || hipMemset(t->vmax, 0, 32) != hipSuccess ||
-      hipMemset(t->hm, 0, 64) != hipSuccess) {
+  if (hipMemset(t->count, 0, 4) != hipSuccess || hipMemset(t->hm, 0, 64) != hipSuccess) {
     gbp_tree_destroy(t);
     return GBP_E_HIP;
   }
@@ -2383,9 +1470,7 @@ int gbp_tree_destroy(gbp_tree *t) {
   if (!t) return GBP_E_BAD_HANDLE;
   Guard g(t->device);
   (void)hipDeviceSynchronize();
-  void *ptrs[] = {t->v,    t->vf,   t->vh,   t->hm,   t->a,    t->g,    t->parent, t->count,
-                  t->vmax, t->isp,  t->isid, t->isv,  t->ibox, t->imed, t->ikey,   t->ival,
-                  t->isort};
+  void *ptrs[] = {t->v, t->vh, t->hm, t->a, t->g, t->parent, t->count};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   delete t;
@@ -2406,14 +1491,12 @@ int gbp_tree_reserve(gbp_tree *t, int64_t capacity, gbp_stream stream) {
     return rc;
   }
   HIPCHK_P(hipMemcpyAsync(t->v, old.v, 64 * old.cap, hipMemcpyDeviceToDevice, s));
-  HIPCHK_P(hipMemcpyAsync(t->vf, old.vf, 4 * NN_PAIR * ((old.cap + 1) / 2), hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->vh, old.vh, 2 * NH_ROW * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->a, old.a, 80 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->g, old.g, 8 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->parent, old.parent, 4 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipStreamSynchronize(s));
   (void)hipFree(old.v);
-  (void)hipFree(old.vf);
   (void)hipFree(old.vh);
   (void)hipFree(old.a);
   (void)hipFree(old.g);
@@ -2504,88 +1587,6 @@ int gbp_tree_device_ptrs(gbp_tree *t, double **states, int32_t **count) {
   return GBP_OK;
 }
 
-int gbp_tree_index_build(gbp_tree *t, const double *bounds, gbp_stream stream) {
-  if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
-  int64_t n = 0;
-  int rc = gbp_tree_size(t, &n, stream);
-  if (rc) return rc;
-  Guard g(t->device);
-  hipStream_t s = (hipStream_t)stream;
-  n &= ~(int64_t)1;  // whole row pairs: the tail then starts on a pair
-  n = std::min<int64_t>(n, NN_INDEX_MAX_ROWS);
-  if (n < 2) {
-    t->idx_n = 0;
-    return GBP_OK;
-  }
-  double bd[4];
-  if (bounds) {
-    for (int k = 0; k < 4; k++) bd[k] = bounds[k];
-  } else {  // the tree's own |x|, |y| bound
-    float vm[2];
-    if ((rc = d2h(vm, t->vmax, 2, s))) return rc;
-    HIPCHK_P(hipStreamSynchronize(s));
-    bd[0] = -(double)vm[0];
-    bd[1] = (double)vm[0];
-    bd[2] = -(double)vm[1];
-    bd[3] = (double)vm[1];
-  }
-  if (!(bd[1] > bd[0]) || !(bd[3] > bd[2]) || !std::isfinite(bd[1] - bd[0]) ||
-      !std::isfinite(bd[3] - bd[2])) {
-    bd[0] = bd[2] = 0.0;  // degenerate (one point, NaN): one key for all, still exact
-    bd[1] = bd[3] = 1.0;
-  }
-  if (n > t->idx_cap) {  // grow (contents rebuilt below)
-    const int64_t cap = std::max<int64_t>(n, 2 * t->idx_cap);
-    const int64_t nc = cap / NN_CH + 2;
-    void *old[] = {t->isp, t->isid, t->isv, t->ibox, t->imed, t->ikey, t->ival, t->isort};
-    HIPCHK_P(hipStreamSynchronize(s));
-    for (void *p : old)
-      if (p) (void)hipFree(p);
-    t->isp = nullptr;
-    t->isid = t->ival = nullptr;
-    t->isv = nullptr;
-    t->ibox = t->imed = nullptr;
-    t->ikey = nullptr;
-    t->isort = nullptr;
-    t->idx_cap = 0;
-    t->idx_n = 0;
-    size_t sort_bytes = 0;
-    if ((rc = gbp_internal_sort_pairs_u32(nullptr, &sort_bytes, nullptr, nullptr, nullptr, nullptr,
-                                          cap, s)))
-      return rc;
-    if (hipMalloc(&t->isp, 4 * NN_PAIR * ((cap + 1) / 2)) != hipSuccess ||
-        hipMalloc(&t->isid, 4 * cap) != hipSuccess || hipMalloc(&t->isv, 64 * cap) != hipSuccess ||
-        hipMalloc(&t->ibox, 64 * nc) != hipSuccess ||
-        hipMalloc(&t->imed, 4 * NN_PAIR * (nc / 2 + 1)) != hipSuccess ||
-        hipMalloc(&t->ikey, 8 * cap) != hipSuccess || hipMalloc(&t->ival, 4 * cap) != hipSuccess ||
-        hipMalloc(&t->isort, std::max<size_t>(sort_bytes, 256)) != hipSuccess)
-      return GBP_E_ALLOC;
-    t->isort_bytes = std::max<size_t>(sort_bytes, 256);
-    t->idx_cap = cap;
-  }
-  const unsigned gr = grid_for(n, TB, 4096);
-  hipLaunchKernelGGL(k_idx_keys, dim3(gr), dim3(TB), 0, s, t->v, n, bd[0], bd[1], bd[2], bd[3],
-                     t->ikey, t->ival);
-  size_t sb = t->isort_bytes;
-  if ((rc = gbp_internal_sort_pairs_u32(t->isort, &sb, t->ikey, t->ikey + t->idx_cap, t->ival,
-                                        t->isid, n, s)))
-    return rc;
-  hipLaunchKernelGGL(k_idx_rows, dim3(gr), dim3(TB), 0, s, t->v, t->isid, n, t->isp, t->isv);
-  hipLaunchKernelGGL(k_idx_boxes, dim3(grid_for((n + NN_CH - 1) / NN_CH, 64, 4096)), dim3(64), 0, s,
-                     t->isp, n, t->ibox, t->imed);
-  HIPCHK_P(hipGetLastError());
-  t->idx_n = (int32_t)n;
-  for (int k = 0; k < 4; k++) t->ibounds[k] = bd[k];
-  return GBP_OK;
-}
-
-int gbp_tree_index_size(gbp_tree *t, int64_t *indexed) {
-  if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
-  if (!indexed) return GBP_E_INVALID_ARG;
-  *indexed = t->idx_n;
-  return GBP_OK;
-}
-
 int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   if (!t || !out) return GBP_E_INVALID_ARG;
   if (max_batch < 1 || max_batch > (1 << 24)) return GBP_E_INVALID_ARG;
@@ -2595,7 +1596,6 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   if (!w) return GBP_E_ALLOC;
   w->device = t->device;
   w->num_cus = t->num_cus;
-  w->nn_mode = t->opt_nn_filter;
   w->nn_stats = t->opt_nn_stats;
   w->bmax = max_batch;
   w->ntiles = (max_batch + CB - 1) / CB + 1;
@@ -2603,7 +1603,7 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   const size_t bytes = sizeof(gbp_plan_status) + 8 * w->ntiles + 64 * b + 4 * b + 64 * b + 4 * b +
                        m * (64 + 80 + 64 + 4 + 4) + b * (4 + 4 + 64 + 80 + 4 + 4) +
                        b * (4 + 4 + 64 + 80 + 4) + NN_MAX_CHUNKS * b * (16 + 16) + 64 * b + 256 +
-                       4 * NN_QCELLS + 4 * NN_QCELLS * b + 4 * b + 64 * 256;
+                       64 * 256;
   if (hipMalloc(&w->block, bytes) != hipSuccess) {
     delete w;
     return GBP_E_ALLOC;
@@ -2634,23 +1634,13 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->kf = carve<uint32_t>(p, b);
   w->nn_d = carve<double>(p, 2 * NN_MAX_CHUNKS * b);   // k_nn_mfma: float4 per slot
   w->nn_i = carve<int32_t>(p, 4 * NN_MAX_CHUNKS * b);  // k_nn_mfma: int4 per slot
-  w->bcnt = carve<int32_t>(p, NN_QCELLS);
-  w->bq = carve<int32_t>(p, (size_t)NN_QCELLS * b);
-  w->qpt = carve<float>(p, b);
-  if ((size_t)(p - (char *)w->block) > bytes || hipMemset(w->tiles, 0, 8 * w->ntiles) != hipSuccess ||
-      hipMemset(w->bcnt, 0, 4 * NN_QCELLS) != hipSuccess) {
+  if ((size_t)(p - (char *)w->block) > bytes || hipMemset(w->tiles, 0, 8 * w->ntiles) != hipSuccess) {
     (void)hipFree(w->block);
     delete w;
     return GBP_E_HIP;
   }
   hipLaunchKernelGGL(k_plan_reset, dim3(1), dim3(1), 0, nullptr, w->st, (int64_t)0);
-  if (hipStreamCreateWithFlags(&w->aux, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&w->ev_a, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&w->ev_b, hipEventDisableTiming) != hipSuccess ||
-      hipDeviceSynchronize() != hipSuccess) {
-    if (w->ev_a) (void)hipEventDestroy(w->ev_a);
-    if (w->ev_b) (void)hipEventDestroy(w->ev_b);
-    if (w->aux) (void)hipStreamDestroy(w->aux);
+  if (hipDeviceSynchronize() != hipSuccess) {
     (void)hipFree(w->block);
     delete w;
     return GBP_E_HIP;
@@ -2664,9 +1654,6 @@ int gbp_plan_ws_destroy(gbp_plan_ws *w) {
   Guard g(w->device);
   (void)hipDeviceSynchronize();
   if (w->block) (void)hipFree(w->block);
-  if (w->ev_a) (void)hipEventDestroy(w->ev_a);
-  if (w->ev_b) (void)hipEventDestroy(w->ev_b);
-  if (w->aux) (void)hipStreamDestroy(w->aux);
   delete w;
   return GBP_OK;
 }
@@ -2715,8 +1702,6 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
     return GBP_E_INVALID_ARG;
   Guard g(t->device);
   hipStream_t s = (hipStream_t)stream;
-  const bool overlap = t->opt_plan_overlap && !t->sampling.state_flag && n_halves > 1;
-  bool drawn = false;  // this half's stage 0 already ran on the second stream
   for (int32_t i = 0; i < n_halves; i++) {
     const int32_t h = first_half + i;
     const int k = h & 1;
@@ -2724,37 +1709,12 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
     const int dir = k ? GBP_REVERSE : GBP_FORWARD;
     const uint64_t ts = k ? stream_b : stream_a;
     const int64_t tb = (int64_t)(h >> 1) * batch;
-    int fs = i == 0 ? first_stage : 0;
-    if (drawn) {
-      HIPCHK_P(hipStreamWaitEvent(s, w->ev_b, 0));
-      fs = std::max(fs, 1);
-    }
-    auto stages = [&](gbp_tree *TT, gbp_tree *OO, int32_t hh, int d, uint64_t tst, int64_t tbase,
-                      int first, int last, hipStream_t st) {
-      return t->storage == GBP_STORAGE_F32
-                 ? enqueue_stages<float>(t, w, TT, OO, hh, d, batch, seed, tst, tbase, adaptive, first,
-                                         last, st)
-                 : enqueue_stages<double>(t, w, TT, OO, hh, d, batch, seed, tst, tbase, adaptive,
-                                          first, last, st);
-    };
-    int rc = stages(T, O, h, dir, ts, tb, fs, 1, s);
-    if (rc) return rc;
-    drawn = false;
-    if (overlap && i + 1 < n_halves) {
-      // half h + 1's draws once this half's compaction has read its own
-      // (the draw buffers are shared), beside this half's search and
-      // validation (VALU draws next to matrix-core and memory-latency work)
-      const int32_t h1 = h + 1;
-      const int k1 = h1 & 1;
-      HIPCHK_P(hipEventRecord(w->ev_a, s));
-      HIPCHK_P(hipStreamWaitEvent(w->aux, w->ev_a, 0));
-      rc = stages(k1 ? Tb : Ta, k1 ? Ta : Tb, h1, k1 ? GBP_REVERSE : GBP_FORWARD,
-                  k1 ? stream_b : stream_a, (int64_t)(h1 >> 1) * batch, 0, 0, w->aux);
-      if (rc) return rc;
-      HIPCHK_P(hipEventRecord(w->ev_b, w->aux));
-      drawn = true;
-    }
-    rc = stages(T, O, h, dir, ts, tb, std::max(fs, 2), 5, s);
+    const int fs = i == 0 ? first_stage : 0;
+    const int rc = t->storage == GBP_STORAGE_F32
+                       ? enqueue_stages<float>(t, w, T, O, h, dir, batch, seed, ts, tb, adaptive, fs,
+                                               5, s)
+                       : enqueue_stages<double>(t, w, T, O, h, dir, batch, seed, ts, tb, adaptive, fs,
+                                                5, s);
     if (rc) return rc;
   }
   return GBP_OK;
@@ -2849,8 +1809,7 @@ int gbp_tree_nearest_dev(gbp_plan_ws *w, gbp_tree *T, int64_t n, const double *q
   Guard g(w->device);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_set_queries, dim3(1), dim3(1), 0, s, w->st, (int32_t)n);
-  return nn_launch(w, &w->st->n_targets, queries, nullptr, T, index, w->num_cus, s,
-                   T->idx_n > 0);
+  return nn_launch(w, &w->st->n_targets, queries, nullptr, T, index, w->num_cus, s);
 }
 
 int gbp_plan_resolve_host(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int direction,

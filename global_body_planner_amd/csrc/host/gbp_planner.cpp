@@ -1548,12 +1548,6 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
   chk(gbp_tree_init(D.tree[1], s_goal.data(), D.stream), "tree init");
   chk(gbp_plan_reset(D.ws, extend_counter_, D.stream), "plan reset");
   int64_t known[2] = {1, 1};
-  // nearest-neighbour indices over the terrain's (x, y) box (GBP_OPT_NN_INDEX)
-  int64_t opt_index = 0;
-  chk(gbp_terrain_get_option(h, GBP_OPT_NN_INDEX, &opt_index), "option");
-  const bool use_index = opt_index > 0;  // the smallest tree searched through its index
-  double bounds[4];
-  chk(gbp_terrain_info(h, nullptr, nullptr, nullptr, bounds, nullptr), "terrain info");
   // half h extends tree h % 2 toward its draws [(h / 2) B, (h / 2 + 1) B)
   // groups grow geometrically: a short search is not charged a long group's
   // tail of gated half-iterations, a long one amortises the status read
@@ -1574,8 +1568,7 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
                              D.stream),
             "tree reserve");
     }
-    // the group's halves, each half's draws beside the previous half's connect
-    // stages (gbp_plan_halves_dev, GBP_OPT_PLAN_OVERLAP)
+    // the group's halves, one stream-ordered kernel sequence
     chk(gbp_plan_halves_dev(h, D.ws, D.tree[0], D.tree[1], half, group, batch, seed_, tstream[0],
                             tstream[1], adaptive, 0, D.stream),
         "plan halves");
@@ -1600,13 +1593,6 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
     if (ps.error & 1u) throw EngineError(GBP_E_HIP, "device planner loop: look-back spin exhausted");
     if (ps.error) throw EngineError(GBP_E_SHAPE, "device planner loop: a tree ran out of capacity");
     for (int k = 0; k < 2; k++) chk(gbp_tree_size(D.tree[k], &known[k], D.stream), "tree size");
-    if (use_index)  // keep each tree's nearest-neighbour index within 1/16 of its size
-      for (int k = 0; k < 2; k++) {
-        int64_t ix = 0;
-        chk(gbp_tree_index_size(D.tree[k], &ix), "index size");
-        if (known[k] >= opt_index && known[k] - ix > std::max<int64_t>(opt_index / 8, ix / 16))
-          chk(gbp_tree_index_build(D.tree[k], bounds, D.stream), "index build");
-      }
     half += group;
     if (ps.done) {
       goal_found = true;
@@ -2106,13 +2092,7 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     if (p->fragile_eps_fm)
       chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_FRAGILE_EPS, p->fragile_eps_fm),
           "fragile eps");
-    if (p->nn_index)
-      chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_NN_INDEX, p->nn_index < 0 ? 0 : p->nn_index),
-          "nn index");
-    chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_NN_FILTER, p->nn_filter), "nn filter");
     chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_NN_STATS, p->nn_stats), "nn stats");
-    if (p->no_overlap)
-      chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_PLAN_OVERLAP, 0), "plan overlap");
     RRTStarConnectClass planner;  // is-a RRTConnectClass: algorithm 0 uses the plain build
     planner.setSeed(p->seed);
     planner.set_state_direction_sampling(p->sampling.state_flag != 0, p->sampling.state_p,

@@ -396,20 +396,6 @@ class DeviceTree:
         check(self._lib.gbp_tree_append_host(self._h, s.shape[0], _np_ptr(s), _np_ptr(a), _np_ptr(p),
                                              None), "tree_append")
 
-    def build_index(self, bounds=None):
-        """gbp_tree_index_build: index the tree's vertices for pruned nearest-
-        neighbour searches (bounds = (x0, xN, y0, yN) of the Morton key, None:
-        the tree's own |x|, |y| bound).  Returns the number of vertices indexed."""
-        b = None if bounds is None else np.ascontiguousarray(bounds, np.float64).reshape(4)
-        check(self._lib.gbp_tree_index_build(self._h, None if b is None else _np_ptr(b), None),
-              "tree_index_build")
-        return self.index_size()
-
-    def index_size(self):
-        c = ctypes.c_int64(0)
-        check(self._lib.gbp_tree_index_size(self._h, ctypes.byref(c)), "tree_index_size")
-        return c.value
-
     def read(self):
         """(states [n][8], actions [n][10], parents [n], g [n]) numpy."""
         n = len(self)
@@ -459,6 +445,15 @@ class PlanWorkspace:
 
     def reset(self, device=0):
         check(self._lib.gbp_plan_reset(self._h, 0, _stream(device)), "plan_reset")
+
+    def halves(self, terrain, ta, tb, first_half, n_halves, batch, seed, stream_a=101,
+               stream_b=102, adaptive=False, first_stage=0, device=0):
+        """gbp_plan_halves_dev: enqueue half-iterations first_half ..
+        first_half + n_halves - 1 of the device planner loop (no host sync)."""
+        check(self._lib.gbp_plan_halves_dev(terrain._h, self._h, ta._h, tb._h, int(first_half),
+                                            int(n_halves), int(batch), int(seed), int(stream_a),
+                                            int(stream_b), int(bool(adaptive)), int(first_stage),
+                                            _stream(device)), "plan_halves")
 
     def nearest(self, tree, queries):
         """gbp_tree_nearest_dev: nearest vertex of `tree` per query (device tensors)."""

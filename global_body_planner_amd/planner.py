@@ -28,9 +28,8 @@ class PlanParams(ctypes.Structure):
                 ("max_time", _D), ("seed", ctypes.c_uint64), ("post_process", ctypes.c_int),
                 ("algorithm", ctypes.c_int), ("max_time_opt", _D),
                 ("sampling", _lib.Sampling), ("fragile_eps_fm", ctypes.c_int64),
-                ("adaptive", ctypes.c_int), ("nn_index", ctypes.c_int64),
-                ("nn_filter", ctypes.c_int), ("nn_stats", ctypes.c_int),
-                ("no_overlap", ctypes.c_int), ("max_halves", ctypes.c_int64),
+                ("adaptive", ctypes.c_int), ("nn_stats", ctypes.c_int),
+                ("max_halves", ctypes.c_int64),
                 ("tree_capacity", ctypes.c_int64), ("tree_v", _P * 2), ("tree_a", _P * 2),
                 ("tree_parent", _P * 2), ("tree_g", _P * 2)]
 
@@ -105,8 +104,8 @@ def start_goal_state(height, x, y):
 
 def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018,
                      post_process=False, device=0, capacity=4096, algorithm=0, max_time_opt=0.0,
-                     sampling=None, fragile_eps=None, adaptive=False, nn_index=0,
-                     nn_filter=0, nn_stats=False, overlap=True, max_halves=0, trees=False,
+                     sampling=None, fragile_eps=None, adaptive=False, nn_stats=False,
+                     max_halves=0, trees=False,
                      tree_capacity=1 << 18):
     """Plan start -> goal on terrain `data` (terrain_data.TerrainData).
 
@@ -126,10 +125,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     sampling: a _lib.Sampling (direction-biased draws, params.yaml:21-27);
     fragile_eps: a wider FRAGILE margin (forces host re-decisions: tests);
     adaptive: the adaptive-step pair checks (params.yaml:16);
-    nn_index: GBP_OPT_NN_INDEX, the smallest tree the device loop searches
-      through its nearest-neighbour index (0: the default, never; < 0: never);
-    nn_filter: GBP_OPT_NN_FILTER, the nearest-neighbour scan (0 matrix cores,
-      1 packed fp32: same results);
+    nn_stats: count the matrix-core search's fp64 re-checks (diagnostics);
     max_halves: algorithms 0, 1, 3 stop after this many half-iterations (a
       replayable run; 0 = no limit);
     trees: also return the final trees (out["a"], out["b"]: v, act, parent, g;
@@ -153,10 +149,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
         p.sampling = sampling
     p.fragile_eps_fm = 0 if fragile_eps is None else int(round(fragile_eps * 1e15))
     p.adaptive = int(bool(adaptive))
-    p.nn_index = int(nn_index)
-    p.nn_filter = int(nn_filter)
     p.nn_stats = int(bool(nn_stats))
-    p.no_overlap = 0 if overlap else 1
     p.max_halves = int(max_halves)
     tb = []
     if trees:

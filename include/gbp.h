@@ -149,23 +149,12 @@ int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage,
                                     1e-12, the smallest accepted): a wider margin flags
                                     and re-decides more attempts on the host, with the
                                     same results (tests use it to force host resolutions) */
-#define GBP_OPT_NN_INDEX     16  /* v > 0: the device planner loop finds the targets'
-                                    nearest vertices through a tree's index
-                                    (gbp_tree_index_build) once it holds >= v vertices;
-                                    0 (default): the full filtered scan, measured faster
-                                    at the planner's tree sizes.  Same
-                                    results either way.                              */
-#define GBP_OPT_NN_FILTER    17  /* the nearest-neighbour scan's filter: 0 (default)
-                                    fp16-split scores on the matrix cores (k_nn_mfma,
-                                    DESIGN §5.3), 1 the packed fp32 VALU filter
-                                    (k_nn_filter).  Same results either way.         */
+/* 16, 17, 19: retired (round 4) — a Morton-sorted nearest-neighbour index, the
+   packed fp32 VALU filter and a two-stream draw overlap, each measured no
+   faster than the default path; setting them is an error     */
 #define GBP_OPT_NN_STATS     18  /* 1: the matrix-core search counts its fp64 re-checks
                                     in gbp_plan_status.stat_nn_* (diagnostics: costs
                                     same-address atomics; default 0)                  */
-#define GBP_OPT_PLAN_OVERLAP 19  /* 1: gbp_plan_halves_dev draws half h + 1's targets on
-                                    a second stream beside half h's search and
-                                    validation; 0 (default): one stream (measured
-                                    faster: 91.9 vs 86.1 M extends/s) */
 #define GBP_KERNEL_DIRECT     0  /* one lane per attempt                              */
 #define GBP_KERNEL_PERSISTENT 1  /* persistent waves, lanes re-packed per sample      */
 int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value);
@@ -401,22 +390,9 @@ int gbp_tree_append_host(gbp_tree *tree, int64_t n, const double *states, const 
  * (n <= its max_batch). */
 int gbp_tree_nearest_dev(gbp_plan_ws *ws, gbp_tree *tree, int64_t n, const double *queries,
                          int32_t *index, gbp_stream stream);
-/* The tree's nearest-neighbour index: PlannerClass::getNearestNeighbor
- * (planner_class.cpp:185-200) made sub-linear for searches with many queries.
- * Vertices [0, n) — n = the tree's size now, rounded down to even; the call
- * synchronises the stream — are sorted by the Morton key of (x, y) over
- * bounds = {x0, xN, y0, yN} (NULL: the tree's own |x|, |y| bound) and cut into
- * chunks of 64 with the 8-D box of their fp32 rows.  gbp_tree_nearest_dev and
- * the planner loop's target searches then skip every chunk whose box is
- * provably farther than a known vertex and scan the vertices appended since
- * the build in full: the same indices as without the index, ties included.
- * Rebuild as the tree grows (buildRRTConnectDevice does once the unindexed
- * tail exceeds an eighth of the index). */
-int gbp_tree_index_build(gbp_tree *tree, const double *bounds, gbp_stream stream);
-int gbp_tree_index_size(gbp_tree *tree, int64_t *indexed);
 /* the tree's device arrays (for gbp_nearest_batch_dev and the like): READ ONLY —
- * vertices are written through init / append only, which also keep the fp32
- * mirror and magnitude bound the nearest-neighbour filter relies on */
+ * vertices are written through init / append only, which also keep the fp16
+ * rows and magnitude bounds the matrix-core search relies on */
 int gbp_tree_device_ptrs(gbp_tree *tree, double **states, int32_t **count);
 
 /* ---- the device planner loop (RRTConnectClass::runRRTConnect,
@@ -467,8 +443,8 @@ typedef struct {
    * half-chunks of 16 rows re-checked, and segments scanned in full */
   int64_t stat_nn_rechecks, stat_nn_scans;
   /* the half whose targets were compacted last, and the counters before it:
-   * a compaction re-run for the same half (after a FRAGILE halt) starts from
-   * them again */
+   * a compaction re-run for the same half (resumed at stage 1 after a FRAGILE
+   * halt) starts from them again */
   int32_t ext_half, ext_pad;
   int64_t ext_prev, stat_targets_prev;
 } gbp_plan_status;
@@ -484,9 +460,10 @@ int gbp_plan_status_read(gbp_plan_ws *ws, gbp_plan_status *out, gbp_stream strea
 /* half-iterations first_half .. first_half + n_halves - 1 (half h extends tree
  * h % 2: Ta FORWARD toward target stream stream_a, Tb REVERSE toward
  * stream_b, draws from index (h / 2) * batch), the first from first_stage:
- * gbp_plan_half_dev for each; with GBP_OPT_PLAN_OVERLAP (and draws that are
- * not direction-biased, so they read only the terrain) half h + 1's draws
- * (stage 0) run on a second stream once half h's compaction is done */
+ * gbp_plan_half_dev for each.  first_stage > 0 resumes a half that halted
+ * (gbp_plan_resolve_host's *resume_stage); a fresh half starts at stage 0.
+ * Half numbers identify a half's draws and must increase between
+ * gbp_plan_reset calls. */
 int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *ws, gbp_tree *Ta, gbp_tree *Tb,
                         int32_t first_half, int32_t n_halves, int64_t batch, uint64_t seed,
                         uint64_t stream_a, uint64_t stream_b, int adaptive, int first_stage,

@@ -616,11 +616,7 @@ typedef struct {
                           // params.yaml:21-27); all zero = off, the reference default
   int64_t fragile_eps_fm; // FRAGILE margin in 1e-15 units (GBP_OPT_FRAGILE_EPS); 0 = default
   int adaptive;           // state_action_pair_check_adaptive_step_size_flag (params.yaml:16)
-  int64_t nn_index;       // GBP_OPT_NN_INDEX: trees of at least this many vertices search
-                          // through their index (0 = the handle's default, off; < 0 = off)
-  int nn_filter;          // GBP_OPT_NN_FILTER: 0 matrix cores (default), 1 packed fp32
   int nn_stats;           // GBP_OPT_NN_STATS: count the search's fp64 re-checks (diagnostics)
-  int no_overlap;         // 1: GBP_OPT_PLAN_OVERLAP off (0 = the handle's default)
   int64_t max_halves;     // algorithms 0, 1, 3: stop after this many half-iterations
                           // (0 = no limit): a run that can be replayed exactly
   int64_t tree_capacity;  // rows of the tree_* buffers (0 = the trees are not returned)

@@ -50,50 +50,6 @@ def test_device_loop_equals_host_batched(gpu, name, xy, batch, seed):
           f"{dev['time_to_first']:.4f} s in {dev['status_reads']} status reads")
 
 
-def test_device_loop_fp32_filter_equals_host_batched(gpu):
-    """The device loop with the packed fp32 nearest-neighbour filter
-    (GBP_OPT_NN_FILTER 1) builds the same trees and path as the host batched
-    planner (and so as the default matrix-core search)."""
-    data = td.by_name("synth-rough-256")
-    O = oracle.OracleTerrain.from_data(data)
-    start, goal = _start_goal(O, 1.0, 2.55, 4.02, 2.55)
-    kw = dict(batch=4096, max_time=120.0, seed=3)
-    host = planner.plan_rrt_connect(data, start, goal, **kw)
-    dev = planner.plan_rrt_connect_device(data, start, goal, nn_filter=1, **kw)
-    assert host["found"] == 1 and dev["found"] == 1
-    assert np.array_equal(dev["states"], host["states"])
-    for k in ("vertices_a", "vertices_b", "targets", "extends", "attempts_checked", "connects"):
-        assert dev[k] == host[k], (k, dev[k], host[k])
-
-
-@pytest.mark.parametrize("name,xy,batch,seed,nn_index", [
-    ("synth-rough-256", (1.0, 2.55, 4.02, 2.55), 4096, 3, 8),
-    ("slope-gridmap", (1.0, 0.0, 8.0, 0.0), 512, 3, 32),
-    ("synth-rough-1024", (1.0, 10.23, 6.8, 10.23), 8192, 5, 64),
-])
-def test_device_loop_nn_index_equals_host_batched(gpu, name, xy, batch, seed, nn_index):
-    """The targets' nearest vertices through the trees' indices (GBP_OPT_NN_INDEX
-    = a small tree size, so the index is built early and rebuilt often as the
-    trees grow; k_nnq_* + k_nn_pruned with an unindexed tail) give the same
-    trees and path as the host batched planner's fp64 scans, bit for bit."""
-    data = td.by_name(name)
-    O = oracle.OracleTerrain.from_data(data)
-    start, goal = _start_goal(O, *xy)
-    kw = dict(batch=batch, max_time=120.0, seed=seed)
-    host = planner.plan_rrt_connect(data, start, goal, **kw)
-    dev = planner.plan_rrt_connect_device(data, start, goal, nn_index=nn_index, **kw)
-    assert host["found"] == 1 and dev["found"] == 1
-    check_path(O, dev, start, goal)
-    assert np.array_equal(dev["states"], host["states"])
-    assert np.array_equal(dev["actions"], host["actions"])
-    for k in ("vertices_a", "vertices_b", "targets", "extends", "attempts_checked", "connects",
-              "fragile_resolved", "depth_capped"):
-        assert dev[k] == host[k], (k, dev[k], host[k])
-    assert max(dev["vertices_a"], dev["vertices_b"]) >= 2 * nn_index  # the index was used
-    print(f"{name} batch {batch} index >= {nn_index}: {dev['vertices_a']}+{dev['vertices_b']} "
-          f"vertices, {dev['extends']} extends")
-
-
 @pytest.mark.parametrize("batch,seed", [(4096, 3), (1024, 8)])
 def test_device_loop_forced_halts_equal_host_batched(gpu, batch, seed):
     """Halt -> gbp_plan_resolve_host -> resume in every stage.  A FRAGILE
@@ -194,26 +150,18 @@ def test_device_tree_api(gpu):
         t.append(s[:1], a[:1], np.array([99], np.int32))  # parent out of range
 
 
-@pytest.mark.parametrize("indexed,nn_filter", [(0.0, 0), (0.0, 1), (1.0, 0), (0.7, 0)])
-def test_tree_nearest_fp32_filter_exact(gpu, indexed, nn_filter):
-    """gbp_tree_nearest_dev (k_nn_filter: fp32 filter, fp64 re-check of the
-    candidates) returns exactly the fp64 scan's index (gbp_nearest_batch_dev,
+def test_tree_nearest_exact(gpu):
+    """gbp_tree_nearest_dev (k_nn_mfma + k_nn_hreduce: fp16-split scores on the
+    matrix cores, a rigorous threshold and fp64 re-checks)
+    returns exactly the fp64 scan's index (gbp_nearest_batch_dev,
     planner_class.cpp:185-200: lowest index among equal distances) on random
     states and on the cases that stress the filter: exact duplicates (ties),
-    vertices that are equal in fp32 but distinct in fp64 (more than NN_CAND of
-    them in one chunk: the overflow scan), magnitudes past the filter's bound
-    (the fp64 scan) and NaN queries (index 0).  `indexed`: the fraction of the
-    tree's vertices put in its nearest-neighbour index (gbp_tree_index_build,
-    k_nn_pruned) before the rest are appended (0: no index; 0.7: an unindexed
-    tail scanned in full beside the pruned chunks).  `nn_filter`
-    (GBP_OPT_NN_FILTER): 0 the fp16-split scores on the matrix cores
-    (k_nn_mfma + k_nn_hreduce), 1 the packed fp32 filter (k_nn_filter); the
-    offsets of 300 and 5000 put the tree past the fp16 rows' range (|v| >= 128:
-    the fp64 scan)."""
+    vertices equal in fp16 / fp32 but distinct in fp64, near-equal distances
+    on 1e-8 shells, magnitudes past the fp16 rows' range (|v| >= 128: the
+    tree is searched in fp64) and NaN queries (index 0)."""
     import global_body_planner_amd as gbp
     data = td.synth_rough(256)
     T = gbp.Terrain.from_data(data, device=0)
-    T.set_option(L.OPT_NN_FILTER, nn_filter)
     rng = np.random.default_rng(5)
     nq = 4096
     ws = gbp.PlanWorkspace(T, nq)
@@ -221,13 +169,7 @@ def test_tree_nearest_fp32_filter_exact(gpu, indexed, nn_filter):
     def check(verts, q, label):
         tree = gbp.DeviceTree(verts[0], device=0, capacity=verts.shape[0] + 1)
         n = verts.shape[0]
-        k = max(1, int(round(indexed * n))) if indexed else n
-        tree.append(verts[1:k], np.zeros((k - 1, 10)), np.zeros(k - 1, np.int32))
-        if indexed:
-            got_n = tree.build_index(data.bounds if label == "random" else None)
-            assert got_n == (k & ~1)
-            if k < n:
-                tree.append(verts[k:], np.zeros((n - k, 10)), np.zeros(n - k, np.int32))
+        tree.append(verts[1:], np.zeros((n - 1, 10)), np.zeros(n - 1, np.int32))
         qt = torch.from_numpy(np.ascontiguousarray(q)).cuda()
         got = ws.nearest(tree, qt).cpu().numpy()
         ref, _ = gbp.nearest(qt, torch.from_numpy(verts).cuda())
@@ -239,19 +181,18 @@ def test_tree_nearest_fp32_filter_exact(gpu, indexed, nn_filter):
     verts = T.sample_states(20000, seed=41, stream_id=1)[0].cpu().numpy()
     q = T.sample_states(nq, seed=42, stream_id=2)[0].cpu().numpy()
     check(verts, q, "random")
-    # odd vertex counts (a chunk ending inside a row pair) and a single vertex
+    # odd vertex counts (a chunk ending inside a unit) and a single vertex
     for nv in (4097, 20000 - 63, 1):
         check(np.ascontiguousarray(verts[:nv]), q, f"odd {nv}")
-    # far from the origin: the dot-product form's cancellation widens the
-    # threshold (eps ~ 10 u R^2), so more candidates and the overflow scan
-    for off in (40.0, 300.0, 5000.0):
+    # far from the origin (|v| near the fp16 rows' bound, and past it: fp64)
+    for off in (40.0, 120.0, 300.0, 5000.0):
         sh = np.zeros(8)
         sh[:2] = off
         check(verts + sh, q + sh, f"offset {off}")
     # near-equal distances: 5 vertices on a unit shell around each query, radii
-    # 1 + O(1e-8), so the fp32 scores order them almost at random and only the
-    # threshold keeps the fp64 minimiser (tests/test_nn_filter_bound.py)
-    for off in (0.0, 300.0):
+    # 1 + O(1e-8): the scores order them almost at random, only the threshold
+    # keeps the fp64 minimiser (tests/test_nn_mfma_bound.py)
+    for off in (0.0, 100.0):
         sh = np.zeros(8)
         sh[:2] = off
         dirs = rng.normal(size=(nq, 5, 8))
@@ -259,8 +200,8 @@ def test_tree_nearest_fp32_filter_exact(gpu, indexed, nn_filter):
         rad = 1.0 + rng.normal(scale=1e-8, size=(nq, 5, 1))
         shell = np.ascontiguousarray(((q + sh)[:, None, :] + dirs * rad).reshape(-1, 8))
         check(shell, q + sh, f"shell {off}")
-    # clusters: 64 centres, 300 vertices each within 1e-9 (fp32-identical),
-    # exact duplicates among them; queries at and near the centres
+    # clusters: 64 centres, 300 vertices each within 1e-9, exact duplicates
+    # among them; queries at and near the centres
     base = verts[:64]
     cl = np.repeat(base, 300, axis=0) + rng.normal(scale=1e-9, size=(64 * 300, 8))
     cl[::7] = np.repeat(base, 300, axis=0)[::7]          # exact copies of a centre
@@ -269,10 +210,35 @@ def test_tree_nearest_fp32_filter_exact(gpu, indexed, nn_filter):
     qc = np.repeat(base, nq // 64, axis=0) + rng.normal(scale=1e-10, size=(nq, 8))
     qc[::3] = np.repeat(base, nq // 64, axis=0)[::3]
     check(cl, qc, "clusters")
-    # magnitudes beyond the fp32 bound, and NaN queries
+    # magnitudes beyond the fp16 rows' range, and NaN queries
     big = verts.copy()
     big[::1000, 2] = 3e16
     qn = q.copy()
     qn[::97, 4] = np.nan
     qn[5::101, 0] = 2e16
     check(big, qn, "big/nan")
+
+
+def test_append_past_capacity_is_reported_not_faulted(gpu):
+    """A device-loop append beyond a tree's reserved capacity (the caller's
+    job, gbp_tree_reserve) is dropped: status.error bit 1 is set, the gate
+    stops every later launch of the sequence (no search reads rows past the
+    capacity) and the tree's count stays at its capacity."""
+    import global_body_planner_amd as gbp
+    data = td.synth_rough(256)
+    T = gbp.Terrain.from_data(data, device=0)
+    O = oracle.OracleTerrain.from_data(data)
+    start, goal = _start_goal(O, 1.0, 2.55, 4.02, 2.55)
+    ws = gbp.PlanWorkspace(T, 4096)
+    ta = gbp.DeviceTree(start, device=0, capacity=2)
+    tb = gbp.DeviceTree(goal, device=0, capacity=2)
+    ws.reset(0)
+    st = None
+    for h in range(40):   # until an extend appends more than one vertex to a 2-row tree
+        ws.halves(T, ta, tb, h, 1, 4096, seed=3)
+        st = ws.status()
+        if st["error"] or st["done"] or st["halt"]:
+            break
+    assert st["error"] & 2, (st["error"], st["done"], st["halt"])
+    assert len(ta) <= 2 and len(tb) <= 2
+    torch.cuda.synchronize()

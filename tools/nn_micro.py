@@ -21,14 +21,12 @@ def main():
     p.add_argument("--queries", type=int, default=20480)
     p.add_argument("--verts", default="5000,20000")
     p.add_argument("--launches", type=int, default=10)
-    p.add_argument("--filters", default="0,1", help="GBP_OPT_NN_FILTER values (0 MFMA, 1 fp32)")
     a = p.parse_args()
     data = td.synth_rough(1024)
     T = gbp.Terrain.from_data(data, device=0)
     q = T.sample_states(a.queries, seed=3, stream_id=2)[0]
     rows = []
-    for nv, filt in [(int(v), int(f)) for v in a.verts.split(",") for f in a.filters.split(",")]:
-        T.set_option(gbp._lib.OPT_NN_FILTER, filt)
+    for nv in [int(v) for v in a.verts.split(",")]:
         T.set_option(gbp._lib.OPT_NN_STATS, 1)
         ws = gbp.PlanWorkspace(T, a.queries)
         vs, _ = T.sample_states(nv, seed=4, stream_id=1)
@@ -60,7 +58,7 @@ def main():
         torch.cuda.synchronize()
         ms_old = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev2]))
         pairs = a.queries * nv
-        rows.append({"filter": filt, "queries": a.queries,
+        rows.append({"queries": a.queries,
                      "verts": nv, "ms": round(ms, 4), "pairs_per_s": round(pairs / (ms * 1e-3), 1),
                      "ms_nearest_batch": round(ms_old, 4), "match": ok,
                      "rechecks_per_query": nst["stat_nn_rechecks"] / a.queries,

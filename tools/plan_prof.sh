@@ -1,14 +1,13 @@
 #!/bin/bash
-# Kernel-trace profiles of device-loop planner runs (tools/plan_run.py), one
-# per GBP_OPT_NN_FILTER setting given in $NN (default: "0 1" = matrix cores, fp32),
-# and the top kernels of each.
+# Kernel-trace profile of a device-loop planner run (tools/plan_run.py) and its
+# top kernels.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 T=${PLAN_TIME:-8}
-for nn in ${NN:-0 1}; do
+for nn in 0; do
   d=gpurun_out/pp_$nn
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o run -- \
-      python3 tools/plan_run.py --max-time $T --nn-filter $nn > $d.log 2>&1 || { echo "run nn=$nn failed"; tail -5 $d.log; exit 1; }
+      python3 tools/plan_run.py --max-time $T > $d.log 2>&1 || { echo "run nn=$nn failed"; tail -5 $d.log; exit 1; }
   grep found $d.log
   f=$(find $d -name "*kernel_stats.csv" | head -1)
   python3 - "$f" <<'PY'

@@ -24,11 +24,7 @@ def main():
     p.add_argument("--seed", type=int, default=20251018)
     p.add_argument("--algorithm", type=int, default=3)
     p.add_argument("--runs", type=int, default=1)
-    p.add_argument("--nn-index", type=int, default=0,
-                   help="GBP_OPT_NN_INDEX (0: default = no index)")
-    p.add_argument("--nn-filter", type=int, default=0, help="GBP_OPT_NN_FILTER (0 MFMA, 1 fp32)")
     p.add_argument("--nn-stats", type=int, default=0, help="GBP_OPT_NN_STATS (re-check counters)")
-    p.add_argument("--overlap", type=int, default=1, help="GBP_OPT_PLAN_OVERLAP")
     a = p.parse_args()
     data = td.by_name(a.terrain)
     (xs, ys), (xg, yg), b = PAIRS[a.terrain]
@@ -38,16 +34,13 @@ def main():
     goal = planner.start_goal_state(h[1], xg, yg)
     for k in range(a.runs):
         out = planner.plan_rrt_connect(data, start, goal, batch=a.batch or b, max_time=a.max_time,
-                                       seed=a.seed + k, algorithm=a.algorithm, nn_index=a.nn_index,
-                                       nn_filter=a.nn_filter, nn_stats=a.nn_stats,
-                                       overlap=bool(a.overlap))
+                                       seed=a.seed + k, algorithm=a.algorithm,
+                                       nn_stats=a.nn_stats)
         run_t = out["time_to_first"] if out["found"] else out["total_time"]
         print(json.dumps({k2: out[k2] for k2 in ("found", "time_to_first", "total_time", "iterations",
                                                    "extends", "vertices_a", "vertices_b", "targets", "nn_rechecks", "nn_scans",
                                                    "fragile_resolved", "status_reads")}
-                         | {"extends_per_s": out["extends"] / max(run_t, 1e-9),
-                            "nn_index": a.nn_index, "nn_filter": a.nn_filter,
-                            "overlap": a.overlap}), flush=True)
+                         | {"extends_per_s": out["extends"] / max(run_t, 1e-9)}), flush=True)
 
 
 if __name__ == "__main__":
