@@ -609,6 +609,89 @@ __global__ __launch_bounds__(256) void k_neighbors(int64_t n_query, const double
   }
 }
 
+// PlannerClass::neighborhoodN (planner_class.cpp:151-171): the n_nearest
+// vertices of smallest stateDistance(q, v), in the order the reference pops
+// its min-heap of std::pair<double, int> (std::greater): ascending distance,
+// equal distances by ascending index.  A NaN distance orders after every
+// number (the reference's heap order is then unspecified).  One wave per
+// query: lane l holds the l-th smallest (distance, index) seen so far; the
+// tree streams past in chunks of 64 vertices (one coalesced 64-B row per
+// lane); a chunk with no candidate below the current n-th key is skipped on
+// one ballot, otherwise it is sorted across the lanes (bitonic network on
+// shuffles) and merged into the list (min against the reversed chunk, then
+// a bitonic merge) — the "k-nearest wavefront scan" of SURVEY config 5.
+__device__ __forceinline__ bool knn_less(double da, int ia, double db, int ib) {
+  return da < db || (da == db && ia < ib);
+}
+// one compare-exchange stage with lane ^ j: keep the smaller key iff `lo`
+__device__ __forceinline__ void knn_cx(double &kd, int &ki, double &od, int j, bool lo) {
+  const double pd = __shfl_xor(kd, j);
+  const int pi = __shfl_xor(ki, j);
+  const double po = __shfl_xor(od, j);
+  const bool take = lo ? knn_less(pd, pi, kd, ki) : knn_less(kd, ki, pd, pi);
+  if (take) {
+    kd = pd;
+    ki = pi;
+    od = po;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_knn(int64_t n_query, const double *__restrict__ q,
+                                             int64_t n_vert, const double *__restrict__ v, int nk,
+                                             int32_t *__restrict__ out, double *__restrict__ dist) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / WAVE);
+  for (int64_t qi = blockIdx.x * (int64_t)(blockDim.x / WAVE) + threadIdx.x / WAVE; qi < n_query;
+       qi += waves) {
+    double qq[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) qq[k] = q[8 * qi + k];
+    // the list: key (kd = the distance with NaN as +inf, ki) and the distance itself
+    double kd = INFINITY, od = __builtin_nan("");
+    int ki = 0x7FFFFFFF;
+    for (int64_t j0 = 0; j0 < n_vert; j0 += WAVE) {
+      const int64_t j = j0 + lane;
+      double cd = INFINITY, co = __builtin_nan("");
+      int ci = 0x7FFFFFFF;
+      if (j < n_vert) {
+        co = state_distance(qq, v + 8 * j);
+        cd = isnan(co) ? INFINITY : co;
+        ci = (int)j;
+      }
+      const double td = __shfl(kd, nk - 1);
+      const int ti = __shfl(ki, nk - 1);
+      if (!__ballot(knn_less(cd, ci, td, ti))) continue;
+      // sort the chunk ascending (bitonic network, 21 stages)
+#pragma unroll
+      for (int k = 2; k <= WAVE; k <<= 1)
+#pragma unroll
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+          const bool up = (lane & k) == 0;
+          knn_cx(cd, ci, co, jj, ((lane & jj) == 0) == up);
+        }
+      // the 64 smallest of list + chunk: lane l against the chunk's lane 63 - l
+      // (a bitonic sequence), then one bitonic merge
+      {
+        const double rd = __shfl(cd, WAVE - 1 - lane);
+        const int ri = __shfl(ci, WAVE - 1 - lane);
+        const double ro = __shfl(co, WAVE - 1 - lane);
+        if (knn_less(rd, ri, kd, ki)) {
+          kd = rd;
+          ki = ri;
+          od = ro;
+        }
+      }
+#pragma unroll
+      for (int jj = WAVE >> 1; jj > 0; jj >>= 1) knn_cx(kd, ki, od, jj, (lane & jj) == 0);
+    }
+    if (lane < nk) {
+      const bool real = ki != 0x7FFFFFFF;
+      out[qi * nk + lane] = real ? ki : -1;
+      if (dist) dist[qi * nk + lane] = real ? od : __builtin_nan("");
+    }
+  }
+}
+
 }  // namespace
 
 // ============================================================================
@@ -1341,6 +1424,22 @@ int gbp_neighbors_batch_dev(int64_t n_query, const double *queries, int64_t n_ve
   return GBP_OK;
 }
 
+int gbp_knn_batch_dev(int64_t n_query, const double *queries, int64_t n_vert,
+                      const double *vertices, int n_nearest, int32_t *out, double *dist,
+                      gbp_stream stream) {
+  if (n_query < 0 || n_vert < 0 || n_nearest < 1 || n_nearest > GBP_KNN_MAX ||
+      (n_query > 0 && (!queries || !out)))
+    return GBP_E_INVALID_ARG;
+  if (n_vert > 0x7FFFFFFE) return GBP_E_SHAPE;
+  if (n_query == 0) return GBP_OK;
+  if (n_vert > 0 && !vertices) return GBP_E_INVALID_ARG;
+  const unsigned grid = (unsigned)std::min<int64_t>((n_query + 3) / 4, 65535);
+  hipLaunchKernelGGL(k_knn, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_query, queries,
+                     n_vert, vertices, n_nearest, out, dist);
+  HIPCHK(hipGetLastError());
+  return GBP_OK;
+}
+
 // ---- host-pointer convenience entry points (see the Stage helper above) ----------
 
 #define H2D(dst, src, bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st))
@@ -1653,6 +1752,33 @@ int gbp_neighbors_batch_host(int64_t n_query, const double *queries, int64_t n_v
   return rc;
 }
 
+int gbp_knn_batch_host(int64_t n_query, const double *queries, int64_t n_vert,
+                       const double *vertices, int n_nearest, int32_t *out, double *dist) {
+  if (n_query <= 0) return n_query == 0 ? GBP_OK : GBP_E_INVALID_ARG;
+  if (!queries || !out || n_nearest < 1 || n_nearest > GBP_KNN_MAX || (n_vert > 0 && !vertices))
+    return GBP_E_INVALID_ARG;
+  void *buf = nullptr;
+  const size_t nout = (size_t)n_query * (size_t)n_nearest;
+  const size_t need = rnd(64 * n_query) + rnd(64 * (n_vert > 0 ? n_vert : 1)) + rnd(4 * nout) +
+                      rnd(8 * nout) + 1024;
+  if (hipMalloc(&buf, need) != hipSuccess) return GBP_E_ALLOC;
+  char *p = (char *)buf;
+  double *dq = (double *)p; p += rnd(64 * n_query);
+  double *dv = (double *)p; p += rnd(64 * (n_vert > 0 ? n_vert : 1));
+  int32_t *dout = (int32_t *)p; p += rnd(4 * nout);
+  double *dd = (double *)p;
+  int rc = GBP_OK;
+  if (hipMemcpy(dq, queries, 64 * n_query, hipMemcpyHostToDevice) != hipSuccess) rc = GBP_E_HIP;
+  if (!rc && n_vert > 0 &&
+      hipMemcpy(dv, vertices, 64 * n_vert, hipMemcpyHostToDevice) != hipSuccess)
+    rc = GBP_E_HIP;
+  if (!rc) rc = gbp_knn_batch_dev(n_query, dq, n_vert, dv, n_nearest, dout, dd, nullptr);
+  if (!rc && hipMemcpy(out, dout, 4 * nout, hipMemcpyDeviceToHost) != hipSuccess) rc = GBP_E_HIP;
+  if (!rc && dist && hipMemcpy(dist, dd, 8 * nout, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = GBP_E_HIP;
+  (void)hipFree(buf);
+  return rc;
+}
 
 // ---- FRAGILE attempts: the glibc re-decision (host/gbp_host_check.cpp) ------------
 int gbp_resolve_fragile_host(gbp_terrain *t, int64_t n, const double *s, const double *a,

@@ -691,21 +691,24 @@ std::vector<State> PlannerClass::randomStateBatch(FastTerrainMap &terrain, int n
   return q;
 }
 
+void PlannerClass::ensure_scratch(int64_t nq) {
+  if (nq <= d_scratch_cap_) return;
+  int64_t cap = std::max<int64_t>(256, d_scratch_cap_);
+  while (cap < nq) cap *= 2;
+  void *p = nullptr;
+  chk(gbp_device_alloc(device_, (size_t)cap * (sizeof(State) + sizeof(int32_t)), &p),
+      "nn scratch alloc");
+  if (d_scratch_) gbp_device_free(d_scratch_);
+  d_scratch_ = p;
+  d_scratch_cap_ = cap;
+}
+
 std::vector<int> PlannerClass::getNearestNeighborBatch(const std::vector<State> &q) {
   std::vector<int> idx(q.size(), 0);
   if (q.empty()) return idx;
   sync_device();
   const int64_t nq = (int64_t)q.size();
-  if (nq > d_scratch_cap_) {
-    int64_t cap = std::max<int64_t>(256, d_scratch_cap_);
-    while (cap < nq) cap *= 2;
-    void *p = nullptr;
-    chk(gbp_device_alloc(device_, (size_t)cap * (sizeof(State) + sizeof(int32_t)), &p),
-        "nn scratch alloc");
-    if (d_scratch_) gbp_device_free(d_scratch_);
-    d_scratch_ = p;
-    d_scratch_cap_ = cap;
-  }
+  ensure_scratch(nq);
   double *dq = (double *)d_scratch_;
   int32_t *di = (int32_t *)(dq + 8 * d_scratch_cap_);
   std::vector<int32_t> out(nq);
@@ -771,6 +774,22 @@ std::vector<std::vector<int>> PlannerClass::neighborhoodDistBatch(const std::vec
 }
 
 std::vector<int> PlannerClass::neighborhoodN(State q, int N) {  // :151-171
+  const int V = (int)vertices_.size();
+  if (!cost_add_yaw_flag_ && N >= 1 && N <= GBP_KNN_MAX && V > 0) {
+    // the engine's k-nearest wavefront scan (gbp_knn_batch_dev): the heap's
+    // pop order, ascending (stateDistance, index)
+    sync_device();
+    ensure_scratch(256);  // one query row + N indices
+    double *dq = (double *)d_scratch_;
+    int32_t *dout = (int32_t *)(dq + 8);
+    std::vector<int32_t> out(N);
+    chk(gbp_memcpy_h2d(dq, q.data(), sizeof(State), nullptr), "knn upload");
+    chk(gbp_knn_batch_dev(1, dq, V, d_vertices_, N, dout, nullptr, nullptr), "neighborhoodN");
+    chk(gbp_memcpy_d2h(out.data(), dout, (size_t)N * sizeof(int32_t), nullptr), "knn download");
+    chk(gbp_stream_synchronize(nullptr), "knn sync");
+    return std::vector<int>(out.begin(), out.begin() + std::min(N, V));
+  }
+  // the yaw-weighted distance (cost_add_yaw, glibc atan2) or N > GBP_KNN_MAX: on the host
   std::vector<std::pair<double, int>> d;
   for (int i = 0; i < (int)vertices_.size(); i++)
     d.push_back({stateDistance(q, vertices_[i], cost_add_yaw_flag_, cost_add_yaw_length_weight_,

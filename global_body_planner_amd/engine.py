@@ -507,6 +507,24 @@ def neighbors(queries, vertices, radius, max_out=256):
     return out, cnt
 
 
+KNN_MAX = 64
+
+
+def knn(queries, vertices, n_nearest):
+    """Batched PlannerClass::neighborhoodN (planner_class.cpp:151-171) on the
+    device: (idx [n, n_nearest] int32, dist [n, n_nearest]) in ascending
+    (distance, index) order, -1 / NaN past the tree's size; n_nearest <= 64."""
+    lib = L.load()
+    q = queries.contiguous()
+    v = vertices.contiguous()
+    n = q.shape[0]
+    out = torch.empty((n, int(n_nearest)), dtype=torch.int32, device=q.device)
+    dist = torch.empty((n, int(n_nearest)), dtype=torch.float64, device=q.device)
+    check(lib.gbp_knn_batch_dev(n, _ptr(q), v.shape[0], _ptr(v), int(n_nearest), _ptr(out),
+                                _ptr(dist), _stream(q.device.index or 0)), "knn")
+    return out, dist
+
+
 def device_count():
     lib = L.load()
     c = ctypes.c_int(0)

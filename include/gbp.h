@@ -355,6 +355,21 @@ int gbp_neighbors_batch_host(int64_t n_query, const double *queries, int64_t n_v
                              const double *vertices, double radius, int max_out, int32_t *out,
                              int32_t *count);
 
+/* ---- k nearest (PlannerClass::neighborhoodN, planner_class.cpp:151-171) ----
+ * out[i][0..k), k = min(n_nearest, n_vert): the vertices of smallest
+ * stateDistance(query_i, v) in the order the reference pops its min-heap of
+ * std::pair<double, int> — ascending distance, equal distances by ascending
+ * index; a NaN distance orders after every number.  dist[i][...] (may be NULL)
+ * their distances; entries k .. n_nearest-1 are -1 / NaN.  1 <= n_nearest <=
+ * GBP_KNN_MAX.  The reference's cost_add_yaw variant (yaw-weighted distance,
+ * glibc atan2) is the host's (include/gbp_planner.h PlannerClass::neighborhoodN). */
+#define GBP_KNN_MAX 64
+int gbp_knn_batch_dev(int64_t n_query, const double *queries, int64_t n_vert,
+                      const double *vertices, int n_nearest, int32_t *out, double *dist,
+                      gbp_stream stream);
+int gbp_knn_batch_host(int64_t n_query, const double *queries, int64_t n_vert,
+                       const double *vertices, int n_nearest, int32_t *out, double *dist);
+
 /* ---- streams ------------------------------------------------------------ */
 int gbp_stream_create(int device, gbp_stream *out);  /* a non-blocking HIP stream */
 int gbp_stream_destroy(gbp_stream stream);

@@ -262,7 +262,9 @@ class PlannerClass {
   // vertices with index < limit[k] (limit empty: all), ascending index
   std::vector<std::vector<int>> neighborhoodDistBatch(const std::vector<State> &q, double dist,
                                                       const std::vector<int> &limit = {});
-  std::vector<int> neighborhoodN(State q, int N);                          // :151-171
+  // :151-171: the engine's k-nearest wavefront scan (N <= GBP_KNN_MAX, plain
+  // stateDistance), else (cost_add_yaw's weighted distance) a host sort
+  std::vector<int> neighborhoodN(State q, int N);
 
   void setStream(uint64_t seed, uint64_t stream_id) {
     seed_ = seed;
@@ -272,6 +274,7 @@ class PlannerClass {
 
  private:
   void sync_device();
+  void ensure_scratch(int64_t nq);
   int device_;
   std::vector<State> vertices_;
   std::vector<Action> actions_;

@@ -76,6 +76,7 @@ def lib():
             "orc_extend_batch": (None, [P, I64, P, P, P, P, I, I, P, P, P, P, P, I]),
             "orc_nearest_batch": (None, [I64, P, I, P, P, P, I]),
             "orc_neighbors_batch": (None, [I64, P, I, P, D, I, P, P, I]),
+            "orc_knn_batch": (None, [I64, P, I, P, I, P, P, I]),
             "orc_sample_states": (None, [P, I64, U64, U64, I64, I, I, P, P, I]),
             "orc_sample_actions": (None, [I64, P, U64, U64, I64, P, I]),
             "orc_sample_states_dir": (None, [P, I64, U64, U64, I64, I, D, I, P, P, P, I]),
@@ -387,6 +388,17 @@ def neighbors_batch(queries, verts, radius, max_out=256, nthreads=1):
     lib().orc_neighbors_batch(q.shape[0], _p(q), v.shape[0], _p(v), float(radius), int(max_out),
                               _p(out), _p(cnt), nthreads)
     return out, cnt
+
+
+def knn_batch(queries, verts, n_nearest, nthreads=1):
+    """planner_class.cpp:151-171 (neighborhoodN): (idx [n, k], dist [n, k])."""
+    q = _c(queries, np.float64).reshape(-1, 8)
+    v = _c(verts, np.float64).reshape(-1, 8)
+    out = np.empty((q.shape[0], n_nearest), np.int32)
+    dist = np.empty((q.shape[0], n_nearest))
+    lib().orc_knn_batch(q.shape[0], _p(q), v.shape[0], _p(v), int(n_nearest), _p(out), _p(dist),
+                        nthreads)
+    return out, dist
 
 
 def apply_stance(s, a, t):

@@ -761,6 +761,45 @@ void orc_neighbors_batch(int64_t n_q, const double *q, int n_vert, const double 
   }
 }
 
+/* PlannerClass::neighborhoodN (planner_class.cpp:151-171): the reference
+ * pushes every (stateDistance, index) into a min-heap of std::pair<double, int>
+ * (std::greater) and pops min(N, size): ascending distance, equal distances by
+ * ascending index.  Restated as a full sort of the keys (NaN distances ordered
+ * after every number, ascending index among them).  out[n_q][n_nearest], -1 /
+ * NaN past the tree's size. */
+typedef struct {
+  double key, d;
+  int i;
+} knn_entry;
+
+static int knn_cmp(const void *pa, const void *pb) {
+  const knn_entry *a = (const knn_entry *)pa, *b = (const knn_entry *)pb;
+  if (a->key < b->key) return -1;
+  if (b->key < a->key) return 1;
+  return (a->i > b->i) - (a->i < b->i);
+}
+
+void orc_knn_batch(int64_t n_q, const double *q, int n_vert, const double *verts, int n_nearest,
+                   int32_t *out, double *dist, int nthreads) {
+  if (nthreads <= 0) nthreads = 1;
+  OMP_FOR
+  for (int64_t i = 0; i < n_q; i++) {
+    knn_entry *e = (knn_entry *)malloc(sizeof(knn_entry) * (size_t)(n_vert > 0 ? n_vert : 1));
+    for (int v = 0; v < n_vert; v++) {
+      double d = orc_state_distance(q + 8 * i, verts + (long)v * 8);
+      e[v].d = d;
+      e[v].key = isnan(d) ? INFINITY : d;
+      e[v].i = v;
+    }
+    qsort(e, (size_t)n_vert, sizeof(knn_entry), knn_cmp);
+    for (int k = 0; k < n_nearest; k++) {
+      out[i * n_nearest + k] = k < n_vert ? e[k].i : -1;
+      if (dist) dist[i * n_nearest + k] = k < n_vert ? e[k].d : NAN;
+    }
+    free(e);
+  }
+}
+
 /* ---- Philox4x32-10 (Salmon et al., SC'11) ------------------------------- */
 static inline void mulhilo32(uint32_t a, uint32_t b, uint32_t *hi, uint32_t *lo) {
   uint64_t p = (uint64_t)a * b;

@@ -117,6 +117,10 @@ void orc_nearest_batch(int64_t n_q, const double *q, int n_vert, const double *v
 void orc_neighbors_batch(int64_t n_q, const double *q, int n_vert, const double *verts,
                          double radius, int max_out, int32_t *out, int32_t *count, int nthreads);
 
+/* planner_class.cpp:151-171 (neighborhoodN): ascending (distance, index) */
+void orc_knn_batch(int64_t n_q, const double *q, int n_vert, const double *verts, int n_nearest,
+                   int32_t *out, double *dist, int nthreads);
+
 /* ---- counter-based samplers (Philox4x32-10), same keys as the engine ---- */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 /* uniform in [0,1): (hi:lo >> 11) * 2^-53 for each of the two 64-bit halves */

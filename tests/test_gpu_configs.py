@@ -29,7 +29,7 @@ import pytest
 import oracle
 from global_body_planner_amd import _lib as L
 from global_body_planner_amd import terrain_data as td
-from tests.helpers import assert_pairs_equal, attempts_oracle, resolver, u32
+from tests.helpers import same_f64, assert_pairs_equal, attempts_oracle, resolver, u32
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -218,6 +218,33 @@ def test_config5_fractal4096_neighbourhoods(gpu):
             k = min(int(rc[i]), 64)
             assert np.array_equal(got[i, :k], ro[i, :k]), i
     assert rc.max() > 0
+
+
+@pytest.mark.parametrize("n_nearest", [1, 8, 64])
+def test_config5_fractal4096_knn(gpu, n_nearest):
+    """PlannerClass::neighborhoodN (planner_class.cpp:151-171) — config 5's
+    "k-nearest wavefront scan" (k_knn, gbp_knn_batch_dev) — on fractal-4096
+    states against the oracle: the heap's pop order (ascending distance,
+    ties by ascending index), indices and distances bit for bit; exact
+    duplicate vertices (ties), a tree smaller than N, NaN components."""
+    import global_body_planner_amd as gbp
+    data, T, O = fractal_pair()
+    verts, _ = O.sample_states(30000, 77, 1, 0, L.STANCE, 256, nthreads=16)
+    q, _ = O.sample_states(1500, 78, 2, 0, L.STANCE, 256, nthreads=16)
+    verts[1000:1200] = verts[5000:5200]        # exact duplicates: ties
+    verts[20000:20100] = q[:100]               # queries' own states (distance 0)
+    verts[::997, 3] = np.nan                   # NaN distances order last
+    q = np.concatenate([q, verts[[5000, 5001, 7]], np.full((1, 8), np.nan)])
+    for nv in (verts.shape[0], 40, 1):
+        vt, qt = torch.from_numpy(np.ascontiguousarray(verts[:nv])).cuda(), torch.from_numpy(q).cuda()
+        idx, dist = gbp.knn(qt, vt, n_nearest)
+        ri, rd = oracle.knn_batch(q, verts[:nv], n_nearest, nthreads=16)
+        assert np.array_equal(idx.cpu().numpy(), ri), (nv, n_nearest)
+        assert np.all(same_f64(dist.cpu().numpy(), rd)), (nv, n_nearest)
+    # a query equal to the duplicated vertex 5000 (== vertex 1000): the lower index first
+    idx, _ = gbp.knn(torch.from_numpy(q[-4:-3]).cuda(), torch.from_numpy(verts).cuda(), n_nearest)
+    assert idx.cpu().numpy()[0, 0] == 1000
+    print(f"k-nearest N={n_nearest}: {q.shape[0]} queries x {verts.shape[0]} vertices bit-exact")
 
 
 def test_config5_rrt_star_fractal4096(gpu):
