@@ -199,9 +199,13 @@ def time_to_first_solution(data, name, runs, max_time, args, rank, world, dev, p
     batch = args.plan_batch or pair["batch"]
     ext_total, time_total = 0, 0.0
     for k in range(runs):
+        # config 4: the ranks' searches stop together at the first solution of
+        # any of them (one all_reduce(MAX) per group of half-iterations)
+        poll = sharding.stop_together(dev) if world > 1 and args.plan_algorithm == 3 else None
         out = planner.plan_rrt_connect(data, start, goal, batch=batch,
                                        max_time=max_time, algorithm=args.plan_algorithm,
-                                       seed=args.seed + 7919 * k + rank, device=dev.index)
+                                       seed=args.seed + 7919 * k + rank, device=dev.index,
+                                       stop_poll=poll)
         ttf = out["time_to_first"] if out["found"] else float("inf")
         ext_total += out["extends"]
         time_total += out["time_to_first"] if out["found"] else out["total_time"]

@@ -1574,11 +1574,11 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
   int group = 2;
   int32_t half = 0;
   gbp_plan_status ps{};
-  while (since() < max_time) {
-    if (st.max_halves > 0) {  // a replayable run: exactly max_halves half-iterations
-      if (half >= st.max_halves) break;
-      group = (int)std::min<int64_t>(group, st.max_halves - half);
-    }
+  // with a stop poll (config 4's restart trees, one per rank) the ranks stop
+  // together: every group ends in one poll, and only its answer ends the loop
+  bool go = max_time > 0;
+  while (go) {
+    if (st.max_halves > 0) group = (int)std::min<int64_t>(group, st.max_halves - half);
     for (int k = 0; k < 2; k++) {  // room for `group` halves of appends
       int64_t c = 0;
       chk(gbp_tree_capacity(D.tree[k], &c), "tree capacity");
@@ -1613,9 +1613,15 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
     if (ps.error) throw EngineError(GBP_E_SHAPE, "device planner loop: a tree ran out of capacity");
     for (int k = 0; k < 2; k++) chk(gbp_tree_size(D.tree[k], &known[k], D.stream), "tree size");
     half += group;
-    if (ps.done) {
-      goal_found = true;
-      break;
+    if (ps.done) goal_found = true;
+    const bool local_stop = ps.done || since() >= max_time ||
+                            (st.max_halves > 0 && half >= st.max_halves);
+    if (st.stop_poll) {
+      st.polls++;
+      go = st.stop_poll(st.stop_ctx, local_stop ? 1 : 0, ps.done ? 1 : 0) == 0;
+      if (!go && !local_stop) st.stopped_by_peer = 1;
+    } else {
+      go = !local_stop;
     }
     group = std::min(group * 2, g_max);
   }
@@ -2126,6 +2132,10 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     BatchStats st;
     TreeDump dump;
     st.max_halves = p->max_halves > 0 ? p->max_halves : 0;
+    if (p->algorithm == 3) {  // one device search per rank: the ranks' polls pair up
+      st.stop_poll = p->stop_poll;
+      st.stop_ctx = p->stop_ctx;
+    }
     if (p->tree_capacity > 0) st.dump = &dump;
     const auto t0 = std::chrono::high_resolution_clock::now();
     const bool found =
@@ -2177,6 +2187,8 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     r->meet_a = st.meet_a;
     r->meet_b = st.meet_b;
     r->halves = st.halves;
+    r->polls = st.polls;
+    r->stopped_by_peer = st.stopped_by_peer;
     if (st.dump)
       for (int k = 0; k < 2; k++) {
         const int64_t n = std::min<int64_t>(p->tree_capacity, (int64_t)dump.v[k].size());

@@ -31,7 +31,11 @@ class PlanParams(ctypes.Structure):
                 ("adaptive", ctypes.c_int), ("nn_stats", ctypes.c_int),
                 ("max_halves", ctypes.c_int64),
                 ("tree_capacity", ctypes.c_int64), ("tree_v", _P * 2), ("tree_a", _P * 2),
-                ("tree_parent", _P * 2), ("tree_g", _P * 2)]
+                ("tree_parent", _P * 2), ("tree_g", _P * 2), ("stop_poll", _P),
+                ("stop_ctx", _P)]
+
+# int (*stop_poll)(void *ctx, int local_stop, int found)
+StopPoll = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int)
 
 
 class PlanResult(ctypes.Structure):
@@ -47,7 +51,8 @@ class PlanResult(ctypes.Structure):
                 ("status_reads", ctypes.c_int64), ("halts", ctypes.c_int64 * 3),
                 ("nn_rechecks", ctypes.c_int64), ("nn_scans", ctypes.c_int64),
                 ("reported_length", _D), ("reported_yaw", _D), ("meet_a", ctypes.c_int32),
-                ("meet_b", ctypes.c_int32), ("halves", ctypes.c_int64)]
+                ("meet_b", ctypes.c_int32), ("halves", ctypes.c_int64),
+                ("polls", ctypes.c_int64), ("stopped_by_peer", ctypes.c_int32)]
 
 
 _planner = None
@@ -106,7 +111,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
                      post_process=False, device=0, capacity=4096, algorithm=0, max_time_opt=0.0,
                      sampling=None, fragile_eps=None, adaptive=False, nn_stats=False,
                      max_halves=0, trees=False,
-                     tree_capacity=1 << 18):
+                     tree_capacity=1 << 18, stop_poll=None):
     """Plan start -> goal on terrain `data` (terrain_data.TerrainData).
 
     algorithm 0: batch-synchronous RRT-Connect, stops at the first solution;
@@ -129,7 +134,10 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     max_halves: algorithms 0, 1, 3 stop after this many half-iterations (a
       replayable run; 0 = no limit);
     trees: also return the final trees (out["a"], out["b"]: v, act, parent, g;
-      algorithms 0, 1, 3), at most tree_capacity rows each."""
+      algorithms 0, 1, 3), at most tree_capacity rows each;
+    stop_poll: algorithm 3 — f(local_stop, found) -> bool called after every
+      group of half-iterations; True stops the search (sharding.stop_together:
+      config 4's ranks stop at the first solution of any of them)."""
     L = load()
     x = np.ascontiguousarray(data.x, dtype=np.float64)
     y = np.ascontiguousarray(data.y, dtype=np.float64)
@@ -151,6 +159,10 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     p.adaptive = int(bool(adaptive))
     p.nn_stats = int(bool(nn_stats))
     p.max_halves = int(max_halves)
+    poll_cb = None
+    if stop_poll is not None:
+        poll_cb = StopPoll(lambda ctx, local, found: 1 if stop_poll(bool(local), bool(found)) else 0)
+        p.stop_poll = ctypes.cast(poll_cb, _P)
     tb = []
     if trees:
         p.tree_capacity = int(tree_capacity)
@@ -165,6 +177,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     actions = np.zeros((capacity, 10))
     rc = L.gbp_plan_rrt_connect(ctypes.byref(p), ctypes.byref(r), states.ctypes.data,
                                 actions.ctypes.data, capacity)
+    del poll_cb
     if rc != 0:
         raise _lib.GbpError(rc, "gbp_plan_rrt_connect")
     out = {k: getattr(r, k) for k, _ in PlanResult._fields_}

@@ -37,6 +37,23 @@ def reduce_run(elapsed_s, counters, device):
     return float(t.item()), [float(v) for v in c.tolist()]
 
 
+def stop_together(device):
+    """Config 4's early stop: a stop poll for
+    planner.plan_rrt_connect(stop_poll=...).  After every group of
+    half-iterations each rank posts its own verdict (found, or out of time)
+    with one all_reduce(MAX) of one number; every rank stops as soon as any
+    rank has (the slower trees stop within one group of the first solution).
+    Every rank must poll (the device loop polls once per group until the
+    answer is stop), so the collectives pair up."""
+    def poll(local_stop, found):
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return local_stop
+        t = torch.tensor([1.0 if local_stop else 0.0], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return bool(t.item() > 0)
+    return poll
+
+
 def pack_path(cost, length, yaw, states, actions, device="cpu", cap=PATH_MAX):
     """Fixed-size best-path record of `cap` states (states [k, 8], actions
     [k-1, 10]).  Never raises: every rank must reach the collective that

@@ -392,6 +392,14 @@ struct TreeDump {
 struct BatchStats {
   int64_t max_halves = 0;     // in: stop after this many half-iterations (0 = no limit)
   TreeDump *dump = nullptr;   // in: receives the final trees when set
+  // in (device loop): called after every group of halves with this rank's own
+  // verdict (local_stop: found, out of time or halves) and whether it found a
+  // path; returns nonzero to stop — config 4's ranks answer it with one
+  // all_reduce(MAX) of local_stop, so they stop together
+  int (*stop_poll)(void *ctx, int local_stop, int found) = nullptr;
+  void *stop_ctx = nullptr;
+  int64_t polls = 0;          // stop polls made
+  int stopped_by_peer = 0;    // the poll stopped a search this rank would have continued
   int64_t halves = 0;         // half-iterations run
   int32_t meet_a = -1, meet_b = -1;  // the joined vertices (RRT*: the best pair)
   int64_t iterations = 0, targets = 0, extends = 0, attempts_checked = 0, connects = 0;
@@ -627,6 +635,8 @@ typedef struct {
   double *tree_a[2];      //   the action reaching each vertex [cap][10] (root: zeros),
   int32_t *tree_parent[2];  // parents (root -1) and g values; rows past the result's
   double *tree_g[2];      //   vertices_a / vertices_b are not written
+  int (*stop_poll)(void *ctx, int local_stop, int found);  // algorithm 3: see BatchStats
+  void *stop_ctx;         //   (NULL: each run stops on its own)
 } gbp_plan_params;
 
 typedef struct {
@@ -651,6 +661,8 @@ typedef struct {
   int32_t meet_a, meet_b;      // algorithms 0 / 3: the vertices of Ta / Tb the first REACHED
                                // connect joined; algorithm 1: the best pair
   int64_t halves;              // half-iterations run
+  int64_t polls;               // algorithm 3 with stop_poll: polls made
+  int32_t stopped_by_peer;     // ... and 1 if another rank's solution ended this search
 } gbp_plan_result;
 
 /* plans from start to goal; path_states[capacity][8] / path_actions[capacity][10]

@@ -103,6 +103,56 @@ def test_config4_restart_trees_best_path_allgather(gpu, name, xy, batch):
     print(f"config 4 (2 ranks, {name}): costs {costs}, best rank {want}, {len(S)} states")
 
 
+def _early_stop_worker(rank, world, port, q, batch):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import global_body_planner_amd as gbp
+        from global_body_planner_amd import planner, sharding
+        data = td.synth_rough(1024)
+        T = gbp.Terrain.from_data(data, device=0)
+        # rank 0: the pair before the wall (solved in milliseconds); rank 1:
+        # SURVEY's pair across the walls (unsolved in 20 s)
+        gx = 6.8 if rank == 0 else 19.42
+        h = T.height_host([[1.0, 10.23], [gx, 10.23]])[0]
+        start = planner.start_goal_state(h[0], 1.0, 10.23)
+        goal = planner.start_goal_state(h[1], gx, 10.23)
+        out = planner.plan_rrt_connect_device(data, start, goal, batch=batch, max_time=30.0,
+                                              seed=20251019 + rank,
+                                              stop_poll=sharding.stop_together("cpu"))
+        q.put((rank, out["found"], out["polls"], out["stopped_by_peer"], out["status_reads"],
+               out["total_time"], out["halves"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config4_early_stop(gpu):
+    """Config 4's optional early termination: after each group
+    of half-iterations every rank posts its found flag with one
+    all_reduce(MAX); a rank whose own search is far from a solution stops
+    within one group of the other rank's first solution (same number of
+    polls), instead of running out its 30-s budget."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_early_stop_worker, args=(r, 2, port, q, 8192)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, f0, p0, s0, _, t0, h0), (r1, f1, p1, s1, _, t1, h1) = res
+    assert f0 == 1 and f1 == 0
+    assert p0 == p1 >= 1               # the same polls: stopped in the same group
+    assert s0 == 0 and s1 == 1         # rank 1 was stopped by rank 0's solution
+    assert t1 < 10.0                   # not its 30-s budget
+    print(f"early stop: rank 0 solved after {h0} halves ({t0:.3f} s), rank 1 stopped after "
+          f"{h1} halves ({t1:.3f} s), {p0} polls each")
+
+
 def _throughput_worker(rank, world, port, q, per_rank, seed):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
