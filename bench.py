@@ -196,7 +196,14 @@ def time_to_first_solution(data, name, runs, max_time, args, rank, world, dev, p
     goal = planner.start_goal_state(h[1], xy[1, 0], xy[1, 1])
     out_runs = []
     best = None
-    batch = args.plan_batch or pair["batch"]
+    # each half-iteration "draws enough targets to issue about
+    # 256k attempts" (config 3; 64k for configs 1-2): pair["batch"] valid
+    # targets x 6 candidates; the draws per half are that many over the
+    # terrain's STANCE-valid fraction of randomState draws (isValidState
+    # filter, rrt_connect.cpp:254), measured here on 65,536 draws
+    q, _ = T.sample_states(65536, seed=args.seed, stream_id=7)
+    pv = float(T.valid_states(q, L.STANCE)[0].float().mean().item())
+    batch = args.plan_batch or int(round(pair["batch"] / max(pv, 0.05)))
     ext_total, time_total = 0, 0.0
     for k in range(runs):
         # config 4: the ranks' searches stop together at the first solution of
@@ -237,7 +244,8 @@ def time_to_first_solution(data, name, runs, max_time, args, rank, world, dev, p
     res = {"terrain": name, "pair": pair_key or name,
            "value": float(np.median(solved)) if solved else None, "unit": "s",
            "solved": f"{len(solved)}/{len(out_runs)}", "runs": out_runs, "best_path": best,
-           "batch": batch, "max_time_s": max_time,
+           "batch": batch, "stance_valid_fraction": round(pv, 4),
+           "targets_per_half": int(round(batch * pv)), "max_time_s": max_time,
            "planner": "buildRRTConnectDevice (search resident on the device)"
                       if args.plan_algorithm == 3 else "buildRRTConnectBatched (host loop)",
            "planner_extends_per_s": round(ext_total / max(time_total, 1e-9), 1),

@@ -162,6 +162,18 @@ __global__ __launch_bounds__(256, W) void k_validate_direct(
 // (lane state machine: gbp_lane.h)
 
 
+// deferred s_new (round 4): a deciding lane queues (attempt, kind, parameter)
+// in its wave's LDS ring instead of forming its s_new closed form under the
+// deciding lanes' divergent mask in every step; once 64 are queued the wave
+// forms all 64 converged (attempt rows re-read from L2) — once per 64
+// decisions instead of once per step (~15 decisions per step and wave at
+// config 3)
+struct SnewRec {
+  int idx, kind;
+  double p;
+};
+constexpr int SN_RING = 2 * 64;  // entries per wave: < 64 left + up to 64 queued in a step
+
 template <class ZT, bool ADAPTIVE, int W, int CM, bool ONE>
 __global__ __launch_bounds__(512, W) void k_validate_persistent(
     TerrainView<ZT> T0, int n, const double *__restrict__ S, const double *__restrict__ A,
@@ -174,6 +186,27 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
   double *const SA = gbp_smem + (CM == 1 ? (T0.nx + T0.ny + 1) & ~1 : 0);  // attempt rows
   double *const wave_rows = SA + (size_t)(threadIdx.x & ~(WAVE - 1)) * SA_ROW;
+  SnewRec *const ring = (SnewRec *)(SA + (size_t)blockDim.x * SA_ROW) + (threadIdx.x / WAVE) * SN_RING;
+  int ring_n = 0;  // wave-uniform
+  // s_new of the ring's first cnt entries, one per lane (converged)
+  auto flush = [&](int cnt) {
+    if (lane < cnt) {
+      const SnewRec r = ring[lane];
+      double sv[8], av[10], o[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) sv[k] = S[8 * (size_t)r.idx + k];
+#pragma unroll
+      for (int k = 0; k < 10; k++) av[k] = A[10 * (size_t)r.idx + k];
+      // one closed form for every kind: sample_state at FWD_STANCE is
+      // apply_stance's expression tree (same operands, same bits)
+      sample_state(sv, av,
+                   r.kind == SN_STANCE_S ? ST_FWD_STANCE
+                                         : (r.kind == SN_FLIGHT_B ? ST_FWD_LAND : ST_REV_STANCE),
+                   r.p, o);
+#pragma unroll
+      for (int k = 0; k < 8; k++) s_new[8 * (size_t)r.idx + k] = o[k];
+    }
+  };
   Lane L;
   L.s = SA + (size_t)threadIdx.x * SA_ROW;
   L.a = L.s + 8;
@@ -295,37 +328,33 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
       }
     }
     asm volatile("" ::: "memory");
-    if (owner) {
-      if (decided) {
-        const size_t i = (size_t)L.idx;
-        uint32_t f = L.f | L.acc.flags;
-        if (L.snew_kind != SN_NONE) f |= GBP_F_SNEW_SET;
-        if (L.tnew_set) f |= GBP_F_TNEW_SET;
-        if (valid) valid[i] = (f & GBP_F_VALID) ? 1 : 0;
-        if (s_new && L.snew_kind != SN_NONE) {
-          double o[8];
-          double sv[8], av[10];
-#pragma unroll
-          for (int k = 0; k < 8; k++) sv[k] = L.s[k];
-#pragma unroll
-          for (int k = 0; k < 10; k++) av[k] = L.a[k];
-          // one closed form for every kind: sample_state at FWD_STANCE is
-          // apply_stance's expression tree (same operands, same bits)
-          sample_state(sv, av,
-                       L.snew_kind == SN_STANCE_S
-                           ? ST_FWD_STANCE
-                           : (L.snew_kind == SN_FLIGHT_B ? ST_FWD_LAND : ST_REV_STANCE),
-                       L.snew_p, o);
-#pragma unroll
-          for (int k = 0; k < 8; k++) s_new[8 * i + k] = o[k];
-        }
-        if (t_new && L.tnew_set) t_new[i] = L.tnew;
-        flags[i] = f;
-        if (counts) counts[i] = (L.acc.G & 0xFFFFu) | (L.acc.V << 16);
-        L.stage = ST_IDLE;
+    const bool fin = owner && decided;
+    const bool queue = fin && s_new && L.snew_kind != SN_NONE;
+    if (fin) {
+      const size_t i = (size_t)L.idx;
+      uint32_t f = L.f | L.acc.flags;
+      if (L.snew_kind != SN_NONE) f |= GBP_F_SNEW_SET;
+      if (L.tnew_set) f |= GBP_F_TNEW_SET;
+      if (valid) valid[i] = (f & GBP_F_VALID) ? 1 : 0;
+      if (t_new && L.tnew_set) t_new[i] = L.tnew;
+      flags[i] = f;
+      if (counts) counts[i] = (L.acc.G & 0xFFFFu) | (L.acc.V << 16);
+    }
+    const unsigned long long qm = __ballot(queue);
+    if (qm) {
+      if (queue) ring[ring_n + __popcll(qm & lt_mask)] = SnewRec{L.idx, L.snew_kind, L.snew_p};
+      ring_n += __popcll(qm);
+      if (ring_n >= WAVE) {
+        flush(WAVE);
+        ring_n -= WAVE;
+        SnewRec r;
+        if (lane < ring_n) r = ring[WAVE + lane];
+        if (lane < ring_n) ring[lane] = r;
       }
     }
+    if (fin) L.stage = ST_IDLE;
   }
+  if (ring_n) flush(ring_n);
 }
 
 // ============================================================================
@@ -712,7 +741,7 @@ int coord_mode(const gbp_terrain *t, bool lds_ok) {
 // the attempt rows with room for the W workgroups of 256 lanes that share a CU
 // (160 KB per CU; the direct kernel has no rows)
 int validate_coord_mode(const gbp_terrain *t, bool direct) {
-  const size_t rows = sizeof(double) * SA_ROW * (size_t)t->opt_block;
+  const size_t rows = (sizeof(double) * SA_ROW + sizeof(SnewRec) * SN_RING / WAVE) * (size_t)t->opt_block;
   const size_t per_cu = std::max<int64_t>(1, t->opt_waves * 256 / t->opt_block) *
                         (stage_bytes(t->nx, t->ny) + rows);
   const bool lds_ok = t->opt_lds_coords && stage_bytes(t->nx, t->ny) + rows <= t->lds_max &&
@@ -750,15 +779,17 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
                          s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn, flags + off, c);
     } else {
       // persistent: one workgroup per resident slot (opt_waves waves per SIMD;
-      // W, the register budget, allows at least that many)
+      // W, the register budget, allows at least that many); LDS: the
+      // coordinate vectors (CM 1), the attempt rows, the s_new rings
       const int64_t resident = (int64_t)t->num_cus * std::max<int64_t>(1, t->opt_waves * 256 / block);
       // every resident slot as long as each wave gets an attempt: a batch
       // smaller than the resident lanes still spreads over every CU, its
       // waves starting with idle lanes that help from the first step
       // (65,536 attempts: 0.084 -> 0.072 ms; 262,144: unchanged)
       const int64_t g = std::max<int64_t>(1, std::min<int64_t>(resident, (m + WAVE - 1) / WAVE));
+      const size_t ring = sizeof(SnewRec) * SN_RING * (size_t)(block / WAVE);
       hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, CM, ONE>), dim3((unsigned)g), dim3(block),
-                         coords + rows, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
+                         coords + rows + ring, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
                          flags + off, c, n_dev, (int)t->opt_helpers,
                          (int)t->opt_xcd_map);
     }

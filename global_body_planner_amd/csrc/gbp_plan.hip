@@ -7,10 +7,12 @@
 // RRTConnectClass::extendBatch + connectBatch), tree T extended toward B
 // random targets, every new vertex connected to the other tree O:
 //
-//   stage 0  k_targets          B draws of PlannerClass::randomState
-//                               (planner_class.cpp:38-76) + isValidState(STANCE)
-//   stage 1  k_compact_targets  the valid targets, in draw order (and their fp16
-//                               rows); a FRAGILE draw halts the sequence here
+//   stage 0-1 k_targets         B draws of PlannerClass::randomState
+//                               (planner_class.cpp:38-76) + isValidState(STANCE),
+//                               the valid ones compacted in draw order (and their
+//                               fp16 rows) in the same launch; a FRAGILE draw
+//                               halts the sequence here (resumed at stage 1:
+//                               k_compact_targets alone)
 //   stage 2  k_nn_mfma/k_nn_hreduce    getNearestNeighbor in T on the matrix cores
 //                               (planner_class.cpp:185-200); extra workgroups of the
 //                               same launch draw newConfig's 6 candidate actions
@@ -211,40 +213,6 @@ __device__ uint32_t ordered_rank(bool keep, unsigned long long *tiles, uint32_t 
   }
   __syncthreads();
   return s_excl + woff + wr;
-}
-
-// ============================================================================
-// stage 0-1: targets
-// ============================================================================
-template <class ZT>
-__global__ __launch_bounds__(TB) void k_targets(TerrainView<ZT> T, gbp_plan_status *st, int64_t n,
-                                                uint64_t seed, uint64_t stream_id, int64_t base,
-                                                double *__restrict__ cand,
-                                                uint32_t *__restrict__ cflag, int32_t half,
-                                                uint64_t seq, gbp_sampling cfg,
-                                                const double *__restrict__ tv,
-                                                const int32_t *__restrict__ tcount,
-                                                const double *__restrict__ ov, int direction) {
-  if (gated(st, seq)) return;
-  // direction-biased draws (rrt_connect.cpp:248-252, :283-287): s_from / s_to
-  // are T's last vertex and O's root (FORWARD half, T = Ta), or O's root and
-  // T's last vertex (REVERSE half, T = Tb), as the trees stand when the half
-  // starts (the batch-synchronous snapshot; batch 1 is the reference's loop)
-  const double *t_last = tv + 8 * (int64_t)(*tcount - 1);
-  const double *s_from = direction == GBP_FORWARD ? t_last : ov;
-  const double *s_to = direction == GBP_FORWARD ? ov : t_last;
-  // FRAGILE draws are flagged here and halt the sequence in the compaction
-  // (k_compact_targets, in stream order), so this kernel may run beside the
-  // previous half's connect stages (gbp_plan_halves_dev)
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    double q[8];
-    sample_state_cfg_try(T, cfg, s_from, s_to, seed, stream_id, base + i, 0, q);  // randomState
-    Acc acc{0, 0, 0};
-    const bool v = is_valid_state(T, q, GBP_STANCE, acc);   // rrt_connect.cpp:254
-    copy8(cand + 8 * i, q);
-    cflag[i] = acc.flags | (v ? GBP_F_VALID : 0u);
-  }
 }
 
 // stateDistance(q, vertex j) exactly as the reference evaluates it
@@ -796,9 +764,78 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
 }
 
 // ============================================================================
-// stage 1: the targets' ordered compaction
+// stages 0-1: targets and their ordered compaction
 // ============================================================================
-// the compacted targets (stage 1), in draw order, and their fp16 query rows
+// the extend stream of a half: RRTClass::extend_counter_ advances by the
+// number of extends (csrc/host/gbp_planner.cpp extendBatch); the re-run of a
+// compaction that halted on a FRAGILE draw (the host resumes the half at
+// stage 1, gbp_plan_resolve_host) starts from the same counters.  Called by
+// the compaction's last workgroup once the grid's total is known.
+__device__ __forceinline__ void commit_targets(gbp_plan_status *st, int32_t half, bool resumed) {
+  const int64_t base = resumed ? st->ext_prev : st->ext_counter;
+  const int64_t tg = resumed ? st->stat_targets_prev : st->stat_targets;
+  st->ext_half = half;
+  st->ext_prev = base;
+  st->stat_targets_prev = tg;
+  st->ext_base = base;
+  st->ext_counter = base + st->n_targets;
+  st->stat_targets = tg + st->n_targets;
+}
+
+// stages 0-1 of a fresh half in one launch: thread i draws target i of T's
+// randomState stream (planner_class.cpp:38-76) and checks isValidState(STANCE)
+// (rrt_connect.cpp:254), then the workgroups rank the valid draws in draw order
+// (ordered_rank: ballot + popcount, decoupled look-back) and write them with
+// their fp16 query rows.  A FRAGILE draw halts the sequence here; the host
+// re-decides it with glibc and resumes the half at stage 1, the compaction
+// alone (k_compact_targets on the patched flags).
+template <class ZT>
+__global__ __launch_bounds__(TB) void k_targets(TerrainView<ZT> T, gbp_plan_status *st, int64_t n,
+                                                uint64_t seed, uint64_t stream_id, int64_t base,
+                                                double *__restrict__ cand,
+                                                uint32_t *__restrict__ cflag,
+                                                double *__restrict__ targets,
+                                                _Float16 *__restrict__ tqh,
+                                                unsigned long long *tiles, uint32_t epoch,
+                                                int32_t half, uint64_t seq, gbp_sampling cfg,
+                                                const double *__restrict__ tv,
+                                                const int32_t *__restrict__ tcount,
+                                                const double *__restrict__ ov, int direction) {
+  if (gated(st, seq)) return;
+  // direction-biased draws (rrt_connect.cpp:248-252, :283-287): s_from / s_to
+  // are T's last vertex and O's root (FORWARD half, T = Ta), or O's root and
+  // T's last vertex (REVERSE half, T = Tb), as the trees stand when the half
+  // starts (the batch-synchronous snapshot; batch 1 is the reference's loop)
+  const double *t_last = tv + 8 * (int64_t)(*tcount - 1);
+  const double *s_from = direction == GBP_FORWARD ? t_last : ov;
+  const double *s_to = direction == GBP_FORWARD ? ov : t_last;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  double q[8];
+  uint32_t f = 0;
+  if (i < n) {
+    sample_state_cfg_try(T, cfg, s_from, s_to, seed, stream_id, base + i, 0, q);  // randomState
+    Acc acc{0, 0, 0};
+    const bool v = is_valid_state(T, q, GBP_STANCE, acc);   // rrt_connect.cpp:254
+    f = acc.flags | (v ? GBP_F_VALID : 0u);
+    copy8(cand + 8 * i, q);
+    cflag[i] = f;
+  }
+  const bool keep = f & GBP_F_VALID;
+  if (__ballot(f & GBP_F_FRAGILE) && (threadIdx.x & (WAVE - 1)) == 0) {  // the targets stage halts
+    atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_TARGETS);
+    st->halt_half = half;
+    raise_gate(st, seq);
+  }
+  const uint32_t r = ordered_rank(keep, tiles, epoch, &st->n_targets, st);
+  if (keep) {
+    copy8(targets + 8 * (size_t)r, q);
+    nn_put_hrow(tqh, nullptr, r, q, false);  // the search's query rows
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) commit_targets(st, half, false);
+}
+
+// stage 1 alone (a half resumed after a FRAGILE draw, on the host-patched
+// flags): the compacted targets in draw order and their fp16 query rows
 __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int64_t n,
                                                         const double *__restrict__ cand,
                                                         const uint32_t *__restrict__ cflag,
@@ -820,21 +857,7 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
     copy8(targets + 8 * (size_t)r, cand + 8 * i);
     nn_put_hrow(tqh, nullptr, r, cand + 8 * i, false);  // the search's query rows
   }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
-    // the extend stream of this half: RRTClass::extend_counter_ advances by
-    // the number of extends (csrc/host/gbp_planner.cpp extendBatch); the re-run
-    // of a compaction that halted on a FRAGILE draw (the host resumes the half
-    // at stage 1, gbp_plan_resolve_host) starts from the same counters
-    const bool again = resumed != 0;
-    const int64_t base = again ? st->ext_prev : st->ext_counter;
-    const int64_t tg = again ? st->stat_targets_prev : st->stat_targets;
-    st->ext_half = half;
-    st->ext_prev = base;
-    st->stat_targets_prev = tg;
-    st->ext_base = base;
-    st->ext_counter = base + st->n_targets;
-    st->stat_targets = tg + st->n_targets;
-  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) commit_targets(st, half, resumed != 0);
 }
 
 // ============================================================================
@@ -1304,14 +1327,15 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   const int cus = t->num_cus;
   gbp_plan_status *st = w->st;
   w->nn_stats = t->opt_nn_stats;
-  if (first_stage <= 0 && last_stage >= 0)
-    hipLaunchKernelGGL(k_targets<ZT>, dim3(grid_for(batch, TB, cus * 8)), dim3(TB), 0, s, V, st,
-                       batch, seed, target_stream, target_base, w->cand, w->cflag, half, ++w->seq,
-                       t->sampling, T->v, T->count, O ? O->v : T->v, direction);
-  if (first_stage <= 1 && last_stage >= 1)
+  if (first_stage <= 0 && last_stage >= 1)  // a fresh half: draws + compaction, one launch
+    hipLaunchKernelGGL(k_targets<ZT>, dim3((unsigned)((batch + TB - 1) / TB)), dim3(TB), 0, s, V,
+                       st, batch, seed, target_stream, target_base, w->cand, w->cflag, w->targets,
+                       w->tqh, w->tiles, next_epoch(w), half, ++w->seq, t->sampling, T->v, T->count,
+                       O ? O->v : T->v, direction);
+  else if (first_stage == 1 && last_stage >= 1)  // resumed after a FRAGILE draw
     hipLaunchKernelGGL(k_compact_targets, dim3(tiles_for(batch)), dim3(CB), 0, s, st, batch,
-                       w->cand, w->cflag, w->targets, w->tqh, w->tiles, next_epoch(w), half,
-                       first_stage == 1 ? 1 : 0, ++w->seq);
+                       w->cand, w->cflag, w->targets, w->tqh, w->tiles, next_epoch(w), half, 1,
+                       ++w->seq);
   if (first_stage <= 2 && last_stage >= 2) {
     // the candidates' actions inside the search unless they are direction-biased
     // (then they depend on s_near: k_extend_prep after the search)
@@ -1598,7 +1622,7 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->num_cus = t->num_cus;
   w->nn_stats = t->opt_nn_stats;
   w->bmax = max_batch;
-  w->ntiles = (max_batch + CB - 1) / CB + 1;
+  w->ntiles = (max_batch + TB - 1) / TB + 1;  // k_targets' 256-draw tiles (k_compact_targets: 1024)
   const int64_t b = max_batch, m = GBP_NUM_GEN_STATES * max_batch;
   const size_t bytes = sizeof(gbp_plan_status) + 8 * w->ntiles + 64 * b + 4 * b + 64 * b + 4 * b +
                        m * (64 + 80 + 64 + 4 + 4) + b * (4 + 4 + 64 + 80 + 4 + 4) +

@@ -11,6 +11,8 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("trace")
     p.add_argument("--halves", type=int, default=4000)
+    p.add_argument("--min-kernels", type=int, default=7,
+                   help="a half-iteration's kernels from k_targets on (fewer: a cut-off half)")
     a = p.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -24,7 +26,7 @@ def main():
             short = re.sub(r"^.*?(k_[a-z0-9_]+).*$", r"\1", n.replace("_ZN12_GLOBAL__N_1", ""))
             short = re.sub(r"^\d+", "", short)
             cur.append((short, int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
-    halves = [h for h in halves if len(h) >= 10][-a.halves:]
+    halves = [h for h in halves if len(h) >= a.min_kernels][-a.halves:]
     pos = collections.defaultdict(list)
     span = []
     for h in halves:
@@ -32,10 +34,13 @@ def main():
             pos[(i, n)].append((e - s) / 1e3)
         span.append((h[-1][2] - h[0][1]) / 1e3)
     tot = 0.0
+    print(f"{'pos':>3} {'kernel':28s} {'calls':>6} {'mean':>8}    {'median':>8} {'p90':>8}")
     for (i, n), v in sorted(pos.items()):
         m = sum(v) / len(v)
         tot += m
-        print(f"{i:3d} {n:28s} {len(v):6d} {m:8.1f} us")
+        vs = sorted(v)
+        med, p90 = vs[len(vs) // 2], vs[min(len(vs) - 1, int(0.9 * len(vs)))]
+        print(f"{i:3d} {n:28s} {len(v):6d} {m:8.1f} us {med:8.1f} {p90:8.1f}")
     print(f"sum of kernel means per half {tot:.1f} us; first-start to last-end per half "
           f"{sum(span) / len(span):.1f} us over {len(halves)} halves")
 
