@@ -8,7 +8,7 @@ OUT=${OUT:-gpurun_out/plan_breakdown.txt}
 d=gpurun_out/pbd
 rm -rf $d
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $d -o run -- \
-    python3 tools/plan_run.py --max-time ${PLAN_TIME:-5} > $d.log 2>&1 || { tail -5 $d.log; exit 1; }
+    python3 tools/plan_run.py --max-time ${PLAN_TIME:-5} ${PLAN_ARGS:-} > $d.log 2>&1 || { tail -5 $d.log; exit 1; }
 f=$(find $d -name "*kernel_trace.csv" | head -1)
 { cat $d.log; python3 tools/plan_breakdown.py "$f" --halves ${HALVES:-4000}; } > $OUT
 find $d -name "*kernel_trace.csv" -delete
