@@ -174,6 +174,17 @@ struct SnewRec {
 };
 constexpr int SN_RING = 2 * 64;  // entries per wave: < 64 left + up to 64 queued in a step
 
+// (diagnostic build, -DGBP_LOOP_PROF: cycles per phase of the persistent loop,
+// per wave, read by gbp_loop_prof_read; tools/loop_prof.py)
+#ifdef GBP_LOOP_PROF
+__device__ unsigned long long gbp_loop_prof[8192 * 12];
+#define LP_T(v) const unsigned long long v = __builtin_readcyclecounter()
+#define LP_ADD(k, a, b) lp[k] += (b) - (a)
+#else
+#define LP_T(v)
+#define LP_ADD(k, a, b)
+#endif
+
 template <class ZT, bool ADAPTIVE, int W, int CM, bool ONE>
 __global__ __launch_bounds__(512, W) void k_validate_persistent(
     TerrainView<ZT> T0, int n, const double *__restrict__ S, const double *__restrict__ A,
@@ -213,8 +224,9 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
   L.stage = ST_IDLE;
   // work source: a fixed contiguous slice [cur, end) per wave, handed out to
   // the wave's idle lanes in order (no atomics).  Dynamic dequeues (one or
-  // eight device-scope heads, chunked, per-workgroup LDS queues) were
-  // measured slower and removed.
+  // eight device-scope heads, chunked, per-workgroup LDS queues; round 4: the
+  // last 15-60 % of a batch in chunks from 64 counters) were measured no
+  // faster and removed.
   unsigned int cur, end;
   {
     const unsigned int waves = gridDim.x * (blockDim.x / WAVE);
@@ -228,7 +240,13 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
     cur = (unsigned int)(((unsigned long long)n * wid) / waves);
     end = (unsigned int)(((unsigned long long)n * (wid + 1)) / waves);
   }
+#ifdef GBP_LOOP_PROF
+  unsigned long long lp[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  lp[8] = __builtin_amdgcn_s_memrealtime();
+  LP_T(lp_start);
+#endif
   for (;;) {
+    LP_T(t0);
     const bool need = L.stage == ST_IDLE;
     unsigned long long m = __ballot(need);
     if (m && cur < end) {
@@ -253,6 +271,8 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
     }
     const unsigned long long act = __ballot(L.stage != ST_IDLE);
     if (!act) break;
+    LP_T(t1);
+    LP_ADD(0, t0, t1);
     const bool owner = L.stage != ST_IDLE;
     asm volatile("" ::: "memory");  // re-read attempt rows per step (no long live ranges)
     // ---- the sample each lane evaluates this step --------------------------
@@ -285,6 +305,8 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
         t_eval = sample_time(st, ps + 8, t);
       }
     }
+    LP_T(t2);
+    LP_ADD(1, t1, t2);
     Acc acc_s{0, vbase + (uint32_t)slot, 0};
     bool ok = false;
     if (has) {
@@ -294,6 +316,8 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
       // its registers): the terrain's one-step guess is exact on both axes
       ok = is_valid_state<ZT, CM, ONE>(T, sc, stage_phase(st), acc_s);
     }
+    LP_T(t3);
+    LP_ADD(2, t2, t3);
     bool decided = false;
     if (owner) {  // the lane's own sample
       L.acc.G += acc_s.G;
@@ -328,6 +352,12 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
       }
     }
     asm volatile("" ::: "memory");
+    LP_T(t4);
+    LP_ADD(3, t3, t4);
+#ifdef GBP_LOOP_PROF
+    lp[6] += tail ? 1 : 0;
+    lp[7] += 1;
+#endif
     const bool fin = owner && decided;
     const bool queue = fin && s_new && L.snew_kind != SN_NONE;
     if (fin) {
@@ -353,8 +383,26 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
       }
     }
     if (fin) L.stage = ST_IDLE;
+    LP_T(t5);
+    LP_ADD(4, t4, t5);
   }
   if (ring_n) flush(ring_n);
+#ifdef GBP_LOOP_PROF
+  LP_T(lp_end);
+  lp[5] = lp_end - lp_start;
+  lp[9] = __builtin_amdgcn_s_memrealtime();
+  {
+    unsigned int hw;  // HW_ID: the wave's SIMD / CU / SE
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    lp[10] = hw;
+    unsigned int xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    lp[11] = xcc;
+  }
+  const unsigned int gw = blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;
+  if (lane == 0 && gw < 8192)
+    for (int k = 0; k < 12; k++) gbp_loop_prof[12 * gw + k] = lp[k];
+#endif
 }
 
 // ============================================================================
@@ -941,6 +989,20 @@ __attribute__((visibility("hidden"))) int gbp_internal_validate_dev_n(
 }
 
 extern "C" {
+
+#ifdef GBP_LOOP_PROF
+// per wave: refill, lane setup / helper plan, sample + isValidState, transition
+// + helper consumption, outputs + s_new ring, whole loop (cycles); tail
+// iterations; iterations
+int gbp_loop_prof_read(unsigned long long *out, int n_waves) {
+  if (!out || n_waves < 0 || n_waves > 8192) return GBP_E_INVALID_ARG;
+  if (hipDeviceSynchronize() != hipSuccess) return GBP_E_HIP;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gbp_loop_prof), sizeof(unsigned long long) * 12 * n_waves) !=
+      hipSuccess)
+    return GBP_E_HIP;
+  return GBP_OK;
+}
+#endif
 
 int gbp_version(void) { return 200; /* 0.2.0: extend flags, FRAGILE re-decision, trees */ }
 

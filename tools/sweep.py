@@ -70,6 +70,7 @@ def main():
     variants = [v + (ex,) for v in variants for ex in itertools.product(*extra_vals)]
     times = {v: [] for v in variants}
     ref = None
+    ref_chk = None
     st = torch.cuda.current_stream()
     for r in range(a.rounds):
         for v in variants:
@@ -96,6 +97,13 @@ def main():
                 T.validate_pairs(s, act, d, adaptive=a.adaptive, out=out)
                 e1.record(st)
             torch.cuda.synchronize()
+            # every round's last launch against the first round's outputs
+            chk = (int(out.flags.to(torch.int64).sum()), int(out.counts.to(torch.int64).sum()),
+                   int((out.s_new.nan_to_num(0.0) * 1e3).to(torch.int64).sum()))
+            if ref_chk is None:
+                ref_chk = chk
+            elif chk != ref_chk:
+                print(f"MISMATCH (round {r}) in variant {v}: {chk} vs {ref_chk}", flush=True)
             times[v].extend(e0.elapsed_time(e1) for e0, e1 in ev)
     rows = []
     for v in variants:
