@@ -27,7 +27,7 @@ def main():
     p.add_argument("--kernels", default="direct,persistent")
     p.add_argument("--waves", default="2,3,4")
     p.add_argument("--block", default="256")
-    p.add_argument("--lds", default="2", help="coordinates: 0 global, 1 LDS, 2 computed (affine)")
+    p.add_argument("--lds", default="1", help="coordinates: 0 global, 1 LDS, 2 computed (affine)")
     p.add_argument("--set", action="append", default=[],
                    help="extra option axis KEY=v1,v2 (KEY: an OPT_* name such as PREFETCH, or its id)")
     p.add_argument("--order", default="batch",
@@ -79,11 +79,12 @@ def main():
                 T.set_option(key, val)
             T.set_option(L.OPT_KERNEL, L.KERNEL_PERSISTENT if k == "persistent" else L.KERNEL_DIRECT)
             T.set_option(L.OPT_WAVES, w)
-            T.set_option(L.OPT_LDS_COORDS, 1 if lds >= 1 else 0)
+            T.set_option(L.OPT_LDS_COORDS, 1 if lds == 1 else 0)
             T.set_option(L.OPT_AFFINE_COORDS, 1 if lds == 2 else 0)
             T.set_option(L.OPT_BLOCK, b)
             out = T.validate_pairs(s, act, d, adaptive=a.adaptive)
             if r == 0:
+                print(f"variant {v}: coordinate mode {T.get_option(L.OPT_COORD_MODE)}", flush=True)
                 sig = (out.valid.cpu().numpy().tobytes(), out.flags.cpu().numpy().tobytes(),
                        out.counts.cpu().numpy().tobytes(), out.s_new.cpu().numpy().tobytes())
                 if ref is None:
