@@ -45,6 +45,8 @@ def run(lib, terrain, batch, seed, opts=(), waves=2048):
     a = raw.astype(np.float64)
     keep = a[:, 7] > 0
     a, raw = a[keep], raw[keep]
+    if os.environ.get("LOOP_PROF_DUMP"):
+        np.save(os.environ["LOOP_PROF_DUMP"] + f"_{terrain}.npy", raw)
     steps = a[:, 7].sum()
     tot = a[:, 5].sum()
     row = {"terrain": terrain, "batch": batch, "waves": int(a.shape[0]),
