@@ -85,6 +85,7 @@ struct gbp_plan_ws {
   uint32_t epoch = 0;          // per-compaction tag of the tile states
   uint64_t seq = 0;            // launch sequence number of the planner kernels (gated())
   int nn_stats = 0;            // GBP_OPT_NN_STATS: k_nn_hreduce counts its re-checks in the status
+  int nn_items = 4096;         // matrix-core search: work items (= waves) per launch
   int64_t ntiles = 0;
   // stage 0-1
   double *cand = nullptr;      // [bmax][8] drawn states
@@ -333,11 +334,11 @@ __device__ __forceinline__ void nn_put_hrow(_Float16 *__restrict__ vh, float *__
 
 // items: query groups (NH_NT tiles) x segments of cps chunks (32 rows); at
 // most NN_MAX_CHUNKS * bmax partial slots (pm[seg * nq + qi])
-__device__ __forceinline__ void nh_geometry(int64_t nq, int64_t nv, int64_t bmax, int64_t &nqg,
-                                            int64_t &nseg, int64_t &cps, int64_t &nch) {
+__device__ __forceinline__ void nh_geometry(int64_t nq, int64_t nv, int64_t bmax, int items,
+                                            int64_t &nqg, int64_t &nseg, int64_t &cps, int64_t &nch) {
   nch = nv > 0 ? (nv + 31) / 32 : 1;
   nqg = nq > 0 ? (nq + 32 * NH_NT - 1) / (32 * NH_NT) : 1;
-  int64_t want = (NH_ITEMS + nqg - 1) / nqg;
+  int64_t want = (items + nqg - 1) / nqg;
   const int64_t slots = (NN_MAX_CHUNKS * bmax) / (nq > 0 ? nq : 1);
   if (want > slots) want = slots;
   if (want > NH_MAX_SEG) want = NH_MAX_SEG;
@@ -493,7 +494,7 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
                                                    const float *__restrict__ hm,
                                                    const int32_t *__restrict__ nv_dev, int64_t bmax,
                                                    float4 *__restrict__ pm, int4 *__restrict__ pid,
-                                                   uint64_t seq, NhPrep<ZT> pp) {
+                                                   uint64_t seq, int n_items, NhPrep<ZT> pp) {
   if (gated(st, seq)) {
     if (PREP && blockIdx.x == pp.first_block && threadIdx.x == 0) st->n_validate = 0;
     return;
@@ -515,7 +516,7 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
   }
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   int64_t nqg, nseg, cps, nch;
-  nh_geometry(nq, nv, bmax, nqg, nseg, cps, nch);
+  nh_geometry(nq, nv, bmax, n_items, nqg, nseg, cps, nch);
   const bool tree_bad = ((const uint32_t *)hm)[8] != 0u || nv <= 0;
   const int lane = threadIdx.x & (WAVE - 1), r = lane & 31, h = lane >> 5;
   const int waves = (PREP ? pp.first_block : (int)gridDim.x) * (NH_TB / WAVE);
@@ -598,11 +599,11 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
                                                        int64_t bmax, const float4 *__restrict__ pm,
                                                        const int4 *__restrict__ pid,
                                                        int32_t *__restrict__ out, uint64_t seq,
-                                                       int stats, double *__restrict__ cs) {
+                                                       int stats, double *__restrict__ cs, int n_items) {
   if (gated(st, seq)) return;
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   int64_t nqg, nseg, cps, nch;
-  nh_geometry(nq, nv, bmax, nqg, nseg, cps, nch);
+  nh_geometry(nq, nv, bmax, n_items, nqg, nseg, cps, nch);
   const bool tree_bad = ((const uint32_t *)hm)[8] != 0u || nv <= 0;
   const int sl = threadIdx.x & (NH_G - 1);
   const int64_t groups = (int64_t)gridDim.x * (NH_RTB / NH_G);
@@ -1297,24 +1298,24 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
               const _Float16 *qh = nullptr, const NhPrep<ZT> *prep = nullptr,
               double *cs = nullptr, bool *prepped = nullptr) {
   if (prepped) *prepped = false;
-  const int gm = num_cus * (NH_ITEMS / 4) / 256;  // the search's workgroups
+  const int gm = w->nn_items / (NH_TB / WAVE);  // the search's workgroups: one wave per item
   if (prep) {
     NhPrep<ZT> pp = *prep;
     pp.first_block = gm;
     const int gp = (int)grid_for(GBP_NUM_GEN_STATES * w->bmax, NH_TB, num_cus * 4);
     hipLaunchKernelGGL((k_nn_mfma<NH_NT, ZT, true>), dim3(gm + gp), dim3(NH_TB), 0, s, w->st,
                        nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
-                       (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, pp);
+                       (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, w->nn_items, pp);
     if (prepped) *prepped = true;
   } else {
     hipLaunchKernelGGL((k_nn_mfma<NH_NT, float, false>), dim3(gm), dim3(NH_TB), 0, s, w->st,
                        nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
-                       (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, NhPrep<float>{});
+                       (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, w->nn_items, NhPrep<float>{});
   }
   hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(NH_G * w->bmax, NH_RTB, num_cus * 8)), dim3(NH_RTB),
                      0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, tr->count, w->bmax,
                      (const float4 *)w->nn_d, (const int4 *)w->nn_i, out, ++w->seq, w->nn_stats,
-                     prep ? cs : nullptr);
+                     prep ? cs : nullptr, w->nn_items);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
 
@@ -1622,6 +1623,9 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->num_cus = t->num_cus;
   w->nn_stats = t->opt_nn_stats;
   w->bmax = max_batch;
+  // 4096 items: 3072 (the waves resident at 162 VGPRs), 2048 and 6144 measured
+  // slower in the planner (profiles/r04l_nn_items.txt)
+  w->nn_items = NH_ITEMS;
   w->ntiles = (max_batch + TB - 1) / TB + 1;  // k_targets' 256-draw tiles (k_compact_targets: 1024)
   const int64_t b = max_batch, m = GBP_NUM_GEN_STATES * max_batch;
   const size_t bytes = sizeof(gbp_plan_status) + 8 * w->ntiles + 64 * b + 4 * b + 64 * b + 4 * b +
