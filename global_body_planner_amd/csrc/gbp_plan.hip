@@ -59,7 +59,7 @@
 #include "gbp_lane.h"
 
 using namespace gbp;
-static_assert(sizeof(gbp_plan_status) == 160, "engine.PlanStatus mirrors this layout");
+static_assert(sizeof(gbp_plan_status) == 168, "engine.PlanStatus mirrors this layout");
 
 // ============================================================================
 // handles
@@ -87,7 +87,14 @@ struct gbp_plan_ws {
   int nn_stats = 0;            // GBP_OPT_NN_STATS: k_nn_hreduce counts its re-checks in the status
   int nn_items = 4096;         // matrix-core search: work items (= waves) per launch
   int64_t ntiles = 0;
-  // stage 0-1
+  // stage 0-1: two sets, by the half's parity (a half's targets are drawn
+  // while the previous half still reads its own); cand..tqh point at the set
+  // of the half being enqueued or resolved (select_targets)
+  struct TargetSet {
+    double *cand, *targets;
+    uint32_t *cflag;
+    _Float16 *tqh;
+  } tset[2] = {};
   double *cand = nullptr;      // [bmax][8] drawn states
   uint32_t *cflag = nullptr;   // [bmax] their isValidState flags
   double *targets = nullptr;   // [bmax][8] the valid ones, in draw order
@@ -169,7 +176,7 @@ __device__ __forceinline__ unsigned long long tile_word(uint32_t epoch, uint32_t
 }
 
 __device__ uint32_t ordered_rank(bool keep, unsigned long long *tiles, uint32_t epoch,
-                                 int32_t *total, gbp_plan_status *st) {
+                                 int32_t *total, gbp_plan_status *st, uint32_t tile, uint32_t ntile) {
   __shared__ uint32_t wsum[CB / WAVE];
   __shared__ uint32_t s_excl;
   const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
@@ -183,7 +190,7 @@ __device__ uint32_t ordered_rank(bool keep, unsigned long long *tiles, uint32_t 
     bsum += wsum[i];
   }
   if (threadIdx.x == 0) {
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = tile;
     uint32_t excl = 0;
     if (b > 0) {
       __hip_atomic_exchange(&tiles[b], tile_word(epoch, 1, bsum), __ATOMIC_RELAXED,
@@ -210,10 +217,14 @@ __device__ uint32_t ordered_rank(bool keep, unsigned long long *tiles, uint32_t 
     __hip_atomic_exchange(&tiles[b], tile_word(epoch, 2, excl + bsum), __ATOMIC_RELAXED,
                           __HIP_MEMORY_SCOPE_AGENT);
     s_excl = excl;
-    if (b == gridDim.x - 1) *total = (int32_t)(excl + bsum);
+    if (b == ntile - 1) *total = (int32_t)(excl + bsum);
   }
   __syncthreads();
   return s_excl + woff + wr;
+}
+__device__ __forceinline__ uint32_t ordered_rank(bool keep, unsigned long long *tiles, uint32_t epoch,
+                                                 int32_t *total, gbp_plan_status *st) {
+  return ordered_rank(keep, tiles, epoch, total, st, blockIdx.x, gridDim.x);
 }
 
 // stateDistance(q, vertex j) exactly as the reference evaluates it
@@ -474,6 +485,23 @@ __device__ __forceinline__ void nh_sweep(const _Float16 *__restrict__ vh, int c0
 // (VALU and transcendental work next to matrix-core work) instead of as a
 // launch of their own after the search (k_extend_prep); the reduce then
 // copies s_near into the candidates (k_nn_hreduce cs).
+// The next half's targets, drawn ahead in the same launch (draw_blocks > 0;
+// gbp_plan_halves_dev, sampling not direction-biased): blocks
+// [0, draw_blocks) draw them into the next half's target set and rank them
+// (ordered_rank over those blocks: their count in status.pre_targets; a
+// FRAGILE draw sets status.pre_fragile = next half + 1).  They come first in
+// the grid so that their latency-bound work overlaps the matrix-core waves.
+struct NhDraw {
+  int draw_blocks;
+  int32_t half;  // the half the draws are for
+  int64_t n, base;
+  uint64_t stream;
+  double *cand, *targets;
+  uint32_t *cflag;
+  _Float16 *tqh;
+  unsigned long long *tiles;
+  uint32_t epoch;
+};
 template <class ZT>
 struct NhPrep {
   TerrainView<ZT> T;
@@ -482,6 +510,7 @@ struct NhPrep {
   gbp_sampling cfg;
   int direction;
   int first_block;  // blocks [first_block, gridDim.x) draw the actions
+  NhDraw dr;        // blocks [0, dr.draw_blocks): the next half's targets
 };
 
 template <int NT, class ZT, bool PREP>
@@ -497,6 +526,29 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
                                                    uint64_t seq, int n_items, NhPrep<ZT> pp) {
   if (gated(st, seq)) {
     if (PREP && blockIdx.x == pp.first_block && threadIdx.x == 0) st->n_validate = 0;
+    return;
+  }
+  if (PREP && (int)blockIdx.x < pp.dr.draw_blocks) {  // the next half's targets (k_targets' work)
+    const NhDraw &d = pp.dr;
+    const int64_t i = blockIdx.x * (int64_t)NH_TB + threadIdx.x;
+    double q[8];
+    uint32_t f = 0;
+    if (i < d.n) {
+      sample_state_cfg_try(pp.T, pp.cfg, q, q, pp.seed, d.stream, d.base + i, 0, q);  // not biased
+      Acc acc{0, 0, 0};
+      const bool v = is_valid_state(pp.T, q, GBP_STANCE, acc);  // rrt_connect.cpp:254
+      f = acc.flags | (v ? GBP_F_VALID : 0u);
+      copy8(d.cand + 8 * i, q);
+      d.cflag[i] = f;
+    }
+    const bool keep = f & GBP_F_VALID;
+    if (__ballot(f & GBP_F_FRAGILE) && (threadIdx.x & (WAVE - 1)) == 0) st->pre_fragile = d.half + 1;
+    const uint32_t r = ordered_rank(keep, d.tiles, d.epoch, &st->pre_targets, st, blockIdx.x,
+                                    (uint32_t)d.draw_blocks);
+    if (keep) {
+      copy8(d.targets + 8 * (size_t)r, q);
+      nn_put_hrow(d.tqh, nullptr, r, q, false);
+    }
     return;
   }
   if (PREP && (int)blockIdx.x >= pp.first_block) {  // the extends' candidate actions
@@ -519,9 +571,10 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
   nh_geometry(nq, nv, bmax, n_items, nqg, nseg, cps, nch);
   const bool tree_bad = ((const uint32_t *)hm)[8] != 0u || nv <= 0;
   const int lane = threadIdx.x & (WAVE - 1), r = lane & 31, h = lane >> 5;
-  const int waves = (PREP ? pp.first_block : (int)gridDim.x) * (NH_TB / WAVE);
+  const int mb = PREP ? pp.dr.draw_blocks : 0;  // the search's first workgroup
+  const int waves = ((PREP ? pp.first_block : (int)gridDim.x) - mb) * (NH_TB / WAVE);
   const int items = (int)(nqg * nseg), ns = (int)nseg;
-  for (int item = __builtin_amdgcn_readfirstlane(blockIdx.x * (NH_TB / WAVE) + threadIdx.x / WAVE);
+  for (int item = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - mb) * (NH_TB / WAVE) + threadIdx.x / WAVE);
        item < items; item += waves) {
     const int qg = item / ns, sg = item - qg * ns;
     const int c0 = sg * (int)cps, c1 = min((int)nch, c0 + (int)cps);
@@ -859,6 +912,21 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
     nn_put_hrow(tqh, nullptr, r, cand + 8 * i, false);  // the search's query rows
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) commit_targets(st, half, resumed != 0);
+}
+
+// stages 0-1 of a half whose targets were drawn ahead (NhDraw): the count
+// and the counters, and the FRAGILE halt at this half's start — what k_targets'
+// last workgroup and its FRAGILE wave would have done
+__global__ void k_commit_pre(gbp_plan_status *st, int32_t half, uint64_t seq) {
+  if (gated(st, seq)) return;
+  if (threadIdx.x != 0) return;
+  st->n_targets = st->pre_targets;
+  commit_targets(st, half, false);
+  if (st->pre_fragile == half + 1) {
+    atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_TARGETS);
+    st->halt_half = half;
+    raise_gate(st, seq);
+  }
 }
 
 // ============================================================================
@@ -1282,6 +1350,15 @@ __global__ void k_extend_out(const gbp_plan_status *st, int64_t n, const int32_t
 
 bool tree_ok(const gbp_tree *t) { return t && t->v && t->count; }
 
+// the target set of half `half` (its parity)
+void select_targets(gbp_plan_ws *w, int32_t half) {
+  const auto &ts = w->tset[half & 1];
+  w->cand = ts.cand;
+  w->cflag = ts.cflag;
+  w->targets = ts.targets;
+  w->tqh = ts.tqh;
+}
+
 uint32_t next_epoch(gbp_plan_ws *w) {
   if (++w->epoch == 0) w->epoch = 1;
   return w->epoch;
@@ -1301,9 +1378,10 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
   const int gm = w->nn_items / (NH_TB / WAVE);  // the search's workgroups: one wave per item
   if (prep) {
     NhPrep<ZT> pp = *prep;
-    pp.first_block = gm;
+    const int gd = pp.dr.draw_blocks;
+    pp.first_block = gd + gm;
     const int gp = (int)grid_for(GBP_NUM_GEN_STATES * w->bmax, NH_TB, num_cus * 4);
-    hipLaunchKernelGGL((k_nn_mfma<NH_NT, ZT, true>), dim3(gm + gp), dim3(NH_TB), 0, s, w->st,
+    hipLaunchKernelGGL((k_nn_mfma<NH_NT, ZT, true>), dim3(gd + gm + gp), dim3(NH_TB), 0, s, w->st,
                        nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
                        (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, w->nn_items, pp);
     if (prepped) *prepped = true;
@@ -1323,12 +1401,15 @@ template <class ZT>
 int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int32_t half,
                    int direction, int64_t batch, uint64_t seed, uint64_t target_stream,
                    int64_t target_base, int adaptive, int first_stage, int last_stage,
-                   hipStream_t s) {
+                   hipStream_t s, bool predrawn = false, const NhDraw *next = nullptr) {
   const TerrainView<ZT> V = view<ZT>(t);
   const int cus = t->num_cus;
   gbp_plan_status *st = w->st;
   w->nn_stats = t->opt_nn_stats;
-  if (first_stage <= 0 && last_stage >= 1)  // a fresh half: draws + compaction, one launch
+  select_targets(w, half);
+  if (predrawn && first_stage <= 0 && last_stage >= 1)  // drawn ahead in the previous half's search
+    hipLaunchKernelGGL(k_commit_pre, dim3(1), dim3(WAVE), 0, s, st, half, ++w->seq);
+  else if (first_stage <= 0 && last_stage >= 1)  // a fresh half: draws + compaction, one launch
     hipLaunchKernelGGL(k_targets<ZT>, dim3((unsigned)((batch + TB - 1) / TB)), dim3(TB), 0, s, V,
                        st, batch, seed, target_stream, target_base, w->cand, w->cflag, w->targets,
                        w->tqh, w->tiles, next_epoch(w), half, ++w->seq, t->sampling, T->v, T->count,
@@ -1340,8 +1421,14 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   if (first_stage <= 2 && last_stage >= 2) {
     // the candidates' actions inside the search unless they are direction-biased
     // (then they depend on s_near: k_extend_prep after the search)
-    const NhPrep<ZT> prep{V, seed, w->ca, t->sampling, direction, 0};
+    NhPrep<ZT> prep{V, seed, w->ca, t->sampling, direction, 0, NhDraw{}};
     const bool early = !t->sampling.action_flag;
+    if (early && next) {
+      prep.dr = *next;
+      prep.dr.draw_blocks = (int)((next->n + NH_TB - 1) / NH_TB);
+      prep.dr.tiles = w->tiles;
+      prep.dr.epoch = next_epoch(w);
+    }
     bool prepped = false;
     int rc = nn_launch<ZT>(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, w->tqh,
                            early ? &prep : nullptr, w->cs, &prepped);
@@ -1628,7 +1715,7 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->nn_items = NH_ITEMS;
   w->ntiles = (max_batch + TB - 1) / TB + 1;  // k_targets' 256-draw tiles (k_compact_targets: 1024)
   const int64_t b = max_batch, m = GBP_NUM_GEN_STATES * max_batch;
-  const size_t bytes = sizeof(gbp_plan_status) + 8 * w->ntiles + 64 * b + 4 * b + 64 * b + 4 * b +
+  const size_t bytes = sizeof(gbp_plan_status) + 8 * w->ntiles + 2 * (64 * b + 4 * b + 64 * b + 64 * b) + 1024 +
                        m * (64 + 80 + 64 + 4 + 4) + b * (4 + 4 + 64 + 80 + 4 + 4) +
                        b * (4 + 4 + 64 + 80 + 4) + NN_MAX_CHUNKS * b * (16 + 16) + 64 * b + 256 +
                        64 * 256;
@@ -1639,10 +1726,13 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   char *p = (char *)w->block;
   w->st = carve<gbp_plan_status>(p, 1);
   w->tiles = carve<unsigned long long>(p, w->ntiles);
-  w->cand = carve<double>(p, 8 * b);
-  w->cflag = carve<uint32_t>(p, b);
-  w->targets = carve<double>(p, 8 * b);
-  w->tqh = carve<_Float16>(p, 32 * b);
+  for (auto &ts : w->tset) {
+    ts.cand = carve<double>(p, 8 * b);
+    ts.cflag = carve<uint32_t>(p, b);
+    ts.targets = carve<double>(p, 8 * b);
+    ts.tqh = carve<_Float16>(p, 32 * b);
+  }
+  select_targets(w, 0);
   w->nn = carve<int32_t>(p, b);
   w->cs = carve<double>(p, 8 * m);
   w->ca = carve<double>(p, 10 * m);
@@ -1730,6 +1820,12 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
     return GBP_E_INVALID_ARG;
   Guard g(t->device);
   hipStream_t s = (hipStream_t)stream;
+  // targets drawn ahead: half h+1's draws do not depend on the trees unless
+  // the sampling is direction-biased, so half h's search launch draws and
+  // ranks them beside its matrix-core waves (NhDraw) and half h+1 starts with
+  // k_commit_pre instead of k_targets.  Same draws, same ranks, same counters.
+  const bool ahead = !t->sampling.state_flag && !t->sampling.action_flag;
+  bool predrawn = false;
   for (int32_t i = 0; i < n_halves; i++) {
     const int32_t h = first_half + i;
     const int k = h & 1;
@@ -1738,12 +1834,28 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
     const uint64_t ts = k ? stream_b : stream_a;
     const int64_t tb = (int64_t)(h >> 1) * batch;
     const int fs = i == 0 ? first_stage : 0;
+    NhDraw nd{};
+    const NhDraw *next = nullptr;
+    if (ahead && i + 1 < n_halves && fs <= 2) {
+      const int32_t h1 = h + 1;
+      const auto &set = w->tset[h1 & 1];
+      nd.half = h1;
+      nd.n = batch;
+      nd.base = (int64_t)(h1 >> 1) * batch;
+      nd.stream = (h1 & 1) ? stream_b : stream_a;
+      nd.cand = set.cand;
+      nd.targets = set.targets;
+      nd.cflag = set.cflag;
+      nd.tqh = set.tqh;
+      next = &nd;
+    }
     const int rc = t->storage == GBP_STORAGE_F32
                        ? enqueue_stages<float>(t, w, T, O, h, dir, batch, seed, ts, tb, adaptive, fs,
-                                               5, s)
+                                               5, s, predrawn && fs == 0, next)
                        : enqueue_stages<double>(t, w, T, O, h, dir, batch, seed, ts, tb, adaptive, fs,
-                                                5, s);
+                                                5, s, predrawn && fs == 0, next);
     if (rc) return rc;
+    predrawn = next != nullptr;
   }
   return GBP_OK;
 }
@@ -1759,6 +1871,7 @@ int gbp_extend_tree_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, int64_t n,
   if (n == 0) return GBP_OK;
   Guard g(t->device);
   hipStream_t s = (hipStream_t)stream;
+  select_targets(w, 0);
   hipLaunchKernelGGL(k_extend_setup, dim3(grid_for(8 * n, TB, t->num_cus * 4)), dim3(TB), 0, s,
                      w->st, n, n_dev, extend_base, targets, w->targets, w->tqh);
   int rc = t->storage == GBP_STORAGE_F32
@@ -1852,6 +1965,7 @@ int gbp_plan_resolve_host(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree 
   if (rc) return rc;
   *resume_stage = -1;
   int64_t k = 0;
+  select_targets(w, st.halt_half >= 0 ? st.halt_half : 0);  // the halted half's target set
   if (st.halt & GBP_PLAN_HALT_TARGETS) {
     // isValidState(s_rand, STANCE) of the half's draws (rrt_connect.cpp:254)
     if (batch < 1 || batch > w->bmax) return GBP_E_INVALID_ARG;

@@ -420,7 +420,8 @@ class PlanStatus(ctypes.Structure):
                 ("gate_seq", ctypes.c_uint64), ("stat_nn_rechecks", ctypes.c_int64),
                 ("stat_nn_scans", ctypes.c_int64), ("ext_half", ctypes.c_int32),
                 ("ext_pad", ctypes.c_int32), ("ext_prev", ctypes.c_int64),
-                ("stat_targets_prev", ctypes.c_int64)]
+                ("stat_targets_prev", ctypes.c_int64), ("pre_targets", ctypes.c_int32),
+                ("pre_fragile", ctypes.c_int32)]
 
 
 class PlanWorkspace:

@@ -462,6 +462,11 @@ typedef struct {
    * halt) starts from them again */
   int32_t ext_half, ext_pad;
   int64_t ext_prev, stat_targets_prev;
+  /* gbp_plan_halves_dev draws a half's targets ahead, inside the previous
+   * half's search launch (sampling not direction-biased): their count, and
+   * (half + 1) when one of those draws was FRAGILE (the half halts at its
+   * start, stage 1, as if its own draws had) */
+  int32_t pre_targets, pre_fragile;
 } gbp_plan_status;
 int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out);
 int gbp_plan_ws_destroy(gbp_plan_ws *ws);

@@ -1,5 +1,6 @@
 """Mean duration per position in the device planner's half-iteration, from a
-rocprofv3 --kernel-trace CSV of tools/plan_run.py (halves start at k_targets);
+rocprofv3 --kernel-trace CSV of tools/plan_run.py (halves start at k_targets, or
+at k_commit_pre when their targets were drawn in the previous half's search);
 the last --halves halves."""
 import argparse
 import csv
@@ -19,7 +20,7 @@ def main():
     halves, cur = [], None
     for r in rows:
         n = r["Kernel_Name"]
-        if "k_targets" in n:
+        if "k_targets" in n or "k_commit_pre" in n:  # a half starts (its targets drawn ahead: k_commit_pre)
             cur = []
             halves.append(cur)
         if cur is not None:
