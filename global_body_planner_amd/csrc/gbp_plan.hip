@@ -528,7 +528,9 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
     if (PREP && blockIdx.x == pp.first_block && threadIdx.x == 0) st->n_validate = 0;
     return;
   }
-  if (PREP && (int)blockIdx.x < pp.dr.draw_blocks) {  // the next half's targets (k_targets' work)
+  // the next half's targets (k_targets' work); float heights only: with fp64
+  // heights the state check's registers would cost the search an occupancy step
+  if constexpr (PREP && std::is_same_v<ZT, float>) if ((int)blockIdx.x < pp.dr.draw_blocks) {
     const NhDraw &d = pp.dr;
     const int64_t i = blockIdx.x * (int64_t)NH_TB + threadIdx.x;
     double q[8];
@@ -1824,7 +1826,8 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
   // the sampling is direction-biased, so half h's search launch draws and
   // ranks them beside its matrix-core waves (NhDraw) and half h+1 starts with
   // k_commit_pre instead of k_targets.  Same draws, same ranks, same counters.
-  const bool ahead = !t->sampling.state_flag && !t->sampling.action_flag;
+  const bool ahead = !t->sampling.state_flag && !t->sampling.action_flag &&
+                     t->storage == GBP_STORAGE_F32;  // (k_nn_mfma<float> only)
   bool predrawn = false;
   for (int32_t i = 0; i < n_halves; i++) {
     const int32_t h = first_half + i;
