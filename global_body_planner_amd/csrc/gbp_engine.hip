@@ -335,6 +335,11 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
       bool chain = owner && !decided && ok;
       const int kmax = (n_idle + n_act - 1) / n_act;
       for (int k = 1; k <= kmax; k++) {
+        // every owner's chain has ended (a failure or a decision): the rest of
+        // the helpers' results are not consumed (config 3 0.1315 -> 0.1206 ms,
+        // config 2 0.0622 -> 0.0506 ms: the loop ran n_idle / n_act rounds of
+        // shuffles and transitions whatever the chains did)
+        if (!__ballot(chain)) break;
         const int j = (k - 1) * n_act + my_rank;
         const bool exists = owner && j < n_idle;
         const int src = exists ? nth_set_bit(idle, j) : lane;

@@ -916,12 +916,16 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) commit_targets(st, half, resumed != 0);
 }
 
-// stages 0-1 of a half whose targets were drawn ahead (NhDraw): the count
-// and the counters, and the FRAGILE halt at this half's start — what k_targets'
-// last workgroup and its FRAGILE wave would have done
-__global__ void k_commit_pre(gbp_plan_status *st, int32_t half, uint64_t seq) {
-  if (gated(st, seq)) return;
-  if (threadIdx.x != 0) return;
+// stages 0-1 of a half whose targets were drawn ahead (NhDraw), run by the
+// last workgroup to finish the previous half's final launch (k_append mode 1)
+// unless that half found its connection, halted or failed: the count and the
+// counters, and the FRAGILE halt at this half's start — what k_targets' last
+// workgroup and its FRAGILE wave would have done
+__device__ void commit_pre(gbp_plan_status *st, int32_t half, uint64_t seq) {
+  const auto ld = [](const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  if (ld(&st->done) || ld(&st->halt) || ld(&st->error)) return;
   st->n_targets = st->pre_targets;
   commit_targets(st, half, false);
   if (st->pre_fragile == half + 1) {
@@ -1049,7 +1053,7 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
                                                int32_t *__restrict__ tp, int32_t *__restrict__ tcount,
                                                int32_t *__restrict__ vtx, unsigned long long *tiles,
                                                uint32_t epoch, int32_t half, int64_t cap,
-                                               uint64_t seq) {
+                                               uint64_t seq, int32_t commit_half) {
   if (gated(st, seq)) return;
   __shared__ int32_t s_base;
   if (threadIdx.x == 0) s_base = *tcount;  // read before this block publishes its count
@@ -1099,6 +1103,18 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
       st->stat_added += added;
     } else {
       st->stat_conn_added += added;
+    }
+  }
+  if (commit_half >= 0) {  // the next half's targets were drawn ahead: commit them
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();
+      uint32_t *fin = &st->commit_fin;  // workgroups finished (reset by the last)
+      if (atomicAdd(fin, 1u) == gridDim.x - 1) {
+        __threadfence();
+        *fin = 0;
+        commit_pre(st, commit_half, seq);
+      }
     }
   }
 }
@@ -1409,9 +1425,9 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   gbp_plan_status *st = w->st;
   w->nn_stats = t->opt_nn_stats;
   select_targets(w, half);
-  if (predrawn && first_stage <= 0 && last_stage >= 1)  // drawn ahead in the previous half's search
-    hipLaunchKernelGGL(k_commit_pre, dim3(1), dim3(WAVE), 0, s, st, half, ++w->seq);
-  else if (first_stage <= 0 && last_stage >= 1)  // a fresh half: draws + compaction, one launch
+  // predrawn: the previous half's search drew this half's targets and its
+  // last launch committed them (commit_pre)
+  if (!predrawn && first_stage <= 0 && last_stage >= 1)  // a fresh half: draws + compaction, one launch
     hipLaunchKernelGGL(k_targets<ZT>, dim3((unsigned)((batch + TB - 1) / TB)), dim3(TB), 0, s, V,
                        st, batch, seed, target_stream, target_base, w->cand, w->cflag, w->targets,
                        w->tqh, w->tiles, next_epoch(w), half, ++w->seq, t->sampling, T->v, T->count,
@@ -1451,7 +1467,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 0, w->eres, w->nn,
                        w->esn, w->ean, T->v, T->vh, T->hm, T->a, T->g, T->parent, T->count, w->evtx,
                        w->tiles,
-                       next_epoch(w), half, T->cap, ++w->seq);
+                       next_epoch(w), half, T->cap, ++w->seq, -1);
   if (!O) return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   const int cdir = direction == GBP_FORWARD ? GBP_REVERSE : GBP_FORWARD;
   if (first_stage <= 4 && last_stage >= 4) {
@@ -1475,7 +1491,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 1, w->kres, w->nno,
                        w->ksn, w->kan, O->v, O->vh, O->hm, O->a, O->g, O->parent, O->count, nullptr,
                        w->tiles,
-                       next_epoch(w), half, O->cap, ++w->seq);
+                       next_epoch(w), half, O->cap, ++w->seq, next ? next->half : -1);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
 
@@ -1824,8 +1840,9 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
   hipStream_t s = (hipStream_t)stream;
   // targets drawn ahead: half h+1's draws do not depend on the trees unless
   // the sampling is direction-biased, so half h's search launch draws and
-  // ranks them beside its matrix-core waves (NhDraw) and half h+1 starts with
-  // k_commit_pre instead of k_targets.  Same draws, same ranks, same counters.
+  // ranks them beside its matrix-core waves (NhDraw) and half h+1 has no
+  // k_targets: half h's last launch (k_append mode 1) commits them
+  // (commit_pre).  Same draws, same ranks, same counters.
   const bool ahead = !t->sampling.state_flag && !t->sampling.action_flag &&
                      t->storage == GBP_STORAGE_F32;  // (k_nn_mfma<float> only)
   bool predrawn = false;

@@ -419,7 +419,7 @@ class PlanStatus(ctypes.Structure):
                 ("stat_fragile_resolved", ctypes.c_int64), ("stat_depth_capped", ctypes.c_int64),
                 ("gate_seq", ctypes.c_uint64), ("stat_nn_rechecks", ctypes.c_int64),
                 ("stat_nn_scans", ctypes.c_int64), ("ext_half", ctypes.c_int32),
-                ("ext_pad", ctypes.c_int32), ("ext_prev", ctypes.c_int64),
+                ("commit_fin", ctypes.c_uint32), ("ext_prev", ctypes.c_int64),
                 ("stat_targets_prev", ctypes.c_int64), ("pre_targets", ctypes.c_int32),
                 ("pre_fragile", ctypes.c_int32)]
 

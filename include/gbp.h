@@ -460,7 +460,8 @@ typedef struct {
   /* the half whose targets were compacted last, and the counters before it:
    * a compaction re-run for the same half (resumed at stage 1 after a FRAGILE
    * halt) starts from them again */
-  int32_t ext_half, ext_pad;
+  int32_t ext_half;
+  uint32_t commit_fin;    /* workgroups of a committing k_append finished (internal) */
   int64_t ext_prev, stat_targets_prev;
   /* gbp_plan_halves_dev draws a half's targets ahead, inside the previous
    * half's search launch (sampling not direction-biased): their count, and

@@ -1,6 +1,6 @@
 """Mean duration per position in the device planner's half-iteration, from a
 rocprofv3 --kernel-trace CSV of tools/plan_run.py (halves start at k_targets, or
-at k_commit_pre when their targets were drawn in the previous half's search);
+after the previous half's second k_append when their targets were drawn ahead);
 the last --halves halves."""
 import argparse
 import csv
@@ -17,12 +17,19 @@ def main():
     a = p.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    halves, cur = [], None
+    halves, cur, appends = [], None, 0
     for r in rows:
         n = r["Kernel_Name"]
-        if "k_targets" in n or "k_commit_pre" in n:  # a half starts (its targets drawn ahead: k_commit_pre)
+        # a half starts at k_targets, or (its targets drawn ahead in the previous
+        # half's search) at the first planner kernel after the previous half's
+        # second k_append
+        if "k_targets" in n or (cur is not None and appends >= 2 and "k_" in n
+                                and "copyBuffer" not in n):
             cur = []
+            appends = 0
             halves.append(cur)
+        if "k_append" in n:
+            appends += 1
         if cur is not None:
             short = re.sub(r"^.*?(k_[a-z0-9_]+).*$", r"\1", n.replace("_ZN12_GLOBAL__N_1", ""))
             short = re.sub(r"^\d+", "", short)
