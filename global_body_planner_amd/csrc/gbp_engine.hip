@@ -794,7 +794,10 @@ int coord_mode(const gbp_terrain *t, bool lds_ok) {
 // the attempt rows with room for the W workgroups of 256 lanes that share a CU
 // (160 KB per CU; the direct kernel has no rows)
 int validate_coord_mode(const gbp_terrain *t, bool direct) {
-  const size_t rows = (sizeof(double) * SA_ROW + sizeof(SnewRec) * SN_RING / WAVE) * (size_t)t->opt_block;
+  // the attempt rows and s_new rings are the persistent kernel's alone
+  // (launch_validate_w allocates neither for the direct kernel)
+  const size_t rows =
+      direct ? 0 : (sizeof(double) * SA_ROW + sizeof(SnewRec) * SN_RING / WAVE) * (size_t)t->opt_block;
   const size_t per_cu = std::max<int64_t>(1, t->opt_waves * 256 / t->opt_block) *
                         (stage_bytes(t->nx, t->ny) + rows);
   const bool lds_ok = t->opt_lds_coords && stage_bytes(t->nx, t->ny) + rows <= t->lds_max &&

@@ -533,7 +533,9 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
   if constexpr (PREP && std::is_same_v<ZT, float>) if ((int)blockIdx.x < pp.dr.draw_blocks) {
     const NhDraw &d = pp.dr;
     const int64_t i = blockIdx.x * (int64_t)NH_TB + threadIdx.x;
-    double q[8];
+    // s_from / s_to are unused: draws ahead are never direction-biased (the
+    // host refuses draw_blocks > 0 with state_flag set); zeroed all the same
+    double q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t f = 0;
     if (i < d.n) {
       sample_state_cfg_try(pp.T, pp.cfg, q, q, pp.seed, d.stream, d.base + i, 0, q);  // not biased
@@ -1106,6 +1108,11 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
     }
   }
   if (commit_half >= 0) {  // the next half's targets were drawn ahead: commit them
+    // every thread's done / error / meet atomics above must be complete (at
+    // agent scope) before this workgroup counts itself finished, or the last
+    // workgroup's commit_pre could miss a REACHED or a capacity error raised
+    // by another wave of this launch
+    __threadfence();
     __syncthreads();
     if (threadIdx.x == 0) {
       __threadfence();
@@ -1442,6 +1449,8 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     NhPrep<ZT> prep{V, seed, w->ca, t->sampling, direction, 0, NhDraw{}};
     const bool early = !t->sampling.action_flag;
     if (early && next) {
+      // the drawn-ahead targets are sampled with s_from / s_to unset
+      if (t->sampling.state_flag) return GBP_E_INVALID_ARG;
       prep.dr = *next;
       prep.dr.draw_blocks = (int)((next->n + NH_TB - 1) / NH_TB);
       prep.dr.tiles = w->tiles;

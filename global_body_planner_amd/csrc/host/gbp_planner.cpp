@@ -1562,72 +1562,99 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
   chk(gbp_stream_create(dev, &D.stream), "stream");
   chk(gbp_plan_ws_create(h, batch, &D.ws), "plan workspace");
   int64_t cap = std::max<int64_t>(1 << 16, 4 * (int64_t)batch);
-  for (int k = 0; k < 2; k++) chk(gbp_tree_create(dev, cap, &D.tree[k]), "tree");
-  chk(gbp_tree_init(D.tree[0], s_start.data(), D.stream), "tree init");
-  chk(gbp_tree_init(D.tree[1], s_goal.data(), D.stream), "tree init");
-  chk(gbp_plan_reset(D.ws, extend_counter_, D.stream), "plan reset");
   int64_t known[2] = {1, 1};
+  for (int k = 0; k < 2; k++) {
+    const int64_t wn = st.warm_n[k];
+    if (wn > 0 && (!st.warm_v[k] || !st.warm_a[k] || !st.warm_parent[k] || st.warm_parent[k][0] != -1))
+      throw EngineError(GBP_E_INVALID_ARG, "warm start: tree arrays");
+    chk(gbp_tree_create(dev, std::max<int64_t>(cap, 2 * wn), &D.tree[k]), "tree");
+    const double *root = wn > 0 ? st.warm_v[k] : (k == 0 ? s_start.data() : s_goal.data());
+    chk(gbp_tree_init(D.tree[k], root, D.stream), "tree init");
+    if (wn > 1)
+      chk(gbp_tree_append_host(D.tree[k], wn - 1, st.warm_v[k] + 8, st.warm_a[k] + 10,
+                               st.warm_parent[k] + 1, D.stream),
+          "warm start: tree append");
+    known[k] = std::max<int64_t>(1, wn);
+  }
+  if (st.warm_half < 0 || st.warm_extend < 0) throw EngineError(GBP_E_INVALID_ARG, "warm start");
+  const int32_t half0 = (int32_t)st.warm_half;
+  if (st.warm_n[0] > 0 || st.warm_n[1] > 0 || half0 > 0) extend_counter_ = st.warm_extend;
+  chk(gbp_plan_reset(D.ws, extend_counter_, D.stream), "plan reset");
   // half h extends tree h % 2 toward its draws [(h / 2) B, (h / 2 + 1) B)
   // groups grow geometrically: a short search is not charged a long group's
   // tail of gated half-iterations, a long one amortises the status read
   const int g_max = (int)std::max<int64_t>(2, std::min<int64_t>(64, (1 << 21) / batch)) & ~1;
   int group = 2;
-  int32_t half = 0;
+  int32_t half = half0;
   gbp_plan_status ps{};
   // with a stop poll (config 4's restart trees, one per rank) the ranks stop
   // together: every group ends in one poll, and only its answer ends the loop
   bool go = max_time > 0;
+  double t_first = -1;  // when this rank first saw its connection (before any poll wait)
   while (go) {
-    if (st.max_halves > 0) group = (int)std::min<int64_t>(group, st.max_halves - half);
-    for (int k = 0; k < 2; k++) {  // room for `group` halves of appends
-      int64_t c = 0;
-      chk(gbp_tree_capacity(D.tree[k], &c), "tree capacity");
-      if (known[k] + (int64_t)group * batch > c)
-        chk(gbp_tree_reserve(D.tree[k], std::max<int64_t>(2 * c, known[k] + (int64_t)group * batch),
-                             D.stream),
-            "tree reserve");
-    }
-    // the group's halves, one stream-ordered kernel sequence
-    chk(gbp_plan_halves_dev(h, D.ws, D.tree[0], D.tree[1], half, group, batch, seed_, tstream[0],
-                            tstream[1], adaptive, 0, D.stream),
-        "plan halves");
-    chk(gbp_plan_status_read(D.ws, &ps, D.stream), "plan status");
-    st.status_reads++;
-    while (ps.halt) {  // FRAGILE: re-decide on the host, resume where the sequence stopped
-      for (int b = 0; b < 3; b++) st.halts[b] += (ps.halt >> b) & 1u;
-      const int32_t h0 = ps.halt_half;
-      const int k = h0 & 1;
-      int resume = -1;
-      int64_t nres = 0;
-      chk(gbp_plan_resolve_host(h, D.ws, D.tree[k], D.tree[k ^ 1], k == 0 ? FORWARD : REVERSE,
-                                batch, adaptive, &resume, &nres, D.stream),
-          "plan resolve");
-      if (resume < 0) throw EngineError(GBP_E_INVALID_ARG, "plan resolve: nothing halted");
-      chk(gbp_plan_halves_dev(h, D.ws, D.tree[0], D.tree[1], h0, half + group - h0, batch, seed_,
-                              tstream[0], tstream[1], adaptive, resume, D.stream),
+    bool local_stop = false;
+    try {
+      if (st.max_halves > 0) group = (int)std::min<int64_t>(group, st.max_halves - (half - half0));
+      for (int k = 0; k < 2; k++) {  // room for `group` halves of appends
+        int64_t c = 0;
+        chk(gbp_tree_capacity(D.tree[k], &c), "tree capacity");
+        if (known[k] + (int64_t)group * batch > c)
+          chk(gbp_tree_reserve(D.tree[k], std::max<int64_t>(2 * c, known[k] + (int64_t)group * batch),
+                               D.stream),
+              "tree reserve");
+      }
+      // the group's halves, one stream-ordered kernel sequence
+      chk(gbp_plan_halves_dev(h, D.ws, D.tree[0], D.tree[1], half, group, batch, seed_, tstream[0],
+                              tstream[1], adaptive, 0, D.stream),
           "plan halves");
       chk(gbp_plan_status_read(D.ws, &ps, D.stream), "plan status");
       st.status_reads++;
+      while (ps.halt) {  // FRAGILE: re-decide on the host, resume where the sequence stopped
+        for (int b = 0; b < 3; b++) st.halts[b] += (ps.halt >> b) & 1u;
+        const int32_t h0 = ps.halt_half;
+        const int k = h0 & 1;
+        int resume = -1;
+        int64_t nres = 0;
+        chk(gbp_plan_resolve_host(h, D.ws, D.tree[k], D.tree[k ^ 1], k == 0 ? FORWARD : REVERSE,
+                                  batch, adaptive, &resume, &nres, D.stream),
+            "plan resolve");
+        if (resume < 0) throw EngineError(GBP_E_INVALID_ARG, "plan resolve: nothing halted");
+        chk(gbp_plan_halves_dev(h, D.ws, D.tree[0], D.tree[1], h0, half + group - h0, batch, seed_,
+                                tstream[0], tstream[1], adaptive, resume, D.stream),
+            "plan halves");
+        chk(gbp_plan_status_read(D.ws, &ps, D.stream), "plan status");
+        st.status_reads++;
+      }
+      if (ps.error & 1u) throw EngineError(GBP_E_HIP, "device planner loop: look-back spin exhausted");
+      if (ps.error) throw EngineError(GBP_E_SHAPE, "device planner loop: a tree ran out of capacity");
+      for (int k = 0; k < 2; k++) chk(gbp_tree_size(D.tree[k], &known[k], D.stream), "tree size");
+      half += group;
+      if (ps.done) goal_found = true;
+      if (ps.done && t_first < 0) t_first = since();
+      local_stop = ps.done || since() >= max_time ||
+                   (st.max_halves > 0 && half - half0 >= st.max_halves);
+    } catch (...) {
+      // the peers are (or will be) blocked in this group's poll: post a stop
+      // so that their collective completes, then fail here
+      if (st.stop_poll) st.stop_poll(st.stop_ctx, 1, 0);
+      throw;
     }
-    if (ps.error & 1u) throw EngineError(GBP_E_HIP, "device planner loop: look-back spin exhausted");
-    if (ps.error) throw EngineError(GBP_E_SHAPE, "device planner loop: a tree ran out of capacity");
-    for (int k = 0; k < 2; k++) chk(gbp_tree_size(D.tree[k], &known[k], D.stream), "tree size");
-    half += group;
-    if (ps.done) goal_found = true;
-    const bool local_stop = ps.done || since() >= max_time ||
-                            (st.max_halves > 0 && half >= st.max_halves);
     if (st.stop_poll) {
       st.polls++;
-      go = st.stop_poll(st.stop_ctx, local_stop ? 1 : 0, ps.done ? 1 : 0) == 0;
+      // nonzero = stop (a failed poll answers stop too: planner.py); a local
+      // stop always ends this rank's loop, whatever the poll answered
+      const int answer = st.stop_poll(st.stop_ctx, local_stop ? 1 : 0, ps.done ? 1 : 0);
+      go = !local_stop && answer == 0;
       if (!go && !local_stop) st.stopped_by_peer = 1;
     } else {
       go = !local_stop;
     }
     group = std::min(group * 2, g_max);
   }
-  elapsed_to_first = std::chrono::high_resolution_clock::now() - t_start;
+  elapsed_to_first = t_first >= 0 ? std::chrono::duration<double>(t_first)
+                                  : std::chrono::duration<double>(since());
   extend_counter_ = ps.ext_counter;
-  const int32_t halves_run = goal_found ? ps.meet_half + 1 : half;
+  const int32_t halves_run = (goal_found ? ps.meet_half + 1 : half) - half0;
   st.halves += halves_run;
   st.iterations += (halves_run + 1) / 2;
   st.targets += ps.stat_targets;
@@ -2135,6 +2162,16 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     if (p->algorithm == 3) {  // one device search per rank: the ranks' polls pair up
       st.stop_poll = p->stop_poll;
       st.stop_ctx = p->stop_ctx;
+      for (int k = 0; k < 2; k++) {  // warm start (a replayable continuation)
+        st.warm_n[k] = p->init_n[k];
+        st.warm_v[k] = p->init_v[k];
+        st.warm_a[k] = p->init_a[k];
+        st.warm_parent[k] = p->init_parent[k];
+      }
+      st.warm_half = p->first_half;
+      st.warm_extend = p->extend_base;
+    } else if (p->init_n[0] || p->init_n[1] || p->first_half || p->extend_base) {
+      return GBP_E_INVALID_ARG;
     }
     if (p->tree_capacity > 0) st.dump = &dump;
     const auto t0 = std::chrono::high_resolution_clock::now();

@@ -32,7 +32,9 @@ class PlanParams(ctypes.Structure):
                 ("max_halves", ctypes.c_int64),
                 ("tree_capacity", ctypes.c_int64), ("tree_v", _P * 2), ("tree_a", _P * 2),
                 ("tree_parent", _P * 2), ("tree_g", _P * 2), ("stop_poll", _P),
-                ("stop_ctx", _P)]
+                ("stop_ctx", _P), ("init_n", ctypes.c_int64 * 2), ("init_v", _P * 2),
+                ("init_a", _P * 2), ("init_parent", _P * 2), ("first_half", ctypes.c_int64),
+                ("extend_base", ctypes.c_int64)]
 
 # int (*stop_poll)(void *ctx, int local_stop, int found)
 StopPoll = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int)
@@ -111,7 +113,8 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
                      post_process=False, device=0, capacity=4096, algorithm=0, max_time_opt=0.0,
                      sampling=None, fragile_eps=None, adaptive=False, nn_stats=False,
                      max_halves=0, trees=False,
-                     tree_capacity=1 << 18, stop_poll=None):
+                     tree_capacity=1 << 18, stop_poll=None, init_trees=None, first_half=0,
+                     extend_base=0):
     """Plan start -> goal on terrain `data` (terrain_data.TerrainData).
 
     algorithm 0: batch-synchronous RRT-Connect, stops at the first solution;
@@ -137,7 +140,13 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
       algorithms 0, 1, 3), at most tree_capacity rows each;
     stop_poll: algorithm 3 — f(local_stop, found) -> bool called after every
       group of half-iterations; True stops the search (sharding.stop_together:
-      config 4's ranks stop at the first solution of any of them)."""
+      config 4's ranks stop at the first solution of any of them);
+    init_trees, first_half, extend_base: algorithm 3 — a warm start, the
+      continuation of a search: init_trees = (a, b) dicts of v [n][8], act
+      [n][10], parent [n] (root first, -1; parents before children), the first
+      half-iteration (its targets are the draws a search from the roots makes
+      there) and the candidate stream's first extend index; max_halves then
+      counts the continuation's halves."""
     L = load()
     x = np.ascontiguousarray(data.x, dtype=np.float64)
     y = np.ascontiguousarray(data.y, dtype=np.float64)
@@ -159,9 +168,26 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     p.adaptive = int(bool(adaptive))
     p.nn_stats = int(bool(nn_stats))
     p.max_halves = int(max_halves)
+    p.first_half, p.extend_base = int(first_half), int(extend_base)
+    warm = []
+    if init_trees is not None:
+        for k, t in enumerate(init_trees):
+            arrs = (np.ascontiguousarray(t["v"], np.float64).reshape(-1, 8),
+                    np.ascontiguousarray(t["act"], np.float64).reshape(-1, 10),
+                    np.ascontiguousarray(t["parent"], np.int32).reshape(-1))
+            warm.append(arrs)
+            p.init_n[k] = arrs[0].shape[0]
+            p.init_v[k], p.init_a[k], p.init_parent[k] = (x.ctypes.data for x in arrs)
     poll_cb = None
     if stop_poll is not None:
-        poll_cb = StopPoll(lambda ctx, local, found: 1 if stop_poll(bool(local), bool(found)) else 0)
+        def _poll(ctx, local, found):
+            # fail safe: an exception cannot cross ctypes (it would read as 0 =
+            # continue), so a poll that raises answers "stop"
+            try:
+                return 1 if stop_poll(bool(local), bool(found)) else 0
+            except BaseException:  # noqa: BLE001 - reported as stop
+                return 1
+        poll_cb = StopPoll(_poll)
         p.stop_poll = ctypes.cast(poll_cb, _P)
     tb = []
     if trees:
@@ -177,7 +203,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     actions = np.zeros((capacity, 10))
     rc = L.gbp_plan_rrt_connect(ctypes.byref(p), ctypes.byref(r), states.ctypes.data,
                                 actions.ctypes.data, capacity)
-    del poll_cb
+    del poll_cb, warm
     if rc != 0:
         raise _lib.GbpError(rc, "gbp_plan_rrt_connect")
     out = {k: getattr(r, k) for k, _ in PlanResult._fields_}

@@ -413,6 +413,17 @@ struct BatchStats {
   int64_t nn_rechecks = 0, nn_scans = 0;  // device loop with GBP_OPT_NN_STATS: the matrix-core
                                           // search's fp64 half-chunk re-checks / segment scans
   double extent_a[4] = {0, 0, 0, 0}, extent_b[4] = {0, 0, 0, 0};  // x_min x_max y_min y_max
+  // in (device loop): a warm start, i.e. a replayable continuation of a search
+  // (0 vertices = from the roots).  Tree k starts as warm_n[k] vertices (root
+  // first, parents before children; g derived as graph_class.cpp:36-42 does),
+  // the first half-iteration is warm_half (its targets are the draws a search
+  // from the roots would make there) and the candidate stream starts at extend
+  // index warm_extend.  max_halves then counts the continuation's halves.
+  int64_t warm_n[2] = {0, 0};
+  const double *warm_v[2] = {nullptr, nullptr};
+  const double *warm_a[2] = {nullptr, nullptr};
+  const int32_t *warm_parent[2] = {nullptr, nullptr};
+  int64_t warm_half = 0, warm_extend = 0;
 };
 
 class RRTConnectClass : public RRTClass {
@@ -637,6 +648,16 @@ typedef struct {
   double *tree_g[2];      //   vertices_a / vertices_b are not written
   int (*stop_poll)(void *ctx, int local_stop, int found);  // algorithm 3: see BatchStats
   void *stop_ctx;         //   (NULL: each run stops on its own)
+  // algorithm 3: warm start (BatchStats::warm_*): init_n[k] vertices of tree k
+  // (0 = the root given by start / goal), states [n][8], actions [n][10] and
+  // parents [n] (root -1, parents before children); the first half-iteration
+  // and the first extend index of the continuation
+  int64_t init_n[2];
+  const double *init_v[2];
+  const double *init_a[2];
+  const int32_t *init_parent[2];
+  int64_t first_half;
+  int64_t extend_base;
 } gbp_plan_params;
 
 typedef struct {

@@ -116,7 +116,8 @@ class _PlanCfg(ctypes.Structure):
                 ("action_flag", ctypes.c_int), ("state_p", ctypes.c_double),
                 ("action_p", ctypes.c_double), ("extend_base", ctypes.c_int64),
                 ("max_halves", ctypes.c_int64), ("star", ctypes.c_int),
-                ("star_delta", ctypes.c_double)]
+                ("star_delta", ctypes.c_double), ("nthreads", ctypes.c_int),
+                ("first_half", ctypes.c_int64), ("warm", ctypes.c_int)]
 
 
 class _PlanOut(ctypes.Structure):
@@ -265,21 +266,33 @@ class OracleTerrain:
 
     def plan(self, start, goal, *, batch, seed, stream_a=101, stream_b=102, max_halves=0,
              adaptive=False, sampling=None, star=False, star_delta=3.0, extend_base=0,
-             capacity=200000):
+             capacity=200000, nthreads=1, init_trees=None, first_half=0):
         """The batch-synchronous RRT-Connect (RRT*-Connect with star=True) the
         engine runs, restated on the CPU (orc_plan): returns a dict with the
         counters, the meeting / best vertices, and each tree's arrays
         ("a"/"b": v, act, parent, g, y).  sampling: dict of gbp_sampling
-        fields (state_flag, state_p, speed_direction, action_flag, action_p)."""
+        fields (state_flag, state_p, speed_direction, action_flag, action_p).
+        nthreads: OpenMP threads for the per-target / per-connection passes
+        (same result for any count: insertion stays in order).
+        init_trees / first_half: a warm start (the continuation of a search):
+        (a, b) dicts of v [n][8], act [n][10], parent [n] (root first, -1),
+        the first half-iteration; max_halves counts the continuation's."""
         trees, keep = [], []
-        for _ in range(2):
+        for k in range(2):
             arrs = dict(v=np.zeros((capacity, 8)), act=np.zeros((capacity, 10)),
                         parent=np.zeros(capacity, np.int32), g=np.zeros(capacity),
                         y=np.zeros(capacity), child=np.zeros(capacity, np.int32),
                         sibling=np.zeros(capacity, np.int32))
+            n0 = 0
+            if init_trees is not None:
+                t = init_trees[k]
+                n0 = int(np.asarray(t["parent"]).shape[0])
+                arrs["v"][:n0] = np.asarray(t["v"], np.float64).reshape(-1, 8)
+                arrs["act"][:n0] = np.asarray(t["act"], np.float64).reshape(-1, 10)
+                arrs["parent"][:n0] = np.asarray(t["parent"], np.int32)
             keep.append(arrs)
-            trees.append(_Tree(capacity, 0, *(arrs[k].ctypes.data for k in
-                                              ("v", "act", "parent", "g", "y", "child", "sibling"))))
+            trees.append(_Tree(capacity, n0, *(arrs[k].ctypes.data for k in
+                                               ("v", "act", "parent", "g", "y", "child", "sibling"))))
         tr = (_Tree * 2)(*trees)
         sm = sampling or {}
         cfg = _PlanCfg(int(batch), int(seed), int(stream_a), int(stream_b), int(bool(adaptive)),
@@ -287,7 +300,8 @@ class OracleTerrain:
                        int(bool(sm.get("speed_direction", False))),
                        int(bool(sm.get("action_flag", False))), float(sm.get("state_p", 0.0)),
                        float(sm.get("action_p", 0.0)), int(extend_base), int(max_halves),
-                       int(bool(star)), float(star_delta))
+                       int(bool(star)), float(star_delta), int(nthreads), int(first_half),
+                       int(init_trees is not None))
         out = _PlanOut()
         st, gl = _c(start, np.float64), _c(goal, np.float64)
         rc = lib().orc_plan(self.ref, _p(st), _p(gl), ctypes.byref(cfg), tr, ctypes.byref(out))

@@ -1368,23 +1368,49 @@ int orc_plan(const orc_terrain *T, const double *start, const double *goal,
   if (B < 1 || !tr || !out) return -1;
   memset(out, 0, sizeof *out);
   out->meet_a = out->meet_b = -1;
+  const int64_t h0 = cfg->warm ? cfg->first_half : 0;
   for (int k = 0; k < 2; k++) {
+    if (cfg->warm && tr[k].n > 0) {
+      /* a continuation: the given vertices in order, each joined to its parent
+       * (graph_class.cpp:36-42: g / y from the parent's) */
+      orc_tree *t = &tr[k];
+      if (t->parent[0] != -1) return -1;
+      t->g[0] = t->y[0] = 0.0;
+      for (int i = 0; i < t->n; i++)
+        if (t->child) t->child[i] = t->sibling[i] = -1;
+      for (int i = 1; i < t->n; i++) {
+        if (t->parent[i] < 0 || t->parent[i] >= i) return -1;
+        tree_add_edge(t, t->parent[i], i);
+      }
+      continue;
+    }
     tr[k].n = 0;
     tree_put(&tr[k], k == 0 ? start : goal, 0, -1, 0.0, 0.0);
   }
   const uint64_t stream[2] = {cfg->stream_a, cfg->stream_b};
-  int64_t draws[2] = {0, 0};
+  /* tree k's draws before half h0: (h >> 1) * B at half h of tree k */
+  int64_t draws[2] = {((h0 + 1) >> 1) * (int64_t)B, (h0 >> 1) * (int64_t)B};
   int64_t ext = cfg->extend_base;
   double *cand = (double *)malloc(sizeof(double) * 8 * (size_t)B);
   double *tgt = (double *)malloc(sizeof(double) * 8 * (size_t)B);
   int *added = (int *)malloc(sizeof(int) * (size_t)B);
   int *nearest = (int *)malloc(sizeof(int) * (size_t)B);
   double *a_ext = (double *)malloc(sizeof(double) * 10 * (size_t)B);
+  /* per-item results of the parallel passes (each item reads only the
+   * half's snapshot of the trees; insertion stays sequential, in order) */
+  int nthreads = cfg->nthreads > 0 ? cfg->nthreads : 1;
+  int *it_nn = (int *)malloc(sizeof(int) * (size_t)B);
+  int *it_r = (int *)malloc(sizeof(int) * (size_t)B);
+  int64_t *it_chk = (int64_t *)malloc(sizeof(int64_t) * (size_t)B);
+  int *it_cap = (int *)malloc(sizeof(int) * (size_t)B);
+  double *it_sn = (double *)malloc(sizeof(double) * 8 * (size_t)B);
+  double *it_an = (double *)malloc(sizeof(double) * 10 * (size_t)B);
+  uint8_t *it_ok = (uint8_t *)malloc((size_t)B);
   double *shared = 0; /* RRT*: (a, b) vertex pairs whose connect REACHED */
   int64_t n_shared = 0, cap_shared = 0;
   double cost_so_far = INFINITY;
   int rc = 0;
-  for (int64_t h = 0; cfg->max_halves <= 0 || h < cfg->max_halves; h++) {
+  for (int64_t h = h0; cfg->max_halves <= 0 || h < h0 + cfg->max_halves; h++) {
     const int k = (int)(h & 1);
     orc_tree *Tt = &tr[k], *O = &tr[k ^ 1];
     const int dir = k == 0 ? GBP_FORWARD : GBP_REVERSE;
@@ -1398,34 +1424,46 @@ int orc_plan(const orc_terrain *T, const double *start, const double *goal,
       const double *last = Tt->v + 8 * (int64_t)(Tt->n - 1), *root = O->v;
       orc_sample_states_dir(T, B, cfg->seed, stream[k], draws[k], cfg->state_flag, cfg->state_p,
                             cfg->state_speed_direction, dir == GBP_FORWARD ? last : root,
-                            dir == GBP_FORWARD ? root : last, cand, 1);
+                            dir == GBP_FORWARD ? root : last, cand, nthreads);
     }
     draws[k] += B;
-    int nt = 0;
+    OMP_FOR
     for (int i = 0; i < B; i++) {
       orc_stats st = {0, 0, 0};
-      if (orc_is_valid_state(T, cand + 8 * i, GBP_STANCE, &st)) memcpy(tgt + 8 * nt++, cand + 8 * i, 64);
+      it_ok[i] = (uint8_t)orc_is_valid_state(T, cand + 8 * i, GBP_STANCE, &st);
     }
+    int nt = 0;
+    for (int i = 0; i < B; i++)
+      if (it_ok[i]) memcpy(tgt + 8 * nt++, cand + 8 * i, 64);
     out->targets += nt;
     out->extends += nt;
     /* extend every target against the snapshot (rrt.cpp:77-102, planner_class.cpp:185-200) */
     const int n0 = Tt->n;
     if (Tt->n + nt > Tt->cap) { rc = -2; break; }
     int n_added = 0;
+    OMP_FOR
     for (int i = 0; i < nt; i++) {
       const double *q = tgt + 8 * i;
       const int nn = orc_nearest(Tt->v, n0, q, 0);
       const double *s_near = Tt->v + 8 * (int64_t)nn;
-      double nrm[3], acts[60], sn[8], an[10];
+      double nrm[3], acts[60];
       int ood = 0, ch;
       uint32_t cnt;
       orc_surface_normal(T, q[0], q[1], nrm, &ood);
       for (int j = 0; j < NUM_GEN_STATES; j++)
         sample_action_any(nrm, dir, cfg->action_flag, cfg->action_p, q, s_near, cfg->seed,
                           EXTD_STREAM, (ext + i) * 8 + j, acts + 10 * j);
-      const int r = orc_extend(T, s_near, q, acts, dir, cfg->adaptive, sn, an, &ch, &cnt);
-      out->attempts += ch >= 0 ? ch + 1 : NUM_GEN_STATES;
-      if (r == GBP_TRAPPED) continue;
+      it_r[i] = orc_extend(T, s_near, q, acts, dir, cfg->adaptive, it_sn + 8 * (int64_t)i,
+                           it_an + 10 * (int64_t)i, &ch, &cnt);
+      it_nn[i] = nn;
+      it_chk[i] = ch >= 0 ? ch + 1 : NUM_GEN_STATES;
+    }
+    for (int i = 0; i < nt; i++) {  /* in target order */
+      const int nn = it_nn[i];
+      const double *s_near = Tt->v + 8 * (int64_t)nn;
+      const double *sn = it_sn + 8 * (int64_t)i, *an = it_an + 10 * (int64_t)i;
+      out->attempts += it_chk[i];
+      if (it_r[i] == GBP_TRAPPED) continue;
       const int idx = Tt->n;
       tree_put(Tt, sn, an, -1, 0.0, 0.0);
       if (!star) { /* rrt.cpp:86-92 */
@@ -1435,7 +1473,7 @@ int orc_plan(const orc_terrain *T, const double *start, const double *goal,
       }
       added[n_added] = idx;
       nearest[n_added] = nn;
-      memcpy(a_ext + 10 * n_added, an, sizeof an);
+      memcpy(a_ext + 10 * n_added, an, 10 * sizeof(double));
       n_added++;
     }
     ext += nt;
@@ -1448,17 +1486,28 @@ int orc_plan(const orc_terrain *T, const double *start, const double *goal,
     const int m0 = O->n;
     if (O->n + n_added > O->cap) { rc = -2; break; }
     int meet = 0;
+    OMP_FOR
     for (int i = 0; i < n_added; i++) {
       const double *q = Tt->v + 8 * (int64_t)added[i];
       const int nn = orc_nearest(O->v, m0, q, 0);
       const double *s_ex = O->v + 8 * (int64_t)nn;
-      double sn[8] = {0}, an[10] = {0};
+      double *sn = it_sn + 8 * (int64_t)i, *an = it_an + 10 * (int64_t)i;
+      memset(sn, 0, 8 * sizeof(double));
+      memset(an, 0, 10 * sizeof(double));
       ac_stats acs = {0, 0};
-      const int r = attempt_connect_ts(T, s_ex, q, orc_pose_distance(q, s_ex) / V_NOM, sn, an, cdir,
-                                       cfg->adaptive, 0, &acs);
+      it_r[i] = attempt_connect_ts(T, s_ex, q, orc_pose_distance(q, s_ex) / V_NOM, sn, an, cdir,
+                                   cfg->adaptive, 0, &acs);
+      it_nn[i] = nn;
+      it_chk[i] = acs.checks;
+      it_cap[i] = acs.capped;
+    }
+    for (int i = 0; i < n_added; i++) {  /* in order of the new vertices */
+      const int nn = it_nn[i], r = it_r[i];
+      const double *s_ex = O->v + 8 * (int64_t)nn;
+      const double *sn = it_sn + 8 * (int64_t)i, *an = it_an + 10 * (int64_t)i;
       out->connects++;
-      out->depth_capped += acs.capped;
-      out->attempts += acs.checks;
+      out->depth_capped += it_cap[i];
+      out->attempts += it_chk[i];
       if (r == GBP_TRAPPED) continue;
       const int idx = O->n;
       tree_put(O, sn, an, -1, 0.0, 0.0);
@@ -1484,7 +1533,7 @@ int orc_plan(const orc_terrain *T, const double *start, const double *goal,
         out->solutions++;
       }
     }
-    out->halves = h + 1;
+    out->halves = h + 1 - h0;
     if (star) {
       /* the cheapest connection so far with the current g values, ranked after
        * each pair of halves (include/gbp_planner.h buildRRTStarConnectBatched) */
@@ -1522,6 +1571,13 @@ int orc_plan(const orc_terrain *T, const double *start, const double *goal,
   free(nearest);
   free(a_ext);
   free(shared);
+  free(it_nn);
+  free(it_r);
+  free(it_chk);
+  free(it_cap);
+  free(it_sn);
+  free(it_an);
+  free(it_ok);
   return rc;
 }
 

@@ -171,6 +171,11 @@ typedef struct {
   int64_t max_halves;        /* stop after this many half-iterations (<= 0: at a solution) */
   int star;                  /* RRT*-Connect: choose-parent + rewire, runs max_halves  */
   double star_delta;         /* rrt_star_connect.h:59 (3.0)                            */
+  int nthreads;              /* OpenMP threads for the per-item passes (<= 1: serial;   */
+                             /* results identical: insertion stays in order)           */
+  int64_t first_half;        /* warm start: the first half-iteration (draw indices)    */
+  int warm;                  /* warm start: tr[k].n vertices given (v, a, parent; root  */
+                             /* first, parents before children), g / y derived         */
 } orc_plan_cfg;
 
 typedef struct {

@@ -431,3 +431,28 @@ def test_engine_matches_golden_vectors(gpu):
             assert_pairs_equal(out, ref, f"golden-gpu {name} ad{ad}",
                                resolve=resolver(T, g[p + "pair_s"], g[p + "pair_a"], g[p + "pair_dir"],
                                                 bool(ad)))
+
+
+def test_config2_exact_batches(gpu):
+    """Config 2's own batches: synth-rough-256, the
+    65,536-attempt seed-20251017 batch bench.py times (workload.make_attempts)
+    and the next one of the 8 it cycles through, through the persistent kernel
+    at the bench's 2-wave launch, against the oracle on every attempt (FRAGILE
+    ones re-decided by the product's own host check, none excluded)."""
+    import global_body_planner_amd as gbp
+    from global_body_planner_amd import workload as W
+    data = td.by_name("synth-rough-256")
+    T = gbp.Terrain.from_data(data, device=0)
+    T.set_option(L.OPT_KERNEL, L.KERNEL_PERSISTENT)
+    T.set_option(L.OPT_WAVES, 2)
+    O = oracle.OracleTerrain.from_data(data)
+    n = 65536
+    for k in (0, 1):
+        s, a, d, _, tries = W.make_attempts(T, n, W.CONFIG_SEEDS[2], index_base=k * n)
+        assert int((tries < 0).sum()) == 0
+        r = T.validate_pairs(s, a, d)
+        gpu_t = (np_(r.valid), np_(r.s_new), np_(r.t_new), u32(r.flags), u32(r.counts))
+        ref = O.validate_pairs(np_(s), np_(a), np_(d), nthreads=16)
+        nfrag = assert_pairs_equal(gpu_t, ref, f"config2 batch {k}", resolve=resolver(T, s, a, d))
+        assert nfrag < 50
+        assert 0 < ref[0].sum() < n

@@ -237,3 +237,46 @@ def test_rmath_accuracy():
     c = np.concatenate([rng.uniform(-1, 1, 200000), [-1.0, 1.0, 0.0]])
     assert ulp(oracle.rmath(3, c), np.arccos(c)).max() <= 8
     assert oracle.rmath(3, [1.0])[0] == 0.0 and oracle.rmath(3, [-1.0])[0] == np.pi
+
+
+@pytest.mark.parametrize("star", [False, True])
+def test_orc_plan_threads_identical(synth, star):
+    """orc_plan's per-item passes on OpenMP threads (the config-3-scale GPU
+    test runs it on the box's cores) give the serial run's trees, counters and
+    meeting vertices bit for bit: each item reads only the half's snapshot and
+    insertion stays in order."""
+    O, start, goal = synth
+    kw = dict(batch=1024, seed=5, max_halves=40 if star else 0, star=star)
+    if star:
+        kw.update(stream_a=401, stream_b=402)
+    one = O.plan(start, goal, nthreads=1, **kw)
+    many = O.plan(start, goal, nthreads=4, **kw)
+    for k, v in one.items():
+        if k in ("a", "b"):
+            for f in ("v", "act", "parent", "g", "y"):
+                assert np.array_equal(bits(v[f]), bits(many[k][f])), (k, f)
+        elif k in ("states", "actions"):
+            assert np.array_equal(bits(v), bits(many[k])), k
+        else:
+            assert (v == many[k]) or (v != v and many[k] != many[k]), k
+
+
+def test_orc_plan_warm_start_is_continuation(synth):
+    """A warm start (the trees after h0 half-iterations, the draw indices of
+    half h0, the candidate stream at the extend counter) continues the search
+    exactly: the same trees as the uninterrupted run (the config-3-scale GPU
+    test continues device-grown trees this way)."""
+    O, start, goal = synth
+    kw = dict(batch=512, seed=9)
+    full = O.plan(start, goal, max_halves=30, **kw)
+    assert not full["found"]
+    first = O.plan(start, goal, max_halves=17, **kw)
+    init = tuple({k: first[t][k] for k in ("v", "act", "parent")} for t in "ab")
+    cont = O.plan(start, goal, max_halves=13, init_trees=init, first_half=17,
+                  extend_base=first["ext_counter"], nthreads=2, **kw)
+    assert cont["halves"] == 13
+    assert cont["targets"] + first["targets"] == full["targets"]
+    assert cont["attempts"] + first["attempts"] == full["attempts"]
+    for t in "ab":
+        for f in ("v", "act", "parent", "g", "y"):
+            assert np.array_equal(bits(cont[t][f]), bits(full[t][f])), (t, f)
