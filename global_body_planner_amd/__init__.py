@@ -15,12 +15,12 @@ from ._lib import (ADVANCED, FLIGHT, FORWARD, REACHED, REVERSE, STANCE, TRAPPED,
                    KERNEL_DIRECT, KERNEL_PERSISTENT)
 from .terrain_data import TerrainData, csv_gridmap, csv_direct, synth_rough, synth_fractal
 from .engine import (Terrain, PairResult, ExtendResult, DeviceTree, PlanWorkspace, nearest,
-                     neighbors, knn, device_count)
+                     neighbors, knn, knn_yaw, device_count)
 
 __all__ = [
     "ADVANCED", "FLIGHT", "FORWARD", "REACHED", "REVERSE", "STANCE", "TRAPPED", "GbpError",
     "KERNEL_DIRECT", "KERNEL_PERSISTENT", "TerrainData", "csv_gridmap", "csv_direct",
     "synth_rough", "synth_fractal", "Terrain", "PairResult", "ExtendResult", "DeviceTree",
-    "PlanWorkspace", "nearest", "neighbors", "knn", "device_count",
+    "PlanWorkspace", "nearest", "neighbors", "knn", "knn_yaw", "device_count",
 ]
 __version__ = "0.2.0"

@@ -44,6 +44,7 @@ EXPORTS = [
     "gbp_extend_batch_dev", "gbp_extend_batch_host",
     "gbp_nearest_batch_dev", "gbp_nearest_batch_host",
     "gbp_neighbors_batch_dev", "gbp_neighbors_batch_host", "gbp_knn_batch_dev", "gbp_knn_batch_host",
+    "gbp_knn_yaw_batch_dev", "gbp_knn_yaw_batch_host", "gbp_host_yaw",
     "gbp_resolve_fragile_host", "gbp_resolve_fragile_states_host", "gbp_extend_resolve_host",
     "gbp_stream_create", "gbp_stream_destroy",
     "gbp_tree_create", "gbp_tree_destroy", "gbp_tree_init", "gbp_tree_reserve", "gbp_tree_capacity",
@@ -160,6 +161,10 @@ def load(path=None):
         "gbp_neighbors_batch_host": (I, [I64, P, I64, P, ctypes.c_double, I, P, P]),
         "gbp_knn_batch_dev": (I, [I64, P, I64, P, I, P, P, P]),
         "gbp_knn_batch_host": (I, [I64, P, I64, P, I, P, P]),
+        "gbp_knn_yaw_batch_dev": (I, [I64, P, P, I64, P, P, ctypes.c_double, ctypes.c_double, I, P,
+                                      P, P]),
+        "gbp_knn_yaw_batch_host": (I, [I64, P, I64, P, ctypes.c_double, ctypes.c_double, I, P, P]),
+        "gbp_host_yaw": (ctypes.c_double, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name, None)

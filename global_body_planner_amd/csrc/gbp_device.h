@@ -724,6 +724,23 @@ __device__ __forceinline__ double state_distance(const double *q1, const double 
   return sqrt(sum);
 }
 
+__device__ __forceinline__ double pose_distance(const double *q1, const double *q2) {
+  double sum = 0;  // planning_utils.cpp:106-115
+#pragma unroll
+  for (int i = 0; i < 3; i++) sum = sum + (q2[i] - q1[i]) * (q2[i] - q1[i]);
+  return sqrt(sum);
+}
+
+// stateYawDistance (planning_utils.h:133-145) on the two states' yaws, which
+// the caller forms with glibc's atan2(q[4], q[3]) as the reference does (no
+// device atan2 reproduces glibc's bits); std::min / std::max as selects
+__device__ __forceinline__ double yaw_distance(double yaw1, double yaw2) {
+  const double yaw_min = (yaw2 < yaw1) ? yaw2 : yaw1;
+  const double yaw_max = (yaw1 < yaw2) ? yaw2 : yaw1;
+  const double a = yaw_max - yaw_min, b = yaw_min + 2 * MY_PI - yaw_max;
+  return (b < a) ? b : a;
+}
+
 // ---- Philox4x32-10 counter RNG (Salmon et al., SC'11) -------------------------
 __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll

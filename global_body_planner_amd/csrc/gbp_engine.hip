@@ -191,7 +191,27 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
     const uint8_t *__restrict__ dir, int dir_all, uint8_t *__restrict__ valid,
     double *__restrict__ s_new, double *__restrict__ t_new, uint32_t *__restrict__ flags,
     uint32_t *__restrict__ counts, const int *__restrict__ n_dev, int helpers, int xcd_map) {
+#ifndef GBP_LDS_TERRAIN
   const TerrainView<ZT> T = CM == 1 ? stage_coords(T0, gbp_smem) : T0;
+#else
+  // A/B variant (upper bound of LDS terrain tiles): the
+  // whole x-pair height array staged in LDS behind the s_new rings (only
+  // terrains small enough: the host checks the fit), every gather from LDS
+  TerrainView<ZT> T = CM == 1 ? stage_coords(T0, gbp_smem) : T0;
+  {
+    ZT *zl = (ZT *)((SnewRec *)(gbp_smem + (CM == 1 ? (T0.nx + T0.ny + 1) & ~1 : 0) +
+                                (size_t)blockDim.x * SA_ROW) +
+                    (blockDim.x / WAVE) * SN_RING);
+    const int nz = 2 * (T0.nx - 1) * T0.ny;  // ZT elements (even: 8-B aligned pairs)
+    typedef ZT zpair __attribute__((ext_vector_type(2)));
+    for (int i = threadIdx.x; i < nz / 2; i += blockDim.x)
+      ((zpair *)zl)[i] = ((const zpair *)T0.z)[i];
+    __syncthreads();
+#ifndef GBP_LDS_TERRAIN_STAGE_ONLY
+    T.z = zl;
+#endif
+  }
+#endif
   if (n_dev) n = *n_dev;  // batch size produced on the device (planner loop)
   const int lane = threadIdx.x & (WAVE - 1);
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
@@ -364,7 +384,22 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
     lp[7] += 1;
 #endif
     const bool fin = owner && decided;
+#ifdef GBP_SNEW_IMMEDIATE
+    // A/B variant: the deciding lane forms s_new from its LDS row at once
+    // (round 3's form; no ring, no re-read of the rows)
+    if (fin && s_new && L.snew_kind != SN_NONE) {
+      double o[8];
+      sample_state(L.s, L.a,
+                   L.snew_kind == SN_STANCE_S ? ST_FWD_STANCE
+                                              : (L.snew_kind == SN_FLIGHT_B ? ST_FWD_LAND : ST_REV_STANCE),
+                   L.snew_p, o);
+#pragma unroll
+      for (int k = 0; k < 8; k++) s_new[8 * (size_t)L.idx + k] = o[k];
+    }
+    const bool queue = false;
+#else
     const bool queue = fin && s_new && L.snew_kind != SN_NONE;
+#endif
     if (fin) {
       const size_t i = (size_t)L.idx;
       uint32_t f = L.f | L.acc.flags;
@@ -718,9 +753,15 @@ __device__ __forceinline__ void knn_cx(double &kd, int &ki, double &od, int j, b
   }
 }
 
+// YAW: the cost_add_yaw distance of neighborhoodN (planner_class.cpp:157-158,
+// planning_utils.h:146-155): poseDistance(q, v) * lw + stateYawDistance(q, v)
+// * yw, the yaws given (glibc atan2, formed by the caller)
+template <bool YAW>
 __global__ __launch_bounds__(256) void k_knn(int64_t n_query, const double *__restrict__ q,
                                              int64_t n_vert, const double *__restrict__ v, int nk,
-                                             int32_t *__restrict__ out, double *__restrict__ dist) {
+                                             int32_t *__restrict__ out, double *__restrict__ dist,
+                                             const double *__restrict__ qyaw,
+                                             const double *__restrict__ vyaw, double lw, double yw) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x / WAVE);
   for (int64_t qi = blockIdx.x * (int64_t)(blockDim.x / WAVE) + threadIdx.x / WAVE; qi < n_query;
@@ -736,7 +777,10 @@ __global__ __launch_bounds__(256) void k_knn(int64_t n_query, const double *__re
       double cd = INFINITY, co = __builtin_nan("");
       int ci = 0x7FFFFFFF;
       if (j < n_vert) {
-        co = state_distance(qq, v + 8 * j);
+        if constexpr (YAW)
+          co = pose_distance(qq, v + 8 * j) * lw + yaw_distance(qyaw[qi], vyaw[j]) * yw;
+        else
+          co = state_distance(qq, v + 8 * j);
         cd = isnan(co) ? INFINITY : co;
         ci = (int)j;
       }
@@ -844,8 +888,14 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
       // (65,536 attempts: 0.084 -> 0.072 ms; 262,144: unchanged)
       const int64_t g = std::max<int64_t>(1, std::min<int64_t>(resident, (m + WAVE - 1) / WAVE));
       const size_t ring = sizeof(SnewRec) * SN_RING * (size_t)(block / WAVE);
+#ifdef GBP_LDS_TERRAIN
+      const size_t zb = sizeof(ZT) * 2 * (size_t)(t->nx - 1) * t->ny;
+      if (coords + rows + ring + zb > t->lds_max) return GBP_E_SHAPE;  // the A/B variant only
+#else
+      const size_t zb = 0;
+#endif
       hipLaunchKernelGGL((k_validate_persistent<ZT, AD, W, CM, ONE>), dim3((unsigned)g), dim3(block),
-                         coords + rows + ring, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
+                         coords + rows + ring + zb, st, T, (int)m, s + 8 * off, a + 10 * off, d, dir_all, v, sn, tn,
                          flags + off, c, n_dev, (int)t->opt_helpers,
                          (int)t->opt_xcd_map);
     }
@@ -1535,8 +1585,26 @@ int gbp_knn_batch_dev(int64_t n_query, const double *queries, int64_t n_vert,
   if (n_query == 0) return GBP_OK;
   if (n_vert > 0 && !vertices) return GBP_E_INVALID_ARG;
   const unsigned grid = (unsigned)std::min<int64_t>((n_query + 3) / 4, 65535);
-  hipLaunchKernelGGL(k_knn, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_query, queries,
-                     n_vert, vertices, n_nearest, out, dist);
+  hipLaunchKernelGGL(k_knn<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_query, queries,
+                     n_vert, vertices, n_nearest, out, dist, nullptr, nullptr, 0.0, 0.0);
+  HIPCHK(hipGetLastError());
+  return GBP_OK;
+}
+
+int gbp_knn_yaw_batch_dev(int64_t n_query, const double *queries, const double *query_yaw,
+                          int64_t n_vert, const double *vertices, const double *vertex_yaw,
+                          double length_weight, double yaw_weight, int n_nearest, int32_t *out,
+                          double *dist, gbp_stream stream) {
+  if (n_query < 0 || n_vert < 0 || n_nearest < 1 || n_nearest > GBP_KNN_MAX ||
+      (n_query > 0 && (!queries || !query_yaw || !out)))
+    return GBP_E_INVALID_ARG;
+  if (n_vert > 0x7FFFFFFE) return GBP_E_SHAPE;
+  if (n_query == 0) return GBP_OK;
+  if (n_vert > 0 && (!vertices || !vertex_yaw)) return GBP_E_INVALID_ARG;
+  const unsigned grid = (unsigned)std::min<int64_t>((n_query + 3) / 4, 65535);
+  hipLaunchKernelGGL(k_knn<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_query, queries,
+                     n_vert, vertices, n_nearest, out, dist, query_yaw, vertex_yaw, length_weight,
+                     yaw_weight);
   HIPCHK(hipGetLastError());
   return GBP_OK;
 }
@@ -1874,6 +1942,47 @@ int gbp_knn_batch_host(int64_t n_query, const double *queries, int64_t n_vert,
       hipMemcpy(dv, vertices, 64 * n_vert, hipMemcpyHostToDevice) != hipSuccess)
     rc = GBP_E_HIP;
   if (!rc) rc = gbp_knn_batch_dev(n_query, dq, n_vert, dv, n_nearest, dout, dd, nullptr);
+  if (!rc && hipMemcpy(out, dout, 4 * nout, hipMemcpyDeviceToHost) != hipSuccess) rc = GBP_E_HIP;
+  if (!rc && dist && hipMemcpy(dist, dd, 8 * nout, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = GBP_E_HIP;
+  (void)hipFree(buf);
+  return rc;
+}
+
+int gbp_knn_yaw_batch_host(int64_t n_query, const double *queries, int64_t n_vert,
+                           const double *vertices, double length_weight, double yaw_weight,
+                           int n_nearest, int32_t *out, double *dist) {
+  if (n_query <= 0) return n_query == 0 ? GBP_OK : GBP_E_INVALID_ARG;
+  if (!queries || !out || n_nearest < 1 || n_nearest > GBP_KNN_MAX || (n_vert > 0 && !vertices))
+    return GBP_E_INVALID_ARG;
+  // the yaws with glibc (planning_utils.h:135-136), as the reference forms them
+  const int64_t nv = n_vert > 0 ? n_vert : 1;
+  std::vector<double> qy((size_t)n_query), vy((size_t)nv, 0.0);
+  for (int64_t i = 0; i < n_query; i++) qy[i] = gbp_host_yaw(queries + 8 * i);
+  for (int64_t j = 0; j < n_vert; j++) vy[j] = gbp_host_yaw(vertices + 8 * j);
+  void *buf = nullptr;
+  const size_t nout = (size_t)n_query * (size_t)n_nearest;
+  const size_t need = rnd(64 * n_query) + rnd(64 * nv) + rnd(8 * n_query) + rnd(8 * nv) +
+                      rnd(4 * nout) + rnd(8 * nout) + 1024;
+  if (hipMalloc(&buf, need) != hipSuccess) return GBP_E_ALLOC;
+  char *p = (char *)buf;
+  double *dq = (double *)p; p += rnd(64 * n_query);
+  double *dv = (double *)p; p += rnd(64 * nv);
+  double *dqy = (double *)p; p += rnd(8 * n_query);
+  double *dvy = (double *)p; p += rnd(8 * nv);
+  int32_t *dout = (int32_t *)p; p += rnd(4 * nout);
+  double *dd = (double *)p;
+  int rc = GBP_OK;
+  if (hipMemcpy(dq, queries, 64 * n_query, hipMemcpyHostToDevice) != hipSuccess) rc = GBP_E_HIP;
+  if (!rc && hipMemcpy(dqy, qy.data(), 8 * n_query, hipMemcpyHostToDevice) != hipSuccess)
+    rc = GBP_E_HIP;
+  if (!rc && n_vert > 0 &&
+      (hipMemcpy(dv, vertices, 64 * n_vert, hipMemcpyHostToDevice) != hipSuccess ||
+       hipMemcpy(dvy, vy.data(), 8 * n_vert, hipMemcpyHostToDevice) != hipSuccess))
+    rc = GBP_E_HIP;
+  if (!rc)
+    rc = gbp_knn_yaw_batch_dev(n_query, dq, dqy, n_vert, dv, dvy, length_weight, yaw_weight,
+                               n_nearest, dout, dd, nullptr);
   if (!rc && hipMemcpy(out, dout, 4 * nout, hipMemcpyDeviceToHost) != hipSuccess) rc = GBP_E_HIP;
   if (!rc && dist && hipMemcpy(dist, dd, 8 * nout, hipMemcpyDeviceToHost) != hipSuccess)
     rc = GBP_E_HIP;

@@ -146,13 +146,6 @@ __device__ __forceinline__ void raise_gate(gbp_plan_status *st, uint64_t seq) {
   atomicMin((unsigned long long *)&st->gate_seq, (unsigned long long)seq);
 }
 
-__device__ __forceinline__ double pose_distance(const double *q1, const double *q2) {
-  double sum = 0;  // planning_utils.cpp:106-115
-#pragma unroll
-  for (int i = 0; i < 3; i++) sum = sum + (q2[i] - q1[i]) * (q2[i] - q1[i]);
-  return sqrt(sum);
-}
-
 __device__ __forceinline__ void copy8(double *d, const double *s) {
 #pragma unroll
   for (int k = 0; k < 8; k++) d[k] = s[k];

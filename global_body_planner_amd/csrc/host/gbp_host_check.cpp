@@ -397,3 +397,9 @@ int attempt_connect(const Terrain &T, const double *s_existing, const double *s0
 }
 
 }  // namespace gbp_host
+
+// the reference's yaw of a state with glibc (planning_utils.h:135-136), for the
+// device's yaw-weighted k-nearest (gbp_knn_yaw_batch_dev takes the yaws)
+extern "C" __attribute__((visibility("default"))) double gbp_host_yaw(const double *s) {
+  return std::atan2(s[4], s[3]);
+}

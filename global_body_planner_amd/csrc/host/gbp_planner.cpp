@@ -532,6 +532,7 @@ PlannerClass::~PlannerClass() {
   if (d_vertices_) gbp_device_free(d_vertices_);
   if (d_scratch_) gbp_device_free(d_scratch_);
   if (d_nbr_) gbp_device_free(d_nbr_);
+  if (d_yaw_) gbp_device_free(d_yaw_);
 }
 
 PlannerClass::PlannerClass(const PlannerClass &o)
@@ -546,10 +547,13 @@ PlannerClass &PlannerClass::operator=(const PlannerClass &o) {
   if (d_vertices_) gbp_device_free(d_vertices_);
   if (d_scratch_) gbp_device_free(d_scratch_);
   if (d_nbr_) gbp_device_free(d_nbr_);
+  if (d_yaw_) gbp_device_free(d_yaw_);
   d_vertices_ = nullptr;
   d_scratch_ = nullptr;
   d_nbr_ = nullptr;
+  d_yaw_ = nullptr;
   d_capacity_ = d_count_ = d_scratch_cap_ = 0;
+  d_yaw_cap_ = d_yaw_count_ = 0;
   d_nbr_bytes_ = 0;
   device_ = o.device_;
   vertices_ = o.vertices_;
@@ -575,6 +579,7 @@ void PlannerClass::init(State s, bool f, double lw, double yw) {  // graph_class
   g_.clear();
   y_.clear();
   d_count_ = 0;
+  d_yaw_count_ = 0;
   addVertex(0, s);
   g_[0] = 0;
   y_[0] = 0;
@@ -594,6 +599,7 @@ void PlannerClass::addVertex(int idx, State s) {
   }
   vertices_[idx] = s;
   if (idx < d_count_) d_count_ = idx;  // re-upload from here
+  if (idx < d_yaw_count_) d_yaw_count_ = idx;
 }
 
 void PlannerClass::addEdge(int idx1, int idx2) {  // graph_class.cpp:36-42
@@ -641,6 +647,28 @@ void PlannerClass::sync_device() {
         "tree upload");
     chk(gbp_stream_synchronize(nullptr), "tree upload");  // pageable source
     d_count_ = V;
+  }
+}
+
+void PlannerClass::sync_yaw() {
+  const int64_t V = (int64_t)vertices_.size();
+  if (V > d_yaw_cap_) {
+    int64_t cap = std::max<int64_t>(1024, d_yaw_cap_);
+    while (cap < V) cap *= 2;
+    void *p = nullptr;
+    chk(gbp_device_alloc(device_, (size_t)cap * sizeof(double), &p), "yaw alloc");
+    if (d_yaw_) gbp_device_free(d_yaw_);
+    d_yaw_ = (double *)p;
+    d_yaw_cap_ = cap;
+    d_yaw_count_ = 0;
+  }
+  if (d_yaw_count_ < V) {
+    std::vector<double> y((size_t)(V - d_yaw_count_));
+    for (int64_t i = d_yaw_count_; i < V; i++) y[i - d_yaw_count_] = gbp_host_yaw(vertices_[i].data());
+    chk(gbp_memcpy_h2d(d_yaw_ + d_yaw_count_, y.data(), y.size() * sizeof(double), nullptr),
+        "yaw upload");
+    chk(gbp_stream_synchronize(nullptr), "yaw upload");  // pageable source
+    d_yaw_count_ = V;
   }
 }
 
@@ -775,21 +803,32 @@ std::vector<std::vector<int>> PlannerClass::neighborhoodDistBatch(const std::vec
 
 std::vector<int> PlannerClass::neighborhoodN(State q, int N) {  // :151-171
   const int V = (int)vertices_.size();
-  if (!cost_add_yaw_flag_ && N >= 1 && N <= GBP_KNN_MAX && V > 0) {
+  if (N >= 1 && N <= GBP_KNN_MAX && V > 0) {
     // the engine's k-nearest wavefront scan (gbp_knn_batch_dev): the heap's
-    // pop order, ascending (stateDistance, index)
+    // pop order, ascending (stateDistance, index); with cost_add_yaw the
+    // weighted distance (:157-158) on the vertices' glibc yaws
     sync_device();
-    ensure_scratch(256);  // one query row + N indices
+    ensure_scratch(256);  // one query row (+ its yaw) + N indices
     double *dq = (double *)d_scratch_;
-    int32_t *dout = (int32_t *)(dq + 8);
+    int32_t *dout = (int32_t *)(dq + 9);
     std::vector<int32_t> out(N);
-    chk(gbp_memcpy_h2d(dq, q.data(), sizeof(State), nullptr), "knn upload");
-    chk(gbp_knn_batch_dev(1, dq, V, d_vertices_, N, dout, nullptr, nullptr), "neighborhoodN");
+    double qrow[9];
+    std::copy(q.begin(), q.end(), qrow);
+    qrow[8] = gbp_host_yaw(q.data());
+    chk(gbp_memcpy_h2d(dq, qrow, sizeof qrow, nullptr), "knn upload");
+    if (cost_add_yaw_flag_) {
+      sync_yaw();
+      chk(gbp_knn_yaw_batch_dev(1, dq, dq + 8, V, d_vertices_, d_yaw_, cost_add_yaw_length_weight_,
+                                cost_add_yaw_yaw_weight_, N, dout, nullptr, nullptr),
+          "neighborhoodN");
+    } else {
+      chk(gbp_knn_batch_dev(1, dq, V, d_vertices_, N, dout, nullptr, nullptr), "neighborhoodN");
+    }
     chk(gbp_memcpy_d2h(out.data(), dout, (size_t)N * sizeof(int32_t), nullptr), "knn download");
     chk(gbp_stream_synchronize(nullptr), "knn sync");
     return std::vector<int>(out.begin(), out.begin() + std::min(N, V));
   }
-  // the yaw-weighted distance (cost_add_yaw, glibc atan2) or N > GBP_KNN_MAX: on the host
+  // N > GBP_KNN_MAX (or an empty tree): on the host
   std::vector<std::pair<double, int>> d;
   for (int i = 0; i < (int)vertices_.size(); i++)
     d.push_back({stateDistance(q, vertices_[i], cost_add_yaw_flag_, cost_add_yaw_length_weight_,
@@ -2134,6 +2173,9 @@ bool RRTStarConnectClass::buildRRTStarConnectBatched(FastTerrainMap &terrain, St
 // ============================================================================
 // flat C entry point
 // ============================================================================
+// the layout planner.py's PlanParams mirrors (tests/test_abi.py)
+static_assert(sizeof(gbp_plan_params) == 456, "gbp_plan_params layout");
+
 extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r,
                                     double *path_states, double *path_actions, int capacity) {
   using namespace gbp_amd;

@@ -526,6 +526,22 @@ def knn(queries, vertices, n_nearest):
     return out, dist
 
 
+def knn_yaw(queries, vertices, n_nearest, length_weight=1.0, yaw_weight=1.0):
+    """PlannerClass::neighborhoodN with cost_add_yaw set (planner_class.cpp:157-158):
+    the key poseDistance * length_weight + stateYawDistance * yaw_weight, the
+    yaws formed with glibc on the host (gbp_knn_yaw_batch_host; the scan runs
+    on the device).  numpy in, (idx [n, n_nearest] int32, dist) numpy out."""
+    lib = L.load()
+    q = np.ascontiguousarray(queries, np.float64).reshape(-1, 8)
+    v = np.ascontiguousarray(vertices, np.float64).reshape(-1, 8)
+    out = np.empty((q.shape[0], int(n_nearest)), np.int32)
+    dist = np.empty((q.shape[0], int(n_nearest)))
+    check(lib.gbp_knn_yaw_batch_host(q.shape[0], _np_ptr(q), v.shape[0], _np_ptr(v),
+                                     float(length_weight), float(yaw_weight), int(n_nearest),
+                                     _np_ptr(out), _np_ptr(dist)), "knn_yaw")
+    return out, dist
+
+
 def device_count():
     lib = L.load()
     c = ctypes.c_int(0)

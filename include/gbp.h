@@ -361,14 +361,29 @@ int gbp_neighbors_batch_host(int64_t n_query, const double *queries, int64_t n_v
  * std::pair<double, int> — ascending distance, equal distances by ascending
  * index; a NaN distance orders after every number.  dist[i][...] (may be NULL)
  * their distances; entries k .. n_nearest-1 are -1 / NaN.  1 <= n_nearest <=
- * GBP_KNN_MAX.  The reference's cost_add_yaw variant (yaw-weighted distance,
- * glibc atan2) is the host's (include/gbp_planner.h PlannerClass::neighborhoodN). */
+ * GBP_KNN_MAX.  The reference's cost_add_yaw variant: gbp_knn_yaw_batch_dev. */
 #define GBP_KNN_MAX 64
 int gbp_knn_batch_dev(int64_t n_query, const double *queries, int64_t n_vert,
                       const double *vertices, int n_nearest, int32_t *out, double *dist,
                       gbp_stream stream);
 int gbp_knn_batch_host(int64_t n_query, const double *queries, int64_t n_vert,
                        const double *vertices, int n_nearest, int32_t *out, double *dist);
+
+/* neighborhoodN with cost_add_yaw set (planner_class.cpp:151-171 with
+ * stateDistance(q, v, true, lw, yw), planning_utils.h:146-155): the order key
+ * is poseDistance(q, v) * length_weight + stateYawDistance(q, v) * yaw_weight,
+ * ordered as gbp_knn_batch_dev.  The yaws atan2(s[4], s[3]) are the caller's
+ * (query_yaw[n_query], vertex_yaw[n_vert], glibc's bits: no device atan2
+ * reproduces them); the _host entry forms them with glibc itself. */
+int gbp_knn_yaw_batch_dev(int64_t n_query, const double *queries, const double *query_yaw,
+                          int64_t n_vert, const double *vertices, const double *vertex_yaw,
+                          double length_weight, double yaw_weight, int n_nearest, int32_t *out,
+                          double *dist, gbp_stream stream);
+int gbp_knn_yaw_batch_host(int64_t n_query, const double *queries, int64_t n_vert,
+                           const double *vertices, double length_weight, double yaw_weight,
+                           int n_nearest, int32_t *out, double *dist);
+/* atan2(s[4], s[3]) with glibc (the reference's yaw of a state, planning_utils.h:135) */
+double gbp_host_yaw(const double *state);
 
 /* ---- streams ------------------------------------------------------------ */
 int gbp_stream_create(int device, gbp_stream *out);  /* a non-blocking HIP stream */

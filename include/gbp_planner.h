@@ -274,6 +274,7 @@ class PlannerClass {
 
  private:
   void sync_device();
+  void sync_yaw();  // the vertices' glibc yaws on the device (cost_add_yaw neighborhoodN)
   void ensure_scratch(int64_t nq);
   int device_;
   std::vector<State> vertices_;
@@ -289,6 +290,8 @@ class PlannerClass {
   int64_t d_scratch_cap_ = 0;
   void *d_nbr_ = nullptr;       // neighbourhood queries + output lists
   size_t d_nbr_bytes_ = 0;
+  double *d_yaw_ = nullptr;     // atan2(v[4], v[3]) per vertex (glibc), uploaded on demand
+  int64_t d_yaw_cap_ = 0, d_yaw_count_ = 0;
   uint64_t seed_ = 1, stream_id_ = 100;
   int64_t draws_ = 0;
 };

@@ -77,6 +77,8 @@ def lib():
             "orc_nearest_batch": (None, [I64, P, I, P, P, P, I]),
             "orc_neighbors_batch": (None, [I64, P, I, P, D, I, P, P, I]),
             "orc_knn_batch": (None, [I64, P, I, P, I, P, P, I]),
+            "orc_knn_yaw_batch": (None, [I64, P, I, P, I, I, D, D, P, P, I]),
+            "orc_state_distance_yaw": (D, [P, P, I, D, D]),
             "orc_sample_states": (None, [P, I64, U64, U64, I64, I, I, P, P, I]),
             "orc_sample_actions": (None, [I64, P, U64, U64, I64, P, I]),
             "orc_sample_states_dir": (None, [P, I64, U64, U64, I64, I, D, I, P, P, P, I]),
@@ -413,6 +415,23 @@ def knn_batch(queries, verts, n_nearest, nthreads=1):
     lib().orc_knn_batch(q.shape[0], _p(q), v.shape[0], _p(v), int(n_nearest), _p(out), _p(dist),
                         nthreads)
     return out, dist
+
+
+def knn_yaw_batch(queries, verts, n_nearest, length_weight, yaw_weight, nthreads=1):
+    """neighborhoodN with cost_add_yaw set (planner_class.cpp:157-158): the key
+    poseDistance * length_weight + stateYawDistance * yaw_weight (glibc atan2)."""
+    q = _c(queries, np.float64).reshape(-1, 8)
+    v = _c(verts, np.float64).reshape(-1, 8)
+    out = np.empty((q.shape[0], n_nearest), np.int32)
+    dist = np.empty((q.shape[0], n_nearest))
+    lib().orc_knn_yaw_batch(q.shape[0], _p(q), v.shape[0], _p(v), int(n_nearest), 1,
+                            float(length_weight), float(yaw_weight), _p(out), _p(dist), nthreads)
+    return out, dist
+
+
+def state_distance_yaw(q1, q2, length_weight, yaw_weight):
+    return lib().orc_state_distance_yaw(_p(_c(q1, np.float64)), _p(_c(q2, np.float64)), 1,
+                                        float(length_weight), float(yaw_weight))
 
 
 def apply_stance(s, a, t):

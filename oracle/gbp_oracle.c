@@ -779,6 +779,34 @@ static int knn_cmp(const void *pa, const void *pb) {
   return (a->i > b->i) - (a->i < b->i);
 }
 
+/* planning_utils.h:146-155: stateDistance(q1, q2, cost_add_yaw_flag, lw, yw) */
+double orc_state_distance_yaw(const double *q1, const double *q2, int flag, double lw, double yw) {
+  if (flag) return orc_pose_distance(q1, q2) * lw + orc_state_yaw_distance(q1, q2) * yw;
+  return orc_state_distance(q1, q2);
+}
+
+/* neighborhoodN, the key stateDistance(q, v, flag, lw, yw) (planner_class.cpp:157-158) */
+void orc_knn_yaw_batch(int64_t n_q, const double *q, int n_vert, const double *verts, int n_nearest,
+                       int flag, double lw, double yw, int32_t *out, double *dist, int nthreads) {
+  if (nthreads <= 0) nthreads = 1;
+  OMP_FOR
+  for (int64_t i = 0; i < n_q; i++) {
+    knn_entry *e = (knn_entry *)malloc(sizeof(knn_entry) * (size_t)(n_vert > 0 ? n_vert : 1));
+    for (int v = 0; v < n_vert; v++) {
+      double d = orc_state_distance_yaw(q + 8 * i, verts + (long)v * 8, flag, lw, yw);
+      e[v].d = d;
+      e[v].key = isnan(d) ? INFINITY : d;
+      e[v].i = v;
+    }
+    qsort(e, (size_t)n_vert, sizeof(knn_entry), knn_cmp);
+    for (int k = 0; k < n_nearest; k++) {
+      out[i * n_nearest + k] = k < n_vert ? e[k].i : -1;
+      if (dist) dist[i * n_nearest + k] = k < n_vert ? e[k].d : NAN;
+    }
+    free(e);
+  }
+}
+
 void orc_knn_batch(int64_t n_q, const double *q, int n_vert, const double *verts, int n_nearest,
                    int32_t *out, double *dist, int nthreads) {
   if (nthreads <= 0) nthreads = 1;

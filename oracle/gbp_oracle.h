@@ -118,6 +118,10 @@ void orc_neighbors_batch(int64_t n_q, const double *q, int n_vert, const double 
                          double radius, int max_out, int32_t *out, int32_t *count, int nthreads);
 
 /* planner_class.cpp:151-171 (neighborhoodN): ascending (distance, index) */
+/* planning_utils.h:146-155 and neighborhoodN with cost_add_yaw (glibc atan2) */
+double orc_state_distance_yaw(const double *q1, const double *q2, int flag, double lw, double yw);
+void orc_knn_yaw_batch(int64_t n_q, const double *q, int n_vert, const double *verts, int n_nearest,
+                       int flag, double lw, double yw, int32_t *out, double *dist, int nthreads);
 void orc_knn_batch(int64_t n_q, const double *q, int n_vert, const double *verts, int n_nearest,
                    int32_t *out, double *dist, int nthreads);
 

@@ -108,9 +108,10 @@ def test_planner_library_exports_and_fails_without_device():
     # the C structs mirror the header layout: ... + max_time_opt (double) +
     # gbp_sampling (32) + fragile_eps_fm (8) + adaptive, nn_stats (4 + 4) +
     # max_halves, tree_capacity (8 + 8) + tree_v / tree_a / tree_parent / tree_g (4 x 2 x 8)
-    # + stop_poll, stop_ctx (8 + 8)
+    # + stop_poll, stop_ctx (8 + 8) + the warm start: init_n, init_v, init_a,
+    # init_parent (4 x 2 x 8), first_half, extend_base (8 + 8)
     assert ctypes.sizeof(planner.PlanParams) == (4 * 3 + 4 + 8 * 6 + 8 * 16 + 8 + 8 + 8 + 8 + 8 +
-                                                 32 + 8 + 8 + 8 + 8 + 64 + 16)
+                                                 32 + 8 + 8 + 8 + 8 + 64 + 16 + 64 + 16)
     assert ctypes.sizeof(planner.PlanResult) == 304
     from global_body_planner_amd import engine
     assert ctypes.sizeof(engine.PlanStatus) == 168   # gbp_plan_status (static_assert in gbp_plan.hip)

@@ -320,3 +320,27 @@ def test_config5_rrt_star_fractal4096(gpu):
     assert out["solutions"] >= 1 and out["rewires"] > 0
     print(f"config 5 RRT*: first solution {out['time_to_first']:.3f} s, cost {out['path_cost']:.3f}, "
           f"{out['rewires']} rewires, {out['vertices_a'] + out['vertices_b']} vertices")
+
+
+@pytest.mark.parametrize("n_nearest", [1, 8, 64])
+def test_knn_cost_add_yaw(gpu, n_nearest):
+    """neighborhoodN with cost_add_yaw set (planner_class.cpp:157-158): the
+    yaw-weighted key poseDistance * lw + stateYawDistance * yw scanned on the
+    device (k_knn<true>, gbp_knn_yaw_batch_host: yaws with glibc on the host)
+    against the oracle, indices and keys bit for bit; ties, NaN, a tree
+    smaller than N, two weightings (params.yaml:17-20 defaults 1 / 1)."""
+    import global_body_planner_amd as gbp
+    data, T, O = fractal_pair()
+    verts, _ = O.sample_states(20000, 81, 1, 0, L.STANCE, 256, nthreads=16)
+    q, _ = O.sample_states(600, 82, 2, 0, L.STANCE, 256, nthreads=16)
+    verts[1000:1200] = verts[5000:5200]        # exact duplicates: ties
+    verts[::997, 4] = np.nan                   # NaN keys order last
+    verts[7, 3:5] = 0.0                        # atan2(0, 0)
+    q = np.concatenate([q, verts[[5000, 7]], np.full((1, 8), np.nan)])
+    for lw, yw in ((1.0, 1.0), (0.7, 3.0)):
+        for nv in (verts.shape[0], 40, 1):
+            idx, dist = gbp.knn_yaw(q, verts[:nv], n_nearest, lw, yw)
+            ri, rd = oracle.knn_yaw_batch(q, verts[:nv], n_nearest, lw, yw, nthreads=16)
+            assert np.array_equal(idx, ri), (nv, n_nearest, lw)
+            assert np.all(same_f64(dist, rd)), (nv, n_nearest, lw)
+    print(f"yaw-weighted k-nearest N={n_nearest}: {q.shape[0]} queries x {verts.shape[0]} bit-exact")

@@ -29,6 +29,9 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("libs", nargs="+")
     p.add_argument("--terrain", default="synth-rough-1024")
+    p.add_argument("--coarse", type=int, default=0,
+                   help="subsample the terrain to every k-th grid line (same extent, "
+                        "k-times coarser cells): a map small enough for the LDS-terrain variant")
     p.add_argument("--batch", type=int, default=262144)
     p.add_argument("--seed", type=int, default=W.CONFIG_SEEDS[3])
     p.add_argument("--waves", default="3")
@@ -38,6 +41,15 @@ def main():
     p.add_argument("--opts", default="", help="'name:OPT=v,OPT=v;name2:...' option variants")
     a = p.parse_args()
     data = td.by_name(a.terrain)
+    if a.coarse > 1:
+        k = a.coarse
+        h = float(data.x[1] - data.x[0]) * k
+        sub = lambda g: None if g is None else np.ascontiguousarray(g[::k, ::k])  # noqa: E731
+        nx, ny = data.z[::k, ::k].shape
+        data = td.TerrainData(np.arange(nx, dtype=np.float64) * h, np.arange(ny, dtype=np.float64) * h,
+                              sub(data.z), sub(data.dx), sub(data.dy), sub(data.dz),
+                              name=f"{data.name}/coarse{k}")
+        print(f"terrain {data.name}: {nx} x {ny}, spacing {h}", flush=True)
     base = gbp.Terrain.from_data(data, device=0)
     s, act, d, _, _ = W.make_attempts(base, a.batch, a.seed)
     Ts = [(os.path.basename(path), gbp.Terrain.from_data(data, device=0, lib=L.load(path)))
