@@ -50,7 +50,7 @@ EXPORTS = [
     "gbp_tree_create", "gbp_tree_destroy", "gbp_tree_init", "gbp_tree_reserve", "gbp_tree_capacity",
     "gbp_tree_size", "gbp_tree_read", "gbp_tree_append_host", "gbp_tree_device_ptrs",
     "gbp_plan_ws_create", "gbp_plan_ws_destroy", "gbp_plan_reset", "gbp_plan_half_dev",
-    "gbp_plan_halves_dev",
+    "gbp_plan_halves_dev", "gbp_plan_star_config",
     "gbp_plan_status_read", "gbp_plan_resolve_host", "gbp_extend_tree_dev",
     "gbp_extend_tree_finish_dev", "gbp_extend_tree_host", "gbp_tree_nearest_dev",
 ]
@@ -150,6 +150,7 @@ def load(path=None):
         "gbp_plan_halves_dev": (I, [P, P, P, P, ctypes.c_int32, ctypes.c_int32, I64, U64, U64, U64,
                                     I, I, P]),
         "gbp_plan_status_read": (I, [P, P, P]),
+        "gbp_plan_star_config": (I, [P, I, ctypes.c_double, I64, I64]),
         "gbp_plan_resolve_host": (I, [P, P, P, P, I, I64, I, P, P, P]),
         "gbp_extend_tree_dev": (I, [P, P, P, I64, P, P, I, I, U64, I64, P, P, P]),
         "gbp_extend_tree_finish_dev": (I, [P, P, P, I64, I, P, P, P]),

@@ -59,7 +59,7 @@
 #include "gbp_lane.h"
 
 using namespace gbp;
-static_assert(sizeof(gbp_plan_status) == 168, "engine.PlanStatus mirrors this layout");
+static_assert(sizeof(gbp_plan_status) == 216, "engine.PlanStatus mirrors this layout");
 
 // ============================================================================
 // handles
@@ -73,6 +73,12 @@ struct gbp_tree {
   double *a = nullptr;        // [cap][10] the action that reached each vertex
   double *g = nullptr;        // [cap] cost to come: g[parent] + poseDistance
   int32_t *parent = nullptr;  // [cap], -1 at the root
+  // successor lists (graph_class.cpp:28-58 successors_), first child / next
+  // sibling: the RRT*-Connect rewiring updates g over a rewired vertex's
+  // subtree (graph_class.cpp:131-138); kept by every append (child order is
+  // immaterial: a child's g depends on its parent's alone)
+  int32_t *child = nullptr, *sibling = nullptr;  // [cap], -1 = none
+  int32_t *bfs = nullptr;     // [2 cap] scratch: the subtree update's two level queues
   int32_t *count = nullptr;   // [1] number of vertices (device resident)
 };
 
@@ -122,6 +128,22 @@ struct gbp_plan_ws {
   double *nn_d = nullptr;
   int32_t *nn_i = nullptr;
   void *block = nullptr;       // the one allocation all of the above live in
+  // RRT*-Connect (gbp_plan_star_config; star = 0: RRT-Connect): stages 6-7
+  int star = 0;
+  double star_delta = 3.0;     // rrt_star_connect.h:59
+  int64_t star_max_pairs = 0, star_max_shared = 0;
+  int32_t *scnt = nullptr;     // [bmax] neighbours per new vertex
+  int32_t *soff = nullptr;     // [bmax + 1] their offsets
+  int32_t *snb = nullptr;      // [max_pairs] the neighbour of each pair
+  int32_t *sown = nullptr;     // [max_pairs] its new vertex (k)
+  int32_t *srowof = nullptr;   // [2 max_pairs] connect check -> pair-check row (-1: none)
+  int32_t *sritem = nullptr;   // [2 max_pairs] row -> connect check
+  double *srs = nullptr;       // [2 max_pairs][8] rows: the pair checks' states
+  double *sra = nullptr;       // [2 max_pairs][10] and actions
+  uint32_t *srf = nullptr;     // [2 max_pairs] their flags
+  int32_t *kvtx = nullptr;     // [bmax] O's vertex of each connection (-1: none)
+  int32_t *sshared = nullptr;  // [max_shared][2] the REACHED connections (a, b)
+  void *star_block = nullptr;
 };
 
 namespace {
@@ -1048,7 +1070,8 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
                                                int32_t *__restrict__ tp, int32_t *__restrict__ tcount,
                                                int32_t *__restrict__ vtx, unsigned long long *tiles,
                                                uint32_t epoch, int32_t half, int64_t cap,
-                                               uint64_t seq, int32_t commit_half) {
+                                               uint64_t seq, int32_t commit_half, int32_t *tch,
+                                               int32_t *tsib, int star) {
   if (gated(st, seq)) return;
   __shared__ int32_t s_base;
   if (threadIdx.x == 0) s_base = *tcount;  // read before this block publishes its count
@@ -1077,8 +1100,12 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
     copy10(ta + 10 * (int64_t)idx, an + 10 * i);
     tp[idx] = p;
     tg[idx] = tg[p] + pose_distance(pv, s);  // graph_class.cpp:36-42 addEdge
+    tch[idx] = -1;
+    // the successor list: RRT*'s extends are joined by the insertion replay
+    // (k_star_replay: choose-parent), everything else here
+    tsib[idx] = (mode == 0 && star) ? -1 : atomicExch(&tch[p], idx);
     if (vtx) vtx[i] = idx;
-    if (mode == 1 && r == GBP_REACHED) {
+    if (mode == 1 && r == GBP_REACHED && !star) {  // RRT*: every REACHED one is kept (k_star_shared)
       atomicMin((unsigned long long *)&st->meet,
                 ((unsigned long long)i << 32) | (unsigned long long)(uint32_t)idx);
       st->meet_half = half;
@@ -1283,6 +1310,430 @@ __global__ __launch_bounds__(TB) void k_connect(TerrainView<ZT> T, gbp_plan_stat
   }
 }
 
+// ============================================================================
+// RRT*-Connect insertion (rrt_star_connect.cpp:12-67), stages 6 and 7
+// ============================================================================
+// After stage 3 has appended the half's new vertices base + k (parent = their
+// nearest vertex, not yet joined), every one is inserted in order as the
+// reference's extend does: its neighbourhood is the vertices before it within
+// delta (neighborhoodDist, planner_class.cpp:173-182, ascending index); the
+// parent is the neighbour that REACHES it cheapest (choose-parent, :31-49),
+// then every neighbour it REACHES more cheaply is rewired under it with the g
+// of its subtree updated (:51-66, graph_class.cpp:131-138).  The connect
+// decisions depend on the states alone, so stage 6 runs all of them at once:
+// two per neighbour pair (choose-parent attemptConnect(s_near, s_new) and
+// rewire attemptConnect(s_new, s_near), the depth-0 REACHED decision), their
+// pair checks on the persistent kernel.  Stage 7 replays the insertions in
+// order (one workgroup: a vertex's choices read the g values its predecessors
+// left), each choice a block-wide reduction.
+
+constexpr int RB = 1024;  // threads of the single-workgroup star kernels
+
+__device__ __forceinline__ int block_sum_tb(int v, int *sh) {
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  for (int o = WAVE / 2; o > 0; o >>= 1) v += __shfl_down(v, o);
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  int t = 0;
+  for (int i = 0; i < (int)(blockDim.x / WAVE); i++) t += sh[i];
+  __syncthreads();
+  return t;
+}
+
+// stage 6a: neighbourhood sizes, one workgroup per new vertex
+__global__ __launch_bounds__(TB) void k_star_count(gbp_plan_status *st, const double *__restrict__ tv,
+                                                   double delta, int32_t *__restrict__ cnt,
+                                                   uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t n = st->n_added, base = st->added_base;
+  __shared__ int sh[TB / WAVE];
+  for (int64_t k = blockIdx.x; k < n; k += gridDim.x) {
+    const int64_t idx = base + k;
+    double q[8];
+    copy8(q, tv + 8 * idx);
+    int c = 0;
+    for (int64_t j = threadIdx.x; j < idx; j += TB) {
+      const double d = state_distance(q, tv + 8 * j);  // planner_class.cpp:178
+      c += (d <= delta && d > 0) ? 1 : 0;
+    }
+    c = block_sum_tb(c, sh);
+    if (threadIdx.x == 0) cnt[k] = c;
+  }
+}
+
+// stage 6b: the pairs' offsets (exclusive scan), one workgroup
+__global__ __launch_bounds__(RB) void k_star_scan(gbp_plan_status *st, const int32_t *__restrict__ cnt,
+                                                  int32_t *__restrict__ off, int64_t max_pairs,
+                                                  int32_t half, uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t n = st->n_added;
+  const int64_t ch = (n + RB - 1) / RB;
+  const int64_t lo = threadIdx.x * ch, hi = min<int64_t>(n, lo + ch);
+  int64_t sum = 0;
+  for (int64_t i = lo; i < hi; i++) sum += cnt[i];
+  __shared__ int64_t part[RB];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t run = 0;
+    for (int i = 0; i < RB; i++) {
+      const int64_t v = part[i];
+      part[i] = run;
+      run += v;
+    }
+    off[n] = (int32_t)min<int64_t>(run, 0x7FFFFFFF);
+    st->star_pairs = (int32_t)min<int64_t>(run, 0x7FFFFFFF);
+    st->star_rows = 0;
+    st->stat_star_connects += 2 * run;  // a choose-parent and a rewire connect per pair
+    if (run > max_pairs) {
+      atomicOr(&st->error, 4u);
+      raise_gate(st, seq);
+    }
+  }
+  __syncthreads();
+  int64_t run = part[threadIdx.x];
+  for (int64_t i = lo; i < hi; i++) {
+    off[i] = (int32_t)min<int64_t>(run, 0x7FFFFFFF);
+    run += cnt[i];
+  }
+}
+
+// stage 6c: the neighbour lists in ascending index (a workgroup per new vertex)
+__global__ __launch_bounds__(TB) void k_star_fill(gbp_plan_status *st, const double *__restrict__ tv,
+                                                  double delta, const int32_t *__restrict__ off,
+                                                  int32_t *__restrict__ nb, int32_t *__restrict__ own,
+                                                  uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t n = st->n_added, base = st->added_base;
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  __shared__ int wc[TB / WAVE];
+  for (int64_t k = blockIdx.x; k < n; k += gridDim.x) {
+    const int64_t idx = base + k;
+    double q[8];
+    copy8(q, tv + 8 * idx);
+    int64_t run = off[k];
+    for (int64_t j0 = 0; j0 < idx; j0 += TB) {
+      const int64_t j = j0 + threadIdx.x;
+      bool hit = false;
+      if (j < idx) {
+        const double d = state_distance(q, tv + 8 * j);
+        hit = d <= delta && d > 0;
+      }
+      const unsigned long long m = __ballot(hit);
+      if (lane == 0) wc[w] = __popcll(m);
+      __syncthreads();
+      int before = 0, total = 0;
+      for (int i = 0; i < TB / WAVE; i++) {
+        if (i < w) before += wc[i];
+        total += wc[i];
+      }
+      if (hit) {
+        const int64_t p = run + before + __popcll(m & ((1ull << lane) - 1ull));
+        nb[p] = (int32_t)j;
+        own[p] = (int32_t)k;
+      }
+      run += total;
+      __syncthreads();
+    }
+  }
+}
+
+// stage 6d: the connect checks' actions (rrt_connect.cpp:20-70 at depth 0,
+// item 2p: choose-parent attemptConnect(s_near, s_new, poseDistance(s_new,
+// s_near) / V_NOM), 2p + 1: rewire attemptConnect(s_new, s_near, ...)); the
+// ones with a valid action become pair-check rows (rowof; the rest are not
+// REACHED: t_s <= KINEMATICS_RES or an invalid action, :23-24, :66)
+__global__ __launch_bounds__(TB) void k_star_prep(gbp_plan_status *st, const double *__restrict__ tv,
+                                                  int dir, const int32_t *__restrict__ nb,
+                                                  const int32_t *__restrict__ own,
+                                                  int32_t *__restrict__ rowof,
+                                                  int32_t *__restrict__ ritem, double *__restrict__ rs,
+                                                  double *__restrict__ ra, uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t m = 2 * (int64_t)st->star_pairs, base = st->added_base;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // whole waves iterate together (the row slots are taken one atomic per wave)
+  for (int64_t c0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~(WAVE - 1)); c0 < m;
+       c0 += stride) {
+    const int64_t c = c0 + lane;
+    bool row = false;
+    double a[10], sp[8];
+    if (c < m) {
+      const int64_t pr = c >> 1;
+      const int64_t idx = base + own[pr], j = nb[pr];
+      double sn[8], sj[8];
+      copy8(sn, tv + 8 * idx);
+      copy8(sj, tv + 8 * j);
+      const bool rewire = c & 1;
+      const double *se = rewire ? sn : sj, *sq = rewire ? sj : sn;  // (s_existing, s)
+      const double t_s = (rewire ? pose_distance(sj, sn) : pose_distance(sn, sj)) / V_NOM;
+      if (t_s > KINEMATICS_RES) {
+        const double *s_start = dir == GBP_FORWARD ? se : sq, *s_goal = dir == GBP_FORWARD ? sq : se;
+        connect_action(s_start, s_goal, t_s, a);
+        row = is_valid_action(a);
+        copy8(sp, dir == GBP_FORWARD ? s_start : s_goal);
+      }
+    }
+    const unsigned long long bm = __ballot(row);
+    int32_t first = 0;
+    if (lane == 0 && bm) first = atomicAdd(&st->star_rows, __popcll(bm));
+    first = __shfl(first, 0);
+    if (c < m) {
+      if (row) {
+        const int32_t pos = first + __popcll(bm & ((1ull << lane) - 1ull));
+        copy8(rs + 8 * (int64_t)pos, sp);
+        copy10(ra + 10 * (int64_t)pos, a);
+        ritem[pos] = (int32_t)c;
+        rowof[c] = pos;
+      } else {
+        rowof[c] = -1;
+      }
+    }
+  }
+}
+
+// stage 6f: after the pair checks: a FRAGILE one halts the sequence (the
+// host re-decides it with glibc and resumes at stage 7)
+__global__ __launch_bounds__(TB) void k_star_gate(gbp_plan_status *st, const uint32_t *__restrict__ rf,
+                                                  int32_t half, uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t n = st->star_rows;
+  bool frag = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    frag = frag || (rf[i] & GBP_F_FRAGILE);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && n)
+    atomicAdd((unsigned long long *)&st->stat_attempts, (unsigned long long)n);
+  if (__ballot(frag) && (threadIdx.x & (WAVE - 1)) == 0) {
+    atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_STAR);
+    st->halt_half = half;
+    raise_gate(st, seq);
+  }
+}
+
+// block-wide (min key, min index) over the RB threads; NaN keys never win
+__device__ void block_argmin(double &key, int64_t &at, double *kd, int64_t *ki) {
+  kd[threadIdx.x] = key;
+  ki[threadIdx.x] = at;
+  __syncthreads();
+  for (int o = RB / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      const double k2 = kd[threadIdx.x + o];
+      const int64_t i2 = ki[threadIdx.x + o];
+      const double k1 = kd[threadIdx.x];
+      const int64_t i1 = ki[threadIdx.x];
+      if (i2 >= 0 && (i1 < 0 || k2 < k1 || (k2 == k1 && i2 < i1))) {
+        kd[threadIdx.x] = k2;
+        ki[threadIdx.x] = i2;
+      }
+    }
+    __syncthreads();
+  }
+  key = kd[0];
+  at = ki[0];
+  __syncthreads();
+}
+
+// g over the subtree below vertex r (graph_class.cpp:131-138: every successor's
+// g = its parent's + poseDistance), level by level through the two queues
+__device__ void subtree_g(const double *__restrict__ tv, double *tg, const int32_t *tch,
+                          const int32_t *tsib, int32_t r, int32_t *q0, int32_t *q1) {
+  __shared__ int32_t s_n, s_next;
+  if (threadIdx.x == 0) {
+    q0[0] = r;
+    s_n = 1;
+    s_next = 0;
+  }
+  __syncthreads();
+  while (s_n > 0) {
+    const int32_t nq = s_n;
+    for (int32_t i = threadIdx.x; i < nq; i += RB) {
+      const int32_t p = q0[i];
+      const double gp = tg[p];
+      for (int32_t c = tch[p]; c >= 0; c = tsib[c]) {
+        tg[c] = gp + pose_distance(tv + 8 * (int64_t)p, tv + 8 * (int64_t)c);
+        q1[atomicAdd(&s_next, 1)] = c;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s_n = s_next;
+      s_next = 0;
+    }
+    int32_t *t = q0;
+    q0 = q1;
+    q1 = t;
+    __syncthreads();
+  }
+}
+
+// stage 7: the ordered replay of rrt_star_connect.cpp:18-66, one workgroup
+__global__ __launch_bounds__(RB) void k_star_replay(gbp_plan_status *st, const double *__restrict__ tv,
+                                                    double *ta, double *tg, int32_t *tp, int32_t *tch,
+                                                    int32_t *tsib, const int32_t *__restrict__ off,
+                                                    const int32_t *__restrict__ nb,
+                                                    const int32_t *__restrict__ rowof,
+                                                    const double *__restrict__ ra,
+                                                    const uint32_t *__restrict__ rf, int32_t *q0,
+                                                    int32_t *q1, uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t n = st->n_added, base = st->added_base;
+  __shared__ double kd[RB];
+  __shared__ int64_t ki[RB];
+  __shared__ int32_t s_min;
+  __shared__ int64_t s_row;
+  int64_t rewires = 0;
+  for (int64_t k = 0; k < n; k++) {
+    const int32_t idx = (int32_t)(base + k);
+    const double *s_new = tv + 8 * (int64_t)idx;
+    const int32_t nn = tp[idx];  // stage 3 wrote the nearest vertex here
+    const int64_t i0 = off[k], i1 = off[k + 1];
+    // choose-parent (:27-44): from the nearest vertex, the first neighbour whose
+    // REACHED connection is strictly cheaper than the best so far — the first
+    // index of the cheapest, when that beats the nearest vertex's
+    double key = INFINITY;
+    int64_t at = -1;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += RB) {
+      const int32_t r = rowof[2 * i];
+      if (r < 0 || !(rf[r] & GBP_F_VALID)) continue;
+      const int32_t j = nb[i];
+      const double gc = tg[j] + pose_distance(tv + 8 * (int64_t)j, s_new);  // :35
+      if (gc == gc && (at < 0 || gc < key)) {  // the first of this thread's minimum
+        key = gc;
+        at = i;
+      }
+    }
+    block_argmin(key, at, kd, ki);
+    if (threadIdx.x == 0) {
+      const double g0 = tg[nn] + pose_distance(s_new, tv + 8 * (int64_t)nn);  // :28
+      int32_t pmin = nn;
+      double gn = g0;
+      int64_t row = -1;
+      if (at >= 0 && key < g0) {
+        pmin = nb[at];
+        gn = key;
+        row = rowof[2 * at];
+      }
+      // addEdge(s_min, s_new) + updateGYValue + addAction (:47-49)
+      tp[idx] = pmin;
+      tsib[idx] = tch[pmin];
+      tch[pmin] = idx;
+      tg[idx] = gn;
+      if (row >= 0) copy10(ta + 10 * (int64_t)idx, ra + 10 * row);
+      s_min = pmin;
+    }
+    __syncthreads();
+    // rewire (:51-66): in neighbour order; a rewire's subtree update can change
+    // the g a later neighbour is tested with, so each round finds the first
+    // neighbour (from the cursor on) that rewires now
+    for (int64_t cur = i0; cur < i1;) {
+      key = 0;
+      at = -1;
+      const double gi = tg[idx];
+      for (int64_t i = cur + threadIdx.x; i < i1; i += RB) {
+        const int32_t j = nb[i];
+        if (j == s_min) continue;
+        const int32_t r = rowof[2 * i + 1];
+        if (r < 0 || !(rf[r] & GBP_F_VALID)) continue;
+        if (tg[j] > (gi + pose_distance(tv + 8 * (int64_t)j, s_new))) {
+          at = i;
+          break;  // a thread's candidates ascend: its first is its least
+        }
+      }
+      block_argmin(key, at, kd, ki);  // key 0 everywhere: the least index
+      if (at < 0) break;
+      if (threadIdx.x == 0) {
+        const int32_t j = nb[at];
+        const int32_t op = tp[j];
+        if (op >= 0) {  // removeEdge(parent, j) (graph_class.cpp:44-58)
+          int32_t *link = &tch[op];
+          while (*link >= 0 && *link != j) link = &tsib[*link];
+          if (*link == j) *link = tsib[j];
+        }
+        tp[j] = idx;  // addEdge(s_new, j)
+        tsib[j] = tch[idx];
+        tch[idx] = j;
+        tg[j] = gi + pose_distance(tv + 8 * (int64_t)j, s_new);  // updateGYValue (:60)
+        copy10(ta + 10 * (int64_t)j, ra + 10 * (int64_t)rowof[2 * at + 1]);
+        s_row = j;
+      }
+      __syncthreads();
+      rewires++;
+      // the rewired vertex's successors (recursion of updateGYValue)
+      const int32_t j = (int32_t)s_row;
+      if (tch[j] >= 0) subtree_g(tv, tg, tch, tsib, j, q0, q1);
+      __syncthreads();
+      cur = at + 1;
+    }
+  }
+  if (threadIdx.x == 0 && rewires) st->stat_rewires += rewires;
+}
+
+// stage 5 (RRT*): the half's REACHED connections appended to the shared list
+// in connection order (rrt_star_connect.cpp:136-175: shared_a / shared_b),
+// then after tree Tb's half the cheapest of all ranked with the current g
+// values (:181-193: strictly cheaper than the best so far; ties to the first)
+__global__ __launch_bounds__(RB) void k_star_shared(gbp_plan_status *st, const int32_t *__restrict__ kres,
+                                                    const int32_t *__restrict__ kvtx, int t_is_a,
+                                                    int32_t *shared, int64_t max_shared, int rank,
+                                                    const double *__restrict__ ga,
+                                                    const double *__restrict__ gb, uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t n = st->n_added, base = st->added_base;
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  __shared__ int wc[RB / WAVE];
+  __shared__ double kd[RB];
+  __shared__ int64_t ki[RB];
+  int64_t ns = st->n_shared;
+  for (int64_t i0 = 0; i0 < n; i0 += RB) {
+    const int64_t i = i0 + threadIdx.x;
+    const bool hit = i < n && kres[i] == GBP_REACHED && kvtx[i] >= 0;
+    const unsigned long long m = __ballot(hit);
+    if (lane == 0) wc[w] = __popcll(m);
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int q = 0; q < RB / WAVE; q++) {
+      if (q < w) before += wc[q];
+      total += wc[q];
+    }
+    if (hit) {
+      const int64_t p = ns + before + __popcll(m & ((1ull << lane) - 1ull));
+      const int32_t tv_ = (int32_t)(base + i), ov = kvtx[i];
+      if (p < max_shared) {
+        shared[2 * p] = t_is_a ? tv_ : ov;
+        shared[2 * p + 1] = t_is_a ? ov : tv_;
+      }
+    }
+    ns += total;
+    __syncthreads();
+  }
+  if (ns > max_shared) {
+    if (threadIdx.x == 0) {
+      atomicOr(&st->error, 4u);
+      raise_gate(st, seq);
+    }
+    return;
+  }
+  if (threadIdx.x == 0) st->n_shared = (int32_t)ns;
+  if (!rank) return;
+  double key = INFINITY;
+  int64_t at = -1;
+  for (int64_t p = threadIdx.x; p < ns; p += RB) {
+    const double c = ga[shared[2 * p]] + gb[shared[2 * p + 1]];
+    if (c == c && (at < 0 || c < key)) {
+      key = c;
+      at = p;
+    }
+  }
+  block_argmin(key, at, kd, ki);
+  if (threadIdx.x == 0 && at >= 0 && key < st->best_cost) {
+    st->best_cost = key;
+    st->best_a = shared[2 * at];
+    st->best_b = shared[2 * at + 1];
+  }
+}
+
 __global__ void k_tree_init(gbp_tree t, double r0, double r1, double r2, double r3, double r4,
                             double r5, double r6, double r7) {
   const double r[8] = {r0, r1, r2, r3, r4, r5, r6, r7};
@@ -1291,6 +1742,8 @@ __global__ void k_tree_init(gbp_tree t, double r0, double r1, double r2, double 
   for (int k = 0; k < 10; k++) t.a[k] = 0.0;
   t.g[0] = 0.0;
   t.parent[0] = -1;
+  t.child[0] = -1;
+  t.sibling[0] = -1;
   *t.count = 1;
 }
 
@@ -1305,6 +1758,12 @@ __global__ void k_tree_append(gbp_tree t, int64_t n, const double *__restrict__ 
     copy10(t.a + 10 * (int64_t)c, a + 10 * i);
     t.parent[c] = p[i];
     t.g[c] = p[i] >= 0 ? t.g[p[i]] + pose_distance(t.v + 8 * (int64_t)p[i], s + 8 * i) : 0.0;
+    t.child[c] = -1;
+    t.sibling[c] = -1;
+    if (p[i] >= 0) {
+      t.sibling[c] = t.child[p[i]];
+      t.child[p[i]] = c;
+    }
   }
   *t.count = c;
 }
@@ -1318,6 +1777,8 @@ __global__ void k_plan_reset(gbp_plan_status *st, int64_t ext_counter) {
   z.ext_half = -1;
   z.meet_half = -1;
   z.ext_counter = ext_counter;
+  z.best_a = z.best_b = -1;
+  z.best_cost = INFINITY;
   *st = z;
 }
 
@@ -1425,18 +1886,22 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   gbp_plan_status *st = w->st;
   w->nn_stats = t->opt_nn_stats;
   select_targets(w, half);
+  // stage order: 0 1 2 3 (RRT*: 6 7) 4 5 — the RRT* insertion runs between
+  // the extends' append and the connects
+  auto ord = [](int x) { return x == 6 ? 31 : x == 7 ? 32 : 10 * x; };
+  auto run = [&](int x) { return ord(first_stage) <= ord(x) && ord(x) <= ord(last_stage); };
   // predrawn: the previous half's search drew this half's targets and its
   // last launch committed them (commit_pre)
-  if (!predrawn && first_stage <= 0 && last_stage >= 1)  // a fresh half: draws + compaction, one launch
+  if (!predrawn && run(0) && run(1))  // a fresh half: draws + compaction, one launch
     hipLaunchKernelGGL(k_targets<ZT>, dim3((unsigned)((batch + TB - 1) / TB)), dim3(TB), 0, s, V,
                        st, batch, seed, target_stream, target_base, w->cand, w->cflag, w->targets,
                        w->tqh, w->tiles, next_epoch(w), half, ++w->seq, t->sampling, T->v, T->count,
                        O ? O->v : T->v, direction);
-  else if (first_stage == 1 && last_stage >= 1)  // resumed after a FRAGILE draw
+  else if (first_stage == 1 && run(1))  // resumed after a FRAGILE draw
     hipLaunchKernelGGL(k_compact_targets, dim3(tiles_for(batch)), dim3(CB), 0, s, st, batch,
                        w->cand, w->cflag, w->targets, w->tqh, w->tiles, next_epoch(w), half, 1,
                        ++w->seq);
-  if (first_stage <= 2 && last_stage >= 2) {
+  if (run(2)) {
     // the candidates' actions inside the search unless they are direction-biased
     // (then they depend on s_near: k_extend_prep after the search)
     NhPrep<ZT> prep{V, seed, w->ca, t->sampling, direction, 0, NhDraw{}};
@@ -1465,14 +1930,36 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
                        w->nn, T->v, w->ca, w->csn, w->cf, w->eres, w->echo, w->esn, w->ean, w->ef,
                        half, ++w->seq);
   }
-  if (first_stage <= 3 && last_stage >= 3)
+  if (run(3))
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 0, w->eres, w->nn,
                        w->esn, w->ean, T->v, T->vh, T->hm, T->a, T->g, T->parent, T->count, w->evtx,
                        w->tiles,
-                       next_epoch(w), half, T->cap, ++w->seq, -1);
+                       next_epoch(w), half, T->cap, ++w->seq, -1, T->child, T->sibling, w->star);
+  if (w->star && run(6)) {
+    // RRT* insertion, stage 6: neighbourhoods, connect checks, their pair checks
+    const unsigned gk = (unsigned)std::max<int64_t>(1, std::min<int64_t>(batch, cus * 8));
+    hipLaunchKernelGGL(k_star_count, dim3(gk), dim3(TB), 0, s, st, T->v, w->star_delta, w->scnt,
+                       ++w->seq);
+    hipLaunchKernelGGL(k_star_scan, dim3(1), dim3(RB), 0, s, st, w->scnt, w->soff,
+                       w->star_max_pairs, half, ++w->seq);
+    hipLaunchKernelGGL(k_star_fill, dim3(gk), dim3(TB), 0, s, st, T->v, w->star_delta, w->soff, w->snb,
+                       w->sown, ++w->seq);
+    const int64_t rmax = 2 * w->star_max_pairs;
+    hipLaunchKernelGGL(k_star_prep, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, T->v,
+                       direction, w->snb, w->sown, w->srowof, w->sritem, w->srs, w->sra, ++w->seq);
+    int rc = gbp_internal_validate_dev_n(t, rmax, &st->star_rows, w->srs, w->sra, nullptr, direction,
+                                         adaptive, nullptr, nullptr, nullptr, w->srf, nullptr, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_star_gate, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, w->srf,
+                       half, ++w->seq);
+  }
+  if (w->star && run(7))  // stage 7: the ordered replay
+    hipLaunchKernelGGL(k_star_replay, dim3(1), dim3(RB), 0, s, st, T->v, T->a, T->g, T->parent,
+                       T->child, T->sibling, w->soff, w->snb, w->srowof, w->sra, w->srf, T->bfs,
+                       T->bfs + T->cap, ++w->seq);
   if (!O) return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   const int cdir = direction == GBP_FORWARD ? GBP_REVERSE : GBP_FORWARD;
-  if (first_stage <= 4 && last_stage >= 4) {
+  if (run(4)) {
     // queries: T's new vertices, rows [added_base, added_base + n_added)
     int rc = nn_launch(w, &st->n_added, T->v, &st->added_base, O, w->nno, cus, s, T->vh);
     if (rc) return rc;
@@ -1489,11 +1976,18 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     }
 #undef GBP_KC
   }
-  if (first_stage <= 5 && last_stage >= 5)
+  if (run(5)) {
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 1, w->kres, w->nno,
-                       w->ksn, w->kan, O->v, O->vh, O->hm, O->a, O->g, O->parent, O->count, nullptr,
-                       w->tiles,
-                       next_epoch(w), half, O->cap, ++w->seq, next ? next->half : -1);
+                       w->ksn, w->kan, O->v, O->vh, O->hm, O->a, O->g, O->parent, O->count,
+                       w->star ? w->kvtx : nullptr, w->tiles, next_epoch(w), half, O->cap, ++w->seq,
+                       next ? next->half : -1, O->child, O->sibling, w->star);
+    if (w->star) {  // the REACHED connections kept; after Tb's half the best one ranked
+      const bool t_is_a = direction == GBP_FORWARD;
+      hipLaunchKernelGGL(k_star_shared, dim3(1), dim3(RB), 0, s, st, w->kres, w->kvtx, t_is_a ? 1 : 0,
+                         w->sshared, w->star_max_shared, (half & 1) ? 1 : 0, t_is_a ? T->g : O->g,
+                         t_is_a ? O->g : T->g, ++w->seq);
+    }
+  }
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
 
@@ -1526,15 +2020,16 @@ T *carve(char *&p, size_t count) {
 int tree_alloc(gbp_tree *t, int64_t cap) {
   double *v = nullptr, *a = nullptr, *g = nullptr;
   _Float16 *vh = nullptr;
-  int32_t *p = nullptr;
+  int32_t *p = nullptr, *ch = nullptr;
   if (hipMalloc(&v, 64 * cap) != hipSuccess) return GBP_E_ALLOC;
   if (hipMalloc(&a, 80 * cap) != hipSuccess || hipMalloc(&g, 8 * cap) != hipSuccess ||
-      hipMalloc(&p, 4 * cap) != hipSuccess ||
+      hipMalloc(&p, 4 * cap) != hipSuccess || hipMalloc(&ch, 16 * cap) != hipSuccess ||
       hipMalloc(&vh, 2 * NH_ROW * ((cap + 63) & ~(int64_t)63)) != hipSuccess) {
     (void)hipFree(v);
     if (a) (void)hipFree(a);
     if (g) (void)hipFree(g);
     if (p) (void)hipFree(p);
+    if (ch) (void)hipFree(ch);
     return GBP_E_ALLOC;
   }
   t->v = v;
@@ -1542,6 +2037,9 @@ int tree_alloc(gbp_tree *t, int64_t cap) {
   t->a = a;
   t->g = g;
   t->parent = p;
+  t->child = ch;        // [cap] first children, [cap] next siblings, [2 cap] queues
+  t->sibling = ch + cap;
+  t->bfs = ch + 2 * cap;
   t->cap = cap;
   return GBP_OK;
 }
@@ -1602,7 +2100,7 @@ int gbp_tree_destroy(gbp_tree *t) {
   if (!t) return GBP_E_BAD_HANDLE;
   Guard g(t->device);
   (void)hipDeviceSynchronize();
-  void *ptrs[] = {t->v, t->vh, t->hm, t->a, t->g, t->parent, t->count};
+  void *ptrs[] = {t->v, t->vh, t->hm, t->a, t->g, t->parent, t->child, t->count};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   delete t;
@@ -1627,12 +2125,15 @@ int gbp_tree_reserve(gbp_tree *t, int64_t capacity, gbp_stream stream) {
   HIPCHK_P(hipMemcpyAsync(t->a, old.a, 80 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->g, old.g, 8 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->parent, old.parent, 4 * old.cap, hipMemcpyDeviceToDevice, s));
+  HIPCHK_P(hipMemcpyAsync(t->child, old.child, 4 * old.cap, hipMemcpyDeviceToDevice, s));
+  HIPCHK_P(hipMemcpyAsync(t->sibling, old.sibling, 4 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipStreamSynchronize(s));
   (void)hipFree(old.v);
   (void)hipFree(old.vh);
   (void)hipFree(old.a);
   (void)hipFree(old.g);
   (void)hipFree(old.parent);
+  (void)hipFree(old.child);
   return GBP_OK;
 }
 
@@ -1792,7 +2293,54 @@ int gbp_plan_ws_destroy(gbp_plan_ws *w) {
   Guard g(w->device);
   (void)hipDeviceSynchronize();
   if (w->block) (void)hipFree(w->block);
+  if (w->star_block) (void)hipFree(w->star_block);
   delete w;
+  return GBP_OK;
+}
+
+int gbp_plan_star_config(gbp_plan_ws *w, int enable, double delta, int64_t max_pairs,
+                         int64_t max_shared) {
+  if (!w) return GBP_E_BAD_HANDLE;
+  if (!enable) {
+    w->star = 0;
+    return GBP_OK;
+  }
+  if (!(delta >= 0) || max_pairs < 1 || max_pairs > (1 << 28) || max_shared < 1 ||
+      max_shared > (1 << 28))
+    return GBP_E_INVALID_ARG;
+  Guard g(w->device);
+  if (w->star_block && (max_pairs > w->star_max_pairs || max_shared > w->star_max_shared)) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(w->star_block);
+    w->star_block = nullptr;
+  }
+  if (!w->star_block) {
+    const int64_t b = w->bmax, r = 2 * max_pairs;
+    const size_t bytes = 4 * b + 4 * (b + 1) + 8 * max_pairs + r * (4 + 4 + 64 + 80 + 4) + 4 * b +
+                         8 * max_shared + 16 * 256;
+    if (hipMalloc(&w->star_block, bytes) != hipSuccess) {
+      w->star_block = nullptr;
+      w->star = 0;
+      return GBP_E_ALLOC;
+    }
+    char *p = (char *)w->star_block;
+    w->scnt = carve<int32_t>(p, b);
+    w->soff = carve<int32_t>(p, b + 1);
+    w->snb = carve<int32_t>(p, max_pairs);
+    w->sown = carve<int32_t>(p, max_pairs);
+    w->srowof = carve<int32_t>(p, r);
+    w->sritem = carve<int32_t>(p, r);
+    w->srs = carve<double>(p, 8 * r);
+    w->sra = carve<double>(p, 10 * r);
+    w->srf = carve<uint32_t>(p, r);
+    w->kvtx = carve<int32_t>(p, b);
+    w->sshared = carve<int32_t>(p, 2 * max_shared);
+    if ((size_t)(p - (char *)w->star_block) > bytes) return GBP_E_HIP;
+    w->star_max_pairs = max_pairs;
+    w->star_max_shared = max_shared;
+  }
+  w->star = 1;
+  w->star_delta = delta;
   return GBP_OK;
 }
 
@@ -1818,7 +2366,7 @@ int gbp_plan_half_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, 
                       int64_t target_index_base, int adaptive, int first_stage,
                       gbp_stream stream) {
   if (!t || !w || !tree_ok(T) || !tree_ok(O)) return GBP_E_BAD_HANDLE;
-  if (batch < 1 || batch > w->bmax || first_stage < 0 || first_stage > 5 ||
+  if (batch < 1 || batch > w->bmax || first_stage < 0 || first_stage > (w->star ? 7 : 5) ||
       (direction != GBP_FORWARD && direction != GBP_REVERSE) || T == O)
     return GBP_E_INVALID_ARG;
   Guard g(t->device);
@@ -1835,8 +2383,8 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
                         uint64_t stream_a, uint64_t stream_b, int adaptive, int first_stage,
                         gbp_stream stream) {
   if (!t || !w || !tree_ok(Ta) || !tree_ok(Tb)) return GBP_E_BAD_HANDLE;
-  if (batch < 1 || batch > w->bmax || first_stage < 0 || first_stage > 5 || n_halves < 0 ||
-      first_half < 0 || Ta == Tb)
+  if (batch < 1 || batch > w->bmax || first_stage < 0 || first_stage > (w->star ? 7 : 5) ||
+      n_halves < 0 || first_half < 0 || Ta == Tb)
     return GBP_E_INVALID_ARG;
   Guard g(t->device);
   hipStream_t s = (hipStream_t)stream;
@@ -1846,7 +2394,8 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
   // k_targets: half h's last launch (k_append mode 1) commits them
   // (commit_pre).  Same draws, same ranks, same counters.
   const bool ahead = !t->sampling.state_flag && !t->sampling.action_flag &&
-                     t->storage == GBP_STORAGE_F32;  // (k_nn_mfma<float> only)
+                     t->storage == GBP_STORAGE_F32 &&  // (k_nn_mfma<float> only)
+                     !w->star;  // (RRT*: the append does not commit)
   bool predrawn = false;
   for (int32_t i = 0; i < n_halves; i++) {
     const int32_t h = first_half + i;
@@ -1858,7 +2407,7 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
     const int fs = i == 0 ? first_stage : 0;
     NhDraw nd{};
     const NhDraw *next = nullptr;
-    if (ahead && i + 1 < n_halves && fs <= 2) {
+    if (ahead && i + 1 < n_halves && (fs <= 2)) {
       const int32_t h1 = h + 1;
       const auto &set = w->tset[h1 & 1];
       nd.half = h1;
@@ -2087,6 +2636,25 @@ int gbp_plan_resolve_host(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree 
       k++;
     }
     *resume_stage = 5;
+  } else if (st.halt & GBP_PLAN_HALT_STAR) {
+    // the RRT* insertion's connect checks (their pair checks, rows of stage 6)
+    const int64_t n = st.star_rows;
+    std::vector<uint32_t> rf(n);
+    if (n && (rc = d2h(rf.data(), w->srf, n, s))) return rc;
+    HIPCHK_P(hipStreamSynchronize(s));
+    for (int64_t i = 0; i < n; i++) {
+      if (!(rf[i] & GBP_F_FRAGILE)) continue;
+      double sv[8], av[10], sn[8], tn = 0;
+      if ((rc = d2h(sv, w->srs + 8 * i, 8, s)) || (rc = d2h(av, w->sra + 10 * i, 10, s))) return rc;
+      HIPCHK_P(hipStreamSynchronize(s));
+      uint32_t f = 0;
+      const bool v = gbp_host::pair_check(t->host, sv, av, direction, adaptive, sn, &tn, &f, nullptr);
+      const uint32_t fr = (f & ~GBP_F_FRAGILE) | (v ? GBP_F_VALID : 0u) | GBP_F_RESOLVED;
+      if ((rc = h2d(w->srf + i, &fr, 1, s))) return rc;
+      HIPCHK_P(hipStreamSynchronize(s));
+      k++;
+    }
+    *resume_stage = 7;
   }
   if (*resume_stage >= 0) {
     st.halt = 0;

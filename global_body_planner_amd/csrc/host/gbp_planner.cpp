@@ -2168,6 +2168,151 @@ bool RRTStarConnectClass::buildRRTStarConnectBatched(FastTerrainMap &terrain, St
   return true;
 }
 
+bool RRTStarConnectClass::buildRRTStarConnectDevice(FastTerrainMap &terrain, State s_start,
+                                                    State s_goal, int batch, double max_time,
+                                                    std::vector<State> &state_sequence,
+                                                    std::vector<Action> &action_sequence,
+                                                    BatchStats *stats) {
+  const auto t_start = std::chrono::high_resolution_clock::now();
+  auto since = [&]() {
+    return std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t_start).count();
+  };
+  goal_found = false;
+  wall_to_first_ = -1;
+  rewires_ = 0;
+  cost_vector_.clear();
+  cost_vector_times_.clear();
+  BatchStats local;
+  BatchStats &st = stats ? *stats : local;
+  gbp_terrain *h = terrain.handle();
+  const int dev = terrain.device();
+  const int adaptive = state_action_pair_check_adaptive_step_size_flag_ ? 1 : 0;
+  // RRT*'s targets are plain randomState draws (extendBatch without O); the
+  // candidates keep the action sampling (rrt.cpp:34, :49)
+  gbp_sampling cfg = samplingConfig();
+  cfg.state_flag = 0;
+  chk(gbp_terrain_set_sampling(h, &cfg), "sampling");
+  DeviceTrees D;
+  chk(gbp_stream_create(dev, &D.stream), "stream");
+  chk(gbp_plan_ws_create(h, batch, &D.ws), "plan workspace");
+  // neighbour pairs of one half (2 connect checks each) and REACHED connections of the run
+  chk(gbp_plan_star_config(D.ws, 1, delta, std::max<int64_t>(1 << 18, 8 * (int64_t)batch), 1 << 22),
+      "star config");
+  int64_t cap = std::max<int64_t>(1 << 16, 4 * (int64_t)batch);
+  for (int k = 0; k < 2; k++) chk(gbp_tree_create(dev, cap, &D.tree[k]), "tree");
+  chk(gbp_tree_init(D.tree[0], s_start.data(), D.stream), "tree init");
+  chk(gbp_tree_init(D.tree[1], s_goal.data(), D.stream), "tree init");
+  chk(gbp_plan_reset(D.ws, extend_counter_, D.stream), "plan reset");
+  int64_t known[2] = {1, 1};
+  const uint64_t tstream[2] = {401, 402};  // buildRRTStarConnectBatched's streams
+  const int g_max = (int)std::max<int64_t>(2, std::min<int64_t>(64, (1 << 21) / batch)) & ~1;
+  int group = 2;
+  int32_t half = 0;
+  gbp_plan_status ps{};
+  while (since() < max_time && (st.max_halves <= 0 || half + 2 <= st.max_halves)) {
+    if (st.max_halves > 0) group = (int)std::min<int64_t>(group, (st.max_halves - half) & ~1LL);
+    for (int k = 0; k < 2; k++) {
+      int64_t c = 0;
+      chk(gbp_tree_capacity(D.tree[k], &c), "tree capacity");
+      if (known[k] + (int64_t)group * batch > c)
+        chk(gbp_tree_reserve(D.tree[k], std::max<int64_t>(2 * c, known[k] + (int64_t)group * batch),
+                             D.stream),
+            "tree reserve");
+    }
+    chk(gbp_plan_halves_dev(h, D.ws, D.tree[0], D.tree[1], half, group, batch, seed_, tstream[0],
+                            tstream[1], adaptive, 0, D.stream),
+        "plan halves");
+    chk(gbp_plan_status_read(D.ws, &ps, D.stream), "plan status");
+    st.status_reads++;
+    while (ps.halt) {  // FRAGILE: re-decide on the host, resume where the sequence stopped
+      for (int b = 0; b < 3; b++) st.halts[b] += (ps.halt >> b) & 1u;
+      const int32_t h0 = ps.halt_half;
+      const int k = h0 & 1;
+      int resume = -1;
+      int64_t nres = 0;
+      chk(gbp_plan_resolve_host(h, D.ws, D.tree[k], D.tree[k ^ 1], k == 0 ? FORWARD : REVERSE,
+                                batch, adaptive, &resume, &nres, D.stream),
+          "plan resolve");
+      if (resume < 0) throw EngineError(GBP_E_INVALID_ARG, "plan resolve: nothing halted");
+      chk(gbp_plan_halves_dev(h, D.ws, D.tree[0], D.tree[1], h0, half + group - h0, batch, seed_,
+                              tstream[0], tstream[1], adaptive, resume, D.stream),
+          "plan halves");
+      chk(gbp_plan_status_read(D.ws, &ps, D.stream), "plan status");
+      st.status_reads++;
+    }
+    if (ps.error & 1u) throw EngineError(GBP_E_HIP, "device planner loop: look-back spin exhausted");
+    if (ps.error & 4u) throw EngineError(GBP_E_SHAPE, "device RRT*: star workspace exhausted");
+    if (ps.error) throw EngineError(GBP_E_SHAPE, "device planner loop: a tree ran out of capacity");
+    for (int k = 0; k < 2; k++) chk(gbp_tree_size(D.tree[k], &known[k], D.stream), "tree size");
+    half += group;
+    if (ps.n_shared > 0 && !goal_found) {
+      goal_found = true;
+      elapsed_to_first = std::chrono::duration<double>(since());
+      wall_to_first_ = elapsed_to_first.count();
+    }
+    if (ps.best_a >= 0 && (cost_vector_.empty() || ps.best_cost < cost_vector_.back())) {
+      cost_vector_.push_back(ps.best_cost);  // the best so far, once per group
+      cost_vector_times_.push_back(since());
+    }
+    group = std::min(group * 2, g_max);
+  }
+  extend_counter_ = ps.ext_counter;
+  rewires_ = ps.stat_rewires;
+  st.halves += half;
+  st.iterations += half / 2;
+  st.targets += ps.stat_targets;
+  st.extends += ps.stat_targets;
+  st.attempts_checked += ps.stat_attempts;
+  st.connects += ps.stat_added + ps.stat_star_connects;
+  st.rewires += ps.stat_rewires;
+  st.solutions += ps.n_shared;
+  st.fragile_resolved += ps.stat_fragile_resolved;
+  st.depth_capped += ps.stat_depth_capped;
+  st.nn_rechecks += ps.stat_nn_rechecks;
+  st.nn_scans += ps.stat_nn_scans;
+  HostTree A, B;
+  read_tree(D.tree[0], D.stream, A);
+  read_tree(D.tree[1], D.stream, B);
+  extent(A, st.extent_a);
+  extent(B, st.extent_b);
+  st.vertices_a = (int64_t)A.v.size();
+  st.vertices_b = (int64_t)B.v.size();
+  num_vertices = (int)(A.v.size() + B.v.size());
+  if (st.dump) {
+    const HostTree *t[2] = {&A, &B};
+    for (int k = 0; k < 2; k++) {
+      st.dump->v[k] = t[k]->v;
+      st.dump->a[k] = t[k]->a;
+      st.dump->parent[k] = t[k]->parent;
+      st.dump->g[k] = t[k]->g;
+    }
+  }
+  best_cost_ = ps.best_a >= 0 ? ps.best_cost : INFINITY_COST;
+  st.meet_a = ps.best_a;
+  st.meet_b = ps.best_b;
+  if (!goal_found || ps.best_a < 0) return false;
+  // rrt_star_connect.cpp:70-89 on the device trees
+  std::vector<int> path_a = host_path(A, ps.best_a);
+  std::vector<int> path_b = host_path(B, ps.best_b);
+  std::reverse(path_b.begin(), path_b.end());
+  std::vector<Action> action_sequence_b;
+  for (size_t i = 0; i + 1 < path_b.size(); ++i) action_sequence_b.push_back(B.a[path_b[i]]);
+  const double yaw_b = path_yaw(B, host_path(B, ps.best_b));
+  path_b.erase(path_b.begin());
+  state_sequence.clear();
+  for (int i : path_a) state_sequence.push_back(A.v[i]);
+  for (int i : path_b) state_sequence.push_back(B.v[i]);
+  action_sequence.clear();
+  for (size_t i = 1; i < path_a.size(); ++i) action_sequence.push_back(A.a[path_a[i]]);
+  action_sequence.insert(action_sequence.end(), action_sequence_b.begin(), action_sequence_b.end());
+  path_length_ = A.g[ps.best_a] + B.g[ps.best_b];
+  path_yaw_ = path_yaw(A, path_a) + yaw_b;
+  path_cost_ = weightedCost(path_length_, path_yaw_);
+  path_duration_ = 0;
+  for (const Action &a : action_sequence) path_duration_ += a[6] + a[7];
+  return true;
+}
+
 }  // namespace gbp_amd
 
 // ============================================================================
@@ -2179,7 +2324,7 @@ static_assert(sizeof(gbp_plan_params) == 456, "gbp_plan_params layout");
 extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r,
                                     double *path_states, double *path_actions, int capacity) {
   using namespace gbp_amd;
-  if (!p || !r || p->batch < 1 || p->algorithm < 0 || p->algorithm > 4) return GBP_E_INVALID_ARG;
+  if (!p || !r || p->batch < 1 || p->algorithm < 0 || p->algorithm > 5) return GBP_E_INVALID_ARG;
   try {
     FastTerrainMap terrain(p->device);
     terrain.loadDataFlat(p->nx, p->ny, p->x, p->y, p->z, p->dx, p->dy, p->dz);
@@ -2221,6 +2366,9 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
         p->algorithm == 1
             ? planner.buildRRTStarConnectBatched(terrain, s0, s1, p->batch, p->max_time, states,
                                                  actions, &st)
+        : p->algorithm == 5
+            ? planner.buildRRTStarConnectDevice(terrain, s0, s1, p->batch, p->max_time, states,
+                                                actions, &st)
         : p->algorithm == 2
             ? planner.buildRRTConnectBatchedAnytime(terrain, s0, s1, p->batch, p->max_time,
                                                     p->max_time_opt, states, actions, &st)
@@ -2282,7 +2430,7 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
       double len = 0;
       for (size_t i = 1; i < states.size(); i++) len += planning_utils::poseDistance(states[i - 1], states[i]);
       r->path_length = len;
-      r->path_cost = p->algorithm == 1 ? planner.bestCost() : planner.pathCost();
+      r->path_cost = (p->algorithm == 1 || p->algorithm == 5) ? planner.bestCost() : planner.pathCost();
       double dur = 0;
       for (const Action &a : actions) dur += a[6] + a[7];
       r->path_duration = dur;

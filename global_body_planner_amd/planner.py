@@ -124,6 +124,8 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
       path as algorithm 0 for the same seed and batch);
     algorithm 4: as 2, each restart's search resident on the device (what
       buildRRTConnect does by default, RRTConnectClass::set_engine_batch);
+    algorithm 5: as 1, the search resident on the device (buildRRTStarConnectDevice:
+      same trees, counters and best connection as algorithm 1);
     algorithm 2: RRTConnectClass::buildRRTConnect's anytime restarts
       (rrt_connect.cpp:323-467) on batch-synchronous trees: restart on the
       growing horizon, post-process every solution, keep the cheapest, stop
@@ -223,9 +225,11 @@ def plan_rrt_connect_device(data, start, goal, **kw):
     return plan_rrt_connect(data, start, goal, algorithm=3, **kw)
 
 
-def plan_rrt_star_connect(data, start, goal, **kw):
-    """RRTStarConnectClass::buildRRTStarConnect, batch-synchronous (algorithm 1)."""
-    return plan_rrt_connect(data, start, goal, algorithm=1, **kw)
+def plan_rrt_star_connect(data, start, goal, device_loop=False, **kw):
+    """RRTStarConnectClass::buildRRTStarConnect, batch-synchronous (algorithm 1;
+    algorithm 5 with device_loop: the search resident on the device, the
+    insertions' choose-parent / rewire replayed in HBM)."""
+    return plan_rrt_connect(data, start, goal, algorithm=5 if device_loop else 1, **kw)
 
 
 def plan_rrt_connect_anytime(data, start, goal, max_time_opt=1.0, device_loop=False, **kw):

@@ -447,11 +447,14 @@ int gbp_tree_device_ptrs(gbp_tree *tree, double **states, int32_t **count);
 #define GBP_PLAN_HALT_TARGETS 1u
 #define GBP_PLAN_HALT_EXTEND  2u
 #define GBP_PLAN_HALT_CONNECT 4u
+#define GBP_PLAN_HALT_STAR    8u  /* RRT*: an insertion's connect check (resume stage 7) */
 typedef struct {
   uint32_t halt;          /* GBP_PLAN_HALT_* of the stage that stopped the sequence */
   uint32_t done;          /* a connection REACHED */
   uint32_t error;         /* must be 0: bit 0 a bounded device spin ran out,
-                             bit 1 an append found its tree full */
+                             bit 1 an append found its tree full, bit 2 (RRT*)
+                             the insertion's neighbour pairs or the REACHED
+                             connections exceeded the workspace */
   int32_t halt_half;      /* the half-iteration that halted */
   int32_t n_targets;      /* valid targets of the last executed half */
   int32_t n_validate;     /* candidates launched (6 n_targets, 0 when gated) */
@@ -483,6 +486,16 @@ typedef struct {
    * (half + 1) when one of those draws was FRAGILE (the half halts at its
    * start, stage 1, as if its own draws had) */
   int32_t pre_targets, pre_fragile;
+  /* RRT*-Connect (gbp_plan_star_config): the last half's neighbour pairs
+   * (new vertex, vertex before it within delta) and their connect checks
+   * launched; the REACHED connections so far (shared_a / shared_b of
+   * rrt_star_connect.cpp:136-175) and the cheapest of them ranked after every
+   * iteration (:181-193, ties to the earliest): best_a / best_b, best_cost
+   * (INFINITY: none); the connect checks of the insertions (2 per pair) and
+   * the rewires */
+  int32_t star_pairs, star_rows, n_shared, best_a, best_b, star_pad;
+  double best_cost;
+  int64_t stat_star_connects, stat_rewires;
 } gbp_plan_status;
 int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out);
 int gbp_plan_ws_destroy(gbp_plan_ws *ws);
@@ -504,6 +517,25 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *ws, gbp_tree *Ta, gbp_tree 
                         int32_t first_half, int32_t n_halves, int64_t batch, uint64_t seed,
                         uint64_t stream_a, uint64_t stream_b, int adaptive, int first_stage,
                         gbp_stream stream);
+/* RRT*-Connect (rrt_star_connect.cpp:12-67, the batched form of
+ * RRTStarConnectClass::buildRRTStarConnectBatched): with enable set, every
+ * half-iteration of gbp_plan_half_dev / gbp_plan_halves_dev inserts its new
+ * vertices as RRT*'s extend does, between stages 3 and 4:
+ *   stage 6  the neighbourhood of each new vertex among the vertices before it
+ *            (stateDistance <= delta, > 0: neighborhoodDist, planner_class.cpp:
+ *            173-182, ascending index), and the two depth-0 connect decisions
+ *            per neighbour (choose-parent attemptConnect(s_near, s_new), rewire
+ *            attemptConnect(s_new, s_near)), their pair checks batched
+ *   stage 7  the insertions replayed in order: choose-parent, addEdge, rewire
+ *            with the g of every rewired subtree updated (graph_class.cpp:131-138)
+ * and stage 5 keeps every REACHED connection (no early stop) and, after tree
+ * Tb's half, ranks the cheapest with the current g values (status best_*).
+ * Targets are never drawn ahead.  max_pairs bounds the neighbour pairs of one
+ * half, max_shared the REACHED connections of a run (status.error bit 2 when
+ * exceeded).  A FRAGILE insertion check halts with GBP_PLAN_HALT_STAR (resume
+ * at stage 7).  enable = 0 returns the workspace to RRT-Connect. */
+int gbp_plan_star_config(gbp_plan_ws *ws, int enable, double delta, int64_t max_pairs,
+                         int64_t max_shared);
 /* re-decides the halted stage's FRAGILE items on the host (T, O, direction,
  * batch of the halted half) and clears the halt; *resume_stage = the stage to
  * resume that half at (-1: nothing was halted) */

@@ -557,6 +557,15 @@ class RRTStarConnectClass : public RRTConnectClass {
   bool buildRRTStarConnectBatched(FastTerrainMap &terrain, State s_start, State s_goal, int batch,
                                   double max_time, std::vector<State> &state_sequence,
                                   std::vector<Action> &action_sequence, BatchStats *stats = nullptr);
+  // The same search resident on the device: gbp_plan_halves_dev with the RRT*
+  // insertion stages (gbp_plan_star_config: neighbourhoods, connect checks and
+  // the ordered choose-parent / rewire replay in HBM, no per-vertex host
+  // loop); same trees, counters and best connection as buildRRTStarConnectBatched
+  // for the same seed and batch.  Runs pairs of half-iterations until max_time
+  // (or stats->max_halves), reading the status once per group.
+  bool buildRRTStarConnectDevice(FastTerrainMap &terrain, State s_start, State s_goal, int batch,
+                                 double max_time, std::vector<State> &state_sequence,
+                                 std::vector<Action> &action_sequence, BatchStats *stats = nullptr);
   double bestCost() const { return best_cost_; }
   int64_t rewires() const { return rewires_; }
 
@@ -634,7 +643,8 @@ typedef struct {
                         // until max_time), 2 rrt-connect with the reference's anytime
                         // restarts (best post-processed path after max_time_opt),
                         // 3 rrt-connect with the search resident on the device
-                        // (same trees and path as 0), 4 = 2 on the device-resident search
+                        // (same trees and path as 0), 4 = 2 on the device-resident search,
+                        // 5 = 1 with the search resident on the device (same trees)
   double max_time_opt;  // algorithm 2: keep restarting until a solution exists and this
                         // many seconds have passed (buildRRTConnect's max_time_opt)
   gbp_sampling sampling;  // direction-biased sampling (RRTClass::set_*_direction_sampling,

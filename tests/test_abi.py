@@ -114,7 +114,7 @@ def test_planner_library_exports_and_fails_without_device():
                                                  32 + 8 + 8 + 8 + 8 + 64 + 16 + 64 + 16)
     assert ctypes.sizeof(planner.PlanResult) == 304
     from global_body_planner_amd import engine
-    assert ctypes.sizeof(engine.PlanStatus) == 168   # gbp_plan_status (static_assert in gbp_plan.hip)
+    assert ctypes.sizeof(engine.PlanStatus) == 216   # gbp_plan_status (static_assert in gbp_plan.hip)
     assert ctypes.sizeof(L.Sampling) == 32
     import torch
     if not torch.cuda.is_available():

@@ -136,19 +136,26 @@ def test_post_process_equals_oracle(gpu, algorithm, name, xy, batch, seed):
           f"path_cost_ {pcost:.4f}")
 
 
+@pytest.mark.parametrize("algorithm,fragile_eps", [(1, None), (5, None), (5, 1e-5)])
 @pytest.mark.parametrize("name,xy,batch,seed,halves", [
     ("synth-rough-256", (1.0, 2.55, 4.02, 2.55), 1024, 3, 300),
     ("slope-gridmap", (1.0, 0.0, 8.0, 0.0), 512, 5, 200),
 ])
-def test_rrt_star_equals_oracle(gpu, name, xy, batch, seed, halves):
-    """Batched RRT*-Connect (algorithm 1): choose-parent + rewire of every new
-    vertex in order (rrt_star_connect.cpp:18-66, neighbourhoods within delta
-    among the vertices before it), the recursive g updates of rewired
-    subtrees (graph_class.cpp:131-138), and the best connection ranked after
-    every iteration, against the oracle's RRT* loop."""
+def test_rrt_star_equals_oracle(gpu, name, xy, batch, seed, halves, algorithm, fragile_eps):
+    """Batched RRT*-Connect — algorithm 1 (host-driven insertion replay) and
+    algorithm 5 (the search resident on the device: neighbourhoods, the
+    insertions' connect checks and the ordered choose-parent / rewire replay
+    in HBM, gbp_plan_star_config): choose-parent + rewire of every new vertex
+    in order (rrt_star_connect.cpp:18-66, neighbourhoods within delta among
+    the vertices before it), the recursive g updates of rewired subtrees
+    (graph_class.cpp:131-138), and the best connection ranked after every
+    iteration, against the oracle's RRT* loop.  A wider FRAGILE margin forces
+    the device loop's halts (the insertion checks' included) and host
+    re-decisions: same trees."""
     data, O, start, goal = _setup(name, xy)
     dev = planner.plan_rrt_star_connect(data, start, goal, batch=batch, max_time=600.0, seed=seed,
-                                        max_halves=halves, trees=True)
+                                        max_halves=halves, trees=True,
+                                        device_loop=algorithm == 5, fragile_eps=fragile_eps)
     ref = O.plan(start, goal, batch=batch, seed=seed, max_halves=halves, star=True, stream_a=401,
                  stream_b=402)
     assert dev["halves"] == ref["halves"] == halves
@@ -160,5 +167,8 @@ def test_rrt_star_equals_oracle(gpu, name, xy, batch, seed, halves):
     if ref["found"]:
         assert (dev["meet_a"], dev["meet_b"]) == (ref["best_a"], ref["best_b"])
         assert dev["path_cost"] == ref["best_cost"]
-    print(f"{name} RRT* batch {batch}: {halves} halves, trees {len(ref['a']['v'])}+"
-          f"{len(ref['b']['v'])}, {ref['rewires']} rewires, {ref['solutions']} connections")
+    if fragile_eps is not None:
+        assert dev["fragile_resolved"] > 0
+    print(f"{name} RRT* batch {batch} alg {algorithm}: {halves} halves, trees {len(ref['a']['v'])}+"
+          f"{len(ref['b']['v'])}, {ref['rewires']} rewires, {ref['solutions']} connections, "
+          f"{dev['fragile_resolved']} re-decided, halts {dev['halts']}")
