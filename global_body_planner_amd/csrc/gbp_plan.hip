@@ -47,6 +47,7 @@
 #include <stdint.h>
 
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -1384,6 +1385,7 @@ __global__ __launch_bounds__(RB) void k_star_scan(gbp_plan_status *st, const int
     off[n] = (int32_t)min<int64_t>(run, 0x7FFFFFFF);
     st->star_pairs = (int32_t)min<int64_t>(run, 0x7FFFFFFF);
     st->star_rows = 0;
+    st->star_vrows = 0;
     st->stat_star_connects += 2 * run;  // a choose-parent and a rewire connect per pair
     if (run > max_pairs) {
       atomicOr(&st->error, 4u);
@@ -1449,7 +1451,13 @@ __global__ __launch_bounds__(TB) void k_star_prep(gbp_plan_status *st, const dou
                                                   int32_t *__restrict__ rowof,
                                                   int32_t *__restrict__ ritem, double *__restrict__ rs,
                                                   double *__restrict__ ra, uint64_t seq) {
-  if (gated(st, seq)) return;
+  // the pair-check launch after this one is the engine's, not gated: when
+  // this half is, it must find no rows (it would re-validate the halted
+  // half's rows in the next half's direction over their flags)
+  if (gated(st, seq)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->star_vrows = 0;
+    return;
+  }
   const int64_t m = 2 * (int64_t)st->star_pairs, base = st->added_base;
   const int lane = threadIdx.x & (WAVE - 1);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -1477,7 +1485,10 @@ __global__ __launch_bounds__(TB) void k_star_prep(gbp_plan_status *st, const dou
     }
     const unsigned long long bm = __ballot(row);
     int32_t first = 0;
-    if (lane == 0 && bm) first = atomicAdd(&st->star_rows, __popcll(bm));
+    if (lane == 0 && bm) {
+      first = atomicAdd(&st->star_rows, __popcll(bm));
+      atomicAdd(&st->star_vrows, __popcll(bm));
+    }
     first = __shfl(first, 0);
     if (c < m) {
       if (row) {
@@ -1537,15 +1548,19 @@ __device__ void block_argmin(double &key, int64_t &at, double *kd, int64_t *ki) 
 
 // g over the subtree below vertex r (graph_class.cpp:131-138: every successor's
 // g = its parent's + poseDistance), level by level through the two queues
-__device__ void subtree_g(const double *__restrict__ tv, double *tg, const int32_t *tch,
-                          const int32_t *tsib, int32_t r, int32_t *q0, int32_t *q1) {
-  __shared__ int32_t s_n, s_next;
+// (bounded: a list that is not a tree — never built here — stops at nv vertices
+// and returns false instead of looping)
+__device__ bool subtree_g(const double *__restrict__ tv, double *tg, const int32_t *tch,
+                          const int32_t *tsib, int32_t r, int32_t *q0, int32_t *q1, int32_t nv) {
+  __shared__ int32_t s_n, s_next, s_total;
   if (threadIdx.x == 0) {
     q0[0] = r;
     s_n = 1;
     s_next = 0;
+    s_total = 1;
   }
   __syncthreads();
+  bool ok = true;
   while (s_n > 0) {
     const int32_t nq = s_n;
     for (int32_t i = threadIdx.x; i < nq; i += RB) {
@@ -1553,12 +1568,16 @@ __device__ void subtree_g(const double *__restrict__ tv, double *tg, const int32
       const double gp = tg[p];
       for (int32_t c = tch[p]; c >= 0; c = tsib[c]) {
         tg[c] = gp + pose_distance(tv + 8 * (int64_t)p, tv + 8 * (int64_t)c);
-        q1[atomicAdd(&s_next, 1)] = c;
+        const int32_t slot = atomicAdd(&s_next, 1);
+        if (slot >= nv) break;
+        q1[slot] = c;
       }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      s_n = s_next;
+      s_total += min(s_next, nv);
+      s_n = (s_next > nv || s_total > nv) ? 0 : s_next;
+      if (s_next > nv || s_total > nv) s_total = -1;
       s_next = 0;
     }
     int32_t *t = q0;
@@ -1566,6 +1585,9 @@ __device__ void subtree_g(const double *__restrict__ tv, double *tg, const int32
     q1 = t;
     __syncthreads();
   }
+  ok = s_total >= 0;
+  __syncthreads();
+  return ok;
 }
 
 // stage 7: the ordered replay of rrt_star_connect.cpp:18-66, one workgroup
@@ -1576,9 +1598,10 @@ __global__ __launch_bounds__(RB) void k_star_replay(gbp_plan_status *st, const d
                                                     const int32_t *__restrict__ rowof,
                                                     const double *__restrict__ ra,
                                                     const uint32_t *__restrict__ rf, int32_t *q0,
-                                                    int32_t *q1, uint64_t seq) {
+                                                    int32_t *q1, const int32_t *tcount, uint64_t seq) {
   if (gated(st, seq)) return;
   const int64_t n = st->n_added, base = st->added_base;
+  const int32_t nv = *tcount;
   __shared__ double kd[RB];
   __shared__ int64_t ki[RB];
   __shared__ int32_t s_min;
@@ -1648,7 +1671,7 @@ __global__ __launch_bounds__(RB) void k_star_replay(gbp_plan_status *st, const d
         const int32_t op = tp[j];
         if (op >= 0) {  // removeEdge(parent, j) (graph_class.cpp:44-58)
           int32_t *link = &tch[op];
-          while (*link >= 0 && *link != j) link = &tsib[*link];
+          for (int32_t step = 0; *link >= 0 && *link != j && step < nv; step++) link = &tsib[*link];
           if (*link == j) *link = tsib[j];
         }
         tp[j] = idx;  // addEdge(s_new, j)
@@ -1662,7 +1685,13 @@ __global__ __launch_bounds__(RB) void k_star_replay(gbp_plan_status *st, const d
       rewires++;
       // the rewired vertex's successors (recursion of updateGYValue)
       const int32_t j = (int32_t)s_row;
-      if (tch[j] >= 0) subtree_g(tv, tg, tch, tsib, j, q0, q1);
+      if (tch[j] >= 0 && !subtree_g(tv, tg, tch, tsib, j, q0, q1, nv)) {
+        if (threadIdx.x == 0) {
+          atomicOr(&st->error, 8u);  // a successor list that is not a tree
+          raise_gate(st, seq);
+        }
+        return;
+      }
       __syncthreads();
       cur = at + 1;
     }
@@ -1947,7 +1976,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     const int64_t rmax = 2 * w->star_max_pairs;
     hipLaunchKernelGGL(k_star_prep, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, T->v,
                        direction, w->snb, w->sown, w->srowof, w->sritem, w->srs, w->sra, ++w->seq);
-    int rc = gbp_internal_validate_dev_n(t, rmax, &st->star_rows, w->srs, w->sra, nullptr, direction,
+    int rc = gbp_internal_validate_dev_n(t, rmax, &st->star_vrows, w->srs, w->sra, nullptr, direction,
                                          adaptive, nullptr, nullptr, nullptr, w->srf, nullptr, s);
     if (rc) return rc;
     hipLaunchKernelGGL(k_star_gate, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, w->srf,
@@ -1956,7 +1985,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   if (w->star && run(7))  // stage 7: the ordered replay
     hipLaunchKernelGGL(k_star_replay, dim3(1), dim3(RB), 0, s, st, T->v, T->a, T->g, T->parent,
                        T->child, T->sibling, w->soff, w->snb, w->srowof, w->sra, w->srf, T->bfs,
-                       T->bfs + T->cap, ++w->seq);
+                       T->bfs + T->cap, T->count, ++w->seq);
   if (!O) return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   const int cdir = direction == GBP_FORWARD ? GBP_REVERSE : GBP_FORWARD;
   if (run(4)) {

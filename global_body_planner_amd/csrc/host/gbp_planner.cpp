@@ -1649,7 +1649,7 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
       chk(gbp_plan_status_read(D.ws, &ps, D.stream), "plan status");
       st.status_reads++;
       while (ps.halt) {  // FRAGILE: re-decide on the host, resume where the sequence stopped
-        for (int b = 0; b < 3; b++) st.halts[b] += (ps.halt >> b) & 1u;
+        for (int b = 0; b < 4; b++) st.halts[b] += (ps.halt >> b) & 1u;
         const int32_t h0 = ps.halt_half;
         const int k = h0 & 1;
         int resume = -1;
@@ -2225,7 +2225,7 @@ bool RRTStarConnectClass::buildRRTStarConnectDevice(FastTerrainMap &terrain, Sta
     chk(gbp_plan_status_read(D.ws, &ps, D.stream), "plan status");
     st.status_reads++;
     while (ps.halt) {  // FRAGILE: re-decide on the host, resume where the sequence stopped
-      for (int b = 0; b < 3; b++) st.halts[b] += (ps.halt >> b) & 1u;
+      for (int b = 0; b < 4; b++) st.halts[b] += (ps.halt >> b) & 1u;
       const int32_t h0 = ps.halt_half;
       const int k = h0 & 1;
       int resume = -1;
@@ -2406,7 +2406,7 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     r->fragile_resolved = st.fragile_resolved;
     r->depth_capped = st.depth_capped;
     r->status_reads = st.status_reads;
-    for (int k = 0; k < 3; k++) r->halts[k] = st.halts[k];
+    for (int k = 0; k < 4; k++) r->halts[k] = st.halts[k];
     r->nn_rechecks = st.nn_rechecks;
     r->nn_scans = st.nn_scans;
     r->reported_length = found ? planner.pathLength() : 0.0;

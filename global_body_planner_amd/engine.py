@@ -423,7 +423,7 @@ class PlanStatus(ctypes.Structure):
                 ("stat_targets_prev", ctypes.c_int64), ("pre_targets", ctypes.c_int32),
                 ("pre_fragile", ctypes.c_int32), ("star_pairs", ctypes.c_int32),
                 ("star_rows", ctypes.c_int32), ("n_shared", ctypes.c_int32),
-                ("best_a", ctypes.c_int32), ("best_b", ctypes.c_int32), ("star_pad", ctypes.c_int32),
+                ("best_a", ctypes.c_int32), ("best_b", ctypes.c_int32), ("star_vrows", ctypes.c_int32),
                 ("best_cost", ctypes.c_double), ("stat_star_connects", ctypes.c_int64),
                 ("stat_rewires", ctypes.c_int64)]
 

@@ -50,7 +50,7 @@ class PlanResult(ctypes.Structure):
                 ("rewires", ctypes.c_int64), ("solutions", ctypes.c_int64),
                 ("extent_a", _D * 4), ("extent_b", _D * 4),
                 ("fragile_resolved", ctypes.c_int64), ("depth_capped", ctypes.c_int64),
-                ("status_reads", ctypes.c_int64), ("halts", ctypes.c_int64 * 3),
+                ("status_reads", ctypes.c_int64), ("halts", ctypes.c_int64 * 4),
                 ("nn_rechecks", ctypes.c_int64), ("nn_scans", ctypes.c_int64),
                 ("reported_length", _D), ("reported_yaw", _D), ("meet_a", ctypes.c_int32),
                 ("meet_b", ctypes.c_int32), ("halves", ctypes.c_int64),

@@ -454,7 +454,8 @@ typedef struct {
   uint32_t error;         /* must be 0: bit 0 a bounded device spin ran out,
                              bit 1 an append found its tree full, bit 2 (RRT*)
                              the insertion's neighbour pairs or the REACHED
-                             connections exceeded the workspace */
+                             connections exceeded the workspace, bit 3 (RRT*)
+                             a successor list that is not a tree */
   int32_t halt_half;      /* the half-iteration that halted */
   int32_t n_targets;      /* valid targets of the last executed half */
   int32_t n_validate;     /* candidates launched (6 n_targets, 0 when gated) */
@@ -493,7 +494,9 @@ typedef struct {
    * iteration (:181-193, ties to the earliest): best_a / best_b, best_cost
    * (INFINITY: none); the connect checks of the insertions (2 per pair) and
    * the rewires */
-  int32_t star_pairs, star_rows, n_shared, best_a, best_b, star_pad;
+  int32_t star_pairs, star_rows, n_shared, best_a, best_b;
+  int32_t star_vrows;     /* rows the insertion's pair-check launch validates: star_rows,
+                             or 0 when its half is gated (the launch itself is not) */
   double best_cost;
   int64_t stat_star_connects, stat_rewires;
 } gbp_plan_status;

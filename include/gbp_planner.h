@@ -411,8 +411,8 @@ struct BatchStats {
   int64_t depth_capped = 0;   // connects stopped at GBP_CONNECT_MAX_DEPTH (TRAPPED)
   int64_t status_reads = 0;   // device loop: host synchronisations
   int64_t fragile_resolved = 0;  // attempts re-decided on the host (GBP_F_RESOLVED)
-  int64_t halts[3] = {0, 0, 0};  // device loop: FRAGILE halts in the targets / extend /
-                                 // connect stage (GBP_PLAN_HALT_*)
+  int64_t halts[4] = {0, 0, 0, 0};  // device loop: FRAGILE halts in the targets / extend /
+                                    // connect / RRT* insertion stage (GBP_PLAN_HALT_*)
   int64_t nn_rechecks = 0, nn_scans = 0;  // device loop with GBP_OPT_NN_STATS: the matrix-core
                                           // search's fp64 half-chunk re-checks / segment scans
   double extent_a[4] = {0, 0, 0, 0}, extent_b[4] = {0, 0, 0, 0};  // x_min x_max y_min y_max
@@ -685,8 +685,8 @@ typedef struct {
   int64_t fragile_resolved;    // decisions re-decided on the host with glibc (GBP_F_RESOLVED)
   int64_t depth_capped;        // connects stopped at GBP_CONNECT_MAX_DEPTH
   int64_t status_reads;        // algorithm 3: host synchronisations of the device loop
-  int64_t halts[3];            // algorithm 3/4: FRAGILE halts in the targets / extend /
-                               // connect stage of the device loop
+  int64_t halts[4];            // algorithm 3/4/5: FRAGILE halts in the targets / extend /
+                               // connect / RRT* insertion stage of the device loop
   int64_t nn_rechecks, nn_scans;  // algorithm 3 with nn_stats: the matrix-core search's
                                   // fp64 half-chunk re-checks and segment scans
   double reported_length, reported_yaw;  // the planner's path_length_ / path_yaw_ (what

@@ -73,7 +73,7 @@ def test_device_loop_forced_halts_equal_host_batched(gpu, batch, seed):
     for k in ("vertices_a", "vertices_b", "targets", "extends", "attempts_checked", "connects",
               "fragile_resolved", "depth_capped"):
         assert dev[k] == host[k], (k, dev[k], host[k])
-    assert all(h > 0 for h in dev["halts"]), dev["halts"]   # targets, extend, connect
+    assert all(h > 0 for h in dev["halts"][:3]), dev["halts"]   # targets, extend, connect
     print(f"batch {batch}: halts {dev['halts']}, {dev['fragile_resolved']} re-decided, "
           f"{dev['status_reads']} status reads")
 

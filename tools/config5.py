@@ -1,13 +1,17 @@
 """BASELINE config 5: RRT*-Connect on synth-fractal-4096 (one tree pair per GPU).
 
-  python tools/config5.py --max-time 20 --batch 256 [--out profiles/r01_config5.json]
+  python tools/config5.py --max-time 20 [--algorithm 5] [--batch 4096] [--out f.json]
   torchrun --nproc-per-node N tools/config5.py ...   (N independent restarts, best path
                                                        shared by one all_gather)
 
 Start (1.0, L/2) and goal 8 m further along +x (the first STANCE-valid points
 scanning outward / inward in 0.02 m steps; z = 0.375 + ground, v = (1,0,0)).
-Reports time to first solution, best tree cost over time, rewires, and the
-engine work rate (pair checks / s) of the anytime RRT*-Connect.
+Reports time to first solution, the best connection's cost, rewires, and the
+engine work rates (pair checks / s, extends / s) of the anytime RRT*-Connect.
+algorithm 5 (default): the search resident on the device (buildRRTStarConnectDevice:
+neighbourhoods, insertion connect checks and the ordered choose-parent / rewire
+replay in HBM); algorithm 1: the host-driven batched loop (round 1's figure).
+bench.py's config5 sub-record calls run_config5().
 """
 import argparse
 import json
@@ -37,31 +41,22 @@ def first_valid(T, x, y, step, n=400):
     return st[k]
 
 
-def main():
-    p = argparse.ArgumentParser()
-    p.add_argument("--terrain", default="synth-fractal-4096")
-    p.add_argument("--batch", type=int, default=256)
-    p.add_argument("--max-time", type=float, default=20.0)
-    p.add_argument("--seed", type=int, default=20251020)
-    p.add_argument("--span", type=float, default=8.0)
-    p.add_argument("--out", default=None)
-    a = p.parse_args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+def run_config5(terrain="synth-fractal-4096", batch=4096, max_time=20.0, seed=20251020, span=8.0,
+                algorithm=5, rank=0, world=1, device=0, data=None):
+    """One RRT*-Connect run per rank (seed + rank), best path all_gathered;
+    returns the record (rank 0's view) for every rank."""
+    dev = torch.device("cuda", device)
     t0 = time.perf_counter()
-    data = td.by_name(a.terrain)
+    if data is None:
+        data = td.by_name(terrain)
     t_gen = time.perf_counter() - t0
-    T = gbp.Terrain.from_data(data, device=local)
+    T = gbp.Terrain.from_data(data, device=device)
     L = data.x[-1]
     start = first_valid(T, 1.0, L / 2, 0.02)
-    goal = first_valid(T, 1.0 + a.span, L / 2, -0.02)
-    out = planner.plan_rrt_star_connect(data, start, goal, batch=a.batch, max_time=a.max_time,
-                                        seed=a.seed + rank, device=local)
+    goal = first_valid(T, 1.0 + span, L / 2, -0.02)
+    out = planner.plan_rrt_star_connect(data, start, goal, batch=batch, max_time=max_time,
+                                        seed=seed + rank, device=device,
+                                        device_loop=algorithm == 5)
     found = bool(out["found"])
     cost = out["path_cost"] if found else float("nan")
     who, best = sharding.gather_best_path(cost, out["path_length"], 0.0,
@@ -70,27 +65,54 @@ def main():
     ttf = torch.tensor([out["time_to_first"] if found else float("inf")], dtype=torch.float64,
                        device=dev)
     work = torch.tensor([float(out["attempts_checked"]), float(out["rewires"]),
-                         float(out["connects"]), float(out["extends"])], dtype=torch.float64,
-                        device=dev)
+                         float(out["connects"]), float(out["extends"]), float(out["total_time"])],
+                        dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(ttf, op=dist.ReduceOp.MIN)
+        t_max = work[4:].clone()
         dist.all_reduce(work, op=dist.ReduceOp.SUM)
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        work[4] = t_max[0]
+    b = sharding.unpack_path(best)
+    wall = float(work[4].item())
+    return {
+        "config": "5: RRT*-Connect, %s, %d GPU(s), %d draws per half, %.1f s anytime" % (
+            terrain, world, batch, max_time),
+        "planner": "buildRRTStarConnectDevice (search resident on the device)" if algorithm == 5
+                   else "buildRRTStarConnectBatched (host-driven insertion replay)",
+        "terrain_gen_s": round(t_gen, 2),
+        "start": start[:3].tolist(), "goal": goal[:3].tolist(),
+        "time_to_first_solution_s": float(ttf.item()),
+        "best_cost": b["cost"], "best_rank": who, "best_path_states": int(b["states"].shape[0]),
+        "pair_checks_per_s": round(float(work[0].item()) / wall, 1),
+        "extends_per_s": round(float(work[3].item()) / wall, 1),
+        "rewires": int(work[1].item()), "connect_checks": int(work[2].item()),
+        "extends": int(work[3].item()),
+        "rank0": {k: out[k] for k in ("iterations", "halves", "targets", "extends",
+                                      "attempts_checked", "connects", "vertices_a", "vertices_b",
+                                      "rewires", "solutions", "total_time", "time_to_first",
+                                      "fragile_resolved", "status_reads")},
+    }
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--terrain", default="synth-fractal-4096")
+    p.add_argument("--batch", type=int, default=4096)
+    p.add_argument("--max-time", type=float, default=20.0)
+    p.add_argument("--seed", type=int, default=20251020)
+    p.add_argument("--span", type=float, default=8.0)
+    p.add_argument("--algorithm", type=int, default=5, choices=(1, 5))
+    p.add_argument("--out", default=None)
+    a = p.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    res = run_config5(a.terrain, a.batch, a.max_time, a.seed, a.span, a.algorithm, rank, world, local)
     if rank == 0:
-        b = sharding.unpack_path(best)
-        res = {
-            "config": "5: RRT*-Connect, %s, %d GPU(s), batch %d, %.1f s anytime" % (
-                a.terrain, world, a.batch, a.max_time),
-            "terrain_gen_s": round(t_gen, 2),
-            "start": start[:3].tolist(), "goal": goal[:3].tolist(),
-            "time_to_first_solution_s": float(ttf.item()),
-            "best_cost": b["cost"], "best_rank": who, "best_path_states": int(b["states"].shape[0]),
-            "pair_checks_per_s": float(work[0].item()) / out["total_time"],
-            "rewires": int(work[1].item()), "connect_checks": int(work[2].item()),
-            "extends": int(work[3].item()),
-            "rank0": {k: out[k] for k in ("iterations", "targets", "extends", "attempts_checked",
-                                          "connects", "vertices_a", "vertices_b", "rewires",
-                                          "solutions", "total_time", "time_to_first")},
-        }
         line = json.dumps(res)
         print(line, flush=True)
         if a.out:
