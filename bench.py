@@ -86,6 +86,11 @@ def parse():
     p.add_argument("--plan-algorithm", type=int, default=3,
                    help="3: the search resident on the device (buildRRTConnectDevice), "
                         "0: the host-driven batched loop (buildRRTConnectBatched)")
+    p.add_argument("--config5-seconds", type=float, default=10.0,
+                   help="config 5 (RRT*-Connect, synth-fractal-4096, the device loop) run "
+                        "length per rank; 0 = skip")
+    p.add_argument("--config5-batch", type=int, default=4096,
+                   help="config 5: randomState draws per half-iteration")
     p.add_argument("--config2", type=int, default=1,
                    help="also measure config 2 (synth-rough-256, 65,536 attempts) (rank 0)")
     p.add_argument("--config2-waves", type=int, default=2,
@@ -479,6 +484,13 @@ def main():
         ttfs1 = time_to_first_solution(td.by_name("slope-gridmap"), "slope-gridmap", 3, 20.0,
                                        args, rank, world, dev)
 
+    config5 = None
+    if args.config5_seconds > 0:  # every rank runs one tree pair (config 4/5 style restarts)
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+        from config5 import run_config5
+        config5 = run_config5(batch=args.config5_batch, max_time=args.config5_seconds,
+                              rank=rank, world=world, device=local)
+
     if rank == 0:
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
         traffic = None
@@ -539,6 +551,7 @@ def main():
             "time_to_first_solution_before_wall": ttfs_near,
             "time_to_first_solution_config2": ttfs2,
             "time_to_first_solution_config1": ttfs1,
+            "config5": config5,
         }
         if args.lookup_micro:
             out["terrain_lookup"] = terrain_lookup_micro(T, data, dev)

@@ -2117,7 +2117,12 @@ int gbp_tree_create(int device, int64_t capacity, gbp_tree **out) {
     gbp_tree_destroy(t);
     return GBP_E_ALLOC;
   }
-  if (hipMemset(t->count, 0, 4) != hipSuccess || hipMemset(t->hm, 0, 64) != hipSuccess) {
+  // the zeroing runs on the null stream, and the caller's planner streams are
+  // non-blocking (gbp_stream_create): it must be complete before this returns,
+  // or it can land after gbp_tree_init's count = 1 on another stream (seen as
+  // a root overwritten by the first append under two processes per GPU)
+  if (hipMemset(t->count, 0, 4) != hipSuccess || hipMemset(t->hm, 0, 64) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
     gbp_tree_destroy(t);
     return GBP_E_HIP;
   }
