@@ -25,7 +25,6 @@ STORAGE_AUTO, STORAGE_F32, STORAGE_F64 = 0, 1, 2
 OPT_KERNEL, OPT_BLOCK, OPT_WAVES, OPT_LDS_COORDS, OPT_HELPERS = 1, 2, 4, 5, 8
 OPT_AFFINE_COORDS, OPT_COORD_MODE, OPT_XCD_MAP, OPT_FAST_RCP, OPT_FRAGILE_EPS = 9, 10, 13, 14, 15
 OPT_NN_STATS = 18
-OPT_NN_INDEX = 19
 PLAN_HALT_TARGETS, PLAN_HALT_EXTEND, PLAN_HALT_CONNECT = 1, 2, 4
 KERNEL_DIRECT, KERNEL_PERSISTENT = 0, 1
 
@@ -51,7 +50,7 @@ EXPORTS = [
     "gbp_tree_create", "gbp_tree_destroy", "gbp_tree_init", "gbp_tree_reserve", "gbp_tree_capacity",
     "gbp_tree_size", "gbp_tree_read", "gbp_tree_append_host", "gbp_tree_device_ptrs",
     "gbp_plan_ws_create", "gbp_plan_ws_destroy", "gbp_plan_reset", "gbp_plan_half_dev",
-    "gbp_plan_halves_dev", "gbp_plan_star_config", "gbp_tree_index_build", "gbp_tree_index_size",
+    "gbp_plan_halves_dev", "gbp_plan_star_config",
     "gbp_plan_status_read", "gbp_plan_resolve_host", "gbp_extend_tree_dev",
     "gbp_extend_tree_finish_dev", "gbp_extend_tree_host", "gbp_tree_nearest_dev",
 ]
@@ -152,8 +151,6 @@ def load(path=None):
                                     I, I, P]),
         "gbp_plan_status_read": (I, [P, P, P]),
         "gbp_plan_star_config": (I, [P, I, ctypes.c_double, I64, I64]),
-        "gbp_tree_index_build": (I, [P, P, P]),
-        "gbp_tree_index_size": (I, [P, P]),
         "gbp_plan_resolve_host": (I, [P, P, P, P, I, I64, I, P, P, P]),
         "gbp_extend_tree_dev": (I, [P, P, P, I64, P, P, I, I, U64, I64, P, P, P]),
         "gbp_extend_tree_finish_dev": (I, [P, P, P, I64, I, P, P, P]),

@@ -1281,10 +1281,6 @@ int gbp_terrain_set_option(gbp_terrain *t, int key, int64_t value) {
     case GBP_OPT_NN_STATS:
       t->opt_nn_stats = value ? 1 : 0;
       return GBP_OK;
-    case GBP_OPT_NN_INDEX:
-      if (value < 0) return GBP_E_INVALID_ARG;
-      t->opt_nn_index = value;
-      return GBP_OK;
     case GBP_OPT_FRAGILE_EPS:  // in 1e-15 units; never below the default margin
       if (value < 1000 || value > 1000000000000000LL) return GBP_E_INVALID_ARG;
       t->fragile_eps = (double)value * 1e-15;
@@ -1307,7 +1303,6 @@ int gbp_terrain_get_option(const gbp_terrain *t, int key, int64_t *value) {
     case GBP_OPT_XCD_MAP: *value = t->opt_xcd_map; return GBP_OK;
     case GBP_OPT_FAST_RCP: *value = t->opt_fast_rcp ? (t->rcp_seed != 0.0 ? 1 : 0) : 0; return GBP_OK;
     case GBP_OPT_NN_STATS: *value = t->opt_nn_stats; return GBP_OK;
-    case GBP_OPT_NN_INDEX: *value = t->opt_nn_index; return GBP_OK;
     case GBP_OPT_FRAGILE_EPS: *value = (int64_t)std::llround(t->fragile_eps * 1e15); return GBP_OK;
     case GBP_OPT_COORD_MODE:  // what the validate kernel of the current options uses
       *value = validate_coord_mode(t, t->opt_kernel == GBP_KERNEL_DIRECT);

@@ -41,7 +41,6 @@ struct gbp_terrain {
   double fragile_eps = gbp::FRAGILE_EPS;  // GBP_OPT_FRAGILE_EPS (>= the default)
   int64_t opt_xcd_map = 0;          // persistent kernel: slices numbered XCD-major
   int opt_nn_stats = 0;             // 1: the matrix-core NN search counts its fp64 re-checks
-  int64_t opt_nn_index = 1;         // GBP_OPT_NN_INDEX (read by the host planner loop)
   gbp_sampling sampling{};          // direction-biased sampling (gbp_terrain_set_sampling), off
   int affine = 0;                   // host-verified affine coordinates (both axes)
   int bx = 0, by = 0;

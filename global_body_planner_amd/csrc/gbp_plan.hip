@@ -81,17 +81,6 @@ struct gbp_tree {
   int32_t *child = nullptr, *sibling = nullptr;  // [cap], -1 = none
   int32_t *bfs = nullptr;     // [2 cap] scratch: the subtree update's two level queues
   int32_t *count = nullptr;   // [1] number of vertices (device resident)
-  // spatial index of the nearest-vertex search (gbp_tree_index_build): the
-  // first ix_n vertices (a multiple of NH_SU) as "positions" sorted by grid
-  // bin of (x, y) — their fp16 rows ixh, position -> vertex ixperm, the
-  // 8-D box of every NH_SU positions ixbox, the first position of every bin
-  // ixoff — and positions past ix_n the vertices themselves (the tail,
-  // appended since).  ix_n = 0: no index.
-  int64_t ix_n = 0, ix_cap = 0;
-  double ix_ext[4] = {0, 1, 0, 1};  // x0, x1, y0, y1 of the bins
-  _Float16 *ixh = nullptr;
-  int32_t *ixperm = nullptr, *ixoff = nullptr, *ixcnt = nullptr;
-  float *ixbox = nullptr;
 };
 
 struct gbp_plan_ws {
@@ -156,14 +145,6 @@ struct gbp_plan_ws {
   int32_t *kvtx = nullptr;     // [bmax] O's vertex of each connection (-1: none)
   int32_t *sshared = nullptr;  // [max_shared][2] the REACHED connections (a, b)
   void *star_block = nullptr;
-  // the targets sorted by grid bin for an indexed tree's search (k_qs_*)
-  int32_t *qperm = nullptr;    // [bmax] sorted position -> target
-  double *qs = nullptr;        // [bmax][8]
-  _Float16 *qhs = nullptr;     // [bmax][NH_ROW]
-  float *qub2 = nullptr;       // [bmax]
-  float *qtile = nullptr;      // [bmax / 32 + 1][NH_QT]
-  int32_t *qcnt = nullptr;     // [NH_BINS] + offsets [NH_BINS + 1] + cursors [NH_BINS]
-  void *qs_block = nullptr;
 };
 
 namespace {
@@ -449,76 +430,6 @@ struct NhTop {
   }
 };
 
-// ---- the spatial index (gbp_tree_index_build) --------------------------------
-// Vertices binned on a 64 x 64 grid over the map in Z order, sorted by bin;
-// a superunit = NH_SU consecutive sorted positions (4 units) with its 8-D box
-// (fp32, rounded outward).  A query tile (32 consecutive queries of a search
-// whose queries were sorted the same way, k_qs_*) has its box too and the
-// largest ub2 of its queries: the squared fp64 distance to SOME vertex (the
-// vertices around the query's bin), so each query's nearest vertex is no
-// farther.  A superunit whose box is farther than that from the tile's box
-// (lower bound > sqrt(ub2 max), margin 1e-5) holds no query's nearest vertex
-// nor one tying with it: the tile skips its units (exact, independent of the
-// fp16 scores' error bounds).  k_nn_hreduce maps positions to vertices and
-// skips such superunits in its segment scans against its own best so far.
-constexpr int NH_SU = 256;      // positions per superunit (8 chunks, 4 units)
-constexpr int NH_BINS = 4096;   // 64 x 64 grid, Z order
-constexpr int NH_QT = 17;       // floats per query tile: lo[8], hi[8], ub2 max
-
-struct NhExt {                  // the bins' grid: cell = (x - x0) * sx (64 per axis)
-  double x0, sx, y0, sy;
-};
-__device__ __forceinline__ int nh_bin(double x, double y, const NhExt &e) {
-  const double fx = (x - e.x0) * e.sx, fy = (y - e.y0) * e.sy;
-  const int cx = fx >= 0 ? (fx < 63.0 ? (int)fx : 63) : 0;  // NaN -> 0
-  const int cy = fy >= 0 ? (fy < 63.0 ? (int)fy : 63) : 0;
-  int b = 0;
-#pragma unroll
-  for (int k = 0; k < 6; k++) b |= (((cx >> k) & 1) << (2 * k)) | (((cy >> k) & 1) << (2 * k + 1));
-  return b;
-}
-__device__ __forceinline__ float nh_down(double x) {
-  const float f = (float)x;
-  return (double)f > x ? nextafterf(f, -INFINITY) : f;
-}
-__device__ __forceinline__ float nh_up(double x) {
-  const float f = (float)x;
-  return (double)f < x ? nextafterf(f, INFINITY) : f;
-}
-
-// the index as a search sees it; n = 0: positions are vertices (no index)
-struct NhIndex {
-  int32_t n;                 // sorted positions
-  const _Float16 *h;         // their fp16 rows
-  const int32_t *perm;       // position -> vertex
-  const float *box;          // [n / NH_SU][16] superunit boxes: lo[8], hi[8]
-  const float *qtile;        // [tiles][NH_QT] of the sorted queries; null: no skipping
-};
-__device__ __forceinline__ int64_t nh_vertex(const NhIndex &ix, int64_t pos) {
-  return pos < ix.n ? (int64_t)ix.perm[pos] : pos;
-}
-
-// which of the wave's NT query tiles skip superunit su (bit u): lanes
-// 8u + k (u < NT, k < 8) hold tile u's bounds on coordinate k (tlo, thi)
-// and its ub2 max (tub); gap^2 summed over k in groups of 8 lanes
-template <int NT>
-__device__ __forceinline__ uint32_t nh_su_skip(const float *__restrict__ box, int su, float tlo,
-                                               float thi, float tub) {
-  const int lane = threadIdx.x & (WAVE - 1), k = lane & 7;
-  const float slo = box[16 * su + k], shi = box[16 * su + 8 + k];
-  const float gap = fmaxf(0.0f, fmaxf(slo - thi, tlo - shi));
-  float g2 = gap * gap;
-  g2 += __shfl_xor(g2, 1);
-  g2 += __shfl_xor(g2, 2);
-  g2 += __shfl_xor(g2, 4);
-  const bool skip = lane < 8 * NT && (lane & 7) == 0 && g2 > tub * (1.0f + 1e-5f);
-  const unsigned long long b = __ballot(skip);
-  uint32_t m = 0;
-#pragma unroll
-  for (int u = 0; u < NT; u++) m |= (uint32_t)((b >> (8 * u)) & 1ull) << u;
-  return m;
-}
-
 // pass of one wave over chunks [c0, c1) (c0 even; wave-uniform, as is nv):
 // NT query tiles (B operands b1, b2).  Lane (r, h) reads row c*32 + r: part
 // h (F_hi / F_lo) for MFMA 1 and part 2 + h (F_hi / norm) for MFMA 2, two
@@ -528,32 +439,10 @@ __device__ __forceinline__ uint32_t nh_su_skip(const float *__restrict__ box, in
 // top-2 bookkeeping runs once per unit
 template <int NT>
 __device__ __forceinline__ void nh_sweep(const _Float16 *__restrict__ vh, int c0, int c1, int nv,
-                                         const nh8 (&b1)[NT], const nh8 (&b2)[NT], NhTop (&t)[NT],
-                                         const NhIndex &ix, float tlo, float thi, float tub) {
+                                         const nh8 (&b1)[NT], const nh8 (&b2)[NT], NhTop (&t)[NT]) {
   const int lane = threadIdx.x & (WAVE - 1), r = lane & 31, h = lane >> 5;
-  const nh8 *tbase = (const nh8 *)vh + (NH_ROW / 8) * r + h;       // positions past ix.n
-  const nh8 *sbase = (const nh8 *)ix.h + (NH_ROW / 8) * r + h;     // sorted positions
+  const nh8 *base = (const nh8 *)vh + (NH_ROW / 8) * r + h;
   constexpr int64_t CS = NH_ROW * 4;  // nh8 per chunk
-  const int sc = ix.n >> 5;           // sorted chunks (a multiple of 8)
-  const bool skipping = ix.qtile != nullptr;
-  int su_c = -1;                      // the superunit whose mask is cached
-  uint32_t su_m = 0;
-  // the tiles that skip chunk c's superunit (sorted positions only)
-  auto mask = [&](int c) -> uint32_t {
-    if (!skipping || c >= sc) return 0u;
-    const int su = c >> 3;
-    if (su != su_c) {
-      su_c = su;
-      su_m = nh_su_skip<NT>(ix.box, su, tlo, thi, tub);
-    }
-    return su_m;
-  };
-  constexpr uint32_t ALL = (1u << NT) - 1u;
-  // the first unit from c on that some tile scores (c even, < uf)
-  auto live_from = [&](int c, int uf) {
-    while (c < uf && mask(c) == ALL) c = min(uf, ((c >> 3) + 1) << 3);
-    return c;
-  };
   // tile u's minimum over its lane-unit: the scores of chunks c and c + 1
   // (TAIL: rows past nv masked, chunk c + 1 absent when c + 1 >= c1)
   auto unit_min = [&](int u, int c, const nh8 (&a)[4], auto tail_tag) {
@@ -575,34 +464,29 @@ __device__ __forceinline__ void nh_sweep(const _Float16 *__restrict__ vh, int c0
     return m;
   };
   auto load = [&](int c, nh8 (&d)[4]) {
-    const nh8 *base = c < sc ? sbase : tbase;  // a unit is all sorted or all tail
     d[0] = base[CS * c];
     d[1] = base[CS * c + 2];
     d[2] = base[CS * (c + 1)];
     d[3] = base[CS * (c + 1) + 2];
   };
-  // full units, the next scored unit's rows in flight while one is scored; a
+  // full units, the next unit's rows in flight while one is scored; a
   // scheduling barrier per tile keeps one tile's accumulators live at a time
   const int uf = min(c1, nv >> 5) & ~1;  // chunks [c0, uf) form full units
-  int c = live_from(c0, uf);
-  if (c < uf) {
+  if (c0 < uf) {
     nh8 a[4], p[4];
-    load(c, a);
-    while (c < uf) {
-      const uint32_t m = mask(c);
-      const int cn = live_from(c + 2, uf);
-      if (cn < uf) load(cn, p);
+    load(c0, a);
+    for (int c = c0; c < uf; c += 2) {
+      if (c + 2 < uf) load(c + 2, p);
 #pragma unroll
       for (int u = 0; u < NT; u++) {
-        if (!((m >> u) & 1u)) t[u].insert(unit_min(u, c, a, std::false_type{}), c >> 1);
+        t[u].insert(unit_min(u, c, a, std::false_type{}), c >> 1);
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int k = 0; k < 4; k++) a[k] = p[k];
-      c = cn;
     }
   }
-  if (uf < c1) {  // the last unit: a lone chunk and/or rows past the tree's end (tail)
+  if (uf < c1) {  // the last unit: a lone chunk and/or rows past the tree's end
     nh8 a[4];
     load(uf, a);  // the row arrays hold whole units
 #pragma unroll
@@ -643,8 +527,6 @@ struct NhPrep {
   int direction;
   int first_block;  // blocks [first_block, gridDim.x) draw the actions
   NhDraw dr;        // blocks [0, dr.draw_blocks): the next half's targets
-  const double *targets = nullptr;  // the targets in their own order (the search's
-                                    // queries may be a sorted copy)
 };
 
 template <int NT, class ZT, bool PREP>
@@ -657,8 +539,7 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
                                                    const float *__restrict__ hm,
                                                    const int32_t *__restrict__ nv_dev, int64_t bmax,
                                                    float4 *__restrict__ pm, int4 *__restrict__ pid,
-                                                   uint64_t seq, int n_items, NhPrep<ZT> pp,
-                                                   NhIndex ix) {
+                                                   uint64_t seq, int n_items, NhPrep<ZT> pp) {
   if (gated(st, seq)) {
     if (PREP && blockIdx.x == pp.first_block && threadIdx.x == 0) st->n_validate = 0;
     return;
@@ -698,9 +579,8 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
       const int64_t i = c / GBP_NUM_GEN_STATES;
       const int j = (int)(c - i * GBP_NUM_GEN_STATES);
       double nrm[3], a[10];
-      const double *tq = pp.targets + 8 * i;
-      surface_normal(pp.T, tq[0], tq[1], nrm);  // rrt.cpp:25
-      sample_action_cfg(nrm, pp.cfg, pp.direction, tq, tq /* unused: not biased */,
+      surface_normal(pp.T, q[8 * i], q[8 * i + 1], nrm);  // rrt.cpp:25
+      sample_action_cfg(nrm, pp.cfg, pp.direction, q + 8 * i, q + 8 * i /* unused: not biased */,
                         pp.seed, GBP_EXTEND_STREAM, (base + i) * 8 + j, a);  // rrt.cpp:34, :49
       copy10(pp.ca + 10 * c, a);
     }
@@ -741,18 +621,7 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
         }
       }
     }
-    // lanes 8u + k: tile u's box on coordinate k and its ub2 max (skipping)
-    float tlo = 0.f, thi = 0.f, tub = -1.f;
-    if (ix.qtile && lane < 8 * NT) {
-      const int64_t tile = qg * NT + (lane >> 3);
-      if (tile * 32 < nq) {
-        const float *qt = ix.qtile + NH_QT * tile;
-        tlo = qt[lane & 7];
-        thi = qt[8 + (lane & 7)];
-        tub = qt[16];
-      }
-    }
-    if (!tree_bad) nh_sweep<NT>(vh, c0, c1, (int)nv, b1, b2, t, ix, tlo, thi, tub);
+    if (!tree_bad) nh_sweep<NT>(vh, c0, c1, (int)nv, b1, b2, t);
     // the two lanes of a query (rows 4h + ...): merge to one entry, the three
     // smallest lane-units (id = 2 unit + h) and a lower bound on the rest:
     // the other lane's three inserted into this lane's list
@@ -803,8 +672,7 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
                                                        int64_t bmax, const float4 *__restrict__ pm,
                                                        const int4 *__restrict__ pid,
                                                        int32_t *__restrict__ out, uint64_t seq,
-                                                       int stats, double *__restrict__ cs, int n_items,
-                                                       NhIndex ix, const int32_t *__restrict__ qperm) {
+                                                       int stats, double *__restrict__ cs, int n_items) {
   if (gated(st, seq)) return;
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   int64_t nqg, nseg, cps, nch;
@@ -840,11 +708,10 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
     if (live && (qbad || tree_bad || !(B < INFINITY))) {  // the whole tree in fp64
       nsc = sl == 0;
       for (int64_t j = sl; j < nv; j += NH_G) {
-        const int64_t vj = nh_vertex(ix, j);
-        const double d = nn_dist64(qq, v + 8 * vj);
-        if (d < best || (d == best && vj < bi)) {  // the lowest vertex at the minimum
+        const double d = nn_dist64(qq, v + 8 * j);
+        if (d < best) {  // ascending per lane: the first index at its minimum
           best = d;
-          bi = (int)vj;
+          bi = (int)j;
         }
       }
     }
@@ -898,11 +765,10 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
             const int64_t j =
                 (int64_t)(h >> 1) * 64 + 32 * b + 4 * (h & 1) + (i & 3) + 8 * (i >> 2);
             if (j < nv) {
-              const int64_t vj = nh_vertex(ix, j);
-              const double d = nn_dist64(qq, v + 8 * vj);
-              if (d < best || (d == best && vj < bi)) {
+              const double d = nn_dist64(qq, v + 8 * j);
+              if (d < best || (d == best && j < bi)) {
                 best = d;
-                bi = (int)vj;
+                bi = (int)j;
               }
             }
           }
@@ -922,36 +788,15 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
 #pragma unroll
         for (int k = 0; k < 8; k++) oq[k] = __shfl(qq[k], src);
         const int64_t ss = s0 + (__ffs(sm) - 1);
-        const int64_t j0 = ss * cps * 32, j1 = min(nv, min(nch, (ss + 1) * cps) * 32);
-        // the owner's best so far (the exact distance of a vertex): a sorted
-        // superunit whose box is farther holds neither the nearest vertex nor
-        // a tie (lower bound in fp64 from the fp32 box, margin 1e-12)
-        const double ob = __shfl(best, src);
+        const int64_t j1 = min(nv, min(nch, (ss + 1) * cps) * 32);
         double wb = INFINITY;
         int wi = 0x7FFFFFFF;
-        for (int64_t p0 = j0; p0 < j1;) {
-          const int64_t p1 = p0 < ix.n ? min(j1, (p0 / NH_SU + 1) * NH_SU) : j1;
-          bool skip = false;
-          if (p0 < ix.n && ob < INFINITY) {
-            const float *bx = ix.box + 16 * (p0 / NH_SU);
-            double lb2 = 0.0;
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-              const double g = fmax(0.0, fmax((double)bx[k] - oq[k], oq[k] - (double)bx[8 + k]));
-              lb2 += g * g;
-            }
-            skip = lb2 * (1.0 - 1e-12) > ob * ob * (1.0 + 1e-12);
+        for (int64_t j = ss * cps * 32 + (threadIdx.x & (WAVE - 1)); j < j1; j += WAVE) {
+          const double d = nn_dist64(oq, v + 8 * j);
+          if (d < wb) {  // ascending per lane
+            wb = d;
+            wi = (int)j;
           }
-          if (!skip)
-            for (int64_t j = p0 + (threadIdx.x & (WAVE - 1)); j < p1; j += WAVE) {
-              const int64_t vj = nh_vertex(ix, j);
-              const double d = nn_dist64(oq, v + 8 * vj);
-              if (d < wb || (d == wb && vj < wi)) {
-                wb = d;
-                wi = (int)vj;
-              }
-            }
-          p0 = p1;
         }
 #pragma unroll
         for (int off = WAVE / 2; off > 0; off >>= 1) {
@@ -977,10 +822,9 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
         bi = oi;
       }
     }
-    const int64_t qo = live && qperm ? (int64_t)qperm[qi] : qi;  // the query's own index
-    if (live && sl == 0) out[qo] = bi == 0x7FFFFFFF ? 0 : bi;
+    if (live && sl == 0) out[qi] = bi == 0x7FFFFFFF ? 0 : bi;
     if (cs && live && sl < GBP_NUM_GEN_STATES)  // s_near of the six candidates (k_extend_prep)
-      copy8(cs + 8 * (qo * GBP_NUM_GEN_STATES + sl), v + 8 * (int64_t)(bi == 0x7FFFFFFF ? 0 : bi));
+      copy8(cs + 8 * (qi * GBP_NUM_GEN_STATES + sl), v + 8 * (int64_t)(bi == 0x7FFFFFFF ? 0 : bi));
     if (!stats) continue;  // diagnostics (GBP_OPT_NN_STATS): same-address atomics serialise
     for (int off = 32; off > 0; off >>= 1) {
       nrc += __shfl_xor(nrc, off);
@@ -1923,192 +1767,6 @@ __global__ __launch_bounds__(RB) void k_star_shared(gbp_plan_status *st, const i
   }
 }
 
-// ============================================================================
-// the spatial index of the nearest-vertex search (NhIndex above)
-// ============================================================================
-// a bin histogram over items [0, n): per-workgroup in LDS, then global
-__device__ void nh_hist(int64_t n, const double *__restrict__ xy8, const NhExt &e,
-                        int32_t *__restrict__ cnt) {
-  __shared__ int32_t h[NH_BINS];
-  for (int b = threadIdx.x; b < NH_BINS; b += blockDim.x) h[b] = 0;
-  __syncthreads();
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    atomicAdd(&h[nh_bin(xy8[8 * i], xy8[8 * i + 1], e)], 1);
-  __syncthreads();
-  for (int b = threadIdx.x; b < NH_BINS; b += blockDim.x)
-    if (h[b]) atomicAdd(&cnt[b], h[b]);
-}
-// exclusive offsets of the NH_BINS counts (one workgroup of 1024); off[NH_BINS] = total
-__device__ void nh_scan(const int32_t *__restrict__ cnt, int32_t *__restrict__ off,
-                        int32_t *__restrict__ cur) {
-  __shared__ int32_t part[1024];
-  constexpr int PER = NH_BINS / 1024;
-  int32_t s = 0;
-  for (int k = 0; k < PER; k++) s += cnt[PER * threadIdx.x + k];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele
-    const int32_t v = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  int32_t run = part[threadIdx.x] - s;
-  for (int k = 0; k < PER; k++) {
-    const int b = PER * threadIdx.x + k;
-    off[b] = run;
-    if (cur) cur[b] = run;
-    run += cnt[b];
-  }
-  if (threadIdx.x == 1023) off[NH_BINS] = run;
-}
-
-__global__ __launch_bounds__(256) void k_ix_hist(int64_t n, const double *__restrict__ v, NhExt e,
-                                                 int32_t *__restrict__ cnt) {
-  nh_hist(n, v, e, cnt);
-}
-__global__ __launch_bounds__(1024) void k_ix_scan(const int32_t *__restrict__ cnt,
-                                                  int32_t *__restrict__ off, int32_t *__restrict__ cur) {
-  nh_scan(cnt, off, cur);
-}
-// the sorted positions: vertex and fp16 row (cur: the bins' next free position)
-__global__ __launch_bounds__(256) void k_ix_scatter(int64_t n, const double *__restrict__ v,
-                                                    const _Float16 *__restrict__ vh, NhExt e,
-                                                    int32_t *__restrict__ cur, int32_t *__restrict__ perm,
-                                                    _Float16 *__restrict__ ixh) {
-  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
-       j += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t pos = atomicAdd(&cur[nh_bin(v[8 * j], v[8 * j + 1], e)], 1);
-    perm[pos] = (int32_t)j;
-    const nh8 *src = (const nh8 *)(vh + (int64_t)NH_ROW * j);
-    nh8 *dst = (nh8 *)(ixh + (int64_t)NH_ROW * pos);
-#pragma unroll
-    for (int k = 0; k < NH_ROW / 8; k++) dst[k] = src[k];
-  }
-}
-// one workgroup of NH_SU per superunit: its 8-D box, rounded outward to fp32
-__global__ __launch_bounds__(NH_SU) void k_ix_box(const double *__restrict__ v,
-                                                  const int32_t *__restrict__ perm,
-                                                  float *__restrict__ box) {
-  __shared__ double lo[NH_SU / WAVE][8], hi[NH_SU / WAVE][8];
-  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
-  const double *x = v + 8 * (int64_t)perm[(int64_t)blockIdx.x * NH_SU + threadIdx.x];
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    double a = x[k], b = x[k];
-    for (int o = WAVE / 2; o > 0; o >>= 1) {
-      a = fmin(a, __shfl_xor(a, o));
-      b = fmax(b, __shfl_xor(b, o));
-    }
-    if (lane == 0) {
-      lo[w][k] = a;
-      hi[w][k] = b;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < 8) {
-    const int k = threadIdx.x;
-    double a = lo[0][k], b = hi[0][k];
-    for (int i = 1; i < NH_SU / WAVE; i++) {
-      a = fmin(a, lo[i][k]);
-      b = fmax(b, hi[i][k]);
-    }
-    // a NaN coordinate anywhere: no bound on that axis
-    const bool nan = a != a || b != b;
-    box[16 * blockIdx.x + k] = nan ? -INFINITY : nh_down(a);
-    box[16 * blockIdx.x + 8 + k] = nan ? INFINITY : nh_up(b);
-  }
-}
-
-// ---- the targets sorted the same way for one search (stage 2) ------------------
-__global__ __launch_bounds__(256) void k_qs_hist(gbp_plan_status *st, const double *__restrict__ q,
-                                                 NhExt e, int32_t *__restrict__ cnt, uint64_t seq) {
-  if (gated(st, seq)) return;
-  nh_hist(st->n_targets, q, e, cnt);
-}
-__global__ __launch_bounds__(1024) void k_qs_scan(gbp_plan_status *st, const int32_t *__restrict__ cnt,
-                                                  int32_t *__restrict__ off, int32_t *__restrict__ cur,
-                                                  uint64_t seq) {
-  if (gated(st, seq)) return;
-  nh_scan(cnt, off, cur);
-}
-// query i to its sorted position: its rows, its index (qperm) and ub2, the
-// squared fp64 distance to the nearest of the 32 sorted vertices around its bin
-__global__ __launch_bounds__(256) void k_qs_scatter(gbp_plan_status *st, const double *__restrict__ q,
-                                                    const _Float16 *__restrict__ qh, NhExt e,
-                                                    int32_t *__restrict__ cur, int32_t *__restrict__ qperm,
-                                                    double *__restrict__ qs, _Float16 *__restrict__ qhs,
-                                                    float *__restrict__ ub2, const double *__restrict__ v,
-                                                    const int32_t *__restrict__ ixoff,
-                                                    const int32_t *__restrict__ ixperm, int32_t ixn,
-                                                    uint64_t seq) {
-  if (gated(st, seq)) return;
-  const int64_t n = st->n_targets;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    double x[8];
-    copy8(x, q + 8 * i);
-    const int b = nh_bin(x[0], x[1], e);
-    const int32_t pos = atomicAdd(&cur[b], 1);
-    qperm[pos] = (int32_t)i;
-    copy8(qs + 8 * (int64_t)pos, x);
-    const nh8 *src = (const nh8 *)(qh + (int64_t)NH_ROW * i);
-    nh8 *dst = (nh8 *)(qhs + (int64_t)NH_ROW * pos);
-#pragma unroll
-    for (int k = 0; k < NH_ROW / 8; k++) dst[k] = src[k];
-    double u = INFINITY;
-    if (ixn >= 32) {
-      const int32_t p0 = max(0, min(ixn - 32, ixoff[b] - 16));
-      for (int r = 0; r < 32; r++) {
-        const double *w = v + 8 * (int64_t)ixperm[p0 + r];
-        double sum = 0;  // nn_dist64's sum: its sqrt is the vertex's distance
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-          const double d = w[k] - x[k];
-          sum = sum + 1.0 * d * d;
-        }
-        u = fmin(u, sum);  // (NaN sums ignored)
-      }
-    }
-    ub2[pos] = nh_up(u);
-  }
-}
-// per tile of 32 sorted queries: box (rounded outward) and the largest ub2
-__global__ __launch_bounds__(256) void k_qs_tiles(gbp_plan_status *st, const double *__restrict__ qs,
-                                                  const float *__restrict__ ub2,
-                                                  float *__restrict__ qtile, uint64_t seq) {
-  if (gated(st, seq)) return;
-  const int64_t n = st->n_targets, ntile = (n + 31) / 32;
-  const int lane = threadIdx.x & (WAVE - 1);
-  // two tiles per wave: lanes 0-31 and 32-63
-  for (int64_t t0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / 32; t0 < (ntile + 1) / 2 * 2;
-       t0 += (int64_t)gridDim.x * blockDim.x / 32) {
-    const int64_t i = 32 * t0 + (lane & 31);
-    const bool live = t0 < ntile && i < n;
-    float out[NH_QT];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const double x = live ? qs[8 * i + k] : 0.0;
-      float a = live ? (x == x ? nh_down(x) : -INFINITY) : INFINITY;
-      float b = live ? (x == x ? nh_up(x) : INFINITY) : -INFINITY;
-      for (int o = 16; o > 0; o >>= 1) {
-        a = fminf(a, __shfl_xor(a, o, 32));
-        b = fmaxf(b, __shfl_xor(b, o, 32));
-      }
-      out[k] = a;
-      out[8 + k] = b;
-    }
-    float u = live ? ub2[i] : -INFINITY;
-    for (int o = 16; o > 0; o >>= 1) u = fmaxf(u, __shfl_xor(u, o, 32));
-    out[16] = u != u ? INFINITY : u;
-    float val = 0.f;  // out[lane & 31] without a dynamically indexed register array
-#pragma unroll
-    for (int k = 0; k < NH_QT; k++) val = (lane & 31) == k ? out[k] : val;
-    if (t0 < ntile && (lane & 31) < NH_QT) qtile[NH_QT * t0 + (lane & 31)] = val;
-  }
-}
-
 __global__ void k_tree_init(gbp_tree t, double r0, double r1, double r2, double r3, double r4,
                             double r5, double r6, double r7) {
   const double r[8] = {r0, r1, r2, r3, r4, r5, r6, r7};
@@ -2223,26 +1881,12 @@ unsigned tiles_for(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + CB - 
 // qh: the queries' fp16 rows (nn_put_hrow layout, same offsets as q), or
 // null (converted in the search); prep: the extends' candidates are drawn
 // inside the search (returns *prepped)
-NhExt nh_ext(const gbp_tree *tr) {
-  const double *e = tr->ix_ext;
-  return NhExt{e[0], 64.0 / (e[1] - e[0]), e[2], 64.0 / (e[3] - e[2])};
-}
-
-// the search's view of tr's index (none: positions are vertices)
-NhIndex nh_index(const gbp_tree *tr, const float *qtile = nullptr) {
-  NhIndex ix{0, nullptr, nullptr, nullptr, nullptr};
-  if (tr->ix_n > 0) ix = NhIndex{(int32_t)tr->ix_n, tr->ixh, tr->ixperm, tr->ixbox, qtile};
-  return ix;
-}
-
 template <class ZT = float>
 int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
               const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s,
               const _Float16 *qh = nullptr, const NhPrep<ZT> *prep = nullptr,
-              double *cs = nullptr, bool *prepped = nullptr, const float *qtile = nullptr,
-              const int32_t *qperm = nullptr) {
+              double *cs = nullptr, bool *prepped = nullptr) {
   if (prepped) *prepped = false;
-  const NhIndex ix = nh_index(tr, qtile);
   const int gm = w->nn_items / (NH_TB / WAVE);  // the search's workgroups: one wave per item
   if (prep) {
     NhPrep<ZT> pp = *prep;
@@ -2251,17 +1895,17 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
     const int gp = (int)grid_for(GBP_NUM_GEN_STATES * w->bmax, NH_TB, num_cus * 4);
     hipLaunchKernelGGL((k_nn_mfma<NH_NT, ZT, true>), dim3(gd + gm + gp), dim3(NH_TB), 0, s, w->st,
                        nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
-                       (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, w->nn_items, pp, ix);
+                       (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, w->nn_items, pp);
     if (prepped) *prepped = true;
   } else {
     hipLaunchKernelGGL((k_nn_mfma<NH_NT, float, false>), dim3(gm), dim3(NH_TB), 0, s, w->st,
                        nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
-                       (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, w->nn_items, NhPrep<float>{}, ix);
+                       (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, w->nn_items, NhPrep<float>{});
   }
   hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(NH_G * w->bmax, NH_RTB, num_cus * 8)), dim3(NH_RTB),
                      0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, tr->count, w->bmax,
                      (const float4 *)w->nn_d, (const int4 *)w->nn_i, out, ++w->seq, w->nn_stats,
-                     prep ? cs : nullptr, w->nn_items, ix, qperm);
+                     prep ? cs : nullptr, w->nn_items);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
 
@@ -2303,29 +1947,9 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
       prep.dr.tiles = w->tiles;
       prep.dr.epoch = next_epoch(w);
     }
-    prep.targets = w->targets;
     bool prepped = false;
-    int rc;
-    if (T->ix_n > 0 && w->qs_block) {
-      // T is indexed: the targets sorted by its bins, so that a wave's query
-      // tiles are compact and skip the superunits they cannot be nearest to
-      const NhExt e = nh_ext(T);
-      int32_t *qoff = w->qcnt + NH_BINS, *qcur = qoff + NH_BINS + 1;
-      const unsigned gq = (unsigned)grid_for(batch, 256, cus * 2);
-      HIPCHK_P(hipMemsetAsync(w->qcnt, 0, sizeof(int32_t) * NH_BINS, s));
-      hipLaunchKernelGGL(k_qs_hist, dim3(gq), dim3(256), 0, s, st, w->targets, e, w->qcnt, ++w->seq);
-      hipLaunchKernelGGL(k_qs_scan, dim3(1), dim3(1024), 0, s, st, w->qcnt, qoff, qcur, ++w->seq);
-      hipLaunchKernelGGL(k_qs_scatter, dim3(gq), dim3(256), 0, s, st, w->targets, w->tqh, e, qcur,
-                         w->qperm, w->qs, w->qhs, w->qub2, T->v, T->ixoff, T->ixperm,
-                         (int32_t)T->ix_n, ++w->seq);
-      hipLaunchKernelGGL(k_qs_tiles, dim3(grid_for((batch + 31) / 32 * 32, 256, cus * 2)), dim3(256), 0,
-                         s, st, w->qs, w->qub2, w->qtile, ++w->seq);
-      rc = nn_launch<ZT>(w, &st->n_targets, w->qs, nullptr, T, w->nn, cus, s, w->qhs,
-                         early ? &prep : nullptr, w->cs, &prepped, w->qtile, w->qperm);
-    } else {
-      rc = nn_launch<ZT>(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, w->tqh,
-                         early ? &prep : nullptr, w->cs, &prepped);
-    }
+    int rc = nn_launch<ZT>(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, w->tqh,
+                           early ? &prep : nullptr, w->cs, &prepped);
     if (rc) return rc;
     const int64_t mmax = batch * GBP_NUM_GEN_STATES;
     if (!prepped)
@@ -2514,8 +2138,7 @@ int gbp_tree_destroy(gbp_tree *t) {
   if (!t) return GBP_E_BAD_HANDLE;
   Guard g(t->device);
   (void)hipDeviceSynchronize();
-  void *ptrs[] = {t->v, t->vh, t->hm, t->a, t->g, t->parent, t->child, t->count,
-                  t->ixh, t->ixperm, t->ixbox, t->ixoff};
+  void *ptrs[] = {t->v, t->vh, t->hm, t->a, t->g, t->parent, t->child, t->count};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   delete t;
@@ -2549,59 +2172,6 @@ int gbp_tree_reserve(gbp_tree *t, int64_t capacity, gbp_stream stream) {
   (void)hipFree(old.g);
   (void)hipFree(old.parent);
   (void)hipFree(old.child);
-  t->ix_n = 0;  // the index keeps its arrays (sized to its own capacity) until the next build
-  return GBP_OK;
-}
-
-int gbp_tree_index_build(gbp_tree *t, const double *extent, gbp_stream stream) {
-  if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
-  if (!extent || !(extent[1] > extent[0]) || !(extent[3] > extent[2])) return GBP_E_INVALID_ARG;
-  Guard g(t->device);
-  hipStream_t s = (hipStream_t)stream;
-  int64_t count = 0;
-  int rc = gbp_tree_size(t, &count, stream);
-  if (rc) return rc;
-  const int64_t n = count / NH_SU * NH_SU;
-  t->ix_n = 0;
-  if (n < NH_SU) return GBP_OK;  // too small to index: positions stay vertices
-  if (t->ix_cap < n) {  // (re)allocate for the tree's capacity
-    HIPCHK_P(hipStreamSynchronize(s));
-    void *ptrs[] = {t->ixh, t->ixperm, t->ixbox, t->ixoff};
-    for (void *p : ptrs)
-      if (p) (void)hipFree(p);
-    t->ixh = nullptr;
-    t->ixperm = t->ixoff = t->ixcnt = nullptr;
-    t->ixbox = nullptr;
-    const int64_t c = t->cap / NH_SU * NH_SU;
-    if (hipMalloc(&t->ixh, 2 * NH_ROW * c) != hipSuccess || hipMalloc(&t->ixperm, 4 * c) != hipSuccess ||
-        hipMalloc(&t->ixbox, 64 * (c / NH_SU)) != hipSuccess ||
-        hipMalloc(&t->ixoff, 4 * (3 * NH_BINS + 1)) != hipSuccess) {
-      t->ix_cap = 0;
-      return GBP_E_ALLOC;
-    }
-    t->ixcnt = t->ixoff + NH_BINS + 1;
-    t->ix_cap = c;
-  }
-  for (int k = 0; k < 4; k++) t->ix_ext[k] = extent[k];
-  const NhExt e = nh_ext(t);
-  int32_t *cur = t->ixcnt + NH_BINS;
-  const unsigned gr = (unsigned)grid_for(n, 256, 1024);
-  HIPCHK_P(hipMemsetAsync(t->ixcnt, 0, sizeof(int32_t) * NH_BINS, s));
-  hipLaunchKernelGGL(k_ix_hist, dim3(gr), dim3(256), 0, s, n, t->v, e, t->ixcnt);
-  hipLaunchKernelGGL(k_ix_scan, dim3(1), dim3(1024), 0, s, t->ixcnt, t->ixoff, cur);
-  hipLaunchKernelGGL(k_ix_scatter, dim3(gr), dim3(256), 0, s, n, t->v, t->vh, e, cur, t->ixperm,
-                     t->ixh);
-  hipLaunchKernelGGL(k_ix_box, dim3((unsigned)(n / NH_SU)), dim3(NH_SU), 0, s, t->v, t->ixperm,
-                     t->ixbox);
-  HIPCHK_P(hipGetLastError());
-  t->ix_n = n;
-  return GBP_OK;
-}
-
-int gbp_tree_index_size(gbp_tree *t, int64_t *indexed) {
-  if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
-  if (!indexed) return GBP_E_INVALID_ARG;
-  *indexed = t->ix_n;
   return GBP_OK;
 }
 
@@ -2609,7 +2179,6 @@ int gbp_tree_init(gbp_tree *t, const double *root, gbp_stream stream) {
   if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
   if (!root) return GBP_E_INVALID_ARG;
   Guard g(t->device);
-  t->ix_n = 0;  // a re-rooted tree drops its index
   hipLaunchKernelGGL(k_tree_init, dim3(1), dim3(1), 0, (hipStream_t)stream, *t, root[0], root[1],
                      root[2], root[3], root[4], root[5], root[6], root[7]);
   HIPCHK_P(hipGetLastError());
@@ -2747,22 +2316,6 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
     delete w;
     return GBP_E_HIP;
   }
-  {  // the sorted targets of an indexed tree's search
-    const size_t qb = 4 * b + 64 * b + 2 * NH_ROW * b + 4 * b + 4 * NH_QT * (b / 32 + 1) +
-                      4 * (3 * NH_BINS + 1) + 8 * 256;
-    if (hipMalloc(&w->qs_block, qb) != hipSuccess) {
-      (void)hipFree(w->block);
-      delete w;
-      return GBP_E_ALLOC;
-    }
-    char *q = (char *)w->qs_block;
-    w->qperm = carve<int32_t>(q, b);
-    w->qs = carve<double>(q, 8 * b);
-    w->qhs = carve<_Float16>(q, NH_ROW * b);
-    w->qub2 = carve<float>(q, b);
-    w->qtile = carve<float>(q, NH_QT * (b / 32 + 1));
-    w->qcnt = carve<int32_t>(q, 3 * NH_BINS + 1);
-  }
   hipLaunchKernelGGL(k_plan_reset, dim3(1), dim3(1), 0, nullptr, w->st, (int64_t)0);
   if (hipDeviceSynchronize() != hipSuccess) {
     (void)hipFree(w->block);
@@ -2779,7 +2332,6 @@ int gbp_plan_ws_destroy(gbp_plan_ws *w) {
   (void)hipDeviceSynchronize();
   if (w->block) (void)hipFree(w->block);
   if (w->star_block) (void)hipFree(w->star_block);
-  if (w->qs_block) (void)hipFree(w->qs_block);
   delete w;
   return GBP_OK;
 }

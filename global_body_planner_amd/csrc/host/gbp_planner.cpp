@@ -1528,35 +1528,6 @@ struct DeviceTrees {
   }
 };
 
-// the device trees' spatial index for the nearest-vertex searches
-// (gbp_tree_index_build, GBP_OPT_NN_INDEX): rebuilt between groups once the
-// vertices appended since the last build reach the option's threshold
-struct TreeIndexer {
-  int64_t opt = 1;
-  double ext[4] = {0, 1, 0, 1};
-  int64_t indexed[2] = {0, 0};
-  TreeIndexer(FastTerrainMap &terrain) {
-    chk(gbp_terrain_get_option(terrain.handle(), GBP_OPT_NN_INDEX, &opt), "nn index option");
-    const std::vector<double> &x = terrain.getXData(), &y = terrain.getYData();
-    if (x.size() < 2 || y.size() < 2) opt = 0;
-    else {
-      ext[0] = x.front();
-      ext[1] = x.back();
-      ext[2] = y.front();
-      ext[3] = y.back();
-    }
-  }
-  void update(gbp_tree *t, int k, int64_t count, gbp_stream s) {
-    if (opt <= 0) return;
-    const int64_t tail = count - indexed[k];
-    const int64_t need = opt == 1 ? std::max<int64_t>(4096, indexed[k] / 8) : opt;
-    if (tail < need) return;
-    chk(gbp_tree_index_build(t, ext, s), "tree index");
-    chk(gbp_tree_index_size(t, &indexed[k]), "tree index");
-  }
-  void dropped(int k) { indexed[k] = 0; }  // gbp_tree_reserve drops the index
-};
-
 struct HostTree {  // a device tree read back once the search ends
   std::vector<State> v;
   std::vector<Action> a;
@@ -1645,7 +1616,6 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
     known[k] = std::max<int64_t>(1, wn);
   }
   if (st.warm_half < 0 || st.warm_extend < 0) throw EngineError(GBP_E_INVALID_ARG, "warm start");
-  TreeIndexer ixr(terrain);
   const int32_t half0 = (int32_t)st.warm_half;
   if (st.warm_n[0] > 0 || st.warm_n[1] > 0 || half0 > 0) extend_counter_ = st.warm_extend;
   chk(gbp_plan_reset(D.ws, extend_counter_, D.stream), "plan reset");
@@ -1667,13 +1637,10 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
       for (int k = 0; k < 2; k++) {  // room for `group` halves of appends
         int64_t c = 0;
         chk(gbp_tree_capacity(D.tree[k], &c), "tree capacity");
-        if (known[k] + (int64_t)group * batch > c) {
+        if (known[k] + (int64_t)group * batch > c)
           chk(gbp_tree_reserve(D.tree[k], std::max<int64_t>(2 * c, known[k] + (int64_t)group * batch),
                                D.stream),
               "tree reserve");
-          ixr.dropped(k);
-        }
-        ixr.update(D.tree[k], k, known[k], D.stream);
       }
       // the group's halves, one stream-ordered kernel sequence
       chk(gbp_plan_halves_dev(h, D.ws, D.tree[0], D.tree[1], half, group, batch, seed_, tstream[0],
@@ -2237,7 +2204,6 @@ bool RRTStarConnectClass::buildRRTStarConnectDevice(FastTerrainMap &terrain, Sta
   chk(gbp_tree_init(D.tree[1], s_goal.data(), D.stream), "tree init");
   chk(gbp_plan_reset(D.ws, extend_counter_, D.stream), "plan reset");
   int64_t known[2] = {1, 1};
-  TreeIndexer ixr(terrain);
   const uint64_t tstream[2] = {401, 402};  // buildRRTStarConnectBatched's streams
   const int g_max = (int)std::max<int64_t>(2, std::min<int64_t>(64, (1 << 21) / batch)) & ~1;
   int group = 2;
@@ -2248,13 +2214,10 @@ bool RRTStarConnectClass::buildRRTStarConnectDevice(FastTerrainMap &terrain, Sta
     for (int k = 0; k < 2; k++) {
       int64_t c = 0;
       chk(gbp_tree_capacity(D.tree[k], &c), "tree capacity");
-      if (known[k] + (int64_t)group * batch > c) {
+      if (known[k] + (int64_t)group * batch > c)
         chk(gbp_tree_reserve(D.tree[k], std::max<int64_t>(2 * c, known[k] + (int64_t)group * batch),
                              D.stream),
             "tree reserve");
-        ixr.dropped(k);
-      }
-      ixr.update(D.tree[k], k, known[k], D.stream);
     }
     chk(gbp_plan_halves_dev(h, D.ws, D.tree[0], D.tree[1], half, group, batch, seed_, tstream[0],
                             tstream[1], adaptive, 0, D.stream),
@@ -2356,7 +2319,7 @@ bool RRTStarConnectClass::buildRRTStarConnectDevice(FastTerrainMap &terrain, Sta
 // flat C entry point
 // ============================================================================
 // the layout planner.py's PlanParams mirrors (tests/test_abi.py)
-static_assert(sizeof(gbp_plan_params) == 464, "gbp_plan_params layout");
+static_assert(sizeof(gbp_plan_params) == 456, "gbp_plan_params layout");
 
 extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r,
                                     double *path_states, double *path_actions, int capacity) {
@@ -2369,9 +2332,6 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
       chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_FRAGILE_EPS, p->fragile_eps_fm),
           "fragile eps");
     chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_NN_STATS, p->nn_stats), "nn stats");
-    if (p->nn_index)  // 1 = the default threshold; >= 2 an explicit one; -1: no index
-      chk(gbp_terrain_set_option(terrain.handle(), GBP_OPT_NN_INDEX, p->nn_index < 0 ? 0 : p->nn_index),
-          "nn index");
     RRTStarConnectClass planner;  // is-a RRTConnectClass: algorithm 0 uses the plain build
     planner.setSeed(p->seed);
     planner.set_state_direction_sampling(p->sampling.state_flag != 0, p->sampling.state_p,

@@ -34,7 +34,7 @@ class PlanParams(ctypes.Structure):
                 ("tree_parent", _P * 2), ("tree_g", _P * 2), ("stop_poll", _P),
                 ("stop_ctx", _P), ("init_n", ctypes.c_int64 * 2), ("init_v", _P * 2),
                 ("init_a", _P * 2), ("init_parent", _P * 2), ("first_half", ctypes.c_int64),
-                ("extend_base", ctypes.c_int64), ("nn_index", ctypes.c_int64)]
+                ("extend_base", ctypes.c_int64)]
 
 # int (*stop_poll)(void *ctx, int local_stop, int found)
 StopPoll = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int)
@@ -114,7 +114,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
                      sampling=None, fragile_eps=None, adaptive=False, nn_stats=False,
                      max_halves=0, trees=False,
                      tree_capacity=1 << 18, stop_poll=None, init_trees=None, first_half=0,
-                     extend_base=0, nn_index=0):
+                     extend_base=0):
     """Plan start -> goal on terrain `data` (terrain_data.TerrainData).
 
     algorithm 0: batch-synchronous RRT-Connect, stops at the first solution;
@@ -148,11 +148,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
       [n][10], parent [n] (root first, -1; parents before children), the first
       half-iteration (its targets are the draws a search from the roots makes
       there) and the candidate stream's first extend index; max_halves then
-      counts the continuation's halves;
-    nn_index: algorithms 3 / 5 — the trees' spatial index of the nearest-vertex
-      search (GBP_OPT_NN_INDEX): 0 the default (rebuilt once max(4096, indexed
-      / 8) vertices were appended since), -1 none, >= 2 rebuilt every that many
-      (tests index small trees); results are the same either way."""
+      counts the continuation's halves."""
     L = load()
     x = np.ascontiguousarray(data.x, dtype=np.float64)
     y = np.ascontiguousarray(data.y, dtype=np.float64)
@@ -175,7 +171,6 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     p.nn_stats = int(bool(nn_stats))
     p.max_halves = int(max_halves)
     p.first_half, p.extend_base = int(first_half), int(extend_base)
-    p.nn_index = int(nn_index)
     warm = []
     if init_trees is not None:
         for k, t in enumerate(init_trees):

@@ -152,10 +152,6 @@ int gbp_terrain_info(const gbp_terrain *t, int *nx, int *ny, int *storage,
 /* 16, 17, 19: retired (round 4) — a Morton-sorted nearest-neighbour index, the
    packed fp32 VALU filter and a two-stream draw overlap, each measured no
    faster than the default path; setting them is an error     */
-#define GBP_OPT_NN_INDEX     19  /* the device planner loop's tree index (gbp_tree_index_build):
-                                    0 never, 1 (default) rebuilt when the vertices appended
-                                    since reach max(4096, indexed / 8), v >= 2: when they
-                                    reach v (tests index small trees) */
 #define GBP_OPT_NN_STATS     18  /* 1: the matrix-core search counts its fp64 re-checks
                                     in gbp_plan_status.stat_nn_* (diagnostics: costs
                                     same-address atomics; default 0)                  */
@@ -424,17 +420,6 @@ int gbp_tree_append_host(gbp_tree *tree, int64_t n, const double *states, const 
  * (n <= its max_batch). */
 int gbp_tree_nearest_dev(gbp_plan_ws *ws, gbp_tree *tree, int64_t n, const double *queries,
                          int32_t *index, gbp_stream stream);
-/* Spatial index of the tree for the device planner's nearest-vertex searches
- * (getNearestNeighbor, planner_class.cpp:185-200; same results, ties to the
- * lowest index): the first (count / 256) * 256 vertices sorted by a 64 x 64
- * grid over extent = {x0, x1, y0, y1} (Z order), with an 8-D box per 256.  A
- * search then sorts its queries the same way and lets each 32-query tile skip
- * the boxes farther than the distance of a vertex near every query of the tile
- * (exact: such boxes hold neither a nearest vertex nor a tie).  Vertices
- * appended later are searched in full until the next build; gbp_tree_reserve
- * drops the index.  Synchronous (reads the count). */
-int gbp_tree_index_build(gbp_tree *tree, const double *extent, gbp_stream stream);
-int gbp_tree_index_size(gbp_tree *tree, int64_t *indexed);  /* vertices indexed (0: none) */
 /* the tree's device arrays (for gbp_nearest_batch_dev and the like): READ ONLY —
  * vertices are written through init / append only, which also keep the fp16
  * rows and magnitude bounds the matrix-core search relies on */

@@ -671,7 +671,6 @@ typedef struct {
   const int32_t *init_parent[2];
   int64_t first_half;
   int64_t extend_base;
-  int64_t nn_index;       // GBP_OPT_NN_INDEX for the device loops (0: the default)
 } gbp_plan_params;
 
 typedef struct {

@@ -242,35 +242,3 @@ def test_append_past_capacity_is_reported_not_faulted(gpu):
     assert st["error"] & 2, (st["error"], st["done"], st["halt"])
     assert len(ta) <= 2 and len(tb) <= 2
     torch.cuda.synchronize()
-
-
-def test_indexed_tree_nearest_matches_scan(gpu):
-    """gbp_tree_nearest_dev on a tree with a spatial index (gbp_tree_index_build:
-    vertices sorted by bin, positions mapped back) equals the fp64 scan with
-    ties to the lowest index: exact duplicates, a dense cluster, a tail of
-    vertices appended after the build (scanned unindexed)."""
-    import ctypes
-    import global_body_planner_amd as gbp
-    data = td.synth_rough(256)
-    T = gbp.Terrain.from_data(data, device=0)
-    verts = T.sample_states(9000, seed=91, stream_id=1)[0].cpu().numpy()
-    verts[4000:4200] = verts[100:300]                       # ties to the lower index
-    verts[5000:6000, :2] = verts[5000:6000, :2] * 0.05 + 1.0   # a dense cluster
-    q = T.sample_states(3000, seed=92, stream_id=2)[0].cpu().numpy()
-    q = np.ascontiguousarray(np.concatenate([q, verts[[150, 4150, 5500, 8500]]]))
-    tree = gbp.DeviceTree(verts[0], device=0, capacity=verts.shape[0] + 1)
-    tree.append(verts[1:8000], np.zeros((7999, 10)), np.zeros(7999, np.int32))
-    ext = np.array([data.x[0], data.x[-1], data.y[0], data.y[-1]], np.float64)
-    lib = L.load()
-    assert lib.gbp_tree_index_build(tree._h, ext.ctypes.data, None) == 0
-    n = ctypes.c_int64(0)
-    assert lib.gbp_tree_index_size(tree._h, ctypes.byref(n)) == 0
-    assert n.value == 8000 // 256 * 256
-    tree.append(verts[8000:], np.zeros((1000, 10)), np.zeros(1000, np.int32))
-    assert lib.gbp_tree_index_size(tree._h, ctypes.byref(n)) == 0 and n.value == 7936
-    ws = gbp.PlanWorkspace(T, q.shape[0])
-    qt = torch.from_numpy(q).cuda()
-    got = ws.nearest(tree, qt).cpu().numpy()
-    ref = gbp.nearest(qt, torch.from_numpy(verts).cuda())[0].cpu().numpy()
-    bad = np.flatnonzero(got != ref)
-    assert bad.size == 0, (bad[:5], got[bad[:5]], ref[bad[:5]])

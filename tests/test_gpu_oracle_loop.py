@@ -172,29 +172,3 @@ def test_rrt_star_equals_oracle(gpu, name, xy, batch, seed, halves, algorithm, f
     print(f"{name} RRT* batch {batch} alg {algorithm}: {halves} halves, trees {len(ref['a']['v'])}+"
           f"{len(ref['b']['v'])}, {ref['rewires']} rewires, {ref['solutions']} connections, "
           f"{dev['fragile_resolved']} re-decided, halts {dev['halts']}")
-
-
-@pytest.mark.parametrize("name,xy,batch,seed,max_halves,sampling", [
-    ("synth-rough-256", (1.0, 2.55, 4.02, 2.55), 1024, 3, 300, None),
-    ("synth-rough-256", (1.0, 2.55, 4.02, 2.55), 4096, 3, 0, DIR_ON),
-    ("slope-gridmap", (1.0, 0.0, 8.0, 0.0), 256, 7, 0, None),
-])
-def test_planner_loop_indexed_equals_oracle(gpu, name, xy, batch, seed, max_halves, sampling):
-    """The device loop with the trees' spatial index rebuilt every 256 new
-    vertices (gbp_tree_index_build; the targets' search on bin-sorted queries
-    skipping superunits, the connects' search through the position map)
-    against orc_plan: the same trees bit for bit (the index changes which
-    rows are scored, never the nearest vertex or its tie-break)."""
-    from global_body_planner_amd import _lib as L
-    data, O, start, goal = _setup(name, xy)
-    kw = dict(batch=batch, max_time=300.0, seed=seed, max_halves=max_halves, trees=True)
-    if sampling is not None:
-        kw["sampling"] = L.sampling(**sampling)
-    dev = planner.plan_rrt_connect(data, start, goal, algorithm=3, nn_index=256, **kw)
-    ref = O.plan(start, goal, batch=batch, seed=seed, max_halves=max_halves, sampling=sampling)
-    assert dev["found"] == ref["found"]
-    assert_counters_equal(dev, ref)
-    assert_trees_equal(dev, ref)
-    assert max(len(ref["a"]["v"]), len(ref["b"]["v"])) >= 256   # an index was built
-    if ref["found"]:
-        assert (dev["meet_a"], dev["meet_b"]) == (ref["meet_a"], ref["meet_b"])

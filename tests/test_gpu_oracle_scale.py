@@ -65,18 +65,14 @@ def _compare(dev, ref):
         assert dev["reported_length"] == ref["path_length"]
 
 
-@pytest.mark.parametrize("nn_index", [0, 256])
-def test_config3_scale_from_roots(gpu, nn_index):
+def test_config3_scale_from_roots(gpu):
     """The bench's "before the wall" pair ((1.0, 10.23) -> (6.8, 10.23)) at
     92,749 draws per half from the roots to its first solution: draw-ahead
-    and the folded commit at full batch, the meet inside a group of halves;
-    with nn_index = 256 the trees' spatial index is rebuilt every 256 new
-    vertices (the targets' search sorted by bin, superunits skipped)."""
+    and the folded commit at full batch, the meet inside a group of halves."""
     data, O = _terrain()
     start, goal = _start_goal(O, 1.0, 10.23, 6.8, 10.23)
     dev = planner.plan_rrt_connect(data, start, goal, algorithm=3, batch=DRAWS, max_time=300.0,
-                                   seed=20251018, trees=True, tree_capacity=1 << 17,
-                                   nn_index=nn_index)
+                                   seed=20251018, trees=True, tree_capacity=1 << 17)
     ref = O.plan(start, goal, batch=DRAWS, seed=20251018, capacity=1 << 17, nthreads=NTHREADS)
     print(f"from the roots: found {ref['found']} at half {ref['meet_half']}, trees "
           f"{len(ref['a']['v'])}+{len(ref['b']['v'])}, {ref['targets']} targets, "
@@ -93,8 +89,7 @@ GROW_HALVES = 20000
 CONT_HALVES = 40
 
 
-@pytest.mark.parametrize("nn_index", [0, -1])
-def test_config3_scale_warm_continuation(gpu, nn_index):
+def test_config3_scale_warm_continuation(gpu):
     """SURVEY's pair ((1.0, 10.23) -> (19.42, 10.23)): the trees the device
     grows in GROW_HALVES half-iterations, then CONT_HALVES more at 92,749
     draws each from the device and from orc_plan, bit for bit — the targets'
@@ -114,12 +109,9 @@ def test_config3_scale_warm_continuation(gpu, nn_index):
     n0 = (len(init[0]["v"]), len(init[1]["v"]))
     assert max(n0) > 10000, n0
     warm = dict(batch=DRAWS, seed=20251018, max_halves=CONT_HALVES)
-    # nn_index 0: the warm trees are indexed at once (the searches skip
-    # superunits); -1: the plain matrix-core search
     dev = planner.plan_rrt_connect(data, start, goal, algorithm=3, max_time=300.0, trees=True,
                                    tree_capacity=cap, nn_stats=True, init_trees=init,
-                                   first_half=GROW_HALVES, extend_base=grown["extends"],
-                                   nn_index=nn_index, **warm)
+                                   first_half=GROW_HALVES, extend_base=grown["extends"], **warm)
     t0 = time.time()
     ref = O.plan(start, goal, capacity=cap, nthreads=NTHREADS, init_trees=init,
                  first_half=GROW_HALVES, extend_base=grown["extends"], **warm)
