@@ -83,6 +83,15 @@ struct gbp_tree {
   int32_t *count = nullptr;   // [1] number of vertices (device resident)
 };
 
+// the look-ahead search's device state (gbp_plan_ws::la), by half % 3 (the
+// drawn-ahead target sets) and by parity (the searched trees' snapshots)
+struct gbp_plan_la {
+  int32_t nt[3];     // valid targets drawn for the half (ordered_rank's total)
+  uint32_t frag[3];  // half + 1 when one of its draws was FRAGILE
+  int32_t nv[2];     // the searched tree's vertex count when its search was launched
+  uint32_t go[2];    // 0: the sequence had stopped when the search was launched (it idles)
+};
+
 struct gbp_plan_ws {
   int device = 0;
   int num_cus = 256;
@@ -94,22 +103,26 @@ struct gbp_plan_ws {
   int nn_stats = 0;            // GBP_OPT_NN_STATS: k_nn_hreduce counts its re-checks in the status
   int nn_items = 4096;         // matrix-core search: work items (= waves) per launch
   int64_t ntiles = 0;
-  // stage 0-1: two sets, by the half's parity (a half's targets are drawn
-  // while the previous half still reads its own); cand..tqh point at the set
-  // of the half being enqueued or resolved (select_targets)
+  // stage 0-1: three sets, by half % 3 (with the look-ahead search, half
+  // h + 2's targets are drawn while half h + 1's are searched and half h
+  // still reads its own); cand..tqh point at the set of the half being
+  // enqueued or resolved (select_targets)
   struct TargetSet {
     double *cand, *targets;
     uint32_t *cflag;
     _Float16 *tqh;
-  } tset[2] = {};
+  } tset[3] = {};
   double *cand = nullptr;      // [bmax][8] drawn states
   uint32_t *cflag = nullptr;   // [bmax] their isValidState flags
   double *targets = nullptr;   // [bmax][8] the valid ones, in draw order
   _Float16 *tqh = nullptr;     // [bmax][NH_ROW] their fp16 rows (k_nn_mfma's queries)
-  // stage 2-3
+  // stage 2-3; nn, cs and ca in two sets by the half's parity (the
+  // look-ahead search of half h + 1 writes its own while half h reads)
   int32_t *nn = nullptr;       // [bmax] nearest vertex of T per target
   double *cs = nullptr;        // [6 bmax][8] candidate s_near
   double *ca = nullptr;        // [6 bmax][10] candidate actions
+  int32_t *nnp[2] = {};
+  double *csp[2] = {}, *cap[2] = {};
   double *csn = nullptr;       // [6 bmax][8] candidate s_new
   uint32_t *cf = nullptr;      // [6 bmax] candidate flags
   uint32_t *cc = nullptr;      // [6 bmax] candidate counts
@@ -126,8 +139,16 @@ struct gbp_plan_ws {
   double *kan = nullptr;       // [bmax][10]
   uint32_t *kf = nullptr;      // [bmax] connect flags
   // nearest-neighbour partials: NN_MAX_CHUNKS * bmax slots, pd[c * nq + qi]
-  double *nn_d = nullptr;
-  int32_t *nn_i = nullptr;
+  // (nn_d2 / nn_i2: the look-ahead search's, on its own stream)
+  double *nn_d = nullptr, *nn_d2 = nullptr;
+  int32_t *nn_i = nullptr, *nn_i2 = nullptr;
+  // the look-ahead search (gbp_plan_halves_dev): half h + 1's targets drawn
+  // and searched on la_stream while half h's extends, connects and appends
+  // run on the caller's stream (la_go: main -> side, la_done: side -> main)
+  gbp_plan_la *la = nullptr;   // device: counts, snapshots, flags
+  unsigned long long *la_tiles = nullptr;  // look-back tiles of the drawn-ahead targets
+  hipStream_t la_stream = nullptr;
+  hipEvent_t la_go = nullptr, la_done = nullptr;
   void *block = nullptr;       // the one allocation all of the above live in
   // RRT*-Connect (gbp_plan_star_config; star = 0: RRT-Connect): stages 6-7
   int star = 0;
@@ -502,11 +523,13 @@ __device__ __forceinline__ void nh_sweep(const _Float16 *__restrict__ vh, int c0
 // launch of their own after the search (k_extend_prep); the reduce then
 // copies s_near into the candidates (k_nn_hreduce cs).
 // The next half's targets, drawn ahead in the same launch (draw_blocks > 0;
-// gbp_plan_halves_dev, sampling not direction-biased): blocks
-// [0, draw_blocks) draw them into the next half's target set and rank them
-// (ordered_rank over those blocks: their count in status.pre_targets; a
-// FRAGILE draw sets status.pre_fragile = next half + 1).  They come first in
-// the grid so that their latency-bound work overlaps the matrix-core waves.
+// gbp_plan_halves_dev, sampling not direction-biased: an inline search draws
+// the next half's, the look-ahead search of half h + 1 those of half h + 2):
+// blocks [0, draw_blocks) draw them into that half's target set and rank them
+// (ordered_rank over those blocks on the look-ahead tiles: their count in
+// gbp_plan_la::nt; a FRAGILE draw sets gbp_plan_la::frag = half + 1, and the
+// half halts at its start in k_la_commit).  They come first in the grid so
+// that their latency-bound work overlaps the matrix-core waves.
 struct NhDraw {
   int draw_blocks;
   int32_t half;  // the half the draws are for
@@ -517,6 +540,13 @@ struct NhDraw {
   _Float16 *tqh;
   unsigned long long *tiles;
   uint32_t epoch;
+  int32_t *count;   // the valid draws' total (gbp_plan_la::nt of the half)
+  uint32_t *frag;   // set to half + 1 on a FRAGILE draw (gbp_plan_la::frag)
+  // an inline search launching the look-ahead one: the next search's tree
+  // snapshot and whether the sequence still runs (gbp_plan_la::nv / go)
+  const int32_t *snap_src;
+  int32_t *snap_dst;
+  uint32_t *go_dst;
 };
 template <class ZT>
 struct NhPrep {
@@ -527,6 +557,10 @@ struct NhPrep {
   int direction;
   int first_block;  // blocks [first_block, gridDim.x) draw the actions
   NhDraw dr;        // blocks [0, dr.draw_blocks): the next half's targets
+  // the look-ahead search (nt set): the half's count is *nt (its drawn-ahead
+  // total), its extend base the counter after the current half's commit
+  // (commit_targets), and n_validate is left to k_la_commit
+  const int32_t *nt;
 };
 
 template <int NT, class ZT, bool PREP>
@@ -539,11 +573,17 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
                                                    const float *__restrict__ hm,
                                                    const int32_t *__restrict__ nv_dev, int64_t bmax,
                                                    float4 *__restrict__ pm, int4 *__restrict__ pid,
-                                                   uint64_t seq, int n_items, NhPrep<ZT> pp) {
+                                                   uint64_t seq, int n_items, NhPrep<ZT> pp,
+                                                   const uint32_t *__restrict__ go) {
+  if (PREP && pp.dr.snap_dst && blockIdx.x == 0 && threadIdx.x == 0) {
+    *pp.dr.snap_dst = *pp.dr.snap_src;
+    *pp.dr.go_dst = gated(st, seq) ? 0u : 1u;
+  }
   if (gated(st, seq)) {
-    if (PREP && blockIdx.x == pp.first_block && threadIdx.x == 0) st->n_validate = 0;
+    if (PREP && !pp.nt && blockIdx.x == pp.first_block && threadIdx.x == 0) st->n_validate = 0;
     return;
   }
+  if (go && *go == 0u) return;  // a look-ahead search launched after the sequence stopped
   // the next half's targets (k_targets' work); float heights only: with fp64
   // heights the state check's registers would cost the search an occupancy step
   if constexpr (PREP && std::is_same_v<ZT, float>) if ((int)blockIdx.x < pp.dr.draw_blocks) {
@@ -562,8 +602,8 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
       d.cflag[i] = f;
     }
     const bool keep = f & GBP_F_VALID;
-    if (__ballot(f & GBP_F_FRAGILE) && (threadIdx.x & (WAVE - 1)) == 0) st->pre_fragile = d.half + 1;
-    const uint32_t r = ordered_rank(keep, d.tiles, d.epoch, &st->pre_targets, st, blockIdx.x,
+    if (__ballot(f & GBP_F_FRAGILE) && (threadIdx.x & (WAVE - 1)) == 0) *d.frag = (uint32_t)d.half + 1;
+    const uint32_t r = ordered_rank(keep, d.tiles, d.epoch, d.count, st, blockIdx.x,
                                     (uint32_t)d.draw_blocks);
     if (keep) {
       copy8(d.targets + 8 * (size_t)r, q);
@@ -572,8 +612,9 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
     return;
   }
   if (PREP && (int)blockIdx.x >= pp.first_block) {  // the extends' candidate actions
-    const int64_t n = st->n_targets, m = n * GBP_NUM_GEN_STATES, base = st->ext_base;
-    if (blockIdx.x == pp.first_block && threadIdx.x == 0) st->n_validate = (int32_t)m;
+    const int64_t n = pp.nt ? *pp.nt : st->n_targets, m = n * GBP_NUM_GEN_STATES;
+    const int64_t base = pp.nt ? st->ext_counter : st->ext_base;
+    if (!pp.nt && blockIdx.x == pp.first_block && threadIdx.x == 0) st->n_validate = (int32_t)m;
     for (int64_t c = (blockIdx.x - pp.first_block) * (int64_t)NH_TB + threadIdx.x; c < m;
          c += (int64_t)(gridDim.x - pp.first_block) * NH_TB) {
       const int64_t i = c / GBP_NUM_GEN_STATES;
@@ -672,8 +713,10 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
                                                        int64_t bmax, const float4 *__restrict__ pm,
                                                        const int4 *__restrict__ pid,
                                                        int32_t *__restrict__ out, uint64_t seq,
-                                                       int stats, double *__restrict__ cs, int n_items) {
+                                                       int stats, double *__restrict__ cs, int n_items,
+                                                       const uint32_t *__restrict__ go) {
   if (gated(st, seq)) return;
+  if (go && *go == 0u) return;  // (k_nn_mfma)
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   int64_t nqg, nseg, cps, nch;
   nh_geometry(nq, nv, bmax, n_items, nqg, nseg, cps, nch);
@@ -934,22 +977,69 @@ __global__ __launch_bounds__(CB) void k_compact_targets(gbp_plan_status *st, int
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) commit_targets(st, half, resumed != 0);
 }
 
-// stages 0-1 of a half whose targets were drawn ahead (NhDraw), run by the
-// last workgroup to finish the previous half's final launch (k_append mode 1)
-// unless that half found its connection, halted or failed: the count and the
-// counters, and the FRAGILE halt at this half's start — what k_targets' last
-// workgroup and its FRAGILE wave would have done
-__device__ void commit_pre(gbp_plan_status *st, int32_t half, uint64_t seq) {
-  const auto ld = [](const uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  if (ld(&st->done) || ld(&st->halt) || ld(&st->error)) return;
-  st->n_targets = st->pre_targets;
-  commit_targets(st, half, false);
-  if (st->pre_fragile == half + 1) {
-    atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_TARGETS);
-    st->halt_half = half;
-    raise_gate(st, seq);
+// stages 0-1 of a half whose targets were drawn ahead and searched by the
+// look-ahead search (gbp_plan_halves_dev), the half's first launch on the
+// caller's stream: the count and the counters, the FRAGILE halt at the half's
+// start (what k_targets' last workgroup and its FRAGILE wave would have done),
+// n_validate; then the search's answer completed: it saw T's first
+// la->nv[half & 1] vertices (the count when it was launched), so every
+// target compares its nearest with the vertices appended since (the previous
+// half's connections) in fp64 — a later vertex wins only when strictly closer,
+// as its index is higher (planner_class.cpp:185-200) — and rewrites its
+// candidates' s_near.  Block 0 also records the next look-ahead search's
+// snapshot of O (the tree the next half extends: unchanged until this half's
+// connects) and whether it should run.
+__global__ __launch_bounds__(TB) void k_la_commit(gbp_plan_status *st, gbp_plan_la *la, int32_t half,
+                                                  const double *__restrict__ targets,
+                                                  const double *__restrict__ tv,
+                                                  const int32_t *__restrict__ tcount,
+                                                  int32_t *__restrict__ nn, double *__restrict__ cs,
+                                                  const int32_t *__restrict__ ocount, uint64_t seq) {
+  const int slot = half % 3, p = half & 1;
+  const bool g = gated(st, seq);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    la->nv[p ^ 1] = *ocount;
+    bool go = !g;
+    if (g) {
+      st->n_validate = 0;  // the validate launch idles
+    } else {
+      const int32_t n = la->nt[slot];
+      st->n_targets = n;
+      commit_targets(st, half, false);
+      const bool frag = la->frag[slot] == (uint32_t)half + 1;
+      la->frag[slot] = 0;
+      if (frag) {  // the targets stage halts
+        atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_TARGETS);
+        st->halt_half = half;
+        raise_gate(st, seq);
+        go = false;
+      }
+      st->n_validate = frag ? 0 : n * GBP_NUM_GEN_STATES;
+    }
+    la->go[p ^ 1] = go ? 1u : 0u;
+  }
+  if (g) return;
+  const int64_t n = la->nt[slot], v0 = la->nv[p], v1 = *tcount;
+  if (v1 <= v0) return;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double q[8];
+    copy8(q, targets + 8 * i);
+    const int32_t j0 = nn[i];
+    int32_t bi = j0;
+    double best = nn_dist64(q, tv + 8 * (int64_t)j0);
+    for (int64_t j = v0; j < v1; j++) {
+      const double d = nn_dist64(q, tv + 8 * j);
+      if (d < best) {
+        best = d;
+        bi = (int32_t)j;
+      }
+    }
+    if (bi != j0) {
+      nn[i] = bi;
+      for (int k = 0; k < GBP_NUM_GEN_STATES; k++)
+        copy8(cs + 8 * (i * GBP_NUM_GEN_STATES + k), tv + 8 * (int64_t)bi);
+    }
   }
 }
 
@@ -1071,7 +1161,7 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
                                                int32_t *__restrict__ tp, int32_t *__restrict__ tcount,
                                                int32_t *__restrict__ vtx, unsigned long long *tiles,
                                                uint32_t epoch, int32_t half, int64_t cap,
-                                               uint64_t seq, int32_t commit_half, int32_t *tch,
+                                               uint64_t seq, int32_t *tch,
                                                int32_t *tsib, int star) {
   if (gated(st, seq)) return;
   __shared__ int32_t s_base;
@@ -1085,13 +1175,11 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
   const bool keep = live && r != GBP_TRAPPED;
   int32_t *total = mode == 0 ? &st->n_added : &st->n_conn_added;
   const uint32_t rank = ordered_rank(keep, tiles, epoch, total, st);
-  bool raised = false;  // this thread set done / error (fenced before the commit below)
   if (keep && (int64_t)base + rank >= cap) {
     // the caller reserved too little: drop, report, and gate every later
     // launch (a search over rows past cap would read out of bounds)
     atomicOr(&st->error, 2u);
     raise_gate(st, seq);
-    raised = true;
     if (vtx) vtx[i] = -1;
   } else if (keep) {
     const int32_t idx = base + (int32_t)rank, p = par[i];
@@ -1114,7 +1202,6 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
       st->meet_half = half;
       atomicOr(&st->done, 1u);
       raise_gate(st, seq);
-      raised = true;
     }
   } else if (live && vtx) {
     vtx[i] = -1;
@@ -1129,24 +1216,6 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
       st->stat_added += added;
     } else {
       st->stat_conn_added += added;
-    }
-  }
-  if (commit_half >= 0) {  // the next half's targets were drawn ahead: commit them
-    // the done / error / meet atomics above must be complete (at agent scope)
-    // before this workgroup counts itself finished, or the last workgroup's
-    // commit_pre could miss a REACHED or a capacity error raised by another
-    // wave of this launch.  Only the raising threads fence: a
-    // fence in every thread cost the launch 10 -> 30 us (r05f breakdown)
-    if (raised) __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __threadfence();
-      uint32_t *fin = &st->commit_fin;  // workgroups finished (reset by the last)
-      if (atomicAdd(fin, 1u) == gridDim.x - 1) {
-        __threadfence();
-        *fin = 0;
-        commit_pre(st, commit_half, seq);
-      }
     }
   }
 }
@@ -1801,7 +1870,8 @@ __global__ void k_tree_append(gbp_tree t, int64_t n, const double *__restrict__ 
   *t.count = c;
 }
 
-__global__ void k_plan_reset(gbp_plan_status *st, int64_t ext_counter) {
+__global__ void k_plan_reset(gbp_plan_status *st, int64_t ext_counter, gbp_plan_la *la) {
+  *la = gbp_plan_la{};  // no drawn-ahead targets, empty snapshots
   gbp_plan_status z;
   memset(&z, 0, sizeof z);
   z.meet = ~0ull;
@@ -1864,11 +1934,14 @@ bool tree_ok(const gbp_tree *t) { return t && t->v && t->count; }
 
 // the target set of half `half` (its parity)
 void select_targets(gbp_plan_ws *w, int32_t half) {
-  const auto &ts = w->tset[half & 1];
+  const auto &ts = w->tset[half % 3];
   w->cand = ts.cand;
   w->cflag = ts.cflag;
   w->targets = ts.targets;
   w->tqh = ts.tqh;
+  w->nn = w->nnp[half & 1];
+  w->cs = w->csp[half & 1];
+  w->ca = w->cap[half & 1];
 }
 
 uint32_t next_epoch(gbp_plan_ws *w) {
@@ -1880,40 +1953,103 @@ unsigned tiles_for(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + CB - 
 
 // qh: the queries' fp16 rows (nn_put_hrow layout, same offsets as q), or
 // null (converted in the search); prep: the extends' candidates are drawn
-// inside the search (returns *prepped)
+// inside the search (returns *prepped); side: the look-ahead search's launch
+// (its own partial slots, never gated, the tree's snapshot count)
+struct NnSide {
+  const int32_t *nv;   // the searched tree's vertex count at the snapshot
+  const uint32_t *go;  // 0: idle
+};
 template <class ZT = float>
 int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
               const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s,
               const _Float16 *qh = nullptr, const NhPrep<ZT> *prep = nullptr,
-              double *cs = nullptr, bool *prepped = nullptr) {
+              double *cs = nullptr, bool *prepped = nullptr, const NnSide *side = nullptr) {
   if (prepped) *prepped = false;
   const int gm = w->nn_items / (NH_TB / WAVE);  // the search's workgroups: one wave per item
+  float4 *pm = (float4 *)(side ? w->nn_d2 : w->nn_d);
+  int4 *pid = (int4 *)(side ? w->nn_i2 : w->nn_i);
+  const int32_t *nv = side ? side->nv : tr->count;
+  const uint32_t *go = side ? side->go : nullptr;
   if (prep) {
     NhPrep<ZT> pp = *prep;
     const int gd = pp.dr.draw_blocks;
     pp.first_block = gd + gm;
     const int gp = (int)grid_for(GBP_NUM_GEN_STATES * w->bmax, NH_TB, num_cus * 4);
     hipLaunchKernelGGL((k_nn_mfma<NH_NT, ZT, true>), dim3(gd + gm + gp), dim3(NH_TB), 0, s, w->st,
-                       nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
-                       (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, w->nn_items, pp);
+                       nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, nv, w->bmax, pm, pid,
+                       side ? 0 : ++w->seq, w->nn_items, pp, go);
     if (prepped) *prepped = true;
   } else {
     hipLaunchKernelGGL((k_nn_mfma<NH_NT, float, false>), dim3(gm), dim3(NH_TB), 0, s, w->st,
-                       nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, tr->count, w->bmax,
-                       (float4 *)w->nn_d, (int4 *)w->nn_i, ++w->seq, w->nn_items, NhPrep<float>{});
+                       nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, nv, w->bmax, pm, pid,
+                       side ? 0 : ++w->seq, w->nn_items, NhPrep<float>{}, go);
   }
   hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(NH_G * w->bmax, NH_RTB, num_cus * 8)), dim3(NH_RTB),
-                     0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, tr->count, w->bmax,
-                     (const float4 *)w->nn_d, (const int4 *)w->nn_i, out, ++w->seq, w->nn_stats,
-                     prep ? cs : nullptr, w->nn_items);
+                     0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, nv, w->bmax,
+                     (const float4 *)pm, (const int4 *)pid, out, side ? 0 : ++w->seq, w->nn_stats,
+                     prep ? cs : nullptr, w->nn_items, go);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
+}
+
+// the look-ahead search of gbp_plan_halves_dev (targets not direction-biased,
+// float heights, RRT-Connect): half h + 1's targets are drawn ahead (by half
+// h's own search launch, or by half h's look-ahead search) and searched in
+// O — the tree half h + 1 extends, unchanged until half h's connects — on
+// la_stream while half h validates, selects, appends and connects on the
+// caller's stream; half h + 1 then starts with k_la_commit (the commit and
+// the vertices O gained since).  Same draws, ranks, nearest vertices and
+// counters as the inline sequence.
+struct LaHalf {
+  bool searched = false;     // this half's targets and search came from the look-ahead
+  bool launch_next = false;  // launch half + 1's look-ahead search
+  bool draw_after = false;   // ... which draws half + 2's targets
+  uint64_t stream_a = 0, stream_b = 0;  // the halves' target streams
+};
+
+// the targets of half h drawn ahead into their set (la->nt / frag count them)
+NhDraw la_draw(gbp_plan_ws *w, int32_t h, int64_t batch, const LaHalf &L) {
+  NhDraw d{};
+  const auto &set = w->tset[h % 3];
+  d.half = h;
+  d.n = batch;
+  d.base = (int64_t)(h >> 1) * batch;
+  d.stream = (h & 1) ? L.stream_b : L.stream_a;
+  d.cand = set.cand;
+  d.targets = set.targets;
+  d.cflag = set.cflag;
+  d.tqh = set.tqh;
+  d.draw_blocks = (int)((batch + NH_TB - 1) / NH_TB);
+  d.tiles = w->la_tiles;
+  d.epoch = next_epoch(w);
+  d.count = &w->la->nt[h % 3];
+  d.frag = &w->la->frag[h % 3];
+  return d;
+}
+
+// enqueue half h1's look-ahead search on la_stream after everything the
+// caller's stream holds so far; X: the tree h1 extends
+int la_launch(gbp_terrain *t, gbp_plan_ws *w, const gbp_tree *X, int32_t h1, int64_t batch,
+              uint64_t seed, const LaHalf &L, hipStream_t s) {
+  HIPCHK_P(hipEventRecord(w->la_go, s));
+  HIPCHK_P(hipStreamWaitEvent(w->la_stream, w->la_go, 0));
+  const int slot = h1 % 3, p = h1 & 1;
+  const auto &set = w->tset[slot];
+  NhPrep<float> prep{view<float>(t), seed, w->cap[p], t->sampling,
+                     (h1 & 1) ? GBP_REVERSE : GBP_FORWARD, 0, NhDraw{}, &w->la->nt[slot]};
+  if (L.draw_after) prep.dr = la_draw(w, h1 + 1, batch, L);
+  const NnSide side{&w->la->nv[p], &w->la->go[p]};
+  int rc = nn_launch<float>(w, &w->la->nt[slot], set.targets, nullptr, X, w->nnp[p], t->num_cus,
+                            w->la_stream, set.tqh, &prep, w->csp[p], nullptr, &side);
+  if (rc) return rc;
+  HIPCHK_P(hipEventRecord(w->la_done, w->la_stream));
+  return GBP_OK;
 }
 
 template <class ZT>
 int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int32_t half,
                    int direction, int64_t batch, uint64_t seed, uint64_t target_stream,
                    int64_t target_base, int adaptive, int first_stage, int last_stage,
-                   hipStream_t s, bool predrawn = false, const NhDraw *next = nullptr) {
+                   hipStream_t s, const LaHalf *la = nullptr) {
   const TerrainView<ZT> V = view<ZT>(t);
   const int cus = t->num_cus;
   gbp_plan_status *st = w->st;
@@ -1923,9 +2059,19 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   // the extends' append and the connects
   auto ord = [](int x) { return x == 6 ? 31 : x == 7 ? 32 : 10 * x; };
   auto run = [&](int x) { return ord(first_stage) <= ord(x) && ord(x) <= ord(last_stage); };
-  // predrawn: the previous half's search drew this half's targets and its
-  // last launch committed them (commit_pre)
-  if (!predrawn && run(0) && run(1))  // a fresh half: draws + compaction, one launch
+  const bool searched = la && la->searched;  // stages 0-2's draws and search done ahead
+  if (searched && first_stage != 0) return GBP_E_INVALID_ARG;
+  if (searched && (!std::is_same_v<ZT, float> || t->sampling.state_flag || t->sampling.action_flag))
+    return GBP_E_INVALID_ARG;
+  if (searched) {
+    HIPCHK_P(hipStreamWaitEvent(s, w->la_done, 0));
+    hipLaunchKernelGGL(k_la_commit, dim3(grid_for(batch, TB, cus * 4)), dim3(TB), 0, s, st, w->la, half,
+                       w->targets, T->v, T->count, w->nn, w->cs, O->count, ++w->seq);
+    if (la->launch_next) {
+      const int rc = la_launch(t, w, O, half + 1, batch, seed, *la, s);
+      if (rc) return rc;
+    }
+  } else if (run(0) && run(1))  // a fresh half: draws + compaction, one launch
     hipLaunchKernelGGL(k_targets<ZT>, dim3((unsigned)((batch + TB - 1) / TB)), dim3(TB), 0, s, V,
                        st, batch, seed, target_stream, target_base, w->cand, w->cflag, w->targets,
                        w->tqh, w->tiles, next_epoch(w), half, ++w->seq, t->sampling, T->v, T->count,
@@ -1937,19 +2083,25 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   if (run(2)) {
     // the candidates' actions inside the search unless they are direction-biased
     // (then they depend on s_near: k_extend_prep after the search)
-    NhPrep<ZT> prep{V, seed, w->ca, t->sampling, direction, 0, NhDraw{}};
+    NhPrep<ZT> prep{V, seed, w->ca, t->sampling, direction, 0, NhDraw{}, nullptr};
     const bool early = !t->sampling.action_flag;
-    if (early && next) {
-      // the drawn-ahead targets are sampled with s_from / s_to unset
-      if (t->sampling.state_flag) return GBP_E_INVALID_ARG;
-      prep.dr = *next;
-      prep.dr.draw_blocks = (int)((next->n + NH_TB - 1) / NH_TB);
-      prep.dr.tiles = w->tiles;
-      prep.dr.epoch = next_epoch(w);
+    const bool launch = !searched && la && la->launch_next;
+    if (launch) {
+      // the next half's targets drawn beside this search (never direction-biased:
+      // s_from / s_to unset) and O's snapshot for its look-ahead search
+      if (!early || t->sampling.state_flag || !O || !std::is_same_v<ZT, float>)
+        return GBP_E_INVALID_ARG;
+      prep.dr = la_draw(w, half + 1, batch, *la);
+      prep.dr.snap_src = O->count;
+      prep.dr.snap_dst = &w->la->nv[(half + 1) & 1];
+      prep.dr.go_dst = &w->la->go[(half + 1) & 1];
     }
-    bool prepped = false;
-    int rc = nn_launch<ZT>(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, w->tqh,
-                           early ? &prep : nullptr, w->cs, &prepped);
+    bool prepped = searched;
+    int rc = GBP_OK;
+    if (!searched)
+      rc = nn_launch<ZT>(w, &st->n_targets, w->targets, nullptr, T, w->nn, cus, s, w->tqh,
+                         early ? &prep : nullptr, w->cs, &prepped);
+    if (!rc && launch) rc = la_launch(t, w, O, half + 1, batch, seed, *la, s);
     if (rc) return rc;
     const int64_t mmax = batch * GBP_NUM_GEN_STATES;
     if (!prepped)
@@ -1967,7 +2119,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 0, w->eres, w->nn,
                        w->esn, w->ean, T->v, T->vh, T->hm, T->a, T->g, T->parent, T->count, w->evtx,
                        w->tiles,
-                       next_epoch(w), half, T->cap, ++w->seq, -1, T->child, T->sibling, w->star);
+                       next_epoch(w), half, T->cap, ++w->seq, T->child, T->sibling, w->star);
   if (w->star && run(6)) {
     // RRT* insertion, stage 6: neighbourhoods, connect checks, their pair checks
     const unsigned gk = (unsigned)std::max<int64_t>(1, std::min<int64_t>(batch, cus * 8));
@@ -2013,7 +2165,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 1, w->kres, w->nno,
                        w->ksn, w->kan, O->v, O->vh, O->hm, O->a, O->g, O->parent, O->count,
                        w->star ? w->kvtx : nullptr, w->tiles, next_epoch(w), half, O->cap, ++w->seq,
-                       next ? next->half : -1, O->child, O->sibling, w->star);
+                       O->child, O->sibling, w->star);
     if (w->star) {  // the REACHED connections kept; after Tb's half the best one ranked
       const bool t_is_a = direction == GBP_FORWARD;
       hipLaunchKernelGGL(k_star_shared, dim3(1), dim3(RB), 0, s, st, w->kres, w->kvtx, t_is_a ? 1 : 0,
@@ -2258,6 +2410,15 @@ int gbp_tree_device_ptrs(gbp_tree *t, double **states, int32_t **count) {
   return GBP_OK;
 }
 
+static void ws_free(gbp_plan_ws *w) {
+  if (w->la_go) (void)hipEventDestroy(w->la_go);
+  if (w->la_done) (void)hipEventDestroy(w->la_done);
+  if (w->la_stream) (void)hipStreamDestroy(w->la_stream);
+  if (w->block) (void)hipFree(w->block);
+  if (w->star_block) (void)hipFree(w->star_block);
+  delete w;
+}
+
 int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   if (!t || !out) return GBP_E_INVALID_ARG;
   if (max_batch < 1 || max_batch > (1 << 24)) return GBP_E_INVALID_ARG;
@@ -2274,9 +2435,9 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->nn_items = NH_ITEMS;
   w->ntiles = (max_batch + TB - 1) / TB + 1;  // k_targets' 256-draw tiles (k_compact_targets: 1024)
   const int64_t b = max_batch, m = GBP_NUM_GEN_STATES * max_batch;
-  const size_t bytes = sizeof(gbp_plan_status) + 8 * w->ntiles + 2 * (64 * b + 4 * b + 64 * b + 64 * b) + 1024 +
-                       m * (64 + 80 + 64 + 4 + 4) + b * (4 + 4 + 64 + 80 + 4 + 4) +
-                       b * (4 + 4 + 64 + 80 + 4) + NN_MAX_CHUNKS * b * (16 + 16) + 64 * b + 256 +
+  const size_t bytes = sizeof(gbp_plan_status) + 16 * w->ntiles + 3 * (64 * b + 4 * b + 64 * b + 64 * b) +
+                       1024 + m * (2 * 64 + 2 * 80 + 64 + 4 + 4) + b * (2 * 4 + 4 + 64 + 80 + 4 + 4) +
+                       b * (4 + 4 + 64 + 80 + 4) + 2 * NN_MAX_CHUNKS * b * (16 + 16) + 64 * b + 512 +
                        64 * 256;
   if (hipMalloc(&w->block, bytes) != hipSuccess) {
     delete w;
@@ -2284,17 +2445,21 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   }
   char *p = (char *)w->block;
   w->st = carve<gbp_plan_status>(p, 1);
+  w->la = carve<gbp_plan_la>(p, 1);
   w->tiles = carve<unsigned long long>(p, w->ntiles);
+  w->la_tiles = carve<unsigned long long>(p, w->ntiles);
   for (auto &ts : w->tset) {
     ts.cand = carve<double>(p, 8 * b);
     ts.cflag = carve<uint32_t>(p, b);
     ts.targets = carve<double>(p, 8 * b);
     ts.tqh = carve<_Float16>(p, 32 * b);
   }
+  for (int k = 0; k < 2; k++) {
+    w->nnp[k] = carve<int32_t>(p, b);
+    w->csp[k] = carve<double>(p, 8 * m);
+    w->cap[k] = carve<double>(p, 10 * m);
+  }
   select_targets(w, 0);
-  w->nn = carve<int32_t>(p, b);
-  w->cs = carve<double>(p, 8 * m);
-  w->ca = carve<double>(p, 10 * m);
   w->csn = carve<double>(p, 8 * m);
   w->cf = carve<uint32_t>(p, m);
   w->cc = carve<uint32_t>(p, m);
@@ -2311,15 +2476,24 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->kf = carve<uint32_t>(p, b);
   w->nn_d = carve<double>(p, 2 * NN_MAX_CHUNKS * b);   // k_nn_mfma: float4 per slot
   w->nn_i = carve<int32_t>(p, 4 * NN_MAX_CHUNKS * b);  // k_nn_mfma: int4 per slot
-  if ((size_t)(p - (char *)w->block) > bytes || hipMemset(w->tiles, 0, 8 * w->ntiles) != hipSuccess) {
-    (void)hipFree(w->block);
-    delete w;
-    return GBP_E_HIP;
+  w->nn_d2 = carve<double>(p, 2 * NN_MAX_CHUNKS * b);
+  w->nn_i2 = carve<int32_t>(p, 4 * NN_MAX_CHUNKS * b);
+  // the look-ahead stream at the lowest priority: the caller's stream carries
+  // the critical path, the search fills the CUs its small launches leave idle
+  int lo = 0, hi = 0;
+  bool ok = (size_t)(p - (char *)w->block) <= bytes &&
+            hipMemset(w->tiles, 0, 8 * w->ntiles) == hipSuccess &&
+            hipMemset(w->la_tiles, 0, 8 * w->ntiles) == hipSuccess &&
+            hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+            hipStreamCreateWithPriority(&w->la_stream, hipStreamNonBlocking, lo) == hipSuccess &&
+            hipEventCreateWithFlags(&w->la_go, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&w->la_done, hipEventDisableTiming) == hipSuccess;
+  if (ok) {
+    hipLaunchKernelGGL(k_plan_reset, dim3(1), dim3(1), 0, nullptr, w->st, (int64_t)0, w->la);
+    ok = hipDeviceSynchronize() == hipSuccess;
   }
-  hipLaunchKernelGGL(k_plan_reset, dim3(1), dim3(1), 0, nullptr, w->st, (int64_t)0);
-  if (hipDeviceSynchronize() != hipSuccess) {
-    (void)hipFree(w->block);
-    delete w;
+  if (!ok) {
+    ws_free(w);
     return GBP_E_HIP;
   }
   *out = w;
@@ -2330,9 +2504,7 @@ int gbp_plan_ws_destroy(gbp_plan_ws *w) {
   if (!w) return GBP_E_BAD_HANDLE;
   Guard g(w->device);
   (void)hipDeviceSynchronize();
-  if (w->block) (void)hipFree(w->block);
-  if (w->star_block) (void)hipFree(w->star_block);
-  delete w;
+  ws_free(w);
   return GBP_OK;
 }
 
@@ -2385,7 +2557,8 @@ int gbp_plan_star_config(gbp_plan_ws *w, int enable, double delta, int64_t max_p
 int gbp_plan_reset(gbp_plan_ws *w, int64_t extend_counter, gbp_stream stream) {
   if (!w) return GBP_E_BAD_HANDLE;
   Guard g(w->device);
-  hipLaunchKernelGGL(k_plan_reset, dim3(1), dim3(1), 0, (hipStream_t)stream, w->st, extend_counter);
+  hipLaunchKernelGGL(k_plan_reset, dim3(1), dim3(1), 0, (hipStream_t)stream, w->st, extend_counter,
+                     w->la);
   HIPCHK_P(hipGetLastError());
   return GBP_OK;
 }
@@ -2426,16 +2599,16 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
     return GBP_E_INVALID_ARG;
   Guard g(t->device);
   hipStream_t s = (hipStream_t)stream;
-  // targets drawn ahead: half h+1's draws do not depend on the trees unless
-  // the sampling is direction-biased, so half h's search launch draws and
-  // ranks them beside its matrix-core waves (NhDraw) and half h+1 has no
-  // k_targets: half h's last launch (k_append mode 1) commits them
-  // (commit_pre).  Same draws, same ranks, same counters.
+  // the look-ahead search (LaHalf, la_launch): half h+1's draws do not depend
+  // on the trees unless the sampling is direction-biased, and its search
+  // needs only O as it stands before half h's connects, so both run on
+  // la_stream beside half h; half h+1 starts with k_la_commit
   const bool ahead = !t->sampling.state_flag && !t->sampling.action_flag &&
-                     t->storage == GBP_STORAGE_F32 &&  // (k_nn_mfma<float> only)
-                     !w->star;  // (RRT*: the append does not commit)
-  bool predrawn = false;
-  for (int32_t i = 0; i < n_halves; i++) {
+                     t->storage == GBP_STORAGE_F32 &&  // (k_nn_mfma<float> draws)
+                     !w->star;  // (RRT*: the insertion reads the extends' tree between halves)
+  bool searched = false, used = false;
+  int rc = GBP_OK;
+  for (int32_t i = 0; i < n_halves && !rc; i++) {
     const int32_t h = first_half + i;
     const int k = h & 1;
     gbp_tree *T = k ? Tb : Ta, *O = k ? Ta : Tb;
@@ -2443,30 +2616,25 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
     const uint64_t ts = k ? stream_b : stream_a;
     const int64_t tb = (int64_t)(h >> 1) * batch;
     const int fs = i == 0 ? first_stage : 0;
-    NhDraw nd{};
-    const NhDraw *next = nullptr;
-    if (ahead && i + 1 < n_halves && (fs <= 2)) {
-      const int32_t h1 = h + 1;
-      const auto &set = w->tset[h1 & 1];
-      nd.half = h1;
-      nd.n = batch;
-      nd.base = (int64_t)(h1 >> 1) * batch;
-      nd.stream = (h1 & 1) ? stream_b : stream_a;
-      nd.cand = set.cand;
-      nd.targets = set.targets;
-      nd.cflag = set.cflag;
-      nd.tqh = set.tqh;
-      next = &nd;
-    }
-    const int rc = t->storage == GBP_STORAGE_F32
-                       ? enqueue_stages<float>(t, w, T, O, h, dir, batch, seed, ts, tb, adaptive, fs,
-                                               5, s, predrawn && fs == 0, next)
-                       : enqueue_stages<double>(t, w, T, O, h, dir, batch, seed, ts, tb, adaptive, fs,
-                                                5, s, predrawn && fs == 0, next);
-    if (rc) return rc;
-    predrawn = next != nullptr;
+    LaHalf L;
+    L.searched = searched;
+    L.launch_next = ahead && i + 1 < n_halves && (searched || fs <= 2);
+    L.draw_after = ahead && i + 2 < n_halves;
+    L.stream_a = stream_a;
+    L.stream_b = stream_b;
+    rc = t->storage == GBP_STORAGE_F32
+             ? enqueue_stages<float>(t, w, T, O, h, dir, batch, seed, ts, tb, adaptive, fs, 5, s, &L)
+             : enqueue_stages<double>(t, w, T, O, h, dir, batch, seed, ts, tb, adaptive, fs, 5, s, &L);
+    searched = L.launch_next;
+    used = used || L.launch_next;
   }
-  return GBP_OK;
+  // nothing of the call stays on la_stream past the caller's stream (a host
+  // that reads the status, reserves or destroys after this sees it finished)
+  if (used) {
+    HIPCHK_P(hipEventRecord(w->la_done, w->la_stream));
+    HIPCHK_P(hipStreamWaitEvent(s, w->la_done, 0));
+  }
+  return rc;
 }
 
 int gbp_extend_tree_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, int64_t n,

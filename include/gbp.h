@@ -480,12 +480,10 @@ typedef struct {
    * a compaction re-run for the same half (resumed at stage 1 after a FRAGILE
    * halt) starts from them again */
   int32_t ext_half;
-  uint32_t commit_fin;    /* workgroups of a committing k_append finished (internal) */
+  uint32_t commit_fin;    /* reserved (unused since the look-ahead search) */
   int64_t ext_prev, stat_targets_prev;
-  /* gbp_plan_halves_dev draws a half's targets ahead, inside the previous
-   * half's search launch (sampling not direction-biased): their count, and
-   * (half + 1) when one of those draws was FRAGILE (the half halts at its
-   * start, stage 1, as if its own draws had) */
+  /* reserved (unused): gbp_plan_halves_dev's drawn-ahead targets are
+   * counted in the workspace's look-ahead state (gbp_plan.hip gbp_plan_la) */
   int32_t pre_targets, pre_fragile;
   /* RRT*-Connect (gbp_plan_star_config): the last half's neighbour pairs
    * (new vertex, vertex before it within delta) and their connect checks
