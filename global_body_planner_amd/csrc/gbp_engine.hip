@@ -1217,6 +1217,7 @@ int gbp_terrain_create(int device, int nx, int ny, const double *x, const double
   }
   if (hipStreamCreateWithFlags(&t->host_stream, hipStreamNonBlocking) != hipSuccess)
     return fail(GBP_E_HIP);
+  (void)gbp_internal_la_stream(device, t->num_cus);  // ahead of any planner's clock
   (void)rc;
   *out = t;
   return GBP_OK;

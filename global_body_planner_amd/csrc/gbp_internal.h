@@ -130,6 +130,10 @@ inline int ensure_ws(void **ws, size_t *have, size_t need) {
   return GBP_OK;
 }
 
+// the device's look-ahead stream of the planner loop (created once per
+// process and device; null on failure); gbp_plan.hip
+hipStream_t gbp_internal_la_stream(int device, int num_cus);
+
 // the persistent validate kernel with the batch size read on the device from
 // n_dev (n_max bounds the grid); gbp_engine.hip
 int gbp_internal_validate_dev_n(gbp_terrain *t, int64_t n_max, const int *n_dev, const double *s,

@@ -50,6 +50,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <new>
 #include <type_traits>
 #include <vector>
@@ -1965,7 +1967,8 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
               const _Float16 *qh = nullptr, const NhPrep<ZT> *prep = nullptr,
               double *cs = nullptr, bool *prepped = nullptr, const NnSide *side = nullptr) {
   if (prepped) *prepped = false;
-  const int gm = w->nn_items / (NH_TB / WAVE);  // the search's workgroups: one wave per item
+  const int items = w->nn_items;
+  const int gm = items / (NH_TB / WAVE);  // the search's workgroups: one wave per item
   float4 *pm = (float4 *)(side ? w->nn_d2 : w->nn_d);
   int4 *pid = (int4 *)(side ? w->nn_i2 : w->nn_i);
   const int32_t *nv = side ? side->nv : tr->count;
@@ -1977,17 +1980,17 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
     const int gp = (int)grid_for(GBP_NUM_GEN_STATES * w->bmax, NH_TB, num_cus * 4);
     hipLaunchKernelGGL((k_nn_mfma<NH_NT, ZT, true>), dim3(gd + gm + gp), dim3(NH_TB), 0, s, w->st,
                        nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, nv, w->bmax, pm, pid,
-                       side ? 0 : ++w->seq, w->nn_items, pp, go);
+                       side ? 0 : ++w->seq, items, pp, go);
     if (prepped) *prepped = true;
   } else {
     hipLaunchKernelGGL((k_nn_mfma<NH_NT, float, false>), dim3(gm), dim3(NH_TB), 0, s, w->st,
                        nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, nv, w->bmax, pm, pid,
-                       side ? 0 : ++w->seq, w->nn_items, NhPrep<float>{}, go);
+                       side ? 0 : ++w->seq, items, NhPrep<float>{}, go);
   }
-  hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(NH_G * w->bmax, NH_RTB, num_cus * 8)), dim3(NH_RTB),
-                     0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, nv, w->bmax,
+  hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(NH_G * w->bmax, NH_RTB, num_cus * 8)),
+                     dim3(NH_RTB), 0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, nv, w->bmax,
                      (const float4 *)pm, (const int4 *)pid, out, side ? 0 : ++w->seq, w->nn_stats,
-                     prep ? cs : nullptr, w->nn_items, go);
+                     prep ? cs : nullptr, items, go);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
 
@@ -2410,10 +2413,49 @@ int gbp_tree_device_ptrs(gbp_tree *t, double **states, int32_t **count) {
   return GBP_OK;
 }
 
+// the look-ahead stream: its search launches would otherwise hold every CU's
+// registers for their whole duration (3 waves per SIMD at 162 VGPRs), and the
+// caller's stream's short latency-bound launches (select, appends, the
+// connects' search) would wait for them; the stream is masked to all XCDs
+// but the last (CUs [0, 7/8 n)), which keeps one XCD for those.  Measured on
+// the planner (config-3 pair, 4-s runs): 170 M extends/s unmasked, 180 M with
+// 224 of 256 CUs, 176 M with 208 or 240; spreading the excluded CUs over the
+// XCDs instead was slower (profiles/r05h_la_knobs*.txt).  GBP_LA_CUS
+// overrides the count (0 or >= n: unmasked, lowest priority).  One stream per
+// device for the process (creating a masked queue takes milliseconds: a
+// planner's time to first solution must not pay it; gbp_terrain_create
+// creates it ahead), shared by the device's workspaces.
+extern "C++" hipStream_t gbp_internal_la_stream(int device, int num_cus) {
+  static std::mutex mu;
+  static std::map<int, hipStream_t> streams;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = streams.find(device);
+  if (it != streams.end()) return it->second;
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  if (prev != device && hipSetDevice(device) != hipSuccess) return nullptr;
+  const char *env = getenv("GBP_LA_CUS");
+  const int n = num_cus, cus = env && *env ? atoi(env) : n - n / 8;
+  hipStream_t st = nullptr;
+  hipError_t e;
+  if (cus > 0 && cus < n) {
+    std::vector<uint32_t> mask((n + 31) / 32, 0u);
+    for (int c = 0; c < cus; c++) mask[c / 32] |= 1u << (c % 32);
+    e = hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data());
+  } else {
+    int lo = 0, hi = 0;
+    e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&st, hipStreamNonBlocking, lo);
+  }
+  if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+  if (e != hipSuccess) return nullptr;
+  streams[device] = st;
+  return st;
+}
+
 static void ws_free(gbp_plan_ws *w) {
   if (w->la_go) (void)hipEventDestroy(w->la_go);
   if (w->la_done) (void)hipEventDestroy(w->la_done);
-  if (w->la_stream) (void)hipStreamDestroy(w->la_stream);
   if (w->block) (void)hipFree(w->block);
   if (w->star_block) (void)hipFree(w->star_block);
   delete w;
@@ -2478,14 +2520,10 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->nn_i = carve<int32_t>(p, 4 * NN_MAX_CHUNKS * b);  // k_nn_mfma: int4 per slot
   w->nn_d2 = carve<double>(p, 2 * NN_MAX_CHUNKS * b);
   w->nn_i2 = carve<int32_t>(p, 4 * NN_MAX_CHUNKS * b);
-  // the look-ahead stream at the lowest priority: the caller's stream carries
-  // the critical path, the search fills the CUs its small launches leave idle
-  int lo = 0, hi = 0;
   bool ok = (size_t)(p - (char *)w->block) <= bytes &&
             hipMemset(w->tiles, 0, 8 * w->ntiles) == hipSuccess &&
             hipMemset(w->la_tiles, 0, 8 * w->ntiles) == hipSuccess &&
-            hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
-            hipStreamCreateWithPriority(&w->la_stream, hipStreamNonBlocking, lo) == hipSuccess &&
+            (w->la_stream = gbp_internal_la_stream(w->device, w->num_cus)) != nullptr &&
             hipEventCreateWithFlags(&w->la_go, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&w->la_done, hipEventDisableTiming) == hipSuccess;
   if (ok) {
