@@ -2425,7 +2425,8 @@ int gbp_tree_device_ptrs(gbp_tree *t, double **states, int32_t **count) {
 // device for the process (creating a masked queue takes milliseconds: a
 // planner's time to first solution must not pay it; gbp_terrain_create
 // creates it ahead), shared by the device's workspaces.
-extern "C++" hipStream_t gbp_internal_la_stream(int device, int num_cus) {
+extern "C++" __attribute__((visibility("hidden"))) hipStream_t gbp_internal_la_stream(int device,
+                                                                             int num_cus) {
   static std::mutex mu;
   static std::map<int, hipStream_t> streams;
   std::lock_guard<std::mutex> lk(mu);
