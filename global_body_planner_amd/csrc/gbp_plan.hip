@@ -144,6 +144,11 @@ struct gbp_plan_ws {
   // (nn_d2 / nn_i2: the look-ahead search's, on its own stream)
   double *nn_d = nullptr, *nn_d2 = nullptr;
   int32_t *nn_i = nullptr, *nn_i2 = nullptr;
+  // the direct search for a few queries (k_nn_small): per-workgroup partials
+  // and the completion count of its last-workgroup reduce
+  double *ns_d = nullptr;
+  int32_t *ns_i = nullptr;
+  uint32_t *ns_fin = nullptr;
   // the look-ahead search (gbp_plan_halves_dev): half h + 1's targets drawn
   // and searched on la_stream while half h's extends, connects and appends
   // run on the caller's stream (la_go: main -> side, la_done: side -> main)
@@ -325,6 +330,10 @@ constexpr double NH_SCALE = 64.0;      // F = 64 v (exact)
 constexpr double NH_LIM = 8192.0;      // |F_k| < 2^13: |F|^2 * 2^-14 < 2^15 fits fp16
 constexpr double NH_NSCALE = 0x1p-14;  // the norm parts are |F|^2 * 2^-14 ...
 constexpr float NH_NCONST = 16384.0f;  // ... times 2^14 on the query side
+constexpr int NS_MAXQ = 32;            // k_nn_small: queries it takes (the connects')
+constexpr int NS_GQ = 4;               // ... scored together per pass
+constexpr int NS_TB = 256;
+constexpr int NS_BLOCKS = 1024;        // its largest grid
 constexpr int NH_NT = 4;               // query tiles (32 queries) per wave
 constexpr int NH_ITEMS = 4096;         // waves a search aims for
 constexpr int NH_MAX_SEG = 64;         // segments per query (the reduce reads them all)
@@ -576,7 +585,7 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
                                                    const int32_t *__restrict__ nv_dev, int64_t bmax,
                                                    float4 *__restrict__ pm, int4 *__restrict__ pid,
                                                    uint64_t seq, int n_items, NhPrep<ZT> pp,
-                                                   const uint32_t *__restrict__ go) {
+                                                   const uint32_t *__restrict__ go, int small_max) {
   if (PREP && pp.dr.snap_dst && blockIdx.x == 0 && threadIdx.x == 0) {
     *pp.dr.snap_dst = *pp.dr.snap_src;
     *pp.dr.go_dst = gated(st, seq) ? 0u : 1u;
@@ -586,6 +595,7 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
     return;
   }
   if (go && *go == 0u) return;  // a look-ahead search launched after the sequence stopped
+  if (!PREP && *nq_dev <= small_max) return;  // k_nn_small has them
   // the next half's targets (k_targets' work); float heights only: with fp64
   // heights the state check's registers would cost the search an occupancy step
   if constexpr (PREP && std::is_same_v<ZT, float>) if ((int)blockIdx.x < pp.dr.draw_blocks) {
@@ -719,9 +729,10 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
                                                        const int4 *__restrict__ pid,
                                                        int32_t *__restrict__ out, uint64_t seq,
                                                        int stats, double *__restrict__ cs, int n_items,
-                                                       const uint32_t *__restrict__ go) {
+                                                       const uint32_t *__restrict__ go, int small_max) {
   if (gated(st, seq)) return;
   if (go && *go == 0u) return;  // (k_nn_mfma)
+  if (*nq_dev <= small_max) return;  // (k_nn_mfma)
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   int64_t nqg, nseg, cps, nch;
   nh_geometry(nq, nv, bmax, n_items, nqg, nseg, cps, nch);
@@ -884,6 +895,91 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
       atomicAdd((unsigned long long *)&st->stat_nn_scans, (unsigned long long)nsc);
     }
   }
+}
+
+// A few queries (the connect stage's: the vertices one half added, ~1-10 at
+// the planner's batch) against a tree of tens of thousands of vertices: the
+// matrix-core search would give each query a few long-running waves and its
+// reduce a latency chain (~25 + 18 us per half at 40k vertices); here every
+// thread scores its vertices in fp64 for up to NS_GQ queries at a time
+// (nn_dist64: the exact stage itself, nothing to re-check), workgroups reduce
+// (distance, index) lexicographically (the lowest index among ties,
+// planner_class.cpp:185-200; NaN never wins, so a NaN query gets index 0 as
+// in k_nn_hreduce) and the last workgroup to finish reduces the partials.
+// k_nn_mfma / k_nn_hreduce return at once when nq <= NS_MAXQ (small_max).
+__device__ __forceinline__ void ns_min(double &d, int &i, double od, int oi) {
+  if (od < d || (od == d && oi < i)) {
+    d = od;
+    i = oi;
+  }
+}
+__global__ __launch_bounds__(NS_TB) void k_nn_small(gbp_plan_status *st, const int32_t *__restrict__ nq_dev,
+                                                     const double *__restrict__ q,
+                                                     const int32_t *__restrict__ q_off_dev,
+                                                     const double *__restrict__ v,
+                                                     const int32_t *__restrict__ nv_dev,
+                                                     int32_t *__restrict__ out, double *__restrict__ pd,
+                                                     int32_t *__restrict__ pi, uint32_t *fin, uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
+  if (nq <= 0 || nq > NS_MAXQ) return;
+  __shared__ double sd[NS_TB / WAVE][NS_GQ];
+  __shared__ int si[NS_TB / WAVE][NS_GQ];
+  __shared__ bool last;
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  for (int64_t k0 = 0; k0 < nq; k0 += NS_GQ) {
+    double qq[NS_GQ][8], bd[NS_GQ];
+    int bi[NS_GQ];
+#pragma unroll
+    for (int g = 0; g < NS_GQ; g++) {
+      const int64_t k = min(k0 + g, nq - 1);
+#pragma unroll
+      for (int c = 0; c < 8; c++) qq[g][c] = q[8 * (q_off + k) + c];
+      bd[g] = INFINITY;
+      bi[g] = 0x7FFFFFFF;
+    }
+    for (int64_t j = blockIdx.x * (int64_t)NS_TB + threadIdx.x; j < nv; j += (int64_t)gridDim.x * NS_TB) {
+#pragma unroll
+      for (int g = 0; g < NS_GQ; g++) ns_min(bd[g], bi[g], nn_dist64(qq[g], v + 8 * j), (int)j);
+    }
+#pragma unroll
+    for (int g = 0; g < NS_GQ; g++) {
+      for (int off = WAVE / 2; off > 0; off >>= 1)
+        ns_min(bd[g], bi[g], __shfl_xor(bd[g], off), __shfl_xor(bi[g], off));
+      if (lane == 0) {
+        sd[w][g] = bd[g];
+        si[w][g] = bi[g];
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < NS_GQ && k0 + threadIdx.x < nq) {
+      double d = sd[0][threadIdx.x];
+      int i = si[0][threadIdx.x];
+      for (int ww = 1; ww < NS_TB / WAVE; ww++) ns_min(d, i, sd[ww][threadIdx.x], si[ww][threadIdx.x]);
+      pd[(k0 + threadIdx.x) * gridDim.x + blockIdx.x] = d;
+      pi[(k0 + threadIdx.x) * gridDim.x + blockIdx.x] = i;
+      __threadfence();  // (before this workgroup counts itself finished)
+    }
+    __syncthreads();
+  }
+  // the last workgroup to finish reduces every query's partials
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(fin, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  for (int64_t k = w; k < nq; k += NS_TB / WAVE) {
+    double d = INFINITY;
+    int i = 0x7FFFFFFF;
+    for (int b = lane; b < (int)gridDim.x; b += WAVE)
+      ns_min(d, i, __hip_atomic_load(&pd[k * gridDim.x + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+             __hip_atomic_load(&pi[k * gridDim.x + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    for (int off = WAVE / 2; off > 0; off >>= 1) ns_min(d, i, __shfl_xor(d, off), __shfl_xor(i, off));
+    if (lane == 0) out[k] = i == 0x7FFFFFFF ? 0 : i;
+  }
+  if (threadIdx.x == 0) *fin = 0;  // reset for the next launch (stream-ordered)
 }
 
 // ============================================================================
@@ -1969,8 +2065,19 @@ template <class ZT = float>
 int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int32_t *q_off_dev,
               const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s,
               const _Float16 *qh = nullptr, const NhPrep<ZT> *prep = nullptr,
-              double *cs = nullptr, bool *prepped = nullptr, const NnSide *side = nullptr) {
+              double *cs = nullptr, bool *prepped = nullptr, const NnSide *side = nullptr,
+              bool small = false) {
   if (prepped) *prepped = false;
+  // small: up to NS_MAXQ queries take the direct fp64 search (k_nn_small),
+  // the matrix-core pair then returns at once (the count is on the device)
+  const int small_max = small && !prep ? NS_MAXQ : 0;
+  if (small_max)
+    // one workgroup per CU of an XCD: in the planner the look-ahead search
+    // holds the other seven (32 blocks 171.8 M extends/s, 64: 171.2, 128:
+    // 169.3, 512: 160.8, the matrix-core pair alone 169.2; r05k_small_ab*.txt)
+    hipLaunchKernelGGL(k_nn_small, dim3(std::max(1, std::min(NS_BLOCKS, num_cus / 8))), dim3(NS_TB), 0, s, w->st,
+                       nq_dev, q, q_off_dev, tr->v, side ? side->nv : tr->count, out, w->ns_d, w->ns_i,
+                       w->ns_fin, side ? 0 : ++w->seq);
   const int items = w->nn_items;
   const int gm = items / (NH_TB / WAVE);  // the search's workgroups: one wave per item
   float4 *pm = (float4 *)(side ? w->nn_d2 : w->nn_d);
@@ -1984,17 +2091,17 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
     const int gp = (int)grid_for(GBP_NUM_GEN_STATES * w->bmax, NH_TB, num_cus * 4);
     hipLaunchKernelGGL((k_nn_mfma<NH_NT, ZT, true>), dim3(gd + gm + gp), dim3(NH_TB), 0, s, w->st,
                        nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, nv, w->bmax, pm, pid,
-                       side ? 0 : ++w->seq, items, pp, go);
+                       side ? 0 : ++w->seq, items, pp, go, 0);
     if (prepped) *prepped = true;
   } else {
     hipLaunchKernelGGL((k_nn_mfma<NH_NT, float, false>), dim3(gm), dim3(NH_TB), 0, s, w->st,
                        nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, nv, w->bmax, pm, pid,
-                       side ? 0 : ++w->seq, items, NhPrep<float>{}, go);
+                       side ? 0 : ++w->seq, items, NhPrep<float>{}, go, small_max);
   }
   hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(NH_G * w->bmax, NH_RTB, num_cus * 8)),
                      dim3(NH_RTB), 0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, nv, w->bmax,
                      (const float4 *)pm, (const int4 *)pid, out, side ? 0 : ++w->seq, w->nn_stats,
-                     prep ? cs : nullptr, items, go);
+                     prep ? cs : nullptr, items, go, small_max);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
 
@@ -2153,7 +2260,8 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   const int cdir = direction == GBP_FORWARD ? GBP_REVERSE : GBP_FORWARD;
   if (run(4)) {
     // queries: T's new vertices, rows [added_base, added_base + n_added)
-    int rc = nn_launch(w, &st->n_added, T->v, &st->added_base, O, w->nno, cus, s, T->vh);
+    int rc = nn_launch<float>(w, &st->n_added, T->v, &st->added_base, O, w->nno, cus, s, T->vh, nullptr,
+                       nullptr, nullptr, nullptr, true);
     if (rc) return rc;
     const int cm = (t->opt_affine && t->affine) ? 2 : 0;
     const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * 4, (batch + 3) / 4));
@@ -2485,7 +2593,7 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   const size_t bytes = sizeof(gbp_plan_status) + 16 * w->ntiles + 3 * (64 * b + 4 * b + 64 * b + 64 * b) +
                        1024 + m * (2 * 64 + 2 * 80 + 64 + 4 + 4) + b * (2 * 4 + 4 + 64 + 80 + 4 + 4) +
                        b * (4 + 4 + 64 + 80 + 4) + 2 * NN_MAX_CHUNKS * b * (16 + 16) + 64 * b + 512 +
-                       64 * 256;
+                       64 * 256 + (size_t)NS_MAXQ * NS_BLOCKS * 12 + 1024;
   if (hipMalloc(&w->block, bytes) != hipSuccess) {
     delete w;
     return GBP_E_ALLOC;
@@ -2525,7 +2633,11 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->nn_i = carve<int32_t>(p, 4 * NN_MAX_CHUNKS * b);  // k_nn_mfma: int4 per slot
   w->nn_d2 = carve<double>(p, 2 * NN_MAX_CHUNKS * b);
   w->nn_i2 = carve<int32_t>(p, 4 * NN_MAX_CHUNKS * b);
+  w->ns_d = carve<double>(p, (int64_t)NS_MAXQ * NS_BLOCKS);
+  w->ns_i = carve<int32_t>(p, (int64_t)NS_MAXQ * NS_BLOCKS);
+  w->ns_fin = carve<uint32_t>(p, 64);
   bool ok = (size_t)(p - (char *)w->block) <= bytes &&
+            hipMemset(w->ns_fin, 0, 4 * 64) == hipSuccess &&
             hipMemset(w->tiles, 0, 8 * w->ntiles) == hipSuccess &&
             hipMemset(w->la_tiles, 0, 8 * w->ntiles) == hipSuccess &&
             (w->la_stream = gbp_internal_la_stream(w->device, w->num_cus)) != nullptr &&
@@ -2770,7 +2882,8 @@ int gbp_tree_nearest_dev(gbp_plan_ws *w, gbp_tree *T, int64_t n, const double *q
   Guard g(w->device);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_set_queries, dim3(1), dim3(1), 0, s, w->st, (int32_t)n);
-  return nn_launch(w, &w->st->n_targets, queries, nullptr, T, index, w->num_cus, s);
+  return nn_launch<float>(w, &w->st->n_targets, queries, nullptr, T, index, w->num_cus, s, nullptr, nullptr,
+                   nullptr, nullptr, nullptr, true);
 }
 
 int gbp_plan_resolve_host(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int direction,

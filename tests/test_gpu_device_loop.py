@@ -217,6 +217,13 @@ def test_tree_nearest_exact(gpu):
     qn[::97, 4] = np.nan
     qn[5::101, 0] = 2e16
     check(big, qn, "big/nan")
+    # a few queries (the connect stage's): the direct fp64 search k_nn_small
+    # takes up to 32, the matrix-core pair the rest; both on the clusters
+    # (ties, exact duplicates), NaN and huge queries and a 1-vertex tree
+    for nqs in (1, 2, 3, 5, 31, 32, 33):
+        check(cl, np.ascontiguousarray(qc[:nqs]), f"few {nqs} clusters")
+        check(big, np.ascontiguousarray(qn[:nqs * 97 + 6:97][:nqs]), f"few {nqs} big/nan")
+    check(np.ascontiguousarray(verts[:1]), np.ascontiguousarray(q[:3]), "few 3 one vertex")
 
 
 def test_append_past_capacity_is_reported_not_faulted(gpu):
