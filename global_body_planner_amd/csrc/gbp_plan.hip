@@ -85,6 +85,21 @@ struct gbp_tree {
   int32_t *count = nullptr;   // [1] number of vertices (device resident)
 };
 
+// the segment scans k_nn_hreduce lists (a fourth unit of a segment within
+// the threshold: the segment's rows in fp64) and their merge; one set for the
+// caller's stream, one for the look-ahead stream
+constexpr int NSC_CAP = 16384;  // listed scans per search (more: scanned in the reduce)
+constexpr int NSC_UNITS = NSC_CAP * 8;  // (scan, part) results: NSC_CAP x NSC_P
+struct NsBuf {
+  int2 *list;               // (query, segment)
+  uint32_t *cnt;            // listed
+  double *ed;               // [NSC_UNITS] a scan part's minimum
+  int32_t *ei;              // ... its index (lowest at that minimum)
+  double *hd;               // [bmax] the reduce's own answer
+  int32_t *hi;
+  int2 *qh;                 // [bmax] a query's first entry and its entries
+};
+
 // the look-ahead search's device state (gbp_plan_ws::la), by half % 3 (the
 // drawn-ahead target sets) and by parity (the searched trees' snapshots)
 struct gbp_plan_la {
@@ -149,6 +164,7 @@ struct gbp_plan_ws {
   double *ns_d = nullptr;
   int32_t *ns_i = nullptr;
   uint32_t *ns_fin = nullptr;
+  NsBuf nsb[2] = {};           // k_nn_scan's lists: the caller's stream, the look-ahead's
   // the look-ahead search (gbp_plan_halves_dev): half h + 1's targets drawn
   // and searched on la_stream while half h's extends, connects and appends
   // run on the caller's stream (la_go: main -> side, la_done: side -> main)
@@ -281,6 +297,15 @@ __device__ __forceinline__ double nn_dist64(const double qq[8], const double *vj
     sum = sum + 1.0 * d * d;
   }
   return sqrt(sum);
+}
+
+// lexicographic (distance, index) minimum: the lowest index among equal
+// distances; a NaN distance never wins
+__device__ __forceinline__ void ns_min(double &d, int &i, double od, int oi) {
+  if (od < d || (od == d && oi < i)) {
+    d = od;
+    i = oi;
+  }
 }
 
 // ============================================================================
@@ -585,7 +610,11 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
                                                    const int32_t *__restrict__ nv_dev, int64_t bmax,
                                                    float4 *__restrict__ pm, int4 *__restrict__ pid,
                                                    uint64_t seq, int n_items, NhPrep<ZT> pp,
-                                                   const uint32_t *__restrict__ go, int small_max) {
+                                                   const uint32_t *__restrict__ go, int small_max,
+                                                   uint32_t *scan_cnt) {
+  // the reduce's scan list starts empty (whatever this launch then does:
+  // k_nn_scan / k_nn_scan_merge run after every search)
+  if (blockIdx.x == 0 && threadIdx.x == 0) *scan_cnt = 0;
   if (PREP && pp.dr.snap_dst && blockIdx.x == 0 && threadIdx.x == 0) {
     *pp.dr.snap_dst = *pp.dr.snap_src;
     *pp.dr.go_dst = gated(st, seq) ? 0u : 1u;
@@ -714,6 +743,10 @@ __global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__
   }
 }
 
+constexpr int NSC_TB = 256;  // k_nn_scan's workgroup
+constexpr int NSC_P = 8;     // ... workgroups per listed scan
+constexpr int NSM_TB = 256;   // k_nn_scan_merge
+
 // 16 lanes per query: B, T(B), the fp64 re-checks, lexicographic (distance,
 // index) minimum; nothing < inf (a NaN query): index 0.  (Writing the six
 // extend candidates from here instead of k_extend_prep was measured slower:
@@ -729,7 +762,8 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
                                                        const int4 *__restrict__ pid,
                                                        int32_t *__restrict__ out, uint64_t seq,
                                                        int stats, double *__restrict__ cs, int n_items,
-                                                       const uint32_t *__restrict__ go, int small_max) {
+                                                       const uint32_t *__restrict__ go, int small_max,
+                                                       NsBuf sb) {
   if (gated(st, seq)) return;
   if (go && *go == 0u) return;  // (k_nn_mfma)
   if (*nq_dev <= small_max) return;  // (k_nn_mfma)
@@ -780,6 +814,7 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
     // critical path)
     const bool part = live && !(qbad || tree_bad || !(B < INFINITY));
     const int gbit = (threadIdx.x & (WAVE - 1)) & ~(NH_G - 1);
+    int qn = 0, qbase = 0;  // the query's scans listed for k_nn_scan (group-uniform)
     constexpr uint32_t GM = NH_G == 32 ? 0xFFFFFFFFu : (1u << NH_G) - 1u;
     for (int64_t s0 = 0; s0 < nseg; s0 += NH_G) {
       const int64_t s = s0 + sl;
@@ -798,9 +833,28 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
       uint32_t cmask = (uint32_t)(__ballot(chk1) >> gbit) & GM;
       uint32_t cmask2 = (uint32_t)(__ballot(chk2) >> gbit) & GM;
       uint32_t cmask3 = (uint32_t)(__ballot(chk3) >> gbit) & GM;
+      const uint32_t sall = (uint32_t)(__ballot(scan) >> gbit) & GM;  // (every lane: a ballot)
+      nsc += sl == 0 ? __popc(sall) : 0;
+      // a query's segment scans go to k_nn_scan, its entries contiguous in the
+      // list (the group's leader reserves them); a query with scans in a later
+      // chunk of 16 segments too (more than 16 segments: small searches) or a
+      // full list scans inline
+      if (sb.list && sall && qn == 0) {
+        const uint32_t k = __popc(sall);
+        uint32_t base = 0;
+        if (sl == 0) base = atomicAdd(sb.cnt, k);
+        base = (uint32_t)__shfl((int)base, gbit);
+        if (base + k <= (uint32_t)NSC_CAP) {
+          if (scan) sb.list[base + __popc(sall & ((1u << sl) - 1u))] = int2{(int)qi, (int)s};
+          scan = false;
+          qn = (int)k;
+          qbase = (int)base;
+        } else if (scan && base + __popc(sall & ((1u << sl) - 1u)) < (uint32_t)NSC_CAP) {
+          sb.list[base + __popc(sall & ((1u << sl) - 1u))] = int2{-1, 0};  // (reserved, unused)
+        }
+      }
       uint32_t smask = (uint32_t)(__ballot(scan) >> gbit) & GM;
       nrc += sl == 0 ? __popc(cmask) + __popc(cmask2) + __popc(cmask3) : 0;
-      nsc += sl == 0 ? __popc(smask) : 0;
       while (__ballot((cmask | cmask2 | cmask3) != 0u)) {
         if (cmask | cmask2 | cmask3) {
           int h;
@@ -885,6 +939,12 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
     if (live && sl == 0) out[qi] = bi == 0x7FFFFFFF ? 0 : bi;
     if (cs && live && sl < GBP_NUM_GEN_STATES)  // s_near of the six candidates (k_extend_prep)
       copy8(cs + 8 * (qi * GBP_NUM_GEN_STATES + sl), v + 8 * (int64_t)(bi == 0x7FFFFFFF ? 0 : bi));
+    // a query with listed scans: its answer so far, for k_nn_scan_merge
+    if (qn && sl == 0) {
+      sb.hd[qi] = best;
+      sb.hi[qi] = bi;
+      sb.qh[qi] = int2{qbase, qn};
+    }
     if (!stats) continue;  // diagnostics (GBP_OPT_NN_STATS): same-address atomics serialise
     for (int off = 32; off > 0; off >>= 1) {
       nrc += __shfl_xor(nrc, off);
@@ -894,6 +954,82 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
       atomicAdd((unsigned long long *)&st->stat_nn_rechecks, (unsigned long long)nrc);
       atomicAdd((unsigned long long *)&st->stat_nn_scans, (unsigned long long)nsc);
     }
+  }
+}
+
+// the listed segment scans (a ~3k-row segment walked by one wave was the
+// reduce's tail: 80 -> 31 us at 40k vertices without it), each over NSC_P
+// workgroups: unit u = (scan u / NSC_P, part u % NSC_P) writes its rows'
+// lexicographic (distance, index) minimum.  k_nn_scan_merge then folds, per
+// query, its scans' units into the reduce's answer and rewrites out / the
+// candidates' s_near where it changed.  Never gated: k_nn_mfma empties the
+// list first thing, whatever the sequence does.
+__global__ __launch_bounds__(NSC_TB) void k_nn_scan(const int32_t *__restrict__ nq_dev,
+                                                    const double *__restrict__ q,
+                                                    const int32_t *__restrict__ q_off_dev,
+                                                    const double *__restrict__ v,
+                                                    const int32_t *__restrict__ nv_dev, int64_t bmax,
+                                                    int n_items, NsBuf sb) {
+  const uint32_t n = min(*sb.cnt, (uint32_t)NSC_CAP);
+  if (n == 0) return;
+  const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
+  int64_t nqg, nseg, cps, nch;
+  nh_geometry(nq, nv, bmax, n_items, nqg, nseg, cps, nch);
+  __shared__ double sd[NSC_TB / WAVE];
+  __shared__ int si[NSC_TB / WAVE];
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  const uint32_t units = n * NSC_P;
+  for (uint32_t e = blockIdx.x; e < units; e += gridDim.x) {
+    const int2 L = sb.list[e / NSC_P];
+    if (L.x < 0) continue;  // (workgroup-uniform)
+    double qq[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) qq[k] = q[8 * (q_off + L.x) + k];
+    const int64_t j0 = L.y * cps * 32, j1 = min(nv, min(nch, (L.y + 1) * cps) * 32);
+    const int64_t len = (j1 - j0 + NSC_P - 1) / NSC_P, p0 = j0 + (e % NSC_P) * len;
+    const int64_t p1 = min(j1, p0 + len);
+    double d = INFINITY;
+    int i = 0x7FFFFFFF;
+    for (int64_t j = p0 + threadIdx.x; j < p1; j += NSC_TB) ns_min(d, i, nn_dist64(qq, v + 8 * j), (int)j);
+    for (int off = WAVE / 2; off > 0; off >>= 1) ns_min(d, i, __shfl_xor(d, off), __shfl_xor(i, off));
+    if (lane == 0) {
+      sd[w] = d;
+      si[w] = i;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int k = 1; k < NSC_TB / WAVE; k++) ns_min(d, i, sd[k], si[k]);
+      sb.ed[e] = d;
+      sb.ei[e] = i;
+    }
+    __syncthreads();
+  }
+}
+
+// per listed query (its first entry): its units folded into the reduce's
+// answer (hd / hi); out and the candidates' s_near rewritten where it changed
+// (the list is emptied by the next search's k_nn_mfma)
+__global__ __launch_bounds__(NSM_TB) void k_nn_scan_merge(NsBuf sb, const double *__restrict__ v,
+                                                          int32_t *__restrict__ out,
+                                                          double *__restrict__ cs) {
+  const uint32_t n = min(*sb.cnt, (uint32_t)NSC_CAP);
+  for (uint32_t e = blockIdx.x * NSM_TB + threadIdx.x; e < n; e += gridDim.x * NSM_TB) {
+    const int qx = sb.list[e].x;
+    if (qx < 0) continue;
+    const int2 h = sb.qh[qx];
+    if (h.x != (int)e) continue;  // not the query's first entry
+    double d = sb.hd[qx];
+    int i = sb.hi[qx];
+    const int i0 = i;
+    for (int f = h.x; f < h.x + h.y; f++)
+#pragma unroll
+      for (int k = 0; k < NSC_P; k++) ns_min(d, i, sb.ed[f * NSC_P + k], sb.ei[f * NSC_P + k]);
+    if (i == i0) continue;
+    const int o = i == 0x7FFFFFFF ? 0 : i;
+    out[qx] = o;
+    if (cs)
+      for (int k = 0; k < GBP_NUM_GEN_STATES; k++)
+        copy8(cs + 8 * ((int64_t)qx * GBP_NUM_GEN_STATES + k), v + 8 * (int64_t)o);
   }
 }
 
@@ -907,12 +1043,6 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
 // planner_class.cpp:185-200; NaN never wins, so a NaN query gets index 0 as
 // in k_nn_hreduce) and the last workgroup to finish reduces the partials.
 // k_nn_mfma / k_nn_hreduce return at once when nq <= NS_MAXQ (small_max).
-__device__ __forceinline__ void ns_min(double &d, int &i, double od, int oi) {
-  if (od < d || (od == d && oi < i)) {
-    d = od;
-    i = oi;
-  }
-}
 __global__ __launch_bounds__(NS_TB) void k_nn_small(gbp_plan_status *st, const int32_t *__restrict__ nq_dev,
                                                      const double *__restrict__ q,
                                                      const int32_t *__restrict__ q_off_dev,
@@ -2091,17 +2221,21 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
     const int gp = (int)grid_for(GBP_NUM_GEN_STATES * w->bmax, NH_TB, num_cus * 4);
     hipLaunchKernelGGL((k_nn_mfma<NH_NT, ZT, true>), dim3(gd + gm + gp), dim3(NH_TB), 0, s, w->st,
                        nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, nv, w->bmax, pm, pid,
-                       side ? 0 : ++w->seq, items, pp, go, 0);
+                       side ? 0 : ++w->seq, items, pp, go, 0, w->nsb[side ? 1 : 0].cnt);
     if (prepped) *prepped = true;
   } else {
     hipLaunchKernelGGL((k_nn_mfma<NH_NT, float, false>), dim3(gm), dim3(NH_TB), 0, s, w->st,
                        nq_dev, q, q_off_dev, qh, tr->vh, tr->hm, nv, w->bmax, pm, pid,
-                       side ? 0 : ++w->seq, items, NhPrep<float>{}, go, small_max);
+                       side ? 0 : ++w->seq, items, NhPrep<float>{}, go, small_max, w->nsb[side ? 1 : 0].cnt);
   }
   hipLaunchKernelGGL(k_nn_hreduce, dim3(grid_for(NH_G * w->bmax, NH_RTB, num_cus * 8)),
                      dim3(NH_RTB), 0, s, w->st, nq_dev, q, q_off_dev, tr->v, tr->hm, nv, w->bmax,
                      (const float4 *)pm, (const int4 *)pid, out, side ? 0 : ++w->seq, w->nn_stats,
-                     prep ? cs : nullptr, items, go, small_max);
+                     prep ? cs : nullptr, items, go, small_max, w->nsb[side ? 1 : 0]);
+  hipLaunchKernelGGL(k_nn_scan, dim3(num_cus * 4), dim3(NSC_TB), 0, s, nq_dev, q, q_off_dev, tr->v, nv,
+                     w->bmax, items, w->nsb[side ? 1 : 0]);
+  hipLaunchKernelGGL(k_nn_scan_merge, dim3(16), dim3(NSM_TB), 0, s, w->nsb[side ? 1 : 0], tr->v, out,
+                     prep ? cs : nullptr);
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
 
@@ -2562,6 +2696,15 @@ extern "C++" __attribute__((visibility("hidden"))) hipStream_t gbp_internal_la_s
   }
   if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
   if (e != hipSuccess) return nullptr;
+  if (streams.empty()) {
+    // destroyed before the HIP runtime's own exit handlers run (registered
+    // earlier, so they run later): a profiler's teardown walking the
+    // process's queues at exit found this one still alive and faulted
+    std::atexit([] {
+      for (auto &kv : streams) (void)hipStreamDestroy(kv.second);
+      streams.clear();
+    });
+  }
   streams[device] = st;
   return st;
 }
@@ -2593,7 +2736,8 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   const size_t bytes = sizeof(gbp_plan_status) + 16 * w->ntiles + 3 * (64 * b + 4 * b + 64 * b + 64 * b) +
                        1024 + m * (2 * 64 + 2 * 80 + 64 + 4 + 4) + b * (2 * 4 + 4 + 64 + 80 + 4 + 4) +
                        b * (4 + 4 + 64 + 80 + 4) + 2 * NN_MAX_CHUNKS * b * (16 + 16) + 64 * b + 512 +
-                       64 * 256 + (size_t)NS_MAXQ * NS_BLOCKS * 12 + 1024;
+                       64 * 256 + (size_t)NS_MAXQ * NS_BLOCKS * 12 + 1024 +
+                       2 * ((size_t)NSC_CAP * 8 + (size_t)NSC_UNITS * 12 + 32 * b + 1024);
   if (hipMalloc(&w->block, bytes) != hipSuccess) {
     delete w;
     return GBP_E_ALLOC;
@@ -2636,8 +2780,19 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->ns_d = carve<double>(p, (int64_t)NS_MAXQ * NS_BLOCKS);
   w->ns_i = carve<int32_t>(p, (int64_t)NS_MAXQ * NS_BLOCKS);
   w->ns_fin = carve<uint32_t>(p, 64);
+  for (auto &sb : w->nsb) {
+    sb.list = carve<int2>(p, NSC_CAP);
+    sb.ed = carve<double>(p, NSC_UNITS);
+    sb.ei = carve<int32_t>(p, NSC_UNITS);
+    sb.cnt = carve<uint32_t>(p, 64);
+    sb.hd = carve<double>(p, b);
+    sb.hi = carve<int32_t>(p, b);
+    sb.qh = carve<int2>(p, b);
+  }
   bool ok = (size_t)(p - (char *)w->block) <= bytes &&
             hipMemset(w->ns_fin, 0, 4 * 64) == hipSuccess &&
+            hipMemset(w->nsb[0].cnt, 0, 4 * 64) == hipSuccess &&
+            hipMemset(w->nsb[1].cnt, 0, 4 * 64) == hipSuccess &&
             hipMemset(w->tiles, 0, 8 * w->ntiles) == hipSuccess &&
             hipMemset(w->la_tiles, 0, 8 * w->ntiles) == hipSuccess &&
             (w->la_stream = gbp_internal_la_stream(w->device, w->num_cus)) != nullptr &&
