@@ -787,19 +787,59 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
       g2 += gk * gk;
     }
     // the group's entries, lane sl reading segments sl, sl + NH_G, ...
-    float B = INFINITY;
+    constexpr int NK = NH_MAX_SEG / NH_G;
+    float B = INFINITY, w4[NK];
 #pragma unroll
-    for (int k = 0; k < NH_MAX_SEG / NH_G; k++) {
+    for (int k = 0; k < NK; k++) {
       const int64_t s = sl + NH_G * k;
-      if (live && s < nseg) B = fminf(B, pm[s * nq + qi].x);
+      const float4 e = live && s < nseg ? pm[s * nq + qi] : float4{INFINITY, INFINITY, INFINITY, INFINITY};
+      B = fminf(B, e.x);
+      w4[k] = e.w;
     }
 #pragma unroll
     for (int off = NH_G / 2; off > 0; off >>= 1) B = fminf(B, __shfl_xor(B, off, NH_G));
     const float T = nh_threshold(B, nh_eps(qq, hm), g2);
     double best = INFINITY;
     int bi = 0x7FFFFFFF, nrc = 0, nsc = 0;
-    if (live && (qbad || tree_bad || !(B < INFINITY))) {  // the whole tree in fp64
-      nsc = sl == 0;
+    bool full = live && (qbad || tree_bad || !(B < INFINITY));
+    const int gbit = (threadIdx.x & (WAVE - 1)) & ~(NH_G - 1);
+    constexpr uint32_t GM = NH_G == 32 ? 0xFFFFFFFFu : (1u << NH_G) - 1u;
+    // segments with a fourth unit within T are scanned in full by k_nn_scan:
+    // the query's entries listed contiguously (its group's leader reserves
+    // them); a full list turns the query into a whole-tree fp64 scan here
+    int qn = 0, qbase = 0;  // (group-uniform)
+    {
+      uint32_t bal[NK], tot = 0;
+#pragma unroll
+      for (int k = 0; k < NK; k++) {
+        bal[k] = (uint32_t)(__ballot(live && !full && sl + NH_G * k < nseg && w4[k] <= T) >> gbit) & GM;
+        tot += __popc(bal[k]);
+      }
+      nsc += sl == 0 ? (int)tot : 0;
+      if (tot) {
+        uint32_t base = 0;
+        if (sl == 0) base = atomicAdd(sb.cnt, tot);
+        base = (uint32_t)__shfl((int)base, gbit);
+        const bool fits = base + tot <= (uint32_t)NSC_CAP;
+        uint32_t off = base;
+#pragma unroll
+        for (int k = 0; k < NK; k++) {
+          if ((bal[k] >> sl) & 1u) {
+            const uint32_t slot = off + __popc(bal[k] & ((1u << sl) - 1u));
+            if (slot < (uint32_t)NSC_CAP)  // (past a full list: reserved, unused)
+              sb.list[slot] = fits ? int2{(int)qi, (int)(sl + NH_G * k)} : int2{-1, 0};
+          }
+          off += __popc(bal[k]);
+        }
+        if (fits) {
+          qn = (int)tot;
+          qbase = (int)base;
+        } else {
+          full = live;
+        }
+      }
+    }
+    if (full) {  // the whole tree in fp64
       for (int64_t j = sl; j < nv; j += NH_G) {
         const double d = nn_dist64(qq, v + 8 * j);
         if (d < best) {  // ascending per lane: the first index at its minimum
@@ -808,22 +848,16 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
         }
       }
     }
-    // the half-chunks to re-check and the segments to scan go round the
-    // group: a half-chunk's 16 rows one per lane, a segment's rows strided
-    // over the 16 lanes (a single lane walking them was the search's
-    // critical path)
-    const bool part = live && !(qbad || tree_bad || !(B < INFINITY));
-    const int gbit = (threadIdx.x & (WAVE - 1)) & ~(NH_G - 1);
-    int qn = 0, qbase = 0;  // the query's scans listed for k_nn_scan (group-uniform)
-    constexpr uint32_t GM = NH_G == 32 ? 0xFFFFFFFFu : (1u << NH_G) - 1u;
+    // the half-chunks to re-check go round the group: a half-chunk's 16 rows
+    // one per lane
+    const bool part = live && !full;
     for (int64_t s0 = 0; s0 < nseg; s0 += NH_G) {
       const int64_t s = s0 + sl;
-      bool chk1 = false, chk2 = false, chk3 = false, scan = false;
+      bool chk1 = false, chk2 = false, chk3 = false;
       int4 hid = {-1, -1, -1, 0};
       if (part && s < nseg) {
         const float4 e = pm[s * nq + qi];  // L2-warm since the first pass
-        scan = e.w <= T;  // a fourth unit within T: the segment in full
-        if (!scan && e.x <= T) {
+        if (!(e.w <= T) && e.x <= T) {  // (a segment in full: listed above)
           hid = pid[s * nq + qi];
           chk1 = hid.x >= 0;
           chk2 = e.y <= T && hid.y >= 0;
@@ -833,27 +867,6 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
       uint32_t cmask = (uint32_t)(__ballot(chk1) >> gbit) & GM;
       uint32_t cmask2 = (uint32_t)(__ballot(chk2) >> gbit) & GM;
       uint32_t cmask3 = (uint32_t)(__ballot(chk3) >> gbit) & GM;
-      const uint32_t sall = (uint32_t)(__ballot(scan) >> gbit) & GM;  // (every lane: a ballot)
-      nsc += sl == 0 ? __popc(sall) : 0;
-      // a query's segment scans go to k_nn_scan, its entries contiguous in the
-      // list (the group's leader reserves them); a query with scans in a later
-      // chunk of 16 segments too (more than 16 segments: small searches) or a
-      // full list scans inline
-      if (sb.list && sall && qn == 0) {
-        const uint32_t k = __popc(sall);
-        uint32_t base = 0;
-        if (sl == 0) base = atomicAdd(sb.cnt, k);
-        base = (uint32_t)__shfl((int)base, gbit);
-        if (base + k <= (uint32_t)NSC_CAP) {
-          if (scan) sb.list[base + __popc(sall & ((1u << sl) - 1u))] = int2{(int)qi, (int)s};
-          scan = false;
-          qn = (int)k;
-          qbase = (int)base;
-        } else if (scan && base + __popc(sall & ((1u << sl) - 1u)) < (uint32_t)NSC_CAP) {
-          sb.list[base + __popc(sall & ((1u << sl) - 1u))] = int2{-1, 0};  // (reserved, unused)
-        }
-      }
-      uint32_t smask = (uint32_t)(__ballot(scan) >> gbit) & GM;
       nrc += sl == 0 ? __popc(cmask) + __popc(cmask2) + __popc(cmask3) : 0;
       while (__ballot((cmask | cmask2 | cmask3) != 0u)) {
         if (cmask | cmask2 | cmask3) {
@@ -885,45 +898,6 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
               }
             }
           }
-        }
-      }
-      // segment scans, the whole wave on one (group, segment) at a time: the
-      // planner's clustered trees ask for a few per launch, and one group
-      // walking ~1k rows alone was the launch's tail
-      for (;;) {
-        const unsigned long long pend = __ballot(smask != 0u);
-        if (!pend) break;
-        const int src = __ffsll((long long)pend) - 1;  // first lane of the owning group
-        const uint32_t sm = (uint32_t)__shfl((int)smask, src);
-        const bool owner = gbit == (src & ~(NH_G - 1));
-        if (owner) smask &= smask - 1u;
-        double oq[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) oq[k] = __shfl(qq[k], src);
-        const int64_t ss = s0 + (__ffs(sm) - 1);
-        const int64_t j1 = min(nv, min(nch, (ss + 1) * cps) * 32);
-        double wb = INFINITY;
-        int wi = 0x7FFFFFFF;
-        int64_t j = ss * cps * 32 + (threadIdx.x & (WAVE - 1));
-        for (; j < j1; j += WAVE) {
-          const double d = nn_dist64(oq, v + 8 * j);
-          if (d < wb) {  // ascending per lane
-            wb = d;
-            wi = (int)j;
-          }
-        }
-#pragma unroll
-        for (int off = WAVE / 2; off > 0; off >>= 1) {
-          const double od = __shfl_xor(wb, off);
-          const int oi = __shfl_xor(wi, off);
-          if (od < wb || (od == wb && oi < wi)) {
-            wb = od;
-            wi = oi;
-          }
-        }
-        if (owner && (wb < best || (wb == best && wi < bi))) {
-          best = wb;
-          bi = wi;
         }
       }
     }
