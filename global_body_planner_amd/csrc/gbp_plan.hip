@@ -91,6 +91,7 @@ struct gbp_tree {
 constexpr int NSC_CAP = 16384;  // listed scans per search (more: scanned in the reduce)
 constexpr int NSC_UNITS = NSC_CAP * 8;  // (scan, part) results: NSC_CAP x NSC_P
 struct NsBuf {
+  uint32_t cap;             // list capacity (NSC_CAP; GBP_NSC_CAP lowers it: tests)
   int2 *list;               // (query, segment)
   uint32_t *cnt;            // listed
   double *ed;               // [NSC_UNITS] a scan part's minimum
@@ -820,13 +821,13 @@ __global__ __launch_bounds__(NH_RTB) void k_nn_hreduce(gbp_plan_status *st,
         uint32_t base = 0;
         if (sl == 0) base = atomicAdd(sb.cnt, tot);
         base = (uint32_t)__shfl((int)base, gbit);
-        const bool fits = base + tot <= (uint32_t)NSC_CAP;
+        const bool fits = base + tot <= sb.cap;
         uint32_t off = base;
 #pragma unroll
         for (int k = 0; k < NK; k++) {
           if ((bal[k] >> sl) & 1u) {
             const uint32_t slot = off + __popc(bal[k] & ((1u << sl) - 1u));
-            if (slot < (uint32_t)NSC_CAP)  // (past a full list: reserved, unused)
+            if (slot < sb.cap)  // (past a full list: reserved, unused)
               sb.list[slot] = fits ? int2{(int)qi, (int)(sl + NH_G * k)} : int2{-1, 0};
           }
           off += __popc(bal[k]);
@@ -944,7 +945,7 @@ __global__ __launch_bounds__(NSC_TB) void k_nn_scan(const int32_t *__restrict__ 
                                                     const double *__restrict__ v,
                                                     const int32_t *__restrict__ nv_dev, int64_t bmax,
                                                     int n_items, NsBuf sb) {
-  const uint32_t n = min(*sb.cnt, (uint32_t)NSC_CAP);
+  const uint32_t n = min(*sb.cnt, sb.cap);
   if (n == 0) return;
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
   int64_t nqg, nseg, cps, nch;
@@ -986,7 +987,7 @@ __global__ __launch_bounds__(NSC_TB) void k_nn_scan(const int32_t *__restrict__ 
 __global__ __launch_bounds__(NSM_TB) void k_nn_scan_merge(NsBuf sb, const double *__restrict__ v,
                                                           int32_t *__restrict__ out,
                                                           double *__restrict__ cs) {
-  const uint32_t n = min(*sb.cnt, (uint32_t)NSC_CAP);
+  const uint32_t n = min(*sb.cnt, sb.cap);
   for (uint32_t e = blockIdx.x * NSM_TB + threadIdx.x; e < n; e += gridDim.x * NSM_TB) {
     const int qx = sb.list[e].x;
     if (qx < 0) continue;
@@ -2755,6 +2756,8 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->ns_i = carve<int32_t>(p, (int64_t)NS_MAXQ * NS_BLOCKS);
   w->ns_fin = carve<uint32_t>(p, 64);
   for (auto &sb : w->nsb) {
+    const char *cenv = getenv("GBP_NSC_CAP");  // (a small list: the fallback's test)
+    sb.cap = (uint32_t)std::max(1, std::min(NSC_CAP, cenv && *cenv ? atoi(cenv) : NSC_CAP));
     sb.list = carve<int2>(p, NSC_CAP);
     sb.ed = carve<double>(p, NSC_UNITS);
     sb.ei = carve<int32_t>(p, NSC_UNITS);

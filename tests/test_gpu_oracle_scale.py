@@ -133,3 +133,27 @@ def test_config3_scale_warm_continuation(gpu):
     for t in "ab":
         for k in ("v", "act", "parent", "g"):
             assert np.array_equal(bits(full[t][k]), bits(dev[t][k])), (t, k)
+
+
+def test_config3_scale_scan_list_overflow(gpu, monkeypatch):
+    """The reduce's list of segment scans (k_nn_scan) full: with a list of 2
+    entries (GBP_NSC_CAP, read when the planner creates its workspace) every
+    further query with scans becomes a whole-tree fp64 scan in the reduce.
+    The warm continuation of the test above, against the oracle."""
+    data, O = _terrain()
+    start, goal = _start_goal(O, 1.0, 10.23, 19.42, 10.23)
+    cap = 1 << 18
+    grown = planner.plan_rrt_connect(data, start, goal, algorithm=3, batch=DRAWS, max_time=300.0,
+                                     seed=20251018, max_halves=GROW_HALVES, trees=True,
+                                     tree_capacity=cap)
+    init = tuple({k: grown[t][k] for k in ("v", "act", "parent")} for t in "ab")
+    warm = dict(batch=DRAWS, seed=20251018, max_halves=CONT_HALVES)
+    monkeypatch.setenv("GBP_NSC_CAP", "2")
+    dev = planner.plan_rrt_connect(data, start, goal, algorithm=3, max_time=300.0, trees=True,
+                                   tree_capacity=cap, nn_stats=True, init_trees=init,
+                                   first_half=GROW_HALVES, extend_base=grown["extends"], **warm)
+    monkeypatch.delenv("GBP_NSC_CAP")
+    ref = O.plan(start, goal, capacity=cap, nthreads=NTHREADS, init_trees=init,
+                 first_half=GROW_HALVES, extend_base=grown["extends"], **warm)
+    _compare(dev, ref)
+    assert dev["nn_scans"] > 2 * 2 * CONT_HALVES  # more than the lists held
