@@ -2890,7 +2890,11 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
   // on the trees unless the sampling is direction-biased, and its search
   // needs only O as it stands before half h's connects, so both run on
   // la_stream beside half h; half h+1 starts with k_la_commit
-  const bool ahead = !t->sampling.state_flag && !t->sampling.action_flag &&
+  static const bool la_off = [] {  // GBP_LA_OFF=1: the inline sequence (A/B, diagnostics)
+    const char *e = getenv("GBP_LA_OFF");
+    return e && *e && *e != '0';
+  }();
+  const bool ahead = !la_off && !t->sampling.state_flag && !t->sampling.action_flag &&
                      t->storage == GBP_STORAGE_F32 &&  // (k_nn_mfma<float> draws)
                      !w->star;  // (RRT*: the insertion reads the extends' tree between halves)
   bool searched = false, used = false;

@@ -32,6 +32,7 @@ def main():
     p.add_argument("--seed0", type=int, default=20251018)
     p.add_argument("--max-time", type=float, default=30.0)
     p.add_argument("--out", default=None)
+    p.add_argument("--algorithm", type=int, default=3, help="3: the device loop (bench.py's)")
     a = p.parse_args()
     data = td.by_name(a.terrain)
     T = gbp.Terrain.from_data(data, device=0)
@@ -44,7 +45,7 @@ def main():
         times = []
         for k in range(a.seeds):
             out = planner.plan_rrt_connect(data, start, goal, batch=b, max_time=a.max_time,
-                                           seed=a.seed0 + 7919 * k)
+                                           seed=a.seed0 + 7919 * k, algorithm=a.algorithm)
             row = {"terrain": a.terrain, "batch": b, "seed": a.seed0 + 7919 * k,
                    "found": out["found"], "ttfs": out["time_to_first"],
                    "total": out["total_time"], "iterations": out["iterations"],
