@@ -2894,9 +2894,10 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
     const char *e = getenv("GBP_LA_OFF");
     return e && *e && *e != '0';
   }();
+  // (RRT* too: its insertion rewires the extended tree's parents and g, not
+  // its vertices, and the connects still append to O after the snapshot)
   const bool ahead = !la_off && !t->sampling.state_flag && !t->sampling.action_flag &&
-                     t->storage == GBP_STORAGE_F32 &&  // (k_nn_mfma<float> draws)
-                     !w->star;  // (RRT*: the insertion reads the extends' tree between halves)
+                     t->storage == GBP_STORAGE_F32;  // (k_nn_mfma<float> draws)
   bool searched = false, used = false;
   int rc = GBP_OK;
   for (int32_t i = 0; i < n_halves && !rc; i++) {
