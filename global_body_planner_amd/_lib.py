@@ -48,7 +48,8 @@ EXPORTS = [
     "gbp_resolve_fragile_host", "gbp_resolve_fragile_states_host", "gbp_extend_resolve_host",
     "gbp_stream_create", "gbp_stream_destroy",
     "gbp_tree_create", "gbp_tree_destroy", "gbp_tree_init", "gbp_tree_reserve", "gbp_tree_capacity",
-    "gbp_tree_size", "gbp_tree_read", "gbp_tree_append_host", "gbp_tree_device_ptrs",
+    "gbp_tree_size", "gbp_tree_read", "gbp_tree_append_host", "gbp_tree_load_host",
+    "gbp_tree_device_ptrs", "gbp_vertex_map_order", "gbp_vertex_map_rank",
     "gbp_plan_ws_create", "gbp_plan_ws_destroy", "gbp_plan_reset", "gbp_plan_half_dev",
     "gbp_plan_halves_dev", "gbp_plan_star_config",
     "gbp_plan_status_read", "gbp_plan_resolve_host", "gbp_extend_tree_dev",
@@ -142,6 +143,9 @@ def load(path=None):
         "gbp_tree_size": (I, [P, P, P]),
         "gbp_tree_read": (I, [P, I64, I64, P, P, P, P, P]),
         "gbp_tree_append_host": (I, [P, I64, P, P, P, P]),
+        "gbp_tree_load_host": (I, [P, I64, P, P, P, P]),
+        "gbp_vertex_map_order": (I, [I64, P]),
+        "gbp_vertex_map_rank": (I, [I64, I64, P]),
         "gbp_tree_device_ptrs": (I, [P, P, P]),
         "gbp_plan_ws_create": (I, [P, I64, P]),
         "gbp_plan_ws_destroy": (I, [P]),

@@ -30,6 +30,7 @@
 #include "gbp.h"
 #include "gbp_device.h"
 #include "gbp_lane.h"
+#include "gbp_um_order.h"
 #include "gbp_internal.h"
 #include "host/gbp_host_check.h"
 
@@ -682,10 +683,10 @@ __global__ __launch_bounds__(256) void k_nearest_tiled(int64_t n_query,
 }
 
 // PlannerClass::neighborhoodDist (planner_class.cpp:173-182): the vertices
-// with 0 < stateDistance(q, v) <= radius, in ascending vertex index (the
-// reference iterates an unordered_map; the engine fixes index order, H9).
-// One workgroup per query; out[q][0..max_out) holds the first max_out
-// neighbours, count[q] the total (may exceed max_out).
+// with 0 < stateDistance(q, v) <= radius, in the order the reference's vertex
+// map (keys 0..n_vert-1) iterates them (gbp_um_order.h), position p holding
+// key um_key_at(p, n_vert).  One workgroup per query; out[q][0..max_out)
+// holds the first max_out neighbours, count[q] the total (may exceed max_out).
 __global__ __launch_bounds__(256) void k_neighbors(int64_t n_query, const double *__restrict__ q,
                                                    int64_t n_vert, const double *__restrict__ v,
                                                    double radius, int max_out,
@@ -699,10 +700,13 @@ __global__ __launch_bounds__(256) void k_neighbors(int64_t n_query, const double
 #pragma unroll
     for (int k = 0; k < 8; k++) qq[k] = q[8 * qi + k];
     int base = 0;
-    for (int64_t j0 = 0; j0 < n_vert; j0 += blockDim.x) {
-      const int64_t j = j0 + threadIdx.x;
+    const int m = n_vert > 0 ? um_epoch(n_vert) : 0;
+    for (int64_t p0 = 0; p0 < n_vert; p0 += blockDim.x) {
+      const int64_t p = p0 + threadIdx.x;
       bool hit = false;
-      if (j < n_vert) {
+      int64_t j = 0;
+      if (p < n_vert) {
+        j = um_key_at(p, n_vert, m);
         const double d = state_distance(qq, v + 8 * j);
         hit = (d <= radius) && (d > 0);
       }
@@ -1573,6 +1577,20 @@ int gbp_neighbors_batch_dev(int64_t n_query, const double *queries, int64_t n_ve
   hipLaunchKernelGGL(k_neighbors, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_query, queries,
                      n_vert, vertices, radius, max_out, out, count);
   HIPCHK(hipGetLastError());
+  return GBP_OK;
+}
+
+int gbp_vertex_map_order(int64_t n, int32_t *out) {
+  if (n < 0 || n > 0x7FFFFFFF || (n > 0 && !out)) return GBP_E_INVALID_ARG;
+  if (n == 0) return GBP_OK;
+  const int m = um_epoch(n);
+  for (int64_t p = 0; p < n; p++) out[p] = (int32_t)um_key_at(p, n, m);
+  return GBP_OK;
+}
+
+int gbp_vertex_map_rank(int64_t key, int64_t n, int64_t *rank) {
+  if (n < 1 || n > 0x7FFFFFFF || key < 0 || key >= n || !rank) return GBP_E_INVALID_ARG;
+  *rank = um_rank(key, n);
   return GBP_OK;
 }
 

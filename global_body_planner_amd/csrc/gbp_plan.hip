@@ -60,6 +60,7 @@
 #include "gbp_device.h"
 #include "gbp_internal.h"
 #include "gbp_lane.h"
+#include "gbp_um_order.h"
 
 using namespace gbp;
 static_assert(sizeof(gbp_plan_status) == 216, "engine.PlanStatus mirrors this layout");
@@ -178,8 +179,10 @@ struct gbp_plan_ws {
   int star = 0;
   double star_delta = 3.0;     // rrt_star_connect.h:59
   int64_t star_max_pairs = 0, star_max_shared = 0;
-  int32_t *scnt = nullptr;     // [bmax] neighbours per new vertex
-  int32_t *soff = nullptr;     // [bmax + 1] their offsets
+  int32_t *scnt = nullptr;     // [star_items] neighbours per scan item (k_star_count)
+  int32_t *sioff = nullptr;    // [star_items] the items' offsets
+  int32_t *soff = nullptr;     // [bmax + 1] each new vertex's first pair
+  int64_t star_items = 0;      // scan items per half (new vertex x position chunk)
   int32_t *snb = nullptr;      // [max_pairs] the neighbour of each pair
   int32_t *sown = nullptr;     // [max_pairs] its new vertex (k)
   int32_t *srowof = nullptr;   // [2 max_pairs] connect check -> pair-check row (-1: none)
@@ -1621,88 +1624,139 @@ __device__ __forceinline__ int block_sum_tb(int v, int *sh) {
   return t;
 }
 
-// stage 6a: neighbourhood sizes, one workgroup per new vertex
-__global__ __launch_bounds__(TB) void k_star_count(gbp_plan_status *st, const double *__restrict__ tv,
-                                                   double delta, int32_t *__restrict__ cnt,
-                                                   uint64_t seq) {
-  if (gated(st, seq)) return;
-  const int64_t n = st->n_added, base = st->added_base;
-  __shared__ int sh[TB / WAVE];
-  for (int64_t k = blockIdx.x; k < n; k += gridDim.x) {
-    const int64_t idx = base + k;
-    double q[8];
-    copy8(q, tv + 8 * idx);
-    int c = 0;
-    for (int64_t j = threadIdx.x; j < idx; j += TB) {
-      const double d = state_distance(q, tv + 8 * j);  // planner_class.cpp:178
-      c += (d <= delta && d > 0) ? 1 : 0;
-    }
-    c = block_sum_tb(c, sh);
-    if (threadIdx.x == 0) cnt[k] = c;
+// The neighbourhoods are scanned in the vertex map's iteration order
+// (gbp_um_order.h: new vertex k sees keys 0..base+k, position p holding key
+// um_key_at(p, base+k+1)), split into chunks of `ch` positions: item
+// (k, c) = positions [c·ch, (c+1)·ch) of vertex k, k-major, so concatenating the
+// items' hits in item order lists each vertex's neighbours in the reference's
+// order.  A half adds a few vertices to trees of tens of thousands: one
+// workgroup per vertex (the round-5 form) left nearly every CU idle.
+constexpr int64_t STAR_CH = 1024;  // positions per item (grown until the items fit)
+
+__device__ __forceinline__ void star_chunking(int64_t n_added, int64_t base, int64_t cap_items,
+                                              int64_t &ch, int64_t &nch) {
+  const int64_t nv = base + n_added;
+  ch = STAR_CH;
+  nch = (nv + ch - 1) / ch;
+  while (n_added * nch > cap_items) {
+    ch *= 2;
+    nch = (nv + ch - 1) / ch;
   }
 }
 
-// stage 6b: the pairs' offsets (exclusive scan), one workgroup
-__global__ __launch_bounds__(RB) void k_star_scan(gbp_plan_status *st, const int32_t *__restrict__ cnt,
-                                                  int32_t *__restrict__ off, int64_t max_pairs,
-                                                  int32_t half, uint64_t seq) {
+// stage 6a: hits per item
+__global__ __launch_bounds__(TB) void k_star_count(gbp_plan_status *st, const double *__restrict__ tv,
+                                                   double delta, int32_t *__restrict__ cnt,
+                                                   int64_t cap_items, uint64_t seq) {
   if (gated(st, seq)) return;
-  const int64_t n = st->n_added;
-  const int64_t ch = (n + RB - 1) / RB;
-  const int64_t lo = threadIdx.x * ch, hi = min<int64_t>(n, lo + ch);
+  const int64_t n = st->n_added, base = st->added_base;
+  int64_t ch, nch;
+  star_chunking(n, base, cap_items, ch, nch);
+  __shared__ int sh[TB / WAVE];
+  for (int64_t it = blockIdx.x; it < n * nch; it += gridDim.x) {
+    const int64_t k = it / nch, c = it - k * nch;
+    const int64_t nk = base + k + 1;  // the map holds keys 0..base+k (rrt_star_connect.cpp:22)
+    const int m = um_epoch(nk);
+    double q[8];
+    copy8(q, tv + 8 * (base + k));
+    const int64_t p1 = min<int64_t>((c + 1) * ch, nk);
+    int hits = 0;
+    for (int64_t p = c * ch + threadIdx.x; p < p1; p += TB) {
+      const int64_t j = um_key_at(p, nk, m);
+      const double d = state_distance(q, tv + 8 * j);  // planner_class.cpp:178
+      hits += (d <= delta && d > 0) ? 1 : 0;
+    }
+    hits = block_sum_tb(hits, sh);
+    if (threadIdx.x == 0) cnt[it] = hits;
+  }
+}
+
+// stage 6b: the items' offsets (exclusive scan, k-major) and each vertex's
+// first pair, one workgroup
+__global__ __launch_bounds__(RB) void k_star_scan(gbp_plan_status *st, const int32_t *__restrict__ cnt,
+                                                  int32_t *__restrict__ ioff, int32_t *__restrict__ off,
+                                                  int64_t max_pairs, int64_t cap_items, int32_t half,
+                                                  uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t n = st->n_added, base = st->added_base;
+  int64_t ch, nch;
+  star_chunking(n, base, cap_items, ch, nch);
+  const int64_t N = n * nch;
+  const int64_t per = (N + RB - 1) / RB;
+  const int64_t lo = min<int64_t>(N, threadIdx.x * per), hi = min<int64_t>(N, lo + per);
   int64_t sum = 0;
   for (int64_t i = lo; i < hi; i++) sum += cnt[i];
-  __shared__ int64_t part[RB];
-  part[threadIdx.x] = sum;
+  // block-wide exclusive scan of the threads' sums: waves, then the wave totals
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  int64_t inc = sum;
+  for (int o = 1; o < WAVE; o <<= 1) {
+    const int64_t u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  __shared__ int64_t wt[RB / WAVE + 1];
+  if (lane == WAVE - 1) wt[w] = inc;
   __syncthreads();
   if (threadIdx.x == 0) {
     int64_t run = 0;
-    for (int i = 0; i < RB; i++) {
-      const int64_t v = part[i];
-      part[i] = run;
+    for (int i = 0; i < RB / WAVE; i++) {
+      const int64_t v = wt[i];
+      wt[i] = run;
       run += v;
     }
-    off[n] = (int32_t)min<int64_t>(run, 0x7FFFFFFF);
-    st->star_pairs = (int32_t)min<int64_t>(run, 0x7FFFFFFF);
+    wt[RB / WAVE] = run;
+  }
+  __syncthreads();
+  const int64_t total = wt[RB / WAVE];
+  int64_t run = wt[w] + inc - sum;
+  for (int64_t i = lo; i < hi; i++) {
+    const int32_t o = (int32_t)min<int64_t>(run, 0x7FFFFFFF);
+    ioff[i] = o;
+    if (i % nch == 0) off[i / nch] = o;  // vertex i / nch starts here
+    run += cnt[i];
+  }
+  if (threadIdx.x == 0) {
+    off[n] = (int32_t)min<int64_t>(total, 0x7FFFFFFF);
+    st->star_pairs = (int32_t)min<int64_t>(total, 0x7FFFFFFF);
     st->star_rows = 0;
     st->star_vrows = 0;
-    st->stat_star_connects += 2 * run;  // a choose-parent and a rewire connect per pair
-    if (run > max_pairs) {
+    st->stat_star_connects += 2 * total;  // a choose-parent and a rewire connect per pair
+    if (total > max_pairs) {
       atomicOr(&st->error, 4u);
       raise_gate(st, seq);
     }
   }
-  __syncthreads();
-  int64_t run = part[threadIdx.x];
-  for (int64_t i = lo; i < hi; i++) {
-    off[i] = (int32_t)min<int64_t>(run, 0x7FFFFFFF);
-    run += cnt[i];
-  }
 }
 
-// stage 6c: the neighbour lists in ascending index (a workgroup per new vertex)
+// stage 6c: the neighbour lists, each item's hits in position order at its offset
 __global__ __launch_bounds__(TB) void k_star_fill(gbp_plan_status *st, const double *__restrict__ tv,
-                                                  double delta, const int32_t *__restrict__ off,
+                                                  double delta, const int32_t *__restrict__ ioff,
                                                   int32_t *__restrict__ nb, int32_t *__restrict__ own,
-                                                  uint64_t seq) {
+                                                  int64_t cap_items, uint64_t seq) {
   if (gated(st, seq)) return;
   const int64_t n = st->n_added, base = st->added_base;
+  int64_t ch, nch;
+  star_chunking(n, base, cap_items, ch, nch);
   const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
   __shared__ int wc[TB / WAVE];
-  for (int64_t k = blockIdx.x; k < n; k += gridDim.x) {
-    const int64_t idx = base + k;
+  for (int64_t it = blockIdx.x; it < n * nch; it += gridDim.x) {
+    const int64_t k = it / nch, c = it - k * nch;
+    const int64_t nk = base + k + 1;
+    const int m = um_epoch(nk);
     double q[8];
-    copy8(q, tv + 8 * idx);
-    int64_t run = off[k];
-    for (int64_t j0 = 0; j0 < idx; j0 += TB) {
-      const int64_t j = j0 + threadIdx.x;
+    copy8(q, tv + 8 * (base + k));
+    const int64_t p1 = min<int64_t>((c + 1) * ch, nk);
+    int64_t run = ioff[it];
+    for (int64_t p0 = c * ch; p0 < p1; p0 += TB) {
+      const int64_t p = p0 + threadIdx.x;
       bool hit = false;
-      if (j < idx) {
+      int64_t j = 0;
+      if (p < p1) {
+        j = um_key_at(p, nk, m);
         const double d = state_distance(q, tv + 8 * j);
         hit = d <= delta && d > 0;
       }
-      const unsigned long long m = __ballot(hit);
-      if (lane == 0) wc[w] = __popcll(m);
+      const unsigned long long bm = __ballot(hit);
+      if (lane == 0) wc[w] = __popcll(bm);
       __syncthreads();
       int before = 0, total = 0;
       for (int i = 0; i < TB / WAVE; i++) {
@@ -1710,9 +1764,9 @@ __global__ __launch_bounds__(TB) void k_star_fill(gbp_plan_status *st, const dou
         total += wc[i];
       }
       if (hit) {
-        const int64_t p = run + before + __popcll(m & ((1ull << lane) - 1ull));
-        nb[p] = (int32_t)j;
-        own[p] = (int32_t)k;
+        const int64_t at = run + before + __popcll(bm & ((1ull << lane) - 1ull));
+        nb[at] = (int32_t)j;
+        own[at] = (int32_t)k;
       }
       run += total;
       __syncthreads();
@@ -2077,6 +2131,37 @@ __global__ void k_tree_append(gbp_tree t, int64_t n, const double *__restrict__ 
   *t.count = c;
 }
 
+// gbp_tree_load_host: the given vertices, successor lists, then g from the
+// root down through the two level queues (one lane: a test's warm start)
+__global__ void k_tree_load(gbp_tree t, int64_t n, const double *__restrict__ s,
+                            const double *__restrict__ a, const int32_t *__restrict__ p) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  for (int64_t i = 0; i < n; i++) {
+    copy8(t.v + 8 * i, s + 8 * i);
+    nn_put_hrow(t.vh, t.hm, i, s + 8 * i, i == 0);
+    copy10(t.a + 10 * i, a + 10 * i);
+    t.parent[i] = p[i];
+    t.child[i] = -1;
+    t.sibling[i] = -1;
+  }
+  for (int64_t i = 1; i < n; i++) {
+    t.sibling[i] = t.child[p[i]];
+    t.child[p[i]] = (int32_t)i;
+  }
+  int32_t *q = t.bfs;
+  int64_t qh = 0, qt = 0;
+  t.g[0] = 0.0;
+  q[qt++] = 0;
+  while (qh < qt) {
+    const int32_t u = q[qh++];
+    for (int32_t c = t.child[u]; c >= 0 && qt < n; c = t.sibling[c]) {
+      t.g[c] = t.g[u] + pose_distance(t.v + 8 * (int64_t)u, t.v + 8 * (int64_t)c);
+      q[qt++] = c;
+    }
+  }
+  *t.count = (int32_t)n;
+}
+
 __global__ void k_plan_reset(gbp_plan_status *st, int64_t ext_counter, gbp_plan_la *la) {
   *la = gbp_plan_la{};  // no drawn-ahead targets, empty snapshots
   gbp_plan_status z;
@@ -2345,13 +2430,13 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
                        next_epoch(w), half, T->cap, ++w->seq, T->child, T->sibling, w->star);
   if (w->star && run(6)) {
     // RRT* insertion, stage 6: neighbourhoods, connect checks, their pair checks
-    const unsigned gk = (unsigned)std::max<int64_t>(1, std::min<int64_t>(batch, cus * 8));
+    const unsigned gk = (unsigned)std::max<int64_t>(1, std::min<int64_t>(w->star_items, cus * 8));
     hipLaunchKernelGGL(k_star_count, dim3(gk), dim3(TB), 0, s, st, T->v, w->star_delta, w->scnt,
-                       ++w->seq);
-    hipLaunchKernelGGL(k_star_scan, dim3(1), dim3(RB), 0, s, st, w->scnt, w->soff,
-                       w->star_max_pairs, half, ++w->seq);
-    hipLaunchKernelGGL(k_star_fill, dim3(gk), dim3(TB), 0, s, st, T->v, w->star_delta, w->soff, w->snb,
-                       w->sown, ++w->seq);
+                       w->star_items, ++w->seq);
+    hipLaunchKernelGGL(k_star_scan, dim3(1), dim3(RB), 0, s, st, w->scnt, w->sioff, w->soff,
+                       w->star_max_pairs, w->star_items, half, ++w->seq);
+    hipLaunchKernelGGL(k_star_fill, dim3(gk), dim3(TB), 0, s, st, T->v, w->star_delta, w->sioff,
+                       w->snb, w->sown, w->star_items, ++w->seq);
     const int64_t rmax = 2 * w->star_max_pairs;
     hipLaunchKernelGGL(k_star_prep, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, T->v,
                        direction, w->snb, w->sown, w->srowof, w->sritem, w->srs, w->sra, ++w->seq);
@@ -2627,6 +2712,47 @@ int gbp_tree_append_host(gbp_tree *t, int64_t n, const double *states, const dou
   return rc;
 }
 
+int gbp_tree_load_host(gbp_tree *t, int64_t n, const double *states, const double *actions,
+                       const int32_t *parents, gbp_stream stream) {
+  if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
+  if (n < 1 || n > 0x7FFFFFFE || !states || !actions || !parents || parents[0] != -1)
+    return GBP_E_INVALID_ARG;
+  // one tree rooted at 0: every parent in range, every vertex reached from the root
+  {
+    std::vector<int32_t> head(n, -1), next(n, -1), queue;
+    for (int64_t i = 1; i < n; i++) {
+      if (parents[i] < 0 || parents[i] >= n || parents[i] == i) return GBP_E_INVALID_ARG;
+      next[i] = head[parents[i]];
+      head[parents[i]] = (int32_t)i;
+    }
+    queue.reserve(n);
+    queue.push_back(0);
+    for (size_t h = 0; h < queue.size() && (int64_t)queue.size() <= n; h++)
+      for (int32_t c = head[queue[h]]; c >= 0; c = next[c]) queue.push_back(c);
+    if ((int64_t)queue.size() != n) return GBP_E_INVALID_ARG;
+  }
+  int rc = GBP_OK;
+  if (n > t->cap) rc = gbp_tree_reserve(t, n, stream);
+  if (rc) return rc;
+  Guard g(t->device);
+  hipStream_t s = (hipStream_t)stream;
+  void *buf = nullptr;
+  HIPCHK_P(hipMalloc(&buf, (size_t)n * (64 + 80 + 4) + 512));
+  char *p = (char *)buf;
+  double *ds = carve<double>(p, 8 * n), *da = carve<double>(p, 10 * n);
+  int32_t *dp = carve<int32_t>(p, n);
+  rc = h2d(ds, states, 8 * n, s);
+  if (!rc) rc = h2d(da, actions, 10 * n, s);
+  if (!rc) rc = h2d(dp, parents, n, s);
+  if (!rc) {
+    hipLaunchKernelGGL(k_tree_load, dim3(1), dim3(1), 0, s, *t, n, ds, da, dp);
+    if (hipGetLastError() != hipSuccess) rc = GBP_E_HIP;
+  }
+  if (hipStreamSynchronize(s) != hipSuccess && !rc) rc = GBP_E_HIP;
+  (void)hipFree(buf);
+  return rc;
+}
+
 int gbp_tree_device_ptrs(gbp_tree *t, double **states, int32_t **count) {
   if (!tree_ok(t)) return GBP_E_BAD_HANDLE;
   if (states) *states = t->v;
@@ -2813,16 +2939,19 @@ int gbp_plan_star_config(gbp_plan_ws *w, int enable, double delta, int64_t max_p
   }
   if (!w->star_block) {
     const int64_t b = w->bmax, r = 2 * max_pairs;
-    const size_t bytes = 4 * b + 4 * (b + 1) + 8 * max_pairs + r * (4 + 4 + 64 + 80 + 4) + 4 * b +
-                         8 * max_shared + 16 * 256;
+    const int64_t items = std::max<int64_t>(4 * b, 1 << 15);
+    const size_t bytes = 8 * items + 4 * (b + 1) + 8 * max_pairs + r * (4 + 4 + 64 + 80 + 4) +
+                         4 * b + 8 * max_shared + 16 * 256;
     if (hipMalloc(&w->star_block, bytes) != hipSuccess) {
       w->star_block = nullptr;
       w->star = 0;
       return GBP_E_ALLOC;
     }
     char *p = (char *)w->star_block;
-    w->scnt = carve<int32_t>(p, b);
+    w->scnt = carve<int32_t>(p, items);
+    w->sioff = carve<int32_t>(p, items);
     w->soff = carve<int32_t>(p, b + 1);
+    w->star_items = items;
     w->snb = carve<int32_t>(p, max_pairs);
     w->sown = carve<int32_t>(p, max_pairs);
     w->srowof = carve<int32_t>(p, r);

@@ -5,6 +5,7 @@
 // sampling goes through include/gbp.h (the HIP engine): there is no CPU
 // evaluation of the validity path here.
 #include "gbp_planner.h"
+#include "../gbp_um_order.h"
 
 #include <algorithm>
 #include <cmath>
@@ -794,6 +795,14 @@ std::vector<std::vector<int>> PlannerClass::neighborhoodDistBatch(const std::vec
       for (int k = 0; k < std::min<int>(cnt[i], max_out); k++) {
         const int v = lst[(size_t)i * max_out + k];
         if (v < lim) out[i].push_back(v);
+      }
+      // the engine lists them in the order the map of all V vertices iterates;
+      // RRT*'s vertex `lim` saw the map of keys 0..lim (rrt_star_connect.cpp:22-28)
+      if (!limit.empty()) {
+        const int64_t n_eff = (int64_t)lim + 1;
+        std::stable_sort(out[i].begin(), out[i].end(), [n_eff](int a, int b) {
+          return gbp::um_rank(a, n_eff) < gbp::um_rank(b, n_eff);
+        });
       }
     }
     break;
@@ -1606,6 +1615,11 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
     const int64_t wn = st.warm_n[k];
     if (wn > 0 && (!st.warm_v[k] || !st.warm_a[k] || !st.warm_parent[k] || st.warm_parent[k][0] != -1))
       throw EngineError(GBP_E_INVALID_ARG, "warm start: tree arrays");
+    // an RRT-Connect tree: every vertex's parent was added before it (the
+    // oracle's warm start refuses anything else, orc_plan)
+    for (int64_t i = 1; i < wn; i++)
+      if (st.warm_parent[k][i] < 0 || st.warm_parent[k][i] >= i)
+        throw EngineError(GBP_E_INVALID_ARG, "warm start: a parent after its child");
     chk(gbp_tree_create(dev, std::max<int64_t>(cap, 2 * wn), &D.tree[k]), "tree");
     const double *root = wn > 0 ? st.warm_v[k] : (k == 0 ? s_start.data() : s_goal.data());
     chk(gbp_tree_init(D.tree[k], root, D.stream), "tree init");
@@ -2199,18 +2213,33 @@ bool RRTStarConnectClass::buildRRTStarConnectDevice(FastTerrainMap &terrain, Sta
   chk(gbp_plan_star_config(D.ws, 1, delta, std::max<int64_t>(1 << 18, 8 * (int64_t)batch), 1 << 22),
       "star config");
   int64_t cap = std::max<int64_t>(1 << 16, 4 * (int64_t)batch);
-  for (int k = 0; k < 2; k++) chk(gbp_tree_create(dev, cap, &D.tree[k]), "tree");
-  chk(gbp_tree_init(D.tree[0], s_start.data(), D.stream), "tree init");
-  chk(gbp_tree_init(D.tree[1], s_goal.data(), D.stream), "tree init");
-  chk(gbp_plan_reset(D.ws, extend_counter_, D.stream), "plan reset");
   int64_t known[2] = {1, 1};
+  for (int k = 0; k < 2; k++) {
+    // warm start (a replayable continuation): the given trees, rewired parents included
+    const int64_t wn = st.warm_n[k];
+    if (wn > 0 && (!st.warm_v[k] || !st.warm_a[k] || !st.warm_parent[k]))
+      throw EngineError(GBP_E_INVALID_ARG, "warm start: tree arrays");
+    chk(gbp_tree_create(dev, std::max<int64_t>(cap, 2 * wn), &D.tree[k]), "tree");
+    if (wn > 0)
+      chk(gbp_tree_load_host(D.tree[k], wn, st.warm_v[k], st.warm_a[k], st.warm_parent[k], D.stream),
+          "warm start: tree load");
+    else
+      chk(gbp_tree_init(D.tree[k], k == 0 ? s_start.data() : s_goal.data(), D.stream), "tree init");
+    known[k] = std::max<int64_t>(1, wn);
+  }
+  if (st.warm_half < 0 || (st.warm_half & 1) || st.warm_extend < 0)
+    throw EngineError(GBP_E_INVALID_ARG, "warm start");
+  const int32_t half0 = (int32_t)st.warm_half;
+  if (st.warm_n[0] > 0 || st.warm_n[1] > 0 || half0 > 0) extend_counter_ = st.warm_extend;
+  chk(gbp_plan_reset(D.ws, extend_counter_, D.stream), "plan reset");
   const uint64_t tstream[2] = {401, 402};  // buildRRTStarConnectBatched's streams
   const int g_max = (int)std::max<int64_t>(2, std::min<int64_t>(64, (1 << 21) / batch)) & ~1;
   int group = 2;
-  int32_t half = 0;
+  int32_t half = half0;
   gbp_plan_status ps{};
-  while (since() < max_time && (st.max_halves <= 0 || half + 2 <= st.max_halves)) {
-    if (st.max_halves > 0) group = (int)std::min<int64_t>(group, (st.max_halves - half) & ~1LL);
+  while (since() < max_time && (st.max_halves <= 0 || half - half0 + 2 <= st.max_halves)) {
+    if (st.max_halves > 0)
+      group = (int)std::min<int64_t>(group, (st.max_halves - (half - half0)) & ~1LL);
     for (int k = 0; k < 2; k++) {
       int64_t c = 0;
       chk(gbp_tree_capacity(D.tree[k], &c), "tree capacity");
@@ -2258,8 +2287,8 @@ bool RRTStarConnectClass::buildRRTStarConnectDevice(FastTerrainMap &terrain, Sta
   }
   extend_counter_ = ps.ext_counter;
   rewires_ = ps.stat_rewires;
-  st.halves += half;
-  st.iterations += half / 2;
+  st.halves += half - half0;
+  st.iterations += (half - half0) / 2;
   st.targets += ps.stat_targets;
   st.extends += ps.stat_targets;
   st.attempts_checked += ps.stat_attempts;
@@ -2346,9 +2375,11 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     BatchStats st;
     TreeDump dump;
     st.max_halves = p->max_halves > 0 ? p->max_halves : 0;
-    if (p->algorithm == 3) {  // one device search per rank: the ranks' polls pair up
-      st.stop_poll = p->stop_poll;
-      st.stop_ctx = p->stop_ctx;
+    if (p->algorithm == 3 || p->algorithm == 5) {
+      if (p->algorithm == 3) {  // one device search per rank: the ranks' polls pair up
+        st.stop_poll = p->stop_poll;
+        st.stop_ctx = p->stop_ctx;
+      }
       for (int k = 0; k < 2; k++) {  // warm start (a replayable continuation)
         st.warm_n[k] = p->init_n[k];
         st.warm_v[k] = p->init_v[k];

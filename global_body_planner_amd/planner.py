@@ -143,12 +143,14 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     stop_poll: algorithm 3 — f(local_stop, found) -> bool called after every
       group of half-iterations; True stops the search (sharding.stop_together:
       config 4's ranks stop at the first solution of any of them);
-    init_trees, first_half, extend_base: algorithm 3 — a warm start, the
-      continuation of a search: init_trees = (a, b) dicts of v [n][8], act
-      [n][10], parent [n] (root first, -1; parents before children), the first
-      half-iteration (its targets are the draws a search from the roots makes
-      there) and the candidate stream's first extend index; max_halves then
-      counts the continuation's halves."""
+    init_trees, first_half, extend_base: algorithms 3 and 5 — a warm start,
+      the continuation of a search: init_trees = (a, b) dicts of v [n][8], act
+      [n][10], parent [n] (root first, -1; algorithm 3: parents before
+      children; algorithm 5: any tree rooted at 0, since rewiring gives
+      vertices later parents), the first half-iteration (its targets are the
+      draws a search from the roots makes there; even for algorithm 5) and the
+      candidate stream's first extend index; max_halves then counts the
+      continuation's halves."""
     L = load()
     x = np.ascontiguousarray(data.x, dtype=np.float64)
     y = np.ascontiguousarray(data.y, dtype=np.float64)

@@ -346,14 +346,25 @@ int gbp_nearest_batch_host(int64_t n_query, const double *queries, int64_t n_ver
 /* ---- radius neighbourhood (PlannerClass::neighborhoodDist,
  *      planner_class.cpp:173-182; used by RRT*-Connect, rrt_star_connect.cpp:28)
  * out[i][0..max_out): the vertices with 0 < stateDistance(query_i, v) <= radius
- * in ascending index (the reference: unordered_map order);
- * count[i] = how many there are (entries beyond max_out are not written). */
+ * in the order the reference's vertex map holding keys 0..n_vert-1 iterates
+ * them (gbp_vertex_map_order); count[i] = how many there are (entries beyond
+ * max_out are not written). */
 int gbp_neighbors_batch_dev(int64_t n_query, const double *queries, int64_t n_vert,
                             const double *vertices, double radius, int max_out, int32_t *out,
                             int32_t *count, gbp_stream stream);
 int gbp_neighbors_batch_host(int64_t n_query, const double *queries, int64_t n_vert,
                              const double *vertices, double radius, int max_out, int32_t *out,
                              int32_t *count);
+
+/* ---- the reference vertex map's iteration order ------------------------------
+ * GraphClass stores a tree's vertices in std::unordered_map<int, State>
+ * (graph_class.h:155) filled with keys 0, 1, ... (graph_class.cpp:28-31) and
+ * neighborhoodDist / RRT*'s choose-parent and rewire loops follow its iteration
+ * order (planner_class.cpp:176-179, rrt_star_connect.cpp:31-64).  The order is
+ * libstdc++'s (GCC 11.4): out[n] = the keys 0..n-1 as iterated; *rank = the
+ * position of `key` (0 <= key < n).  Host functions, no device needed. */
+int gbp_vertex_map_order(int64_t n, int32_t *out);
+int gbp_vertex_map_rank(int64_t key, int64_t n, int64_t *rank);
 
 /* ---- k nearest (PlannerClass::neighborhoodN, planner_class.cpp:151-171) ----
  * out[i][0..k), k = min(n_nearest, n_vert): the vertices of smallest
@@ -414,6 +425,14 @@ int gbp_tree_read(gbp_tree *tree, int64_t first, int64_t n, double *states, doub
  * the device; parents may name vertices appended earlier in the same call */
 int gbp_tree_append_host(gbp_tree *tree, int64_t n, const double *states, const double *actions,
                          const int32_t *parents, gbp_stream stream);
+/* replaces the tree with n >= 1 given vertices: an RRT*-Connect tree, whose
+ * rewiring gives vertices parents added after them (rrt_star_connect.cpp:55-62).
+ * parents[0] = -1, every other parent in [0, n) and the whole a tree rooted at
+ * vertex 0 (else GBP_E_INVALID_ARG, nothing changed); g is derived on the
+ * device from the root down (graph_class.cpp:131-138 keeps g[c] = g[parent] +
+ * poseDistance).  Synchronises the stream. */
+int gbp_tree_load_host(gbp_tree *tree, int64_t n, const double *states, const double *actions,
+                       const int32_t *parents, gbp_stream stream);
 /* PlannerClass::getNearestNeighbor (planner_class.cpp:185-200) for n device
  * queries[n][8] against the tree (count read on the device): index[n], ties to
  * the lowest index like gbp_nearest_batch_dev.  Uses ws's status and scratch

@@ -76,6 +76,10 @@ def lib():
             "orc_extend_batch": (None, [P, I64, P, P, P, P, I, I, P, P, P, P, P, I]),
             "orc_nearest_batch": (None, [I64, P, I, P, P, P, I]),
             "orc_neighbors_batch": (None, [I64, P, I, P, D, I, P, P, I]),
+            "orc_neighbors_batch_ordered": (None, [I64, P, I, P, D, I, P, P, I, I]),
+            "orc_um_rank": (I64, [I64, I64]),
+            "orc_um_order": (None, [I64, P]),
+            "orc_star_insert_one": (I, [P, P, I, I, P, D, I, I, I, P]),
             "orc_knn_batch": (None, [I64, P, I, P, I, P, P, I]),
             "orc_knn_yaw_batch": (None, [I64, P, I, P, I, I, D, D, P, P, I]),
             "orc_state_distance_yaw": (D, [P, P, I, D, D]),
@@ -119,7 +123,8 @@ class _PlanCfg(ctypes.Structure):
                 ("action_p", ctypes.c_double), ("extend_base", ctypes.c_int64),
                 ("max_halves", ctypes.c_int64), ("star", ctypes.c_int),
                 ("star_delta", ctypes.c_double), ("nthreads", ctypes.c_int),
-                ("first_half", ctypes.c_int64), ("warm", ctypes.c_int)]
+                ("first_half", ctypes.c_int64), ("warm", ctypes.c_int),
+                ("star_order", ctypes.c_int)]
 
 
 class _PlanOut(ctypes.Structure):
@@ -268,7 +273,8 @@ class OracleTerrain:
 
     def plan(self, start, goal, *, batch, seed, stream_a=101, stream_b=102, max_halves=0,
              adaptive=False, sampling=None, star=False, star_delta=3.0, extend_base=0,
-             capacity=200000, nthreads=1, init_trees=None, first_half=0):
+             capacity=200000, nthreads=1, init_trees=None, first_half=0,
+             star_order="reference"):
         """The batch-synchronous RRT-Connect (RRT*-Connect with star=True) the
         engine runs, restated on the CPU (orc_plan): returns a dict with the
         counters, the meeting / best vertices, and each tree's arrays
@@ -278,7 +284,10 @@ class OracleTerrain:
         (same result for any count: insertion stays in order).
         init_trees / first_half: a warm start (the continuation of a search):
         (a, b) dicts of v [n][8], act [n][10], parent [n] (root first, -1),
-        the first half-iteration; max_halves counts the continuation's."""
+        the first half-iteration; max_halves counts the continuation's.
+        star_order: RRT* neighbourhoods in the vertex map's iteration order
+        ("reference", planner_class.cpp:176-179) or "ascending" index (the
+        pre-round-6 form, kept to show the two build different trees)."""
         trees, keep = [], []
         for k in range(2):
             arrs = dict(v=np.zeros((capacity, 8)), act=np.zeros((capacity, 10)),
@@ -303,7 +312,7 @@ class OracleTerrain:
                        int(bool(sm.get("action_flag", False))), float(sm.get("state_p", 0.0)),
                        float(sm.get("action_p", 0.0)), int(extend_base), int(max_halves),
                        int(bool(star)), float(star_delta), int(nthreads), int(first_half),
-                       int(init_trees is not None))
+                       int(init_trees is not None), {"reference": 0, "ascending": 1}[star_order])
         out = _PlanOut()
         st, gl = _c(start, np.float64), _c(goal, np.float64)
         rc = lib().orc_plan(self.ref, _p(st), _p(gl), ctypes.byref(cfg), tr, ctypes.byref(out))
@@ -317,6 +326,30 @@ class OracleTerrain:
             res["states"], res["actions"] = _join_path(res["a"], res["b"], res["meet_a"],
                                                        res["meet_b"])
         return res
+
+    def star_insert_one(self, v, parent, idx, nn, a_new, direction, delta=3.0,
+                        order="reference", adaptive=False):
+        """One RRT* insertion (rrt_star_connect.cpp:18-66, orc_star_insert_one):
+        v [idx+1][8] (vertex idx newly added), parent [idx] a tree rooted at 0,
+        nearest vertex nn, newConfig's action a_new.  Returns the tree after
+        choose-parent and rewire (v, act, parent, g, y) and the rewire count."""
+        v = _c(v, np.float64).reshape(-1, 8)
+        n = idx + 1
+        arrs = dict(v=v[:n].copy(), act=np.zeros((n, 10)), parent=np.full(n, -1, np.int32),
+                    g=np.zeros(n), y=np.zeros(n), child=np.zeros(n, np.int32),
+                    sibling=np.zeros(n, np.int32))
+        arrs["parent"][:idx] = np.asarray(parent, np.int32)[:idx]
+        arrs["act"][idx] = _c(a_new, np.float64)
+        t = _Tree(n, n, *(arrs[k].ctypes.data for k in
+                          ("v", "act", "parent", "g", "y", "child", "sibling")))
+        rw = ctypes.c_int64(0)
+        rc = lib().orc_star_insert_one(self.ref, ctypes.byref(t), int(idx), int(nn),
+                                       _p(arrs["act"][idx].copy()), float(delta), int(direction),
+                                       int(bool(adaptive)),
+                                       {"reference": 0, "ascending": 1}[order], ctypes.byref(rw))
+        if rc != 0:
+            raise RuntimeError(f"orc_star_insert_one returned {rc}")
+        return {k: arrs[k] for k in ("v", "act", "parent", "g", "y")}, rw.value
 
     def post_process_path(self, states, actions, adaptive=False):
         """rrt_connect.cpp:139-227 -> (states, actions, path_length_, path_yaw_, path_cost_)."""
@@ -395,15 +428,31 @@ def nearest_batch(queries, verts, nthreads=1):
     return idx, dist
 
 
-def neighbors_batch(queries, verts, radius, max_out=256, nthreads=1):
-    """planner_class.cpp:173-182, ascending index: (out [n, max_out] -1 padded, count [n])."""
+def neighbors_batch(queries, verts, radius, max_out=256, nthreads=1, order="reference"):
+    """planner_class.cpp:173-182 over a map holding the rows of `verts` as keys
+    0..n-1, in its iteration order ("reference") or ascending index:
+    (out [n, max_out] -1 padded, count [n])."""
     q = _c(queries, np.float64).reshape(-1, 8)
     v = _c(verts, np.float64).reshape(-1, 8)
     out = np.full((q.shape[0], max_out), -1, np.int32)
     cnt = np.empty(q.shape[0], np.int32)
-    lib().orc_neighbors_batch(q.shape[0], _p(q), v.shape[0], _p(v), float(radius), int(max_out),
-                              _p(out), _p(cnt), nthreads)
+    lib().orc_neighbors_batch_ordered(q.shape[0], _p(q), v.shape[0], _p(v), float(radius),
+                                      int(max_out), _p(out), _p(cnt),
+                                      {"reference": 0, "ascending": 1}[order], nthreads)
     return out, cnt
+
+
+def um_rank(keys, n):
+    """Positions of `keys` when a std::unordered_map<int, State> holding keys
+    0..n-1 (graph_class.h:155) is iterated (libstdc++, orc_um_rank)."""
+    return np.array([lib().orc_um_rank(int(k), int(n)) for k in np.atleast_1d(keys)], np.int64)
+
+
+def um_order(n):
+    """The keys 0..n-1 in that map's iteration order (orc_um_order)."""
+    out = np.empty(int(n), np.int32)
+    lib().orc_um_order(int(n), _p(out))
+    return out
 
 
 def knn_batch(queries, verts, n_nearest, nthreads=1):

@@ -741,20 +741,121 @@ void orc_nearest_batch(int64_t n_q, const double *q, int n_vert, const double *v
   }
 }
 
-/* PlannerClass::neighborhoodDist (planner_class.cpp:173-182): vertices with
- * stateDistance <= dist and > 0, in ascending index (the engine's order; the
- * reference iterates an unordered_map) */
+/* ---- the iteration order of GraphClass::vertices ----------------------------
+ * graph_class.h:155 keeps the vertices in a std::unordered_map<int, State>
+ * filled by operator[] with keys 0, 1, 2, ... (graph_class.cpp:28-31, :141-145;
+ * a tree is never erased from), and neighborhoodDist / getNearestNeighbor walk
+ * it begin() to end() (planner_class.cpp:176-179, :190-198).  libstdc++ (GCC
+ * 11.4, this image's g++; the third-party arithmetic SURVEY §8(c) names) keeps
+ * one singly linked list: a key whose bucket is empty is linked at the FRONT,
+ * and a rehash relinks the nodes in list order, each at the front of the new
+ * list — it reverses the list.  With int keys hashed to themselves and the load
+ * factor <= 1 every key below the bucket count has a bucket of its own, so the
+ * order of keys 0..n-1 is
+ *     order(n) = [n-1, n-2, ..., r] ++ reverse(order(r))
+ * where r is the last rehash point <= n-1: the element counts at which
+ * _Prime_rehash_policy::_M_need_rehash grows the table (the first insertion
+ * into the single-bucket empty map, then every time the size reaches the
+ * bucket count; bucket counts from __prime_list, growth factor 2).  The points
+ * below were read from libstdc++'s own policy object and are checked against a
+ * real std::unordered_map by tests/test_um_order.py. */
+static const int64_t UM_REHASH[] = {
+    0,        13,       29,        59,        127,       257,       541,
+    1109,     2357,     5087,      10273,     20753,     42043,     85229,
+    172933,   351061,   712697,    1447153,   2938679,   5967347,   12117689,
+    24607243, 49969847, 101473717, 206062531, 418451333, 849749479, 1725587117};
+#define UM_NREHASH ((int)(sizeof UM_REHASH / sizeof UM_REHASH[0]))
+
+/* index of the last rehash point <= n - 1 (n >= 1) */
+static int um_epoch(int64_t n) {
+  int m = 0;
+  while (m + 1 < UM_NREHASH && UM_REHASH[m + 1] <= n - 1) m++;
+  return m;
+}
+
+/* position of key k (0 <= k < n) when a map holding keys 0..n-1 is iterated */
+int64_t orc_um_rank(int64_t k, int64_t n) {
+  /* rank(k, n) = n-1-k in the front run, else n-1-rank(k, r): k's place in
+   * reverse(order(r)), which fills the last r places */
+  int64_t acc = 0, sign = 1;
+  for (;;) {
+    const int64_t r = UM_REHASH[um_epoch(n)];
+    if (k >= r) return acc + sign * (n - 1 - k);
+    acc += sign * (n - 1);
+    sign = -sign;
+    n = r;
+  }
+}
+
+/* the segments of order(n): key ranges [lo, hi) walked descending (desc = 1)
+ * or ascending, in iteration order; returns their count (<= UM_NREHASH) */
+static int um_segments(int64_t n, int64_t *lo, int64_t *hi, int *desc) {
+  if (n <= 0) return 0;
+  const int m = um_epoch(n);
+  int c = 0;
+  /* order(n) = desc[R_m, n) ++ desc[R_{m-2}, R_{m-1}) ++ ... ++ asc[R_{m-3}, R_{m-2}) ++ asc[R_{m-1}, R_m) */
+  for (int j = m; j >= 0; j -= 2) {
+    lo[c] = UM_REHASH[j];
+    hi[c] = j == m ? n : UM_REHASH[j + 1];
+    desc[c++] = 1;
+  }
+  for (int j = (m - 1) & 1; j <= m - 1; j += 2) {
+    lo[c] = UM_REHASH[j];
+    hi[c] = UM_REHASH[j + 1];
+    desc[c++] = 0;
+  }
+  return c;
+}
+
+/* the keys 0..n-1 in iteration order */
+void orc_um_order(int64_t n, int32_t *out) {
+  int64_t lo[2 * UM_NREHASH], hi[2 * UM_NREHASH];
+  int desc[2 * UM_NREHASH];
+  const int ns = um_segments(n, lo, hi, desc);
+  int64_t p = 0;
+  for (int s = 0; s < ns; s++) {
+    if (desc[s])
+      for (int64_t k = hi[s] - 1; k >= lo[s]; k--) out[p++] = (int32_t)k;
+    else
+      for (int64_t k = lo[s]; k < hi[s]; k++) out[p++] = (int32_t)k;
+  }
+}
+
+/* PlannerClass::neighborhoodDist (planner_class.cpp:173-182): the vertices
+ * 0..n_vert-1 with 0 < stateDistance <= dist, in the map's iteration order
+ * (order = 0) or ascending index (order = 1, the engine's form before round 6,
+ * kept for the tests that show the two differ) */
 void orc_neighbors_batch(int64_t n_q, const double *q, int n_vert, const double *verts,
                          double radius, int max_out, int32_t *out, int32_t *count, int nthreads) {
+  orc_neighbors_batch_ordered(n_q, q, n_vert, verts, radius, max_out, out, count, 0, nthreads);
+}
+
+void orc_neighbors_batch_ordered(int64_t n_q, const double *q, int n_vert, const double *verts,
+                                 double radius, int max_out, int32_t *out, int32_t *count,
+                                 int order, int nthreads) {
   if (nthreads <= 0) nthreads = 1;
+  int64_t lo[2 * UM_NREHASH], hi[2 * UM_NREHASH];
+  int desc[2 * UM_NREHASH];
+  int ns = 1;
+  if (order == 0) {
+    ns = um_segments(n_vert, lo, hi, desc);
+  } else {
+    lo[0] = 0;
+    hi[0] = n_vert;
+    desc[0] = 0;
+  }
   OMP_FOR
   for (int64_t i = 0; i < n_q; i++) {
     int c = 0;
-    for (int v = 0; v < n_vert; v++) {
-      if ((orc_state_distance(q + 8 * i, verts + (long)v * 8) <= radius) &&
-          orc_state_distance(q + 8 * i, verts + (long)v * 8) > 0) {
-        if (c < max_out) out[i * (int64_t)max_out + c] = v;
-        c++;
+    for (int s = 0; s < ns; s++) {
+      const int64_t len = hi[s] - lo[s];
+      for (int64_t t = 0; t < len; t++) {
+        const int64_t v = desc[s] ? hi[s] - 1 - t : lo[s] + t;
+        if ((orc_state_distance(q + 8 * i, verts + v * 8) <= radius) &&
+            orc_state_distance(q + 8 * i, verts + v * 8) > 0) {
+          if (c < max_out) out[i * (int64_t)max_out + c] = (int32_t)v;
+          c++;
+        }
       }
     }
     count[i] = c;
@@ -1332,17 +1433,23 @@ static int connect_reached(const orc_terrain *T, const double *s_existing, const
 
 /* rrt_star_connect.cpp:18-66 for the vertex `idx` just added to t (its
  * nearest `nn`, newConfig's action a_new): choose-parent among the vertices
- * before it within `delta` (planner_class.cpp:173-182, ascending index), then
- * rewire them through it */
+ * within `delta` — neighborhoodDist (planner_class.cpp:173-182) over the map
+ * that now holds keys 0..idx (addVertex at :22 precedes it), in the map's
+ * iteration order (order 0; 1 = ascending index) — then rewire them through
+ * it.  Both loops are order-dependent: a choose-parent tie goes to the first
+ * neighbour, and a rewire lowers the g of a whole subtree that a later
+ * neighbour's test (:59) then reads. */
 static void star_insert(const orc_terrain *T, orc_tree *t, int idx, int nn, const double *a_new,
-                        double delta, int direction, int adaptive, orc_plan_out *out) {
+                        double delta, int direction, int adaptive, int order, orc_plan_out *out) {
   const double *s_new = t->v + 8 * (int64_t)idx;
   const double *s_nearest = t->v + 8 * (int64_t)nn;
   int nb_n = 0;
   int *nb = (int *)malloc(sizeof(int) * (size_t)(idx > 0 ? idx : 1));
-  for (int j = 0; j < idx; j++) {
-    const double *vj = t->v + 8 * (int64_t)j;
-    if ((orc_state_distance(s_new, vj) <= delta) && orc_state_distance(s_new, vj) > 0) nb[nb_n++] = j;
+  {
+    int32_t cnt = 0;
+    /* the key idx itself is at distance 0 and never listed */
+    orc_neighbors_batch_ordered(1, s_new, idx + 1, t->v, delta, idx > 0 ? idx : 1, nb, &cnt, order, 1);
+    nb_n = cnt;
   }
   out->connects += 2 * (int64_t)nb_n; /* a choose-parent and a rewire connect per neighbour */
   int s_min = nn;
@@ -1389,6 +1496,52 @@ static void star_insert(const orc_terrain *T, orc_tree *t, int idx, int nn, cons
   free(nb);
 }
 
+/* vertices 0..n-1 of an RRT* tree given by parents alone (any tree rooted at
+ * 0): successor lists, then g / y from the root down (every updateGYValue
+ * keeps g[c] == g[parent] + poseDistance, graph_class.cpp:131-138, so these
+ * are the bits the grown tree holds); -1 if it is not one tree rooted at 0 */
+static int tree_derive_star(orc_tree *t, int n) {
+  if (!t->child || n < 1 || t->parent[0] != -1) return -1;
+  for (int i = 0; i < n; i++) t->child[i] = t->sibling[i] = -1;
+  for (int i = 1; i < n; i++) {
+    const int p = t->parent[i];
+    if (p < 0 || p >= n || p == i) return -1;
+    t->sibling[i] = t->child[p];
+    t->child[p] = i;
+  }
+  t->g[0] = t->y[0] = 0.0;
+  int *queue = (int *)malloc(sizeof(int) * (size_t)n);
+  int qh = 0, qt = 0;
+  queue[qt++] = 0;
+  while (qh < qt) {
+    const int p = queue[qh++];
+    const double *vp = t->v + 8 * (int64_t)p;
+    for (int c = t->child[p]; c >= 0; c = t->sibling[c]) {
+      if (qt >= n) break;
+      const double *vc = t->v + 8 * (int64_t)c;
+      t->g[c] = t->g[p] + orc_pose_distance(vp, vc);
+      t->y[c] = t->y[p] + orc_state_yaw_distance(vp, vc);
+      queue[qt++] = c;
+    }
+  }
+  free(queue);
+  return qt == n ? 0 : -1;
+}
+
+int orc_star_insert_one(const orc_terrain *T, orc_tree *t, int idx, int nn, const double *a_new,
+                        double delta, int direction, int adaptive, int order, int64_t *rewires) {
+  if (!t || idx < 1 || idx >= t->cap || nn < 0 || nn >= idx) return -1;
+  if (tree_derive_star(t, idx) != 0) return -1;
+  t->n = idx + 1;
+  t->parent[idx] = -1;
+  t->child[idx] = t->sibling[idx] = -1;
+  orc_plan_out out;
+  memset(&out, 0, sizeof out);
+  star_insert(T, t, idx, nn, a_new, delta, direction, adaptive, order, &out);
+  if (rewires) *rewires = out.rewires;
+  return 0;
+}
+
 int orc_plan(const orc_terrain *T, const double *start, const double *goal,
              const orc_plan_cfg *cfg, orc_tree *tr, orc_plan_out *out) {
   const int B = cfg->batch;
@@ -1406,10 +1559,15 @@ int orc_plan(const orc_terrain *T, const double *start, const double *goal,
       t->g[0] = t->y[0] = 0.0;
       for (int i = 0; i < t->n; i++)
         if (t->child) t->child[i] = t->sibling[i] = -1;
-      for (int i = 1; i < t->n; i++) {
-        if (t->parent[i] < 0 || t->parent[i] >= i) return -1;
-        tree_add_edge(t, t->parent[i], i);
+      if (!star) {
+        for (int i = 1; i < t->n; i++) {
+          if (t->parent[i] < 0 || t->parent[i] >= i) return -1;
+          tree_add_edge(t, t->parent[i], i);
+        }
+        continue;
       }
+      /* RRT*: rewiring gives vertices parents added after them */
+      if (tree_derive_star(t, t->n) != 0) return -1;
       continue;
     }
     tr[k].n = 0;
@@ -1508,7 +1666,7 @@ int orc_plan(const orc_terrain *T, const double *start, const double *goal,
     if (star) {
       for (int i = 0; i < n_added; i++)
         star_insert(T, Tt, added[i], nearest[i], a_ext + 10 * i, cfg->star_delta, dir, cfg->adaptive,
-                    out);
+                    cfg->star_order, out);
     }
     /* connect each new vertex to the other tree (rrt_connect.cpp:98-120) */
     const int m0 = O->n;

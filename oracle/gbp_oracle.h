@@ -114,8 +114,18 @@ void orc_extend_batch(const orc_terrain *T, int64_t n, const double *s_near,
                       uint32_t *counts, int nthreads);
 void orc_nearest_batch(int64_t n_q, const double *q, int n_vert, const double *verts,
                        int32_t *idx, double *dist, int nthreads);
+/* planner_class.cpp:173-182 in the vertex map's iteration order (see
+ * orc_um_order); the _ordered form takes order 1 = ascending index */
 void orc_neighbors_batch(int64_t n_q, const double *q, int n_vert, const double *verts,
                          double radius, int max_out, int32_t *out, int32_t *count, int nthreads);
+void orc_neighbors_batch_ordered(int64_t n_q, const double *q, int n_vert, const double *verts,
+                                 double radius, int max_out, int32_t *out, int32_t *count,
+                                 int order, int nthreads);
+/* libstdc++ std::unordered_map<int, State> filled with keys 0..n-1
+ * (graph_class.cpp:28-31): key k's position when iterated, and all n keys in
+ * iteration order */
+int64_t orc_um_rank(int64_t k, int64_t n);
+void orc_um_order(int64_t n, int32_t *out);
 
 /* planner_class.cpp:151-171 (neighborhoodN): ascending (distance, index) */
 /* planning_utils.h:146-155 and neighborhoodN with cost_add_yaw (glibc atan2) */
@@ -179,7 +189,10 @@ typedef struct {
                              /* results identical: insertion stays in order)           */
   int64_t first_half;        /* warm start: the first half-iteration (draw indices)    */
   int warm;                  /* warm start: tr[k].n vertices given (v, a, parent; root  */
-                             /* first, parents before children), g / y derived         */
+                             /* first, parents before children — RRT*: any tree rooted */
+                             /* at 0), g / y derived                                   */
+  int star_order;            /* RRT* neighbourhoods: 0 the vertex map's iteration order */
+                             /* (the reference), 1 ascending index (tests only)        */
 } orc_plan_cfg;
 
 typedef struct {
@@ -192,6 +205,15 @@ typedef struct {
   int best_a, best_b;        /* RRT*: the cheapest connection ranked after each iteration */
   double best_cost;
 } orc_plan_out;
+
+/* one RRT* insertion (rrt_star_connect.cpp:18-66): t holds vertices 0..idx
+ * (v), the parents of 0..idx-1 (a tree rooted at 0; g / y and the successor
+ * lists are derived), vertex idx newly added with nearest vertex nn and
+ * newConfig's action a_new; choose-parent and rewire update t's parent / a /
+ * g / y in place.  order: 0 the vertex map's iteration order, 1 ascending
+ * index.  Returns 0 or -1 (bad arguments). */
+int orc_star_insert_one(const orc_terrain *T, orc_tree *t, int idx, int nn, const double *a_new,
+                        double delta, int direction, int adaptive, int order, int64_t *rewires);
 
 /* tr[0] = Ta (start, FORWARD), tr[1] = Tb (goal, REVERSE); returns 0, -1 (bad
  * arguments) or -2 (a tree's capacity is exhausted) */

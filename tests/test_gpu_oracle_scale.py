@@ -157,3 +157,109 @@ def test_config3_scale_scan_list_overflow(gpu, monkeypatch):
                  first_half=GROW_HALVES, extend_base=grown["extends"], **warm)
     _compare(dev, ref)
     assert dev["nn_scans"] > 2 * 2 * CONT_HALVES  # more than the lists held
+
+
+# ---- config 5: RRT*-Connect on synth-fractal-4096 at the bench's own scale ------
+# (VERDICT r05 "next" #2).  bench.py's config5 runs 4096 draws per half for 10 s:
+# ~24.5k halves, trees of ~58k + 53k vertices, ~147k rewires.  The device grows
+# the trees past 40k vertices each; then the device and orc_plan(star) continue
+# from the same trees, bit for bit: neighbourhoods of ~60 vertices in the map's
+# iteration order over chunked scans, rewired subtrees' g updates through deep
+# subtrees (k_star_replay's subtree_g), the look-ahead search on RRT* trees.
+STAR_DRAWS = 4096
+STAR_SEED = 20251020
+STAR_GROW = 18000
+STAR_CONT = 24
+
+
+def _star_terrain():
+    if "f" not in _cache:
+        data = td.by_name("synth-fractal-4096")
+        _cache["f"] = (data, oracle.OracleTerrain.from_data(data))
+    oracle.set_scan_mode(1)
+    return _cache["f"]
+
+
+def _first_valid(O, x, y, step, n=400):
+    """tools/config5.py first_valid on the oracle: z = 0.375 + ground, v = (1, 0, 0)."""
+    xs = x + step * np.arange(n)
+    h, _, _ = O.height_batch(np.stack([xs, np.full(n, y)], 1))
+    st = np.zeros((n, 8))
+    st[:, 0], st[:, 1], st[:, 2], st[:, 3] = xs, y, 0.375 + h, 1.0
+    v, _, _ = O.valid_states(st, 1)
+    return st[int(np.argmax(v > 0))]
+
+
+def test_config5_star_scale_warm_continuation(gpu):
+    """Config 5's own scale: trees grown by the device past 40k vertices each
+    (STAR_GROW halves at 4096 draws), then STAR_CONT more halves from the
+    device (algorithm 5) and from orc_plan(star) — vertices, actions, parents,
+    g, rewires and the best connection bit for bit.  The warm start derives g
+    from the root down on both sides; that equals the grown trees' g (every
+    updateGYValue keeps g[c] = g[parent] + poseDistance), and the continuation
+    equals the uninterrupted device run."""
+    data, O = _star_terrain()
+    L = data.x[-1]
+    start = _first_valid(O, 1.0, L / 2, 0.02)
+    goal = _first_valid(O, 9.0, L / 2, -0.02)
+    cap = 1 << 17
+    t0 = time.time()
+    grown = planner.plan_rrt_star_connect(data, start, goal, batch=STAR_DRAWS, max_time=300.0,
+                                          seed=STAR_SEED, max_halves=STAR_GROW, trees=True,
+                                          tree_capacity=cap, device_loop=True)
+    t_grow = time.time() - t0
+    assert grown["halves"] == STAR_GROW
+    init = tuple({k: grown[t][k] for k in ("v", "act", "parent")} for t in "ab")
+    n0 = (len(init[0]["v"]), len(init[1]["v"]))
+    assert min(n0) > 40000, n0
+    # RRT* trees: rewiring gave vertices later parents
+    assert any(np.any(grown[t]["parent"][1:] > np.arange(1, len(grown[t]["parent"]))) for t in "ab")
+    warm = dict(batch=STAR_DRAWS, seed=STAR_SEED, max_halves=STAR_CONT)
+    dev = planner.plan_rrt_star_connect(data, start, goal, max_time=300.0, trees=True,
+                                        tree_capacity=cap, device_loop=True, init_trees=init,
+                                        first_half=STAR_GROW, extend_base=grown["extends"], **warm)
+    t0 = time.time()
+    ref = O.plan(start, goal, capacity=cap, nthreads=NTHREADS, init_trees=init, star=True,
+                 stream_a=401, stream_b=402, first_half=STAR_GROW, extend_base=grown["extends"],
+                 **warm)
+    t_ref = time.time() - t0
+    print(f"config 5: grown {STAR_GROW} halves in {t_grow:.2f} s: trees {n0[0]}+{n0[1]} "
+          f"({grown['rewires']} rewires); continuation {STAR_CONT} halves: "
+          f"+{len(ref['a']['v']) - n0[0]}+{len(ref['b']['v']) - n0[1]} vertices, "
+          f"{ref['rewires']} rewires, {ref['targets']} targets, {ref['attempts']} pair checks, "
+          f"{ref['solutions']} connections; device {dev['rewires']} rewires, "
+          f"{dev['fragile_resolved']} re-decided; oracle {t_ref:.1f} s on {NTHREADS} threads")
+    assert dev["halves"] == ref["halves"] == STAR_CONT
+    assert dev["rewires"] == ref["rewires"] > 0
+    assert dev["solutions"] == ref["solutions"]
+    assert_counters_equal(dev, ref)
+    assert_trees_equal(dev, ref)
+    if ref["best_a"] >= 0:
+        assert (dev["meet_a"], dev["meet_b"]) == (ref["best_a"], ref["best_b"])
+        assert dev["path_cost"] == ref["best_cost"]
+    # the warm start's g, derived from the root down, is the grown trees' g
+    for i, t in enumerate("ab"):
+        par, v = init[i]["parent"], init[i]["v"]
+        kids = [[] for _ in range(len(par))]
+        for c in range(1, len(par)):
+            kids[par[c]].append(c)
+        g = np.zeros(len(par))
+        queue = [0]
+        for u in queue:
+            for c in kids[u]:
+                g[c] = g[u] + oracle.pose_distance(v[u], v[c])
+                queue.append(c)
+        assert len(queue) == len(par)
+        assert np.array_equal(bits(g), bits(grown[t]["g"])), t
+    # a rewire re-rooted a subtree: vertices below a rewired one, parent kept, g lowered
+    lowered = sum(int(np.sum((ref[t]["parent"][:len(init[i]["v"])] == init[i]["parent"]) &
+                             (ref[t]["g"][:len(init[i]["v"])] < grown[t]["g"][:len(init[i]["v"])])))
+                  for i, t in enumerate("ab"))
+    assert lowered > 0
+    # the continuation is the uninterrupted run's
+    full = planner.plan_rrt_star_connect(data, start, goal, batch=STAR_DRAWS, max_time=300.0,
+                                         seed=STAR_SEED, max_halves=STAR_GROW + STAR_CONT,
+                                         trees=True, tree_capacity=cap, device_loop=True)
+    for t in "ab":
+        for k in ("v", "act", "parent", "g"):
+            assert np.array_equal(bits(full[t][k]), bits(dev[t][k])), (t, k)
