@@ -82,6 +82,7 @@ struct gbp_tree {
   // subtree (graph_class.cpp:131-138); kept by every append (child order is
   // immaterial: a child's g depends on its parent's alone)
   int32_t *child = nullptr, *sibling = nullptr;  // [cap], -1 = none
+  int32_t *prev = nullptr;    // [cap] previous sibling (-1: first child): O(1) removeEdge
   int32_t *bfs = nullptr;     // [2 cap] scratch: the subtree update's two level queues
   int32_t *count = nullptr;   // [1] number of vertices (device resident)
 };
@@ -179,18 +180,31 @@ struct gbp_plan_ws {
   int star = 0;
   double star_delta = 3.0;     // rrt_star_connect.h:59
   int64_t star_max_pairs = 0, star_max_shared = 0;
-  int32_t *scnt = nullptr;     // [star_items] neighbours per scan item (k_star_count)
-  int32_t *sioff = nullptr;    // [star_items] the items' offsets
-  int32_t *soff = nullptr;     // [bmax + 1] each new vertex's first pair
   int64_t star_items = 0;      // scan items per half (new vertex x position chunk)
-  int32_t *snb = nullptr;      // [max_pairs] the neighbour of each pair
-  int32_t *sown = nullptr;     // [max_pairs] its new vertex (k)
-  int32_t *srowof = nullptr;   // [2 max_pairs] connect check -> pair-check row (-1: none)
-  int32_t *sritem = nullptr;   // [2 max_pairs] row -> connect check
-  double *srs = nullptr;       // [2 max_pairs][8] rows: the pair checks' states
-  double *sra = nullptr;       // [2 max_pairs][10] and actions
-  uint32_t *srf = nullptr;     // [2 max_pairs] their flags
+  // a half's insertion buffers, one set per tree (half & 1): half h's replay
+  // runs on star_stream beside half h's connects and half h + 1, which fills
+  // the other set; half h + 2 refills this one only after the replay (its
+  // stage 5 waits for it first)
+  struct StarSet {
+    int32_t *scnt = nullptr;     // [star_items] neighbours per scan item (k_star_count)
+    int32_t *sioff = nullptr;    // [star_items] the items' offsets
+    int32_t *soff = nullptr;     // [bmax + 1] each new vertex's first pair
+    int32_t *snb = nullptr;      // [max_pairs] the neighbour of each pair
+    int32_t *sown = nullptr;     // [max_pairs] its new vertex (k)
+    int32_t *srowof = nullptr;   // [2 max_pairs] connect check -> pair-check row (-1: none)
+    int32_t *sritem = nullptr;   // [2 max_pairs] row -> connect check
+    double *srs = nullptr;       // [2 max_pairs][8] rows: the pair checks' states
+    double *sra = nullptr;       // [2 max_pairs][10] and actions
+    uint32_t *srf = nullptr;     // [2 max_pairs] their flags
+    int64_t *meta = nullptr;     // [4] n_added, added_base, pairs (k_star_scan); shared count (k_star_shared)
+  } ss[2];
   int32_t *kvtx = nullptr;     // [bmax] O's vertex of each connection (-1: none)
+  // the replay (and the best connection's ranking) off the caller's stream:
+  // e6 (stage 6 done) and e5 (stage 5 done) main -> star, rdone[k] star -> main
+  // (tree k's last replay / ranking), sdone the call's join
+  hipStream_t star_stream = nullptr;
+  hipEvent_t star_e6 = nullptr, star_e5 = nullptr, star_rdone[2] = {nullptr, nullptr},
+             star_sdone = nullptr;
   int32_t *sshared = nullptr;  // [max_shared][2] the REACHED connections (a, b)
   void *star_block = nullptr;
 };
@@ -1372,7 +1386,7 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
                                                int32_t *__restrict__ vtx, unsigned long long *tiles,
                                                uint32_t epoch, int32_t half, int64_t cap,
                                                uint64_t seq, int32_t *tch,
-                                               int32_t *tsib, int star) {
+                                               int32_t *tsib, int32_t *tprev, int star) {
   if (gated(st, seq)) return;
   __shared__ int32_t s_base;
   if (threadIdx.x == 0) s_base = *tcount;  // read before this block publishes its count
@@ -1403,8 +1417,19 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
     tg[idx] = tg[p] + pose_distance(pv, s);  // graph_class.cpp:36-42 addEdge
     tch[idx] = -1;
     // the successor list: RRT*'s extends are joined by the insertion replay
-    // (k_star_replay: choose-parent), everything else here
-    tsib[idx] = (mode == 0 && star) ? -1 : atomicExch(&tch[p], idx);
+    // (k_star_replay: choose-parent), everything else here.  A vertex is its
+    // parent's first child once linked: its previous-sibling slot is cleared
+    // before the exchange publishes it, and the next vertex linked to the same
+    // parent (the only one the exchange returns it to) sets it afterwards.
+    tprev[idx] = -1;
+    if (mode == 0 && star) {
+      tsib[idx] = -1;
+    } else {
+      __threadfence();
+      const int32_t h = atomicExch(&tch[p], idx);
+      tsib[idx] = h;
+      if (h >= 0) tprev[h] = idx;
+    }
     if (vtx) vtx[i] = idx;
     if (mode == 1 && r == GBP_REACHED && !star) {  // RRT*: every REACHED one is kept (k_star_shared)
       atomicMin((unsigned long long *)&st->meet,
@@ -1675,8 +1700,8 @@ __global__ __launch_bounds__(TB) void k_star_count(gbp_plan_status *st, const do
 // first pair, one workgroup
 __global__ __launch_bounds__(RB) void k_star_scan(gbp_plan_status *st, const int32_t *__restrict__ cnt,
                                                   int32_t *__restrict__ ioff, int32_t *__restrict__ off,
-                                                  int64_t max_pairs, int64_t cap_items, int32_t half,
-                                                  uint64_t seq) {
+                                                  int64_t *__restrict__ meta, int64_t max_pairs,
+                                                  int64_t cap_items, int32_t half, uint64_t seq) {
   if (gated(st, seq)) return;
   const int64_t n = st->n_added, base = st->added_base;
   int64_t ch, nch;
@@ -1717,6 +1742,10 @@ __global__ __launch_bounds__(RB) void k_star_scan(gbp_plan_status *st, const int
   if (threadIdx.x == 0) {
     off[n] = (int32_t)min<int64_t>(total, 0x7FFFFFFF);
     st->star_pairs = (int32_t)min<int64_t>(total, 0x7FFFFFFF);
+    // the replay's own copy: it runs beside the next half, which rewrites st's
+    meta[0] = n;
+    meta[1] = base;
+    meta[2] = min<int64_t>(total, 0x7FFFFFFF);
     st->star_rows = 0;
     st->star_vrows = 0;
     st->stat_star_connects += 2 * total;  // a choose-parent and a rewire connect per pair
@@ -1880,147 +1909,298 @@ __device__ void block_argmin(double &key, int64_t &at, double *kd, int64_t *ki) 
   __syncthreads();
 }
 
+// Stage 7 runs on ONE wave: a half inserts a few vertices (~3 at config 5),
+// each with ~100 neighbours, ~2 rewires and subtree updates of ~17 vertices
+// over ~1-2 levels (oracle statistics of config 5's continuation), so its
+// length is a chain of dependent steps — a 1024-thread workgroup paid a
+// 10-barrier reduction ladder per choice and a 16-wave barrier per subtree
+// level (61 us per half); one wave reduces by shuffles and its barriers
+// cost nothing.
+constexpr int RW = 64;
+
+// wave-wide lexicographic (key, position) minimum; position < 0 never wins,
+// NaN keys never win (the loops only keep comparable keys)
+__device__ __forceinline__ void wave_argmin(double &key, int64_t &at) {
+#pragma unroll
+  for (int o = RW / 2; o > 0; o >>= 1) {
+    const double k2 = __shfl_xor(key, o);
+    const int64_t i2 = __shfl_xor(at, o);
+    if (i2 >= 0 && (at < 0 || k2 < key || (k2 == key && i2 < at))) {
+      key = k2;
+      at = i2;
+    }
+  }
+}
+
+// wave-wide least non-negative position (-1 if none)
+__device__ __forceinline__ int64_t wave_first(int64_t at) {
+#pragma unroll
+  for (int o = RW / 2; o > 0; o >>= 1) {
+    const int64_t i2 = __shfl_xor(at, o);
+    if (i2 >= 0 && (at < 0 || i2 < at)) at = i2;
+  }
+  return at;
+}
+
 // g over the subtree below vertex r (graph_class.cpp:131-138: every successor's
-// g = its parent's + poseDistance), level by level through the two queues
-// (bounded: a list that is not a tree — never built here — stops at nv vertices
-// and returns false instead of looping)
+// g = its parent's + poseDistance), level by level, the wave's lanes taking a
+// level's vertices; the queues hold (vertex, g) in LDS up to RQ entries per
+// level, in the tree's scratch past that (bounded: a list that is not a tree —
+// never built here — stops at nv vertices and returns false)
+constexpr int RQ = 2048;
 __device__ bool subtree_g(const double *__restrict__ tv, double *tg, const int32_t *tch,
-                          const int32_t *tsib, int32_t r, int32_t *q0, int32_t *q1, int32_t nv) {
-  __shared__ int32_t s_n, s_next, s_total;
+                          const int32_t *tsib, int32_t r, double gr, int32_t *q0, int32_t *q1,
+                          int32_t nv) {
+  __shared__ int32_t lq[2][RQ];
+  __shared__ double lg[2][RQ];
+  __shared__ int32_t s_next;
+  int32_t nq = 1, total = 1, cur = 0;
   if (threadIdx.x == 0) {
-    q0[0] = r;
-    s_n = 1;
+    lq[0][0] = r;
+    lg[0][0] = gr;
     s_next = 0;
-    s_total = 1;
   }
   __syncthreads();
-  bool ok = true;
-  while (s_n > 0) {
-    const int32_t nq = s_n;
-    for (int32_t i = threadIdx.x; i < nq; i += RB) {
-      const int32_t p = q0[i];
-      const double gp = tg[p];
+  while (nq > 0) {
+    for (int32_t i = threadIdx.x; i < nq; i += RW) {
+      const int32_t p = i < RQ ? lq[cur][i] : q0[i];
+      const double gp = i < RQ ? lg[cur][i] : tg[p];
+      double vp[8];
+      copy8(vp, tv + 8 * (int64_t)p);
       for (int32_t c = tch[p]; c >= 0; c = tsib[c]) {
-        tg[c] = gp + pose_distance(tv + 8 * (int64_t)p, tv + 8 * (int64_t)c);
+        const double gc = gp + pose_distance(vp, tv + 8 * (int64_t)c);
+        tg[c] = gc;
         const int32_t slot = atomicAdd(&s_next, 1);
         if (slot >= nv) break;
-        q1[slot] = c;
+        if (slot < RQ) {
+          lq[cur ^ 1][slot] = c;
+          lg[cur ^ 1][slot] = gc;
+        } else {
+          q1[slot] = c;
+        }
       }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      s_total += min(s_next, nv);
-      s_n = (s_next > nv || s_total > nv) ? 0 : s_next;
-      if (s_next > nv || s_total > nv) s_total = -1;
-      s_next = 0;
-    }
+    const int32_t next = s_next;
+    __syncthreads();
+    if (threadIdx.x == 0) s_next = 0;
+    total += min(next, nv);
+    if (next > nv || total > nv) return false;
+    nq = next;
     int32_t *t = q0;
     q0 = q1;
     q1 = t;
+    cur ^= 1;
     __syncthreads();
   }
-  ok = s_total >= 0;
-  __syncthreads();
-  return ok;
+  return true;
 }
 
-// stage 7: the ordered replay of rrt_star_connect.cpp:18-66, one workgroup
-__global__ __launch_bounds__(RB) void k_star_replay(gbp_plan_status *st, const double *__restrict__ tv,
+// addEdge(p, c)'s successor entry: c becomes p's first child
+__device__ __forceinline__ void link_child(int32_t *tch, int32_t *tsib, int32_t *tprev, int32_t p,
+                                           int32_t c) {
+  const int32_t h = tch[p];
+  tsib[c] = h;
+  tprev[c] = -1;
+  if (h >= 0) tprev[h] = c;
+  tch[p] = c;
+}
+
+// the half's pairs, what the replay needs of them that no insertion changes:
+// the neighbour, poseDistance(neighbour, s_new) (:35 and :59 alike, argument
+// order included) and whether its choose-parent (bit 0) / rewire (bit 1)
+// connection REACHED; the first RP in LDS (the prologue fills them), the rest
+// recomputed from global memory where read
+constexpr int RP = 2048;  // pairs held in LDS (config 5: ~300 per half)
+constexpr int RS = 4;     // a lane's neighbour slots per insertion in registers
+constexpr int RK = 512;   // new vertices held in LDS (their nearest vertex and g0's distance)
+
+struct PairInfo {
+  int32_t j;
+  uint32_t f;
+  double d;
+};
+
+__device__ __forceinline__ PairInfo pair_info_global(int64_t i, const double *__restrict__ tv,
+                                                     int64_t base, const int32_t *__restrict__ nb,
+                                                     const int32_t *__restrict__ own,
+                                                     const int32_t *__restrict__ rowof,
+                                                     const uint32_t *__restrict__ rf) {
+  PairInfo pi;
+  pi.j = nb[i];
+  const int32_t r0 = rowof[2 * i], r1 = rowof[2 * i + 1];
+  pi.f = ((r0 >= 0 && (rf[r0] & GBP_F_VALID)) ? 1u : 0u) |
+         ((r1 >= 0 && (rf[r1] & GBP_F_VALID)) ? 2u : 0u);
+  pi.d = pose_distance(tv + 8 * (int64_t)pi.j, tv + 8 * (base + own[i]));
+  return pi;
+}
+
+// stage 7: the ordered replay of rrt_star_connect.cpp:18-66, one wave
+__global__ __launch_bounds__(RW) void k_star_replay(gbp_plan_status *st, const double *__restrict__ tv,
                                                     double *ta, double *tg, int32_t *tp, int32_t *tch,
-                                                    int32_t *tsib, const int32_t *__restrict__ off,
+                                                    int32_t *tsib, int32_t *tprev,
+                                                    const int32_t *__restrict__ off,
                                                     const int32_t *__restrict__ nb,
+                                                    const int32_t *__restrict__ own,
                                                     const int32_t *__restrict__ rowof,
                                                     const double *__restrict__ ra,
-                                                    const uint32_t *__restrict__ rf, int32_t *q0,
+                                                    const uint32_t *__restrict__ rf,
+                                                    const int64_t *__restrict__ meta, int32_t *q0,
                                                     int32_t *q1, const int32_t *tcount, uint64_t seq) {
   if (gated(st, seq)) return;
-  const int64_t n = st->n_added, base = st->added_base;
+  const int64_t n = meta[0], base = meta[1], npairs = meta[2];
   const int32_t nv = *tcount;
-  __shared__ double kd[RB];
-  __shared__ int64_t ki[RB];
-  __shared__ int32_t s_min;
-  __shared__ int64_t s_row;
+  const int lane = threadIdx.x;
+  __shared__ int32_t lj[RP];
+  __shared__ uint32_t lf[RP];
+  __shared__ double ld[RP];
+  __shared__ int32_t lnn[RK], loff[RK + 1];
+  __shared__ double ld0[RK];
+  // prologue: every pair's static part and every new vertex's nearest vertex,
+  // its offsets and poseDistance(s_new, s_nearest) (:28), all lanes at once
+  for (int64_t i = lane; i < min<int64_t>(npairs, RP); i += RW) {
+    const PairInfo pi = pair_info_global(i, tv, base, nb, own, rowof, rf);
+    lj[i] = pi.j;
+    lf[i] = pi.f;
+    ld[i] = pi.d;
+  }
+  for (int64_t k = lane; k < min<int64_t>(n, RK); k += RW) {
+    const int32_t nn = tp[base + k];  // stage 3 wrote the nearest vertex here
+    lnn[k] = nn;
+    ld0[k] = pose_distance(tv + 8 * (base + k), tv + 8 * (int64_t)nn);
+    loff[k] = off[k];
+  }
+  const int64_t nk_l = n < RK ? n : RK;
+  if (lane == 0) loff[nk_l] = off[nk_l];
+  __syncthreads();
+  auto pair = [&](int64_t i) -> PairInfo {
+    if (i < RP) return PairInfo{lj[i], lf[i], ld[i]};
+    return pair_info_global(i, tv, base, nb, own, rowof, rf);
+  };
   int64_t rewires = 0;
   for (int64_t k = 0; k < n; k++) {
     const int32_t idx = (int32_t)(base + k);
-    const double *s_new = tv + 8 * (int64_t)idx;
-    const int32_t nn = tp[idx];  // stage 3 wrote the nearest vertex here
-    const int64_t i0 = off[k], i1 = off[k + 1];
+    const int32_t nn = k < RK ? lnn[k] : tp[idx];
+    const double d0 = k < RK ? ld0[k] : pose_distance(tv + 8 * (int64_t)idx, tv + 8 * (int64_t)nn);
+    const int64_t i0 = k < RK ? loff[k] : off[k], i1 = k + 1 <= RK ? loff[k + 1] : off[k + 1];
+    // this lane's first RS neighbours (positions i0 + lane + RW s)
+    int32_t sj[RS];
+    uint32_t sf[RS];
+    double sd[RS];
+#pragma unroll
+    for (int q = 0; q < RS; q++) {
+      const int64_t i = i0 + lane + RW * q;
+      sf[q] = 0;
+      sj[q] = 0;
+      sd[q] = 0;
+      if (i < i1) {
+        const PairInfo pi = pair(i);
+        sj[q] = pi.j;
+        sf[q] = pi.f;
+        sd[q] = pi.d;
+      }
+    }
+    const int64_t ix = i0 + (int64_t)RW * RS;  // positions past the slots
     // choose-parent (:27-44): from the nearest vertex, the first neighbour whose
     // REACHED connection is strictly cheaper than the best so far — the first
-    // index of the cheapest, when that beats the nearest vertex's
+    // in the map's order of the cheapest, when that beats the nearest vertex's
     double key = INFINITY;
     int64_t at = -1;
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += RB) {
-      const int32_t r = rowof[2 * i];
-      if (r < 0 || !(rf[r] & GBP_F_VALID)) continue;
-      const int32_t j = nb[i];
-      const double gc = tg[j] + pose_distance(tv + 8 * (int64_t)j, s_new);  // :35
-      if (gc == gc && (at < 0 || gc < key)) {  // the first of this thread's minimum
+    double gq[RS];
+#pragma unroll
+    for (int q = 0; q < RS; q++) gq[q] = (sf[q] & 1u) ? tg[sj[q]] : 0.0;
+    const double g0 = tg[nn] + d0;  // :28
+#pragma unroll
+    for (int q = 0; q < RS; q++) {
+      if (!(sf[q] & 1u)) continue;
+      const double gc = gq[q] + sd[q];  // :35
+      if (gc == gc && (at < 0 || gc < key)) {  // the first of this lane's minimum
+        key = gc;
+        at = i0 + lane + RW * q;
+      }
+    }
+    for (int64_t i = ix + lane; i < i1; i += RW) {
+      const PairInfo pi = pair(i);
+      if (!(pi.f & 1u)) continue;
+      const double gc = tg[pi.j] + pi.d;
+      if (gc == gc && (at < 0 || gc < key)) {
         key = gc;
         at = i;
       }
     }
-    block_argmin(key, at, kd, ki);
-    if (threadIdx.x == 0) {
-      const double g0 = tg[nn] + pose_distance(s_new, tv + 8 * (int64_t)nn);  // :28
-      int32_t pmin = nn;
-      double gn = g0;
-      int64_t row = -1;
-      if (at >= 0 && key < g0) {
-        pmin = nb[at];
-        gn = key;
-        row = rowof[2 * at];
-      }
-      // addEdge(s_min, s_new) + updateGYValue + addAction (:47-49)
-      tp[idx] = pmin;
-      tsib[idx] = tch[pmin];
-      tch[pmin] = idx;
-      tg[idx] = gn;
-      if (row >= 0) copy10(ta + 10 * (int64_t)idx, ra + 10 * row);
-      s_min = pmin;
+    wave_argmin(key, at);
+    int32_t pmin = nn;
+    double gn = g0;
+    int64_t row = -1;
+    if (at >= 0 && key < g0) {
+      pmin = pair(at).j;
+      gn = key;
+      row = rowof[2 * at];
     }
+    // addEdge(s_min, s_new) + updateGYValue + addAction (:47-49)
+    if (lane == 0) {
+      tp[idx] = pmin;
+      link_child(tch, tsib, tprev, pmin, idx);
+      tg[idx] = gn;
+    }
+    if (row >= 0 && lane < 10) ta[10 * (int64_t)idx + lane] = ra[10 * row + lane];
     __syncthreads();
     // rewire (:51-66): in neighbour order; a rewire's subtree update can change
     // the g a later neighbour is tested with, so each round finds the first
     // neighbour (from the cursor on) that rewires now
     for (int64_t cur = i0; cur < i1;) {
-      key = 0;
-      at = -1;
       const double gi = tg[idx];
-      for (int64_t i = cur + threadIdx.x; i < i1; i += RB) {
-        const int32_t j = nb[i];
-        if (j == s_min) continue;
-        const int32_t r = rowof[2 * i + 1];
-        if (r < 0 || !(rf[r] & GBP_F_VALID)) continue;
-        if (tg[j] > (gi + pose_distance(tv + 8 * (int64_t)j, s_new))) {
-          at = i;
-          break;  // a thread's candidates ascend: its first is its least
+#pragma unroll
+      for (int q = 0; q < RS; q++)
+        gq[q] = ((sf[q] & 2u) && sj[q] != pmin && i0 + lane + RW * q >= cur) ? tg[sj[q]] : 0.0;
+      at = -1;
+#pragma unroll
+      for (int q = 0; q < RS; q++) {
+        const int64_t i = i0 + lane + RW * q;
+        if (at < 0 && (sf[q] & 2u) && sj[q] != pmin && i >= cur && gq[q] > (gi + sd[q])) at = i;
+      }
+      if (at < 0) {
+        for (int64_t i = max(ix, cur) + ((lane - (max(ix, cur) - i0)) % RW + RW) % RW; i < i1; i += RW) {
+          const PairInfo pi = pair(i);
+          if (!(pi.f & 2u) || pi.j == pmin) continue;
+          if (tg[pi.j] > (gi + pi.d)) {
+            at = i;
+            break;  // a lane's candidates ascend: its first is its least
+          }
         }
       }
-      block_argmin(key, at, kd, ki);  // key 0 everywhere: the least index
+      at = wave_first(at);
       if (at < 0) break;
-      if (threadIdx.x == 0) {
-        const int32_t j = nb[at];
-        const int32_t op = tp[j];
-        if (op >= 0) {  // removeEdge(parent, j) (graph_class.cpp:44-58)
-          int32_t *link = &tch[op];
-          for (int32_t step = 0; *link >= 0 && *link != j && step < nv; step++) link = &tsib[*link];
-          if (*link == j) *link = tsib[j];
+      const PairInfo pj = pair(at);
+      const int32_t j = pj.j;
+      const int64_t rrow = rowof[2 * at + 1];
+      const double gj = gi + pj.d;  // updateGYValue (:60)
+      if (lane == 0) {
+        // removeEdge(parent, j) (graph_class.cpp:44-58) + addEdge(s_new, j): j
+        // leaves its parent's list (never s_new's: s_new's children are the
+        // vertices rewired before it) for the head of s_new's; every load first
+        const int32_t op = tp[j], pv = tprev[j], nx = tsib[j], h = tch[idx];
+        const int32_t oh = op >= 0 ? tch[op] : -1;
+        if (op >= 0) {
+          if (pv >= 0)
+            tsib[pv] = nx;
+          else if (oh == j)
+            tch[op] = nx;
+          if (nx >= 0) tprev[nx] = pv;
         }
-        tp[j] = idx;  // addEdge(s_new, j)
-        tsib[j] = tch[idx];
+        tsib[j] = h;
+        tprev[j] = -1;
+        if (h >= 0) tprev[h] = j;
         tch[idx] = j;
-        tg[j] = gi + pose_distance(tv + 8 * (int64_t)j, s_new);  // updateGYValue (:60)
-        copy10(ta + 10 * (int64_t)j, ra + 10 * (int64_t)rowof[2 * at + 1]);
-        s_row = j;
+        tp[j] = idx;
+        tg[j] = gj;
       }
+      if (lane < 10) ta[10 * (int64_t)j + lane] = ra[10 * rrow + lane];
       __syncthreads();
       rewires++;
       // the rewired vertex's successors (recursion of updateGYValue)
-      const int32_t j = (int32_t)s_row;
-      if (tch[j] >= 0 && !subtree_g(tv, tg, tch, tsib, j, q0, q1, nv)) {
-        if (threadIdx.x == 0) {
+      if (tch[j] >= 0 && !subtree_g(tv, tg, tch, tsib, j, gj, q0, q1, nv)) {
+        if (lane == 0) {
           atomicOr(&st->error, 8u);  // a successor list that is not a tree
           raise_gate(st, seq);
         }
@@ -2030,24 +2210,20 @@ __global__ __launch_bounds__(RB) void k_star_replay(gbp_plan_status *st, const d
       cur = at + 1;
     }
   }
-  if (threadIdx.x == 0 && rewires) st->stat_rewires += rewires;
+  if (lane == 0 && rewires) st->stat_rewires += rewires;
 }
 
 // stage 5 (RRT*): the half's REACHED connections appended to the shared list
-// in connection order (rrt_star_connect.cpp:136-175: shared_a / shared_b),
-// then after tree Tb's half the cheapest of all ranked with the current g
-// values (:181-193: strictly cheaper than the best so far; ties to the first)
+// in connection order (rrt_star_connect.cpp:136-175: shared_a / shared_b);
+// meta[3] keeps the list's length for the ranking after Tb's half
 __global__ __launch_bounds__(RB) void k_star_shared(gbp_plan_status *st, const int32_t *__restrict__ kres,
                                                     const int32_t *__restrict__ kvtx, int t_is_a,
-                                                    int32_t *shared, int64_t max_shared, int rank,
-                                                    const double *__restrict__ ga,
-                                                    const double *__restrict__ gb, uint64_t seq) {
+                                                    int32_t *shared, int64_t max_shared,
+                                                    int64_t *__restrict__ meta, uint64_t seq) {
   if (gated(st, seq)) return;
   const int64_t n = st->n_added, base = st->added_base;
   const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
   __shared__ int wc[RB / WAVE];
-  __shared__ double kd[RB];
-  __shared__ int64_t ki[RB];
   int64_t ns = st->n_shared;
   for (int64_t i0 = 0; i0 < n; i0 += RB) {
     const int64_t i = i0 + threadIdx.x;
@@ -2078,8 +2254,23 @@ __global__ __launch_bounds__(RB) void k_star_shared(gbp_plan_status *st, const i
     }
     return;
   }
-  if (threadIdx.x == 0) st->n_shared = (int32_t)ns;
-  if (!rank) return;
+  if (threadIdx.x == 0) {
+    st->n_shared = (int32_t)ns;
+    meta[3] = ns;
+  }
+}
+
+// after Tb's half (star_stream, behind both trees' replays): the cheapest
+// of the meta[3] connections listed so far ranked with the current g values
+// (:181-193: strictly cheaper than the best so far; ties to the first)
+__global__ __launch_bounds__(RB) void k_star_rank(gbp_plan_status *st, const int32_t *__restrict__ shared,
+                                                  const int64_t *__restrict__ meta,
+                                                  const double *__restrict__ ga,
+                                                  const double *__restrict__ gb, uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t ns = meta[3];
+  __shared__ double kd[RB];
+  __shared__ int64_t ki[RB];
   double key = INFINITY;
   int64_t at = -1;
   for (int64_t p = threadIdx.x; p < ns; p += RB) {
@@ -2107,6 +2298,7 @@ __global__ void k_tree_init(gbp_tree t, double r0, double r1, double r2, double 
   t.parent[0] = -1;
   t.child[0] = -1;
   t.sibling[0] = -1;
+  t.prev[0] = -1;
   *t.count = 1;
 }
 
@@ -2123,8 +2315,11 @@ __global__ void k_tree_append(gbp_tree t, int64_t n, const double *__restrict__ 
     t.g[c] = p[i] >= 0 ? t.g[p[i]] + pose_distance(t.v + 8 * (int64_t)p[i], s + 8 * i) : 0.0;
     t.child[c] = -1;
     t.sibling[c] = -1;
+    t.prev[c] = -1;
     if (p[i] >= 0) {
-      t.sibling[c] = t.child[p[i]];
+      const int32_t h = t.child[p[i]];
+      t.sibling[c] = h;
+      if (h >= 0) t.prev[h] = c;
       t.child[p[i]] = c;
     }
   }
@@ -2143,9 +2338,12 @@ __global__ void k_tree_load(gbp_tree t, int64_t n, const double *__restrict__ s,
     t.parent[i] = p[i];
     t.child[i] = -1;
     t.sibling[i] = -1;
+    t.prev[i] = -1;
   }
   for (int64_t i = 1; i < n; i++) {
-    t.sibling[i] = t.child[p[i]];
+    const int32_t h = t.child[p[i]];
+    t.sibling[i] = h;
+    if (h >= 0) t.prev[h] = (int32_t)i;
     t.child[p[i]] = (int32_t)i;
   }
   int32_t *q = t.bfs;
@@ -2427,29 +2625,39 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 0, w->eres, w->nn,
                        w->esn, w->ean, T->v, T->vh, T->hm, T->a, T->g, T->parent, T->count, w->evtx,
                        w->tiles,
-                       next_epoch(w), half, T->cap, ++w->seq, T->child, T->sibling, w->star);
+                       next_epoch(w), half, T->cap, ++w->seq, T->child, T->sibling, T->prev, w->star);
+  const int kT = direction == GBP_FORWARD ? 0 : 1;  // T's tree index (Ta 0, Tb 1)
+  gbp_plan_ws::StarSet &S = w->ss[half & 1];
   if (w->star && run(6)) {
     // RRT* insertion, stage 6: neighbourhoods, connect checks, their pair checks
     const unsigned gk = (unsigned)std::max<int64_t>(1, std::min<int64_t>(w->star_items, cus * 8));
-    hipLaunchKernelGGL(k_star_count, dim3(gk), dim3(TB), 0, s, st, T->v, w->star_delta, w->scnt,
+    hipLaunchKernelGGL(k_star_count, dim3(gk), dim3(TB), 0, s, st, T->v, w->star_delta, S.scnt,
                        w->star_items, ++w->seq);
-    hipLaunchKernelGGL(k_star_scan, dim3(1), dim3(RB), 0, s, st, w->scnt, w->sioff, w->soff,
+    hipLaunchKernelGGL(k_star_scan, dim3(1), dim3(RB), 0, s, st, S.scnt, S.sioff, S.soff, S.meta,
                        w->star_max_pairs, w->star_items, half, ++w->seq);
-    hipLaunchKernelGGL(k_star_fill, dim3(gk), dim3(TB), 0, s, st, T->v, w->star_delta, w->sioff,
-                       w->snb, w->sown, w->star_items, ++w->seq);
+    hipLaunchKernelGGL(k_star_fill, dim3(gk), dim3(TB), 0, s, st, T->v, w->star_delta, S.sioff,
+                       S.snb, S.sown, w->star_items, ++w->seq);
     const int64_t rmax = 2 * w->star_max_pairs;
     hipLaunchKernelGGL(k_star_prep, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, T->v,
-                       direction, w->snb, w->sown, w->srowof, w->sritem, w->srs, w->sra, ++w->seq);
-    int rc = gbp_internal_validate_dev_n(t, rmax, &st->star_vrows, w->srs, w->sra, nullptr, direction,
-                                         adaptive, nullptr, nullptr, nullptr, w->srf, nullptr, s);
+                       direction, S.snb, S.sown, S.srowof, S.sritem, S.srs, S.sra, ++w->seq);
+    int rc = gbp_internal_validate_dev_n(t, rmax, &st->star_vrows, S.srs, S.sra, nullptr, direction,
+                                         adaptive, nullptr, nullptr, nullptr, S.srf, nullptr, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_star_gate, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, w->srf,
+    hipLaunchKernelGGL(k_star_gate, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, S.srf,
                        half, ++w->seq);
   }
-  if (w->star && run(7))  // stage 7: the ordered replay
-    hipLaunchKernelGGL(k_star_replay, dim3(1), dim3(RB), 0, s, st, T->v, T->a, T->g, T->parent,
-                       T->child, T->sibling, w->soff, w->snb, w->srowof, w->sra, w->srf, T->bfs,
-                       T->bfs + T->cap, T->count, ++w->seq);
+  if (w->star && run(7)) {
+    // stage 7, the ordered replay, on star_stream: it changes T's parents, g
+    // and successor lists only, which nothing reads before half h + 1's
+    // stage 5 (its appends into T wait for it: rdone[kT]); the connects of
+    // this half and the next half's extends of O run beside it
+    HIPCHK_P(hipEventRecord(w->star_e6, s));
+    HIPCHK_P(hipStreamWaitEvent(w->star_stream, w->star_e6, 0));
+    hipLaunchKernelGGL(k_star_replay, dim3(1), dim3(RW), 0, w->star_stream, st, T->v, T->a, T->g,
+                       T->parent, T->child, T->sibling, T->prev, S.soff, S.snb, S.sown, S.srowof,
+                       S.sra, S.srf, S.meta, T->bfs, T->bfs + T->cap, T->count, ++w->seq);
+    HIPCHK_P(hipEventRecord(w->star_rdone[kT], w->star_stream));
+  }
   if (!O) return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   const int cdir = direction == GBP_FORWARD ? GBP_REVERSE : GBP_FORWARD;
   if (run(4)) {
@@ -2471,15 +2679,26 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
 #undef GBP_KC
   }
   if (run(5)) {
+    // O's last replay (half h - 1's, on star_stream) before appending into O
+    if (w->star) HIPCHK_P(hipStreamWaitEvent(s, w->star_rdone[1 - kT], 0));
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 1, w->kres, w->nno,
                        w->ksn, w->kan, O->v, O->vh, O->hm, O->a, O->g, O->parent, O->count,
                        w->star ? w->kvtx : nullptr, w->tiles, next_epoch(w), half, O->cap, ++w->seq,
-                       O->child, O->sibling, w->star);
+                       O->child, O->sibling, O->prev, w->star);
     if (w->star) {  // the REACHED connections kept; after Tb's half the best one ranked
       const bool t_is_a = direction == GBP_FORWARD;
       hipLaunchKernelGGL(k_star_shared, dim3(1), dim3(RB), 0, s, st, w->kres, w->kvtx, t_is_a ? 1 : 0,
-                         w->sshared, w->star_max_shared, (half & 1) ? 1 : 0, t_is_a ? T->g : O->g,
-                         t_is_a ? O->g : T->g, ++w->seq);
+                         w->sshared, w->star_max_shared, S.meta, ++w->seq);
+      if (half & 1) {
+        // on star_stream behind this half's replay (Tb's g final) and half h - 1's
+        // (Ta's); the next replay of Ta queues behind it, and half h + 1's
+        // appends into Tb wait for it (rdone[kT] moves past it)
+        HIPCHK_P(hipEventRecord(w->star_e5, s));
+        HIPCHK_P(hipStreamWaitEvent(w->star_stream, w->star_e5, 0));
+        hipLaunchKernelGGL(k_star_rank, dim3(1), dim3(RB), 0, w->star_stream, st, w->sshared, S.meta,
+                           t_is_a ? T->g : O->g, t_is_a ? O->g : T->g, ++w->seq);
+        HIPCHK_P(hipEventRecord(w->star_rdone[kT], w->star_stream));
+      }
     }
   }
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
@@ -2517,7 +2736,7 @@ int tree_alloc(gbp_tree *t, int64_t cap) {
   int32_t *p = nullptr, *ch = nullptr;
   if (hipMalloc(&v, 64 * cap) != hipSuccess) return GBP_E_ALLOC;
   if (hipMalloc(&a, 80 * cap) != hipSuccess || hipMalloc(&g, 8 * cap) != hipSuccess ||
-      hipMalloc(&p, 4 * cap) != hipSuccess || hipMalloc(&ch, 16 * cap) != hipSuccess ||
+      hipMalloc(&p, 4 * cap) != hipSuccess || hipMalloc(&ch, 20 * cap) != hipSuccess ||
       hipMalloc(&vh, 2 * NH_ROW * ((cap + 63) & ~(int64_t)63)) != hipSuccess) {
     (void)hipFree(v);
     if (a) (void)hipFree(a);
@@ -2531,9 +2750,10 @@ int tree_alloc(gbp_tree *t, int64_t cap) {
   t->a = a;
   t->g = g;
   t->parent = p;
-  t->child = ch;        // [cap] first children, [cap] next siblings, [2 cap] queues
+  t->child = ch;  // [cap] first children, [cap] next / [cap] previous siblings, [2 cap] queues
   t->sibling = ch + cap;
-  t->bfs = ch + 2 * cap;
+  t->prev = ch + 2 * cap;
+  t->bfs = ch + 3 * cap;
   t->cap = cap;
   return GBP_OK;
 }
@@ -2626,6 +2846,7 @@ int gbp_tree_reserve(gbp_tree *t, int64_t capacity, gbp_stream stream) {
   HIPCHK_P(hipMemcpyAsync(t->parent, old.parent, 4 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->child, old.child, 4 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipMemcpyAsync(t->sibling, old.sibling, 4 * old.cap, hipMemcpyDeviceToDevice, s));
+  HIPCHK_P(hipMemcpyAsync(t->prev, old.prev, 4 * old.cap, hipMemcpyDeviceToDevice, s));
   HIPCHK_P(hipStreamSynchronize(s));
   (void)hipFree(old.v);
   (void)hipFree(old.vh);
@@ -2813,6 +3034,13 @@ extern "C++" __attribute__((visibility("hidden"))) hipStream_t gbp_internal_la_s
 static void ws_free(gbp_plan_ws *w) {
   if (w->la_go) (void)hipEventDestroy(w->la_go);
   if (w->la_done) (void)hipEventDestroy(w->la_done);
+  if (w->star_stream) {
+    (void)hipStreamSynchronize(w->star_stream);
+    hipEvent_t ev[] = {w->star_e6, w->star_e5, w->star_rdone[0], w->star_rdone[1], w->star_sdone};
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(w->star_stream);
+  }
   if (w->block) (void)hipFree(w->block);
   if (w->star_block) (void)hipFree(w->star_block);
   delete w;
@@ -2940,30 +3168,59 @@ int gbp_plan_star_config(gbp_plan_ws *w, int enable, double delta, int64_t max_p
   if (!w->star_block) {
     const int64_t b = w->bmax, r = 2 * max_pairs;
     const int64_t items = std::max<int64_t>(4 * b, 1 << 15);
-    const size_t bytes = 8 * items + 4 * (b + 1) + 8 * max_pairs + r * (4 + 4 + 64 + 80 + 4) +
-                         4 * b + 8 * max_shared + 16 * 256;
+    const size_t bytes = 2 * (8 * items + 4 * (b + 1) + 8 * max_pairs + r * (4 + 4 + 64 + 80 + 4) +
+                              32 + 11 * 256) +
+                         4 * b + 8 * max_shared + 4 * 256;
     if (hipMalloc(&w->star_block, bytes) != hipSuccess) {
       w->star_block = nullptr;
       w->star = 0;
       return GBP_E_ALLOC;
     }
     char *p = (char *)w->star_block;
-    w->scnt = carve<int32_t>(p, items);
-    w->sioff = carve<int32_t>(p, items);
-    w->soff = carve<int32_t>(p, b + 1);
+    for (auto &S : w->ss) {
+      S.scnt = carve<int32_t>(p, items);
+      S.sioff = carve<int32_t>(p, items);
+      S.soff = carve<int32_t>(p, b + 1);
+      S.snb = carve<int32_t>(p, max_pairs);
+      S.sown = carve<int32_t>(p, max_pairs);
+      S.srowof = carve<int32_t>(p, r);
+      S.sritem = carve<int32_t>(p, r);
+      S.srs = carve<double>(p, 8 * r);
+      S.sra = carve<double>(p, 10 * r);
+      S.srf = carve<uint32_t>(p, r);
+      S.meta = carve<int64_t>(p, 4);
+    }
     w->star_items = items;
-    w->snb = carve<int32_t>(p, max_pairs);
-    w->sown = carve<int32_t>(p, max_pairs);
-    w->srowof = carve<int32_t>(p, r);
-    w->sritem = carve<int32_t>(p, r);
-    w->srs = carve<double>(p, 8 * r);
-    w->sra = carve<double>(p, 10 * r);
-    w->srf = carve<uint32_t>(p, r);
     w->kvtx = carve<int32_t>(p, b);
     w->sshared = carve<int32_t>(p, 2 * max_shared);
     if ((size_t)(p - (char *)w->star_block) > bytes) return GBP_E_HIP;
     w->star_max_pairs = max_pairs;
     w->star_max_shared = max_shared;
+  }
+  if (!w->star_stream) {
+    // the workspace's own (a device-wide stream would make one planner's joins
+    // wait for another's replays), CU-masked to the last n/8 CUs, the ones
+    // la_stream leaves free: a masked stream has a hardware queue of its own,
+    // while a plain one shares one of the process's GPU_MAX_HW_QUEUES (4)
+    // round-robin — with the caller's stream the replay then ran in line with
+    // the connects it should overlap (config 5: 52 vs 66 M pair checks/s with
+    // 8 queues)
+    const int n = w->num_cus, lo = n - n / 8;
+    std::vector<uint32_t> mask((n + 31) / 32, 0u);
+    for (int c = lo; c < n; c++) mask[c / 32] |= 1u << (c % 32);
+    const hipError_t e = (lo > 0 && lo < n)
+                             ? hipExtStreamCreateWithCUMask(&w->star_stream, (uint32_t)mask.size(),
+                                                            mask.data())
+                             : hipStreamCreateWithFlags(&w->star_stream, hipStreamNonBlocking);
+    if (e != hipSuccess ||
+        hipEventCreateWithFlags(&w->star_e6, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&w->star_e5, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&w->star_rdone[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&w->star_rdone[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&w->star_sdone, hipEventDisableTiming) != hipSuccess) {
+      w->star = 0;
+      return GBP_E_HIP;
+    }
   }
   w->star = 1;
   w->star_delta = delta;
@@ -2998,11 +3255,17 @@ int gbp_plan_half_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, 
     return GBP_E_INVALID_ARG;
   Guard g(t->device);
   hipStream_t s = (hipStream_t)stream;
-  if (t->storage == GBP_STORAGE_F32)
-    return enqueue_stages<float>(t, w, T, O, half, direction, batch, seed, target_stream,
-                                 target_index_base, adaptive, first_stage, 5, s);
-  return enqueue_stages<double>(t, w, T, O, half, direction, batch, seed, target_stream,
-                                target_index_base, adaptive, first_stage, 5, s);
+  const int rc = t->storage == GBP_STORAGE_F32
+                     ? enqueue_stages<float>(t, w, T, O, half, direction, batch, seed, target_stream,
+                                             target_index_base, adaptive, first_stage, 5, s)
+                     : enqueue_stages<double>(t, w, T, O, half, direction, batch, seed,
+                                              target_stream, target_index_base, adaptive,
+                                              first_stage, 5, s);
+  if (w->star) {  // the replay and ranking on star_stream end before the caller's stream goes on
+    HIPCHK_P(hipEventRecord(w->star_sdone, w->star_stream));
+    HIPCHK_P(hipStreamWaitEvent(s, w->star_sdone, 0));
+  }
+  return rc;
 }
 
 int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *Tb,
@@ -3049,11 +3312,15 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
     searched = L.launch_next;
     used = used || L.launch_next;
   }
-  // nothing of the call stays on la_stream past the caller's stream (a host
-  // that reads the status, reserves or destroys after this sees it finished)
-  if (used) {
-    HIPCHK_P(hipEventRecord(w->la_done, w->la_stream));
-    HIPCHK_P(hipStreamWaitEvent(s, w->la_done, 0));
+  // nothing of the call stays on la_stream or star_stream past the caller's
+  // stream (a host that reads the status, reserves or destroys after this sees
+  // it finished).  la_done already follows this call's last look-ahead launch
+  // (re-recording it on the device-wide la_stream would also wait for other
+  // workspaces' searches: ADVICE r05)
+  if (used) HIPCHK_P(hipStreamWaitEvent(s, w->la_done, 0));
+  if (w->star) {
+    HIPCHK_P(hipEventRecord(w->star_sdone, w->star_stream));
+    HIPCHK_P(hipStreamWaitEvent(s, w->star_sdone, 0));
   }
   return rc;
 }
@@ -3268,17 +3535,18 @@ int gbp_plan_resolve_host(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree 
     // the RRT* insertion's connect checks (their pair checks, rows of stage 6)
     const int64_t n = st.star_rows;
     std::vector<uint32_t> rf(n);
-    if (n && (rc = d2h(rf.data(), w->srf, n, s))) return rc;
+    const gbp_plan_ws::StarSet &S = w->ss[st.halt_half & 1];
+    if (n && (rc = d2h(rf.data(), S.srf, n, s))) return rc;
     HIPCHK_P(hipStreamSynchronize(s));
     for (int64_t i = 0; i < n; i++) {
       if (!(rf[i] & GBP_F_FRAGILE)) continue;
       double sv[8], av[10], sn[8], tn = 0;
-      if ((rc = d2h(sv, w->srs + 8 * i, 8, s)) || (rc = d2h(av, w->sra + 10 * i, 10, s))) return rc;
+      if ((rc = d2h(sv, S.srs + 8 * i, 8, s)) || (rc = d2h(av, S.sra + 10 * i, 10, s))) return rc;
       HIPCHK_P(hipStreamSynchronize(s));
       uint32_t f = 0;
       const bool v = gbp_host::pair_check(t->host, sv, av, direction, adaptive, sn, &tn, &f, nullptr);
       const uint32_t fr = (f & ~GBP_F_FRAGILE) | (v ? GBP_F_VALID : 0u) | GBP_F_RESOLVED;
-      if ((rc = h2d(w->srf + i, &fr, 1, s))) return rc;
+      if ((rc = h2d(S.srf + i, &fr, 1, s))) return rc;
       HIPCHK_P(hipStreamSynchronize(s));
       k++;
     }

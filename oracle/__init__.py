@@ -80,6 +80,7 @@ def lib():
             "orc_um_rank": (I64, [I64, I64]),
             "orc_um_order": (None, [I64, P]),
             "orc_star_insert_one": (I, [P, P, I, I, P, D, I, I, I, P]),
+            "orc_star_stats": (None, [P, I]),
             "orc_knn_batch": (None, [I64, P, I, P, I, P, P, I]),
             "orc_knn_yaw_batch": (None, [I64, P, I, P, I, I, D, D, P, P, I]),
             "orc_state_distance_yaw": (D, [P, P, I, D, D]),
@@ -440,6 +441,15 @@ def neighbors_batch(queries, verts, radius, max_out=256, nthreads=1, order="refe
                                       int(max_out), _p(out), _p(cnt),
                                       {"reference": 0, "ascending": 1}[order], nthreads)
     return out, cnt
+
+
+def star_stats(reset=False):
+    """orc_star_stats: RRT* insertion diagnostics (see gbp_oracle.h)."""
+    out = np.zeros(8, np.int64)
+    lib().orc_star_stats(_p(out), int(bool(reset)))
+    keys = ("insertions", "neighbours", "max_neighbours", "rewires", "subtree_vertices",
+            "max_subtree", "subtree_depth_sum", "max_depth")
+    return dict(zip(keys, out.tolist()))
 
 
 def um_rank(keys, n):

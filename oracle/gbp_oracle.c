@@ -1400,15 +1400,34 @@ static void tree_remove_edge(orc_tree *t, int p, int c) {
   if (*link == c) *link = t->sibling[c];
 }
 
+/* RRT* insertion statistics (orc_star_stats; diagnostics only): insertions,
+ * neighbours, max neighbours, rewires, subtree vertices updated by rewires,
+ * largest such subtree, summed subtree depths, deepest subtree */
+static int64_t g_star_stats[8];
+static int64_t g_gy_nodes, g_gy_depth;
+
+void orc_star_stats(int64_t out[8], int reset) {
+  for (int i = 0; i < 8; i++) {
+    if (out) out[i] = g_star_stats[i];
+    if (reset) g_star_stats[i] = 0;
+  }
+}
+
 /* graph_class.cpp:131-138 (recursive over the successors) */
-static void tree_update_gy(orc_tree *t, int idx, double g, double y) {
+static void tree_update_gy_d(orc_tree *t, int idx, double g, double y, int64_t depth) {
   t->g[idx] = g;
   t->y[idx] = y;
+  g_gy_nodes++;
+  if (depth > g_gy_depth) g_gy_depth = depth;
   for (int c = t->child ? t->child[idx] : -1; c >= 0; c = t->sibling[c]) {
     const double *vi = t->v + 8 * (int64_t)idx, *vc = t->v + 8 * (int64_t)c;
-    tree_update_gy(t, c, t->g[idx] + orc_pose_distance(vi, vc),
-                   t->y[idx] + orc_state_yaw_distance(vi, vc));
+    tree_update_gy_d(t, c, t->g[idx] + orc_pose_distance(vi, vc),
+                     t->y[idx] + orc_state_yaw_distance(vi, vc), depth + 1);
   }
+}
+
+static void tree_update_gy(orc_tree *t, int idx, double g, double y) {
+  tree_update_gy_d(t, idx, g, y, 0);
 }
 
 /* attemptConnect's depth-0 decision only (callers that test == REACHED,
@@ -1452,6 +1471,9 @@ static void star_insert(const orc_terrain *T, orc_tree *t, int idx, int nn, cons
     nb_n = cnt;
   }
   out->connects += 2 * (int64_t)nb_n; /* a choose-parent and a rewire connect per neighbour */
+  g_star_stats[0]++;
+  g_star_stats[1] += nb_n;
+  if (nb_n > g_star_stats[2]) g_star_stats[2] = nb_n;
   int s_min = nn;
   double a_sel[10], a_c[10];
   memcpy(a_sel, a_new, sizeof a_sel);
@@ -1487,8 +1509,14 @@ static void star_insert(const orc_terrain *T, orc_tree *t, int idx, int nn, cons
         (t->g[j] > (t->g[idx] + orc_pose_distance(s_near, s_new)))) {
       tree_remove_edge(t, t->parent[j], j);
       tree_add_edge(t, idx, j);
+      g_gy_nodes = g_gy_depth = 0;
       tree_update_gy(t, j, t->g[idx] + orc_pose_distance(s_near, s_new),
                      t->y[idx] + orc_state_yaw_distance(s_near, s_new));
+      g_star_stats[4] += g_gy_nodes;
+      if (g_gy_nodes > g_star_stats[5]) g_star_stats[5] = g_gy_nodes;
+      g_star_stats[6] += g_gy_depth;
+      if (g_gy_depth > g_star_stats[7]) g_star_stats[7] = g_gy_depth;
+      g_star_stats[3]++;
       memcpy(t->a + 10 * (int64_t)j, a_c, sizeof a_c);
       out->rewires++;
     }

@@ -215,6 +215,11 @@ typedef struct {
 int orc_star_insert_one(const orc_terrain *T, orc_tree *t, int idx, int nn, const double *a_new,
                         double delta, int direction, int adaptive, int order, int64_t *rewires);
 
+/* diagnostics of the RRT* insertions run so far (process-wide, serial):
+ * [insertions, neighbours, max neighbours, rewires, subtree vertices updated,
+ * largest subtree, summed subtree depths, deepest subtree]; reset clears */
+void orc_star_stats(int64_t out[8], int reset);
+
 /* tr[0] = Ta (start, FORWARD), tr[1] = Tb (goal, REVERSE); returns 0, -1 (bad
  * arguments) or -2 (a tree's capacity is exhausted) */
 int orc_plan(const orc_terrain *T, const double *start, const double *goal,
