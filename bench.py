@@ -415,13 +415,39 @@ def _cpu_model():
     return None
 
 
+def config5_cpu_baseline(c5, halves=2):
+    """Config 5's CPU baseline: the oracle's RRT*-Connect loop (orc_plan with
+    star; the reference's O(N) bracket scans), 1 thread, on the same terrain
+    with the same start / goal, seed, streams and draws as the device run,
+    from the roots for `halves` half-iterations (~14 s of CPU work)."""
+    import oracle
+    data = td.by_name("synth-fractal-4096")
+    O = oracle.OracleTerrain.from_data(data)
+    oracle.set_scan_mode(0)
+    b = int(c5["batch"])
+    t0 = time.perf_counter()
+    r = O.plan(np.array(c5["start_state"]), np.array(c5["goal_state"]), batch=b,
+               seed=int(c5["seed"]), max_halves=halves, star=True, stream_a=401, stream_b=402,
+               capacity=1 << 16, nthreads=1)
+    dt = time.perf_counter() - t0
+    return {"value": round(r["attempts"] / dt, 1), "unit": "pair checks/s", "cores": 1,
+            "kind": "port", "extends_per_s": round(r["extends"] / dt, 1),
+            "sample": f"orc_plan(star) from the roots, {halves} half-iterations x {b} draws "
+                      f"({r['attempts']} pair checks, {r['extends']} extends, linear bracket "
+                      f"scans) in {dt:.1f} s on {_cpu_model() or 'the host'}"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = None
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # what the process group itself reports (torchrun's WORLD_SIZE is only
+        # what the launcher asked for): a SCALE line shows RCCL saw N ranks
+        world, backend = dist.get_world_size(), dist.get_backend()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -489,7 +515,9 @@ def main():
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
         from config5 import run_config5
         config5 = run_config5(batch=args.config5_batch, max_time=args.config5_seconds,
-                              rank=rank, world=world, device=local)
+                              rank=rank, world=world, device=local, split=world == 1)
+        if world == 1 and args.cpu_seconds > 0:
+            config5["cpu_baseline"] = config5_cpu_baseline(config5)
 
     if rank == 0:
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
@@ -510,6 +538,7 @@ def main():
             "value": round(value, 1),
             "unit": "extend-attempts/s",
             "n_gpus": world,
+            "dist_backend": backend,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),

@@ -51,7 +51,7 @@ EXPORTS = [
     "gbp_tree_size", "gbp_tree_read", "gbp_tree_append_host", "gbp_tree_load_host",
     "gbp_tree_device_ptrs", "gbp_vertex_map_order", "gbp_vertex_map_rank",
     "gbp_plan_ws_create", "gbp_plan_ws_destroy", "gbp_plan_reset", "gbp_plan_half_dev",
-    "gbp_plan_halves_dev", "gbp_plan_star_config",
+    "gbp_plan_halves_dev", "gbp_plan_star_config", "gbp_plan_stage_timing", "gbp_plan_stage_times",
     "gbp_plan_status_read", "gbp_plan_resolve_host", "gbp_extend_tree_dev",
     "gbp_extend_tree_finish_dev", "gbp_extend_tree_host", "gbp_tree_nearest_dev",
 ]
@@ -155,6 +155,8 @@ def load(path=None):
                                     I, I, P]),
         "gbp_plan_status_read": (I, [P, P, P]),
         "gbp_plan_star_config": (I, [P, I, ctypes.c_double, I64, I64]),
+        "gbp_plan_stage_timing": (I, [P, I]),
+        "gbp_plan_stage_times": (I, [P, P, I, P, I]),
         "gbp_plan_resolve_host": (I, [P, P, P, P, I, I64, I, P, P, P]),
         "gbp_extend_tree_dev": (I, [P, P, P, I64, P, P, I, I, U64, I64, P, P, P]),
         "gbp_extend_tree_finish_dev": (I, [P, P, P, I64, I, P, P, P]),

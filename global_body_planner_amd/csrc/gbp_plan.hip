@@ -205,6 +205,18 @@ struct gbp_plan_ws {
   hipStream_t star_stream = nullptr;
   hipEvent_t star_e6 = nullptr, star_e5 = nullptr, star_rdone[2] = {nullptr, nullptr},
              star_sdone = nullptr;
+  // gbp_plan_stage_timing: a ring of per-half timing events (start, after
+  // stage 3, after stage 6, replay start / end, end), read back once complete
+  bool timing = false;
+  struct TimedHalf {
+    hipEvent_t ev[6] = {};
+    bool pending = false, star = false;
+    int32_t half = 0;
+  };
+  TimedHalf *tring = nullptr;  // [ntring] (a plain array: no template of a gbp type exported)
+  size_t ntring = 0, tnext = 0;
+  double tsum[5] = {0, 0, 0, 0, 0};
+  int64_t tcount = 0;
   int32_t *sshared = nullptr;  // [max_shared][2] the REACHED connections (a, b)
   void *star_block = nullptr;
 };
@@ -2551,6 +2563,38 @@ int la_launch(gbp_terrain *t, gbp_plan_ws *w, const gbp_tree *X, int32_t h1, int
   return GBP_OK;
 }
 
+// gbp_plan_stage_timing: fold every completed timed half into the sums
+void timing_collect(gbp_plan_ws *w, bool wait) {
+  for (size_t i = 0; i < w->ntring; i++) {
+    auto &h = w->tring[i];
+    if (!h.pending) continue;
+    if (wait) (void)hipEventSynchronize(h.ev[5]);
+    if (hipEventQuery(h.ev[5]) != hipSuccess) continue;
+    float ms[5] = {0, 0, 0, 0, 0};
+    (void)hipEventElapsedTime(&ms[0], h.ev[0], h.ev[5]);
+    (void)hipEventElapsedTime(&ms[1], h.ev[0], h.ev[1]);
+    if (h.star) {
+      (void)hipEventElapsedTime(&ms[2], h.ev[1], h.ev[2]);
+      (void)hipEventElapsedTime(&ms[3], h.ev[3], h.ev[4]);
+      (void)hipEventElapsedTime(&ms[4], h.ev[2], h.ev[5]);
+    } else {
+      (void)hipEventElapsedTime(&ms[4], h.ev[1], h.ev[5]);
+    }
+    for (int k = 0; k < 5; k++) w->tsum[k] += 1e3 * (double)ms[k];
+    w->tcount++;
+    h.pending = false;
+  }
+}
+
+// the next timing slot (its previous half folded in first), or nullptr
+gbp_plan_ws::TimedHalf *timing_slot(gbp_plan_ws *w) {
+  if (!w->timing || !w->ntring) return nullptr;
+  gbp_plan_ws::TimedHalf *h = &w->tring[w->tnext];
+  w->tnext = (w->tnext + 1) % w->ntring;
+  if (h->pending) timing_collect(w, true);
+  return h;
+}
+
 template <class ZT>
 int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int32_t half,
                    int direction, int64_t batch, uint64_t seed, uint64_t target_stream,
@@ -2567,6 +2611,13 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   auto run = [&](int x) { return ord(first_stage) <= ord(x) && ord(x) <= ord(last_stage); };
   const bool searched = la && la->searched;  // stages 0-2's draws and search done ahead
   if (searched && first_stage != 0) return GBP_E_INVALID_ARG;
+  // whole halves only (a resumed one is not timed)
+  gbp_plan_ws::TimedHalf *th = (O && first_stage == 0 && last_stage == 5) ? timing_slot(w) : nullptr;
+  if (th) {
+    th->star = w->star != 0;
+    th->half = half;
+    HIPCHK_P(hipEventRecord(th->ev[0], s));
+  }
   if (searched && (!std::is_same_v<ZT, float> || t->sampling.state_flag || t->sampling.action_flag))
     return GBP_E_INVALID_ARG;
   if (searched) {
@@ -2626,6 +2677,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
                        w->esn, w->ean, T->v, T->vh, T->hm, T->a, T->g, T->parent, T->count, w->evtx,
                        w->tiles,
                        next_epoch(w), half, T->cap, ++w->seq, T->child, T->sibling, T->prev, w->star);
+  if (th) HIPCHK_P(hipEventRecord(th->ev[1], s));
   const int kT = direction == GBP_FORWARD ? 0 : 1;  // T's tree index (Ta 0, Tb 1)
   gbp_plan_ws::StarSet &S = w->ss[half & 1];
   if (w->star && run(6)) {
@@ -2645,6 +2697,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     if (rc) return rc;
     hipLaunchKernelGGL(k_star_gate, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, S.srf,
                        half, ++w->seq);
+    if (th) HIPCHK_P(hipEventRecord(th->ev[2], s));
   }
   if (w->star && run(7)) {
     // stage 7, the ordered replay, on star_stream: it changes T's parents, g
@@ -2653,6 +2706,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     // this half and the next half's extends of O run beside it
     HIPCHK_P(hipEventRecord(w->star_e6, s));
     HIPCHK_P(hipStreamWaitEvent(w->star_stream, w->star_e6, 0));
+    if (th) HIPCHK_P(hipEventRecord(th->ev[3], w->star_stream));
     hipLaunchKernelGGL(k_star_replay, dim3(1), dim3(RW), 0, w->star_stream, st, T->v, T->a, T->g,
                        T->parent, T->child, T->sibling, T->prev, S.soff, S.snb, S.sown, S.srowof,
                        S.sra, S.srf, S.meta, T->bfs, T->bfs + T->cap, T->count, ++w->seq);
@@ -2700,6 +2754,11 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
         HIPCHK_P(hipEventRecord(w->star_rdone[kT], w->star_stream));
       }
     }
+  }
+  if (th) {
+    if (th->star) HIPCHK_P(hipEventRecord(th->ev[4], w->star_stream));
+    HIPCHK_P(hipEventRecord(th->ev[5], s));
+    th->pending = true;
   }
   return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
 }
@@ -3032,6 +3091,13 @@ extern "C++" __attribute__((visibility("hidden"))) hipStream_t gbp_internal_la_s
 }
 
 static void ws_free(gbp_plan_ws *w) {
+  if (w->ntring) {
+    (void)hipDeviceSynchronize();
+    for (size_t i = 0; i < w->ntring; i++)
+      for (auto &e : w->tring[i].ev)
+        if (e) (void)hipEventDestroy(e);
+    delete[] w->tring;
+  }
   if (w->la_go) (void)hipEventDestroy(w->la_go);
   if (w->la_done) (void)hipEventDestroy(w->la_done);
   if (w->star_stream) {
@@ -3227,6 +3293,35 @@ int gbp_plan_star_config(gbp_plan_ws *w, int enable, double delta, int64_t max_p
   return GBP_OK;
 }
 
+int gbp_plan_stage_timing(gbp_plan_ws *w, int enable) {
+  if (!w) return GBP_E_BAD_HANDLE;
+  Guard g(w->device);
+  if (enable && !w->ntring) {
+    w->tring = new (std::nothrow) gbp_plan_ws::TimedHalf[256];
+    if (!w->tring) return GBP_E_ALLOC;
+    w->ntring = 256;
+    for (size_t i = 0; i < w->ntring; i++)
+      for (auto &e : w->tring[i].ev)
+        if (hipEventCreate(&e) != hipSuccess) return GBP_E_HIP;
+  }
+  w->timing = enable != 0;
+  return GBP_OK;
+}
+
+int gbp_plan_stage_times(gbp_plan_ws *w, double *us, int n, int64_t *halves, int reset) {
+  if (!w) return GBP_E_BAD_HANDLE;
+  if (!us || n < 5) return GBP_E_INVALID_ARG;
+  Guard g(w->device);
+  timing_collect(w, false);
+  for (int k = 0; k < 5; k++) us[k] = w->tsum[k];
+  if (halves) *halves = w->tcount;
+  if (reset) {
+    for (double &x : w->tsum) x = 0;
+    w->tcount = 0;
+  }
+  return GBP_OK;
+}
+
 int gbp_plan_reset(gbp_plan_ws *w, int64_t extend_counter, gbp_stream stream) {
   if (!w) return GBP_E_BAD_HANDLE;
   Guard g(w->device);
@@ -3292,6 +3387,9 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *Ta, gbp_tree *
                      t->storage == GBP_STORAGE_F32;  // (k_nn_mfma<float> draws)
   bool searched = false, used = false;
   int rc = GBP_OK;
+  if (first_stage != 0)  // a resume: the halted half and the gated ones after it ran nothing
+    for (size_t i = 0; i < w->ntring; i++)
+      if (w->tring[i].pending && w->tring[i].half >= first_half) w->tring[i].pending = false;
   for (int32_t i = 0; i < n_halves && !rc; i++) {
     const int32_t h = first_half + i;
     const int k = h & 1;

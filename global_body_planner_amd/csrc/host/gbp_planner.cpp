@@ -1609,6 +1609,7 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
   DeviceTrees D;
   chk(gbp_stream_create(dev, &D.stream), "stream");
   chk(gbp_plan_ws_create(h, batch, &D.ws), "plan workspace");
+  if (st.stage_timing) chk(gbp_plan_stage_timing(D.ws, 1), "stage timing");
   int64_t cap = std::max<int64_t>(1 << 16, 4 * (int64_t)batch);
   int64_t known[2] = {1, 1};
   for (int k = 0; k < 2; k++) {
@@ -1707,6 +1708,13 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
   elapsed_to_first = t_first >= 0 ? std::chrono::duration<double>(t_first)
                                   : std::chrono::duration<double>(since());
   extend_counter_ = ps.ext_counter;
+  if (st.stage_timing) {
+    double us[5];
+    int64_t nh = 0;
+    chk(gbp_plan_stage_times(D.ws, us, 5, &nh, 1), "stage times");
+    for (int k = 0; k < 5; k++) st.stage_us[k] += us[k];
+    st.stage_halves += nh;
+  }
   const int32_t halves_run = (goal_found ? ps.meet_half + 1 : half) - half0;
   st.halves += halves_run;
   st.iterations += (halves_run + 1) / 2;
@@ -2212,6 +2220,7 @@ bool RRTStarConnectClass::buildRRTStarConnectDevice(FastTerrainMap &terrain, Sta
   // neighbour pairs of one half (2 connect checks each) and REACHED connections of the run
   chk(gbp_plan_star_config(D.ws, 1, delta, std::max<int64_t>(1 << 18, 8 * (int64_t)batch), 1 << 22),
       "star config");
+  if (st.stage_timing) chk(gbp_plan_stage_timing(D.ws, 1), "stage timing");
   int64_t cap = std::max<int64_t>(1 << 16, 4 * (int64_t)batch);
   int64_t known[2] = {1, 1};
   for (int k = 0; k < 2; k++) {
@@ -2287,6 +2296,13 @@ bool RRTStarConnectClass::buildRRTStarConnectDevice(FastTerrainMap &terrain, Sta
   }
   extend_counter_ = ps.ext_counter;
   rewires_ = ps.stat_rewires;
+  if (st.stage_timing) {
+    double us[5];
+    int64_t nh = 0;
+    chk(gbp_plan_stage_times(D.ws, us, 5, &nh, 1), "stage times");
+    for (int k = 0; k < 5; k++) st.stage_us[k] += us[k];
+    st.stage_halves += nh;
+  }
   st.halves += half - half0;
   st.iterations += (half - half0) / 2;
   st.targets += ps.stat_targets;
@@ -2348,7 +2364,8 @@ bool RRTStarConnectClass::buildRRTStarConnectDevice(FastTerrainMap &terrain, Sta
 // flat C entry point
 // ============================================================================
 // the layout planner.py's PlanParams mirrors (tests/test_abi.py)
-static_assert(sizeof(gbp_plan_params) == 456, "gbp_plan_params layout");
+static_assert(sizeof(gbp_plan_params) == 464, "gbp_plan_params layout");
+static_assert(sizeof(gbp_plan_result) == 360, "gbp_plan_result layout");
 
 extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r,
                                     double *path_states, double *path_actions, int capacity) {
@@ -2375,6 +2392,7 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     BatchStats st;
     TreeDump dump;
     st.max_halves = p->max_halves > 0 ? p->max_halves : 0;
+    st.stage_timing = p->stage_timing != 0;
     if (p->algorithm == 3 || p->algorithm == 5) {
       if (p->algorithm == 3) {  // one device search per rank: the ranks' polls pair up
         st.stop_poll = p->stop_poll;
@@ -2429,6 +2447,8 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     r->vertices_b = st.vertices_b;
     r->n_states = found ? (int)states.size() : 0;
     r->rewires = st.rewires;
+    for (int k = 0; k < 5; k++) r->stage_us[k] = st.stage_us[k];
+    r->stage_halves = st.stage_halves;
     r->solutions = st.solutions;
     for (int k = 0; k < 4; k++) {
       r->extent_a[k] = st.extent_a[k];

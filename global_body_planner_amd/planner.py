@@ -34,7 +34,7 @@ class PlanParams(ctypes.Structure):
                 ("tree_parent", _P * 2), ("tree_g", _P * 2), ("stop_poll", _P),
                 ("stop_ctx", _P), ("init_n", ctypes.c_int64 * 2), ("init_v", _P * 2),
                 ("init_a", _P * 2), ("init_parent", _P * 2), ("first_half", ctypes.c_int64),
-                ("extend_base", ctypes.c_int64)]
+                ("extend_base", ctypes.c_int64), ("stage_timing", ctypes.c_int)]
 
 # int (*stop_poll)(void *ctx, int local_stop, int found)
 StopPoll = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int)
@@ -54,7 +54,8 @@ class PlanResult(ctypes.Structure):
                 ("nn_rechecks", ctypes.c_int64), ("nn_scans", ctypes.c_int64),
                 ("reported_length", _D), ("reported_yaw", _D), ("meet_a", ctypes.c_int32),
                 ("meet_b", ctypes.c_int32), ("halves", ctypes.c_int64),
-                ("polls", ctypes.c_int64), ("stopped_by_peer", ctypes.c_int32)]
+                ("polls", ctypes.c_int64), ("stopped_by_peer", ctypes.c_int32),
+                ("stage_us", _D * 5), ("stage_halves", ctypes.c_int64)]
 
 
 _planner = None
@@ -114,7 +115,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
                      sampling=None, fragile_eps=None, adaptive=False, nn_stats=False,
                      max_halves=0, trees=False,
                      tree_capacity=1 << 18, stop_poll=None, init_trees=None, first_half=0,
-                     extend_base=0):
+                     extend_base=0, stage_timing=False):
     """Plan start -> goal on terrain `data` (terrain_data.TerrainData).
 
     algorithm 0: batch-synchronous RRT-Connect, stops at the first solution;
@@ -150,7 +151,11 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
       vertices later parents), the first half-iteration (its targets are the
       draws a search from the roots makes there; even for algorithm 5) and the
       candidate stream's first extend index; max_halves then counts the
-      continuation's halves."""
+      continuation's halves.
+    stage_timing: algorithms 3 / 5 — time every half-iteration's stage groups
+      with hipEvents (diagnostics): out["stage_us"] = summed microseconds of
+      [the half, stages 0-3, 6, 7 (its own stream), 4-5] over
+      out["stage_halves"] halves."""
     L = load()
     x = np.ascontiguousarray(data.x, dtype=np.float64)
     y = np.ascontiguousarray(data.y, dtype=np.float64)
@@ -171,6 +176,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     p.fragile_eps_fm = 0 if fragile_eps is None else int(round(fragile_eps * 1e15))
     p.adaptive = int(bool(adaptive))
     p.nn_stats = int(bool(nn_stats))
+    p.stage_timing = int(bool(stage_timing))
     p.max_halves = int(max_halves)
     p.first_half, p.extend_base = int(first_half), int(extend_base)
     warm = []
@@ -213,6 +219,7 @@ def plan_rrt_connect(data, start, goal, *, batch=64, max_time=5.0, seed=20251018
     out = {k: getattr(r, k) for k, _ in PlanResult._fields_}
     out["extent_a"], out["extent_b"] = list(r.extent_a), list(r.extent_b)
     out["halts"] = list(r.halts)
+    out["stage_us"] = list(r.stage_us)
     for name, arrs, nv in zip("ab", tb, (r.vertices_a, r.vertices_b)):
         m = min(int(nv), tree_capacity)
         out[name] = {k: v[:m].copy() for k, v in arrs.items()}

@@ -556,6 +556,19 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *ws, gbp_tree *Ta, gbp_tree 
  * at stage 7).  enable = 0 returns the workspace to RRT-Connect. */
 int gbp_plan_star_config(gbp_plan_ws *ws, int enable, double delta, int64_t max_pairs,
                          int64_t max_shared);
+/* diagnostics: per half-iteration timing events (hipEvents with timing, on
+ * the streams the stages run on) while enabled; gbp_plan_stage_times adds up
+ * every timed half completed so far, in microseconds:
+ *   us[0] the whole half (its first launch's start to stage 5's end),
+ *   us[1] stages 0-3 (targets, the extends' search, their pair checks, select,
+ *         append), us[2] stage 6 (RRT*: neighbourhoods, connect checks and
+ *         their pair checks), us[3] stage 7 on the replay's stream (RRT*:
+ *         replay, plus the best connection's ranking after Tb's halves),
+ *   us[4] stages 4-5 (the connects' search, attemptConnect, append)
+ * and *halves the number of halves summed (n >= 5; reset clears).  A half's
+ * events are read once the caller has synchronised its stream (status read). */
+int gbp_plan_stage_timing(gbp_plan_ws *ws, int enable);
+int gbp_plan_stage_times(gbp_plan_ws *ws, double *us, int n, int64_t *halves, int reset);
 /* re-decides the halted stage's FRAGILE items on the host (T, O, direction,
  * batch of the halted half) and clears the halt; *resume_stage = the stage to
  * resume that half at (-1: nothing was halted) */

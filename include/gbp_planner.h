@@ -427,6 +427,11 @@ struct BatchStats {
   const double *warm_a[2] = {nullptr, nullptr};
   const int32_t *warm_parent[2] = {nullptr, nullptr};
   int64_t warm_half = 0, warm_extend = 0;
+  // diagnostics (device loop): time each half-iteration's stage groups
+  // (gbp_plan_stage_timing) into stage_us (half, stages 0-3, 6, 7, 4-5)
+  bool stage_timing = false;
+  double stage_us[5] = {0, 0, 0, 0, 0};
+  int64_t stage_halves = 0;
 };
 
 class RRTConnectClass : public RRTClass {
@@ -671,6 +676,8 @@ typedef struct {
   const int32_t *init_parent[2];
   int64_t first_half;
   int64_t extend_base;
+  int stage_timing;       // algorithms 3 / 5: time every half-iteration's stage groups
+                          // (gbp_plan_stage_timing; diagnostics, adds events per half)
 } gbp_plan_params;
 
 typedef struct {
@@ -697,6 +704,9 @@ typedef struct {
   int64_t halves;              // half-iterations run
   int64_t polls;               // algorithm 3 with stop_poll: polls made
   int32_t stopped_by_peer;     // ... and 1 if another rank's solution ended this search
+  double stage_us[5];          // with stage_timing: summed per-half microseconds
+                               // (gbp_plan_stage_times: half, stages 0-3, 6, 7, 4-5)
+  int64_t stage_halves;        //   over this many timed halves
 } gbp_plan_result;
 
 /* plans from start to goal; path_states[capacity][8] / path_actions[capacity][10]

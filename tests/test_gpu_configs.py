@@ -73,6 +73,9 @@ def _config4_worker(rank, world, port, q, name, xy, batch):
     # config 4's own terrain, the goal on the start side of the 0.55-m step at
     # x = 7.0 (bench.py TTFS_PAIRS "synth-rough-1024-near", tools/wall_check.py)
     ("synth-rough-1024", (1.0, 10.23, 6.8, 10.23), 8192),
+    # ... and at config 3's own per-half draws (SURVEY's 43,690 targets after
+    # the STANCE filter: bench.py's planner batch, tests/test_gpu_oracle_scale.py)
+    ("synth-rough-1024", (1.0, 10.23, 6.8, 10.23), 92749),
 ])
 def test_config4_restart_trees_best_path_allgather(gpu, name, xy, batch):
     import torch.multiprocessing as mp

@@ -169,6 +169,8 @@ def test_rrt_star_equals_oracle(gpu, name, xy, batch, seed, halves, algorithm, f
         assert dev["path_cost"] == ref["best_cost"]
     if fragile_eps is not None:
         assert dev["fragile_resolved"] > 0
+        if algorithm == 5:  # the insertion checks' own halt (resume at the replay) ran
+            assert dev["halts"][3] > 0, dev["halts"]
     print(f"{name} RRT* batch {batch} alg {algorithm}: {halves} halves, trees {len(ref['a']['v'])}+"
           f"{len(ref['b']['v'])}, {ref['rewires']} rewires, {ref['solutions']} connections, "
           f"{dev['fragile_resolved']} re-decided, halts {dev['halts']}")

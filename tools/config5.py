@@ -41,10 +41,36 @@ def first_valid(T, x, y, step, n=400):
     return st[k]
 
 
+STAGES = ("half", "stages 0-3: targets, extends' search, pair checks, select, append",
+          "stage 6: neighbourhoods (k_star_count/scan/fill), connect checks (k_star_prep, "
+          "pair checks, k_star_gate)",
+          "stage 7 on its own stream: k_star_replay (+ k_star_rank after Tb's halves)",
+          "stages 4-5: connects' search, k_connect, append, k_star_shared")
+
+
+def stage_split(data, start, goal, batch, max_time, seed, device):
+    """The same run again with per-half timing events (gbp_plan_stage_timing):
+    microseconds per half-iteration of each stage group; stage 7 runs beside
+    stages 4-5 and the next half, so the groups do not add up to the half."""
+    out = planner.plan_rrt_star_connect(data, start, goal, batch=batch, max_time=max_time,
+                                        seed=seed, device=device, device_loop=True,
+                                        stage_timing=True)
+    nh = max(1, int(out["stage_halves"]))
+    split = {name: round(us / nh, 2) for name, us in zip(STAGES, out["stage_us"])}
+    return {"us_per_half": split, "timed_halves": int(out["stage_halves"]),
+            "halves": int(out["halves"]),
+            "k_star_on_caller_stream_us_per_half": split[STAGES[2]],
+            "k_star_replay_side_stream_us_per_half": split[STAGES[3]],
+            "source": "hipEvents per half on the streams the stages run on (a second run of "
+                      "the same length with timing on)"}
+
+
 def run_config5(terrain="synth-fractal-4096", batch=4096, max_time=20.0, seed=20251020, span=8.0,
-                algorithm=5, rank=0, world=1, device=0, data=None):
+                algorithm=5, rank=0, world=1, device=0, data=None, split=False):
     """One RRT*-Connect run per rank (seed + rank), best path all_gathered;
-    returns the record (rank 0's view) for every rank."""
+    returns the record (rank 0's view) for every rank.  split: add the
+    per-stage time split (a second timed run).  (bench.py adds the CPU
+    baseline: the oracle's RRT* loop.)"""
     dev = torch.device("cuda", device)
     t0 = time.perf_counter()
     if data is None:
@@ -75,13 +101,17 @@ def run_config5(terrain="synth-fractal-4096", batch=4096, max_time=20.0, seed=20
         work[4] = t_max[0]
     b = sharding.unpack_path(best)
     wall = float(work[4].item())
-    return {
+    extra = {}
+    if split and algorithm == 5:
+        extra["stage_split"] = stage_split(data, start, goal, batch, max_time, seed + rank, device)
+    return {**extra,
         "config": "5: RRT*-Connect, %s, %d GPU(s), %d draws per half, %.1f s anytime" % (
             terrain, world, batch, max_time),
         "planner": "buildRRTStarConnectDevice (search resident on the device)" if algorithm == 5
                    else "buildRRTStarConnectBatched (host-driven insertion replay)",
         "terrain_gen_s": round(t_gen, 2),
         "start": start[:3].tolist(), "goal": goal[:3].tolist(),
+        "start_state": start.tolist(), "goal_state": goal.tolist(), "seed": seed, "batch": batch,
         "time_to_first_solution_s": float(ttf.item()),
         "best_cost": b["cost"], "best_rank": who, "best_path_states": int(b["states"].shape[0]),
         "pair_checks_per_s": round(float(work[0].item()) / wall, 1),
@@ -104,6 +134,7 @@ def main():
     p.add_argument("--span", type=float, default=8.0)
     p.add_argument("--algorithm", type=int, default=5, choices=(1, 5))
     p.add_argument("--out", default=None)
+    p.add_argument("--split", action="store_true", help="add the per-stage time split")
     a = p.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -111,7 +142,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
-    res = run_config5(a.terrain, a.batch, a.max_time, a.seed, a.span, a.algorithm, rank, world, local)
+    res = run_config5(a.terrain, a.batch, a.max_time, a.seed, a.span, a.algorithm, rank, world, local,
+                      split=a.split)
     if rank == 0:
         line = json.dumps(res)
         print(line, flush=True)
