@@ -175,6 +175,22 @@ struct SnewRec {
 };
 constexpr int SN_RING = 2 * 64;  // entries per wave: < 64 left + up to 64 queued in a step
 
+// -DGBP_XWAVE (A/B variant): the workgroup-level helper
+// exchange.  Waves pair up (w, w ^ 1).  A wave whose own work is done does
+// not exit while its partner still runs: it becomes 64 more helpers of the
+// partner's owners.  Per step the partner (in its tail) publishes its owners'
+// (stage, t, ts, V) in its box and raises seq; the helper wave evaluates the
+// samples helpers n_idle .. n_idle + 63 would (same slot / owner rule, rows
+// read from the partner's LDS rows), writes the result words and raises ack;
+// the partner consumes them after its own helpers', in slot order.
+struct XBox {
+  int seq, ack, fin, n_idle;
+  unsigned long long act;
+  int st[64];
+  uint32_t vb[64], r0[64], r1[64];
+  double t[64], ts[64];
+};
+
 // (diagnostic build, -DGBP_LOOP_PROF: cycles per phase of the persistent loop,
 // per wave, read by gbp_loop_prof_read; tools/loop_prof.py)
 #ifdef GBP_LOOP_PROF
@@ -239,6 +255,22 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
       for (int k = 0; k < 8; k++) s_new[8 * (size_t)r.idx + k] = o[k];
     }
   };
+#ifdef GBP_XWAVE
+  XBox *const xbox = (XBox *)((SnewRec *)(SA + (size_t)blockDim.x * SA_ROW) + (blockDim.x / WAVE) * SN_RING);
+  const int wv = threadIdx.x / WAVE;
+  XBox *const mybox = xbox + wv;
+  XBox *const pbox = xbox + (wv ^ 1);
+  const bool has_partner = (wv ^ 1) < (int)(blockDim.x / WAVE);
+  double *const partner_rows = SA + (size_t)((wv ^ 1) * WAVE) * SA_ROW;
+  if (lane == 0) {
+    mybox->seq = 0;
+    mybox->ack = 0;
+    mybox->fin = 0;
+  }
+  __syncthreads();
+  int myseq = 0, served = 0;
+  bool fin_sent = false;
+#endif
   Lane L;
   L.s = SA + (size_t)threadIdx.x * SA_ROW;
   L.a = L.s + 8;
@@ -291,7 +323,33 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
       cur += take;
     }
     const unsigned long long act = __ballot(L.stage != ST_IDLE);
+#ifdef GBP_XWAVE
+    // this wave's work is done: serve the partner's requests until it is done
+    bool serve = false;
+    if (!act) {
+      if (!has_partner) break;
+      if (!fin_sent) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&mybox->fin, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        fin_sent = true;
+      }
+      int pseq, pfin;
+      for (;;) {
+        pseq = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&pbox->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+        pfin = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&pbox->fin, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (pseq != served || pfin) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (pseq == served) break;  // the partner finished with no request pending
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      served = pseq;
+      serve = true;
+    }
+#else
     if (!act) break;
+#endif
     LP_T(t1);
     LP_ADD(0, t0, t1);
     const bool owner = L.stage != ST_IDLE;
@@ -311,6 +369,42 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
     double t_eval = owner ? stage_time(L) : 0.0;
     uint32_t vbase = L.acc.V;
     bool has = owner;
+#ifdef GBP_XWAVE
+    // a tail step with the partner free: publish the owners' loop state
+    bool xhelp = false;
+    if (tail && !serve && has_partner) {
+      xhelp = __builtin_amdgcn_readfirstlane(
+                  __hip_atomic_load(&pbox->fin, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0;
+      if (xhelp) {
+        mybox->st[lane] = L.stage;
+        mybox->t[lane] = L.t;
+        mybox->ts[lane] = L.ts;
+        mybox->vb[lane] = L.acc.V;
+        if (lane == 0) {
+          mybox->act = act;
+          mybox->n_idle = WAVE - n_act;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        myseq++;
+        if (lane == 0) __hip_atomic_store(&mybox->seq, myseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    if (serve) {
+      // helper n_idle + lane of the partner's owners (the rule of the tail below)
+      const unsigned long long pact = pbox->act;
+      const int pn = __popcll(pact);
+      const int j = pbox->n_idle + lane;
+      const int src = nth_set_bit(pact, j % pn);
+      slot = 1 + j / pn;
+      ps = partner_rows + src * SA_ROW;
+      st = pbox->st[src];
+      double t = pbox->t[src], ts = pbox->ts[src];
+      vbase = pbox->vb[src];
+      has = true;
+      for (int k = 0; k < slot && has; k++) has = advance_on_success<ADAPTIVE>(st, ps + 8, t, ts);
+      t_eval = sample_time(st, ps + 8, t);
+    } else
+#endif
     if (tail) {
       const unsigned long long idle = ~act;
       const int j = __popcll(idle & lt_mask);
@@ -339,6 +433,16 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
     }
     LP_T(t3);
     LP_ADD(2, t2, t3);
+#ifdef GBP_XWAVE
+    if (serve) {  // the results, then the acknowledgement
+      pbox->r0[lane] = (acc_s.flags & 0xFFFFu) | (ok ? 1u << 16 : 0u) | (has ? 1u << 17 : 0u) |
+                       ((acc_s.V - (vbase + (uint32_t)slot)) << 18);
+      pbox->r1[lane] = acc_s.G;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&pbox->ack, served, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      continue;
+    }
+#endif
     bool decided = false;
     if (owner) {  // the lane's own sample
       L.acc.G += acc_s.G;
@@ -349,12 +453,25 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
     if (tail) {  // consume helper results in slot order
       const unsigned long long idle = ~act;
       const int n_idle = WAVE - n_act;
+#ifdef GBP_XWAVE
+      // the partner's 64 helpers come after this wave's own (helpers n_idle ..)
+      int n_help = n_idle;
+      if (xhelp) {
+        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                   &mybox->ack, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != myseq)
+          __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        n_help += WAVE;
+      }
+#else
+      const int n_help = n_idle;
+#endif
       const uint32_t w0 = (acc_s.flags & 0xFFFFu) | (ok ? 1u << 16 : 0u) | (has ? 1u << 17 : 0u) |
                           ((acc_s.V - (vbase + (uint32_t)slot)) << 18);
       const uint32_t w1 = acc_s.G;
       const int my_rank = __popcll(act & lt_mask);
       bool chain = owner && !decided && ok;
-      const int kmax = (n_idle + n_act - 1) / n_act;
+      const int kmax = (n_help + n_act - 1) / n_act;
       for (int k = 1; k <= kmax; k++) {
         // every owner's chain has ended (a failure or a decision): the rest of
         // the helpers' results are not consumed (config 3 0.1315 -> 0.1206 ms,
@@ -362,9 +479,15 @@ __global__ __launch_bounds__(512, W) void k_validate_persistent(
         // shuffles and transitions whatever the chains did)
         if (!__ballot(chain)) break;
         const int j = (k - 1) * n_act + my_rank;
-        const bool exists = owner && j < n_idle;
-        const int src = exists ? nth_set_bit(idle, j) : lane;
-        const uint32_t r0 = __shfl(w0, src), r1 = __shfl(w1, src);
+        const bool exists = owner && j < n_help;
+        const int src = (exists && j < n_idle) ? nth_set_bit(idle, j) : lane;
+        uint32_t r0 = __shfl(w0, src), r1 = __shfl(w1, src);
+#ifdef GBP_XWAVE
+        if (exists && j >= n_idle) {
+          r0 = mybox->r0[j - n_idle];
+          r1 = mybox->r1[j - n_idle];
+        }
+#endif
         if (chain && exists && ((r0 >> 17) & 1u)) {
           L.acc.G += r1;
           L.acc.V += (r0 >> 18) & 1u;
@@ -895,6 +1018,8 @@ int launch_validate_w(gbp_terrain *t, int64_t n, const double *s, const double *
 #ifdef GBP_LDS_TERRAIN
       const size_t zb = sizeof(ZT) * 2 * (size_t)(t->nx - 1) * t->ny;
       if (coords + rows + ring + zb > t->lds_max) return GBP_E_SHAPE;  // the A/B variant only
+#elif defined(GBP_XWAVE)
+      const size_t zb = sizeof(XBox) * (size_t)(block / WAVE);  // the helper exchange's boxes
 #else
       const size_t zb = 0;
 #endif
