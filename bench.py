@@ -415,11 +415,11 @@ def _cpu_model():
     return None
 
 
-def config5_cpu_baseline(c5, halves=2):
+def config5_cpu_baseline(c5, halves=8):
     """Config 5's CPU baseline: the oracle's RRT*-Connect loop (orc_plan with
     star; the reference's O(N) bracket scans), 1 thread, on the same terrain
     with the same start / goal, seed, streams and draws as the device run,
-    from the roots for `halves` half-iterations (~14 s of CPU work)."""
+    from the roots for `halves` half-iterations (~12 s on the GPU box's EPYC)."""
     import oracle
     data = td.by_name("synth-fractal-4096")
     O = oracle.OracleTerrain.from_data(data)

@@ -3063,7 +3063,11 @@ extern "C++" __attribute__((visibility("hidden"))) hipStream_t gbp_internal_la_s
   if (hipGetDevice(&prev) != hipSuccess) prev = -1;
   if (prev != device && hipSetDevice(device) != hipSuccess) return nullptr;
   const char *env = getenv("GBP_LA_CUS");
-  const int n = num_cus, cus = env && *env ? atoi(env) : n - n / 8;
+  // the last XCD's CUs left out (from the device's XCC count, not
+  // an assumed 8; one XCC or an unknown count: unmasked)
+  int xcc = 0;
+  if (hipDeviceGetAttribute(&xcc, hipDeviceAttributeNumberOfXccs, device) != hipSuccess) xcc = 0;
+  const int n = num_cus, cus = env && *env ? atoi(env) : (xcc >= 2 ? n - n / xcc : n);
   hipStream_t st = nullptr;
   hipError_t e;
   if (cus > 0 && cus < n) {
@@ -3271,7 +3275,9 @@ int gbp_plan_star_config(gbp_plan_ws *w, int enable, double delta, int64_t max_p
     // round-robin — with the caller's stream the replay then ran in line with
     // the connects it should overlap (config 5: 52 vs 66 M pair checks/s with
     // 8 queues)
-    const int n = w->num_cus, lo = n - n / 8;
+    int xcc = 0;
+    if (hipDeviceGetAttribute(&xcc, hipDeviceAttributeNumberOfXccs, w->device) != hipSuccess) xcc = 0;
+    const int n = w->num_cus, lo = xcc >= 2 ? n - n / xcc : n;
     std::vector<uint32_t> mask((n + 31) / 32, 0u);
     for (int c = lo; c < n; c++) mask[c / 32] |= 1u << (c % 32);
     const hipError_t e = (lo > 0 && lo < n)
