@@ -167,6 +167,8 @@ struct gbp_plan_ws {
   double *ns_d = nullptr;
   int32_t *ns_i = nullptr;
   uint32_t *ns_fin = nullptr;
+  int ns_grid = 1;             // its workgroups (one per CU of an XCD)
+  int64_t ns_capq = 0;         // queries its partials hold (ns_grid x ns_capq slots)
   NsBuf nsb[2] = {};           // k_nn_scan's lists: the caller's stream, the look-ahead's
   // the look-ahead search (gbp_plan_halves_dev): half h + 1's targets drawn
   // and searched on la_stream while half h's extends, connects and appends
@@ -1053,10 +1055,11 @@ __global__ __launch_bounds__(NS_TB) void k_nn_small(gbp_plan_status *st, const i
                                                      const double *__restrict__ v,
                                                      const int32_t *__restrict__ nv_dev,
                                                      int32_t *__restrict__ out, double *__restrict__ pd,
-                                                     int32_t *__restrict__ pi, uint32_t *fin, uint64_t seq) {
+                                                     int32_t *__restrict__ pi, uint32_t *fin, int64_t capq,
+                                                     uint64_t seq) {
   if (gated(st, seq)) return;
   const int64_t nq = *nq_dev, nv = *nv_dev, q_off = q_off_dev ? *q_off_dev : 0;
-  if (nq <= 0 || nq > NS_MAXQ) return;
+  if (nq <= 0 || nq > capq) return;
   __shared__ double sd[NS_TB / WAVE][NS_GQ];
   __shared__ int si[NS_TB / WAVE][NS_GQ];
   __shared__ bool last;
@@ -2466,18 +2469,26 @@ int nn_launch(gbp_plan_ws *w, const int32_t *nq_dev, const double *q, const int3
               const gbp_tree *tr, int32_t *out, int num_cus, hipStream_t s,
               const _Float16 *qh = nullptr, const NhPrep<ZT> *prep = nullptr,
               double *cs = nullptr, bool *prepped = nullptr, const NnSide *side = nullptr,
-              bool small = false) {
+              bool small = false, bool small_any = false) {
   if (prepped) *prepped = false;
   // small: up to NS_MAXQ queries take the direct fp64 search (k_nn_small),
   // the matrix-core pair then returns at once (the count is on the device)
   const int small_max = small && !prep ? NS_MAXQ : 0;
+  // ... and when k_nn_small's partials hold a whole batch of queries (the
+  // workspace's max_batch, which bounds the count), it takes every count and
+  // the other four launches are not made at all: in the steady state of the
+  // planner and of config 5 they returned at once but cost ~21 us of the
+  // caller's stream per half (the connects' queries are the half's new
+  // vertices, a few; a large count is slower this way, never wrong)
+  const bool direct_only = small_any && small_max && !side && w->ns_capq >= w->bmax;
   if (small_max)
     // one workgroup per CU of an XCD: in the planner the look-ahead search
     // holds the other seven (32 blocks 171.8 M extends/s, 64: 171.2, 128:
     // 169.3, 512: 160.8, the matrix-core pair alone 169.2; r05k_small_ab*.txt)
-    hipLaunchKernelGGL(k_nn_small, dim3(std::max(1, std::min(NS_BLOCKS, num_cus / 8))), dim3(NS_TB), 0, s, w->st,
-                       nq_dev, q, q_off_dev, tr->v, side ? side->nv : tr->count, out, w->ns_d, w->ns_i,
-                       w->ns_fin, side ? 0 : ++w->seq);
+    hipLaunchKernelGGL(k_nn_small, dim3(w->ns_grid), dim3(NS_TB), 0, s, w->st, nq_dev, q, q_off_dev,
+                       tr->v, side ? side->nv : tr->count, out, w->ns_d, w->ns_i, w->ns_fin,
+                       direct_only ? w->ns_capq : (int64_t)NS_MAXQ, side ? 0 : ++w->seq);
+  if (direct_only) return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
   const int items = w->nn_items;
   const int gm = items / (NH_TB / WAVE);  // the search's workgroups: one wave per item
   float4 *pm = (float4 *)(side ? w->nn_d2 : w->nn_d);
@@ -2717,7 +2728,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   if (run(4)) {
     // queries: T's new vertices, rows [added_base, added_base + n_added)
     int rc = nn_launch<float>(w, &st->n_added, T->v, &st->added_base, O, w->nno, cus, s, T->vh, nullptr,
-                       nullptr, nullptr, nullptr, true);
+                       nullptr, nullptr, nullptr, true, true);
     if (rc) return rc;
     const int cm = (t->opt_affine && t->affine) ? 2 : 0;
     const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * 4, (batch + 3) / 4));
@@ -3132,10 +3143,15 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->nn_items = NH_ITEMS;
   w->ntiles = (max_batch + TB - 1) / TB + 1;  // k_targets' 256-draw tiles (k_compact_targets: 1024)
   const int64_t b = max_batch, m = GBP_NUM_GEN_STATES * max_batch;
-  const size_t bytes = sizeof(gbp_plan_status) + 16 * w->ntiles + 3 * (64 * b + 4 * b + 64 * b + 64 * b) +
+  // k_nn_small's partials: NS_MAXQ queries per workgroup, or a whole batch
+  // when that stays within 2^22 slots (~48 MB; bench's planner: 92,749 x 32)
+  w->ns_grid = std::max(1, std::min(NS_BLOCKS, t->num_cus / 8));
+  w->ns_capq = (int64_t)w->ns_grid * b <= ((int64_t)1 << 22) ? std::max<int64_t>(b, NS_MAXQ) : NS_MAXQ;
+  const size_t nsbytes = (size_t)w->ns_grid * w->ns_capq * 12 + 512;
+  const size_t bytes = nsbytes + sizeof(gbp_plan_status) + 16 * w->ntiles + 3 * (64 * b + 4 * b + 64 * b + 64 * b) +
                        1024 + m * (2 * 64 + 2 * 80 + 64 + 4 + 4) + b * (2 * 4 + 4 + 64 + 80 + 4 + 4) +
                        b * (4 + 4 + 64 + 80 + 4) + 2 * NN_MAX_CHUNKS * b * (16 + 16) + 64 * b + 512 +
-                       64 * 256 + (size_t)NS_MAXQ * NS_BLOCKS * 12 + 1024 +
+                       64 * 256 + 0 /* ns partials: below */ + 1024 +
                        2 * ((size_t)NSC_CAP * 8 + (size_t)NSC_UNITS * 12 + 32 * b + 1024);
   if (hipMalloc(&w->block, bytes) != hipSuccess) {
     delete w;
@@ -3176,8 +3192,8 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->nn_i = carve<int32_t>(p, 4 * NN_MAX_CHUNKS * b);  // k_nn_mfma: int4 per slot
   w->nn_d2 = carve<double>(p, 2 * NN_MAX_CHUNKS * b);
   w->nn_i2 = carve<int32_t>(p, 4 * NN_MAX_CHUNKS * b);
-  w->ns_d = carve<double>(p, (int64_t)NS_MAXQ * NS_BLOCKS);
-  w->ns_i = carve<int32_t>(p, (int64_t)NS_MAXQ * NS_BLOCKS);
+  w->ns_d = carve<double>(p, (int64_t)w->ns_grid * w->ns_capq);
+  w->ns_i = carve<int32_t>(p, (int64_t)w->ns_grid * w->ns_capq);
   w->ns_fin = carve<uint32_t>(p, 64);
   for (auto &sb : w->nsb) {
     const char *cenv = getenv("GBP_NSC_CAP");  // (a small list: the fallback's test)
