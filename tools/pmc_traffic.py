@@ -39,9 +39,15 @@ def main(d):
             acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, cs in acc.items():
         summary["counters"][k] = {c: sum(v) / len(v) for c, v in cs.items()}
-    val = [k for k in summary["counters"] if "k_validate" in k]
+    # the headline's launch: the k_validate variant with the longest average
+    # dispatch in the trace (the planner's own, if any ran, are shorter)
+    kv = sorted((n for n in summary["kernels"] if "k_validate" in n),
+                key=lambda n: -summary["kernels"][n]["avg_ns"])
+    val = [k for k in kv if k in summary["counters"]] or \
+        [k for k in summary["counters"] if "k_validate" in k]
     if val:
         c = summary["counters"][val[0]]
+        summary["validate_kernel"] = val[0]
         fetch = c.get("FETCH_SIZE")
         write = c.get("WRITE_SIZE")
         if fetch is not None and write is not None:
@@ -54,7 +60,8 @@ def main(d):
     with open(os.path.join(d, "summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     if "validate_hbm_bytes_per_launch" in summary:  # what bench.py reads (profiles/pmc_traffic.json)
-        k = [n for n in summary["kernels"] if "k_validate" in n]
+        k = [summary["validate_kernel"]] if summary.get("validate_kernel") in summary["kernels"] else \
+            [n for n in summary["kernels"] if "k_validate" in n]
         with open(os.path.join(d, "pmc_traffic.json"), "w") as f:
             json.dump({"terrain": os.environ.get("PMC_TERRAIN", "synth-rough-1024"),
                        "batch": int(os.environ.get("PMC_BATCH", "262144")),

@@ -13,7 +13,7 @@ OUT=gpurun_out/prof
 mkdir -p $OUT
 # --streams 1: every launch serial, so the per-dispatch durations are the
 # kernel's own (overlapped launches on several streams stretch each other)
-ARGS=${PROF_ARGS:---steps 20 --warmup 3 --cpu-seconds 0 --ttfs-runs 0 --streams 1 --lookup-micro 0 --config2 0 --fresh-batches 0}
+ARGS=${PROF_ARGS:---steps 20 --warmup 3 --cpu-seconds 0 --ttfs-runs 0 --streams 1 --lookup-micro 0 --config2 0 --fresh-batches 0 --config5-seconds 0}
 TAG=${PROF_TAG:-run}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o $TAG -- \
     python3 bench.py $ARGS > $OUT/trace_bench.log 2>&1 || { echo "trace pass failed rc=$?"; exit 1; }
