@@ -211,13 +211,13 @@ struct gbp_plan_ws {
   // stage 3, after stage 6, replay start / end, end), read back once complete
   bool timing = false;
   struct TimedHalf {
-    hipEvent_t ev[6] = {};
+    hipEvent_t ev[8] = {};  // + [6] after stage 6's connect actions, [7] after their pair checks
     bool pending = false, star = false;
     int32_t half = 0;
   };
   TimedHalf *tring = nullptr;  // [ntring] (a plain array: no template of a gbp type exported)
   size_t ntring = 0, tnext = 0;
-  double tsum[5] = {0, 0, 0, 0, 0};
+  double tsum[7] = {0, 0, 0, 0, 0, 0, 0};
   int64_t tcount = 0;
   int32_t *sshared = nullptr;  // [max_shared][2] the REACHED connections (a, b)
   void *star_block = nullptr;
@@ -2581,17 +2581,19 @@ void timing_collect(gbp_plan_ws *w, bool wait) {
     if (!h.pending) continue;
     if (wait) (void)hipEventSynchronize(h.ev[5]);
     if (hipEventQuery(h.ev[5]) != hipSuccess) continue;
-    float ms[5] = {0, 0, 0, 0, 0};
+    float ms[7] = {0, 0, 0, 0, 0, 0, 0};
     (void)hipEventElapsedTime(&ms[0], h.ev[0], h.ev[5]);
     (void)hipEventElapsedTime(&ms[1], h.ev[0], h.ev[1]);
     if (h.star) {
       (void)hipEventElapsedTime(&ms[2], h.ev[1], h.ev[2]);
       (void)hipEventElapsedTime(&ms[3], h.ev[3], h.ev[4]);
       (void)hipEventElapsedTime(&ms[4], h.ev[2], h.ev[5]);
+      (void)hipEventElapsedTime(&ms[5], h.ev[1], h.ev[6]);
+      (void)hipEventElapsedTime(&ms[6], h.ev[6], h.ev[7]);
     } else {
       (void)hipEventElapsedTime(&ms[4], h.ev[1], h.ev[5]);
     }
-    for (int k = 0; k < 5; k++) w->tsum[k] += 1e3 * (double)ms[k];
+    for (int k = 0; k < 7; k++) w->tsum[k] += 1e3 * (double)ms[k];
     w->tcount++;
     h.pending = false;
   }
@@ -2703,9 +2705,11 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     const int64_t rmax = 2 * w->star_max_pairs;
     hipLaunchKernelGGL(k_star_prep, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, T->v,
                        direction, S.snb, S.sown, S.srowof, S.sritem, S.srs, S.sra, ++w->seq);
+    if (th) HIPCHK_P(hipEventRecord(th->ev[6], s));
     int rc = gbp_internal_validate_dev_n(t, rmax, &st->star_vrows, S.srs, S.sra, nullptr, direction,
                                          adaptive, nullptr, nullptr, nullptr, S.srf, nullptr, s);
     if (rc) return rc;
+    if (th) HIPCHK_P(hipEventRecord(th->ev[7], s));
     hipLaunchKernelGGL(k_star_gate, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, S.srf,
                        half, ++w->seq);
     if (th) HIPCHK_P(hipEventRecord(th->ev[2], s));
@@ -3335,7 +3339,7 @@ int gbp_plan_stage_times(gbp_plan_ws *w, double *us, int n, int64_t *halves, int
   if (!us || n < 5) return GBP_E_INVALID_ARG;
   Guard g(w->device);
   timing_collect(w, false);
-  for (int k = 0; k < 5; k++) us[k] = w->tsum[k];
+  for (int k = 0; k < std::min(n, 7); k++) us[k] = w->tsum[k];
   if (halves) *halves = w->tcount;
   if (reset) {
     for (double &x : w->tsum) x = 0;

@@ -1709,10 +1709,10 @@ bool RRTConnectClass::buildRRTConnectDevice(FastTerrainMap &terrain, State s_sta
                                   : std::chrono::duration<double>(since());
   extend_counter_ = ps.ext_counter;
   if (st.stage_timing) {
-    double us[5];
+    double us[7];
     int64_t nh = 0;
-    chk(gbp_plan_stage_times(D.ws, us, 5, &nh, 1), "stage times");
-    for (int k = 0; k < 5; k++) st.stage_us[k] += us[k];
+    chk(gbp_plan_stage_times(D.ws, us, 7, &nh, 1), "stage times");
+    for (int k = 0; k < 7; k++) st.stage_us[k] += us[k];
     st.stage_halves += nh;
   }
   const int32_t halves_run = (goal_found ? ps.meet_half + 1 : half) - half0;
@@ -2297,10 +2297,10 @@ bool RRTStarConnectClass::buildRRTStarConnectDevice(FastTerrainMap &terrain, Sta
   extend_counter_ = ps.ext_counter;
   rewires_ = ps.stat_rewires;
   if (st.stage_timing) {
-    double us[5];
+    double us[7];
     int64_t nh = 0;
-    chk(gbp_plan_stage_times(D.ws, us, 5, &nh, 1), "stage times");
-    for (int k = 0; k < 5; k++) st.stage_us[k] += us[k];
+    chk(gbp_plan_stage_times(D.ws, us, 7, &nh, 1), "stage times");
+    for (int k = 0; k < 7; k++) st.stage_us[k] += us[k];
     st.stage_halves += nh;
   }
   st.halves += half - half0;
@@ -2365,7 +2365,7 @@ bool RRTStarConnectClass::buildRRTStarConnectDevice(FastTerrainMap &terrain, Sta
 // ============================================================================
 // the layout planner.py's PlanParams mirrors (tests/test_abi.py)
 static_assert(sizeof(gbp_plan_params) == 464, "gbp_plan_params layout");
-static_assert(sizeof(gbp_plan_result) == 360, "gbp_plan_result layout");
+static_assert(sizeof(gbp_plan_result) == 376, "gbp_plan_result layout");
 
 extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r,
                                     double *path_states, double *path_actions, int capacity) {
@@ -2447,7 +2447,7 @@ extern "C" int gbp_plan_rrt_connect(const gbp_plan_params *p, gbp_plan_result *r
     r->vertices_b = st.vertices_b;
     r->n_states = found ? (int)states.size() : 0;
     r->rewires = st.rewires;
-    for (int k = 0; k < 5; k++) r->stage_us[k] = st.stage_us[k];
+    for (int k = 0; k < 7; k++) r->stage_us[k] = st.stage_us[k];
     r->stage_halves = st.stage_halves;
     r->solutions = st.solutions;
     for (int k = 0; k < 4; k++) {

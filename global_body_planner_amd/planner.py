@@ -55,7 +55,7 @@ class PlanResult(ctypes.Structure):
                 ("reported_length", _D), ("reported_yaw", _D), ("meet_a", ctypes.c_int32),
                 ("meet_b", ctypes.c_int32), ("halves", ctypes.c_int64),
                 ("polls", ctypes.c_int64), ("stopped_by_peer", ctypes.c_int32),
-                ("stage_us", _D * 5), ("stage_halves", ctypes.c_int64)]
+                ("stage_us", _D * 7), ("stage_halves", ctypes.c_int64)]
 
 
 _planner = None

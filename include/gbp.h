@@ -564,7 +564,9 @@ int gbp_plan_star_config(gbp_plan_ws *ws, int enable, double delta, int64_t max_
  *         append), us[2] stage 6 (RRT*: neighbourhoods, connect checks and
  *         their pair checks), us[3] stage 7 on the replay's stream (RRT*:
  *         replay, plus the best connection's ranking after Tb's halves),
- *   us[4] stages 4-5 (the connects' search, attemptConnect, append)
+ *   us[4] stages 4-5 (the connects' search, attemptConnect, append),
+ *   with n >= 7 also us[5] stage 6 up to its pair checks (neighbourhoods,
+ *   connect actions) and us[6] those pair checks,
  * and *halves the number of halves summed (n >= 5; reset clears).  A half's
  * events are read once the caller has synchronised its stream (status read). */
 int gbp_plan_stage_timing(gbp_plan_ws *ws, int enable);

@@ -430,7 +430,7 @@ struct BatchStats {
   // diagnostics (device loop): time each half-iteration's stage groups
   // (gbp_plan_stage_timing) into stage_us (half, stages 0-3, 6, 7, 4-5)
   bool stage_timing = false;
-  double stage_us[5] = {0, 0, 0, 0, 0};
+  double stage_us[7] = {0, 0, 0, 0, 0, 0, 0};
   int64_t stage_halves = 0;
 };
 
@@ -704,8 +704,9 @@ typedef struct {
   int64_t halves;              // half-iterations run
   int64_t polls;               // algorithm 3 with stop_poll: polls made
   int32_t stopped_by_peer;     // ... and 1 if another rank's solution ended this search
-  double stage_us[5];          // with stage_timing: summed per-half microseconds
-                               // (gbp_plan_stage_times: half, stages 0-3, 6, 7, 4-5)
+  double stage_us[7];          // with stage_timing: summed per-half microseconds
+                               // (gbp_plan_stage_times: half, stages 0-3, 6, 7, 4-5,
+                               // stage 6 before / in its pair checks)
   int64_t stage_halves;        //   over this many timed halves
 } gbp_plan_result;
 

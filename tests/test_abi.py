@@ -112,8 +112,8 @@ def test_planner_library_exports_and_fails_without_device():
     # init_parent (4 x 2 x 8), first_half, extend_base (8 + 8), stage_timing (4 + 4 padding)
     assert ctypes.sizeof(planner.PlanParams) == (4 * 3 + 4 + 8 * 6 + 8 * 16 + 8 + 8 + 8 + 8 + 8 +
                                                  32 + 8 + 8 + 8 + 8 + 64 + 16 + 64 + 16 + 8)
-    # ... + stage_us[5], stage_halves (40 + 8)
-    assert ctypes.sizeof(planner.PlanResult) == 312 + 48
+    # ... + stage_us[7], stage_halves (56 + 8)
+    assert ctypes.sizeof(planner.PlanResult) == 312 + 64
     from global_body_planner_amd import engine
     assert ctypes.sizeof(engine.PlanStatus) == 216   # gbp_plan_status (static_assert in gbp_plan.hip)
     assert ctypes.sizeof(L.Sampling) == 32
