@@ -183,6 +183,7 @@ struct gbp_plan_ws {
   double star_delta = 3.0;     // rrt_star_connect.h:59
   int64_t star_max_pairs = 0, star_max_shared = 0;
   int64_t star_items = 0;      // scan items per half (new vertex x position chunk)
+  int star_check_wave = 1;     // stage 6e: k_star_check (0: the persistent validate kernel, A/B)
   // a half's insertion buffers, one set per tree (half & 1): half h's replay
   // runs on star_stream beside half h's connects and half h + 1, which fills
   // the other set; half h + 2 refills this one only after the replay (its
@@ -1531,6 +1532,8 @@ __device__ bool wave_pair_check(const TerrainView<ZT> &T, const double *s_in, co
       ok = is_valid_state<ZT, CM>(T, sc, stage_phase(stg), acc);
     }
     const unsigned long long okm = __ballot(ok), hasm = __ballot(has);
+#ifdef GBP_SEQ_REPLAY
+    // A/B arm: the samples replayed one at a time
     for (int j = 0; j < WAVE; j++) {
       if (!((hasm >> j) & 1ull)) break;
       const uint32_t fj = __shfl(acc.flags, j), gj = __shfl(acc.G, j);
@@ -1545,6 +1548,70 @@ __device__ bool wave_pair_check(const TerrainView<ZT> &T, const double *s_in, co
       decided = transition<ADAPTIVE>(L, okj);
       if (decided || !okj) break;
     }
+#else
+    // The replay in parallel.  hasm is a prefix of the lanes (a lane past a
+    // deciding sample has none); the run [0, j0) of passing samples ends at
+    // the first failing or LIMIT one.  Each lane of the run applies its own
+    // sample's success transition to its speculated pre-state (stg, t, ts:
+    // the same arithmetic the in-order replay performs), so the attempt's
+    // state after the run is the last run lane's; s_new / t_new are the last
+    // ones a run lane set; G, flags and V add up over the run.  Then the
+    // stop lane's sample, if any, goes through the in-order transition.
+    const unsigned long long limm = __ballot(has && (acc.flags & GBP_F_LIMIT));
+    const unsigned long long stopm = hasm & (~okm | limm);
+    const int j0 = stopm ? __builtin_ctzll(stopm) : __popcll(hasm);
+    const bool inrun = lane < j0;
+    Lane P = L;
+    P.stage = stg;
+    P.t = t;
+    P.ts = ts;
+    P.f = stage_bits((uint32_t)stg);
+    P.snew_kind = SN_NONE;
+    P.tnew_set = 0;
+    bool dec = false;
+    if (inrun) dec = transition<ADAPTIVE>(P, true);
+    uint32_t g = inrun ? acc.G : 0u, fl = inrun ? acc.flags : 0u;
+#pragma unroll
+    for (int o = WAVE / 2; o > 0; o >>= 1) {
+      g += __shfl_xor(g, o);
+      fl |= __shfl_xor(fl, o);
+    }
+    L.acc.G += g;
+    L.acc.flags |= fl;
+    L.acc.V += (uint32_t)j0;
+    if (j0 > 0) {
+      const int jl = j0 - 1;
+      L.stage = __shfl(P.stage, jl);
+      L.t = __shfl(P.t, jl);
+      L.ts = __shfl(P.ts, jl);
+      L.tpre = __shfl(P.tpre, jl);
+      L.f = __shfl(P.f, jl);
+      decided = __shfl((int)dec, jl) != 0;
+      const unsigned long long sm = __ballot(inrun && P.snew_kind != SN_NONE);
+      if (sm) {
+        const int js = 63 - __builtin_clzll(sm);
+        L.snew_kind = __shfl(P.snew_kind, js);
+        L.snew_p = __shfl(P.snew_p, js);
+      }
+      const unsigned long long tm = __ballot(inrun && P.tnew_set);
+      if (tm) {
+        const int jt = 63 - __builtin_clzll(tm);
+        L.tnew = __shfl(P.tnew, jt);
+        L.tnew_set = 1;
+      }
+    }
+    if (!decided && stopm) {
+      const uint32_t fj = __shfl(acc.flags, j0), gj = __shfl(acc.G, j0);
+      L.acc.G += gj;
+      L.acc.flags |= fj;
+      if (fj & GBP_F_LIMIT) {
+        decided = true;
+      } else {
+        L.acc.V += 1;
+        decided = transition<ADAPTIVE>(L, ((okm >> j0) & 1ull) != 0);
+      }
+    }
+#endif
   }
   uint32_t f = L.f | L.acc.flags;
   if (L.snew_kind != SN_NONE) {
@@ -1879,6 +1946,30 @@ __global__ __launch_bounds__(TB) void k_star_prep(gbp_plan_status *st, const dou
         rowof[c] = -1;
       }
     }
+  }
+}
+
+// stage 6e: the rows' pair checks, one wave per row (wave_pair_check, as
+// k_connect: its 64 lanes evaluate 64 successive samples of the row's
+// action, then replay them in order).  These rows are few (hundreds per
+// half) and long (connect actions, tens of samples): the persistent
+// validate kernel's fixed cost is ~90 us for them, this one's a few steps
+// of one wave per row.  Flags as gbp_validate's (no s_new / t_new kept).
+template <class ZT, bool ADAPTIVE, int CM>
+__global__ __launch_bounds__(TB) void k_star_check(TerrainView<ZT> T, gbp_plan_status *st, int dir,
+                                                   const double *__restrict__ rs,
+                                                   const double *__restrict__ ra,
+                                                   uint32_t *__restrict__ rf, uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t n = st->star_vrows;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+  const int64_t nw = (int64_t)gridDim.x * blockDim.x / WAVE;
+  for (int64_t r = wv; r < n; r += nw) {
+    double sn[8], tn = 0;
+    uint32_t f = 0;
+    wave_pair_check<ZT, ADAPTIVE, CM>(T, rs + 8 * r, ra + 10 * r, dir, sn, tn, f);
+    if (lane == 0) rf[r] = f;
   }
 }
 
@@ -2706,9 +2797,24 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     hipLaunchKernelGGL(k_star_prep, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, T->v,
                        direction, S.snb, S.sown, S.srowof, S.sritem, S.srs, S.sra, ++w->seq);
     if (th) HIPCHK_P(hipEventRecord(th->ev[6], s));
-    int rc = gbp_internal_validate_dev_n(t, rmax, &st->star_vrows, S.srs, S.sra, nullptr, direction,
-                                         adaptive, nullptr, nullptr, nullptr, S.srf, nullptr, s);
-    if (rc) return rc;
+    if (w->star_check_wave) {
+      const int cm = (t->opt_affine && t->affine) ? 2 : 0;
+      const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * 8, (rmax + 3) / 4));
+      const uint64_t cseq = ++w->seq;
+#define GBP_SC(AD, CM)                                                                        \
+  hipLaunchKernelGGL((k_star_check<ZT, AD, CM>), dim3(g), dim3(TB), 0, s, V, st, direction, S.srs, \
+                     S.sra, S.srf, cseq)
+      if (adaptive) {
+        if (cm == 2) GBP_SC(true, 2); else GBP_SC(true, 0);
+      } else {
+        if (cm == 2) GBP_SC(false, 2); else GBP_SC(false, 0);
+      }
+#undef GBP_SC
+    } else {
+      int rc = gbp_internal_validate_dev_n(t, rmax, &st->star_vrows, S.srs, S.sra, nullptr, direction,
+                                           adaptive, nullptr, nullptr, nullptr, S.srf, nullptr, s);
+      if (rc) return rc;
+    }
     if (th) HIPCHK_P(hipEventRecord(th->ev[7], s));
     hipLaunchKernelGGL(k_star_gate, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, S.srf,
                        half, ++w->seq);
@@ -3199,6 +3305,10 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->ns_d = carve<double>(p, (int64_t)w->ns_grid * w->ns_capq);
   w->ns_i = carve<int32_t>(p, (int64_t)w->ns_grid * w->ns_capq);
   w->ns_fin = carve<uint32_t>(p, 64);
+  {
+    const char *e = getenv("GBP_STAR_CHECK");  // "persistent": the A/B's other arm
+    w->star_check_wave = (e && !strcmp(e, "persistent")) ? 0 : 1;
+  }
   for (auto &sb : w->nsb) {
     const char *cenv = getenv("GBP_NSC_CAP");  // (a small list: the fallback's test)
     sb.cap = (uint32_t)std::max(1, std::min(NSC_CAP, cenv && *cenv ? atoi(cenv) : NSC_CAP));
