@@ -183,23 +183,22 @@ struct gbp_plan_ws {
   double star_delta = 3.0;     // rrt_star_connect.h:59
   int64_t star_max_pairs = 0, star_max_shared = 0;
   int64_t star_items = 0;      // scan items per half (new vertex x position chunk)
-  int star_check_wave = 1;     // stage 6e: k_star_check (0: the persistent validate kernel, A/B)
   // a half's insertion buffers, one set per tree (half & 1): half h's replay
   // runs on star_stream beside half h's connects and half h + 1, which fills
   // the other set; half h + 2 refills this one only after the replay (its
   // stage 5 waits for it first)
   struct StarSet {
-    int32_t *scnt = nullptr;     // [star_items] neighbours per scan item (k_star_count)
+    unsigned long long *scnt = nullptr;  // [star_items] neighbours per scan item (k_star_count: tile_word)
     int32_t *sioff = nullptr;    // [star_items] the items' offsets
     int32_t *soff = nullptr;     // [bmax + 1] each new vertex's first pair
     int32_t *snb = nullptr;      // [max_pairs] the neighbour of each pair
     int32_t *sown = nullptr;     // [max_pairs] its new vertex (k)
     int32_t *srowof = nullptr;   // [2 max_pairs] connect check -> pair-check row (-1: none)
-    int32_t *sritem = nullptr;   // [2 max_pairs] row -> connect check
     double *srs = nullptr;       // [2 max_pairs][8] rows: the pair checks' states
     double *sra = nullptr;       // [2 max_pairs][10] and actions
     uint32_t *srf = nullptr;     // [2 max_pairs] their flags
-    int64_t *meta = nullptr;     // [4] n_added, added_base, pairs (k_star_scan); shared count (k_star_shared)
+    int64_t *meta = nullptr;     // [4] n_added, added_base, pairs (k_star_count's scan); shared count (k_star_shared)
+    uint32_t *sfin = nullptr;    // [64] k_star_count's finished-workgroup count (zeroed, self-resetting)
   } ss[2];
   int32_t *kvtx = nullptr;     // [bmax] O's vertex of each connection (-1: none)
   // the replay (and the best connection's ranking) off the caller's stream:
@@ -562,6 +561,56 @@ __device__ __forceinline__ void nh_sweep(const _Float16 *__restrict__ vh, int c0
   // full units, the next unit's rows in flight while one is scored; a
   // scheduling barrier per tile keeps one tile's accumulators live at a time
   const int uf = min(c1, nv >> 5) & ~1;  // chunks [c0, uf) form full units
+#ifndef GBP_NN_SERIAL
+  // Full units, software-pipelined over two accumulators: a chunk's scores
+  // (two MFMAs) are reduced while the next chunk's MFMAs run, so the wave's
+  // VALU minimum and top-3 insert overlap its own matrix work instead of
+  // waiting for it (the serial form, -DGBP_NN_SERIAL, scores a tile's two
+  // chunks and then reduces them).  Job order: (tile 0, chunk c), (tile 0,
+  // c + 1), (tile 1, c), ... then the next unit's (tile 0, c + 2) from the
+  // rows loaded a unit ahead.
+  if (c0 < uf) {
+    auto score = [&](const nh8 (&a)[4], int k, int u) {
+      nhacc acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * k], b1[u], nhacc{}, 0, 0, 0);
+      return __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * k + 1], b2[u], acc, 0, 0, 0);
+    };
+    // one unit's tiles; NEXT: the last tile's slots score the next unit's
+    // first jobs (a branch-free body, so that the scheduling barriers hold
+    // the order)
+    auto unit = [&](const nh8 (&a)[4], const nh8 (&p)[4], int c, nhacc &X, nhacc &Y, auto next_tag) {
+      constexpr bool NEXT = decltype(next_tag)::value;
+#pragma unroll
+      for (int u = 0; u < NT; u++) {
+        float m = nh_min16(X);
+        __builtin_amdgcn_sched_barrier(0);
+        if (u + 1 < NT)
+          X = score(a, 0, u + 1);
+        else if (NEXT)
+          X = score(p, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        m = nh_min2(m, nh_min16(Y));
+        t[u].insert(m, c >> 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (u + 1 < NT)
+          Y = score(a, 1, u + 1);
+        else if (NEXT)
+          Y = score(p, 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    nh8 a[4], p[4];
+    load(c0, a);
+    nhacc X = score(a, 0, 0), Y = score(a, 1, 0);
+    int c = c0;
+    for (; c + 2 < uf; c += 2) {
+      load(c + 2, p);
+      unit(a, p, c, X, Y, std::true_type{});
+#pragma unroll
+      for (int k = 0; k < 4; k++) a[k] = p[k];
+    }
+    unit(a, a, c, X, Y, std::false_type{});
+  }
+#else
   if (c0 < uf) {
     nh8 a[4], p[4];
     load(c0, a);
@@ -576,6 +625,7 @@ __device__ __forceinline__ void nh_sweep(const _Float16 *__restrict__ vh, int c0
       for (int k = 0; k < 4; k++) a[k] = p[k];
     }
   }
+#endif
   if (uf < c1) {  // the last unit: a lone chunk and/or rows past the tree's end
     nh8 a[4];
     load(uf, a);  // the row arrays hold whole units
@@ -632,8 +682,15 @@ struct NhPrep {
   const int32_t *nt;
 };
 
+// three waves per SIMD (168 VGPRs): the pipelined sweep's two live
+// accumulators would otherwise take it to 189 and two waves; the few values
+// it spills around the sweep cost less (planner 5-s runs 181.4 vs 177.8 M
+// extends/s, the serial sweep 179.5; profiles/r06i_nn_pipe_ab.txt)
+#ifndef GBP_NN_WPE
+#define GBP_NN_WPE __attribute__((amdgpu_waves_per_eu(3)))
+#endif
 template <int NT, class ZT, bool PREP>
-__global__ __launch_bounds__(NH_TB) void k_nn_mfma(gbp_plan_status *__restrict__ st,
+__global__ __launch_bounds__(NH_TB) GBP_NN_WPE void k_nn_mfma(gbp_plan_status *__restrict__ st,
                                                    const int32_t *__restrict__ nq_dev,
                                                    const double *__restrict__ q,
                                                    const int32_t *__restrict__ q_off_dev,
@@ -1751,48 +1808,35 @@ __device__ __forceinline__ void star_chunking(int64_t n_added, int64_t base, int
   }
 }
 
-// stage 6a: hits per item
-__global__ __launch_bounds__(TB) void k_star_count(gbp_plan_status *st, const double *__restrict__ tv,
-                                                   double delta, int32_t *__restrict__ cnt,
-                                                   int64_t cap_items, uint64_t seq) {
-  if (gated(st, seq)) return;
-  const int64_t n = st->n_added, base = st->added_base;
-  int64_t ch, nch;
-  star_chunking(n, base, cap_items, ch, nch);
-  __shared__ int sh[TB / WAVE];
-  for (int64_t it = blockIdx.x; it < n * nch; it += gridDim.x) {
-    const int64_t k = it / nch, c = it - k * nch;
-    const int64_t nk = base + k + 1;  // the map holds keys 0..base+k (rrt_star_connect.cpp:22)
-    const int m = um_epoch(nk);
-    double q[8];
-    copy8(q, tv + 8 * (base + k));
-    const int64_t p1 = min<int64_t>((c + 1) * ch, nk);
-    int hits = 0;
-    for (int64_t p = c * ch + threadIdx.x; p < p1; p += TB) {
-      const int64_t j = um_key_at(p, nk, m);
-      const double d = state_distance(q, tv + 8 * j);  // planner_class.cpp:178
-      hits += (d <= delta && d > 0) ? 1 : 0;
+// stage 6a: hits per item; the grid's last workgroup to finish then scans
+// them (star_scan_items: the items' offsets, k-major, and each vertex's
+// first pair) — one launch, not a count and a one-workgroup scan
+// an item's count, published by its workgroup as tile_word(epoch, 1, hits)
+// with one agent-scope exchange (no fence: the word carries its own epoch)
+__device__ __forceinline__ int64_t star_item_count(gbp_plan_status *st, unsigned long long *cnt,
+                                                   int64_t i, uint32_t ep) {
+  uint32_t spins = 0;
+  for (;;) {
+    const unsigned long long x =
+        __hip_atomic_fetch_add(&cnt[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)(x >> 32) == ep) return (int64_t)(x & 0x3FFFFFFFu);
+    if (++spins > LOOKBACK_SPIN_LIMIT) {  // bounded: report, never hang
+      atomicOr(&st->error, 1u);
+      return 0;
     }
-    hits = block_sum_tb(hits, sh);
-    if (threadIdx.x == 0) cnt[it] = hits;
+    __builtin_amdgcn_s_sleep(2);
   }
 }
 
-// stage 6b: the items' offsets (exclusive scan, k-major) and each vertex's
-// first pair, one workgroup
-__global__ __launch_bounds__(RB) void k_star_scan(gbp_plan_status *st, const int32_t *__restrict__ cnt,
-                                                  int32_t *__restrict__ ioff, int32_t *__restrict__ off,
-                                                  int64_t *__restrict__ meta, int64_t max_pairs,
-                                                  int64_t cap_items, int32_t half, uint64_t seq) {
-  if (gated(st, seq)) return;
-  const int64_t n = st->n_added, base = st->added_base;
-  int64_t ch, nch;
-  star_chunking(n, base, cap_items, ch, nch);
-  const int64_t N = n * nch;
-  const int64_t per = (N + RB - 1) / RB;
+__device__ void star_scan_items(gbp_plan_status *st, unsigned long long *cnt, uint32_t ep, int64_t N,
+                                int64_t nch, int64_t n, int64_t base, int32_t *__restrict__ ioff,
+                                int32_t *__restrict__ off, int64_t *__restrict__ meta,
+                                int64_t max_pairs, uint64_t seq) {
+  const int nt = (int)blockDim.x;
+  const int64_t per = (N + nt - 1) / nt;
   const int64_t lo = min<int64_t>(N, threadIdx.x * per), hi = min<int64_t>(N, lo + per);
   int64_t sum = 0;
-  for (int64_t i = lo; i < hi; i++) sum += cnt[i];
+  for (int64_t i = lo; i < hi; i++) sum += star_item_count(st, cnt, i, ep);
   // block-wide exclusive scan of the threads' sums: waves, then the wave totals
   const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
   int64_t inc = sum;
@@ -1805,7 +1849,7 @@ __global__ __launch_bounds__(RB) void k_star_scan(gbp_plan_status *st, const int
   __syncthreads();
   if (threadIdx.x == 0) {
     int64_t run = 0;
-    for (int i = 0; i < RB / WAVE; i++) {
+    for (int i = 0; i < nt / WAVE; i++) {
       const int64_t v = wt[i];
       wt[i] = run;
       run += v;
@@ -1819,7 +1863,7 @@ __global__ __launch_bounds__(RB) void k_star_scan(gbp_plan_status *st, const int
     const int32_t o = (int32_t)min<int64_t>(run, 0x7FFFFFFF);
     ioff[i] = o;
     if (i % nch == 0) off[i / nch] = o;  // vertex i / nch starts here
-    run += cnt[i];
+    run += star_item_count(st, cnt, i, ep);
   }
   if (threadIdx.x == 0) {
     off[n] = (int32_t)min<int64_t>(total, 0x7FFFFFFF);
@@ -1828,14 +1872,57 @@ __global__ __launch_bounds__(RB) void k_star_scan(gbp_plan_status *st, const int
     meta[0] = n;
     meta[1] = base;
     meta[2] = min<int64_t>(total, 0x7FFFFFFF);
-    st->star_rows = 0;
-    st->star_vrows = 0;
+    st->star_rows = (int32_t)min<int64_t>(2 * total, 0x7FFFFFFF);  // rows = checks (k_star_check)
+    st->star_vrows = st->star_rows;
     st->stat_star_connects += 2 * total;  // a choose-parent and a rewire connect per pair
     if (total > max_pairs) {
       atomicOr(&st->error, 4u);
       raise_gate(st, seq);
     }
   }
+}
+
+__global__ __launch_bounds__(TB) void k_star_count(gbp_plan_status *st, const double *__restrict__ tv,
+                                                   double delta, unsigned long long *cnt,
+                                                   int32_t *__restrict__ ioff, int32_t *__restrict__ off,
+                                                   int64_t *__restrict__ meta, int64_t max_pairs,
+                                                   uint32_t *__restrict__ fin, int64_t cap_items,
+                                                   uint64_t seq) {
+  if (gated(st, seq)) return;
+  const int64_t n = st->n_added, base = st->added_base;
+  int64_t ch, nch;
+  star_chunking(n, base, cap_items, ch, nch);
+  // the workgroups with an item take part in the finish count (the grid is
+  // sized for the largest half; most of it exits here); with no items
+  // workgroup 0 alone scans (an empty list still resets the half's counts)
+  const int64_t N = n * nch, parts = max<int64_t>(1, min<int64_t>(gridDim.x, N));
+  const uint32_t ep = (uint32_t)seq;  // this launch's epoch (seq grows every launch)
+  if ((int64_t)blockIdx.x >= parts) return;
+  __shared__ int sh[TB / WAVE];
+  __shared__ bool last;
+  for (int64_t it = blockIdx.x; it < N; it += gridDim.x) {
+    const int64_t k = it / nch, c = it - k * nch;
+    const int64_t nk = base + k + 1;  // the map holds keys 0..base+k (rrt_star_connect.cpp:22)
+    const int m = um_epoch(nk);
+    double q[8];
+    copy8(q, tv + 8 * (base + k));
+    const int64_t p1 = min<int64_t>((c + 1) * ch, nk);
+    int hits = 0;
+    for (int64_t p = c * ch + threadIdx.x; p < p1; p += TB) {
+      const int64_t j = um_key_at(p, nk, m);
+      const double d = state_distance(q, tv + 8 * j);  // planner_class.cpp:178
+      hits += (d <= delta && d > 0) ? 1 : 0;
+    }
+    hits = block_sum_tb(hits, sh);
+    if (threadIdx.x == 0)
+      __hip_atomic_exchange(&cnt[it], tile_word(ep, 1, (uint32_t)hits), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) last = atomicAdd(fin, 1u) == (uint32_t)(parts - 1);
+  __syncthreads();
+  if (!last) return;
+  star_scan_items(st, cnt, ep, N, nch, n, base, ioff, off, meta, max_pairs, seq);
+  if (threadIdx.x == 0) *fin = 0;  // reset for the next half (stream-ordered)
 }
 
 // stage 6c: the neighbour lists, each item's hits in position order at its offset
@@ -1885,111 +1972,77 @@ __global__ __launch_bounds__(TB) void k_star_fill(gbp_plan_status *st, const dou
   }
 }
 
-// stage 6d: the connect checks' actions (rrt_connect.cpp:20-70 at depth 0,
-// item 2p: choose-parent attemptConnect(s_near, s_new, poseDistance(s_new,
-// s_near) / V_NOM), 2p + 1: rewire attemptConnect(s_new, s_near, ...)); the
-// ones with a valid action become pair-check rows (rowof; the rest are not
-// REACHED: t_s <= KINEMATICS_RES or an invalid action, :23-24, :66)
-__global__ __launch_bounds__(TB) void k_star_prep(gbp_plan_status *st, const double *__restrict__ tv,
-                                                  int dir, const int32_t *__restrict__ nb,
-                                                  const int32_t *__restrict__ own,
-                                                  int32_t *__restrict__ rowof,
-                                                  int32_t *__restrict__ ritem, double *__restrict__ rs,
-                                                  double *__restrict__ ra, uint64_t seq) {
-  // the pair-check launch after this one is the engine's, not gated: when
-  // this half is, it must find no rows (it would re-validate the halted
-  // half's rows in the next half's direction over their flags)
-  if (gated(st, seq)) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->star_vrows = 0;
-    return;
-  }
-  const int64_t m = 2 * (int64_t)st->star_pairs, base = st->added_base;
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  // whole waves iterate together (the row slots are taken one atomic per wave)
-  for (int64_t c0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~(WAVE - 1)); c0 < m;
-       c0 += stride) {
-    const int64_t c = c0 + lane;
-    bool row = false;
-    double a[10], sp[8];
-    if (c < m) {
-      const int64_t pr = c >> 1;
-      const int64_t idx = base + own[pr], j = nb[pr];
-      double sn[8], sj[8];
-      copy8(sn, tv + 8 * idx);
-      copy8(sj, tv + 8 * j);
-      const bool rewire = c & 1;
-      const double *se = rewire ? sn : sj, *sq = rewire ? sj : sn;  // (s_existing, s)
-      const double t_s = (rewire ? pose_distance(sj, sn) : pose_distance(sn, sj)) / V_NOM;
-      if (t_s > KINEMATICS_RES) {
-        const double *s_start = dir == GBP_FORWARD ? se : sq, *s_goal = dir == GBP_FORWARD ? sq : se;
-        connect_action(s_start, s_goal, t_s, a);
-        row = is_valid_action(a);
-        copy8(sp, dir == GBP_FORWARD ? s_start : s_goal);
-      }
-    }
-    const unsigned long long bm = __ballot(row);
-    int32_t first = 0;
-    if (lane == 0 && bm) {
-      first = atomicAdd(&st->star_rows, __popcll(bm));
-      atomicAdd(&st->star_vrows, __popcll(bm));
-    }
-    first = __shfl(first, 0);
-    if (c < m) {
-      if (row) {
-        const int32_t pos = first + __popcll(bm & ((1ull << lane) - 1ull));
-        copy8(rs + 8 * (int64_t)pos, sp);
-        copy10(ra + 10 * (int64_t)pos, a);
-        ritem[pos] = (int32_t)c;
-        rowof[c] = pos;
-      } else {
-        rowof[c] = -1;
-      }
-    }
-  }
+// stage 6d's connect check c of the half's pairs (rrt_connect.cpp:20-70 at
+// depth 0; pair c >> 1 = (new vertex idx, neighbour j); c even: choose-parent
+// attemptConnect(s_near, s_new, poseDistance(s_new, s_near) / V_NOM), odd:
+// rewire attemptConnect(s_new, s_near, ...)): whether it needs a pair check
+// (the rest are not REACHED: t_s <= KINEMATICS_RES or an invalid action,
+// :23-24, :66), its action a and the state sp the check starts from
+__device__ __forceinline__ bool star_row(const double *__restrict__ tv, int dir, int64_t idx,
+                                         int64_t j, bool rewire, double (&a)[10], double (&sp)[8]) {
+  double sn[8], sj[8];
+  copy8(sn, tv + 8 * idx);
+  copy8(sj, tv + 8 * j);
+  const double *se = rewire ? sn : sj, *sq = rewire ? sj : sn;  // (s_existing, s)
+  const double t_s = (rewire ? pose_distance(sj, sn) : pose_distance(sn, sj)) / V_NOM;
+  if (!(t_s > KINEMATICS_RES)) return false;
+  const double *s_start = dir == GBP_FORWARD ? se : sq, *s_goal = dir == GBP_FORWARD ? sq : se;
+  connect_action(s_start, s_goal, t_s, a);
+  copy8(sp, dir == GBP_FORWARD ? s_start : s_goal);
+  return is_valid_action(a);
 }
 
-// stage 6e: the rows' pair checks, one wave per row (wave_pair_check, as
-// k_connect: its 64 lanes evaluate 64 successive samples of the row's
-// action, then replay them in order).  These rows are few (hundreds per
-// half) and long (connect actions, tens of samples): the persistent
-// validate kernel's fixed cost is ~90 us for them, this one's a few steps
-// of one wave per row.  Flags as gbp_validate's (no s_new / t_new kept).
+// stage 6e: the connect checks, one wave per check c: its action
+// (star_row, every lane alike) and, when it has one, its pair check
+// (wave_pair_check, as k_connect: the 64 lanes evaluate 64 successive
+// samples of the action, then replay them in order).  The checks are few
+// (hundreds per half) and their actions long (connect actions, tens of
+// samples): the persistent validate kernel's fixed cost was ~90 us for them
+// (63 us per half in the planner), this one's a few steps of one wave per
+// check.  Rows are the checks themselves (row c: rs / ra / rf[c], rowof[c]
+// = c or -1; rf[c] = 0 for a check with no pair check); flags as
+// gbp_validate's (no s_new / t_new kept).  A FRAGILE decision halts the
+// sequence (the host re-decides it with glibc and resumes at stage 7).
 template <class ZT, bool ADAPTIVE, int CM>
 __global__ __launch_bounds__(TB) void k_star_check(TerrainView<ZT> T, gbp_plan_status *st, int dir,
-                                                   const double *__restrict__ rs,
-                                                   const double *__restrict__ ra,
-                                                   uint32_t *__restrict__ rf, uint64_t seq) {
+                                                   const double *__restrict__ tv,
+                                                   const int32_t *__restrict__ nb,
+                                                   const int32_t *__restrict__ own,
+                                                   int32_t *__restrict__ rowof, double *__restrict__ rs,
+                                                   double *__restrict__ ra, uint32_t *__restrict__ rf,
+                                                   int32_t half, uint64_t seq) {
   if (gated(st, seq)) return;
-  const int64_t n = st->star_vrows;
+  const int64_t m = 2 * (int64_t)st->star_pairs, base = st->added_base;
   const int lane = threadIdx.x & (WAVE - 1);
   const int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
   const int64_t nw = (int64_t)gridDim.x * blockDim.x / WAVE;
-  for (int64_t r = wv; r < n; r += nw) {
-    double sn[8], tn = 0;
+  uint32_t rows = 0;
+  for (int64_t c = wv; c < m; c += nw) {
+    double a[10], sp[8];
+    const int64_t pr = c >> 1;
+    const bool row = star_row(tv, dir, base + own[pr], nb[pr], (c & 1) != 0, a, sp);
     uint32_t f = 0;
-    wave_pair_check<ZT, ADAPTIVE, CM>(T, rs + 8 * r, ra + 10 * r, dir, sn, tn, f);
-    if (lane == 0) rf[r] = f;
+    if (row) {
+      double sn[8], tn = 0;
+      wave_pair_check<ZT, ADAPTIVE, CM>(T, sp, a, dir, sn, tn, f);
+      rows++;
+    }
+    if (lane == 0) {
+      rowof[c] = row ? (int32_t)c : -1;
+      rf[c] = f;
+      if (row) {
+        copy8(rs + 8 * c, sp);
+        copy10(ra + 10 * c, a);
+      }
+      if (f & GBP_F_FRAGILE) {
+        atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_STAR);
+        st->halt_half = half;
+        raise_gate(st, seq);
+      }
+    }
   }
-}
-
-// stage 6f: after the pair checks: a FRAGILE one halts the sequence (the
-// host re-decides it with glibc and resumes at stage 7)
-__global__ __launch_bounds__(TB) void k_star_gate(gbp_plan_status *st, const uint32_t *__restrict__ rf,
-                                                  int32_t half, uint64_t seq) {
-  if (gated(st, seq)) return;
-  const int64_t n = st->star_rows;
-  bool frag = false;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    frag = frag || (rf[i] & GBP_F_FRAGILE);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && n)
-    atomicAdd((unsigned long long *)&st->stat_attempts, (unsigned long long)n);
-  if (__ballot(frag) && (threadIdx.x & (WAVE - 1)) == 0) {
-    atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_STAR);
-    st->halt_half = half;
-    raise_gate(st, seq);
-  }
+  if (lane == 0 && rows)  // the pair checks (engine attempts) made
+    atomicAdd((unsigned long long *)&st->stat_attempts, (unsigned long long)rows);
 }
 
 // block-wide (min key, min index) over the RB threads; NaN keys never win
@@ -2788,36 +2841,24 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     // RRT* insertion, stage 6: neighbourhoods, connect checks, their pair checks
     const unsigned gk = (unsigned)std::max<int64_t>(1, std::min<int64_t>(w->star_items, cus * 8));
     hipLaunchKernelGGL(k_star_count, dim3(gk), dim3(TB), 0, s, st, T->v, w->star_delta, S.scnt,
-                       w->star_items, ++w->seq);
-    hipLaunchKernelGGL(k_star_scan, dim3(1), dim3(RB), 0, s, st, S.scnt, S.sioff, S.soff, S.meta,
-                       w->star_max_pairs, w->star_items, half, ++w->seq);
+                       S.sioff, S.soff, S.meta, w->star_max_pairs, S.sfin, w->star_items, ++w->seq);
     hipLaunchKernelGGL(k_star_fill, dim3(gk), dim3(TB), 0, s, st, T->v, w->star_delta, S.sioff,
                        S.snb, S.sown, w->star_items, ++w->seq);
-    const int64_t rmax = 2 * w->star_max_pairs;
-    hipLaunchKernelGGL(k_star_prep, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, T->v,
-                       direction, S.snb, S.sown, S.srowof, S.sritem, S.srs, S.sra, ++w->seq);
     if (th) HIPCHK_P(hipEventRecord(th->ev[6], s));
-    if (w->star_check_wave) {
-      const int cm = (t->opt_affine && t->affine) ? 2 : 0;
-      const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * 8, (rmax + 3) / 4));
-      const uint64_t cseq = ++w->seq;
+    const int64_t rmax = 2 * w->star_max_pairs;  // connect checks, one wave each
+    const int cm = (t->opt_affine && t->affine) ? 2 : 0;
+    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * 8, (rmax + 3) / 4));
+    const uint64_t cseq = ++w->seq;
 #define GBP_SC(AD, CM)                                                                        \
-  hipLaunchKernelGGL((k_star_check<ZT, AD, CM>), dim3(g), dim3(TB), 0, s, V, st, direction, S.srs, \
-                     S.sra, S.srf, cseq)
-      if (adaptive) {
-        if (cm == 2) GBP_SC(true, 2); else GBP_SC(true, 0);
-      } else {
-        if (cm == 2) GBP_SC(false, 2); else GBP_SC(false, 0);
-      }
-#undef GBP_SC
+  hipLaunchKernelGGL((k_star_check<ZT, AD, CM>), dim3(g), dim3(TB), 0, s, V, st, direction, T->v, \
+                     S.snb, S.sown, S.srowof, S.srs, S.sra, S.srf, half, cseq)
+    if (adaptive) {
+      if (cm == 2) GBP_SC(true, 2); else GBP_SC(true, 0);
     } else {
-      int rc = gbp_internal_validate_dev_n(t, rmax, &st->star_vrows, S.srs, S.sra, nullptr, direction,
-                                           adaptive, nullptr, nullptr, nullptr, S.srf, nullptr, s);
-      if (rc) return rc;
+      if (cm == 2) GBP_SC(false, 2); else GBP_SC(false, 0);
     }
+#undef GBP_SC
     if (th) HIPCHK_P(hipEventRecord(th->ev[7], s));
-    hipLaunchKernelGGL(k_star_gate, dim3(grid_for(rmax, TB, cus * 4)), dim3(TB), 0, s, st, S.srf,
-                       half, ++w->seq);
     if (th) HIPCHK_P(hipEventRecord(th->ev[2], s));
   }
   if (w->star && run(7)) {
@@ -3305,10 +3346,6 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   w->ns_d = carve<double>(p, (int64_t)w->ns_grid * w->ns_capq);
   w->ns_i = carve<int32_t>(p, (int64_t)w->ns_grid * w->ns_capq);
   w->ns_fin = carve<uint32_t>(p, 64);
-  {
-    const char *e = getenv("GBP_STAR_CHECK");  // "persistent": the A/B's other arm
-    w->star_check_wave = (e && !strcmp(e, "persistent")) ? 0 : 1;
-  }
   for (auto &sb : w->nsb) {
     const char *cenv = getenv("GBP_NSC_CAP");  // (a small list: the fallback's test)
     sb.cap = (uint32_t)std::max(1, std::min(NSC_CAP, cenv && *cenv ? atoi(cenv) : NSC_CAP));
@@ -3368,8 +3405,8 @@ int gbp_plan_star_config(gbp_plan_ws *w, int enable, double delta, int64_t max_p
   if (!w->star_block) {
     const int64_t b = w->bmax, r = 2 * max_pairs;
     const int64_t items = std::max<int64_t>(4 * b, 1 << 15);
-    const size_t bytes = 2 * (8 * items + 4 * (b + 1) + 8 * max_pairs + r * (4 + 4 + 64 + 80 + 4) +
-                              32 + 11 * 256) +
+    const size_t bytes = 2 * (12 * items + 4 * (b + 1) + 8 * max_pairs + r * (4 + 4 + 64 + 80 + 4) +
+                              32 + 12 * 256) +
                          4 * b + 8 * max_shared + 4 * 256;
     if (hipMalloc(&w->star_block, bytes) != hipSuccess) {
       w->star_block = nullptr;
@@ -3378,22 +3415,26 @@ int gbp_plan_star_config(gbp_plan_ws *w, int enable, double delta, int64_t max_p
     }
     char *p = (char *)w->star_block;
     for (auto &S : w->ss) {
-      S.scnt = carve<int32_t>(p, items);
+      S.scnt = carve<unsigned long long>(p, items);
       S.sioff = carve<int32_t>(p, items);
       S.soff = carve<int32_t>(p, b + 1);
       S.snb = carve<int32_t>(p, max_pairs);
       S.sown = carve<int32_t>(p, max_pairs);
       S.srowof = carve<int32_t>(p, r);
-      S.sritem = carve<int32_t>(p, r);
       S.srs = carve<double>(p, 8 * r);
       S.sra = carve<double>(p, 10 * r);
       S.srf = carve<uint32_t>(p, r);
       S.meta = carve<int64_t>(p, 4);
+      S.sfin = carve<uint32_t>(p, 64);
     }
     w->star_items = items;
     w->kvtx = carve<int32_t>(p, b);
     w->sshared = carve<int32_t>(p, 2 * max_shared);
     if ((size_t)(p - (char *)w->star_block) > bytes) return GBP_E_HIP;
+    for (auto &S : w->ss)  // (epoch 0 is never a launch's: seq starts at 1)
+      if (hipMemset(S.sfin, 0, 4 * 64) != hipSuccess ||
+          hipMemset(S.scnt, 0, 8 * (size_t)items) != hipSuccess)
+        return GBP_E_HIP;
     w->star_max_pairs = max_pairs;
     w->star_max_shared = max_shared;
   }

@@ -512,8 +512,8 @@ typedef struct {
    * (INFINITY: none); the connect checks of the insertions (2 per pair) and
    * the rewires */
   int32_t star_pairs, star_rows, n_shared, best_a, best_b;
-  int32_t star_vrows;     /* rows the insertion's pair-check launch validates: star_rows,
-                             or 0 when its half is gated (the launch itself is not) */
+  int32_t star_vrows;     /* = star_rows (round 6: the rows are the connect checks
+                             themselves, k_star_check; kept for the layout) */
   double best_cost;
   int64_t stat_star_connects, stat_rewires;
 } gbp_plan_status;

@@ -1,7 +1,6 @@
 """From a rocprofv3 kernel trace of config 5 (tools/c5_prof.sh with C5_KEEP=1):
 durations of each half's two pair-check launches (the extends' candidates after
-k_la_commit / k_targets, and the insertions' connect actions: k_star_check, or
-the persistent kernel after k_star_prep under GBP_STAR_CHECK=persistent),
+k_la_commit / k_targets, and the insertions' connect checks, k_star_check),
 and what ran on the GPU meanwhile.
     python3 tools/c5_trace.py gpurun_out/<tag>_prof"""
 import csv
@@ -16,22 +15,12 @@ for path in glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True):
         rows.extend(csv.DictReader(f))
 ev = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r.get("Queue_Id", ""),
               r.get("Grid_Size", ""), r.get("Workgroup_Size", "")) for r in rows))
-cand, star, star_after = [], [], []
-last = None
+cand, star = [], []
 for s, e, n, q, g, wg in ev:
-    if "k_star_prep" in n:
-        last = "prep"
-    elif "k_la_commit" in n or "k_select" in n:
-        last = None
     if "k_star_check" in n:
         star.append(e - s)
-        last = None
     elif "k_validate_persistent" in n:
-        if last == "prep":
-            star.append(e - s)
-            last = None
-        else:
-            cand.append(e - s)
+        cand.append(e - s)
 print("candidate checks: n %d median %.1f us" % (len(cand), np.median(cand) / 1e3 if cand else 0))
 print("insertion checks: n %d median %.1f us, p90 %.1f" % (
     len(star), np.median(star) / 1e3 if star else 0, np.percentile(star, 90) / 1e3 if star else 0))

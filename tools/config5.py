@@ -42,12 +42,12 @@ def first_valid(T, x, y, step, n=400):
 
 
 STAGES = ("half", "stages 0-3: targets, extends' search, pair checks, select, append",
-          "stage 6: neighbourhoods (k_star_count/scan/fill), connect checks (k_star_prep, "
-          "pair checks, k_star_gate)",
+          "stage 6: neighbourhoods (k_star_count with its scan, k_star_fill), the connect "
+          "checks and their pair checks (k_star_check)",
           "stage 7 on its own stream: k_star_replay (+ k_star_rank after Tb's halves)",
           "stages 4-5: connects' search, k_connect, append, k_star_shared",
-          "stage 6 up to its pair checks: k_star_count, k_star_scan, k_star_fill, k_star_prep",
-          "stage 6's pair checks (the insertions' connect actions, k_validate_persistent)")
+          "stage 6 up to its pair checks: k_star_count, k_star_fill",
+          "stage 6's connect checks (actions and pair checks, k_star_check)")
 
 
 def stage_split(data, start, goal, batch, max_time, seed, device):
@@ -62,7 +62,7 @@ def stage_split(data, start, goal, batch, max_time, seed, device):
     split = {name: round(us / nh, 2) for name, us in zip(STAGES, out["stage_us"])}
     return {"us_per_half": split, "timed_halves": int(out["stage_halves"]),
             "halves": int(out["halves"]),
-            # stage 6 less its pair checks: k_star_count, _scan, _fill, _prep, _gate
+            # stage 6 less its pair checks: k_star_count, k_star_fill
             "k_star_on_caller_stream_us_per_half": round(split[STAGES[2]] - split[STAGES[6]], 2),
             "k_star_replay_side_stream_us_per_half": split[STAGES[3]],
             "source": "hipEvents per half on the streams the stages run on (a second run of "
