@@ -1882,7 +1882,7 @@ __device__ void star_scan_items(gbp_plan_status *st, unsigned long long *cnt, ui
   }
 }
 
-__global__ __launch_bounds__(TB) void k_star_count(gbp_plan_status *st, const double *__restrict__ tv,
+__global__ __launch_bounds__(RB) void k_star_count(gbp_plan_status *st, const double *__restrict__ tv,
                                                    double delta, unsigned long long *cnt,
                                                    int32_t *__restrict__ ioff, int32_t *__restrict__ off,
                                                    int64_t *__restrict__ meta, int64_t max_pairs,
@@ -1898,7 +1898,7 @@ __global__ __launch_bounds__(TB) void k_star_count(gbp_plan_status *st, const do
   const int64_t N = n * nch, parts = max<int64_t>(1, min<int64_t>(gridDim.x, N));
   const uint32_t ep = (uint32_t)seq;  // this launch's epoch (seq grows every launch)
   if ((int64_t)blockIdx.x >= parts) return;
-  __shared__ int sh[TB / WAVE];
+  __shared__ int sh[RB / WAVE];
   __shared__ bool last;
   for (int64_t it = blockIdx.x; it < N; it += gridDim.x) {
     const int64_t k = it / nch, c = it - k * nch;
@@ -1908,7 +1908,7 @@ __global__ __launch_bounds__(TB) void k_star_count(gbp_plan_status *st, const do
     copy8(q, tv + 8 * (base + k));
     const int64_t p1 = min<int64_t>((c + 1) * ch, nk);
     int hits = 0;
-    for (int64_t p = c * ch + threadIdx.x; p < p1; p += TB) {
+    for (int64_t p = c * ch + threadIdx.x; p < p1; p += blockDim.x) {
       const int64_t j = um_key_at(p, nk, m);
       const double d = state_distance(q, tv + 8 * j);  // planner_class.cpp:178
       hits += (d <= delta && d > 0) ? 1 : 0;
@@ -1926,7 +1926,7 @@ __global__ __launch_bounds__(TB) void k_star_count(gbp_plan_status *st, const do
 }
 
 // stage 6c: the neighbour lists, each item's hits in position order at its offset
-__global__ __launch_bounds__(TB) void k_star_fill(gbp_plan_status *st, const double *__restrict__ tv,
+__global__ __launch_bounds__(RB) void k_star_fill(gbp_plan_status *st, const double *__restrict__ tv,
                                                   double delta, const int32_t *__restrict__ ioff,
                                                   int32_t *__restrict__ nb, int32_t *__restrict__ own,
                                                   int64_t cap_items, uint64_t seq) {
@@ -1935,7 +1935,7 @@ __global__ __launch_bounds__(TB) void k_star_fill(gbp_plan_status *st, const dou
   int64_t ch, nch;
   star_chunking(n, base, cap_items, ch, nch);
   const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
-  __shared__ int wc[TB / WAVE];
+  __shared__ int wc[RB / WAVE];
   for (int64_t it = blockIdx.x; it < n * nch; it += gridDim.x) {
     const int64_t k = it / nch, c = it - k * nch;
     const int64_t nk = base + k + 1;
@@ -1944,7 +1944,7 @@ __global__ __launch_bounds__(TB) void k_star_fill(gbp_plan_status *st, const dou
     copy8(q, tv + 8 * (base + k));
     const int64_t p1 = min<int64_t>((c + 1) * ch, nk);
     int64_t run = ioff[it];
-    for (int64_t p0 = c * ch; p0 < p1; p0 += TB) {
+    for (int64_t p0 = c * ch; p0 < p1; p0 += blockDim.x) {
       const int64_t p = p0 + threadIdx.x;
       bool hit = false;
       int64_t j = 0;
@@ -1957,7 +1957,7 @@ __global__ __launch_bounds__(TB) void k_star_fill(gbp_plan_status *st, const dou
       if (lane == 0) wc[w] = __popcll(bm);
       __syncthreads();
       int before = 0, total = 0;
-      for (int i = 0; i < TB / WAVE; i++) {
+      for (int i = 0; i < (int)(blockDim.x / WAVE); i++) {
         if (i < w) before += wc[i];
         total += wc[i];
       }
@@ -2840,9 +2840,9 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   if (w->star && run(6)) {
     // RRT* insertion, stage 6: neighbourhoods, connect checks, their pair checks
     const unsigned gk = (unsigned)std::max<int64_t>(1, std::min<int64_t>(w->star_items, cus * 8));
-    hipLaunchKernelGGL(k_star_count, dim3(gk), dim3(TB), 0, s, st, T->v, w->star_delta, S.scnt,
+    hipLaunchKernelGGL(k_star_count, dim3(gk), dim3(RB), 0, s, st, T->v, w->star_delta, S.scnt,
                        S.sioff, S.soff, S.meta, w->star_max_pairs, S.sfin, w->star_items, ++w->seq);
-    hipLaunchKernelGGL(k_star_fill, dim3(gk), dim3(TB), 0, s, st, T->v, w->star_delta, S.sioff,
+    hipLaunchKernelGGL(k_star_fill, dim3(gk), dim3(RB), 0, s, st, T->v, w->star_delta, S.sioff,
                        S.snb, S.sown, w->star_items, ++w->seq);
     if (th) HIPCHK_P(hipEventRecord(th->ev[6], s));
     const int64_t rmax = 2 * w->star_max_pairs;  // connect checks, one wave each
