@@ -183,6 +183,8 @@ struct gbp_plan_ws {
   double star_delta = 3.0;     // rrt_star_connect.h:59
   int64_t star_max_pairs = 0, star_max_shared = 0;
   int64_t star_items = 0;      // scan items per half (new vertex x position chunk)
+  int star_grid = 0;           // count / fill workgroups cap (GBP_STAR_GRID, tests; 0: none)
+  int64_t star_ch = 1024;      // map positions per scan item before growth (STAR_CH)
   // a half's insertion buffers, one set per tree (half & 1): half h's replay
   // runs on star_stream beside half h's connects and half h + 1, which fills
   // the other set; half h + 2 refills this one only after the replay (its
@@ -1798,9 +1800,9 @@ __device__ __forceinline__ int block_sum_tb(int v, int *sh) {
 constexpr int64_t STAR_CH = 1024;  // positions per item (grown until the items fit)
 
 __device__ __forceinline__ void star_chunking(int64_t n_added, int64_t base, int64_t cap_items,
-                                              int64_t &ch, int64_t &nch) {
+                                              int64_t ch0, int64_t &ch, int64_t &nch) {
   const int64_t nv = base + n_added;
-  ch = STAR_CH;
+  ch = ch0;  // STAR_CH (GBP_STAR_CH in tests); cap_items >= the batch >= n_added: it ends
   nch = (nv + ch - 1) / ch;
   while (n_added * nch > cap_items) {
     ch *= 2;
@@ -1887,11 +1889,11 @@ __global__ __launch_bounds__(RB) void k_star_count(gbp_plan_status *st, const do
                                                    int32_t *__restrict__ ioff, int32_t *__restrict__ off,
                                                    int64_t *__restrict__ meta, int64_t max_pairs,
                                                    uint32_t *__restrict__ fin, int64_t cap_items,
-                                                   uint64_t seq) {
+                                                   int64_t ch0, uint64_t seq) {
   if (gated(st, seq)) return;
   const int64_t n = st->n_added, base = st->added_base;
   int64_t ch, nch;
-  star_chunking(n, base, cap_items, ch, nch);
+  star_chunking(n, base, cap_items, ch0, ch, nch);
   // the workgroups with an item take part in the finish count (the grid is
   // sized for the largest half; most of it exits here); with no items
   // workgroup 0 alone scans (an empty list still resets the half's counts)
@@ -1929,11 +1931,11 @@ __global__ __launch_bounds__(RB) void k_star_count(gbp_plan_status *st, const do
 __global__ __launch_bounds__(RB) void k_star_fill(gbp_plan_status *st, const double *__restrict__ tv,
                                                   double delta, const int32_t *__restrict__ ioff,
                                                   int32_t *__restrict__ nb, int32_t *__restrict__ own,
-                                                  int64_t cap_items, uint64_t seq) {
+                                                  int64_t cap_items, int64_t ch0, uint64_t seq) {
   if (gated(st, seq)) return;
   const int64_t n = st->n_added, base = st->added_base;
   int64_t ch, nch;
-  star_chunking(n, base, cap_items, ch, nch);
+  star_chunking(n, base, cap_items, ch0, ch, nch);
   const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
   __shared__ int wc[RB / WAVE];
   for (int64_t it = blockIdx.x; it < n * nch; it += gridDim.x) {
@@ -2839,11 +2841,13 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   gbp_plan_ws::StarSet &S = w->ss[half & 1];
   if (w->star && run(6)) {
     // RRT* insertion, stage 6: neighbourhoods, connect checks, their pair checks
-    const unsigned gk = (unsigned)std::max<int64_t>(1, std::min<int64_t>(w->star_items, cus * 8));
+    unsigned gk = (unsigned)std::max<int64_t>(1, std::min<int64_t>(w->star_items, cus * 8));
+    if (w->star_grid > 0) gk = std::min<unsigned>(gk, (unsigned)w->star_grid);
     hipLaunchKernelGGL(k_star_count, dim3(gk), dim3(RB), 0, s, st, T->v, w->star_delta, S.scnt,
-                       S.sioff, S.soff, S.meta, w->star_max_pairs, S.sfin, w->star_items, ++w->seq);
+                       S.sioff, S.soff, S.meta, w->star_max_pairs, S.sfin, w->star_items, w->star_ch,
+                       ++w->seq);
     hipLaunchKernelGGL(k_star_fill, dim3(gk), dim3(RB), 0, s, st, T->v, w->star_delta, S.sioff,
-                       S.snb, S.sown, w->star_items, ++w->seq);
+                       S.snb, S.sown, w->star_items, w->star_ch, ++w->seq);
     if (th) HIPCHK_P(hipEventRecord(th->ev[6], s));
     const int64_t rmax = 2 * w->star_max_pairs;  // connect checks, one wave each
     const int cm = (t->opt_affine && t->affine) ? 2 : 0;
@@ -3404,7 +3408,14 @@ int gbp_plan_star_config(gbp_plan_ws *w, int enable, double delta, int64_t max_p
   }
   if (!w->star_block) {
     const int64_t b = w->bmax, r = 2 * max_pairs;
-    const int64_t items = std::max<int64_t>(4 * b, 1 << 15);
+    int64_t items = std::max<int64_t>(4 * b, 1 << 15);
+    // (tests: GBP_STAR_ITEMS, at least the batch, and GBP_STAR_CH small grow
+    // the chunks; GBP_STAR_GRID below makes every count / fill workgroup take
+    // several items)
+    const char *ie = getenv("GBP_STAR_ITEMS");
+    if (ie && *ie) items = std::max<int64_t>(b, atoll(ie));
+    const char *ce = getenv("GBP_STAR_CH");
+    w->star_ch = ce && *ce ? std::max<int64_t>(1, atoll(ce)) : STAR_CH;
     const size_t bytes = 2 * (12 * items + 4 * (b + 1) + 8 * max_pairs + r * (4 + 4 + 64 + 80 + 4) +
                               32 + 12 * 256) +
                          4 * b + 8 * max_shared + 4 * 256;
@@ -3428,6 +3439,8 @@ int gbp_plan_star_config(gbp_plan_ws *w, int enable, double delta, int64_t max_p
       S.sfin = carve<uint32_t>(p, 64);
     }
     w->star_items = items;
+    const char *ge = getenv("GBP_STAR_GRID");
+    w->star_grid = ge && *ge ? std::max(1, atoi(ge)) : 0;
     w->kvtx = carve<int32_t>(p, b);
     w->sshared = carve<int32_t>(p, 2 * max_shared);
     if ((size_t)(p - (char *)w->star_block) > bytes) return GBP_E_HIP;

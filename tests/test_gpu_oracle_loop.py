@@ -174,3 +174,27 @@ def test_rrt_star_equals_oracle(gpu, name, xy, batch, seed, halves, algorithm, f
     print(f"{name} RRT* batch {batch} alg {algorithm}: {halves} halves, trees {len(ref['a']['v'])}+"
           f"{len(ref['b']['v'])}, {ref['rewires']} rewires, {ref['solutions']} connections, "
           f"{dev['fragile_resolved']} re-decided, halts {dev['halts']}")
+
+
+def test_rrt_star_small_item_capacity_equals_oracle(gpu, monkeypatch):
+    """The device RRT*'s neighbourhood scan with its sizes forced small (read
+    when the planner creates its workspace): items of one map position and
+    room for only the batch's 1,024 items per half (k_star_count / k_star_fill
+    double the chunk until a half's items fit), over 2 workgroups (each takes
+    several items; the last of the two to finish scans them all).  Same trees
+    as the oracle."""
+    name, xy, batch, seed, halves = "synth-rough-256", (1.0, 2.55, 4.02, 2.55), 1024, 3, 300
+    data, O, start, goal = _setup(name, xy)
+    monkeypatch.setenv("GBP_STAR_ITEMS", "1")  # (raised to the batch)
+    monkeypatch.setenv("GBP_STAR_CH", "1")
+    monkeypatch.setenv("GBP_STAR_GRID", "2")
+    dev = planner.plan_rrt_star_connect(data, start, goal, batch=batch, max_time=600.0, seed=seed,
+                                        max_halves=halves, trees=True, device_loop=True)
+    for k in ("GBP_STAR_ITEMS", "GBP_STAR_CH", "GBP_STAR_GRID"):
+        monkeypatch.delenv(k)
+    ref = O.plan(start, goal, batch=batch, seed=seed, max_halves=halves, star=True, stream_a=401,
+                 stream_b=402)
+    assert dev["halves"] == ref["halves"] == halves
+    assert dev["rewires"] == ref["rewires"] > 0
+    assert_counters_equal(dev, ref)
+    assert_trees_equal(dev, ref)
