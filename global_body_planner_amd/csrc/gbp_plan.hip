@@ -3296,6 +3296,10 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   // 4096 items: 3072 (the waves resident at 162 VGPRs), 2048 and 6144 measured
   // slower in the planner (profiles/r04l_nn_items.txt)
   w->nn_items = NH_ITEMS;
+  {
+    const char *e = getenv("GBP_NN_ITEMS");  // (A/B sweeps; whole workgroups of NH_TB / WAVE waves)
+    if (e && *e) w->nn_items = std::max(NH_TB / WAVE, std::min(1 << 16, atoi(e))) & ~(NH_TB / WAVE - 1);
+  }
   w->ntiles = (max_batch + TB - 1) / TB + 1;  // k_targets' 256-draw tiles (k_compact_targets: 1024)
   const int64_t b = max_batch, m = GBP_NUM_GEN_STATES * max_batch;
   // k_nn_small's partials: NS_MAXQ queries per workgroup, or a whole batch
