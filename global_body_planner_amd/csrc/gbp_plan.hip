@@ -3305,6 +3305,10 @@ int gbp_plan_ws_create(gbp_terrain *t, int64_t max_batch, gbp_plan_ws **out) {
   // k_nn_small's partials: NS_MAXQ queries per workgroup, or a whole batch
   // when that stays within 2^22 slots (~48 MB; bench's planner: 92,749 x 32)
   w->ns_grid = std::max(1, std::min(NS_BLOCKS, t->num_cus / 8));
+  {
+    const char *e = getenv("GBP_NS_GRID");  // (A/B sweeps)
+    if (e && *e) w->ns_grid = std::max(1, std::min(1024, atoi(e)));
+  }
   w->ns_capq = (int64_t)w->ns_grid * b <= ((int64_t)1 << 22) ? std::max<int64_t>(b, NS_MAXQ) : NS_MAXQ;
   const size_t nsbytes = (size_t)w->ns_grid * w->ns_capq * 12 + 512;
   const size_t bytes = nsbytes + sizeof(gbp_plan_status) + 16 * w->ntiles + 3 * (64 * b + 4 * b + 64 * b + 64 * b) +
