@@ -1798,6 +1798,15 @@ __device__ __forceinline__ int block_sum_tb(int v, int *sh) {
 // order.  A half adds a few vertices to trees of tens of thousands: one
 // workgroup per vertex (the round-5 form) left nearly every CU idle.
 constexpr int64_t STAR_CH = 1024;  // positions per item (grown until the items fit)
+#ifndef GBP_STAR_GK
+#define GBP_STAR_GK 1  // k_star_count / k_star_fill workgroups per CU
+#endif
+#ifndef GBP_STAR_GC
+#define GBP_STAR_GC 2  // k_star_check workgroups (4 waves) per CU
+#endif
+#ifndef GBP_CONNECT_GC
+#define GBP_CONNECT_GC 4  // k_connect workgroups (4 waves, one connection each) per CU
+#endif
 
 __device__ __forceinline__ void star_chunking(int64_t n_added, int64_t base, int64_t cap_items,
                                               int64_t ch0, int64_t &ch, int64_t &nch) {
@@ -2841,7 +2850,10 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   gbp_plan_ws::StarSet &S = w->ss[half & 1];
   if (w->star && run(6)) {
     // RRT* insertion, stage 6: neighbourhoods, connect checks, their pair checks
-    unsigned gk = (unsigned)std::max<int64_t>(1, std::min<int64_t>(w->star_items, cus * 8));
+    // one 1024-thread workgroup per CU at most (a half has ~100-200 items at
+    // config 5; more are taken grid-stride): a grid of 8 per CU, nearly all
+    // exiting at once, cost its dispatch
+    unsigned gk = (unsigned)std::max<int64_t>(1, std::min<int64_t>(w->star_items, cus * GBP_STAR_GK));
     if (w->star_grid > 0) gk = std::min<unsigned>(gk, (unsigned)w->star_grid);
     hipLaunchKernelGGL(k_star_count, dim3(gk), dim3(RB), 0, s, st, T->v, w->star_delta, S.scnt,
                        S.sioff, S.soff, S.meta, w->star_max_pairs, S.sfin, w->star_items, w->star_ch,
@@ -2851,7 +2863,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     if (th) HIPCHK_P(hipEventRecord(th->ev[6], s));
     const int64_t rmax = 2 * w->star_max_pairs;  // connect checks, one wave each
     const int cm = (t->opt_affine && t->affine) ? 2 : 0;
-    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * 8, (rmax + 3) / 4));
+    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * GBP_STAR_GC, (rmax + 3) / 4));
     const uint64_t cseq = ++w->seq;
 #define GBP_SC(AD, CM)                                                                        \
   hipLaunchKernelGGL((k_star_check<ZT, AD, CM>), dim3(g), dim3(TB), 0, s, V, st, direction, T->v, \
@@ -2886,7 +2898,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
                        nullptr, nullptr, nullptr, true, true);
     if (rc) return rc;
     const int cm = (t->opt_affine && t->affine) ? 2 : 0;
-    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * 4, (batch + 3) / 4));
+    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * GBP_CONNECT_GC, (batch + 3) / 4));
     const uint64_t kseq = ++w->seq;
 #define GBP_KC(AD, CM)                                                                         \
   hipLaunchKernelGGL((k_connect<ZT, AD, CM>), dim3(g), dim3(TB), 0, s, V, st, cdir, T->v, O->v, \
