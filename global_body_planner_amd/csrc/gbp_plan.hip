@@ -199,7 +199,7 @@ struct gbp_plan_ws {
     double *srs = nullptr;       // [2 max_pairs][8] rows: the pair checks' states
     double *sra = nullptr;       // [2 max_pairs][10] and actions
     uint32_t *srf = nullptr;     // [2 max_pairs] their flags
-    int64_t *meta = nullptr;     // [4] n_added, added_base, pairs (k_star_count's scan); shared count (k_star_shared)
+    int64_t *meta = nullptr;     // [4] n_added, added_base, pairs (k_star_count's scan); shared count (stage-5 append)
     uint32_t *sfin = nullptr;    // [64] k_star_count's finished-workgroup count (zeroed, self-resetting)
   } ss[2];
   int32_t *kvtx = nullptr;     // [bmax] O's vertex of each connection (-1: none)
@@ -1447,6 +1447,23 @@ __global__ __launch_bounds__(TB) void k_select(gbp_plan_status *st, const double
 // ============================================================================
 // stages 3 and 5: ordered appends (rrt.cpp:86-92, rrt_connect.cpp:107-116)
 // ============================================================================
+// RRT*'s list of the connections kept (rrt_star_connect.cpp:136-175:
+// shared_a / shared_b), built by the stage-5 append itself when `list` is
+// set (round 6; a one-workgroup launch after it before): the REACHED
+// connections that were appended, in connection order, after the n_shared
+// listed before — a second ordered look-back over tiles of their own
+// (tiles2, epoch2; the grid's total in *tot2), the last tile publishing
+// n_shared and meta[3] (the list's length for the ranking after Tb's half)
+struct StarShared {
+  int32_t *list = nullptr;
+  int64_t max_shared = 0;
+  int64_t *meta = nullptr;
+  unsigned long long *tiles2 = nullptr;
+  uint32_t epoch2 = 0;
+  int32_t *tot2 = nullptr;
+  int t_is_a = 0;
+};
+
 // mode 0: extend successors of the current targets into T (parent = nn[i]);
 // mode 1: connections of the new vertices into O (parent = nno[k]), the first
 // REACHED one in order recorded as the meeting point.
@@ -1461,7 +1478,8 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
                                                int32_t *__restrict__ vtx, unsigned long long *tiles,
                                                uint32_t epoch, int32_t half, int64_t cap,
                                                uint64_t seq, int32_t *tch,
-                                               int32_t *tsib, int32_t *tprev, int star) {
+                                               int32_t *tsib, int32_t *tprev, int star,
+                                               StarShared sh = StarShared{}) {
   if (gated(st, seq)) return;
   __shared__ int32_t s_base;
   if (threadIdx.x == 0) s_base = *tcount;  // read before this block publishes its count
@@ -1506,7 +1524,7 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
       if (h >= 0) tprev[h] = idx;
     }
     if (vtx) vtx[i] = idx;
-    if (mode == 1 && r == GBP_REACHED && !star) {  // RRT*: every REACHED one is kept (k_star_shared)
+    if (mode == 1 && r == GBP_REACHED && !star) {  // RRT*: every REACHED one is kept (StarShared)
       atomicMin((unsigned long long *)&st->meet,
                 ((unsigned long long)i << 32) | (unsigned long long)(uint32_t)idx);
       st->meet_half = half;
@@ -1515,6 +1533,27 @@ __global__ __launch_bounds__(CB) void k_append(gbp_plan_status *st, int mode,
     }
   } else if (live && vtx) {
     vtx[i] = -1;
+  }
+  if (sh.list) {  // (mode 1, RRT*: every block reaches here; ns read before any publishes)
+    const int64_t ns = st->n_shared;
+    const bool hit = keep && r == GBP_REACHED && (int64_t)base + rank < cap;
+    const uint32_t r2 = ordered_rank(hit, sh.tiles2, sh.epoch2, sh.tot2, st);
+    if (hit && ns + (int64_t)r2 < sh.max_shared) {
+      // connection i joins T's new vertex added_base + i to O's appended row
+      const int32_t tv_ = (int32_t)(st->added_base + i), ov = (int32_t)(base + rank);
+      sh.list[2 * (ns + r2)] = sh.t_is_a ? tv_ : ov;
+      sh.list[2 * (ns + r2) + 1] = sh.t_is_a ? ov : tv_;
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+      const int64_t tot = ns + *sh.tot2;
+      if (tot > sh.max_shared) {
+        atomicOr(&st->error, 4u);
+        raise_gate(st, seq);
+      } else {
+        st->n_shared = (int32_t)tot;
+        sh.meta[3] = tot;
+      }
+    }
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
     // the rows actually written (the appended count is clamped at cap)
@@ -2383,53 +2422,6 @@ __global__ __launch_bounds__(RW) void k_star_replay(gbp_plan_status *st, const d
   if (lane == 0 && rewires) st->stat_rewires += rewires;
 }
 
-// stage 5 (RRT*): the half's REACHED connections appended to the shared list
-// in connection order (rrt_star_connect.cpp:136-175: shared_a / shared_b);
-// meta[3] keeps the list's length for the ranking after Tb's half
-__global__ __launch_bounds__(RB) void k_star_shared(gbp_plan_status *st, const int32_t *__restrict__ kres,
-                                                    const int32_t *__restrict__ kvtx, int t_is_a,
-                                                    int32_t *shared, int64_t max_shared,
-                                                    int64_t *__restrict__ meta, uint64_t seq) {
-  if (gated(st, seq)) return;
-  const int64_t n = st->n_added, base = st->added_base;
-  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
-  __shared__ int wc[RB / WAVE];
-  int64_t ns = st->n_shared;
-  for (int64_t i0 = 0; i0 < n; i0 += RB) {
-    const int64_t i = i0 + threadIdx.x;
-    const bool hit = i < n && kres[i] == GBP_REACHED && kvtx[i] >= 0;
-    const unsigned long long m = __ballot(hit);
-    if (lane == 0) wc[w] = __popcll(m);
-    __syncthreads();
-    int before = 0, total = 0;
-    for (int q = 0; q < RB / WAVE; q++) {
-      if (q < w) before += wc[q];
-      total += wc[q];
-    }
-    if (hit) {
-      const int64_t p = ns + before + __popcll(m & ((1ull << lane) - 1ull));
-      const int32_t tv_ = (int32_t)(base + i), ov = kvtx[i];
-      if (p < max_shared) {
-        shared[2 * p] = t_is_a ? tv_ : ov;
-        shared[2 * p + 1] = t_is_a ? ov : tv_;
-      }
-    }
-    ns += total;
-    __syncthreads();
-  }
-  if (ns > max_shared) {
-    if (threadIdx.x == 0) {
-      atomicOr(&st->error, 4u);
-      raise_gate(st, seq);
-    }
-    return;
-  }
-  if (threadIdx.x == 0) {
-    st->n_shared = (int32_t)ns;
-    meta[3] = ns;
-  }
-}
-
 // after Tb's half (star_stream, behind both trees' replays): the cheapest
 // of the meta[3] connections listed so far ranked with the current g values
 // (:181-193: strictly cheaper than the best so far; ties to the first)
@@ -2913,14 +2905,23 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
   if (run(5)) {
     // O's last replay (half h - 1's, on star_stream) before appending into O
     if (w->star) HIPCHK_P(hipStreamWaitEvent(s, w->star_rdone[1 - kT], 0));
+    const bool t_is_a = direction == GBP_FORWARD;
+    StarShared ssh;
+    if (w->star) {  // the REACHED connections kept, listed by the append itself
+      ssh.list = w->sshared;
+      ssh.max_shared = w->star_max_shared;
+      ssh.meta = S.meta;
+      ssh.tiles2 = w->tiles + tiles_for(batch);
+      ssh.tot2 = (int32_t *)(S.sfin + 8);
+      ssh.t_is_a = t_is_a ? 1 : 0;
+    }
+    const uint32_t ep1 = next_epoch(w);
+    if (w->star) ssh.epoch2 = next_epoch(w);
     hipLaunchKernelGGL(k_append, dim3(tiles_for(batch)), dim3(CB), 0, s, st, 1, w->kres, w->nno,
                        w->ksn, w->kan, O->v, O->vh, O->hm, O->a, O->g, O->parent, O->count,
-                       w->star ? w->kvtx : nullptr, w->tiles, next_epoch(w), half, O->cap, ++w->seq,
-                       O->child, O->sibling, O->prev, w->star);
-    if (w->star) {  // the REACHED connections kept; after Tb's half the best one ranked
-      const bool t_is_a = direction == GBP_FORWARD;
-      hipLaunchKernelGGL(k_star_shared, dim3(1), dim3(RB), 0, s, st, w->kres, w->kvtx, t_is_a ? 1 : 0,
-                         w->sshared, w->star_max_shared, S.meta, ++w->seq);
+                       w->star ? w->kvtx : nullptr, w->tiles, ep1, half, O->cap, ++w->seq,
+                       O->child, O->sibling, O->prev, w->star, ssh);
+    if (w->star) {  // after Tb's half the best connection ranked
       if (half & 1) {
         // on star_stream behind this half's replay (Tb's g final) and half h - 1's
         // (Ta's); the next replay of Ta queues behind it, and half h + 1's

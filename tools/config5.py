@@ -45,7 +45,7 @@ STAGES = ("half", "stages 0-3: targets, extends' search, pair checks, select, ap
           "stage 6: neighbourhoods (k_star_count with its scan, k_star_fill), the connect "
           "checks and their pair checks (k_star_check)",
           "stage 7 on its own stream: k_star_replay (+ k_star_rank after Tb's halves)",
-          "stages 4-5: connects' search, k_connect, append, k_star_shared",
+          "stages 4-5: connects' search, k_connect, append (with the shared list)",
           "stage 6 up to its pair checks: k_star_count, k_star_fill",
           "stage 6's connect checks (actions and pair checks, k_star_check)")
 
