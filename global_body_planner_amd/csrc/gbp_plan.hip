@@ -1881,7 +1881,7 @@ __device__ __forceinline__ int64_t star_item_count(gbp_plan_status *st, unsigned
 __device__ void star_scan_items(gbp_plan_status *st, unsigned long long *cnt, uint32_t ep, int64_t N,
                                 int64_t nch, int64_t n, int64_t base, int32_t *__restrict__ ioff,
                                 int32_t *__restrict__ off, int64_t *__restrict__ meta,
-                                int64_t max_pairs, uint64_t seq) {
+                                int64_t max_pairs, int32_t half, uint64_t seq) {
   const int nt = (int)blockDim.x;
   const int64_t per = (N + nt - 1) / nt;
   const int64_t lo = min<int64_t>(N, threadIdx.x * per), hi = min<int64_t>(N, lo + per);
@@ -1924,10 +1924,12 @@ __device__ void star_scan_items(gbp_plan_status *st, unsigned long long *cnt, ui
     meta[2] = min<int64_t>(total, 0x7FFFFFFF);
     st->star_rows = (int32_t)min<int64_t>(2 * total, 0x7FFFFFFF);  // rows = checks (k_star_check)
     st->star_vrows = st->star_rows;
-    st->stat_star_connects += 2 * total;  // a choose-parent and a rewire connect per pair
-    if (total > max_pairs) {
-      atomicOr(&st->error, 4u);
+    if (total > max_pairs) {  // the host grows the sets and resumes this half at stage 6
+      atomicOr(&st->halt, (uint32_t)GBP_PLAN_HALT_STAR_PAIRS);
+      st->halt_half = half;
       raise_gate(st, seq);
+    } else {
+      st->stat_star_connects += 2 * total;  // a choose-parent and a rewire connect per pair
     }
   }
 }
@@ -1937,7 +1939,7 @@ __global__ __launch_bounds__(RB) void k_star_count(gbp_plan_status *st, const do
                                                    int32_t *__restrict__ ioff, int32_t *__restrict__ off,
                                                    int64_t *__restrict__ meta, int64_t max_pairs,
                                                    uint32_t *__restrict__ fin, int64_t cap_items,
-                                                   int64_t ch0, uint64_t seq) {
+                                                   int64_t ch0, int32_t half, uint64_t seq) {
   if (gated(st, seq)) return;
   const int64_t n = st->n_added, base = st->added_base;
   int64_t ch, nch;
@@ -1971,7 +1973,7 @@ __global__ __launch_bounds__(RB) void k_star_count(gbp_plan_status *st, const do
   if (threadIdx.x == 0) last = atomicAdd(fin, 1u) == (uint32_t)(parts - 1);
   __syncthreads();
   if (!last) return;
-  star_scan_items(st, cnt, ep, N, nch, n, base, ioff, off, meta, max_pairs, seq);
+  star_scan_items(st, cnt, ep, N, nch, n, base, ioff, off, meta, max_pairs, half, seq);
   if (threadIdx.x == 0) *fin = 0;  // reset for the next half (stream-ordered)
 }
 
@@ -2849,7 +2851,7 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     if (w->star_grid > 0) gk = std::min<unsigned>(gk, (unsigned)w->star_grid);
     hipLaunchKernelGGL(k_star_count, dim3(gk), dim3(RB), 0, s, st, T->v, w->star_delta, S.scnt,
                        S.sioff, S.soff, S.meta, w->star_max_pairs, S.sfin, w->star_items, w->star_ch,
-                       ++w->seq);
+                       half, ++w->seq);
     hipLaunchKernelGGL(k_star_fill, dim3(gk), dim3(RB), 0, s, st, T->v, w->star_delta, S.sioff,
                        S.snb, S.sown, w->star_items, w->star_ch, ++w->seq);
     if (th) HIPCHK_P(hipEventRecord(th->ev[6], s));
@@ -3422,8 +3424,22 @@ int gbp_plan_star_config(gbp_plan_ws *w, int enable, double delta, int64_t max_p
       max_shared > (1 << 28))
     return GBP_E_INVALID_ARG;
   Guard g(w->device);
+  {
+    const char *pe = getenv("GBP_STAR_PAIRS");  // (tests: a small first size, grown by the halts)
+    if (pe && *pe && !w->star_block) max_pairs = std::max<int64_t>(1, std::min<int64_t>(max_pairs, atoll(pe)));
+  }
+  // a larger block keeps the run's list of kept connections (the ranking
+  // after Tb's halves reads all of it); the per-half sets are rebuilt by the
+  // half that resumes (GBP_PLAN_HALT_STAR_PAIRS)
+  std::vector<int32_t> keep_shared;
   if (w->star_block && (max_pairs > w->star_max_pairs || max_shared > w->star_max_shared)) {
     (void)hipDeviceSynchronize();
+    max_pairs = std::max(max_pairs, w->star_max_pairs);
+    max_shared = std::max(max_shared, w->star_max_shared);
+    keep_shared.resize(2 * (size_t)w->star_max_shared);
+    if (hipMemcpy(keep_shared.data(), w->sshared, 8 * (size_t)w->star_max_shared,
+                  hipMemcpyDeviceToHost) != hipSuccess)
+      return GBP_E_HIP;
     (void)hipFree(w->star_block);
     w->star_block = nullptr;
   }
@@ -3469,6 +3485,9 @@ int gbp_plan_star_config(gbp_plan_ws *w, int enable, double delta, int64_t max_p
       if (hipMemset(S.sfin, 0, 4 * 64) != hipSuccess ||
           hipMemset(S.scnt, 0, 8 * (size_t)items) != hipSuccess)
         return GBP_E_HIP;
+    if (!keep_shared.empty() &&
+        hipMemcpy(w->sshared, keep_shared.data(), 4 * keep_shared.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return GBP_E_HIP;
     w->star_max_pairs = max_pairs;
     w->star_max_shared = max_shared;
   }
@@ -3741,7 +3760,12 @@ int gbp_plan_resolve_host(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree 
   *resume_stage = -1;
   int64_t k = 0;
   select_targets(w, st.halt_half >= 0 ? st.halt_half : 0);  // the halted half's target set
-  if (st.halt & GBP_PLAN_HALT_TARGETS) {
+  if (st.halt & GBP_PLAN_HALT_STAR_PAIRS) {
+    // nothing to re-decide: the caller has grown the insertion sets
+    // (gbp_plan_star_config); the half redoes its stage 6
+    if (2 * (int64_t)st.star_pairs > 2 * w->star_max_pairs) return GBP_E_SHAPE;
+    *resume_stage = 6;
+  } else if (st.halt & GBP_PLAN_HALT_TARGETS) {
     // isValidState(s_rand, STANCE) of the half's draws (rrt_connect.cpp:254)
     if (batch < 1 || batch > w->bmax) return GBP_E_INVALID_ARG;
     std::vector<uint32_t> fl(batch);

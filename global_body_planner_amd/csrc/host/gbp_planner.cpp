@@ -2218,8 +2218,8 @@ bool RRTStarConnectClass::buildRRTStarConnectDevice(FastTerrainMap &terrain, Sta
   chk(gbp_stream_create(dev, &D.stream), "stream");
   chk(gbp_plan_ws_create(h, batch, &D.ws), "plan workspace");
   // neighbour pairs of one half (2 connect checks each) and REACHED connections of the run
-  chk(gbp_plan_star_config(D.ws, 1, delta, std::max<int64_t>(1 << 18, 8 * (int64_t)batch), 1 << 22),
-      "star config");
+  int64_t star_pairs_cap = std::max<int64_t>(1 << 18, 8 * (int64_t)batch);
+  chk(gbp_plan_star_config(D.ws, 1, delta, star_pairs_cap, 1 << 22), "star config");
   if (st.stage_timing) chk(gbp_plan_stage_timing(D.ws, 1), "stage timing");
   int64_t cap = std::max<int64_t>(1 << 16, 4 * (int64_t)batch);
   int64_t known[2] = {1, 1};
@@ -2268,6 +2268,13 @@ bool RRTStarConnectClass::buildRRTStarConnectDevice(FastTerrainMap &terrain, Sta
       const int k = h0 & 1;
       int resume = -1;
       int64_t nres = 0;
+      if (ps.halt & GBP_PLAN_HALT_STAR_PAIRS) {
+        // a half's neighbour pairs outgrew the insertion sets: grow them (the
+        // run's kept connections stay) and redo the half's stage 6
+        st.star_grows++;
+        star_pairs_cap = std::max<int64_t>(2 * star_pairs_cap, (int64_t)ps.star_pairs + ps.star_pairs / 4);
+        chk(gbp_plan_star_config(D.ws, 1, delta, star_pairs_cap, 1 << 22), "star config (grow)");
+      }
       chk(gbp_plan_resolve_host(h, D.ws, D.tree[k], D.tree[k ^ 1], k == 0 ? FORWARD : REVERSE,
                                 batch, adaptive, &resume, &nres, D.stream),
           "plan resolve");

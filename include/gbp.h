@@ -467,6 +467,9 @@ int gbp_tree_device_ptrs(gbp_tree *tree, double **states, int32_t **count);
 #define GBP_PLAN_HALT_EXTEND  2u
 #define GBP_PLAN_HALT_CONNECT 4u
 #define GBP_PLAN_HALT_STAR    8u  /* RRT*: an insertion's connect check (resume stage 7) */
+#define GBP_PLAN_HALT_STAR_PAIRS 16u /* RRT*: a half's neighbour pairs (status.star_pairs) exceed
+                                        max_pairs: gbp_plan_star_config with at least that many,
+                                        then gbp_plan_resolve_host (resume stage 6) */
 typedef struct {
   uint32_t halt;          /* GBP_PLAN_HALT_* of the stage that stopped the sequence */
   uint32_t done;          /* a connection REACHED */
@@ -543,17 +546,21 @@ int gbp_plan_halves_dev(gbp_terrain *t, gbp_plan_ws *ws, gbp_tree *Ta, gbp_tree 
  * vertices as RRT*'s extend does, between stages 3 and 4:
  *   stage 6  the neighbourhood of each new vertex among the vertices before it
  *            (stateDistance <= delta, > 0: neighborhoodDist, planner_class.cpp:
- *            173-182, ascending index), and the two depth-0 connect decisions
+ *            173-182, in the vertex map's iteration order), and the two depth-0 connect decisions
  *            per neighbour (choose-parent attemptConnect(s_near, s_new), rewire
  *            attemptConnect(s_new, s_near)), their pair checks batched
  *   stage 7  the insertions replayed in order: choose-parent, addEdge, rewire
  *            with the g of every rewired subtree updated (graph_class.cpp:131-138)
  * and stage 5 keeps every REACHED connection (no early stop) and, after tree
  * Tb's half, ranks the cheapest with the current g values (status best_*).
- * Targets are never drawn ahead.  max_pairs bounds the neighbour pairs of one
- * half, max_shared the REACHED connections of a run (status.error bit 2 when
- * exceeded).  A FRAGILE insertion check halts with GBP_PLAN_HALT_STAR (resume
- * at stage 7).  enable = 0 returns the workspace to RRT-Connect. */
+ * max_pairs sizes the neighbour pairs of one half: a half with more halts
+ * with GBP_PLAN_HALT_STAR_PAIRS (status.star_pairs = the count; calling this
+ * again with a larger max_pairs reallocates the sets and keeps the run's
+ * list of kept connections, and gbp_plan_resolve_host resumes the half at
+ * stage 6).  max_shared bounds the REACHED connections of a run (status.error
+ * bit 2 when exceeded).  A FRAGILE insertion check halts with
+ * GBP_PLAN_HALT_STAR (resume at stage 7).  enable = 0 returns the workspace
+ * to RRT-Connect. */
 int gbp_plan_star_config(gbp_plan_ws *ws, int enable, double delta, int64_t max_pairs,
                          int64_t max_shared);
 /* diagnostics: per half-iteration timing events (hipEvents with timing, on

@@ -413,6 +413,7 @@ struct BatchStats {
   int64_t fragile_resolved = 0;  // attempts re-decided on the host (GBP_F_RESOLVED)
   int64_t halts[4] = {0, 0, 0, 0};  // device loop: FRAGILE halts in the targets / extend /
                                     // connect / RRT* insertion stage (GBP_PLAN_HALT_*)
+  int64_t star_grows = 0;           // device RRT*: insertion sets grown (GBP_PLAN_HALT_STAR_PAIRS)
   int64_t nn_rechecks = 0, nn_scans = 0;  // device loop with GBP_OPT_NN_STATS: the matrix-core
                                           // search's fp64 half-chunk re-checks / segment scans
   double extent_a[4] = {0, 0, 0, 0}, extent_b[4] = {0, 0, 0, 0};  // x_min x_max y_min y_max

@@ -198,3 +198,28 @@ def test_rrt_star_small_item_capacity_equals_oracle(gpu, monkeypatch):
     assert dev["rewires"] == ref["rewires"] > 0
     assert_counters_equal(dev, ref)
     assert_trees_equal(dev, ref)
+
+
+def test_rrt_star_insertion_sets_grow_equals_oracle(gpu, monkeypatch):
+    """The device RRT*'s insertion sets sized for 16 neighbour pairs
+    (GBP_STAR_PAIRS, read when the planner first configures them): every
+    half with more halts at its neighbourhood scan (GBP_PLAN_HALT_STAR_PAIRS),
+    the host grows the sets (keeping the run's list of kept connections) and
+    the half redoes its stage 6.  Same trees, rewires and best connection as
+    the oracle."""
+    name, xy, batch, seed, halves = "synth-rough-256", (1.0, 2.55, 4.02, 2.55), 1024, 3, 300
+    data, O, start, goal = _setup(name, xy)
+    monkeypatch.setenv("GBP_STAR_PAIRS", "16")
+    dev = planner.plan_rrt_star_connect(data, start, goal, batch=batch, max_time=600.0, seed=seed,
+                                        max_halves=halves, trees=True, device_loop=True)
+    monkeypatch.delenv("GBP_STAR_PAIRS")
+    ref = O.plan(start, goal, batch=batch, seed=seed, max_halves=halves, star=True, stream_a=401,
+                 stream_b=402)
+    assert dev["halves"] == ref["halves"] == halves
+    assert dev["rewires"] == ref["rewires"] > 0
+    assert dev["found"] == ref["found"] and dev["solutions"] == ref["solutions"]
+    assert_counters_equal(dev, ref)
+    assert_trees_equal(dev, ref)
+    if ref["found"]:
+        assert (dev["meet_a"], dev["meet_b"]) == (ref["best_a"], ref["best_b"])
+        assert dev["path_cost"] == ref["best_cost"]
