@@ -185,6 +185,7 @@ struct gbp_plan_ws {
   int64_t star_items = 0;      // scan items per half (new vertex x position chunk)
   int star_grid = 0;           // count / fill workgroups cap (GBP_STAR_GRID, tests; 0: none)
   int64_t star_ch = 1024;      // map positions per scan item before growth (STAR_CH)
+  int32_t star_lds[3] = {-1, -1, -1};  // the replay's LDS limits (GBP_STAR_LDS, tests; -1: RP, RK, RQ)
   // a half's insertion buffers, one set per tree (half & 1): half h's replay
   // runs on star_stream beside half h's connects and half h + 1, which fills
   // the other set; half h + 2 refills this one only after the replay (its
@@ -2161,7 +2162,7 @@ __device__ __forceinline__ int64_t wave_first(int64_t at) {
 constexpr int RQ = 2048;
 __device__ bool subtree_g(const double *__restrict__ tv, double *tg, const int32_t *tch,
                           const int32_t *tsib, int32_t r, double gr, int32_t *q0, int32_t *q1,
-                          int32_t nv) {
+                          int32_t nv, int32_t rq) {
   __shared__ int32_t lq[2][RQ];
   __shared__ double lg[2][RQ];
   __shared__ int32_t s_next;
@@ -2174,8 +2175,8 @@ __device__ bool subtree_g(const double *__restrict__ tv, double *tg, const int32
   __syncthreads();
   while (nq > 0) {
     for (int32_t i = threadIdx.x; i < nq; i += RW) {
-      const int32_t p = i < RQ ? lq[cur][i] : q0[i];
-      const double gp = i < RQ ? lg[cur][i] : tg[p];
+      const int32_t p = i < rq ? lq[cur][i] : q0[i];
+      const double gp = i < rq ? lg[cur][i] : tg[p];
       double vp[8];
       copy8(vp, tv + 8 * (int64_t)p);
       for (int32_t c = tch[p]; c >= 0; c = tsib[c]) {
@@ -2183,7 +2184,7 @@ __device__ bool subtree_g(const double *__restrict__ tv, double *tg, const int32
         tg[c] = gc;
         const int32_t slot = atomicAdd(&s_next, 1);
         if (slot >= nv) break;
-        if (slot < RQ) {
+        if (slot < rq) {
           lq[cur ^ 1][slot] = c;
           lg[cur ^ 1][slot] = gc;
         } else {
@@ -2226,6 +2227,11 @@ constexpr int RP = 2048;  // pairs held in LDS (config 5: ~300 per half)
 constexpr int RS = 4;     // a lane's neighbour slots per insertion in registers
 constexpr int RK = 512;   // new vertices held in LDS (their nearest vertex and g0's distance)
 
+// what the replay keeps in LDS (tests shrink it: GBP_STAR_LDS = "rp,rk,rq")
+struct StarLds {
+  int32_t rp = RP, rk = RK, rq = RQ;
+};
+
 struct PairInfo {
   int32_t j;
   uint32_t f;
@@ -2257,8 +2263,10 @@ __global__ __launch_bounds__(RW) void k_star_replay(gbp_plan_status *st, const d
                                                     const double *__restrict__ ra,
                                                     const uint32_t *__restrict__ rf,
                                                     const int64_t *__restrict__ meta, int32_t *q0,
-                                                    int32_t *q1, const int32_t *tcount, uint64_t seq) {
+                                                    int32_t *q1, const int32_t *tcount, StarLds lim,
+                                                    uint64_t seq) {
   if (gated(st, seq)) return;
+  const int32_t rp = lim.rp, rk = lim.rk;  // (RP, RK; smaller in tests: the global paths)
   const int64_t n = meta[0], base = meta[1], npairs = meta[2];
   const int32_t nv = *tcount;
   const int lane = threadIdx.x;
@@ -2269,31 +2277,31 @@ __global__ __launch_bounds__(RW) void k_star_replay(gbp_plan_status *st, const d
   __shared__ double ld0[RK];
   // prologue: every pair's static part and every new vertex's nearest vertex,
   // its offsets and poseDistance(s_new, s_nearest) (:28), all lanes at once
-  for (int64_t i = lane; i < min<int64_t>(npairs, RP); i += RW) {
+  for (int64_t i = lane; i < min<int64_t>(npairs, rp); i += RW) {
     const PairInfo pi = pair_info_global(i, tv, base, nb, own, rowof, rf);
     lj[i] = pi.j;
     lf[i] = pi.f;
     ld[i] = pi.d;
   }
-  for (int64_t k = lane; k < min<int64_t>(n, RK); k += RW) {
+  for (int64_t k = lane; k < min<int64_t>(n, rk); k += RW) {
     const int32_t nn = tp[base + k];  // stage 3 wrote the nearest vertex here
     lnn[k] = nn;
     ld0[k] = pose_distance(tv + 8 * (base + k), tv + 8 * (int64_t)nn);
     loff[k] = off[k];
   }
-  const int64_t nk_l = n < RK ? n : RK;
+  const int64_t nk_l = n < rk ? n : rk;
   if (lane == 0) loff[nk_l] = off[nk_l];
   __syncthreads();
   auto pair = [&](int64_t i) -> PairInfo {
-    if (i < RP) return PairInfo{lj[i], lf[i], ld[i]};
+    if (i < rp) return PairInfo{lj[i], lf[i], ld[i]};
     return pair_info_global(i, tv, base, nb, own, rowof, rf);
   };
   int64_t rewires = 0;
   for (int64_t k = 0; k < n; k++) {
     const int32_t idx = (int32_t)(base + k);
-    const int32_t nn = k < RK ? lnn[k] : tp[idx];
-    const double d0 = k < RK ? ld0[k] : pose_distance(tv + 8 * (int64_t)idx, tv + 8 * (int64_t)nn);
-    const int64_t i0 = k < RK ? loff[k] : off[k], i1 = k + 1 <= RK ? loff[k + 1] : off[k + 1];
+    const int32_t nn = k < rk ? lnn[k] : tp[idx];
+    const double d0 = k < rk ? ld0[k] : pose_distance(tv + 8 * (int64_t)idx, tv + 8 * (int64_t)nn);
+    const int64_t i0 = k < rk ? loff[k] : off[k], i1 = k + 1 <= rk ? loff[k + 1] : off[k + 1];
     // this lane's first RS neighbours (positions i0 + lane + RW s)
     int32_t sj[RS];
     uint32_t sf[RS];
@@ -2410,7 +2418,7 @@ __global__ __launch_bounds__(RW) void k_star_replay(gbp_plan_status *st, const d
       __syncthreads();
       rewires++;
       // the rewired vertex's successors (recursion of updateGYValue)
-      if (tch[j] >= 0 && !subtree_g(tv, tg, tch, tsib, j, gj, q0, q1, nv)) {
+      if (tch[j] >= 0 && !subtree_g(tv, tg, tch, tsib, j, gj, q0, q1, nv, lim.rq)) {
         if (lane == 0) {
           atomicOr(&st->error, 8u);  // a successor list that is not a tree
           raise_gate(st, seq);
@@ -2879,9 +2887,15 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     HIPCHK_P(hipEventRecord(w->star_e6, s));
     HIPCHK_P(hipStreamWaitEvent(w->star_stream, w->star_e6, 0));
     if (th) HIPCHK_P(hipEventRecord(th->ev[3], w->star_stream));
+    StarLds lds;
+    if (w->star_lds[0] >= 0) {
+      lds.rp = w->star_lds[0];
+      lds.rk = w->star_lds[1];
+      lds.rq = w->star_lds[2];
+    }
     hipLaunchKernelGGL(k_star_replay, dim3(1), dim3(RW), 0, w->star_stream, st, T->v, T->a, T->g,
                        T->parent, T->child, T->sibling, T->prev, S.soff, S.snb, S.sown, S.srowof,
-                       S.sra, S.srf, S.meta, T->bfs, T->bfs + T->cap, T->count, ++w->seq);
+                       S.sra, S.srf, S.meta, T->bfs, T->bfs + T->cap, T->count, lds, ++w->seq);
     HIPCHK_P(hipEventRecord(w->star_rdone[kT], w->star_stream));
   }
   if (!O) return hipGetLastError() == hipSuccess ? GBP_OK : GBP_E_HIP;
@@ -3451,6 +3465,15 @@ int gbp_plan_star_config(gbp_plan_ws *w, int enable, double delta, int64_t max_p
     // several items)
     const char *ie = getenv("GBP_STAR_ITEMS");
     if (ie && *ie) items = std::max<int64_t>(b, atoll(ie));
+    const char *le = getenv("GBP_STAR_LDS");
+    if (le && *le) {
+      int a = RP, b2 = RK, c = RQ;
+      if (sscanf(le, "%d,%d,%d", &a, &b2, &c) == 3) {
+        w->star_lds[0] = std::max(0, std::min(a, RP));
+        w->star_lds[1] = std::max(0, std::min(b2, RK));
+        w->star_lds[2] = std::max(1, std::min(c, RQ));
+      }
+    }
     const char *ce = getenv("GBP_STAR_CH");
     w->star_ch = ce && *ce ? std::max<int64_t>(1, atoll(ce)) : STAR_CH;
     const size_t bytes = 2 * (12 * items + 4 * (b + 1) + 8 * max_pairs + r * (4 + 4 + 64 + 80 + 4) +

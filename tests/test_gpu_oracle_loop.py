@@ -200,6 +200,26 @@ def test_rrt_star_small_item_capacity_equals_oracle(gpu, monkeypatch):
     assert_trees_equal(dev, ref)
 
 
+def test_rrt_star_replay_global_paths_equal_oracle(gpu, monkeypatch):
+    """k_star_replay with its LDS holdings cut to 2 pairs, 1 new vertex and a
+    1-entry subtree queue (GBP_STAR_LDS, read when the planner configures
+    the insertion): every later pair, vertex and queued subtree vertex is
+    read from / written to global memory, the paths config 5's halves never
+    reach (~300 pairs, ~3 vertices).  Same trees as the oracle."""
+    name, xy, batch, seed, halves = "synth-rough-256", (1.0, 2.55, 4.02, 2.55), 1024, 3, 300
+    data, O, start, goal = _setup(name, xy)
+    monkeypatch.setenv("GBP_STAR_LDS", "2,1,1")
+    dev = planner.plan_rrt_star_connect(data, start, goal, batch=batch, max_time=600.0, seed=seed,
+                                        max_halves=halves, trees=True, device_loop=True)
+    monkeypatch.delenv("GBP_STAR_LDS")
+    ref = O.plan(start, goal, batch=batch, seed=seed, max_halves=halves, star=True, stream_a=401,
+                 stream_b=402)
+    assert dev["halves"] == ref["halves"] == halves
+    assert dev["rewires"] == ref["rewires"] > 0
+    assert_counters_equal(dev, ref)
+    assert_trees_equal(dev, ref)
+
+
 def test_rrt_star_insertion_sets_grow_equals_oracle(gpu, monkeypatch):
     """The device RRT*'s insertion sets sized for 16 neighbour pairs
     (GBP_STAR_PAIRS, read when the planner first configures them): every
