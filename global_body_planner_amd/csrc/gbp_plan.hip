@@ -183,7 +183,7 @@ struct gbp_plan_ws {
   double star_delta = 3.0;     // rrt_star_connect.h:59
   int64_t star_max_pairs = 0, star_max_shared = 0;
   int64_t star_items = 0;      // scan items per half (new vertex x position chunk)
-  int star_grid = 0;           // count / fill workgroups cap (GBP_STAR_GRID, tests; 0: none)
+  int star_grid = 0;           // count / fill / check workgroups cap (GBP_STAR_GRID, tests; 0: none)
   int64_t star_ch = 1024;      // map positions per scan item before growth (STAR_CH)
   int32_t star_lds[3] = {-1, -1, -1};  // the replay's LDS limits (GBP_STAR_LDS, tests; -1: RP, RK, RQ)
   // a half's insertion buffers, one set per tree (half & 1): half h's replay
@@ -2865,7 +2865,8 @@ int enqueue_stages(gbp_terrain *t, gbp_plan_ws *w, gbp_tree *T, gbp_tree *O, int
     if (th) HIPCHK_P(hipEventRecord(th->ev[6], s));
     const int64_t rmax = 2 * w->star_max_pairs;  // connect checks, one wave each
     const int cm = (t->opt_affine && t->affine) ? 2 : 0;
-    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * GBP_STAR_GC, (rmax + 3) / 4));
+    unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cus * GBP_STAR_GC, (rmax + 3) / 4));
+    if (w->star_grid > 0) g = std::min<unsigned>(g, (unsigned)w->star_grid);  // (tests: several checks a wave)
     const uint64_t cseq = ++w->seq;
 #define GBP_SC(AD, CM)                                                                        \
   hipLaunchKernelGGL((k_star_check<ZT, AD, CM>), dim3(g), dim3(TB), 0, s, V, st, direction, T->v, \

@@ -181,8 +181,9 @@ def test_rrt_star_small_item_capacity_equals_oracle(gpu, monkeypatch):
     when the planner creates its workspace): items of one map position and
     room for only the batch's 1,024 items per half (k_star_count / k_star_fill
     double the chunk until a half's items fit), over 2 workgroups (each takes
-    several items; the last of the two to finish scans them all).  Same trees
-    as the oracle."""
+    several items; the last of the two to finish scans them all), and the
+    connect checks on 2 workgroups of 4 waves (each wave several checks).
+    Same trees as the oracle."""
     name, xy, batch, seed, halves = "synth-rough-256", (1.0, 2.55, 4.02, 2.55), 1024, 3, 300
     data, O, start, goal = _setup(name, xy)
     monkeypatch.setenv("GBP_STAR_ITEMS", "1")  # (raised to the batch)
