@@ -26,5 +26,8 @@ for x in r[:24]:
     print(f'{int(x["Calls"]):8d} {float(x["AverageNs"]) / 1e3:9.2f}us {tot / halves:8.2f}us/half {x["Name"][:80]}')
 print(f"k_star_* per half: {star / halves:.2f} us")
 PY
-[ -n "$C5_KEEP" ] && python3 tools/c5_trace.py $d | tee -a gpurun_out/${TAG}_prof_summary.txt
+if [ -n "$C5_KEEP" ]; then
+  python3 tools/c5_trace.py $d | tee -a gpurun_out/${TAG}_prof_summary.txt
+  python3 tools/c5_gaps.py $d | tee -a gpurun_out/${TAG}_prof_summary.txt
+fi
 find $d -name "*kernel_trace.csv" -delete
