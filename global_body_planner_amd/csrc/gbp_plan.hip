@@ -29,6 +29,16 @@
 //   stage 5  k_append          non-TRAPPED connections appended to O in order;
 //                               the first REACHED one ends the search
 //
+// RRT*-Connect (gbp_plan_star_config) inserts T's new vertices between
+// stages 3 and 4 (rrt_star_connect.cpp:18-66):
+//   stage 6  k_star_count       neighbourhoods in the vertex map's order, chunked
+//                               (its last workgroup scans the items' offsets)
+//            k_star_fill        the neighbour lists
+//            k_star_check       one wave per connect check: its action and pair check
+//   stage 7  k_star_replay      (own stream) the ordered choose-parent / rewire replay
+// and stage 5's append also lists every REACHED connection (the ranking,
+// k_star_rank, follows Tb's halves on the replay's stream).
+//
 // Every count (targets, candidates, appended vertices) stays on the device:
 // the host enqueues many half-iterations and reads one small status record
 // per group.  The appends are ordered compactions: a wave ballot + popcount
