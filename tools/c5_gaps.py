@@ -17,13 +17,16 @@ for path in glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True):
 
 
 def short(n):
-    n = n.split("(")[0]
-    for key in ("k_", "__amd"):
-        i = n.find(key)
-        if i >= 0:
-            n = n[i:]
-            break
-    return n.split("<")[0][:28]
+    n = n.replace("(anonymous namespace)::", "")
+    if n.startswith("void "):
+        n = n[5:]
+    if n.startswith("_ZN12_GLOBAL__N_1"):  # mangled: _ZN12_GLOBAL__N_1<len><name>...
+        i = len("_ZN12_GLOBAL__N_1")
+        j = i
+        while j < len(n) and n[j].isdigit():
+            j += 1
+        n = n[j:j + int(n[i:j])] if j > i else n
+    return n.split("(")[0].split("<")[0][:28]
 
 
 byq = collections.defaultdict(list)
@@ -37,6 +40,7 @@ for q, ev in sorted(byq.items(), key=lambda kv: -len(kv[1])):
     for (s0, e0, n0), (s1, e1, n1) in zip(ev, ev[1:]):
         gaps[(n0, n1)].append(s1 - e0)
     print(f"queue {q}: {len(ev)} kernels, busy {busy / span:.2f} of its span")
-    top = sorted(gaps.items(), key=lambda kv: -len(kv[1]) * np.median(kv[1]))[:14]
+    top = sorted(gaps.items(), key=lambda kv: -len(kv[1]) * np.mean(kv[1]))[:16]
     for (a, b), g in top:
-        print(f"  {a:28s} -> {b:28s} n {len(g):6d} median gap {np.median(g) / 1e3:7.2f} us")
+        print(f"  {a:28s} -> {b:28s} n {len(g):6d} median gap {np.median(g) / 1e3:7.2f} us, "
+              f"mean {np.mean(g) / 1e3:7.2f} us")
